@@ -1,0 +1,219 @@
+"""fugu query hot path on MI355X: queries/sec + p50 latency on a synthetic
+10M-doc Zipf corpus, 3-term AND, BM25 top-100 (BASELINE.json `metric`).
+
+A step = one batch of 1024 planned queries through the gfx950 pipeline
+(k_conj -> k_filter -> k_final) with the plan and the index resident in HBM.
+N > 1 (torchrun, one rank per GPU): rank r holds namespace r (its own 10M-doc
+corpus, weak scaling); every step also all-gathers the per-shard top-100 over
+RCCL and merges them on the device (fan-out query over all namespaces).
+
+Prints ONE JSON line on rank 0.  See DESIGN.md §Measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "queries/sec + p50 latency, 10M-doc Zipf corpus, 3-term AND, top-100"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--docs", type=int, default=10_000_000)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--terms", type=int, default=3)
+    ap.add_argument("--mixed", action="store_true", help="1-5 terms per query (config C3) instead of 3")
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="bound on the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--p50-queries", type=int, default=200)
+    ap.add_argument("--threads", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{local}")
+
+    from fugu_amd import native, synth
+
+    threads = args.threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 8, 16)
+    t0 = time.time()
+    # namespace r: its own corpus (seeds offset by rank); rank 0 is the standard corpus
+    corp = synth.corpus(args.docs, synth.VOCAB, 1.0, synth.SEED_L + rank, synth.SEED_T + rank, threads=threads)
+    log(f"[bench] corpus {args.docs} docs, {len(corp.tok)} tokens in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    ctx = native.Context((local,))
+    ix = native.Index.from_docs(ctx, corp.off, corp.tok, synth.VOCAB, threads=threads, keep_host=True)
+    st = ix.stats()
+    log(f"[bench] index: {st.n_postings} postings, {st.device_bytes / 2**30:.2f} GiB in HBM, built in "
+        f"{time.time() - t0:.1f}s")
+
+    m_min, m_max = (1, 5) if args.mixed else (args.terms, args.terms)
+    q_off_all, terms_all = synth.queries(4096, m_min, m_max)
+    nq = args.batch
+    q_off = q_off_all[: nq + 1].copy()
+    terms = terms_all[: q_off[-1]].copy()
+    K = args.k
+    plan = ix.plan(q_off, terms, K)
+    info = plan.info()
+    log(f"[bench] plan: {info.total_chunks} work items, workspace {info.workspace_bytes / 2**20:.1f} MiB")
+
+    out_s = torch.empty(nq * K, dtype=torch.float32, device=dev)
+    out_d = torch.empty(nq * K, dtype=torch.int32, device=dev)
+    out_n = torch.empty(nq, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        plan.execute(stream.cuda_stream, out_s.data_ptr(), out_d.data_ptr(), out_n.data_ptr())
+        if world > 1:
+            from fugu_amd.shard import gather_packed, merge_on_device
+            s, d, c = gather_packed(out_s, out_d, out_n)
+            merge_on_device(s, d, c, nq, K, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    plan.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    plan.profile(False)
+    ms_k, n_prof = plan.kernel_ms()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_queries = nq * world * args.steps
+    qps = total_queries / elapsed
+
+    # ---- p50 latency at batch = 1 (host query in, host hits out: plan + PCIe + kernels)
+    lat = []
+    for i in range(min(args.p50_queries, nq)):
+        a, b = int(q_off[i]), int(q_off[i + 1])
+        one_off = np.array([0, b - a], np.uint32)
+        t1 = time.perf_counter()
+        ix.search_batch(one_off, terms[a:b], K)
+        lat.append(time.perf_counter() - t1)
+    p50_ms = float(np.median(lat) * 1e3) if lat else None
+
+    # ---- roofline of the dominant kernel (k_conj), SURVEY.md §8(d) algorithmic bytes
+    bm = ix.bytes_model(q_off, terms, K)
+    alg_bytes = float(bm[:, 2].sum())
+    conj_ms = ms_k[0] / max(n_prof, 1)
+    achieved = alg_bytes / (conj_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_file = os.environ.get("FUGU_PMC_BYTES")
+    if pmc_file and os.path.exists(pmc_file):
+        with open(pmc_file) as f:
+            traffic = json.load(f).get("k_conj_hbm_bytes_per_launch")
+
+    # ---- CPU baseline: the oracle (tantivy's algorithm restated in C) on host cores, rank 0, N=1 only
+    cpu = None
+    parity = None
+    s_gpu = out_s.cpu().numpy().reshape(nq, K)
+    d_gpu = out_d.cpu().numpy().view(np.uint32).reshape(nq, K)
+    n_gpu = out_n.cpu().numpy()
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import oracle as orc
+        t0 = time.time()
+        ref = orc.OracleIndex(synth.VOCAB, corp.off, corp.tok, threads=threads)
+        log(f"[bench] oracle index built in {time.time() - t0:.1f}s")
+        done, wall, lats = 0, 0.0, []
+        mism = 0
+        while done < nq and wall < args.cpu_seconds:
+            hi = min(nq, done + 128)
+            sub_off = (q_off[done:hi + 1] - q_off[done]).astype(np.uint32)
+            sub_terms = terms[q_off[done]:q_off[hi]]
+            rs, rd, rn, w, l = ref.search_batch(sub_off, sub_terms, K, threads=threads, latencies=True)
+            wall += w
+            lats.append(l)
+            for j in range(hi - done):
+                i = done + j
+                m = int(rn[j])
+                if (int(n_gpu[i]) != m or not np.array_equal(d_gpu[i, :m], rd[j, :m])
+                        or not np.allclose(s_gpu[i, :m], rs[j, :m], rtol=1e-5, atol=0)):
+                    mism += 1
+            done = hi
+        lat_all = np.concatenate(lats)
+        cpu = {"value": round(done / wall, 2), "unit": "queries/s", "cores": threads, "kind": "port",
+               "sample": f"first {done} queries of the same 1024-query batch, {threads} threads x whole queries, "
+                         f"warm in-RAM index (tantivy 0.24.1 algorithm restated in C: oracle/fugu_oracle.c)",
+               "p50_ms": round(float(np.median(lat_all)) * 1e-6, 4)}
+        parity = {"queries_checked": done, "mismatches": mism, "rule": "doc ids exact, scores rtol 1e-5"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(qps, 1),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32+f32",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"{'C3 mixed 1-5' if args.mixed else str(args.terms) + '-term'} AND, BM25 top-{K}, "
+                             f"{args.docs // 1_000_000}M-doc Zipf s=1.0 corpus per namespace, batch {nq}"),
+                "n_docs": args.docs, "vocab": synth.VOCAB, "batch": nq, "k": K,
+                "terms": "1-5" if args.mixed else args.terms, "namespaces": world,
+                "parallelism": f"namespace-shard x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
+            },
+            "p50_ms": round(p50_ms, 4) if p50_ms is not None else None,
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "k_conj", "kernel_ms": round(conj_ms, 4),
+                "alg_bytes_per_launch": alg_bytes,
+            },
+            "kernels_ms_per_step": {"k_conj": round(ms_k[0] / max(n_prof, 1), 4),
+                                    "k_filter": round(ms_k[1] / max(n_prof, 1), 4),
+                                    "k_final": round(ms_k[2] / max(n_prof, 1), 4)},
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "speedup_vs_cpu": round(qps / cpu["value"], 1) if cpu else None,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

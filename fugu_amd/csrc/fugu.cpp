@@ -1,0 +1,778 @@
+// libfugu host side: index snapshot build + HBM upload, batch planning,
+// execution and the C ABI of include/fugu.h.
+//
+// The BM25 statistics follow tantivy 0.24.1 as fugu uses it (SURVEY.md
+// Appendix A): N = max_doc (deleted docs included), avgdl = total tokens / N,
+// idf = ln(1 + (N - df + 0.5) / (df + 0.5)), weight = idf * (1 + K1), tf cache
+// K1 * ((1 - B) + B * FIELD_NORMS_TABLE[id] / avgdl).  They are computed here,
+// on the host, in that operation order with the host libm, so the device only
+// multiplies/divides precomputed f32 values (bit-identical to the CPU path).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fugu.h"
+#include "fg_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) return fail(FG_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+// ---------------------------------------------------------------- tantivy constants
+constexpr float kK1 = 1.2f;
+constexpr float kB = 0.75f;
+
+struct FieldNormTable {
+  uint32_t v[256];
+  FieldNormTable() {
+    uint32_t i = 0;
+    for (; i <= 40; ++i) v[i] = i;
+    uint64_t x = 40, step = 2;
+    while (i < 256) {
+      for (int j = 0; j < 8 && i < 256; ++j) { x += step; v[i++] = (uint32_t)x; }
+      step <<= 1;
+    }
+  }
+};
+const FieldNormTable& fn_table() {
+  static const FieldNormTable t;
+  return t;
+}
+// FIELD_NORMS_TABLE.binary_search(n).unwrap_or_else(|i| i - 1)
+uint8_t fieldnorm_id(uint64_t n) {
+  const uint32_t* t = fn_table().v;
+  uint32_t x = n > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)n;
+  return (uint8_t)(std::upper_bound(t, t + 256, x) - t - 1);
+}
+float bm25_weight(uint64_t df, uint64_t n_docs) {
+  float x = ((float)(n_docs - df) + 0.5f) / ((float)df + 0.5f);
+  return logf(1.0f + x) * (1.0f + kK1);
+}
+void bm25_cache(float avgdl, float* out) {
+  const uint32_t* t = fn_table().v;
+  for (int i = 0; i < 256; ++i) out[i] = kK1 * ((1.0f - kB) + (kB * (float)t[i]) / avgdl);
+}
+
+template <class F>
+void parallel_ranges(uint32_t n, int threads, F&& f) {
+  if (threads <= 1 || n < 1024) { f(0, 0u, n); return; }
+  std::vector<std::thread> ts;
+  uint32_t step = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    uint32_t b = std::min<uint64_t>((uint64_t)t * step, n), e = std::min<uint64_t>((uint64_t)(t + 1) * step, n);
+    ts.emplace_back([&f, t, b, e] { f(t, b, e); });
+  }
+  for (auto& t : ts) t.join();
+}
+
+int hw_threads(int req) {
+  if (req > 0) return std::min(req, 256);
+  unsigned h = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(h, 64u));
+}
+
+// Host-side postings before upload (merged text U name per term).
+struct HostPostings {
+  uint32_t n_docs = 0, n_terms = 0;
+  std::vector<uint64_t> off;      // [V+1]
+  std::vector<uint32_t> doc, tf;  // tf packed lo16 text / hi16 name
+  std::vector<uint32_t> df_text, df_name;
+  std::vector<uint8_t> fn_text, fn_name;
+  std::vector<uint32_t> alive;    // bitset, empty when no deletes
+  uint64_t tot[2] = {0, 0};
+  bool has_name = false;
+};
+
+struct DevAllocs {
+  std::vector<void*> ptrs;
+  int dev = 0;
+  ~DevAllocs() {
+    if (ptrs.empty()) return;
+    (void)hipSetDevice(dev);
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+};
+
+}  // namespace
+
+struct fg_ctx {
+  std::vector<int> devs;
+};
+
+struct fg_index {
+  std::atomic<int> refs{1};
+  int dev = 0;
+  uint32_t n_docs = 0, n_terms = 0;
+  bool has_name = false;
+  uint64_t n_postings = 0, device_bytes = 0;
+  uint64_t tot[2] = {0, 0};
+  float avgdl[2] = {0, 0};
+  float cache[512];
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> df_text, df_name;
+  std::vector<float> w_text, w_name;
+  std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model
+  fg::DevIndex d{};
+  DevAllocs mem;
+};
+
+struct fg_plan {
+  fg_index* ix = nullptr;
+  uint32_t nq = 0, k = 0, total_chunks = 0;
+  int mode = FG_MODE_AND;
+  fg::DevPlan d{};
+  float* own_score = nullptr;
+  uint32_t* own_doc = nullptr;
+  uint32_t* own_n = nullptr;
+  void* zero_region = nullptr;
+  size_t zero_bytes = 0;
+  uint64_t ws_bytes = 0;
+  DevAllocs mem;
+  hipStream_t last_stream = nullptr;
+  bool profile = false;
+  std::vector<hipEvent_t> pending;  // 4 per profiled execute
+  double ms[3] = {0, 0, 0};
+  uint32_t n_prof = 0;
+  ~fg_plan() {
+    for (hipEvent_t e : pending) (void)hipEventDestroy(e);
+    if (ix) fg_index_release(ix);
+  }
+};
+
+namespace {
+
+template <class T>
+int dev_upload(DevAllocs& m, const T* src, size_t n, T** out, uint64_t* bytes) {
+  size_t b = std::max<size_t>(n * sizeof(T), 16);
+  void* p = nullptr;
+  if (hipMalloc(&p, b) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", b);
+  m.ptrs.push_back(p);
+  if (n) HIPCHK(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  *out = static_cast<T*>(p);
+  *bytes += b;
+  return FG_OK;
+}
+
+int check_device(int dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(FG_ENODEV, "no HIP device visible");
+  if (dev < 0 || dev >= n) return fail(FG_ENODEV, "device %d out of range (%d visible)", dev, n);
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(FG_ENODEV, "device %d is %s; libfugu is built for gfx950 only", dev, prop.gcnArchName);
+  return FG_OK;
+}
+
+// Stats, weights, skip index, upload.  Consumes hp.
+int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
+  auto ix = std::make_unique<fg_index>();
+  ix->dev = dev;
+  ix->mem.dev = dev;
+  ix->n_docs = hp.n_docs;
+  ix->n_terms = hp.n_terms;
+  ix->has_name = hp.has_name;
+  ix->n_postings = hp.off[hp.n_terms];
+  ix->tot[0] = hp.tot[0];
+  ix->tot[1] = hp.tot[1];
+  const uint64_t N = hp.n_docs;
+  for (int f = 0; f < 2; ++f) {
+    ix->avgdl[f] = (float)hp.tot[f] / (float)N;  // total_num_tokens as f32 / N as f32
+    bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
+  }
+  const uint32_t V = hp.n_terms;
+  ix->w_text.resize(V);
+  ix->w_name.resize(V);
+  for (uint32_t t = 0; t < V; ++t) {
+    ix->w_text[t] = bm25_weight(hp.df_text[t], N);
+    ix->w_name[t] = bm25_weight(hp.df_name[t], N);
+  }
+  // skip index: last doc of every 128-posting block
+  std::vector<uint32_t> skip_off(V + 1);
+  uint64_t nb = 0;
+  for (uint32_t t = 0; t < V; ++t) {
+    skip_off[t] = (uint32_t)nb;
+    nb += (hp.off[t + 1] - hp.off[t] + fg::kBlock - 1) / fg::kBlock;
+  }
+  if (nb > 0xFFFFFFFFull) return fail(FG_EINVAL, "too many skip blocks");
+  skip_off[V] = (uint32_t)nb;
+  std::vector<uint32_t> skip(nb);
+  for (uint32_t t = 0; t < V; ++t) {
+    uint64_t b = hp.off[t], n = hp.off[t + 1] - b;
+    uint32_t so = skip_off[t];
+    for (uint64_t k = 0; k * fg::kBlock < n; ++k) {
+      uint64_t end = std::min<uint64_t>((k + 1) * fg::kBlock, n);
+      skip[so + k] = hp.doc[b + end - 1];
+    }
+  }
+  HIPCHK(hipSetDevice(dev));
+  uint64_t bytes = 0;
+  int rc;
+  uint32_t *d_doc, *d_tf, *d_skip, *d_skip_off, *d_alive = nullptr;
+  uint64_t* d_off;
+  float *d_wt, *d_wn, *d_cache;
+  uint8_t *d_fnt, *d_fnn;
+  if ((rc = dev_upload(ix->mem, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, hp.tf.data(), hp.tf.size(), &d_tf, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, hp.off.data(), hp.off.size(), &d_off, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, skip.data(), skip.size(), &d_skip, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, skip_off.data(), skip_off.size(), &d_skip_off, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, ix->w_text.data(), V, &d_wt, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, ix->w_name.data(), V, &d_wn, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, hp.fn_text.data(), hp.fn_text.size(), &d_fnt, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, hp.fn_name.data(), hp.fn_name.size(), &d_fnn, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
+  if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
+  ix->d = fg::DevIndex{d_doc, d_tf, d_off, d_skip, d_skip_off, d_wt, d_wn, d_fnt, d_fnn, d_alive, d_cache,
+                       hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
+  ix->device_bytes = bytes;
+  ix->off = std::move(hp.off);
+  ix->df_text = std::move(hp.df_text);
+  ix->df_name = std::move(hp.df_name);
+  if (keep_host) ix->h_doc = std::move(hp.doc);
+  *out = ix.release();
+  return FG_OK;
+}
+
+// Sorted (term, tf) runs of one field of one doc into `runs` (term << 0, tf).
+inline void doc_runs(const uint32_t* tok, uint64_t len, std::vector<uint32_t>& scratch,
+                     std::vector<std::pair<uint32_t, uint32_t>>& runs) {
+  runs.clear();
+  if (!len) return;
+  scratch.assign(tok, tok + len);
+  std::sort(scratch.begin(), scratch.end());
+  for (size_t i = 0; i < scratch.size();) {
+    size_t j = i;
+    while (j < scratch.size() && scratch[j] == scratch[i]) ++j;
+    runs.emplace_back(scratch[i], (uint32_t)(j - i));
+    i = j;
+  }
+}
+
+}  // namespace
+
+// ================================================================ C ABI
+extern "C" {
+
+const char* fg_last_error(void) { return g_err.c_str(); }
+const char* fg_version(void) { return "libfugu 0.1 (gfx950)"; }
+
+int fg_device_count(int* out) {
+  if (!out) return fail(FG_EINVAL, "out is NULL");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *out = n;
+  return FG_OK;
+}
+
+int fg_ctx_create(int ndev, const int* devs, fg_ctx** out) {
+  if (!out || ndev < 0 || (ndev > 0 && !devs)) return fail(FG_EINVAL, "bad arguments");
+  auto c = std::make_unique<fg_ctx>();
+  if (ndev == 0) {
+    int n = 0;
+    fg_device_count(&n);
+    if (n == 0) return fail(FG_ENODEV, "no HIP device visible");
+    c->devs.push_back(0);
+  } else {
+    c->devs.assign(devs, devs + ndev);
+  }
+  for (int d : c->devs) {
+    int rc = check_device(d);
+    if (rc) return rc;
+  }
+  *out = c.release();
+  return FG_OK;
+}
+
+int fg_ctx_destroy(fg_ctx* ctx) {
+  delete ctx;
+  return FG_OK;
+}
+
+int fg_index_build_from_docs(fg_ctx* ctx, int dev, const fg_docs_input* in, fg_index** out) {
+  if (!ctx || !in || !out || !in->text_off || (!in->text_tok && in->text_off[in->n_docs] > 0))
+    return fail(FG_EINVAL, "bad arguments");
+  if (in->n_docs == 0) return fail(FG_EINVAL, "empty index (n_docs == 0)");
+  if (in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs must be < 2^31 (tantivy DocId)");
+  if (std::find(ctx->devs.begin(), ctx->devs.end(), dev) == ctx->devs.end())
+    return fail(FG_EINVAL, "device %d not in context", dev);
+  const uint32_t N = in->n_docs, V = in->n_terms;
+  const bool has_name_in = in->name_off && in->name_tok;
+  const int T = hw_threads(in->threads);
+  HostPostings hp;
+  hp.n_docs = N;
+  hp.n_terms = V;
+  hp.fn_text.resize(N);
+  hp.fn_name.assign(N, 0);
+  // pass 1: per-thread counts (merged df, df_text, df_name), fieldnorms
+  std::vector<std::vector<uint32_t>> cnt(T), dft(T), dfn(T);
+  std::vector<uint64_t> tot_t(T, 0), tot_n(T, 0);
+  std::atomic<bool> bad{false};
+  parallel_ranges(N, T, [&](int t, uint32_t b, uint32_t e) {
+    cnt[t].assign(V, 0);
+    dft[t].assign(V, 0);
+    dfn[t].assign(V, 0);
+    std::vector<uint32_t> scratch;
+    std::vector<std::pair<uint32_t, uint32_t>> rt, rn;
+    for (uint32_t d = b; d < e; ++d) {
+      uint64_t lt = in->text_off[d + 1] - in->text_off[d];
+      uint64_t ln = has_name_in ? in->name_off[d + 1] - in->name_off[d] : 0;
+      tot_t[t] += lt;
+      tot_n[t] += ln;
+      hp.fn_text[d] = fieldnorm_id(lt);
+      if (has_name_in) hp.fn_name[d] = fieldnorm_id(ln);
+      doc_runs(in->text_tok + in->text_off[d], lt, scratch, rt);
+      if (has_name_in) doc_runs(in->name_tok + in->name_off[d], ln, scratch, rn); else rn.clear();
+      size_t i = 0, j = 0;
+      while (i < rt.size() || j < rn.size()) {
+        uint32_t a = i < rt.size() ? rt[i].first : 0xFFFFFFFFu;
+        uint32_t c = j < rn.size() ? rn[j].first : 0xFFFFFFFFu;
+        uint32_t term = std::min(a, c);
+        if (term >= V) { bad = true; return; }
+        cnt[t][term]++;
+        if (a == term) { dft[t][term]++; ++i; }
+        if (c == term) { dfn[t][term]++; ++j; }
+      }
+    }
+  });
+  if (bad) return fail(FG_EINVAL, "token id >= n_terms");
+  const int used = (int)std::count_if(cnt.begin(), cnt.end(), [](auto& v) { return !v.empty(); });
+  hp.off.assign(V + 1, 0);
+  hp.df_text.assign(V, 0);
+  hp.df_name.assign(V, 0);
+  // per-thread write cursors (reuse cnt as u64 cursors via a separate array)
+  std::vector<std::vector<uint64_t>> cur(used);
+  for (int t = 0; t < used; ++t) cur[t].resize(V);
+  uint64_t acc = 0;
+  for (uint32_t term = 0; term < V; ++term) {
+    hp.off[term] = acc;
+    for (int t = 0; t < used; ++t) {
+      cur[t][term] = acc;
+      acc += cnt[t][term];
+      hp.df_text[term] += dft[t][term];
+      hp.df_name[term] += dfn[t][term];
+    }
+  }
+  hp.off[V] = acc;
+  cnt.clear();
+  dft.clear();
+  dfn.clear();
+  for (int t = 0; t < used; ++t) { hp.tot[0] += tot_t[t]; hp.tot[1] += tot_n[t]; }
+  hp.has_name = hp.tot[1] > 0;
+  try {
+    hp.doc.resize(acc);
+    hp.tf.resize(acc);
+  } catch (...) {
+    return fail(FG_EOOM, "host postings (%llu) allocation failed", (unsigned long long)acc);
+  }
+  // pass 2: fill (thread t's docs land after threads < t within each term)
+  parallel_ranges(N, T, [&](int t, uint32_t b, uint32_t e) {
+    std::vector<uint32_t> scratch;
+    std::vector<std::pair<uint32_t, uint32_t>> rt, rn;
+    std::vector<uint64_t>& c = cur[t];
+    for (uint32_t d = b; d < e; ++d) {
+      uint64_t lt = in->text_off[d + 1] - in->text_off[d];
+      uint64_t ln = has_name_in ? in->name_off[d + 1] - in->name_off[d] : 0;
+      doc_runs(in->text_tok + in->text_off[d], lt, scratch, rt);
+      if (has_name_in) doc_runs(in->name_tok + in->name_off[d], ln, scratch, rn); else rn.clear();
+      size_t i = 0, j = 0;
+      while (i < rt.size() || j < rn.size()) {
+        uint32_t a = i < rt.size() ? rt[i].first : 0xFFFFFFFFu;
+        uint32_t cc = j < rn.size() ? rn[j].first : 0xFFFFFFFFu;
+        uint32_t term = std::min(a, cc);
+        uint32_t tt = 0, tn = 0;
+        if (a == term) { tt = std::min<uint32_t>(rt[i].second, 0xFFFF); ++i; }
+        if (cc == term) { tn = std::min<uint32_t>(rn[j].second, 0xFFFF); ++j; }
+        uint64_t p = c[term]++;
+        hp.doc[p] = d;
+        hp.tf[p] = tt | (tn << 16);
+      }
+    }
+  });
+  if (in->deleted) {
+    hp.alive.assign((N + 31) / 32, 0);
+    for (uint32_t d = 0; d < N; ++d)
+      if (!in->deleted[d]) hp.alive[d >> 5] |= 1u << (d & 31);
+  }
+  return finish_index(dev, hp, in->keep_host_postings != 0, out);
+}
+
+int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out) {
+  if (!ctx || !in || !out || !in->term_off || !in->fn_text) return fail(FG_EINVAL, "bad arguments");
+  if (in->n_docs == 0 || in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs out of range");
+  if (std::find(ctx->devs.begin(), ctx->devs.end(), dev) == ctx->devs.end())
+    return fail(FG_EINVAL, "device %d not in context", dev);
+  HostPostings hp;
+  const uint32_t N = in->n_docs, V = in->n_terms;
+  hp.n_docs = N;
+  hp.n_terms = V;
+  hp.off.assign(in->term_off, in->term_off + V + 1);
+  const uint64_t P = hp.off[V];
+  hp.doc.assign(in->doc, in->doc + P);
+  hp.tf.resize(P);
+  hp.df_text.assign(V, 0);
+  hp.df_name.assign(V, 0);
+  for (uint32_t t = 0; t < V; ++t) {
+    if (hp.off[t + 1] < hp.off[t]) return fail(FG_EINVAL, "term_off not monotone at %u", t);
+    for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) {
+      uint32_t tt = in->tf_text ? in->tf_text[p] : 0, tn = in->tf_name ? in->tf_name[p] : 0;
+      if (!tt && !tn) return fail(FG_EINVAL, "posting %llu has tf 0 in both fields", (unsigned long long)p);
+      if (hp.doc[p] >= N || (p > hp.off[t] && hp.doc[p] <= hp.doc[p - 1]))
+        return fail(FG_EINVAL, "postings of term %u not strictly ascending / in range", t);
+      hp.tf[p] = tt | (tn << 16);
+      hp.df_text[t] += tt ? 1 : 0;
+      hp.df_name[t] += tn ? 1 : 0;
+    }
+  }
+  hp.fn_text.assign(in->fn_text, in->fn_text + N);
+  if (in->fn_name) hp.fn_name.assign(in->fn_name, in->fn_name + N); else hp.fn_name.assign(N, 0);
+  hp.tot[0] = in->tot_tokens[0];
+  hp.tot[1] = in->tot_tokens[1];
+  hp.has_name = hp.tot[1] > 0;
+  if (in->deleted) {
+    hp.alive.assign((N + 31) / 32, 0);
+    for (uint32_t d = 0; d < N; ++d)
+      if (!in->deleted[d]) hp.alive[d >> 5] |= 1u << (d & 31);
+  }
+  return finish_index(dev, hp, true, out);
+}
+
+int fg_index_retain(fg_index* ix) {
+  if (!ix) return fail(FG_EINVAL, "NULL index");
+  ix->refs.fetch_add(1);
+  return FG_OK;
+}
+
+int fg_index_release(fg_index* ix) {
+  if (!ix) return FG_OK;
+  if (ix->refs.fetch_sub(1) == 1) delete ix;
+  return FG_OK;
+}
+
+int fg_index_stats_get(const fg_index* ix, fg_index_stats* o) {
+  if (!ix || !o) return fail(FG_EINVAL, "bad arguments");
+  o->n_docs = ix->n_docs;
+  o->n_terms = ix->n_terms;
+  o->n_postings = ix->n_postings;
+  o->device_bytes = ix->device_bytes;
+  o->tot_tokens[0] = ix->tot[0];
+  o->tot_tokens[1] = ix->tot[1];
+  o->avgdl[0] = ix->avgdl[0];
+  o->avgdl[1] = ix->avgdl[1];
+  o->has_name = ix->has_name;
+  o->device = ix->dev;
+  return FG_OK;
+}
+
+uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term) {
+  if (!ix || term >= ix->n_terms) return 0;
+  if (field == FG_FIELD_TEXT) return ix->df_text[term];
+  if (field == FG_FIELD_NAME) return ix->df_name[term];
+  return ix->off[term + 1] - ix->off[term];
+}
+
+int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512) {
+  if (!ix) return fail(FG_EINVAL, "NULL index");
+  if (term < ix->n_terms) {
+    if (w_text) *w_text = ix->w_text[term];
+    if (w_name) *w_name = ix->w_name[term];
+  } else {
+    if (w_text) *w_text = bm25_weight(0, ix->n_docs);
+    if (w_name) *w_name = bm25_weight(0, ix->n_docs);
+  }
+  if (cache512) std::memcpy(cache512, ix->cache, sizeof ix->cache);
+  return FG_OK;
+}
+
+// ---------------------------------------------------------------- planning
+int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out) {
+  if (!ix || !q || !out || (q->n_queries && (!q->q_off || !q->terms))) return fail(FG_EINVAL, "bad arguments");
+  if (k < 1) return fail(FG_EINVAL, "k must be >= 1 (TopDocs::with_limit asserts limit >= 1)");
+  if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k=%u > FG_MAX_K=%d", k, FG_MAX_K);
+  if (q->mode != FG_MODE_AND && q->mode != FG_MODE_OR) return fail(FG_EINVAL, "bad mode %d", q->mode);
+  const uint32_t nq = q->n_queries;
+  std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), chunk_start(nq + 1);
+  std::vector<uint64_t> cand_off(nq + 1);
+  uint64_t chunks = 0, cand = 0;
+  for (uint32_t i = 0; i < nq; ++i) {
+    const uint32_t b = q->q_off[i], e = q->q_off[i + 1];
+    if (e < b) return fail(FG_EINVAL, "q_off not monotone at query %u", i);
+    const uint32_t m = e - b;
+    if (m == 0) return fail(FG_EUNSUPPORTED, "query %u is empty (AllQuery runs on the CPU path)", i);
+    if (m > fg::kMaxTerms) return fail(FG_EUNSUPPORTED, "query %u has %u terms (> %u)", i, m, fg::kMaxTerms);
+    if (q->mode == FG_MODE_OR && m > 1)
+      return fail(FG_EUNSUPPORTED, "query %u: multi-term disjunction runs on the CPU path in v1", i);
+    // tantivy intersect_scorers: children sorted by cost (union cost = df_text + df_name), stable
+    struct T { uint64_t cost; uint32_t pos, term; };
+    T ts[fg::kMaxTerms];
+    bool missing = false;
+    for (uint32_t j = 0; j < m; ++j) {
+      uint32_t t = q->terms[b + j];
+      uint64_t cost = 0;
+      if (t >= ix->n_terms) missing = true; else cost = (uint64_t)ix->df_text[t] + ix->df_name[t];
+      if (cost == 0) missing = true;
+      ts[j] = T{cost, j, t};
+    }
+    std::stable_sort(ts, ts + m, [](const T& x, const T& y) { return x.cost < y.cost; });
+    q_m[i] = m;
+    for (uint32_t j = 0; j < m; ++j) q_terms[(size_t)i * fg::kMaxTerms + j] = missing ? 0 : ts[j].term;
+    uint64_t df0 = missing ? 0 : ix->off[ts[0].term + 1] - ix->off[ts[0].term];
+    lead[i] = (uint32_t)df0;
+    uint64_t nch = (df0 + fg::kChunk - 1) / fg::kChunk;
+    chunk_start[i] = (uint32_t)chunks;
+    cand_off[i] = cand;
+    chunks += nch;
+    cand += nch * k;
+    if (chunks > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%llu work items)", (unsigned long long)chunks);
+  }
+  chunk_start[nq] = (uint32_t)chunks;
+  cand_off[nq] = cand;
+  std::vector<uint32_t> chunk_q(chunks);
+  for (uint32_t i = 0; i < nq; ++i)
+    for (uint32_t c = chunk_start[i]; c < chunk_start[i + 1]; ++c) chunk_q[c] = i;
+
+  auto p = std::make_unique<fg_plan>();
+  p->nq = nq;
+  p->k = k;
+  p->mode = q->mode;
+  p->total_chunks = (uint32_t)chunks;
+  p->mem.dev = ix->dev;
+  // one allocation: [inputs | zeroed (thresh, cand_cnt) | workspace | outputs]
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t s_qm = al(4ull * nq), s_qt = al(4ull * nq * fg::kMaxTerms), s_lead = al(4ull * nq),
+               s_cs = al(4ull * (nq + 1)), s_cq = al(4ull * chunks), s_co = al(8ull * (nq + 1));
+  const size_t s_in = s_qm + s_qt + s_lead + s_cs + s_cq + s_co;
+  const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq);
+  const size_t s_sc = al(4ull * chunks), s_sk = al(8ull * chunks * k), s_ck = al(8ull * cand);
+  const size_t s_os = al(4ull * nq * k), s_od = al(4ull * nq * k), s_on = al(4ull * nq);
+  const size_t total = s_in + s_thr + s_cc + s_sc + s_sk + s_ck + s_os + s_od + s_on;
+  HIPCHK(hipSetDevice(ix->dev));
+  char* base = nullptr;
+  if (hipMalloc((void**)&base, std::max<size_t>(total, 256)) != hipSuccess)
+    return fail(FG_EOOM, "plan workspace hipMalloc(%zu) failed", total);
+  p->mem.ptrs.push_back(base);
+  p->ws_bytes = total;
+  std::vector<char> staging(s_in, 0);
+  size_t o = 0;
+  auto put = [&](const void* src, size_t bytes, size_t slot) {
+    if (bytes) std::memcpy(staging.data() + o, src, bytes);
+    void* dptr = base + o;
+    o += slot;
+    return dptr;
+  };
+  p->d.q_m = (const uint32_t*)put(q_m.data(), 4ull * nq, s_qm);
+  p->d.q_terms = (const uint32_t*)put(q_terms.data(), 4ull * nq * fg::kMaxTerms, s_qt);
+  p->d.q_lead_df = (const uint32_t*)put(lead.data(), 4ull * nq, s_lead);
+  p->d.chunk_start = (const uint32_t*)put(chunk_start.data(), 4ull * (nq + 1), s_cs);
+  p->d.chunk_q = (const uint32_t*)put(chunk_q.data(), 4ull * chunks, s_cq);
+  p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
+  HIPCHK(hipMemcpy(base, staging.data(), s_in, hipMemcpyHostToDevice));
+  char* cur = base + s_in;
+  p->zero_region = cur;
+  p->zero_bytes = s_thr + s_cc;
+  p->d.thresh = (uint64_t*)cur;
+  cur += s_thr;
+  p->d.cand_cnt = (uint32_t*)cur;
+  cur += s_cc;
+  p->d.slot_cnt = (uint32_t*)cur;
+  cur += s_sc;
+  p->d.slot_keys = (uint64_t*)cur;
+  cur += s_sk;
+  p->d.cand_keys = (uint64_t*)cur;
+  cur += s_ck;
+  p->own_score = (float*)cur;
+  cur += s_os;
+  p->own_doc = (uint32_t*)cur;
+  cur += s_od;
+  p->own_n = (uint32_t*)cur;
+  p->d.n_queries = nq;
+  p->d.total_chunks = (uint32_t)chunks;
+  p->d.k = k;
+  p->d.mode = (uint32_t)q->mode;
+  fg_index_retain(ix);
+  p->ix = ix;
+  *out = p.release();
+  return FG_OK;
+}
+
+int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_n) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIPCHK(hipSetDevice(p->ix->dev));
+  float* os = d_out_score ? d_out_score : p->own_score;
+  uint32_t* od = d_out_doc ? d_out_doc : p->own_doc;
+  uint32_t* on = d_out_n ? d_out_n : p->own_n;
+  HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
+  hipEvent_t ev[4] = {};
+  if (p->profile) {
+    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipEventRecord(ev[0], s));
+  }
+  HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
+  if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
+  HIPCHK(fg::launch_filter(p->d, s));
+  if (p->profile) HIPCHK(hipEventRecord(ev[2], s));
+  HIPCHK(fg::launch_final(p->d, os, od, on, s));
+  if (p->profile) {
+    HIPCHK(hipEventRecord(ev[3], s));
+    p->pending.insert(p->pending.end(), ev, ev + 4);
+  }
+  p->last_stream = s;
+  return FG_OK;
+}
+
+int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  HIPCHK(hipSetDevice(p->ix->dev));
+  HIPCHK(hipStreamSynchronize(p->last_stream));
+  const size_t nk = (size_t)p->nq * p->k;
+  if (out_score) HIPCHK(hipMemcpy(out_score, p->own_score, 4 * nk, hipMemcpyDeviceToHost));
+  if (out_doc) HIPCHK(hipMemcpy(out_doc, p->own_doc, 4 * nk, hipMemcpyDeviceToHost));
+  if (out_n) HIPCHK(hipMemcpy(out_n, p->own_n, 4ull * p->nq, hipMemcpyDeviceToHost));
+  return FG_OK;
+}
+
+int fg_plan_info_get(const fg_plan* p, fg_plan_info* o) {
+  if (!p || !o) return fail(FG_EINVAL, "bad arguments");
+  o->n_queries = p->nq;
+  o->k = p->k;
+  o->total_chunks = p->total_chunks;
+  o->workspace_bytes = p->ws_bytes;
+  return FG_OK;
+}
+
+int fg_plan_profile(fg_plan* p, int enable) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  p->profile = enable != 0;
+  return FG_OK;
+}
+
+int fg_plan_kernel_ms(fg_plan* p, double* ms_out, uint32_t* n_out) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  HIPCHK(hipSetDevice(p->ix->dev));
+  for (size_t i = 0; i + 3 < p->pending.size(); i += 4) {
+    HIPCHK(hipEventSynchronize(p->pending[i + 3]));
+    for (int kx = 0; kx < 3; ++kx) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, p->pending[i + kx], p->pending[i + kx + 1]));
+      p->ms[kx] += ms;
+    }
+    p->n_prof++;
+  }
+  for (hipEvent_t e : p->pending) (void)hipEventDestroy(e);
+  p->pending.clear();
+  if (ms_out) for (int kx = 0; kx < 3; ++kx) ms_out[kx] = p->ms[kx];
+  if (n_out) *n_out = p->n_prof;
+  p->ms[0] = p->ms[1] = p->ms[2] = 0;
+  p->n_prof = 0;
+  return FG_OK;
+}
+
+int fg_plan_destroy(fg_plan* p) {
+  delete p;
+  return FG_OK;
+}
+
+int fg_search_batch(fg_index* ix, const fg_query_batch* q, uint32_t k, float* out_score, uint32_t* out_doc,
+                    uint32_t* out_n) {
+  fg_plan* p = nullptr;
+  int rc = fg_plan_create(ix, q, k, &p);
+  if (rc) return rc;
+  std::unique_ptr<fg_plan> guard(p);
+  if ((rc = fg_plan_execute(p, nullptr, nullptr, nullptr, nullptr))) return rc;
+  return fg_plan_results(p, out_score, out_doc, out_n);
+}
+
+int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* d_score, const uint32_t* d_doc,
+                    const uint32_t* d_n, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_shard,
+                    uint32_t* d_out_n, void* stream) {
+  if (n_shards == 0 || n_shards > 64 || k == 0 || !d_score || !d_doc || !d_n || !d_out_score || !d_out_doc || !d_out_n)
+    return fail(FG_EINVAL, "bad arguments");
+  HIPCHK(fg::launch_merge(n_shards, n_queries, k, d_score, d_doc, d_n, d_out_score, d_out_doc, d_out_shard, d_out_n,
+                          static_cast<hipStream_t>(stream)));
+  return FG_OK;
+}
+
+// ---------------------------------------------------------------- bytes model
+int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out) {
+  if (!ix || !q || !out) return fail(FG_EINVAL, "bad arguments");
+  if (ix->h_doc.empty() && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
+  const double F = ix->has_name ? 2.0 : 1.0;
+  std::vector<uint32_t> S;
+  for (uint32_t i = 0; i < q->n_queries; ++i) {
+    const uint32_t b = q->q_off[i], m = q->q_off[i + 1] - b;
+    double* o = out + 4ull * i;
+    struct L { uint64_t n, off; uint32_t pos; };
+    std::vector<L> ls;
+    bool missing = false;
+    for (uint32_t j = 0; j < m; ++j) {
+      uint32_t t = q->terms[b + j];
+      if (t >= ix->n_terms || ix->off[t + 1] == ix->off[t]) { missing = true; break; }
+      ls.push_back(L{ix->off[t + 1] - ix->off[t], ix->off[t], j});
+    }
+    if (m == 0 || missing) { o[0] = o[1] = o[2] = o[3] = 0; continue; }
+    if (m == 1) {
+      double df = (double)ls[0].n;
+      o[0] = o[1] = 8.0 * df;
+      o[2] = 8.0 * df + 8.0 * std::min<double>(df, k);
+      o[3] = df;
+      continue;
+    }
+    std::stable_sort(ls.begin(), ls.end(), [](const L& x, const L& y) { return x.n < y.n; });
+    double bmerge = 0;
+    for (auto& l : ls) bmerge += 8.0 * (double)l.n;
+    double bskip = 8.0 * (double)ls[0].n;
+    S.assign(ix->h_doc.begin() + ls[0].off, ix->h_doc.begin() + ls[0].off + ls[0].n);
+    for (size_t t = 1; t < ls.size(); ++t) {
+      const uint32_t* d = ix->h_doc.data() + ls[t].off;
+      const uint64_t n = ls[t].n;
+      uint64_t blocks = 0, lb = 0;
+      int64_t last_block = -1;
+      size_t keep = 0;
+      for (size_t x = 0; x < S.size(); ++x) {
+        lb = std::lower_bound(d + lb, d + n, S[x]) - d;
+        if (lb < n) {
+          int64_t blk = (int64_t)(lb / fg::kBlock);
+          if (blk != last_block) { ++blocks; last_block = blk; }
+          if (d[lb] == S[x]) S[keep++] = S[x];
+        }
+      }
+      S.resize(keep);
+      bskip += 1024.0 * (double)blocks + 4.0 * (double)((n + fg::kBlock - 1) / fg::kBlock);
+    }
+    const double ns = (double)S.size();
+    o[0] = bmerge;
+    o[1] = bskip;
+    o[2] = std::min(bmerge, bskip) + F * ns + 8.0 * std::min<double>(ns, k);
+    o[3] = ns;
+  }
+  return FG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,332 @@
+"""ctypes binding of libfugu (include/fugu.h).
+
+Plumbing only: every search runs in libfugu.so's gfx950 kernels.  There is no
+Python or CPU fallback in this package -- if the library is missing the import
+fails, and if no gfx950 device is visible :class:`Context` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+# torch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1.  Only one HIP
+# runtime can own the device in a process, and libfugu's NEEDED
+# libamdhip64.so.7 binds by soname to whichever is loaded first: load torch's
+# first so torch (streams, RCCL) and libfugu share it (tools/diag_runtime.py).
+import torch  # noqa: F401,E402
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfugu.so")
+
+FG_OK = 0
+FG_EINVAL = -1
+FG_ENODEV = -2
+FG_EOOM = -3
+FG_EHIP = -4
+FG_EUNSUPPORTED = -5
+FG_MAX_TERMS = 16
+FG_MAX_K = 1024
+FG_TERM_MISSING = 0xFFFFFFFF
+MODE_AND = 0
+MODE_OR = 1
+
+# every symbol include/fugu.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "fg_device_count", "fg_ctx_create", "fg_ctx_destroy", "fg_last_error", "fg_version",
+    "fg_index_build_from_docs", "fg_index_build", "fg_index_retain", "fg_index_release",
+    "fg_index_stats_get", "fg_index_df", "fg_index_bm25",
+    "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
+    "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_destroy",
+    "fg_search_batch", "fg_merge_shards", "fg_bytes_model",
+)
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libfugu.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+        "(there is no CPU fallback for the device path)")
+
+_lib = C.CDLL(LIB_PATH)
+
+_p = C.c_void_p
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_u16p = C.POINTER(C.c_uint16)
+_u8p = C.POINTER(C.c_uint8)
+_f32p = C.POINTER(C.c_float)
+_f64p = C.POINTER(C.c_double)
+
+
+class DocsInput(C.Structure):
+    _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("text_off", _u64p), ("text_tok", _u32p),
+                ("name_off", _u64p), ("name_tok", _u32p), ("deleted", _u8p), ("threads", C.c_int),
+                ("keep_host_postings", C.c_int)]
+
+
+class IndexInput(C.Structure):
+    _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("term_off", _u64p), ("doc", _u32p),
+                ("tf_text", _u16p), ("tf_name", _u16p), ("fn_text", _u8p), ("fn_name", _u8p),
+                ("tot_tokens", C.c_uint64 * 2), ("deleted", _u8p)]
+
+
+class QueryBatch(C.Structure):
+    _fields_ = [("n_queries", C.c_uint32), ("q_off", _u32p), ("terms", _u32p), ("mode", C.c_int)]
+
+
+class IndexStats(C.Structure):
+    _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("n_postings", C.c_uint64),
+                ("device_bytes", C.c_uint64), ("tot_tokens", C.c_uint64 * 2), ("avgdl", C.c_float * 2),
+                ("has_name", C.c_int), ("device", C.c_int)]
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("n_queries", C.c_uint32), ("k", C.c_uint32), ("total_chunks", C.c_uint32),
+                ("workspace_bytes", C.c_uint64)]
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_sig("fg_device_count", C.c_int, C.POINTER(C.c_int))
+_sig("fg_ctx_create", C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(_p))
+_sig("fg_ctx_destroy", C.c_int, _p)
+_sig("fg_last_error", C.c_char_p)
+_sig("fg_version", C.c_char_p)
+_sig("fg_index_build_from_docs", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(_p))
+_sig("fg_index_build", C.c_int, _p, C.c_int, C.POINTER(IndexInput), C.POINTER(_p))
+_sig("fg_index_retain", C.c_int, _p)
+_sig("fg_index_release", C.c_int, _p)
+_sig("fg_index_stats_get", C.c_int, _p, C.POINTER(IndexStats))
+_sig("fg_index_df", C.c_uint64, _p, C.c_int, C.c_uint32)
+_sig("fg_index_bm25", C.c_int, _p, C.c_uint32, _f32p, _f32p, _f32p)
+_sig("fg_plan_create", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
+_sig("fg_plan_execute", C.c_int, _p, _p, _p, _p, _p)
+_sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
+_sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
+_sig("fg_plan_profile", C.c_int, _p, C.c_int)
+_sig("fg_plan_kernel_ms", C.c_int, _p, _f64p, _u32p)
+_sig("fg_plan_destroy", C.c_int, _p)
+_sig("fg_search_batch", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f32p, _u32p, _u32p)
+_sig("fg_merge_shards", C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p)
+_sig("fg_bytes_model", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f64p)
+
+
+class FuguError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libfugu error {code}: {msg}")
+        self.code = code
+
+
+class Unsupported(FuguError):
+    """FG_EUNSUPPORTED: the query is outside the device subset (host CPU path)."""
+
+
+def _check(rc: int):
+    if rc != FG_OK:
+        msg = (_lib.fg_last_error() or b"").decode(errors="replace")
+        if rc == FG_EUNSUPPORTED:
+            raise Unsupported(rc, msg)
+        raise FuguError(rc, msg)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def lib():
+    return _lib
+
+
+def version() -> str:
+    return _lib.fg_version().decode()
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(_lib.fg_device_count(C.byref(n)))
+    return n.value
+
+
+class Context:
+    def __init__(self, devices=(0,)):
+        devs = (C.c_int * len(devices))(*devices)
+        h = _p()
+        _check(_lib.fg_ctx_create(len(devices), devs, C.byref(h)))
+        self._h = h
+        self.devices = tuple(devices)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            _lib.fg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class Stats:
+    n_docs: int
+    n_terms: int
+    n_postings: int
+    device_bytes: int
+    tot_tokens: tuple
+    avgdl: tuple
+    has_name: bool
+    device: int
+
+
+def _u64(a):
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+class Index:
+    """An immutable device snapshot of one namespace's docs index."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def from_docs(cls, ctx: Context, text_off, text_tok, n_terms: int, name_off=None, name_tok=None,
+                  deleted=None, device: int | None = None, threads: int = 0, keep_host: bool = True):
+        text_off = _u64(text_off)
+        text_tok = _u32(text_tok)
+        name_off = None if name_off is None else _u64(name_off)
+        name_tok = None if name_tok is None else _u32(name_tok)
+        deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint8)
+        n_docs = len(text_off) - 1
+        inp = DocsInput(n_docs, n_terms, _ptr(text_off, _u64p), _ptr(text_tok, _u32p), _ptr(name_off, _u64p),
+                        _ptr(name_tok, _u32p), _ptr(deleted, _u8p), threads, 1 if keep_host else 0)
+        h = _p()
+        dev = ctx.devices[0] if device is None else device
+        _check(_lib.fg_index_build_from_docs(ctx.handle, dev, C.byref(inp), C.byref(h)))
+        return cls(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stats(self) -> Stats:
+        s = IndexStats()
+        _check(_lib.fg_index_stats_get(self._h, C.byref(s)))
+        return Stats(s.n_docs, s.n_terms, s.n_postings, s.device_bytes, tuple(s.tot_tokens), tuple(s.avgdl),
+                     bool(s.has_name), s.device)
+
+    def df(self, term: int, field: int = -1) -> int:
+        return int(_lib.fg_index_df(self._h, field, term))
+
+    def bm25(self, term: int):
+        wt, wn = C.c_float(), C.c_float()
+        cache = np.zeros(512, np.float32)
+        _check(_lib.fg_index_bm25(self._h, term, C.byref(wt), C.byref(wn), _ptr(cache, _f32p)))
+        return wt.value, wn.value, cache
+
+    def plan(self, q_off, terms, k: int, mode: int = MODE_AND) -> "Plan":
+        return Plan(self, q_off, terms, k, mode)
+
+    def search_batch(self, q_off, terms, k: int, mode: int = MODE_AND):
+        q_off = _u32(q_off)
+        terms = _u32(terms)
+        nq = len(q_off) - 1
+        qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode)
+        score = np.zeros(nq * k, np.float32)
+        doc = np.zeros(nq * k, np.uint32)
+        n = np.zeros(nq, np.uint32)
+        _check(_lib.fg_search_batch(self._h, C.byref(qb), k, _ptr(score, _f32p), _ptr(doc, _u32p), _ptr(n, _u32p)))
+        return score.reshape(nq, k), doc.reshape(nq, k), n
+
+    def bytes_model(self, q_off, terms, k: int, mode: int = MODE_AND):
+        q_off = _u32(q_off)
+        terms = _u32(terms)
+        nq = len(q_off) - 1
+        qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode)
+        out = np.zeros(4 * nq, np.float64)
+        _check(_lib.fg_bytes_model(self._h, C.byref(qb), k, _ptr(out, _f64p)))
+        return out.reshape(nq, 4)
+
+    def close(self):
+        if self._h:
+            _lib.fg_index_release(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Plan:
+    """A batch planned on the host and resident in HBM (fg_plan_create)."""
+
+    def __init__(self, index: Index, q_off, terms, k: int, mode: int = MODE_AND):
+        self._q_off = _u32(q_off)
+        self._terms = _u32(terms)
+        self.n_queries = len(self._q_off) - 1
+        self.k = k
+        qb = QueryBatch(self.n_queries, _ptr(self._q_off, _u32p), _ptr(self._terms, _u32p), mode)
+        h = _p()
+        _check(_lib.fg_plan_create(index.handle, C.byref(qb), k, C.byref(h)))
+        self._h = h
+        self.index = index
+
+    def info(self) -> PlanInfo:
+        i = PlanInfo()
+        _check(_lib.fg_plan_info_get(self._h, C.byref(i)))
+        return i
+
+    def execute(self, stream: int | None = None, out_score: int | None = None, out_doc: int | None = None,
+                out_n: int | None = None):
+        """Asynchronous launch; `stream` and outputs are raw device addresses (ints)."""
+        _check(_lib.fg_plan_execute(self._h, stream, out_score, out_doc, out_n))
+
+    def results(self):
+        nq, k = self.n_queries, self.k
+        score = np.zeros(nq * k, np.float32)
+        doc = np.zeros(nq * k, np.uint32)
+        n = np.zeros(nq, np.uint32)
+        _check(_lib.fg_plan_results(self._h, _ptr(score, _f32p), _ptr(doc, _u32p), _ptr(n, _u32p)))
+        return score.reshape(nq, k), doc.reshape(nq, k), n
+
+    def profile(self, enable: bool = True):
+        _check(_lib.fg_plan_profile(self._h, 1 if enable else 0))
+
+    def kernel_ms(self):
+        ms = np.zeros(3, np.float64)
+        n = C.c_uint32(0)
+        _check(_lib.fg_plan_kernel_ms(self._h, _ptr(ms, _f64p), C.byref(n)))
+        return ms, n.value
+
+    def close(self):
+        if self._h:
+            _lib.fg_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def merge_shards(n_shards: int, n_queries: int, k: int, d_score: int, d_doc: int, d_n: int, d_out_score: int,
+                 d_out_doc: int, d_out_shard: int | None, d_out_n: int, stream: int | None = None):
+    _check(_lib.fg_merge_shards(n_shards, n_queries, k, d_score, d_doc, d_n, d_out_score, d_out_doc, d_out_shard,
+                                d_out_n, stream))

@@ -1,0 +1,174 @@
+/*
+ * fugu.h -- C ABI of libfugu: MI355X (gfx950) execution of fugu's query hot
+ * path (conjunctive posting-list intersection + BM25 + top-k).
+ *
+ * Drop-in boundary.  In fugu the replaceable call is
+ *     searcher.search(&base_query, &TopDocs::with_limit(offset + per_page))
+ * inside Dataset::search (reference src/db/search.rs:74-218, the call at
+ * :162), reached from perform_search (src/server/handlers/search.rs:350-402)
+ * and search_endpoint (:152-207).  A host (Rust over `extern "C"`, or the C++
+ * host in fugu_amd/csrc/host.cpp) keeps query parsing, the term dictionary and
+ * doc fetch, and calls this library for step A.4 of SURVEY.md §3.  The Rust
+ * binding a maintainer would add is written out in INTEGRATION.md.
+ *
+ * Conventions: plain pointers and sizes; 0 = FG_OK, negative = error (message
+ * in fg_last_error(), thread-local).  The caller owns every host buffer; the
+ * library copies inputs.  Handles own device memory.  An fg_index is an
+ * immutable, refcounted snapshot (tantivy Searcher semantics: a reader keeps
+ * the segments it opened, src/db/core.rs:290-297).  All entry points are
+ * thread-safe per handle except fg_plan_* on the SAME plan.
+ */
+#ifndef FUGU_H
+#define FUGU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FG_OK 0
+#define FG_EINVAL (-1)        /* bad argument (e.g. k == 0: tantivy asserts limit >= 1) */
+#define FG_ENODEV (-2)        /* no usable gfx950 device */
+#define FG_EOOM (-3)          /* host or device allocation failed */
+#define FG_EHIP (-4)          /* HIP runtime error */
+#define FG_EUNSUPPORTED (-5)  /* query outside the device subset: the host runs its CPU path */
+
+#define FG_MAX_TERMS 16        /* terms per query on the device path */
+#define FG_MAX_K 1024          /* largest k on the device path */
+#define FG_TERM_MISSING 0xFFFFFFFFu /* a query term absent from the term dictionary */
+
+#define FG_MODE_AND 0 /* `t1 AND t2 ...` / `+t1 +t2`: Must clauses (src/db/search.rs:112 parser) */
+#define FG_MODE_OR 1  /* `t1 t2 ...`: the parser's default Should conjunction */
+
+#define FG_FIELD_TEXT 0
+#define FG_FIELD_NAME 1
+
+typedef struct fg_ctx fg_ctx;
+typedef struct fg_index fg_index;
+typedef struct fg_plan fg_plan;
+
+/* ---- context ------------------------------------------------------------ */
+/* Replaces: nothing in fugu (single process, no devices); the per-process
+ * state the Rust AppState (src/server/server_main.rs:16-19) would hold. */
+int fg_device_count(int* out);
+int fg_ctx_create(int ndev, const int* devs, fg_ctx** out);
+int fg_ctx_destroy(fg_ctx* ctx);
+const char* fg_last_error(void);
+const char* fg_version(void);
+
+/* ---- index snapshot ------------------------------------------------------ */
+/* Documents as analyzed token streams: for each doc the term ids produced by
+ * the "default" analyzer (SimpleTokenizer -> RemoveLong(40) -> LowerCaser) on
+ * the `text` and `name` fields, in order.  This is what NamedIndex::upsert
+ * feeds tantivy (src/db/document.rs:23-67, build_full_document :116-139).
+ * Field lengths (token counts) become fieldnorms; tf = occurrences. */
+typedef struct fg_docs_input {
+  uint32_t n_docs;
+  uint32_t n_terms;          /* vocabulary size: every token < n_terms */
+  const uint64_t* text_off;  /* [n_docs+1] */
+  const uint32_t* text_tok;  /* [text_off[n_docs]] */
+  const uint64_t* name_off;  /* [n_docs+1] or NULL (no `name` values) */
+  const uint32_t* name_tok;  /* or NULL */
+  const uint8_t* deleted;    /* [n_docs] 1 = deleted-not-merged, or NULL */
+  int threads;               /* host threads for the inversion (<= 0: all) */
+  int keep_host_postings;    /* keep a host copy (needed by fg_bytes_model) */
+} fg_docs_input;
+
+/* Replaces: Index::open_or_create + IndexWriter commit + Searcher snapshot
+ * (src/db/core.rs:229-267, :290-297).  Builds the HBM layout of DESIGN.md on
+ * device `dev` of ctx. */
+int fg_index_build_from_docs(fg_ctx* ctx, int dev, const fg_docs_input* in, fg_index** out);
+
+/* Postings already inverted by the host (SURVEY.md §8b proposal): merged
+ * text U name postings per term, CSR by term id, docs ascending. */
+typedef struct fg_index_input {
+  uint32_t n_docs;
+  uint32_t n_terms;
+  const uint64_t* term_off;  /* [n_terms+1] */
+  const uint32_t* doc;       /* [term_off[n_terms]] */
+  const uint16_t* tf_text;   /* 0 when the doc has the term only in `name` */
+  const uint16_t* tf_name;   /* 0 when the doc has the term only in `text` */
+  const uint8_t* fn_text;    /* [n_docs] fieldnorm ids (fieldnorm/code.rs) */
+  const uint8_t* fn_name;    /* [n_docs] */
+  uint64_t tot_tokens[2];    /* total_num_tokens of text / name, deleted docs included */
+  const uint8_t* deleted;    /* [n_docs] or NULL */
+} fg_index_input;
+int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out);
+
+int fg_index_retain(fg_index* ix);
+int fg_index_release(fg_index* ix);
+
+typedef struct fg_index_stats {
+  uint32_t n_docs;
+  uint32_t n_terms;
+  uint64_t n_postings;
+  uint64_t device_bytes;
+  uint64_t tot_tokens[2];
+  float avgdl[2];
+  int has_name;
+  int device;
+} fg_index_stats;
+int fg_index_stats_get(const fg_index* ix, fg_index_stats* out);
+/* doc_freq of `term` in `field` (tantivy Searcher::doc_freq), and the merged
+ * (text U name) posting-list length when field < 0. */
+uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term);
+/* Bm25Weight pieces the device uses, for host-side checks. */
+int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512);
+
+/* ---- query batches -------------------------------------------------------- */
+typedef struct fg_query_batch {
+  uint32_t n_queries;
+  const uint32_t* q_off;  /* [n_queries+1] */
+  const uint32_t* terms;  /* term ids in query order; FG_TERM_MISSING allowed */
+  int mode;               /* FG_MODE_AND or FG_MODE_OR (OR: single-term only in v1) */
+} fg_query_batch;
+
+/* Plan a batch: host-side query planning (tantivy Weight creation: terms
+ * ordered by cost, query/intersection.rs) and upload of the plan to HBM.
+ * Returns FG_EUNSUPPORTED for queries outside the device subset (empty query
+ * = AllQuery, > FG_MAX_TERMS terms, multi-term OR, k > FG_MAX_K). */
+int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out);
+/* Run a planned batch on `stream` (hipStream_t, NULL = default stream).
+ * Outputs are device pointers [n_queries*k], [n_queries*k], [n_queries]; NULL
+ * outputs use the plan's own buffers.  Asynchronous. */
+int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_n);
+/* Copy the plan's own result buffers to host (synchronises the plan's stream). */
+int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n);
+typedef struct fg_plan_info {
+  uint32_t n_queries;
+  uint32_t k;
+  uint32_t total_chunks;
+  uint64_t workspace_bytes;
+} fg_plan_info;
+int fg_plan_info_get(const fg_plan* p, fg_plan_info* out);
+/* Per-kernel HIP-event timing of every execute while enabled.  ms_out[3] =
+ * summed device time of (k_conj, k_filter, k_final); *n_out = executes. */
+int fg_plan_profile(fg_plan* p, int enable);
+int fg_plan_kernel_ms(fg_plan* p, double* ms_out, uint32_t* n_out);
+int fg_plan_destroy(fg_plan* p);
+
+/* Synchronous convenience: plan + execute + copy back.  Host buffers
+ * out_score/out_doc [n_queries*k] in (score desc, doc asc) order, out_n
+ * [n_queries] = min(k, hits).  This is the call Dataset::search would make in
+ * place of searcher.search(..., TopDocs::with_limit(k)). */
+int fg_search_batch(fg_index* ix, const fg_query_batch* q, uint32_t k, float* out_score, uint32_t* out_doc,
+                    uint32_t* out_n);
+
+/* Cross-shard merge: per-shard top-k lists gathered from
+ * n_shards GPUs (RCCL all-gather) merged into the global top-k by (score
+ * desc, shard asc, doc asc).  Device pointers, layout [n_shards][n_queries][k]
+ * and [n_shards][n_queries]. */
+int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* d_score, const uint32_t* d_doc,
+                    const uint32_t* d_n, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_shard,
+                    uint32_t* d_out_n, void* stream);
+
+/* SURVEY.md §8(d) algorithmic bytes per query: out[4*i..] = {B_merge, B_skip,
+ * B, |I|}.  Host analysis over the host posting copy (keep_host_postings). */
+int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FUGU_H */

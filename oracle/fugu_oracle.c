@@ -1,0 +1,637 @@
+/*
+ * fugu_oracle.c -- CPU ORACLE / TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the query path fugu delegates to tantivy 0.24.1
+ * (crates.io, Cargo.lock:4609-4612; not vendored under /root/reference):
+ *   fugu call site  : src/db/search.rs:108-127 (QueryParser over [text,name]),
+ *                     src/db/search.rs:154-162 (TopDocs::with_limit(offset+per_page)),
+ *                     src/db/schemas.rs:10,14 (text/name = TEXT|STORED),
+ *                     src/db/document.rs:116-139 (what is indexed into text/name).
+ *   upstream pieces restated:
+ *     fieldnorm/code.rs      FIELD_NORMS_TABLE, fieldnorm_to_id      -> or_fieldnorm_*
+ *     query/bm25.rs          idf, Bm25Weight, tf cache               -> or_idf, bm25_*
+ *     postings/{segment_postings,skip}.rs: 128-doc blocks + last_doc skip    -> TermCur
+ *     query/union/           Should(text:t, name:t), SumCombiner     -> UnionCur
+ *     query/intersection.rs  leapfrog, children sorted by cost       -> conj_search
+ *     collector/top_*.rs     TopNComputer (2K buffer, median cut)    -> TopN
+ *
+ * PARITY STATUS: "parity unpinned" -- the reference ships no test, fixture or
+ * golden vector for this path and cannot be built or
+ * imported here (no rustc/cargo, tantivy not vendored).  The restatement is
+ * pinned to the hand-derived known-answer test of SURVEY.md Appendix C and
+ * cross-checked against an independent numpy restatement
+ * (tests/golden/gen_golden.py) on small corpora.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library.  It is the checker and the CPU baseline, never the
+ * product path.  Deliberate simplification vs tantivy (documented in
+ * DESIGN.md): blocks hold raw u32 doc ids / tfs instead of bitpacked deltas,
+ * which makes this baseline FASTER than tantivy, never slower.
+ *
+ * Build: oracle/Makefile (gcc -O3 -march=native -ffp-contract=off).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define OR_BLOCK 128u
+#define OR_TERMINATED 0x7FFFFFFFu /* tantivy: TERMINATED = i32::MAX as u32 */
+#define OR_MAX_TERMS 64
+
+static const float OR_K1 = 1.2f; /* query/bm25.rs K1 */
+static const float OR_B = 0.75f; /* query/bm25.rs B */
+
+/* ---------------------------------------------------------------- fieldnorm */
+/* fieldnorm/code.rs: 0..=40 exact, then groups of 8 with step 2,4,8,...; 256 entries. */
+static uint32_t g_table[256];
+static int g_table_ready = 0;
+
+static void table_init(void) {
+  if (g_table_ready) return;
+  uint32_t i = 0;
+  for (; i <= 40; ++i) g_table[i] = i;
+  uint64_t v = 40, step = 2;
+  while (i < 256) {
+    for (int j = 0; j < 8 && i < 256; ++j) { v += step; g_table[i++] = (uint32_t)v; }
+    step <<= 1;
+  }
+  g_table_ready = 1;
+}
+
+void or_fieldnorm_table(uint32_t* out) { table_init(); memcpy(out, g_table, sizeof g_table); }
+
+/* FIELD_NORMS_TABLE.binary_search(n).unwrap_or_else(|i| i - 1) */
+uint8_t or_fieldnorm_to_id(uint32_t n) {
+  table_init();
+  uint32_t lo = 0, hi = 256; /* first index with table > n */
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (g_table[mid] <= n) lo = mid + 1; else hi = mid;
+  }
+  return (uint8_t)(lo - 1);
+}
+
+/* ---------------------------------------------------------------- bm25 */
+/* bm25.rs idf(): ((N - df) as f32 + 0.5) / (df as f32 + 0.5), then (1 + x).ln() */
+float or_idf(uint64_t df, uint64_t n) {
+  float x = ((float)(n - df) + 0.5f) / ((float)df + 0.5f);
+  return logf(1.0f + x);
+}
+
+/* Bm25Weight::new: idf * (1 + K1) (boost 1.0 multiplies exactly) */
+float or_term_weight(uint64_t df, uint64_t n) { return or_idf(df, n) * (1.0f + OR_K1); }
+
+/* compute_tf_cache: K1 * (1 - B + B * fieldnorm as f32 / avg) */
+void or_bm25_cache(float avgdl, float* out) {
+  table_init();
+  for (int i = 0; i < 256; ++i) out[i] = OR_K1 * ((1.0f - OR_B) + (OR_B * (float)g_table[i]) / avgdl);
+}
+
+/* ---------------------------------------------------------------- index */
+typedef struct {
+  uint32_t n;        /* doc_freq in this field */
+  uint32_t* doc;     /* sorted doc ids */
+  uint32_t* tf;      /* term freqs */
+  uint32_t* last;    /* skip list: last doc of each 128-doc block */
+} Postings;
+
+typedef struct or_index {
+  uint32_t n_docs, n_terms;
+  int has_name;
+  Postings* fld[2];         /* [0]=text, [1]=name, each [n_terms] */
+  uint32_t* store_doc[2];
+  uint32_t* store_tf[2];
+  uint32_t* store_last[2];
+  uint8_t* fn[2];           /* fieldnorm ids [n_docs] */
+  uint8_t* deleted;         /* nullable [n_docs] */
+  uint64_t tot[2];          /* total_num_tokens per field (deleted docs included) */
+  float avgdl[2];
+  float cache[2][256];
+} or_index;
+
+typedef struct {
+  const uint64_t* off;
+  const uint32_t* tok;
+  uint32_t n_docs, n_terms;
+  uint32_t b, e;
+  uint32_t* df;   /* per-thread counts [n_terms] */
+  uint64_t* pos;  /* per-thread write cursors [n_terms] (fill pass) */
+  Postings* post;
+  int pass;
+} BuildJob;
+
+static int cmp_u32(const void* a, const void* b) {
+  uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  return (x > y) - (x < y);
+}
+
+static void* build_worker(void* arg) {
+  BuildJob* j = (BuildJob*)arg;
+  uint32_t buf[4096];
+  for (uint32_t d = j->b; d < j->e; ++d) {
+    uint64_t s = j->off[d], e = j->off[d + 1];
+    uint32_t len = (uint32_t)(e - s);
+    uint32_t* t = len <= 4096 ? buf : (uint32_t*)malloc(sizeof(uint32_t) * len);
+    memcpy(t, j->tok + s, sizeof(uint32_t) * len);
+    qsort(t, len, sizeof(uint32_t), cmp_u32);
+    for (uint32_t i = 0; i < len;) {
+      uint32_t k = i;
+      while (k < len && t[k] == t[i]) ++k;
+      uint32_t term = t[i];
+      if (j->pass == 0) {
+        j->df[term]++;
+      } else {
+        uint64_t p = j->pos[term]++;
+        Postings* P = &j->post[term];
+        P->doc[p] = d;
+        P->tf[p] = k - i;
+      }
+      i = k;
+    }
+    if (t != buf) free(t);
+  }
+  return NULL;
+}
+
+static int build_field(or_index* ix, int f, const uint64_t* off, const uint32_t* tok, int threads) {
+  uint32_t nt = ix->n_terms, nd = ix->n_docs;
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  BuildJob* jobs = (BuildJob*)calloc((size_t)threads, sizeof(BuildJob));
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  uint32_t step = (nd + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].off = off; jobs[t].tok = tok; jobs[t].n_docs = nd; jobs[t].n_terms = nt;
+    jobs[t].b = t * step < nd ? t * step : nd;
+    jobs[t].e = (t + 1) * step < nd ? (t + 1) * step : nd;
+    jobs[t].df = (uint32_t*)calloc(nt, sizeof(uint32_t));
+    jobs[t].pos = (uint64_t*)calloc(nt, sizeof(uint64_t));
+    jobs[t].pass = 0;
+  }
+  for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, build_worker, &jobs[t]);
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  /* term df and per-thread start offsets */
+  Postings* post = (Postings*)calloc(nt, sizeof(Postings));
+  uint64_t total = 0, nblocks = 0;
+  for (uint32_t term = 0; term < nt; ++term) {
+    uint64_t df = 0;
+    for (int t = 0; t < threads; ++t) { jobs[t].pos[term] = df; df += jobs[t].df[term]; }
+    post[term].n = (uint32_t)df;
+    total += df;
+    nblocks += (df + OR_BLOCK - 1) / OR_BLOCK;
+  }
+  uint32_t* sdoc = (uint32_t*)malloc(sizeof(uint32_t) * (total ? total : 1));
+  uint32_t* stf = (uint32_t*)malloc(sizeof(uint32_t) * (total ? total : 1));
+  uint32_t* slast = (uint32_t*)malloc(sizeof(uint32_t) * (nblocks ? nblocks : 1));
+  if (!sdoc || !stf || !slast) return -1;
+  uint64_t o = 0, ob = 0;
+  for (uint32_t term = 0; term < nt; ++term) {
+    post[term].doc = sdoc + o; post[term].tf = stf + o; post[term].last = slast + ob;
+    o += post[term].n;
+    ob += (post[term].n + OR_BLOCK - 1) / OR_BLOCK;
+  }
+  for (int t = 0; t < threads; ++t) { jobs[t].post = post; jobs[t].pass = 1; }
+  for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, build_worker, &jobs[t]);
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  for (uint32_t term = 0; term < nt; ++term) {
+    Postings* P = &post[term];
+    uint32_t nb = (P->n + OR_BLOCK - 1) / OR_BLOCK;
+    for (uint32_t b = 0; b < nb; ++b) {
+      uint32_t end = (b + 1) * OR_BLOCK < P->n ? (b + 1) * OR_BLOCK : P->n;
+      P->last[b] = P->doc[end - 1];
+    }
+  }
+  for (int t = 0; t < threads; ++t) { free(jobs[t].df); free(jobs[t].pos); }
+  free(jobs); free(th);
+  ix->fld[f] = post; ix->store_doc[f] = sdoc; ix->store_tf[f] = stf; ix->store_last[f] = slast;
+  /* fieldnorms: number of tokens that reached the index (post-filter count) */
+  ix->fn[f] = (uint8_t*)malloc(nd ? nd : 1);
+  uint64_t tot = 0;
+  for (uint32_t d = 0; d < nd; ++d) {
+    uint64_t len = off ? off[d + 1] - off[d] : 0;
+    tot += len;
+    ix->fn[f][d] = or_fieldnorm_to_id(len > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)len);
+  }
+  ix->tot[f] = tot;
+  return 0;
+}
+
+void or_index_free(or_index* ix) {
+  if (!ix) return;
+  for (int f = 0; f < 2; ++f) {
+    free(ix->fld[f]); free(ix->store_doc[f]); free(ix->store_tf[f]); free(ix->store_last[f]); free(ix->fn[f]);
+  }
+  free(ix->deleted);
+  free(ix);
+}
+
+/*
+ * text_off/text_tok: per-doc token term ids of the `text` field (after the
+ * "default" analyzer), name_* likewise for `name` (nullable: no name field
+ * values).  deleted: nullable, 1 = deleted-not-yet-merged (still counted in
+ * N/df/total tokens, excluded from results: Appendix A.7).
+ */
+or_index* or_index_build(uint32_t n_docs, uint32_t n_terms, const uint64_t* text_off, const uint32_t* text_tok,
+                         const uint64_t* name_off, const uint32_t* name_tok, const uint8_t* deleted, int threads) {
+  table_init();
+  or_index* ix = (or_index*)calloc(1, sizeof(or_index));
+  ix->n_docs = n_docs; ix->n_terms = n_terms;
+  static const uint64_t zero_off_dummy = 0;
+  (void)zero_off_dummy;
+  if (build_field(ix, 0, text_off, text_tok, threads)) { or_index_free(ix); return NULL; }
+  if (name_off && name_tok) {
+    if (build_field(ix, 1, name_off, name_tok, threads)) { or_index_free(ix); return NULL; }
+    ix->has_name = 1;
+  } else {
+    /* empty name field: every doc has fieldnorm 0, no postings */
+    ix->fld[1] = (Postings*)calloc(n_terms, sizeof(Postings));
+    ix->fn[1] = (uint8_t*)calloc(n_docs ? n_docs : 1, 1);
+    ix->tot[1] = 0;
+  }
+  if (deleted) {
+    ix->deleted = (uint8_t*)malloc(n_docs ? n_docs : 1);
+    memcpy(ix->deleted, deleted, n_docs);
+  }
+  for (int f = 0; f < 2; ++f) {
+    ix->avgdl[f] = (float)ix->tot[f] / (float)n_docs; /* total_num_tokens as f32 / N as f32 */
+    or_bm25_cache(ix->avgdl[f], ix->cache[f]);
+  }
+  return ix;
+}
+
+uint32_t or_df(const or_index* ix, int field, uint32_t term) { return term < ix->n_terms ? ix->fld[field][term].n : 0; }
+uint64_t or_total_tokens(const or_index* ix, int field) { return ix->tot[field]; }
+float or_avgdl(const or_index* ix, int field) { return ix->avgdl[field]; }
+void or_cache(const or_index* ix, int field, float* out) { memcpy(out, ix->cache[field], sizeof(float) * 256); }
+uint8_t or_fieldnorm_id_of(const or_index* ix, int field, uint32_t doc) { return ix->fn[field][doc]; }
+
+/* ---------------------------------------------------------------- cursors */
+typedef struct {
+  const Postings* p;
+  uint32_t cur;
+  float weight;
+  const float* cache;
+  const uint8_t* fn;
+} TermCur;
+
+static inline uint32_t tc_doc(const TermCur* c) { return c->cur < c->p->n ? c->p->doc[c->cur] : OR_TERMINATED; }
+static inline uint32_t tc_advance(TermCur* c) { if (c->cur < c->p->n) c->cur++; return tc_doc(c); }
+
+/* SegmentPostings::seek: skip reader walks block last_doc entries forward, then
+ * searches inside the block. */
+static uint32_t tc_seek(TermCur* c, uint32_t target) {
+  uint32_t d = tc_doc(c);
+  if (d >= target) return d;
+  const Postings* p = c->p;
+  uint32_t nb = (p->n + OR_BLOCK - 1) / OR_BLOCK;
+  uint32_t b = c->cur / OR_BLOCK;
+  while (b < nb && p->last[b] < target) ++b;
+  if (b == nb) { c->cur = p->n; return OR_TERMINATED; }
+  uint32_t lo = b * OR_BLOCK > c->cur ? b * OR_BLOCK : c->cur;
+  uint32_t hi = (b + 1) * OR_BLOCK < p->n ? (b + 1) * OR_BLOCK : p->n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (p->doc[mid] < target) lo = mid + 1; else hi = mid;
+  }
+  c->cur = lo;
+  return tc_doc(c);
+}
+
+/* Bm25Weight::score(fieldnorm_id, tf) = weight * (tf / (tf + cache[id])) */
+static inline float tc_score(const TermCur* c) {
+  uint32_t d = c->p->doc[c->cur];
+  float tf = (float)c->p->tf[c->cur];
+  float norm = c->cache[c->fn[d]];
+  return c->weight * (tf / (tf + norm));
+}
+
+/* One query term over default fields [text, name]: Should(text:t, name:t),
+ * BufferedUnionScorer with SumCombiner (score starts at 0.0). */
+typedef struct {
+  TermCur f[2];
+  uint32_t doc;
+  uint64_t cost; /* DocSet::cost of a union = sum of children (df_text + df_name) */
+} UnionCur;
+
+static inline uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+static void uc_init(UnionCur* u, const or_index* ix, uint32_t term) {
+  uint64_t n = ix->n_docs;
+  for (int f = 0; f < 2; ++f) {
+    static const Postings empty = {0, NULL, NULL, NULL};
+    u->f[f].p = term < ix->n_terms ? &ix->fld[f][term] : &empty;
+    u->f[f].cur = 0;
+    u->f[f].weight = or_term_weight(u->f[f].p->n, n);
+    u->f[f].cache = ix->cache[f];
+    u->f[f].fn = ix->fn[f];
+  }
+  u->doc = min_u32(tc_doc(&u->f[0]), tc_doc(&u->f[1]));
+  u->cost = (uint64_t)u->f[0].p->n + u->f[1].p->n;
+}
+static inline uint32_t uc_advance(UnionCur* u) {
+  for (int f = 0; f < 2; ++f) if (tc_doc(&u->f[f]) == u->doc) tc_advance(&u->f[f]);
+  u->doc = min_u32(tc_doc(&u->f[0]), tc_doc(&u->f[1]));
+  return u->doc;
+}
+static inline uint32_t uc_seek(UnionCur* u, uint32_t target) {
+  if (u->doc >= target) return u->doc;
+  tc_seek(&u->f[0], target);
+  tc_seek(&u->f[1], target);
+  u->doc = min_u32(tc_doc(&u->f[0]), tc_doc(&u->f[1]));
+  return u->doc;
+}
+static inline float uc_score(const UnionCur* u) {
+  float s = 0.0f;
+  for (int f = 0; f < 2; ++f) if (tc_doc(&u->f[f]) == u->doc) s += tc_score(&u->f[f]);
+  return s;
+}
+
+/* ---------------------------------------------------------------- TopN */
+typedef struct { float score; uint32_t doc; } Hit;
+
+/* ComparableDoc ordering with REVERSE_ORDER: score descending, then doc ascending */
+static int hit_cmp(const void* a, const void* b) {
+  const Hit* x = (const Hit*)a; const Hit* y = (const Hit*)b;
+  if (x->score > y->score) return -1;
+  if (x->score < y->score) return 1;
+  return (x->doc > y->doc) - (x->doc < y->doc);
+}
+
+typedef struct {
+  Hit* buf;
+  uint32_t len, top_n, cap;
+  int has_thr;
+  float thr;
+} TopN;
+
+static void topn_init(TopN* t, uint32_t k) {
+  t->top_n = k; t->cap = 2 * k; t->len = 0; t->has_thr = 0; t->thr = -3.40282347e+38f;
+  t->buf = (Hit*)malloc(sizeof(Hit) * t->cap);
+}
+/* truncate_top_n: the element at sorted index top_n becomes the threshold */
+static float topn_truncate(TopN* t) {
+  qsort(t->buf, t->len, sizeof(Hit), hit_cmp);
+  float median = t->buf[t->top_n].score;
+  t->len = t->top_n;
+  t->thr = median; t->has_thr = 1;
+  return median;
+}
+static void topn_push(TopN* t, float score, uint32_t doc) {
+  if (t->has_thr && score < t->thr) return;
+  if (t->len == t->cap) topn_truncate(t);
+  t->buf[t->len].score = score; t->buf[t->len].doc = doc; t->len++;
+}
+static uint32_t topn_finish(TopN* t, float* out_score, uint32_t* out_doc) {
+  if (t->len > t->top_n) topn_truncate(t);
+  qsort(t->buf, t->len, sizeof(Hit), hit_cmp);
+  for (uint32_t i = 0; i < t->len; ++i) { out_score[i] = t->buf[i].score; out_doc[i] = t->buf[i].doc; }
+  uint32_t n = t->len;
+  free(t->buf);
+  return n;
+}
+/* the callback of for_each_pruning: push, return the current threshold */
+static inline float collect(TopN* t, const or_index* ix, uint32_t doc, float score) {
+  if (!(ix->deleted && ix->deleted[doc])) topn_push(t, score, doc);
+  return t->has_thr ? t->thr : -3.40282347e+38f;
+}
+
+/* ---------------------------------------------------------------- search */
+typedef struct { UnionCur* c; uint64_t cost; uint32_t qpos; } Child;
+
+static int child_cmp(const void* a, const void* b) {
+  const Child* x = (const Child*)a; const Child* y = (const Child*)b;
+  if (x->cost != y->cost) return x->cost < y->cost ? -1 : 1;
+  return (x->qpos > y->qpos) - (x->qpos < y->qpos); /* sort_by_key is stable */
+}
+
+/* intersection.rs go_to_first_doc */
+static uint32_t go_to_first_doc(UnionCur** ds, uint32_t n) {
+  uint32_t cand = 0;
+  for (uint32_t i = 0; i < n; ++i) if (ds[i]->doc > cand) cand = ds[i]->doc;
+  for (;;) {
+    int again = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t s = uc_seek(ds[i], cand);
+      if (s > cand) { cand = ds[i]->doc; again = 1; break; }
+    }
+    if (!again) return cand;
+  }
+}
+
+/* Intersection::advance (leapfrog on the two rarest, then probe the others) */
+static uint32_t isect_advance(UnionCur** ds, uint32_t n) {
+  UnionCur* left = ds[0];
+  UnionCur* right = ds[1];
+  uint32_t cand = uc_advance(left);
+  if (cand == OR_TERMINATED) return OR_TERMINATED;
+  for (;;) {
+    for (;;) {
+      uint32_t rd = uc_seek(right, cand);
+      cand = uc_seek(left, rd);
+      if (cand == rd) break;
+    }
+    if (cand == OR_TERMINATED) return OR_TERMINATED;
+    uint32_t next = cand;
+    for (uint32_t i = 2; i < n; ++i) {
+      uint32_t s = uc_seek(ds[i], cand);
+      if (s > cand) { next = s; break; }
+    }
+    if (next == cand) return cand;
+    cand = uc_seek(left, next);
+    if (cand == OR_TERMINATED) return OR_TERMINATED;
+  }
+}
+
+/* Intersection::score = left + right + others.sum() (fold from 0.0) */
+static inline float isect_score(UnionCur** ds, uint32_t n) {
+  float others = 0.0f;
+  for (uint32_t i = 2; i < n; ++i) others += uc_score(ds[i]);
+  return uc_score(ds[0]) + uc_score(ds[1]) + others;
+}
+
+/*
+ * mode 0: conjunction  `t1 AND t2 AND ...` (Must clauses)
+ * mode 1: disjunction  `t1 t2 ...`         (default operator: Should)
+ * k >= 1 (TopDocs::with_limit asserts limit >= 1).
+ * Returns number of hits written (<= k), or -1 on bad arguments.
+ */
+int or_search(const or_index* ix, const uint32_t* terms, uint32_t m, int mode, uint32_t k, float* out_score,
+              uint32_t* out_doc) {
+  if (k < 1 || m < 1 || m > OR_MAX_TERMS) return -1;
+  UnionCur cur[OR_MAX_TERMS];
+  Child ch[OR_MAX_TERMS];
+  UnionCur* ds[OR_MAX_TERMS];
+  for (uint32_t i = 0; i < m; ++i) {
+    uc_init(&cur[i], ix, terms[i]);
+    ch[i].c = &cur[i]; ch[i].cost = cur[i].cost; ch[i].qpos = i;
+  }
+  TopN top;
+  topn_init(&top, k);
+  float thr = -3.40282347e+38f;
+  if (mode == 0 && m == 1) {
+    /* a single term: the top-level query is the field union itself */
+    UnionCur* u = &cur[0];
+    for (uint32_t d = u->doc; d != OR_TERMINATED; d = uc_advance(u)) {
+      float s = uc_score(u);
+      if (s > thr) thr = collect(&top, ix, d, s);
+    }
+  } else if (mode == 0) {
+    qsort(ch, m, sizeof(Child), child_cmp);
+    for (uint32_t i = 0; i < m; ++i) ds[i] = ch[i].c;
+    uint32_t d = go_to_first_doc(ds, m);
+    while (d != OR_TERMINATED) {
+      float s = isect_score(ds, m);
+      if (s > thr) thr = collect(&top, ix, d, s);
+      d = isect_advance(ds, m);
+    }
+  } else {
+    /* pure disjunction over the per-term unions, SumCombiner in clause order */
+    for (;;) {
+      uint32_t d = OR_TERMINATED;
+      for (uint32_t i = 0; i < m; ++i) d = min_u32(d, cur[i].doc);
+      if (d == OR_TERMINATED) break;
+      float s = 0.0f;
+      for (uint32_t i = 0; i < m; ++i) if (cur[i].doc == d) s += uc_score(&cur[i]);
+      if (s > thr) thr = collect(&top, ix, d, s);
+      for (uint32_t i = 0; i < m; ++i) if (cur[i].doc == d) uc_advance(&cur[i]);
+    }
+  }
+  return (int)topn_finish(&top, out_score, out_doc);
+}
+
+/* ---------------------------------------------------------------- batch (CPU baseline) */
+typedef struct {
+  const or_index* ix;
+  const uint32_t* q_off; const uint32_t* q_terms;
+  uint32_t nq; int mode; uint32_t k;
+  float* out_score; uint32_t* out_doc; uint32_t* out_n;
+  double* lat_ns;
+  volatile uint32_t next;
+  pthread_mutex_t mu;
+} BatchCtx;
+
+static double now_ns(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec * 1e9 + (double)ts.tv_nsec;
+}
+
+static void* batch_worker(void* arg) {
+  BatchCtx* c = (BatchCtx*)arg;
+  for (;;) {
+    uint32_t q = __atomic_fetch_add(&c->next, 1u, __ATOMIC_RELAXED);
+    if (q >= c->nq) break;
+    double t0 = now_ns();
+    int n = or_search(c->ix, c->q_terms + c->q_off[q], c->q_off[q + 1] - c->q_off[q], c->mode, c->k,
+                      c->out_score + (size_t)q * c->k, c->out_doc + (size_t)q * c->k);
+    double t1 = now_ns();
+    c->out_n[q] = n < 0 ? 0 : (uint32_t)n;
+    if (c->lat_ns) c->lat_ns[q] = t1 - t0;
+  }
+  return NULL;
+}
+
+/* Each thread runs whole queries (a tokio worker per request, tantivy's
+ * single-threaded executor).  Returns the wall time in seconds. */
+double or_search_batch(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, uint32_t nq, int mode,
+                       uint32_t k, float* out_score, uint32_t* out_doc, uint32_t* out_n, double* lat_ns, int threads) {
+  BatchCtx c;
+  memset(&c, 0, sizeof c);
+  c.ix = ix; c.q_off = q_off; c.q_terms = q_terms; c.nq = nq; c.mode = mode; c.k = k;
+  c.out_score = out_score; c.out_doc = out_doc; c.out_n = out_n; c.lat_ns = lat_ns; c.next = 0;
+  if (threads < 1) threads = 1;
+  if (threads > 512) threads = 512;
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  double t0 = now_ns();
+  for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, batch_worker, &c);
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  double t1 = now_ns();
+  free(th);
+  return (t1 - t0) * 1e-9;
+}
+
+/* ---------------------------------------------------------------- bytes model */
+/* per-query algorithmic bytes over the merged
+ * (text U name) posting list of each term.
+ *   B_merge = sum 8*df_t
+ *   B_skip  = 8*df_min + sum_{t != min} (1024*blocks_t + 4*ceil(df_t/128))
+ *   B       = min(B_merge, B_skip) + F*|I| + 8*min(K,|I|);  1-term: 8*df + 8*min(K,df)
+ * out[0]=B_merge out[1]=B_skip out[2]=B out[3]=|I|
+ */
+static uint32_t* merged_docs(const or_index* ix, uint32_t term, uint32_t* n_out) {
+  if (term >= ix->n_terms) { *n_out = 0; return NULL; }
+  const Postings* a = &ix->fld[0][term];
+  const Postings* b = &ix->fld[1][term];
+  uint32_t* out = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)a->n + b->n + 1));
+  uint32_t i = 0, j = 0, n = 0;
+  while (i < a->n || j < b->n) {
+    uint32_t x = i < a->n ? a->doc[i] : OR_TERMINATED;
+    uint32_t y = j < b->n ? b->doc[j] : OR_TERMINATED;
+    uint32_t d = x < y ? x : y;
+    out[n++] = d;
+    if (x == d) ++i;
+    if (y == d) ++j;
+  }
+  *n_out = n;
+  return out;
+}
+
+typedef struct { uint32_t* d; uint32_t n; uint32_t qpos; } MList;
+static int mlist_cmp(const void* a, const void* b) {
+  const MList* x = (const MList*)a; const MList* y = (const MList*)b;
+  if (x->n != y->n) return x->n < y->n ? -1 : 1;
+  return (x->qpos > y->qpos) - (x->qpos < y->qpos);
+}
+
+int or_bytes_model(const or_index* ix, const uint32_t* terms, uint32_t m, uint32_t k, double* out) {
+  if (m < 1 || m > OR_MAX_TERMS) return -1;
+  MList L[OR_MAX_TERMS];
+  for (uint32_t i = 0; i < m; ++i) { L[i].d = merged_docs(ix, terms[i], &L[i].n); L[i].qpos = i; }
+  double F = ix->has_name ? 2.0 : 1.0;
+  if (m == 1) {
+    double df = L[0].n;
+    out[0] = out[1] = 8.0 * df;
+    out[2] = 8.0 * df + 8.0 * (df < k ? df : k);
+    out[3] = df;
+    free(L[0].d);
+    return 0;
+  }
+  qsort(L, m, sizeof(MList), mlist_cmp);
+  double bmerge = 0;
+  for (uint32_t i = 0; i < m; ++i) bmerge += 8.0 * L[i].n;
+  double bskip = 8.0 * L[0].n;
+  uint32_t ns = L[0].n;
+  uint32_t* S = (uint32_t*)malloc(sizeof(uint32_t) * (ns + 1));
+  if (ns) memcpy(S, L[0].d, sizeof(uint32_t) * ns);
+  for (uint32_t t = 1; t < m; ++t) {
+    const uint32_t* d = L[t].d;
+    uint32_t n = L[t].n;
+    uint64_t blocks = 0;
+    int64_t last_block = -1;
+    uint32_t keep = 0, lb = 0;
+    for (uint32_t i = 0; i < ns; ++i) {
+      uint32_t c = S[i];
+      /* lower_bound(t, c); candidates ascend so lb moves forward */
+      uint32_t lo = lb, hi = n;
+      while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (d[mid] < c) lo = mid + 1; else hi = mid; }
+      lb = lo;
+      if (lb < n) {
+        int64_t blk = lb / OR_BLOCK;
+        if (blk != last_block) { ++blocks; last_block = blk; }
+        if (d[lb] == c) S[keep++] = c;
+      }
+    }
+    ns = keep;
+    bskip += 1024.0 * (double)blocks + 4.0 * (double)((n + OR_BLOCK - 1) / OR_BLOCK);
+  }
+  double bmin = bmerge < bskip ? bmerge : bskip;
+  out[0] = bmerge; out[1] = bskip;
+  out[2] = bmin + F * ns + 8.0 * (ns < k ? ns : k);
+  out[3] = ns;
+  free(S);
+  for (uint32_t i = 0; i < m; ++i) free(L[i].d);
+  return 0;
+}

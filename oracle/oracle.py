@@ -1,0 +1,156 @@
+"""ctypes loader of the CPU oracle (fugu_oracle.c) -- TEST INFRASTRUCTURE.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  Parity status: "parity unpinned" (see fugu_oracle.c header
+and DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfugu_oracle.so")
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} missing: run `make -C oracle`")
+_lib = C.CDLL(LIB_PATH)
+
+_p = C.c_void_p
+_lib.or_index_build.restype = _p
+_lib.or_index_build.argtypes = [C.c_uint32, C.c_uint32, _p, _p, _p, _p, _p, C.c_int]
+_lib.or_index_free.restype = None
+_lib.or_index_free.argtypes = [_p]
+_lib.or_df.restype = C.c_uint32
+_lib.or_df.argtypes = [_p, C.c_int, C.c_uint32]
+_lib.or_total_tokens.restype = C.c_uint64
+_lib.or_total_tokens.argtypes = [_p, C.c_int]
+_lib.or_avgdl.restype = C.c_float
+_lib.or_avgdl.argtypes = [_p, C.c_int]
+_lib.or_cache.restype = None
+_lib.or_cache.argtypes = [_p, C.c_int, _p]
+_lib.or_fieldnorm_table.restype = None
+_lib.or_fieldnorm_table.argtypes = [_p]
+_lib.or_fieldnorm_to_id.restype = C.c_uint8
+_lib.or_fieldnorm_to_id.argtypes = [C.c_uint32]
+_lib.or_fieldnorm_id_of.restype = C.c_uint8
+_lib.or_fieldnorm_id_of.argtypes = [_p, C.c_int, C.c_uint32]
+_lib.or_idf.restype = C.c_float
+_lib.or_idf.argtypes = [C.c_uint64, C.c_uint64]
+_lib.or_term_weight.restype = C.c_float
+_lib.or_term_weight.argtypes = [C.c_uint64, C.c_uint64]
+_lib.or_bm25_cache.restype = None
+_lib.or_bm25_cache.argtypes = [C.c_float, _p]
+_lib.or_search.restype = C.c_int
+_lib.or_search.argtypes = [_p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p]
+_lib.or_search_batch.restype = C.c_double
+_lib.or_search_batch.argtypes = [_p, _p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p, _p, _p, C.c_int]
+_lib.or_bytes_model.restype = C.c_int
+_lib.or_bytes_model.argtypes = [_p, _p, C.c_uint32, C.c_uint32, _p]
+
+AND = 0
+OR = 1
+
+
+def fieldnorm_table():
+    t = np.zeros(256, np.uint32)
+    _lib.or_fieldnorm_table(t.ctypes.data)
+    return t
+
+
+def fieldnorm_to_id(n: int) -> int:
+    return int(_lib.or_fieldnorm_to_id(n))
+
+
+def idf(df: int, n: int) -> float:
+    return float(_lib.or_idf(df, n))
+
+
+def term_weight(df: int, n: int) -> float:
+    return float(_lib.or_term_weight(df, n))
+
+
+def bm25_cache(avgdl: float):
+    out = np.zeros(256, np.float32)
+    _lib.or_bm25_cache(C.c_float(avgdl), out.ctypes.data)
+    return out
+
+
+class OracleIndex:
+    def __init__(self, n_terms: int, text_off, text_tok, name_off=None, name_tok=None, deleted=None,
+                 threads: int = 1):
+        self._keep = [np.ascontiguousarray(text_off, np.uint64), np.ascontiguousarray(text_tok, np.uint32)]
+        n_docs = len(self._keep[0]) - 1
+        no = nt = dl = None
+        if name_off is not None:
+            no = np.ascontiguousarray(name_off, np.uint64)
+            nt = np.ascontiguousarray(name_tok, np.uint32)
+            self._keep += [no, nt]
+        if deleted is not None:
+            dl = np.ascontiguousarray(deleted, np.uint8)
+            self._keep.append(dl)
+        self._h = _lib.or_index_build(n_docs, n_terms, self._keep[0].ctypes.data, self._keep[1].ctypes.data,
+                                      None if no is None else no.ctypes.data, None if nt is None else nt.ctypes.data,
+                                      None if dl is None else dl.ctypes.data, threads)
+        if not self._h:
+            raise MemoryError("oracle index build failed")
+        self.n_docs = n_docs
+        self.n_terms = n_terms
+
+    def df(self, term: int, field: int = 0) -> int:
+        return int(_lib.or_df(self._h, field, term))
+
+    def total_tokens(self, field: int = 0) -> int:
+        return int(_lib.or_total_tokens(self._h, field))
+
+    def avgdl(self, field: int = 0) -> float:
+        return float(_lib.or_avgdl(self._h, field))
+
+    def cache(self, field: int = 0):
+        out = np.zeros(256, np.float32)
+        _lib.or_cache(self._h, field, out.ctypes.data)
+        return out
+
+    def fieldnorm_id(self, doc: int, field: int = 0) -> int:
+        return int(_lib.or_fieldnorm_id_of(self._h, field, doc))
+
+    def search(self, terms, k: int, mode: int = AND):
+        t = np.ascontiguousarray(terms, np.uint32)
+        score = np.zeros(k, np.float32)
+        doc = np.zeros(k, np.uint32)
+        n = _lib.or_search(self._h, t.ctypes.data, len(t), mode, k, score.ctypes.data, doc.ctypes.data)
+        if n < 0:
+            raise ValueError("oracle rejected the query")
+        return score[:n].copy(), doc[:n].copy()
+
+    def search_batch(self, q_off, q_terms, k: int, mode: int = AND, threads: int = 1, latencies: bool = False):
+        q_off = np.ascontiguousarray(q_off, np.uint32)
+        q_terms = np.ascontiguousarray(q_terms, np.uint32)
+        nq = len(q_off) - 1
+        score = np.zeros(nq * k, np.float32)
+        doc = np.zeros(nq * k, np.uint32)
+        n = np.zeros(nq, np.uint32)
+        lat = np.zeros(nq, np.float64) if latencies else None
+        wall = _lib.or_search_batch(self._h, q_off.ctypes.data, q_terms.ctypes.data, nq, mode, k, score.ctypes.data,
+                                    doc.ctypes.data, n.ctypes.data, None if lat is None else lat.ctypes.data, threads)
+        return score.reshape(nq, k), doc.reshape(nq, k), n, wall, lat
+
+    def bytes_model(self, terms, k: int):
+        t = np.ascontiguousarray(terms, np.uint32)
+        out = np.zeros(4, np.float64)
+        rc = _lib.or_bytes_model(self._h, t.ctypes.data, len(t), k, out.ctypes.data)
+        if rc != 0:
+            raise ValueError("bad query")
+        return out
+
+    def close(self):
+        if self._h:
+            _lib.or_index_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,103 @@
+"""numpy mirror of fugu_amd/csrc/synth.cpp (test infrastructure).
+
+Used to prove the C generator is bit-exact against its written spec
+ and by tests/golden/gen_golden.py.  Also generates the
+`name` field and deletion masks of the golden corpora, which only tests use.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+
+def mix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+    return z ^ (z >> np.uint64(31))
+
+
+def h2(s, a):
+    a = np.asarray(a, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return mix64(np.uint64(s) + GOLDEN * (a + np.uint64(1)))
+
+
+def h3(s, a, b):
+    b = np.asarray(b, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return mix64(h2(s, a) + GOLDEN * (b + np.uint64(1)))
+
+
+class Zipf:
+    def __init__(self, v: int, s: float):
+        r = np.arange(1, v + 1, dtype=np.float64)
+        w = 1.0 / r if s == 1.0 else np.power(r, -s)
+        self.cum = np.cumsum(w)  # sequential accumulate == the C loop
+        self.total = self.cum[-1]
+        self.v = v
+
+    def rank(self, h):
+        h = np.asarray(h, dtype=np.uint64)
+        u = (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+        x = u * self.total
+        return np.searchsorted(self.cum[:-1], x, side="right").astype(np.int64) + 1
+
+
+def doc_lengths(n_docs: int, seed_l: int, len_min: int = 8, len_span: int = 113, doc_begin: int = 0):
+    d = np.arange(doc_begin, doc_begin + n_docs, dtype=np.uint64)
+    return (np.uint64(len_min) + h2(seed_l, d) % np.uint64(len_span)).astype(np.int64)
+
+
+def corpus(n_docs: int, vocab: int, s: float, seed_l: int, seed_t: int, len_min: int = 8, len_span: int = 113):
+    lens = doc_lengths(n_docs, seed_l, len_min, len_span)
+    off = np.zeros(n_docs + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    doc = np.repeat(np.arange(n_docs, dtype=np.uint64), lens)
+    j = np.arange(int(off[-1]), dtype=np.uint64) - np.repeat(off[:-1], lens)
+    z = Zipf(vocab, s)
+    tok = (z.rank(h3(seed_t, doc, j)) - 1).astype(np.uint32)
+    return off, tok
+
+
+def queries(n_queries: int, m_min: int, m_max: int, max_rank: int, s: float, seed_q: int):
+    z = Zipf(max_rank, s)
+    q_off = [0]
+    terms = []
+    for q in range(n_queries):
+        m = m_min + int(h2(seed_q + 1, q) % np.uint64(m_max - m_min + 1))
+        got = []
+        i = 0
+        while len(got) < m:
+            t = int(z.rank(h3(seed_q, q, i))) - 1
+            if t not in got:
+                got.append(t)
+            i += 1
+        terms += got
+        q_off.append(len(terms))
+    return np.array(q_off, np.uint32), np.array(terms, np.uint32)
+
+
+def names(n_docs: int, vocab: int, seed: int, max_len: int = 3, s: float = 1.0, present_every: int = 3):
+    """`name` field of golden corpora: every `present_every`-th doc (by hash)
+    gets 1..max_len tokens drawn from Zipf(s) over the first `vocab` ranks."""
+    d = np.arange(n_docs, dtype=np.uint64)
+    hd = h2(seed, d)
+    has = (hd % np.uint64(present_every)) == 0
+    lens = np.where(has, 1 + (hd >> np.uint64(8)) % np.uint64(max_len), 0).astype(np.int64)
+    off = np.zeros(n_docs + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    doc = np.repeat(d, lens)
+    j = np.arange(int(off[-1]), dtype=np.uint64) - np.repeat(off[:-1], lens)
+    z = Zipf(vocab, s)
+    tok = (z.rank(h3(seed ^ 0xA5A5, doc, j)) - 1).astype(np.uint32)
+    return off, tok
+
+
+def deleted_mask(n_docs: int, seed: int, every: int = 7):
+    d = np.arange(n_docs, dtype=np.uint64)
+    return ((h2(seed, d) % np.uint64(every)) == 0).astype(np.uint8)
