@@ -2,7 +2,7 @@
 10M-doc Zipf corpus, 3-term AND, BM25 top-100 (BASELINE.json `metric`).
 
 A step = one batch of 1024 planned queries through the gfx950 pipeline
-(k_conj -> k_filter -> k_final) with the plan and the index resident in HBM.
+(k_conj -> k_final) with the plan and the index resident in HBM.
 N > 1 (torchrun, one rank per GPU): rank r holds namespace r (its own 10M-doc
 corpus, weak scaling); every step also all-gathers the per-shard top-100 over
 RCCL and merges them on the device (fan-out query over all namespaces).
@@ -204,8 +204,7 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
             },
             "kernels_ms_per_step": {"k_conj": round(ms_k[0] / max(n_prof, 1), 4),
-                                    "k_filter": round(ms_k[1] / max(n_prof, 1), 4),
-                                    "k_final": round(ms_k[2] / max(n_prof, 1), 4)},
+                                    "k_final": round(ms_k[1] / max(n_prof, 1), 4)},
             "cpu_baseline": cpu,
             "parity": parity,
             "speedup_vs_cpu": round(qps / cpu["value"], 1) if cpu else None,

@@ -1,5 +1,5 @@
-// Internal layout shared by the host side (index.cpp, plan.cpp, api.cpp) and
-// the gfx950 kernels (kernels.hip).  See DESIGN.md §HBM layout.
+// Internal layout shared by the host side (fugu.cpp) and the gfx950 kernels
+// (kernels.hip).  See DESIGN.md §HBM layout.
 #pragma once
 #include <cstdint>
 
@@ -7,27 +7,43 @@
 
 namespace fg {
 
-constexpr uint32_t kBlock = 128;          // postings per skip block (tantivy: 128-doc blocks)
+constexpr uint32_t kBlock = 128;          // tantivy block size (bytes model only)
+constexpr uint32_t kBucketTarget = 32;    // directory: expected postings per bucket (one 128-B line)
 constexpr uint32_t kThreads = 256;        // 4 waves of 64 per workgroup
-constexpr uint32_t kItems = 8;            // candidates per lane
-constexpr uint32_t kChunk = kThreads * kItems;   // 2048 candidates of the lead list per workgroup
+constexpr uint32_t kItems = 8;            // lead candidates per lane
+constexpr uint32_t kChunk = kThreads * kItems;   // 2048 lead candidates per work item
 constexpr uint32_t kWaveSpan = kChunk / 4;       // 512 consecutive candidates per wave
-constexpr uint32_t kSeg = 2048;           // LDS staging budget per wave (u32 doc ids)
 constexpr uint32_t kMaxTerms = 16;        // terms per query (FG_MAX_TERMS)
 constexpr uint32_t kMaxK = 1024;          // largest top-k the device select supports
-constexpr uint32_t kFinalCap = 4096;      // candidates kept in LDS by the final select
+constexpr uint32_t kFinalCap = 8192;      // candidates kept in LDS by the final select
+constexpr uint32_t kDenseDiv = 8;         // terms in >= 1/8 of the docs also get a dense tf table
+constexpr uint32_t kMaxDense = 4096;      // at most this many dense tables per index
+constexpr uint32_t kGroupsPerQuery = 64;  // a query's chunks are split into ~this many work items
+constexpr uint32_t kMaxGroup = 16;        // ... of at most this many chunks each
 constexpr uint32_t kHistBins = 2048;      // 11-bit radix digits
 
 constexpr uint32_t kModeAnd = 0;
 constexpr uint32_t kModeOr = 1;
 
 // Device view of one namespace snapshot (all pointers device-resident).
+//
+// Per term t the postings are doc[off[t] .. off[t+1]) (ascending) with tf[]
+// alongside, and a doc -> position directory: bucket b covers docs
+// [b << B_t, (b+1) << B_t) and dir[dir_off[t] + b] = first position in the
+// list with doc >= b << B_t (the last entry is df_t).  B_t is chosen so a
+// bucket holds ~32 postings (one 128-B line of doc ids); a probe is one
+// directory load and a <= S_t step search inside one or two lines.  Terms that
+// occur in >= 1/8 of the docs (and only in `text`) additionally get a dense
+// doc-indexed u16 tf table: a probe into them is one coalesced 2-B load.
 struct DevIndex {
   const uint32_t* doc;       // [P] doc ids, CSR by term, ascending within a term
   const uint32_t* tf;        // [P] packed: lo16 = tf in `text`, hi16 = tf in `name`
   const uint64_t* off;       // [V+1] posting offsets
-  const uint32_t* skip;      // [S] last doc id of each 128-posting block
-  const uint32_t* skip_off;  // [V+1] skip offsets
+  const uint32_t* dir;       // [D] bucket directory (positions within the list)
+  const uint32_t* dir_off;   // [V] first directory entry of each term
+  const uint32_t* tmeta;     // [V] bits 0-7 = B_t (bucket shift), bits 8-15 = S_t (search steps),
+                             //     bits 16-31 = dense slot + 1 (0: no dense table)
+  const uint16_t* dense;     // [n_dense * N] doc-indexed tf_text of the densest terms (0 = absent)
   const float* w_text;       // [V] idf(df_text)*(1+K1)
   const float* w_name;       // [V] idf(df_name)*(1+K1)
   const uint8_t* fn_text;    // [N] fieldnorm ids
@@ -39,7 +55,10 @@ struct DevIndex {
   uint32_t has_name;
 };
 
-// Device view of one planned batch.
+// Device view of one planned batch.  Work items (query, 2048-candidate chunk
+// of the query's lead list) are ordered as a doc sweep across the batch:
+// items covering similar doc ranges of different queries run together, so the
+// segments of hot posting lists they probe are shared through L2 / MALL.
 struct DevPlan {
   uint32_t n_queries;
   uint32_t total_chunks;
@@ -48,16 +67,18 @@ struct DevPlan {
   const uint32_t* q_m;          // [nq] terms per query
   const uint32_t* q_terms;      // [nq * kMaxTerms] term ids, intersection (cost) order
   const uint32_t* q_lead_df;    // [nq] length of the lead list (0 => empty result)
-  const uint32_t* chunk_start;  // [nq+1] first work item of each query
-  const uint32_t* chunk_q;      // [total_chunks] query of each work item
-  const uint64_t* cand_off;     // [nq+1] capacity offsets of the per-query candidate lists
-  // workspace (zeroed per execution where noted)
-  uint64_t* thresh;             // [nq] monotone lower bound on the k-th best key (zeroed)
-  uint32_t* slot_cnt;           // [total_chunks] keys written by each work item
-  uint64_t* slot_keys;          // [total_chunks * k]
-  uint32_t* cand_cnt;           // [nq] (zeroed)
-  uint64_t* cand_keys;          // [cand_off[nq]]
+  const uint32_t* work_q;       // [total_chunks] query of each work item (sweep order)
+  const uint32_t* work_c;       // [total_chunks] first chunk of the item's group
+  const uint32_t* work_n;       // [total_chunks] chunks in the item's group (<= kMaxGroup)
+  const uint64_t* cand_off;     // [nq+1] candidate-list capacity offsets (work items of q * k)
+  // workspace, zeroed per run
+  uint64_t* thresh;             // [nq] monotone lower bound on the k-th best key
+  uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list
+  uint64_t* cand_keys;          // [cand_off[nq]] per-query candidate lists
+  uint64_t* diag;               // diagnostic builds only (-DFG_DIAG): per-workgroup stamps
 };
+
+constexpr uint32_t kDiagPerWg = 8;  // u64 stamps per workgroup in diagnostic builds
 
 // Key of a hit: larger is better.  (score bits << 32) | ~doc orders by
 // score descending, then doc ascending (tantivy ComparableDoc order); scores
@@ -76,7 +97,6 @@ __host__ __device__ inline uint32_t key_doc(uint64_t k) { return 0xFFFFFFFFu - (
 
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
-hipError_t launch_filter(const DevPlan& pl, hipStream_t s);
 hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,

@@ -130,7 +130,8 @@ struct fg_index {
   int dev = 0;
   uint32_t n_docs = 0, n_terms = 0;
   bool has_name = false;
-  uint64_t n_postings = 0, device_bytes = 0;
+  uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0;
+  uint32_t n_dense = 0;
   uint64_t tot[2] = {0, 0};
   float avgdl[2] = {0, 0};
   float cache[512];
@@ -152,12 +153,13 @@ struct fg_plan {
   uint32_t* own_n = nullptr;
   void* zero_region = nullptr;
   size_t zero_bytes = 0;
+  size_t diag_words = 0;
   uint64_t ws_bytes = 0;
   DevAllocs mem;
   hipStream_t last_stream = nullptr;
   bool profile = false;
-  std::vector<hipEvent_t> pending;  // 4 per profiled execute
-  double ms[3] = {0, 0, 0};
+  std::vector<hipEvent_t> pending;  // 3 per profiled execute
+  double ms[2] = {0, 0};
   uint32_t n_prof = 0;
   ~fg_plan() {
     for (hipEvent_t e : pending) (void)hipEventDestroy(e);
@@ -213,44 +215,88 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
     ix->w_text[t] = bm25_weight(hp.df_text[t], N);
     ix->w_name[t] = bm25_weight(hp.df_name[t], N);
   }
-  // skip index: last doc of every 128-posting block
-  std::vector<uint32_t> skip_off(V + 1);
-  uint64_t nb = 0;
+  // doc -> position bucket directory (fg_internal.h DevIndex): bucket width
+  // 2^B_t docs with B_t the largest shift keeping ~32 postings per bucket
+  std::vector<uint32_t> dir_off(V), tmeta(V);
+  uint64_t nd = 0;
   for (uint32_t t = 0; t < V; ++t) {
-    skip_off[t] = (uint32_t)nb;
-    nb += (hp.off[t + 1] - hp.off[t] + fg::kBlock - 1) / fg::kBlock;
+    const uint64_t n = hp.off[t + 1] - hp.off[t];
+    uint32_t B = 0;
+    if (n == 0) B = 31;
+    else while (B < 31 && (n << (B + 1)) <= (uint64_t)fg::kBucketTarget * N) ++B;
+    const uint64_t nbk = ((N - 1) >> B) + 1;
+    if (nd > 0xFFFFFFFFull) return fail(FG_EINVAL, "directory too large");
+    dir_off[t] = (uint32_t)nd;
+    tmeta[t] = B;
+    nd += nbk + 1;
   }
-  if (nb > 0xFFFFFFFFull) return fail(FG_EINVAL, "too many skip blocks");
-  skip_off[V] = (uint32_t)nb;
-  std::vector<uint32_t> skip(nb);
-  for (uint32_t t = 0; t < V; ++t) {
-    uint64_t b = hp.off[t], n = hp.off[t + 1] - b;
-    uint32_t so = skip_off[t];
-    for (uint64_t k = 0; k * fg::kBlock < n; ++k) {
-      uint64_t end = std::min<uint64_t>((k + 1) * fg::kBlock, n);
-      skip[so + k] = hp.doc[b + end - 1];
+  std::vector<uint32_t> dir(nd);
+  parallel_ranges(V, hw_threads(0), [&](int, uint32_t tb, uint32_t te) {
+    for (uint32_t t = tb; t < te; ++t) {
+      const uint64_t b0 = hp.off[t], n = hp.off[t + 1] - b0;
+      const uint32_t B = tmeta[t];
+      const uint64_t nbk = ((N - 1) >> B) + 1;
+      uint32_t* dt = dir.data() + dir_off[t];
+      uint64_t p = 0;
+      uint32_t maxocc = 0;
+      for (uint64_t b = 0; b <= nbk; ++b) {
+        const uint64_t lo = b << B;
+        while (p < n && hp.doc[b0 + p] < lo) ++p;
+        dt[b] = (uint32_t)p;
+        if (b) maxocc = std::max<uint32_t>(maxocc, dt[b] - dt[b - 1]);
+      }
+      uint32_t S = 0;
+      while ((1ull << S) <= maxocc) ++S;  // 2^S > largest bucket
+      tmeta[t] = B | (S << 8);
     }
+  });
+  // dense doc-indexed tf tables for the densest text-only terms
+  std::vector<uint32_t> dense_terms;
+  for (uint32_t t = 0; t < V && dense_terms.size() < fg::kMaxDense; ++t) {
+    const uint64_t n = hp.off[t + 1] - hp.off[t];
+    if (n * fg::kDenseDiv >= N && hp.df_name[t] == 0) dense_terms.push_back(t);
   }
+  std::vector<uint16_t> dense;
+  try {
+    dense.assign(dense_terms.size() * (size_t)N, 0);
+  } catch (...) {
+    return fail(FG_EOOM, "dense tables (%zu terms) allocation failed", dense_terms.size());
+  }
+  parallel_ranges((uint32_t)dense_terms.size(), std::min<int>(hw_threads(0), (int)dense_terms.size()),
+                  [&](int, uint32_t a, uint32_t e) {
+                    for (uint32_t s = a; s < e; ++s) {
+                      const uint32_t t = dense_terms[s];
+                      uint16_t* row = dense.data() + (size_t)s * N;
+                      for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) row[hp.doc[p]] = (uint16_t)(hp.tf[p] & 0xFFFFu);
+                      tmeta[t] |= (s + 1) << 16;
+                    }
+                  });
+  ix->n_dense = (uint32_t)dense_terms.size();
   HIPCHK(hipSetDevice(dev));
   uint64_t bytes = 0;
   int rc;
-  uint32_t *d_doc, *d_tf, *d_skip, *d_skip_off, *d_alive = nullptr;
+  uint16_t* d_dense = nullptr;
+  uint32_t *d_doc, *d_tf, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr;
   uint64_t* d_off;
   float *d_wt, *d_wn, *d_cache;
   uint8_t *d_fnt, *d_fnn;
   if ((rc = dev_upload(ix->mem, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.tf.data(), hp.tf.size(), &d_tf, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.off.data(), hp.off.size(), &d_off, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, skip.data(), skip.size(), &d_skip, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, skip_off.data(), skip_off.size(), &d_skip_off, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, dir.data(), dir.size(), &d_dir, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, dense.data(), dense.size(), &d_dense, &bytes))) return rc;
+  std::vector<uint16_t>().swap(dense);
   if ((rc = dev_upload(ix->mem, ix->w_text.data(), V, &d_wt, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, ix->w_name.data(), V, &d_wn, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.fn_text.data(), hp.fn_text.size(), &d_fnt, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.fn_name.data(), hp.fn_name.size(), &d_fnn, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
   if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
-  ix->d = fg::DevIndex{d_doc, d_tf, d_off, d_skip, d_skip_off, d_wt, d_wn, d_fnt, d_fnn, d_alive, d_cache,
-                       hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
+  ix->d = fg::DevIndex{d_doc, d_tf, d_off, d_dir, d_dir_off, d_tmeta, d_dense, d_wt, d_wn, d_fnt, d_fnn, d_alive,
+                       d_cache, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
+  ix->dir_entries = nd;
   ix->device_bytes = bytes;
   ix->off = std::move(hp.off);
   ix->df_text = std::move(hp.df_text);
@@ -517,9 +563,8 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k=%u > FG_MAX_K=%d", k, FG_MAX_K);
   if (q->mode != FG_MODE_AND && q->mode != FG_MODE_OR) return fail(FG_EINVAL, "bad mode %d", q->mode);
   const uint32_t nq = q->n_queries;
-  std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), chunk_start(nq + 1);
-  std::vector<uint64_t> cand_off(nq + 1);
-  uint64_t chunks = 0, cand = 0;
+  std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), nchunk(nq);
+  uint64_t chunks = 0;
   for (uint32_t i = 0; i < nq; ++i) {
     const uint32_t b = q->q_off[i], e = q->q_off[i + 1];
     if (e < b) return fail(FG_EINVAL, "q_off not monotone at query %u", i);
@@ -533,7 +578,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     T ts[fg::kMaxTerms];
     bool missing = false;
     for (uint32_t j = 0; j < m; ++j) {
-      uint32_t t = q->terms[b + j];
+      const uint32_t t = q->terms[b + j];
       uint64_t cost = 0;
       if (t >= ix->n_terms) missing = true; else cost = (uint64_t)ix->df_text[t] + ix->df_name[t];
       if (cost == 0) missing = true;
@@ -542,20 +587,38 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     std::stable_sort(ts, ts + m, [](const T& x, const T& y) { return x.cost < y.cost; });
     q_m[i] = m;
     for (uint32_t j = 0; j < m; ++j) q_terms[(size_t)i * fg::kMaxTerms + j] = missing ? 0 : ts[j].term;
-    uint64_t df0 = missing ? 0 : ix->off[ts[0].term + 1] - ix->off[ts[0].term];
+    const uint64_t df0 = missing ? 0 : ix->off[ts[0].term + 1] - ix->off[ts[0].term];
     lead[i] = (uint32_t)df0;
-    uint64_t nch = (df0 + fg::kChunk - 1) / fg::kChunk;
-    chunk_start[i] = (uint32_t)chunks;
-    cand_off[i] = cand;
-    chunks += nch;
-    cand += nch * k;
-    if (chunks > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%llu work items)", (unsigned long long)chunks);
+    nchunk[i] = (uint32_t)((df0 + fg::kChunk - 1) / fg::kChunk);
+    chunks += nchunk[i];
+    if (chunks > 0x7FFFFFFFull)
+      return fail(FG_EUNSUPPORTED, "batch too large (%llu work items)", (unsigned long long)chunks);
   }
-  chunk_start[nq] = (uint32_t)chunks;
-  cand_off[nq] = cand;
-  std::vector<uint32_t> chunk_q(chunks);
-  for (uint32_t i = 0; i < nq; ++i)
-    for (uint32_t c = chunk_start[i]; c < chunk_start[i + 1]; ++c) chunk_q[c] = i;
+  // work items: each query's chunks in ~kGroupsPerQuery groups of <= kMaxGroup
+  // consecutive chunks, ordered as a doc sweep across the batch (group g of n
+  // covers ~[g/n, (g+1)/n) of the doc space), ties by query
+  struct W { double key; uint32_t q, c, n; };
+  std::vector<W> items;
+  std::vector<uint32_t> ngroup(nq);
+  for (uint32_t i = 0; i < nq; ++i) {
+    const uint32_t nch = nchunk[i];
+    const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
+    const uint32_t ng = (nch + G - 1) / G;
+    ngroup[i] = ng;
+    for (uint32_t g = 0; g < ng; ++g)
+      items.push_back(W{(g + 0.5) / ng, i, g * G, std::min(G, nch - g * G)});
+  }
+  std::stable_sort(items.begin(), items.end(), [](const W& a, const W& b) { return a.key < b.key; });
+  chunks = items.size();  // from here on: work items
+  std::vector<uint32_t> work_q(chunks), work_c(chunks), work_n(chunks);
+  std::vector<uint64_t> cand_off(nq + 1, 0);
+  for (uint64_t w = 0; w < chunks; ++w) {
+    work_q[w] = items[w].q;
+    work_c[w] = items[w].c;
+    work_n[w] = items[w].n;
+  }
+  // each work item appends at most k keys to its query's candidate list
+  for (uint32_t i = 0; i < nq; ++i) cand_off[i + 1] = cand_off[i] + (uint64_t)ngroup[i] * k;
 
   auto p = std::make_unique<fg_plan>();
   p->nq = nq;
@@ -563,15 +626,21 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->mode = q->mode;
   p->total_chunks = (uint32_t)chunks;
   p->mem.dev = ix->dev;
-  // one allocation: [inputs | zeroed (thresh, cand_cnt) | workspace | outputs]
+  // one allocation: [inputs | zeroed (thresh, cand_cnt) | candidates | outputs]
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t s_qm = al(4ull * nq), s_qt = al(4ull * nq * fg::kMaxTerms), s_lead = al(4ull * nq),
-               s_cs = al(4ull * (nq + 1)), s_cq = al(4ull * chunks), s_co = al(8ull * (nq + 1));
-  const size_t s_in = s_qm + s_qt + s_lead + s_cs + s_cq + s_co;
+               s_wq = al(4ull * chunks), s_wc = al(4ull * chunks), s_wn = al(4ull * chunks),
+               s_co = al(8ull * (nq + 1));
+  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co;
   const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq);
-  const size_t s_sc = al(4ull * chunks), s_sk = al(8ull * chunks * k), s_ck = al(8ull * cand);
+  const size_t s_ck = al(8ull * cand_off[nq]);
   const size_t s_os = al(4ull * nq * k), s_od = al(4ull * nq * k), s_on = al(4ull * nq);
-  const size_t total = s_in + s_thr + s_cc + s_sc + s_sk + s_ck + s_os + s_od + s_on;
+#ifdef FG_DIAG
+  const size_t s_dg = al(8ull * fg::kDiagPerWg * (chunks + nq));
+#else
+  const size_t s_dg = 0;
+#endif
+  const size_t total = s_in + s_thr + s_cc + s_ck + s_os + s_od + s_on + s_dg;
   HIPCHK(hipSetDevice(ix->dev));
   char* base = nullptr;
   if (hipMalloc((void**)&base, std::max<size_t>(total, 256)) != hipSuccess)
@@ -589,8 +658,9 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.q_m = (const uint32_t*)put(q_m.data(), 4ull * nq, s_qm);
   p->d.q_terms = (const uint32_t*)put(q_terms.data(), 4ull * nq * fg::kMaxTerms, s_qt);
   p->d.q_lead_df = (const uint32_t*)put(lead.data(), 4ull * nq, s_lead);
-  p->d.chunk_start = (const uint32_t*)put(chunk_start.data(), 4ull * (nq + 1), s_cs);
-  p->d.chunk_q = (const uint32_t*)put(chunk_q.data(), 4ull * chunks, s_cq);
+  p->d.work_q = (const uint32_t*)put(work_q.data(), 4ull * chunks, s_wq);
+  p->d.work_c = (const uint32_t*)put(work_c.data(), 4ull * chunks, s_wc);
+  p->d.work_n = (const uint32_t*)put(work_n.data(), 4ull * chunks, s_wn);
   p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
   HIPCHK(hipMemcpy(base, staging.data(), s_in, hipMemcpyHostToDevice));
   char* cur = base + s_in;
@@ -600,10 +670,6 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   cur += s_thr;
   p->d.cand_cnt = (uint32_t*)cur;
   cur += s_cc;
-  p->d.slot_cnt = (uint32_t*)cur;
-  cur += s_sc;
-  p->d.slot_keys = (uint64_t*)cur;
-  cur += s_sk;
   p->d.cand_keys = (uint64_t*)cur;
   cur += s_ck;
   p->own_score = (float*)cur;
@@ -611,6 +677,9 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->own_doc = (uint32_t*)cur;
   cur += s_od;
   p->own_n = (uint32_t*)cur;
+  cur += s_on;
+  p->d.diag = s_dg ? (uint64_t*)cur : nullptr;
+  p->diag_words = s_dg / 8;
   p->d.n_queries = nq;
   p->d.total_chunks = (uint32_t)chunks;
   p->d.k = k;
@@ -629,19 +698,17 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
   uint32_t* od = d_out_doc ? d_out_doc : p->own_doc;
   uint32_t* on = d_out_n ? d_out_n : p->own_n;
   HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
-  hipEvent_t ev[4] = {};
+  hipEvent_t ev[3] = {};
   if (p->profile) {
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventRecord(ev[0], s));
   }
   HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
   if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
-  HIPCHK(fg::launch_filter(p->d, s));
-  if (p->profile) HIPCHK(hipEventRecord(ev[2], s));
   HIPCHK(fg::launch_final(p->d, os, od, on, s));
   if (p->profile) {
-    HIPCHK(hipEventRecord(ev[3], s));
-    p->pending.insert(p->pending.end(), ev, ev + 4);
+    HIPCHK(hipEventRecord(ev[2], s));
+    p->pending.insert(p->pending.end(), ev, ev + 3);
   }
   p->last_stream = s;
   return FG_OK;
@@ -676,9 +743,9 @@ int fg_plan_profile(fg_plan* p, int enable) {
 int fg_plan_kernel_ms(fg_plan* p, double* ms_out, uint32_t* n_out) {
   if (!p) return fail(FG_EINVAL, "NULL plan");
   HIPCHK(hipSetDevice(p->ix->dev));
-  for (size_t i = 0; i + 3 < p->pending.size(); i += 4) {
-    HIPCHK(hipEventSynchronize(p->pending[i + 3]));
-    for (int kx = 0; kx < 3; ++kx) {
+  for (size_t i = 0; i + 2 < p->pending.size(); i += 3) {
+    HIPCHK(hipEventSynchronize(p->pending[i + 2]));
+    for (int kx = 0; kx < 2; ++kx) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, p->pending[i + kx], p->pending[i + kx + 1]));
       p->ms[kx] += ms;
@@ -687,10 +754,22 @@ int fg_plan_kernel_ms(fg_plan* p, double* ms_out, uint32_t* n_out) {
   }
   for (hipEvent_t e : p->pending) (void)hipEventDestroy(e);
   p->pending.clear();
-  if (ms_out) for (int kx = 0; kx < 3; ++kx) ms_out[kx] = p->ms[kx];
+  if (ms_out) for (int kx = 0; kx < 2; ++kx) ms_out[kx] = p->ms[kx];
   if (n_out) *n_out = p->n_prof;
-  p->ms[0] = p->ms[1] = p->ms[2] = 0;
+  p->ms[0] = p->ms[1] = 0;
   p->n_prof = 0;
+  return FG_OK;
+}
+
+int fg_plan_diag(fg_plan* p, uint64_t* out, size_t n_words, uint32_t* cand_cnt) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  HIPCHK(hipSetDevice(p->ix->dev));
+  HIPCHK(hipStreamSynchronize(p->last_stream));
+  if (cand_cnt) HIPCHK(hipMemcpy(cand_cnt, p->d.cand_cnt, 4ull * p->nq, hipMemcpyDeviceToHost));
+  if (out && n_words) {
+    if (!p->d.diag) return fail(FG_EUNSUPPORTED, "not a diagnostic build (-DFG_DIAG)");
+    HIPCHK(hipMemcpy(out, p->d.diag, 8 * std::min(n_words, p->diag_words), hipMemcpyDeviceToHost));
+  }
   return FG_OK;
 }
 

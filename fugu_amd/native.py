@@ -19,7 +19,9 @@ import numpy as np
 import torch  # noqa: F401,E402
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfugu.so")
+# FUGU_LIB selects an alternative build of the same ABI (the -DFG_DIAG
+# diagnostic build used by tools/diag_phases.py); default: the product build.
+LIB_PATH = os.environ.get("FUGU_LIB") or os.path.join(_HERE, "libfugu.so")
 
 FG_OK = 0
 FG_EINVAL = -1
@@ -39,7 +41,7 @@ EXPORTS = (
     "fg_index_build_from_docs", "fg_index_build", "fg_index_retain", "fg_index_release",
     "fg_index_stats_get", "fg_index_df", "fg_index_bm25",
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
-    "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_destroy",
+    "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_merge_shards", "fg_bytes_model",
 )
 
@@ -111,6 +113,7 @@ _sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
 _sig("fg_plan_profile", C.c_int, _p, C.c_int)
 _sig("fg_plan_kernel_ms", C.c_int, _p, _f64p, _u32p)
+_sig("fg_plan_diag", C.c_int, _p, _u64p, C.c_size_t, _u32p)
 _sig("fg_plan_destroy", C.c_int, _p)
 _sig("fg_search_batch", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f32p, _u32p, _u32p)
 _sig("fg_merge_shards", C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p)
@@ -309,10 +312,24 @@ class Plan:
         _check(_lib.fg_plan_profile(self._h, 1 if enable else 0))
 
     def kernel_ms(self):
-        ms = np.zeros(3, np.float64)
+        """(summed ms of k_conj, k_final over the profiled executes, executes)."""
+        ms = np.zeros(2, np.float64)
         n = C.c_uint32(0)
         _check(_lib.fg_plan_kernel_ms(self._h, _ptr(ms, _f64p), C.byref(n)))
         return ms, n.value
+
+    def candidate_counts(self):
+        cnt = np.zeros(self.n_queries, np.uint32)
+        _check(_lib.fg_plan_diag(self._h, None, 0, _ptr(cnt, _u32p)))
+        return cnt
+
+    def diag(self):
+        """Per-workgroup phase stamps of the last execute (FG_DIAG builds only)."""
+        info = self.info()
+        n = 8 * (info.total_chunks + self.n_queries)
+        out = np.zeros(n, np.uint64)
+        _check(_lib.fg_plan_diag(self._h, _ptr(out, _u64p), n, None))
+        return out.reshape(-1, 8)[: info.total_chunks], out.reshape(-1, 8)[info.total_chunks:]
 
     def close(self):
         if self._h:

@@ -143,10 +143,15 @@ typedef struct fg_plan_info {
   uint64_t workspace_bytes;
 } fg_plan_info;
 int fg_plan_info_get(const fg_plan* p, fg_plan_info* out);
-/* Per-kernel HIP-event timing of every execute while enabled.  ms_out[3] =
- * summed device time of (k_conj, k_filter, k_final); *n_out = executes. */
+/* Per-kernel HIP-event timing of every execute while enabled.  ms_out[2] =
+ * summed device time of (k_conj, k_final); *n_out = executes.  Resets. */
 int fg_plan_profile(fg_plan* p, int enable);
 int fg_plan_kernel_ms(fg_plan* p, double* ms_out, uint32_t* n_out);
+/* Diagnostics of the last execute: per-query candidate counts (cand_cnt
+ * [n_queries], may be NULL) and, in -DFG_DIAG builds only, 8 u64 phase stamps
+ * per workgroup (k_conj work items, then k_final queries); FG_EUNSUPPORTED
+ * for the stamps in product builds. */
+int fg_plan_diag(fg_plan* p, uint64_t* out, size_t n_words, uint32_t* cand_cnt);
 int fg_plan_destroy(fg_plan* p);
 
 /* Synchronous convenience: plan + execute + copy back.  Host buffers

@@ -1,0 +1,85 @@
+"""Per-workgroup phase timing of k_conj / k_final from the -DFG_DIAG build.
+
+Run on the GPU box:  FUGU_LIB=fugu_amd/libfugu_diag.so python tools/diag_phases.py [--docs N]
+Stamps are s_memrealtime (100 MHz, 10 ns).  Prints a JSON summary.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pct(a, ps=(50, 90, 99, 100)):
+    a = np.asarray(a, np.float64)
+    if a.size == 0:
+        return {}
+    return {f"p{p}": round(float(np.percentile(a, p)), 2) for p in ps}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=10_000_000)
+    ap.add_argument("--terms", type=int, default=3)
+    ap.add_argument("--mixed", action="store_true")
+    ap.add_argument("--k", type=int, default=100)
+    args = ap.parse_args()
+    from fugu_amd import native, synth
+    ctx = native.Context((0,))
+    corp = synth.corpus(args.docs, threads=16)
+    ix = native.Index.from_docs(ctx, corp.off, corp.tok, synth.VOCAB, threads=16)
+    q_off, terms = synth.queries(1024, 1 if args.mixed else args.terms, 5 if args.mixed else args.terms)
+    plan = ix.plan(q_off, terms, args.k)
+    for _ in range(3):
+        plan.execute()
+    plan.results()
+    conj, fin = plan.diag()
+    cc = plan.candidate_counts()
+    us = 1e-2  # 10 ns ticks -> us
+    c_start, c_probe, c_keys, c_sel, c_end = (conj[:, i].astype(np.int64) for i in range(5))
+    dur = (c_end - c_start) * us
+    t0 = c_start.min()
+    nchk = (conj[:, 6] >> np.uint64(40)).astype(np.int64)
+    out = {
+        "k_conj": {
+            "work_items": int(len(conj)),
+            "chunks": int(nchk.sum()),
+            "span_us": round(float((c_end.max() - t0) * us), 1),
+            "wg_us": pct(dur),
+            "wg_us_sum": round(float(dur.sum()), 1),
+            "probe_us_sum": round(float(c_probe.sum() * us), 1),
+            "keys_us_sum": round(float(c_keys.sum() * us), 1),
+            "select_us_sum": round(float(c_sel.sum() * us), 1),
+            "appended_per_chunk": pct(conj[:, 5].astype(np.float64) / np.maximum(nchk, 1)),
+            "written_total": int(conj[:, 7].sum()),
+        },
+    }
+    f_start, f_read, f_sel, f_end = (fin[:, i].astype(np.int64) for i in range(4))
+    fdur = (f_end - f_start) * us
+    out["k_final"] = {
+        "span_us": round(float((f_end.max() - f_start.min()) * us), 1),
+        "wg_us": pct(fdur),
+        "read_us": pct((f_read - f_start) * us),
+        "select_us": pct((f_sel - f_read) * us),
+        "sort_us": pct((f_end - f_sel) * us),
+        "cand_cnt": pct(cc),
+        "slowest": [{"q": int(i), "us": round(float(fdur[i]), 1), "cand": int(cc[i]), "nk": int(fin[i, 6])}
+                    for i in np.argsort(-fdur)[:8]],
+        "start_spread_us": round(float((f_start.max() - f_start.min()) * us), 1),
+    }
+    # per-query k_conj cost
+    qid = (conj[:, 6] & 0xFFFFFFFF).astype(np.int64)
+    per_q = np.bincount(qid, weights=dur, minlength=len(q_off) - 1)
+    top = np.argsort(-per_q)[:8]
+    out["heaviest_queries"] = [{"q": int(i), "wg_us_sum": round(float(per_q[i]), 1),
+                                "items": int((qid == i).sum()), "cand": int(cc[i]),
+                                "dfs": [ix.df(int(t)) for t in terms[q_off[i]:q_off[i + 1]]]} for i in top]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
