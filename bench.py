@@ -52,13 +52,17 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(0)
+    # one rank per GPU; FUGU_DIST_BACKEND=gloo rehearses the N>1 flow with
+    # several ranks on fewer GPUs (the driver's runs use RCCL, one GPU each)
+    backend = os.environ.get("FUGU_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from fugu_amd import native, synth
 
@@ -113,7 +117,7 @@ def main():
     plan.profile(False)
     ms_k, n_prof = plan.kernel_ms()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -135,11 +139,18 @@ def main():
     alg_bytes = float(bm[:, 2].sum())
     conj_ms = ms_k[0] / max(n_prof, 1)
     achieved = alg_bytes / (conj_ms * 1e-3) / 1e9
+    # HBM bytes per k_conj launch from rocprofv3 PMC (FETCH_SIZE x2 gfx950
+    # correction + WRITE_SIZE), collected by tools/profile_bench.sh on this
+    # exact workload and committed under profiles/ (profiles/latest.json)
     traffic = None
-    pmc_file = os.environ.get("FUGU_PMC_BYTES")
-    if pmc_file and os.path.exists(pmc_file):
+    pmc_file = os.environ.get("FUGU_PMC_BYTES") or os.path.join(ROOT, "profiles", "latest.json")
+    if os.path.exists(pmc_file):
         with open(pmc_file) as f:
-            traffic = json.load(f).get("k_conj_hbm_bytes_per_launch")
+            pmc = json.load(f)
+        wl = pmc.get("workload", {})
+        if (not wl or (wl.get("n_docs") == args.docs and wl.get("batch") == nq and wl.get("k") == K
+                       and wl.get("terms") == (args.terms if not args.mixed else "1-5"))):
+            traffic = pmc.get("k_conj_hbm_bytes_per_launch")
 
     # ---- CPU baseline: the oracle (tantivy's algorithm restated in C) on host cores, rank 0, N=1 only
     cpu = None
@@ -202,6 +213,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "k_conj", "kernel_ms": round(conj_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
+                "alg_model": "SURVEY.md 8(d) B(q): tantivy block-decode bytes (1 KiB per probed 128-posting block)",
+                "hbm_gbs_measured": (round(traffic / (conj_ms * 1e-3) / 1e9, 1) if traffic else None),
+                "hbm_frac_measured": (round(traffic / (conj_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None),
             },
             "kernels_ms_per_step": {"k_conj": round(ms_k[0] / max(n_prof, 1), 4),
                                     "k_final": round(ms_k[1] / max(n_prof, 1), 4)},

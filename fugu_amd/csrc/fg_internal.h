@@ -10,7 +10,13 @@ namespace fg {
 constexpr uint32_t kBlock = 128;          // tantivy block size (bytes model only)
 constexpr uint32_t kBucketTarget = 32;    // directory: expected postings per bucket (one 128-B line)
 constexpr uint32_t kThreads = 256;        // 4 waves of 64 per workgroup
-constexpr uint32_t kItems = 8;            // lead candidates per lane
+#ifndef FG_ITEMS
+#define FG_ITEMS 8
+#endif
+#ifndef FG_KARY
+#define FG_KARY 0
+#endif
+constexpr uint32_t kItems = FG_ITEMS;     // lead candidates per lane
 constexpr uint32_t kChunk = kThreads * kItems;   // 2048 lead candidates per work item
 constexpr uint32_t kWaveSpan = kChunk / 4;       // 512 consecutive candidates per wave
 constexpr uint32_t kMaxTerms = 16;        // terms per query (FG_MAX_TERMS)

@@ -194,8 +194,14 @@ __device__ void bitonic_sort_desc(uint64_t* s, uint32_t P) {
 // TopNComputer: append, truncate to the exact k-th when the buffer passes
 // 2048 keys) and, once per chunk, publishes its k-th key to the query's
 // threshold and reads the best one any workgroup has published.
-constexpr uint32_t kBuf = 2 * kChunk;   // kept keys (<= kTrunc) + one chunk of hits
-constexpr uint32_t kTrunc = kChunk;
+#ifndef FG_TRUNC
+#define FG_TRUNC 1024
+#endif
+#ifndef FG_WAVES
+#define FG_WAVES 4  // tools/ab_variants.py: 3 -> 4 waves/SIMD took k_conj 3.18 -> 2.58 ms
+#endif
+constexpr uint32_t kTrunc = FG_TRUNC;           // truncate the local buffer past this (>= kMaxK)
+constexpr uint32_t kBuf = kTrunc + kChunk;       // kept keys (<= kTrunc) + one chunk of hits
 
 struct ConjShared {
   alignas(16) uint64_t buf[kBuf];
@@ -227,7 +233,9 @@ __device__ uint64_t truncate_topk(ConjShared& sh, uint32_t n, uint32_t K) {
   return T;  // keys are unique: exactly K kept
 }
 
-__global__ __launch_bounds__(kThreads) void k_conj(DevIndex ix, DevPlan pl) {
+// FG_WAVES: minimum waves per SIMD the register allocation must allow (the
+// kernel is bound by memory latency, so occupancy is its main lever)
+__global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPlan pl) {
   __shared__ ConjShared sh;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
 

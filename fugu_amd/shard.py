@@ -3,10 +3,10 @@
 One process per GPU; rank r holds namespace r's snapshot.  A fan-out query
 runs on every shard, the per-shard top-k lists are exchanged with ONE
 all-gather per batch (RCCL over xGMI when the group is "nccl"), and the global
-top-k is merged on the device by (score desc, shard asc, doc asc).  Scores are
-not renormalised across namespaces: each namespace keeps its own BM25
-statistics, exactly as each fugu namespace is its own tantivy index
-(src/db/core.rs:49-79).
+top-k is merged on the device by (score desc, shard asc, doc asc)
+(fg_merge_shards).  Scores are not renormalised across namespaces: each
+namespace keeps its own BM25 statistics, exactly as each fugu namespace is its
+own tantivy index (src/db/core.rs:49-79).
 """
 from __future__ import annotations
 
@@ -14,34 +14,32 @@ import torch
 import torch.distributed as dist
 
 
-def gather_topk(score: torch.Tensor, doc: torch.Tensor, n: torch.Tensor, group=None):
-    """All-gather per-shard top-k buffers ([nq*k], [nq*k], [nq]) into
-    ([world, nq*k], [world, nq*k], [world, nq]).  One collective per tensor."""
-    world = dist.get_world_size(group)
-    out_s = torch.empty((world,) + tuple(score.shape), dtype=score.dtype, device=score.device)
-    out_d = torch.empty((world,) + tuple(doc.shape), dtype=doc.dtype, device=doc.device)
-    out_n = torch.empty((world,) + tuple(n.shape), dtype=n.dtype, device=n.device)
-    dist.all_gather_into_tensor(out_s, score.contiguous(), group=group)
-    dist.all_gather_into_tensor(out_d, doc.contiguous(), group=group)
-    dist.all_gather_into_tensor(out_n, n.contiguous(), group=group)
-    return out_s, out_d, out_n
-
-
 def pack_topk(score: torch.Tensor, doc: torch.Tensor, n: torch.Tensor) -> torch.Tensor:
     """One int32 buffer [nq*k*2 + nq] so a batch needs a single all-gather."""
-    return torch.cat([score.view(torch.int32), doc.view(torch.int32), n.view(torch.int32)])
+    return torch.cat([score.reshape(-1).view(torch.int32), doc.reshape(-1).view(torch.int32),
+                      n.reshape(-1).view(torch.int32)])
 
 
-def gather_packed(score: torch.Tensor, doc: torch.Tensor, n: torch.Tensor, group=None):
-    world = dist.get_world_size(group)
-    buf = pack_topk(score, doc, n)
-    out = torch.empty((world, buf.numel()), dtype=torch.int32, device=buf.device)
-    dist.all_gather_into_tensor(out, buf, group=group)
-    nk = score.numel()
+def unpack_topk(out: torch.Tensor, nk: int):
     s = out[:, :nk].contiguous().view(torch.float32)
     d = out[:, nk:2 * nk].contiguous()
     c = out[:, 2 * nk:].contiguous()
     return s, d, c
+
+
+def gather_packed(score: torch.Tensor, doc: torch.Tensor, n: torch.Tensor, group=None):
+    """All-gather per-shard top-k buffers; returns ([world, nq*k] f32, [world, nq*k] i32, [world, nq] i32)
+    on the input's device.  RCCL gathers device memory directly; a gloo group
+    (CPU rehearsal of the N>1 path) goes through host memory."""
+    world = dist.get_world_size(group)
+    buf = pack_topk(score, doc, n)
+    via_host = dist.get_backend(group) == "gloo" and buf.is_cuda
+    src = buf.cpu() if via_host else buf
+    out = torch.empty(world * src.numel(), dtype=torch.int32, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    if via_host:
+        out = out.to(buf.device)
+    return unpack_topk(out.view(world, src.numel()), score.numel())
 
 
 def merge_on_device(s: torch.Tensor, d: torch.Tensor, c: torch.Tensor, nq: int, k: int, stream=None):

@@ -1,0 +1,96 @@
+"""N > 1 path on CPU: world_size-2 gloo group, one namespace per rank.
+
+Each rank searches its own namespace (the CPU oracle stands in for the
+device, whose per-shard results are checked against the same oracle by the
+gpu tests), the per-shard top-k lists go through fugu_amd.shard.gather_packed
+(the exact collective bench.py uses), and the merged fan-out result must equal
+searching every namespace and merging by (score desc, shard asc, doc asc).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _shard_results(rank, n_docs, q_off, terms, k):
+    import sys
+    sys.path.insert(0, ROOT)
+    from fugu_amd import synth
+    from oracle import oracle as orc
+    c = synth.corpus(n_docs, 1 << 16, 1.0, synth.SEED_L + rank, synth.SEED_T + rank)
+    ix = orc.OracleIndex(1 << 16, c.off, c.tok)
+    s, d, n, _, _ = ix.search_batch(q_off, terms, k)
+    return s, d, n
+
+
+def _worker(rank, world, port, n_docs, k, outq):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fugu_amd.shard import gather_packed
+    from fugu_amd import synth
+    q_off, terms = synth.queries(64, 1, 3, max_rank=1 << 9)
+    s, d, n = _shard_results(rank, n_docs, q_off, terms, k)
+    gs, gd, gn = gather_packed(torch.from_numpy(s.reshape(-1)), torch.from_numpy(d.reshape(-1).view(np.int32)),
+                               torch.from_numpy(n.view(np.int32)))
+    if rank == 0:
+        outq.put((gs.numpy(), gd.numpy().view(np.uint32), gn.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_fanout_matches_direct_merge():
+    world, n_docs, k = 2, 3000, 10
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_docs, k, outq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    got = None
+    for _ in range(240):
+        try:
+            got = outq.get(timeout=1)
+            break
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, "a rank failed"
+    assert got is not None, "rank 0 produced no result"
+    gs, gd, gn = got
+    from fugu_amd import synth
+    from shard_ref import merge_topk_numpy
+    q_off, terms = synth.queries(64, 1, 3, max_rank=1 << 9)
+    nq = len(q_off) - 1
+    per = [_shard_results(r, n_docs, q_off, terms, k) for r in range(world)]
+    # the gathered buffers are exactly the per-shard results
+    for r in range(world):
+        assert np.array_equal(gn[r], per[r][2])
+        assert np.array_equal(gd[r].reshape(nq, k), per[r][1])
+        assert np.array_equal(gs[r].reshape(nq, k), per[r][0])
+    sc = np.stack([gs[r].reshape(nq, k) for r in range(world)])
+    dc = np.stack([gd[r].reshape(nq, k) for r in range(world)])
+    ms, md, msh, mn = merge_topk_numpy(sc, dc, gn.astype(np.int64), k)
+    for q in range(nq):
+        rows = sorted([(float(per[r][0][q, i]), r, int(per[r][1][q, i]))
+                       for r in range(world) for i in range(int(per[r][2][q]))], key=lambda x: (-x[0], x[1], x[2]))[:k]
+        assert mn[q] == len(rows)
+        assert [(int(msh[q, i]), int(md[q, i])) for i in range(mn[q])] == [(r[1], r[2]) for r in rows]

@@ -78,6 +78,22 @@ def main():
     out["heaviest_queries"] = [{"q": int(i), "wg_us_sum": round(float(per_q[i]), 1),
                                 "items": int((qid == i).sum()), "cand": int(cc[i]),
                                 "dfs": [ix.df(int(t)) for t in terms[q_off[i]:q_off[i + 1]]]} for i in top]
+    # WG time by query class: lead density and how many probed lists are dense tables
+    n_docs = args.docs
+    cls = {}
+    for i in range(len(q_off) - 1):
+        ts = terms[q_off[i]:q_off[i + 1]].tolist()
+        dfs = sorted(ix.df(int(t)) for t in ts)
+        lead = dfs[0] / n_docs
+        dense = sum(1 for d in dfs[1:] if d * 8 >= n_docs)
+        key = f"lead>={2 ** int(np.floor(np.log2(max(lead, 1e-9))))}|dense_probes={dense}/{len(dfs) - 1}"
+        c = cls.setdefault(key, [0.0, 0, 0])
+        c[0] += float(per_q[i])
+        c[1] += 1
+        c[2] += dfs[0]
+    tot = sum(v[0] for v in cls.values())
+    out["time_by_class"] = {k: {"share": round(v[0] / tot, 4), "queries": v[1], "lead_postings": v[2]}
+                            for k, v in sorted(cls.items(), key=lambda kv: -kv[1][0])}
     print(json.dumps(out, indent=1))
 
 

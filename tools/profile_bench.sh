@@ -9,7 +9,9 @@ set -euo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 TAG=${1:-r01}
 shift || true
-ARGS="--steps 5 --warmup 1 --no-cpu --p50-queries 5 $*"
+# --p50-queries 0: only the batch dispatches, so the trace's average k_conj
+# duration is the batch kernel the bench's roofline line is computed on
+ARGS="--steps 5 --warmup 1 --no-cpu --p50-queries 0 $*"
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
