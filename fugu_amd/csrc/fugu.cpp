@@ -38,7 +38,14 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIPCHK(x)                                                                    \
+}  // namespace
+
+// shared with host.cpp so fg_last_error() reports host-side failures too
+void fg_set_last_error(const std::string& msg) { g_err = msg; }
+
+namespace {
+
+#define HIPCHK(x)                                                                  \
   do {                                                                               \
     hipError_t e_ = (x);                                                             \
     if (e_ != hipSuccess) return fail(FG_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \

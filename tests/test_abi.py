@@ -13,8 +13,8 @@ import pytest
 from conftest import ROOT
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "fugu.h")).read()
+def header_functions(header="fugu.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(fg_[a-z0-9_]+)\s*\(", src)))
 
@@ -31,16 +31,19 @@ def test_library_exports_every_declared_symbol():
     assert os.path.exists(lib_path), "libfugu.so not built"
     out = subprocess.run(["nm", "-D", "--defined-only", lib_path], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"\bT (fg_[a-z0-9_]+)$", out, flags=re.M))
-    missing = [f for f in header_functions() if f not in exported]
+    declared = header_functions() + header_functions("fugu_host.h")
+    missing = [f for f in declared if f not in exported]
     assert not missing, missing
     lib = ctypes.CDLL(lib_path)
-    for f in header_functions():
+    for f in declared:
         getattr(lib, f)
 
 
 def test_python_binding_matches_header():
     from fugu_amd import native
     assert sorted(native.EXPORTS) == header_functions()
+    from fugu_amd import db
+    assert sorted(db.HOST_EXPORTS) == header_functions("fugu_host.h")
 
 
 def test_version_and_errors_without_device():

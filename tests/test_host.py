@@ -1,0 +1,286 @@
+"""Host mirror (include/fugu_host.h): analyzer, query-parser subset, namespace
+registry, upsert semantics and response shapes.  CPU tests use a db without a
+device context (fg_db_create(ctx=NULL)); the end-to-end tests against the
+oracle are marked gpu.
+
+Reference behaviour followed:
+  analyzer      src/db/schemas.rs:10,14 (SimpleTokenizer, RemoveLongFilter(40), LowerCaser)
+  parser        src/db/search.rs:108-127 (QueryParser over [text, name])
+  validation    src/object.rs:31-78, src/db/config.rs:302-315
+  upsert        src/db/document.rs:23-67 (delete_term on the RAW id, then add_document)
+  responses     src/server/handlers/search.rs:56-65,184-195,350-402
+"""
+import json
+import random
+import unicodedata
+
+import numpy as np
+import pytest
+
+from conftest import hits_of
+
+
+@pytest.fixture(scope="module")
+def db():
+    from fugu_amd import db as fdb
+    return fdb
+
+
+def py_analyze(s):
+    """Restatement: runs of alphanumeric chars, drop >= 40 UTF-8 bytes, per-char lowercase."""
+    out, cur = [], []
+    for ch in s + " ":
+        if ch.isalnum():
+            cur.append(ch)
+            continue
+        if cur:
+            t = "".join(cur)
+            if len(t.encode()) < 40:
+                out.append("".join(c.lower() for c in t))
+            cur = []
+    return out
+
+
+# ------------------------------------------------------------------ analyzer
+def test_analyzer_known_answers(db):
+    assert db.analyze("Hello, World!") == ["hello", "world"]
+    assert db.analyze("") == []
+    assert db.analyze("  ...  ") == []
+    assert db.analyze("foo_bar-baz") == ["foo", "bar", "baz"]  # '_' is not alphanumeric
+    assert db.analyze("x" * 39 + " " + "y" * 40) == ["x" * 39]  # RemoveLongFilter limit 40
+    # the limit is in UTF-8 bytes of the original token: 20 x 'é' = 40 bytes -> dropped
+    assert db.analyze("é" * 19 + " " + "é" * 20) == ["é" * 19]
+    assert db.analyze("İstanbul ΣΑΣ Straße") == ["i̇stanbul", "σασ", "straße"]  # per char, no final sigma
+    assert db.analyze("１２３ⅫⅣ") == ["１２３ⅻⅳ"]  # Nd fullwidth digits, Nl roman numerals
+    # Rust char::is_alphabetic includes Other_Alphabetic marks and circled letters
+    assert db.analyze("नःि Ⓐb") == ["नःि", "ⓐb"]
+    assert db.analyze("àb") == ["a", "b"]  # U+0300 is Mn without Other_Alphabetic
+    assert db.analyze("日本語 テキスト") == ["日本語", "テキスト"]
+    assert db.analyze("emoji😀split") == ["emoji", "split"]
+
+
+def test_analyzer_matches_restatement_randomized(db):
+    pools = [
+        [chr(c) for c in range(0x20, 0x7F)],
+        [chr(c) for c in range(0xA0, 0x180)],
+        [chr(c) for c in range(0x370, 0x400) if unicodedata.category(chr(c)) != "Cn"],
+        [chr(c) for c in range(0x400, 0x460)],
+        [chr(c) for c in range(0x4E00, 0x4E40)],
+        ["😀", "→", "—", "\t", "\n", "  "],
+    ]
+    rng = random.Random(1234)
+    for _ in range(300):
+        n = rng.randint(0, 120)
+        s = "".join(rng.choice(rng.choice(pools)) for _ in range(n))
+        assert db.analyze(s) == py_analyze(s), repr(s)
+
+
+def test_alnum_table_extends_python_isalnum_only_with_marks():
+    """kAlnumRanges = Python isalnum (L*, N*) + Other_Alphabetic (Mn/Mc/So marks)."""
+    import os
+    import re
+    from conftest import ROOT
+    src = open(os.path.join(ROOT, "fugu_amd", "csrc", "unicode_tables.inc")).read()
+    body = src[src.index("kAlnumRanges"):src.index("kLower")]
+    ranges = [(int(a, 16), int(b, 16)) for a, b in re.findall(r"\{0x([0-9A-F]+), 0x([0-9A-F]+)\}", body)]
+    table = np.zeros(0x110000, bool)
+    for a, b in ranges:
+        table[a:b + 1] = True
+    py = np.array([chr(c).isalnum() if not 0xD800 <= c <= 0xDFFF else False for c in range(0x110000)])
+    py[:0x80] = False  # ASCII handled inline in host.cpp
+    assert not (py & ~table).any()
+    extra = np.nonzero(table & ~py)[0]
+    cats = {unicodedata.category(chr(c)) for c in extra}
+    assert cats <= {"Mn", "Mc", "So"}, cats
+
+
+# ------------------------------------------------------------------ parser
+def test_parser_device_subset(db):
+    AND, OR = 0, 1
+    assert db.parse_query("rust") == (AND, ["rust"])
+    assert db.parse_query("Rust") == (AND, ["rust"])
+    assert db.parse_query("  rust  ") == (AND, ["rust"])
+    assert db.parse_query("foo AND Bar AND baz") == (AND, ["foo", "bar", "baz"])
+    assert db.parse_query("+foo +bar") == (AND, ["foo", "bar"])
+    assert db.parse_query("foo bar") == (OR, ["foo", "bar"])
+    assert db.parse_query("straße ÜBER") == (OR, ["straße", "über"])
+
+
+@pytest.mark.parametrize("q", ["", "   ", "a -b", "name:x", '"a b"', "foo-bar", "a OR b", "a AND", "AND a",
+                               "a AND b OR c", "(a b)", "a^2", "a~1", "fo*", "a AND AND b", "+a b", "..."])
+def test_parser_rejects_outside_subset(db, q):
+    from fugu_amd import native
+    with pytest.raises(native.Unsupported):
+        db.parse_query(q)
+
+
+# ------------------------------------------------------------------ registry / ingest
+def test_namespace_registry(db):
+    d = db.Database(default_namespace="fugu_db")
+    assert d.namespaces() == ["fugu_db"]
+    d.create_namespace("docs")
+    d.create_namespace("a.b-c_d")
+    assert json.loads(d.namespaces_json()) == {"status": "success", "namespaces": ["a.b-c_d", "docs", "fugu_db"]}
+    for bad in ["", "a/b", "a\\b", "a:b", "a*b", "a?b", 'a"b', "a<b", "a>b", "a|b"]:
+        with pytest.raises(db.native.FuguError) as e:
+            d.create_namespace(bad)
+        assert e.value.code == db.native.FG_EINVAL
+    with pytest.raises(db.Exists):
+        d.create_namespace("docs")
+    d.delete_namespace("docs")
+    with pytest.raises(db.NotFound):
+        d.delete_namespace("docs")
+    with pytest.raises(db.NotFound):
+        d.upsert(db.ObjectRecord("x", "y"), "docs")
+    assert d.namespaces() == ["a.b-c_d", "fugu_db"]
+
+
+def test_object_record_validation(db):
+    d = db.Database()
+    ok = dict(text="hello")
+    cases = [
+        (db.ObjectRecord("", "t"), "Object ID cannot be empty"),
+        (db.ObjectRecord("x" * 257, "t"), "Object ID too long"),
+        (db.ObjectRecord("x", ""), "Object text cannot be empty"),
+        (db.ObjectRecord("x", "t" * 10001), "Text too long"),
+    ]
+    for rec, msg in cases:
+        with pytest.raises(db.native.FuguError) as e:
+            d.upsert(rec)
+        assert msg in str(e.value)
+    d.upsert(db.ObjectRecord("x" * 256, "t" * 10000))
+    d.create_namespace("has space")
+    with pytest.raises(db.native.FuguError) as e:
+        d.upsert(db.ObjectRecord("x", **ok), "has space")
+    assert "Invalid namespace format" in str(e.value)
+    assert d.doc_count() == (1, 1)
+
+
+def test_upsert_deletes_by_raw_id_term(db):
+    """delete_term(id_field, raw id) matches the TOKENIZED id field: lowercase
+    single-token ids replace, ids with capitals/punctuation accumulate."""
+    d = db.Database()
+    d.upsert(db.ObjectRecord("doc1", "a"))
+    d.upsert(db.ObjectRecord("doc1", "b"))
+    assert d.doc_count() == (2, 1)
+    d.upsert(db.ObjectRecord("Doc2", "a"))
+    d.upsert(db.ObjectRecord("Doc2", "b"))
+    assert d.doc_count() == (4, 3)
+    d.upsert(db.ObjectRecord("my-doc", "a"))     # tokens: my, doc
+    d.upsert(db.ObjectRecord("my-doc", "b"))     # raw "my-doc" matches no token
+    assert d.doc_count() == (6, 5)
+    d.upsert(db.ObjectRecord("doc", "c"))        # raw "doc" matches the "doc" token of both my-doc docs
+    assert d.doc_count() == (7, 4)
+
+
+def test_commit_needs_a_device_and_search_before_commit_is_empty(db):
+    d = db.Database()
+    d.upsert(db.ObjectRecord("a", "hello world"))
+    with pytest.raises(db.native.FuguError) as e:
+        d.commit()
+    assert e.value.code == db.native.FG_ENODEV
+    assert d.search(None, "hello") == []
+    r = json.loads(d.search_json(None, "hello", page=0, per_page=0))
+    assert r == {"results": [], "total": 0, "page": 0, "per_page": 20, "query": "hello"}  # per_page clamp
+    r = json.loads(d.search_json(None, "hello", page=2, per_page=5, shape=db.SHAPE_POST_SEARCH))
+    assert r == {"status": "success", "query": "hello", "filters": [], "page": 2, "per_page": 5, "total": 0,
+                 "results": []}
+    with pytest.raises(db.NotFound) as e:
+        d.search_json("nope", "hello")
+    assert "Namespace 'nope' not found" in str(e.value)
+    with pytest.raises(db.native.Unsupported):
+        d.search(None, "a -b")
+    with pytest.raises(db.native.Unsupported):
+        d.search(None, "hello", page=1000, per_page=100)  # offset + per_page > FG_MAX_K
+
+
+# ------------------------------------------------------------------ end to end on the device
+WORDS = ["Alpha", "beta", "Gamma", "delta", "épsilon", "ZETA", "eta", "théta", "iota", "kappa", "lambda", "mu",
+         "nu", "xi", "omicron", "pi", "rho", "sigma", "tau", "upsilon", "phi", "chi", "psi", "omega", "日本",
+         "straße", "1999", "x86"]
+
+
+def build_corpus(seed, n):
+    rng = random.Random(seed)
+    recs = []
+    for i in range(n):
+        words = [rng.choice(WORDS[:rng.randint(3, len(WORDS))]) for _ in range(rng.randint(1, 30))]
+        seps = [rng.choice([" ", ", ", ". ", "\n", " - "]) for _ in words]
+        text = "".join(w + s for w, s in zip(words, seps))
+        rid = rng.choice([f"doc{i}", f"doc{rng.randint(0, max(0, i - 1))}", f"Doc{i}", f"d-{i % 50}"])
+        meta = {"name": " ".join(rng.choice(WORDS) for _ in range(rng.randint(1, 3)))} if rng.random() < 0.5 \
+            else ({"tag": i} if rng.random() < 0.3 else None)
+        recs.append((rid, text, meta))
+    return recs
+
+
+def oracle_of(recs):
+    """Token-id CSR + deleted mask restated in Python from the reference semantics."""
+    from oracle import oracle as orc
+    dic, text, name, ids, deleted = {}, [], [], [], []
+
+    def intern(s):
+        return [dic.setdefault(t, len(dic)) for t in py_analyze(s)]
+    for rid, t, meta in recs:
+        for j, toks in enumerate(ids):
+            if rid in toks:
+                deleted[j] = 1
+        text.append(intern(t))
+        nm = meta.get("name") if meta else None
+        name.append(intern(nm) if isinstance(nm, str) else [])
+        ids.append(py_analyze(rid))
+        deleted.append(0)
+    from conftest import tokens_to_csr
+    to, tt = tokens_to_csr(text)
+    no, nt = tokens_to_csr(name)
+    ix = orc.OracleIndex(max(1, len(dic)), to, tt, no, nt, np.array(deleted, np.uint8))
+    return ix, dic
+
+
+@pytest.mark.gpu
+def test_db_end_to_end_vs_oracle(db):
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("docs")
+    recs = build_corpus(7, 3000)
+    for rid, t, meta in recs:
+        d.upsert(db.ObjectRecord(rid, t, metadata=meta), "docs")
+    d.commit("docs")
+    ix, dic = oracle_of(recs)
+    assert d.doc_count("docs")[0] == len(recs)
+    rng = random.Random(99)
+    checked = 0
+    for _ in range(60):
+        m = rng.randint(1, 4)
+        ws = [rng.choice(WORDS) for _ in range(m)]
+        q = ws[0] if m == 1 else (" AND ".join(ws) if rng.random() < 0.5 else " ".join("+" + w for w in ws))
+        page, per_page = rng.randint(0, 3), rng.choice([1, 5, 10, 20])
+        got = d.search("docs", q, page, per_page)
+        terms = [dic.get(t, native.FG_TERM_MISSING) for t in (py_analyze(w)[0] for w in ws)]
+        s, dd = ix.search(np.array(terms, np.uint32), (page + 1) * per_page)
+        want = hits_of(s, dd)[page * per_page:]
+        assert hits_of([g[0] for g in got], [g[1] for g in got]) == want, q
+        checked += len(want)
+        # the JSON shape carries the same hits: ids of the docs, shortest-f32 scores
+        r = json.loads(d.search_json("docs", q, page, per_page, include_text=True))
+        assert r["total"] == len(want) and r["page"] == page and r["per_page"] == per_page and r["query"] == q
+        for h, (doc, bits) in zip(r["results"], want):
+            assert h["id"] == recs[doc][0] and h["text"] == recs[doc][1]
+            assert np.float32(h["score"]).view(np.uint32) == bits
+            assert h["metadata"] == recs[doc][2] and h["facets"] is None
+    assert checked > 100
+    r = json.loads(d.search_json("docs", WORDS[1], 0, 3))
+    assert all("text" not in h for h in r["results"])
+    # a second batch of upserts is invisible until commit, then visible
+    before = d.search("docs", "brandnewword")
+    d.add_file("docs", "notes.txt", "brandnewword appears here")
+    assert before == []
+    got = d.search("docs", "brandnewword")
+    assert len(got) == 1 and got[0][1] == len(recs)
+    r = json.loads(d.search_json("docs", "brandnewword", shape=db.SHAPE_POST_SEARCH))
+    assert r["results"][0]["id"] == "notes.txt" and r["results"][0]["metadata"] == {"name": "notes.txt"}
+    with pytest.raises(native.Unsupported):
+        d.search("docs", "alpha beta")  # multi-term OR: host CPU path in v1
