@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p50-queries", type=int, default=200)
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the secondary workloads (C3 mixed AND, disjunctive OR top-1000)")
+    ap.add_argument("--extra-steps", type=int, default=5)
     args = ap.parse_args()
 
     import torch
@@ -155,6 +158,7 @@ def main():
     # ---- CPU baseline: the oracle (tantivy's algorithm restated in C) on host cores, rank 0, N=1 only
     cpu = None
     parity = None
+    ref = None
     s_gpu = out_s.cpu().numpy().reshape(nq, K)
     d_gpu = out_d.cpu().numpy().view(np.uint32).reshape(nq, K)
     n_gpu = out_n.cpu().numpy()
@@ -185,6 +189,64 @@ def main():
                          f"warm in-RAM index (tantivy 0.24.1 algorithm restated in C: oracle/fugu_oracle.c)",
                "p50_ms": round(float(np.median(lat_all)) * 1e-6, 4)}
         parity = {"queries_checked": done, "mismatches": mism, "rule": "doc ids exact, scores rtol 1e-5"}
+
+    # ---- secondary workloads on the same index (rank 0, N=1): SURVEY §8(d) C3 and the
+    # disjunctive C5 query shape (k_disj), each timed the same way and parity-sampled
+    extra = None
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = {}
+        specs = [("C3_mixed_and", 1, 5, 100, native.MODE_AND), ("C5_or_top1000", 2, 5, 1000, native.MODE_OR)]
+        for name, a_min, a_max, kk, mode in specs:
+            qo_all, qt_all = synth.queries(4096, a_min, a_max)
+            qo = qo_all[: nq + 1].copy()
+            qt = qt_all[: qo[-1]].copy()
+            pl2 = ix.plan(qo, qt, kk, mode=mode)
+            os2 = torch.empty(nq * kk, dtype=torch.float32, device=dev)
+            od2 = torch.empty(nq * kk, dtype=torch.int32, device=dev)
+            on2 = torch.empty(nq, dtype=torch.int32, device=dev)
+            for _ in range(2):
+                pl2.execute(stream.cuda_stream, os2.data_ptr(), od2.data_ptr(), on2.data_ptr())
+            torch.cuda.synchronize()
+            pl2.profile(True)
+            t1 = time.perf_counter()
+            for _ in range(args.extra_steps):
+                pl2.execute(stream.cuda_stream, os2.data_ptr(), od2.data_ptr(), on2.data_ptr())
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t1
+            pl2.profile(False)
+            kms, kn = pl2.kernel_ms()
+            dfs = np.array([ix.df(int(t)) for t in qt], np.float64)
+            merge_bytes = 8.0 * dfs.sum()  # every posting of every clause once (exhaustive merge/union)
+            ent = {"value": round(nq * args.extra_steps / el, 1), "unit": "queries/s",
+                   "ms_per_step": round(el * 1e3 / args.extra_steps, 4), "batch": nq, "k": kk,
+                   "terms": f"{a_min}-{a_max}", "mode": "AND" if mode == native.MODE_AND else "OR",
+                   "kernel": "k_conj" if mode == native.MODE_AND else "k_disj",
+                   "kernel_ms": round(kms[0] / max(kn, 1), 4), "k_final_ms": round(kms[1] / max(kn, 1), 4),
+                   "merge_bytes_per_launch": merge_bytes,
+                   "merge_equiv_gbs": round(merge_bytes / (kms[0] / max(kn, 1) * 1e-3) / 1e9, 1)}
+            if ref is not None:
+                s2 = os2.cpu().numpy().reshape(nq, kk)
+                d2 = od2.cpu().numpy().view(np.uint32).reshape(nq, kk)
+                n2 = on2.cpu().numpy()
+                done, wall, mism = 0, 0.0, 0
+                budget = args.cpu_seconds / 2
+                while done < nq and wall < budget:
+                    hi = min(nq, done + 32)
+                    so = (qo[done:hi + 1] - qo[done]).astype(np.uint32)
+                    rs, rd, rn, w, _ = ref.search_batch(so, qt[qo[done]:qo[hi]], kk, mode=mode, threads=threads)
+                    wall += w
+                    for j in range(hi - done):
+                        i, m = done + j, int(rn[j])
+                        if (int(n2[i]) != m or not np.array_equal(d2[i, :m], rd[j, :m])
+                                or not np.allclose(s2[i, :m], rs[j, :m], rtol=1e-5, atol=0)):
+                            mism += 1
+                    done = hi
+                ent["cpu_baseline"] = {"value": round(done / wall, 2), "unit": "queries/s", "cores": threads,
+                                       "kind": "port", "sample": f"first {done} queries, exhaustive oracle"}
+                ent["parity"] = {"queries_checked": done, "mismatches": mism}
+            extra[name] = ent
+            log(f"[bench] {name}: {ent['value']} q/s, {ent['kernel']} {ent['kernel_ms']} ms")
+            del pl2
 
     if rank == 0:
         out = {
@@ -222,6 +284,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "speedup_vs_cpu": round(qps / cpu["value"], 1) if cpu else None,
+            "secondary": extra,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

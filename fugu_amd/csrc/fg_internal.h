@@ -27,6 +27,8 @@ constexpr uint32_t kMaxDense = 4096;      // at most this many dense tables per 
 constexpr uint32_t kGroupsPerQuery = 64;  // a query's chunks are split into ~this many work items
 constexpr uint32_t kMaxGroup = 16;        // ... of at most this many chunks each
 constexpr uint32_t kHistBins = 2048;      // 11-bit radix digits
+constexpr uint32_t kDisjTileShift = 12;   // k_disj: 4096-doc tiles
+constexpr uint32_t kDisjMaxGroup = 64;    // ... at most this many tiles per work item
 
 constexpr uint32_t kModeAnd = 0;
 constexpr uint32_t kModeOr = 1;
@@ -56,6 +58,7 @@ struct DevIndex {
   const uint8_t* fn_name;    // [N] fieldnorm ids (all 0 when no `name` values)
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
   const float* cache;        // [512] bm25 tf cache: [0,256) text, [256,512) name
+  const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   uint32_t n_docs;
   uint32_t n_terms;
   uint32_t has_name;
@@ -74,8 +77,8 @@ struct DevPlan {
   const uint32_t* q_terms;      // [nq * kMaxTerms] term ids, intersection (cost) order
   const uint32_t* q_lead_df;    // [nq] length of the lead list (0 => empty result)
   const uint32_t* work_q;       // [total_chunks] query of each work item (sweep order)
-  const uint32_t* work_c;       // [total_chunks] first chunk of the item's group
-  const uint32_t* work_n;       // [total_chunks] chunks in the item's group (<= kMaxGroup)
+  const uint32_t* work_c;       // [total_chunks] first chunk of the item's group (k_disj: first tile)
+  const uint32_t* work_n;       // [total_chunks] chunks in the item's group (k_disj: tiles)
   const uint64_t* cand_off;     // [nq+1] candidate-list capacity offsets (work items of q * k)
   // workspace, zeroed per run
   uint64_t* thresh;             // [nq] monotone lower bound on the k-th best key
@@ -103,6 +106,7 @@ __host__ __device__ inline uint32_t key_doc(uint64_t k) { return 0xFFFFFFFFu - (
 
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
+hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,

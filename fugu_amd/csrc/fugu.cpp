@@ -85,6 +85,20 @@ void bm25_cache(float avgdl, float* out) {
   const uint32_t* t = fn_table().v;
   for (int i = 0; i < 256; ++i) out[i] = kK1 * ((1.0f - kB) + (kB * (float)t[i]) / avgdl);
 }
+// kernels.hip term_score on the host (same f32 operations; -ffp-contract=off)
+float term_score_host(uint32_t tfp, uint32_t fn_t, uint32_t fn_n, float wt, float wn, const float* cache) {
+  float s = 0.0f;
+  const uint32_t tt = tfp & 0xFFFFu, tn = tfp >> 16;
+  if (tt) {
+    const float tf = (float)tt;
+    s += wt * (tf / (tf + cache[fn_t]));
+  }
+  if (tn) {
+    const float tf = (float)tn;
+    s += wn * (tf / (tf + cache[256 + fn_n]));
+  }
+  return s;
+}
 
 template <class F>
 void parallel_ranges(uint32_t n, int threads, F&& f) {
@@ -144,6 +158,7 @@ struct fg_index {
   float cache[512];
   std::vector<uint64_t> off;
   std::vector<uint32_t> df_text, df_name;
+  std::vector<uint32_t> first_doc, last_doc;
   std::vector<float> w_text, w_name;
   std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model
   fg::DevIndex d{};
@@ -238,19 +253,33 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
     nd += nbk + 1;
   }
   std::vector<uint32_t> dir(nd);
+  // bucket score maxima (parallel to dir): the per-bucket upper bound the
+  // disjunctive kernel prunes with (block-max WAND / MaxScore bounds)
+  std::vector<float> bmax(nd, 0.0f);
+  const bool has_name = hp.has_name;
   parallel_ranges(V, hw_threads(0), [&](int, uint32_t tb, uint32_t te) {
     for (uint32_t t = tb; t < te; ++t) {
       const uint64_t b0 = hp.off[t], n = hp.off[t + 1] - b0;
       const uint32_t B = tmeta[t];
       const uint64_t nbk = ((N - 1) >> B) + 1;
       uint32_t* dt = dir.data() + dir_off[t];
+      float* bm = bmax.data() + dir_off[t];
+      const float wt = ix->w_text[t], wn = ix->w_name[t];
       uint64_t p = 0;
       uint32_t maxocc = 0;
       for (uint64_t b = 0; b <= nbk; ++b) {
         const uint64_t lo = b << B;
-        while (p < n && hp.doc[b0 + p] < lo) ++p;
+        float mx = 0.0f;
+        while (p < n && hp.doc[b0 + p] < lo) {
+          const uint32_t d = hp.doc[b0 + p], tfp = hp.tf[b0 + p];
+          mx = std::max(mx, term_score_host(tfp, hp.fn_text[d], has_name ? hp.fn_name[d] : 0, wt, wn, ix->cache));
+          ++p;
+        }
         dt[b] = (uint32_t)p;
-        if (b) maxocc = std::max<uint32_t>(maxocc, dt[b] - dt[b - 1]);
+        if (b) {
+          maxocc = std::max<uint32_t>(maxocc, dt[b] - dt[b - 1]);
+          bm[b - 1] = mx;
+        }
       }
       uint32_t S = 0;
       while ((1ull << S) <= maxocc) ++S;  // 2^S > largest bucket
@@ -285,12 +314,14 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
   uint16_t* d_dense = nullptr;
   uint32_t *d_doc, *d_tf, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr;
   uint64_t* d_off;
-  float *d_wt, *d_wn, *d_cache;
+  float *d_wt, *d_wn, *d_cache, *d_bmax;
   uint8_t *d_fnt, *d_fnn;
   if ((rc = dev_upload(ix->mem, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.tf.data(), hp.tf.size(), &d_tf, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.off.data(), hp.off.size(), &d_off, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, dir.data(), dir.size(), &d_dir, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, bmax.data(), bmax.size(), &d_bmax, &bytes))) return rc;
+  std::vector<float>().swap(bmax);
   if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, dense.data(), dense.size(), &d_dense, &bytes))) return rc;
@@ -302,7 +333,15 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
   if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
   if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
   ix->d = fg::DevIndex{d_doc, d_tf, d_off, d_dir, d_dir_off, d_tmeta, d_dense, d_wt, d_wn, d_fnt, d_fnn, d_alive,
-                       d_cache, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
+                       d_cache, d_bmax, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
+  // per-term doc span (disjunctive plans skip the tiles outside it)
+  ix->first_doc.assign(V, 0);
+  ix->last_doc.assign(V, 0);
+  for (uint32_t t = 0; t < V; ++t)
+    if (hp.off[t + 1] > hp.off[t]) {
+      ix->first_doc[t] = hp.doc[hp.off[t]];
+      ix->last_doc[t] = hp.doc[hp.off[t + 1] - 1];
+    }
   ix->dir_entries = nd;
   ix->device_bytes = bytes;
   ix->off = std::move(hp.off);
@@ -570,16 +609,48 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k=%u > FG_MAX_K=%d", k, FG_MAX_K);
   if (q->mode != FG_MODE_AND && q->mode != FG_MODE_OR) return fail(FG_EINVAL, "bad mode %d", q->mode);
   const uint32_t nq = q->n_queries;
+  const bool disj = q->mode == FG_MODE_OR;
   std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), nchunk(nq);
   uint64_t chunks = 0;
+  // work items: each query's chunks (AND) or doc tiles (OR) in ~kGroupsPerQuery
+  // groups, ordered as a doc sweep across the batch (a group centred at doc
+  // fraction x runs with the other queries' groups near x), ties by query
+  struct W { double key; uint32_t q, c, n; };
+  std::vector<W> items;
+  std::vector<uint32_t> ngroup(nq, 0);
   for (uint32_t i = 0; i < nq; ++i) {
     const uint32_t b = q->q_off[i], e = q->q_off[i + 1];
     if (e < b) return fail(FG_EINVAL, "q_off not monotone at query %u", i);
     const uint32_t m = e - b;
     if (m == 0) return fail(FG_EUNSUPPORTED, "query %u is empty (AllQuery runs on the CPU path)", i);
     if (m > fg::kMaxTerms) return fail(FG_EUNSUPPORTED, "query %u has %u terms (> %u)", i, m, fg::kMaxTerms);
-    if (q->mode == FG_MODE_OR && m > 1)
-      return fail(FG_EUNSUPPORTED, "query %u: multi-term disjunction runs on the CPU path in v1", i);
+    if (disj) {
+      // Should clauses in clause order (SumCombiner order); a clause on a term
+      // absent from the snapshot matches nothing and is dropped
+      uint32_t mm = 0, dlo = 0xFFFFFFFFu, dhi = 0;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t t = q->terms[b + j];
+        if (t >= ix->n_terms || ix->off[t + 1] == ix->off[t]) continue;
+        q_terms[(size_t)i * fg::kMaxTerms + mm++] = t;
+        dlo = std::min(dlo, ix->first_doc[t]);
+        dhi = std::max(dhi, ix->last_doc[t]);
+      }
+      q_m[i] = mm;
+      if (!mm) continue;
+      const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
+      const uint32_t nt = thi - tlo + 1;
+      const uint32_t G = std::min<uint32_t>(fg::kDisjMaxGroup,
+                                            std::max<uint32_t>(1, (nt + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
+      const uint32_t ng = (nt + G - 1) / G;
+      ngroup[i] = ng;
+      for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t t0 = tlo + g * G, n = std::min(G, nt - g * G);
+        const double mid = ((double)t0 + 0.5 * n) * (double)(1u << fg::kDisjTileShift) / (double)ix->n_docs;
+        items.push_back(W{mid, i, t0, n});
+      }
+      if (items.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", items.size());
+      continue;
+    }
     // tantivy intersect_scorers: children sorted by cost (union cost = df_text + df_name), stable
     struct T { uint64_t cost; uint32_t pos, term; };
     T ts[fg::kMaxTerms];
@@ -600,14 +671,6 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     chunks += nchunk[i];
     if (chunks > 0x7FFFFFFFull)
       return fail(FG_EUNSUPPORTED, "batch too large (%llu work items)", (unsigned long long)chunks);
-  }
-  // work items: each query's chunks in ~kGroupsPerQuery groups of <= kMaxGroup
-  // consecutive chunks, ordered as a doc sweep across the batch (group g of n
-  // covers ~[g/n, (g+1)/n) of the doc space), ties by query
-  struct W { double key; uint32_t q, c, n; };
-  std::vector<W> items;
-  std::vector<uint32_t> ngroup(nq);
-  for (uint32_t i = 0; i < nq; ++i) {
     const uint32_t nch = nchunk[i];
     const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
     const uint32_t ng = (nch + G - 1) / G;
@@ -710,7 +773,8 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventRecord(ev[0], s));
   }
-  HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
+  if (p->mode == FG_MODE_OR) HIPCHK(fg::launch_disj(p->ix->d, p->d, s));
+  else HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
   if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
   HIPCHK(fg::launch_final(p->d, os, od, on, s));
   if (p->profile) {

@@ -211,26 +211,55 @@ struct ConjShared {
   uint64_t thr;
 };
 
-// Keep exactly the K largest of sh.buf[0, n) at the front; returns the K-th key.
-__device__ uint64_t truncate_topk(ConjShared& sh, uint32_t n, uint32_t K) {
+// Keep exactly the K largest of buf[0, n) at the front (n <= Cap); returns the K-th key.
+template <uint32_t Cap>
+__device__ uint64_t truncate_keys(uint64_t* buf, uint32_t* n_buf, uint32_t* hist, uint32_t* scratch, uint32_t n,
+                                  uint32_t K) {
   const uint32_t tid = threadIdx.x;
-  const uint64_t T = select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
-    for (uint32_t i = tid; i < n; i += kThreads) f(sh.buf[i]);
+  const uint64_t T = select_kth(K, hist, scratch, [&](auto&& f) {
+    for (uint32_t i = tid; i < n; i += kThreads) f(buf[i]);
   });
-  constexpr uint32_t R = kBuf / kThreads;
+  constexpr uint32_t R = Cap / kThreads;
   uint64_t v[R];
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t i = r * kThreads + tid;
-    v[r] = i < n ? sh.buf[i] : 0;
+    v[r] = i < n ? buf[i] : 0;
   }
   __syncthreads();
-  if (tid == 0) sh.n_buf = 0;
+  if (tid == 0) *n_buf = 0;
   __syncthreads();
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) wave_append(r * kThreads + tid < n && v[r] >= T, v[r], sh.buf, &sh.n_buf, kBuf);
+  for (uint32_t r = 0; r < R; ++r) wave_append(r * kThreads + tid < n && v[r] >= T, v[r], buf, n_buf, Cap);
   __syncthreads();
   return T;  // keys are unique: exactly K kept
+}
+
+__device__ inline uint64_t truncate_topk(ConjShared& sh, uint32_t n, uint32_t K) {
+  return truncate_keys<kBuf>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+}
+
+// Append the kept keys of buf[0, n) that clear `cur` to query q's candidate list.
+__device__ uint32_t flush_candidates(const DevPlan& pl, uint32_t q, const uint64_t* buf, uint32_t n, uint64_t cur,
+                                     uint32_t* scratch) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t mine = 0;
+  for (uint32_t i = tid; i < n; i += kThreads) mine += buf[i] >= cur ? 1u : 0u;
+  const uint32_t before = block_exclusive_scan(mine, scratch);
+  if (tid == kThreads - 1) scratch[6] = before + mine;
+  __syncthreads();
+  const uint32_t total = scratch[6];
+  if (total) {
+    if (tid == 0) scratch[7] = atomicAdd(&pl.cand_cnt[q], total);
+    __syncthreads();
+    uint64_t* out = pl.cand_keys + pl.cand_off[q] + scratch[7];
+    uint32_t at = before;
+    for (uint32_t i = tid; i < n; i += kThreads) {
+      const uint64_t k = buf[i];
+      if (k >= cur) out[at++] = k;
+    }
+  }
+  return total;
 }
 
 // FG_WAVES: minimum waves per SIMD the register allocation must allow (the
@@ -386,24 +415,8 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   }
 
   // write the kept keys that still clear the freshest threshold
-  const uint32_t n = sh.n_buf;
-  const uint64_t cur = sh.thr;
-  uint32_t mine = 0;
-  for (uint32_t i = tid; i < n; i += kThreads) mine += sh.buf[i] >= cur ? 1u : 0u;
-  const uint32_t before = block_exclusive_scan(mine, sh.scratch);
-  if (tid == kThreads - 1) sh.scratch[6] = before + mine;
-  __syncthreads();
-  const uint32_t total = sh.scratch[6];
-  if (total) {
-    if (tid == 0) sh.scratch[7] = atomicAdd(&pl.cand_cnt[q], total);
-    __syncthreads();
-    uint64_t* out = pl.cand_keys + pl.cand_off[q] + sh.scratch[7];
-    uint32_t at = before;
-    for (uint32_t i = tid; i < n; i += kThreads) {
-      const uint64_t k = sh.buf[i];
-      if (k >= cur) out[at++] = k;
-    }
-  }
+  const uint32_t total = flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
+  (void)total;
   FG_STAMP(w, 0, t_start);
   FG_STAMP(w, 1, t_probe);
   FG_STAMP(w, 2, t_keys);
@@ -412,6 +425,302 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   FG_STAMP(w, 5, n_app);
   FG_STAMP(w, 6, ((uint64_t)nc << 40) | ((uint64_t)m << 32) | q);
   FG_STAMP(w, 7, total);
+}
+
+// ---------------------------------------------------------------- k_disj
+// Pure disjunction `t1 t2 ...` (Should clauses; query/union + SumCombiner,
+// boolean_weight.rs): score = 0.0 + s_1 + s_2 + ... over the clauses a doc
+// matches, in clause order.  A work item is a run of consecutive 4096-doc
+// tiles of one query.  Per tile:
+//   1. each wave resolves its clauses' posting range inside the tile through
+//      the bucket directory and the clause's upper bound = max of the bucket
+//      maxima (DevIndex::bmax) the tile overlaps;
+//   2. MaxScore split against the query's threshold: sorted by bound, the
+//      longest prefix of clauses whose summed bound cannot reach the threshold
+//      is "non-essential" -- a doc matching only those cannot enter the top-k.
+//      All clauses non-essential: the tile is skipped outright;
+//   3. the essential clauses' postings are scatter-added into an LDS score
+//      array indexed by doc - tile start, clause by clause (one barrier per
+//      clause, so each doc's sum is formed in clause order: exact when every
+//      clause is essential);
+//   4. docs whose accumulated score (+ the non-essential bound, when some
+//      clauses were skipped) clears the threshold become hits -- or, in the
+//      pruned case, candidates that are rescored exactly by probing every
+//      clause through the directory, in clause order;
+//   5. hits go through the same local top-k buffer / threshold publication as
+//      k_conj, and k_final selects the query's top-k.
+// Bounds are compared after inflating by 2^-17 relative, which covers any
+// f32 summation-order difference for <= 16 clauses, so the
+// pruning never drops a true top-k doc: results equal the exhaustive union.
+constexpr uint32_t kTileShift = kDisjTileShift;
+constexpr uint32_t kTile = 1u << kTileShift;   // docs per tile (LDS score array: 16 KB)
+constexpr uint32_t kRound = 1024;              // scan round: entries per workgroup pass
+constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one round of hits
+
+struct DisjShared {
+  float acc[kTile];
+  alignas(16) uint64_t buf[kBufD];
+  uint32_t cand[kRound];
+  uint32_t hist[kHistBins];
+  uint32_t scratch[8];
+  uint32_t t_lo[kMaxTerms], t_hi[kMaxTerms];
+  float t_ub[kMaxTerms];
+  uint32_t n_buf, n_cand, ess, tile_mode;
+  float ub_ne;
+  uint64_t thr;
+};
+
+__device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f; }  // 1 + 2^-17
+
+__device__ inline bool doc_alive(const DevIndex& ix, uint32_t d) {
+  return !ix.alive || ((ix.alive[d >> 5] >> (d & 31)) & 1u);
+}
+
+// packed tf of term t in doc d (0: absent) -- one directory probe (k_conj's
+// search, one item)
+__device__ inline uint32_t probe_tf(const DevIndex& ix, uint32_t t, uint32_t d) {
+  const uint32_t meta = ix.tmeta[t];
+  const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu, dslot = meta >> 16;
+  if (dslot) return ix.dense[(size_t)(dslot - 1) * ix.n_docs + d];
+  const uint64_t bi = ix.off[t];
+  const uint32_t* __restrict__ di = ix.doc + bi;
+  const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[t];
+  const uint32_t b = d >> B;
+  uint32_t pos = dir[b];
+  const uint32_t hi = dir[b + 1];
+  for (uint32_t st = S; st > 0; --st) {
+    const uint32_t half = 1u << (st - 1);
+    const uint32_t idx = pos + half - 1;
+    if (idx < hi && di[idx] < d) pos += half;
+  }
+  return (pos < hi && di[pos] == d) ? ix.tf[bi + pos] : 0u;
+}
+
+// Wave-cooperative: postings of term t in docs [d0, d1) = positions [lo, hi)
+// of its list, and the largest bucket maximum over the buckets they live in.
+__device__ inline void tile_range(const DevIndex& ix, uint32_t t, uint32_t d0, uint32_t d1, uint32_t& lo,
+                                  uint32_t& hi, float& ub) {
+  const uint32_t lane = lane_id();
+  const uint32_t meta = ix.tmeta[t];
+  const uint32_t B = meta & 0xFFu;
+  const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[t];
+  const float* __restrict__ bm = ix.bmax + ix.dir_off[t];
+  float mx = 0.0f;
+  if (B <= kTileShift) {
+    // the tile is a whole number of buckets
+    const uint32_t b0 = d0 >> B, b1 = ((d1 - 1) >> B) + 1;
+    lo = dir[b0];
+    hi = dir[b1];
+    for (uint32_t b = b0 + lane; b < b1; b += 64) mx = fmaxf(mx, bm[b]);
+  } else {
+    // one bucket holds the tile: count its postings below d0 and below d1
+    const uint32_t b = d0 >> B;
+    const uint32_t p0 = dir[b], p1 = dir[b + 1];
+    const uint32_t* __restrict__ di = ix.doc + ix.off[t];
+    uint32_t below0 = 0, below1 = 0;
+    for (uint32_t p = p0; p < p1; p += 64) {
+      const uint32_t x = p + lane < p1 ? di[p + lane] : 0xFFFFFFFFu;
+      below0 += (uint32_t)__popcll(__ballot(x < d0));
+      below1 += (uint32_t)__popcll(__ballot(x < d1));
+    }
+    lo = p0 + below0;
+    hi = p0 + below1;
+    mx = bm[b];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  ub = lo == hi ? 0.0f : mx;
+}
+
+// Append u32 `v` (when keep) to an LDS list, one LDS atomic per wave.
+__device__ inline void wave_append_u32(bool keep, uint32_t v, uint32_t* list, uint32_t* count, uint32_t cap) {
+  const uint32_t lane = lane_id();
+  const unsigned long long bal = __ballot(keep);
+  const uint32_t nw = (uint32_t)__popcll(bal);
+  if (!nw) return;
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(count, nw);
+  base = (uint32_t)__shfl((int)base, 0, 64);
+  const uint32_t at = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+  if (keep && at < cap) list[at] = v;
+}
+
+#ifndef FG_DISJ_WAVES
+#define FG_DISJ_WAVES 3
+#endif
+
+__global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, DevPlan pl) {
+  __shared__ DisjShared sh;
+  const uint32_t tid = threadIdx.x, wv = wave_id();
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
+  const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+
+  const uint32_t q = pl.work_q[w];
+  const uint32_t tile0 = pl.work_c[w], ntile = pl.work_n[w];
+  const uint32_t m = pl.q_m[q];
+  const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
+  const uint32_t K = pl.k;
+  unsigned long long* gthr = reinterpret_cast<unsigned long long*>(&pl.thresh[q]);
+  if (tid == 0) {
+    sh.n_buf = 0;
+    sh.thr = atomicMax(gthr, 0ull);
+  }
+  __syncthreads();
+
+  for (uint32_t tt = 0; tt < ntile; ++tt) {
+    const uint32_t d0 = (tile0 + tt) << kTileShift;
+    const uint32_t d1 = min(d0 + kTile, ix.n_docs);
+    // 1. per-clause ranges and bounds (wave w: clauses w, w+4, ...)
+    for (uint32_t i = wv; i < m; i += kThreads / 64) {
+      uint32_t lo, hi;
+      float ub;
+      tile_range(ix, terms[i], d0, d1, lo, hi, ub);
+      if (lane_id() == 0) {
+        sh.t_lo[i] = lo;
+        sh.t_hi[i] = hi;
+        sh.t_ub[i] = ub;
+      }
+    }
+    __syncthreads();
+    // 2. MaxScore split (one thread; m <= 16)
+    if (tid == 0) {
+      const uint64_t thr = sh.thr;
+      uint32_t ord[kMaxTerms];
+      for (uint32_t i = 0; i < m; ++i) {
+        uint32_t j = i;
+        while (j > 0 && sh.t_ub[ord[j - 1]] > sh.t_ub[i]) { ord[j] = ord[j - 1]; --j; }
+        ord[j] = i;
+      }
+      float s = 0.0f;
+      uint32_t P = 0;
+#ifdef FG_DISJ_NOPRUNE
+      for (; P < 0; ++P) {
+#else
+      for (; P < m; ++P) {
+#endif
+        const float s2 = s + sh.t_ub[ord[P]];
+        if (make_key(inflate_bound(s2), d0) >= thr) break;
+        s = s2;
+      }
+      uint32_t ess = 0, any = 0;
+      for (uint32_t j = P; j < m; ++j) {
+        ess |= 1u << ord[j];
+        any |= sh.t_hi[ord[j]] > sh.t_lo[ord[j]] ? 1u : 0u;
+      }
+      sh.ess = ess;
+      sh.ub_ne = s;
+      sh.tile_mode = (P == m || !any) ? 0u : (P == 0 ? 1u : 2u);  // 0 skip, 1 exact, 2 filter + rescore
+#if defined(FG_DISJ_DBG) && FG_DISJ_DBG == 2
+      if (P == m && m > 0) { sh.tile_mode = 1u; sh.ess = (1u << m) - 1u; }
+#endif
+    }
+    __syncthreads();
+    const uint32_t mode = sh.tile_mode;
+    if (mode == 0) continue;  // uniform across the workgroup
+    const uint32_t ess = sh.ess;
+    // 3. scatter-add the essential clauses, clause by clause
+    for (uint32_t i = tid; i < kTile; i += kThreads) sh.acc[i] = 0.0f;
+    __syncthreads();
+    for (uint32_t i = 0; i < m; ++i) {
+      if (!((ess >> i) & 1u)) continue;
+      const uint32_t t = terms[i];
+      const uint64_t bi = ix.off[t];
+      const float wt = ix.w_text[t], wn = ix.w_name[t];
+      const uint32_t lo = sh.t_lo[i], hi = sh.t_hi[i];
+      for (uint32_t p0 = lo; p0 < hi; p0 += 4 * kThreads) {
+        uint32_t dd[4], tf[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t p = p0 + j * kThreads + tid;
+          dd[j] = p < hi ? ix.doc[bi + p] : kInvalid;
+          tf[j] = p < hi ? ix.tf[bi + p] : 0u;
+        }
+        uint32_t fn[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) fn[j] = dd[j] != kInvalid ? load_fn(ix, dd[j]) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+          if (dd[j] != kInvalid) sh.acc[dd[j] - d0] += term_score(tf[j], fn[j], wt, wn, ix.cache);
+      }
+      __syncthreads();
+    }
+    // 4./5. hits (exact) or candidates (filter + rescore) in rounds of kRound docs
+    const float ub_ne = sh.ub_ne;
+    const uint32_t span = d1 - d0;
+    for (uint32_t r0 = 0; r0 < span; r0 += kRound) {
+      const uint64_t thr = sh.thr;
+      if (mode == 1) {
+#pragma unroll
+        for (uint32_t j = 0; j < kRound / kThreads; ++j) {
+          const uint32_t i = r0 + j * kThreads + tid;
+          const float sc = i < span ? sh.acc[i] : 0.0f;
+          uint64_t key = 0;
+          bool keep = sc > 0.0f && doc_alive(ix, d0 + i);
+          if (keep) {
+            key = make_key(sc, d0 + i);
+            keep = key >= thr;
+          }
+          wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
+        }
+      } else {
+        if (tid == 0) sh.n_cand = 0;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kRound / kThreads; ++j) {
+          const uint32_t i = r0 + j * kThreads + tid;
+          const float sc = i < span ? sh.acc[i] : 0.0f;
+#if defined(FG_DISJ_DBG) && FG_DISJ_DBG == 1
+          const bool keep = sc > 0.0f && doc_alive(ix, d0 + i);
+#else
+          const bool keep = sc > 0.0f && make_key(inflate_bound(sc + ub_ne), d0 + i) >= thr && doc_alive(ix, d0 + i);
+#endif
+          wave_append_u32(keep, d0 + i, sh.cand, &sh.n_cand, kRound);
+        }
+        __syncthreads();
+        const uint32_t nc = sh.n_cand;
+        for (uint32_t c0 = 0; c0 < nc; c0 += kThreads) {
+          const uint32_t c = c0 + tid;
+          uint64_t key = 0;
+          bool keep = c < nc;
+          if (keep) {
+            const uint32_t d = sh.cand[c];
+            const uint32_t fnp = load_fn(ix, d);
+            float sc = 0.0f;
+            for (uint32_t i = 0; i < m; ++i) {
+              const uint32_t t = terms[i];
+              const uint32_t tfp = probe_tf(ix, t, d);
+              if (tfp) sc += term_score(tfp, fnp, ix.w_text[t], ix.w_name[t], ix.cache);
+            }
+            key = make_key(sc, d);
+            keep = key >= thr;
+          }
+          wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
+        }
+      }
+      __syncthreads();
+      const uint32_t n = sh.n_buf;
+      __syncthreads();  // every thread has read n before the next round appends
+      if (n > kTrunc) {
+        const uint64_t T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+        if (tid == 0 && T > sh.thr) sh.thr = T;
+        __syncthreads();
+      }
+    }
+    // publish the local k-th key, read the best published one
+    const uint32_t n = sh.n_buf;
+    uint64_t local_T = 0;
+    if (n > K) {
+      local_T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+    }
+    if (tid == 0) {
+      const uint64_t mine = local_T > sh.thr ? local_T : sh.thr;
+      const uint64_t old = atomicMax(gthr, (unsigned long long)mine);
+      sh.thr = old > mine ? old : mine;
+    }
+    __syncthreads();
+  }
+  flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
 }
 
 // ---------------------------------------------------------------- k_final
@@ -536,6 +845,12 @@ __global__ __launch_bounds__(kThreads) void k_merge(uint32_t n_shards, uint32_t 
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   if (pl.total_chunks == 0) return hipSuccess;
   k_conj<<<pl.total_chunks, kThreads, 0, s>>>(ix, pl);
+  return hipGetLastError();
+}
+
+hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
+  if (pl.total_chunks == 0) return hipSuccess;
+  k_disj<<<pl.total_chunks, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 

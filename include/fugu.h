@@ -122,7 +122,7 @@ typedef struct fg_query_batch {
   uint32_t n_queries;
   const uint32_t* q_off;  /* [n_queries+1] */
   const uint32_t* terms;  /* term ids in query order; FG_TERM_MISSING allowed */
-  int mode;               /* FG_MODE_AND or FG_MODE_OR (OR: single-term only in v1) */
+  int mode;               /* FG_MODE_AND (Must clauses) or FG_MODE_OR (Should clauses, k_disj) */
 } fg_query_batch;
 
 /* Plan a batch: host-side query planning (tantivy Weight creation: terms

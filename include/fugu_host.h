@@ -25,7 +25,7 @@
  *   fg_parse_query     the QueryParser subset the device runs
  *
  * Queries outside the device subset (phrases, field:, -, boosts, empty =
- * AllQuery, facet filters, multi-term OR in v1) return FG_EUNSUPPORTED: the
+ * AllQuery, facet filters) return FG_EUNSUPPORTED: the
  * reference host then runs tantivy; this library never answers them on the CPU.
  */
 #ifndef FUGU_HOST_H

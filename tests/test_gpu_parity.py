@@ -44,13 +44,11 @@ def batch(queries):
 def check_fixture_queries(native, ix, queries):
     by_k = {}
     for q in queries:
-        if q["mode"] == "or" and len(q["terms"]) > 1:
-            continue  # multi-term disjunction: CPU path in v1 (FG_EUNSUPPORTED), tested below
-        by_k.setdefault(q["k"], []).append(q)
+        by_k.setdefault((q["k"], q["mode"]), []).append(q)
     n_checked = 0
-    for k, qs in by_k.items():
+    for (k, mode), qs in by_k.items():
         q_off, terms = batch([q["terms"] for q in qs])
-        s, d, n = ix.search_batch(q_off, terms, k)
+        s, d, n = ix.search_batch(q_off, terms, k, mode=native.MODE_OR if mode == "or" else native.MODE_AND)
         for i, q in enumerate(qs):
             got = hits_of(s[i, :n[i]], d[i, :n[i]])
             assert got == q["hits"], (q["terms"], got[:5], q["hits"][:5])
@@ -62,7 +60,7 @@ def test_kat_appendix_c(native, ctx):
     fx = load_golden("kat_appendix_c.json")
     n, nt, off, tok, *_ = golden_corpus(fx)
     ix = native.Index.from_docs(ctx, off, tok, nt)
-    assert check_fixture_queries(native, ix, fx["queries"]) == 3
+    assert check_fixture_queries(native, ix, fx["queries"]) == 4
     s, d, cnt = ix.search_batch(*batch([[0, 1]]), 10)
     assert d[0, :2].tolist() == [1, 0]
     assert s[0, 0] == np.float32(0.80418402) and s[0, 1] == np.float32(0.62927824)
@@ -93,8 +91,6 @@ def test_unsupported_and_invalid(native, ctx):
     n, nt, off, tok, *_ = golden_corpus(fx)
     ix = native.Index.from_docs(ctx, off, tok, nt)
     with pytest.raises(native.Unsupported):
-        ix.search_batch(*batch([[0, 1]]), 10, mode=native.MODE_OR)
-    with pytest.raises(native.Unsupported):
         ix.search_batch(np.array([0, 0], np.uint32), np.array([], np.uint32), 10)  # empty query = AllQuery
     with pytest.raises(native.FuguError) as e:
         ix.search_batch(*batch([[0]]), 0)
@@ -104,6 +100,11 @@ def test_unsupported_and_invalid(native, ctx):
     # a term missing from the dictionary empties a conjunction
     s, d, cnt = ix.search_batch(*batch([[0, native.FG_TERM_MISSING], [0]]), 5)
     assert cnt.tolist() == [0, 2]
+    # ... and drops out of a disjunction (a clause matching nothing)
+    s2, d2, cnt2 = ix.search_batch(*batch([[0, native.FG_TERM_MISSING], [native.FG_TERM_MISSING]]), 5,
+                                   mode=native.MODE_OR)
+    assert cnt2.tolist() == [2, 0] and d2[0, :2].tolist() == d[1, :2].tolist()
+    assert s2[0, :2].tolist() == s[1, :2].tolist()
 
 
 # ---------------------------------------------------------------- synthetic Zipf corpora vs the oracle
@@ -124,12 +125,14 @@ def gpu_1m(native, ctx, corpus_1m):
     return native.Index.from_docs(ctx, corpus_1m.off, corpus_1m.tok, 1 << 20, threads=16)
 
 
-@pytest.mark.parametrize("m_min,m_max,k", [(3, 3, 100), (1, 5, 100), (2, 2, 1), (2, 4, 1000)])
-def test_zipf_1m_vs_oracle(native, gpu_1m, oracle_1m, m_min, m_max, k):
+@pytest.mark.parametrize("m_min,m_max,k,mode", [(3, 3, 100, 0), (1, 5, 100, 0), (2, 2, 1, 0), (2, 4, 1000, 0),
+                                                (2, 3, 100, 1), (1, 5, 1000, 1), (2, 5, 10, 1)])
+def test_zipf_1m_vs_oracle(native, gpu_1m, oracle_1m, m_min, m_max, k, mode):
     from fugu_amd import synth
-    q_off, terms = synth.queries(1024 if k <= 100 else 256, m_min, m_max)
-    s, d, n = gpu_1m.search_batch(q_off, terms, k)
-    rs, rd, rn, _, _ = oracle_1m.search_batch(q_off, terms, k, threads=16)
+    nq = (1024 if k <= 100 else 256) if mode == 0 else 128
+    q_off, terms = synth.queries(nq, m_min, m_max)
+    s, d, n = gpu_1m.search_batch(q_off, terms, k, mode=mode)
+    rs, rd, rn, _, _ = oracle_1m.search_batch(q_off, terms, k, mode=mode, threads=16)
     assert np.array_equal(n, rn)
     for i in range(len(q_off) - 1):
         assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], (i, terms[q_off[i]:q_off[i + 1]].tolist()))

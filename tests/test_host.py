@@ -274,6 +274,13 @@ def test_db_end_to_end_vs_oracle(db):
     assert checked > 100
     r = json.loads(d.search_json("docs", WORDS[1], 0, 3))
     assert all("text" not in h for h in r["results"])
+    # bare terms = Should clauses (k_disj), scored in clause order
+    for q in ["alpha beta", "Gamma straße 1999 x86", "omega omega psi"]:
+        ws = q.split()
+        terms = [dic.get(py_analyze(w)[0], native.FG_TERM_MISSING) for w in ws]
+        s, dd = ix.search(np.array(terms, np.uint32), 40, mode=1)
+        got = d.search("docs", q, 1, 20)
+        assert hits_of([g[0] for g in got], [g[1] for g in got]) == hits_of(s, dd)[20:], q
     # a second batch of upserts is invisible until commit, then visible
     before = d.search("docs", "brandnewword")
     d.add_file("docs", "notes.txt", "brandnewword appears here")
@@ -282,5 +289,3 @@ def test_db_end_to_end_vs_oracle(db):
     assert len(got) == 1 and got[0][1] == len(recs)
     r = json.loads(d.search_json("docs", "brandnewword", shape=db.SHAPE_POST_SEARCH))
     assert r["results"][0]["id"] == "notes.txt" and r["results"][0]["metadata"] == {"name": "notes.txt"}
-    with pytest.raises(native.Unsupported):
-        d.search("docs", "alpha beta")  # multi-term OR: host CPU path in v1
