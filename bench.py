@@ -242,7 +242,9 @@ def main():
                             mism += 1
                     done = hi
                 ent["cpu_baseline"] = {"value": round(done / wall, 2), "unit": "queries/s", "cores": threads,
-                                       "kind": "port", "sample": f"first {done} queries, exhaustive oracle"}
+                                       "kind": "port",
+                                       "sample": f"first {done} queries of the batch, oracle/fugu_oracle.c "
+                                                 f"({'leapfrog intersection' if mode == native.MODE_AND else 'exhaustive union, SumCombiner'})"}
                 ent["parity"] = {"queries_checked": done, "mismatches": mism}
             extra[name] = ent
             log(f"[bench] {name}: {ent['value']} q/s, {ent['kernel']} {ent['kernel_ms']} ms")

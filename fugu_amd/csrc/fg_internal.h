@@ -28,7 +28,9 @@ constexpr uint32_t kGroupsPerQuery = 64;  // a query's chunks are split into ~th
 constexpr uint32_t kMaxGroup = 16;        // ... of at most this many chunks each
 constexpr uint32_t kHistBins = 2048;      // 11-bit radix digits
 constexpr uint32_t kDisjTileShift = 12;   // k_disj: 4096-doc tiles
-constexpr uint32_t kDisjMaxGroup = 64;    // ... at most this many tiles per work item
+constexpr uint32_t kDisjMaxGroup = 32;    // ... at most this many tiles per work item
+constexpr uint32_t kNumTopK = 4;          // per-term K-th best scores kept for these K
+constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 100, 1000};
 
 constexpr uint32_t kModeAnd = 0;
 constexpr uint32_t kModeOr = 1;
@@ -59,6 +61,8 @@ struct DevIndex {
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
   const float* cache;        // [512] bm25 tf cache: [0,256) text, [256,512) name
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
+  const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
+  const uint32_t* toff;      // [V] first tmax entry of each term, or 0xFFFFFFFF (bucket >= tile: use bmax)
   uint32_t n_docs;
   uint32_t n_terms;
   uint32_t has_name;
@@ -80,6 +84,7 @@ struct DevPlan {
   const uint32_t* work_c;       // [total_chunks] first chunk of the item's group (k_disj: first tile)
   const uint32_t* work_n;       // [total_chunks] chunks in the item's group (k_disj: tiles)
   const uint64_t* cand_off;     // [nq+1] candidate-list capacity offsets (work items of q * k)
+  const uint64_t* q_thr0;       // [nq] starting threshold key (k_disj: per-term top-K bound), 0 = none
   // workspace, zeroed per run
   uint64_t* thresh;             // [nq] monotone lower bound on the k-th best key
   uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list
@@ -87,7 +92,7 @@ struct DevPlan {
   uint64_t* diag;               // diagnostic builds only (-DFG_DIAG): per-workgroup stamps
 };
 
-constexpr uint32_t kDiagPerWg = 8;  // u64 stamps per workgroup in diagnostic builds
+constexpr uint32_t kDiagPerWg = 16;  // u64 stamps per workgroup in diagnostic builds
 
 // Key of a hit: larger is better.  (score bits << 32) | ~doc orders by
 // score descending, then doc ascending (tantivy ComparableDoc order); scores

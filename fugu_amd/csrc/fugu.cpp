@@ -159,6 +159,7 @@ struct fg_index {
   std::vector<uint64_t> off;
   std::vector<uint32_t> df_text, df_name;
   std::vector<uint32_t> first_doc, last_doc;
+  std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
   std::vector<float> w_text, w_name;
   std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model
   fg::DevIndex d{};
@@ -256,8 +257,13 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
   // bucket score maxima (parallel to dir): the per-bucket upper bound the
   // disjunctive kernel prunes with (block-max WAND / MaxScore bounds)
   std::vector<float> bmax(nd, 0.0f);
+  // per-term K-th best score over alive docs for K in kTopKs: a doc among a
+  // term's top K scores at least that much in any disjunction containing the
+  // term, so the query's K-th best is >= it (k_disj's starting threshold)
+  ix->ktop.assign((size_t)V * fg::kNumTopK, 0.0f);
   const bool has_name = hp.has_name;
   parallel_ranges(V, hw_threads(0), [&](int, uint32_t tb, uint32_t te) {
+    std::vector<float> sc;
     for (uint32_t t = tb; t < te; ++t) {
       const uint64_t b0 = hp.off[t], n = hp.off[t + 1] - b0;
       const uint32_t B = tmeta[t];
@@ -272,7 +278,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
         float mx = 0.0f;
         while (p < n && hp.doc[b0 + p] < lo) {
           const uint32_t d = hp.doc[b0 + p], tfp = hp.tf[b0 + p];
-          mx = std::max(mx, term_score_host(tfp, hp.fn_text[d], has_name ? hp.fn_name[d] : 0, wt, wn, ix->cache));
+          const float v = term_score_host(tfp, hp.fn_text[d], has_name ? hp.fn_name[d] : 0, wt, wn, ix->cache);
+          mx = std::max(mx, v);
+          if (hp.alive.empty() || ((hp.alive[d >> 5] >> (d & 31)) & 1u)) sc.push_back(v);
           ++p;
         }
         dt[b] = (uint32_t)p;
@@ -284,6 +292,38 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
       uint32_t S = 0;
       while ((1ull << S) <= maxocc) ++S;  // 2^S > largest bucket
       tmeta[t] = B | (S << 8);
+      for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
+        const uint32_t K = fg::kTopKs[j];
+        if (sc.size() < K) break;
+        std::nth_element(sc.begin(), sc.begin() + (K - 1), sc.end(), std::greater<float>());
+        ix->ktop[(size_t)t * fg::kNumTopK + j] = sc[K - 1];
+      }
+      sc.clear();
+    }
+  });
+  // per-term tile maxima (4096-doc tiles of k_disj) for terms whose buckets are
+  // no wider than a tile: one load gives a clause's bound over a tile
+  std::vector<uint32_t> toff(V, 0xFFFFFFFFu);
+  const uint64_t n_tiles = ((uint64_t)N + (1u << fg::kDisjTileShift) - 1) >> fg::kDisjTileShift;
+  uint64_t ntm = 0;
+  for (uint32_t t = 0; t < V; ++t)
+    if ((tmeta[t] & 0xFFu) <= fg::kDisjTileShift && hp.off[t + 1] > hp.off[t]) {
+      if (ntm + n_tiles > 0xFFFFFFFFull) break;
+      toff[t] = (uint32_t)ntm;
+      ntm += n_tiles;
+    }
+  std::vector<float> tmax(ntm, 0.0f);
+  parallel_ranges(V, hw_threads(0), [&](int, uint32_t tb, uint32_t te) {
+    for (uint32_t t = tb; t < te; ++t) {
+      if (toff[t] == 0xFFFFFFFFu) continue;
+      const uint32_t B = tmeta[t] & 0xFFu;
+      const uint64_t nbk = ((N - 1) >> B) + 1;
+      const float* bm = bmax.data() + dir_off[t];
+      float* tm = tmax.data() + toff[t];
+      for (uint64_t b = 0; b < nbk; ++b) {
+        const uint64_t tile = (b << B) >> fg::kDisjTileShift;
+        tm[tile] = std::max(tm[tile], bm[b]);
+      }
     }
   });
   // dense doc-indexed tf tables for the densest text-only terms
@@ -312,9 +352,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
   uint64_t bytes = 0;
   int rc;
   uint16_t* d_dense = nullptr;
-  uint32_t *d_doc, *d_tf, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr;
+  uint32_t *d_doc, *d_tf, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr, *d_toff;
   uint64_t* d_off;
-  float *d_wt, *d_wn, *d_cache, *d_bmax;
+  float *d_wt, *d_wn, *d_cache, *d_bmax, *d_tmax;
   uint8_t *d_fnt, *d_fnn;
   if ((rc = dev_upload(ix->mem, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.tf.data(), hp.tf.size(), &d_tf, &bytes))) return rc;
@@ -322,6 +362,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
   if ((rc = dev_upload(ix->mem, dir.data(), dir.size(), &d_dir, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, bmax.data(), bmax.size(), &d_bmax, &bytes))) return rc;
   std::vector<float>().swap(bmax);
+  if ((rc = dev_upload(ix->mem, tmax.data(), tmax.size(), &d_tmax, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, toff.data(), toff.size(), &d_toff, &bytes))) return rc;
+  std::vector<float>().swap(tmax);
   if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, dense.data(), dense.size(), &d_dense, &bytes))) return rc;
@@ -333,7 +376,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
   if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
   if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
   ix->d = fg::DevIndex{d_doc, d_tf, d_off, d_dir, d_dir_off, d_tmeta, d_dense, d_wt, d_wn, d_fnt, d_fnn, d_alive,
-                       d_cache, d_bmax, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
+                       d_cache, d_bmax, d_tmax, d_toff, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
   // per-term doc span (disjunctive plans skip the tiles outside it)
   ix->first_doc.assign(V, 0);
   ix->last_doc.assign(V, 0);
@@ -611,6 +654,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   const uint32_t nq = q->n_queries;
   const bool disj = q->mode == FG_MODE_OR;
   std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), nchunk(nq);
+  std::vector<uint64_t> thr0(nq, 0);
   uint64_t chunks = 0;
   // work items: each query's chunks (AND) or doc tiles (OR) in ~kGroupsPerQuery
   // groups, ordered as a doc sweep across the batch (a group centred at doc
@@ -637,6 +681,15 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
       }
       q_m[i] = mm;
       if (!mm) continue;
+      // starting threshold: the best per-clause K'-th score for the smallest stored K' >= k
+      for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
+        if (fg::kTopKs[j] < k) continue;
+        float v = 0.0f;
+        for (uint32_t c = 0; c < mm; ++c)
+          v = std::max(v, ix->ktop[(size_t)q_terms[(size_t)i * fg::kMaxTerms + c] * fg::kNumTopK + j]);
+        if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
+        break;
+      }
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
       const uint32_t G = std::min<uint32_t>(fg::kDisjMaxGroup,
@@ -700,8 +753,8 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t s_qm = al(4ull * nq), s_qt = al(4ull * nq * fg::kMaxTerms), s_lead = al(4ull * nq),
                s_wq = al(4ull * chunks), s_wc = al(4ull * chunks), s_wn = al(4ull * chunks),
-               s_co = al(8ull * (nq + 1));
-  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co;
+               s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq);
+  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0;
   const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq);
   const size_t s_ck = al(8ull * cand_off[nq]);
   const size_t s_os = al(4ull * nq * k), s_od = al(4ull * nq * k), s_on = al(4ull * nq);
@@ -732,6 +785,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.work_c = (const uint32_t*)put(work_c.data(), 4ull * chunks, s_wc);
   p->d.work_n = (const uint32_t*)put(work_n.data(), 4ull * chunks, s_wn);
   p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
+  p->d.q_thr0 = (const uint64_t*)put(thr0.data(), 8ull * nq, s_t0);
   HIPCHK(hipMemcpy(base, staging.data(), s_in, hipMemcpyHostToDevice));
   char* cur = base + s_in;
   p->zero_region = cur;

@@ -430,43 +430,64 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
 // ---------------------------------------------------------------- k_disj
 // Pure disjunction `t1 t2 ...` (Should clauses; query/union + SumCombiner,
 // boolean_weight.rs): score = 0.0 + s_1 + s_2 + ... over the clauses a doc
-// matches, in clause order.  A work item is a run of consecutive 4096-doc
-// tiles of one query.  Per tile:
-//   1. each wave resolves its clauses' posting range inside the tile through
-//      the bucket directory and the clause's upper bound = max of the bucket
-//      maxima (DevIndex::bmax) the tile overlaps;
-//   2. MaxScore split against the query's threshold: sorted by bound, the
-//      longest prefix of clauses whose summed bound cannot reach the threshold
-//      is "non-essential" -- a doc matching only those cannot enter the top-k.
-//      All clauses non-essential: the tile is skipped outright;
-//   3. the essential clauses' postings are scatter-added into an LDS score
-//      array indexed by doc - tile start, clause by clause (one barrier per
-//      clause, so each doc's sum is formed in clause order: exact when every
-//      clause is essential);
-//   4. docs whose accumulated score (+ the non-essential bound, when some
-//      clauses were skipped) clears the threshold become hits -- or, in the
-//      pruned case, candidates that are rescored exactly by probing every
-//      clause through the directory, in clause order;
-//   5. hits go through the same local top-k buffer / threshold publication as
-//      k_conj, and k_final selects the query's top-k.
-// Bounds are compared after inflating by 2^-17 relative, which covers any
-// f32 summation-order difference for <= 16 clauses, so the
-// pruning never drops a true top-k doc: results equal the exhaustive union.
+// matches, in clause order.  A work item is a run of <= 32 consecutive
+// 4096-doc tiles of one query.
+//   R. all (tile, clause) posting ranges and bounds at once, one thread per
+//      pair: [lo, hi) from the bucket directory, the bound from the per-term
+//      tile maxima (DevIndex::tmax) or the bucket maximum (bmax);
+//   S. MaxScore split per tile (one thread per tile) against the query's
+//      threshold: sorted by bound, the longest prefix of clauses whose summed
+//      bound cannot reach it is non-essential (a doc matching only those cannot
+//      enter the top-k); all clauses non-essential: the tile is skipped;
+//   E. tiles where every clause is essential (low threshold) are scored
+//      exhaustively: the clauses' postings are scatter-added into an LDS score
+//      array clause by clause (so each doc's sum is formed in clause order);
+//   P. the other tiles are posting-driven: the postings of their essential
+//      clauses are streamed as one flat list in passes of 1024.  A posting of
+//      clause c at doc d is a candidate when s_c(d) plus the other clauses'
+//      bounds (tile bound, then the bucket maximum at d) can reach the
+//      threshold; candidates are rescored exactly by probing every clause
+//      through the directory ((candidate, clause) pairs in parallel) and summed
+//      in clause order.  A doc found through several essential clauses is kept
+//      only from the first of them that it matches, so keys stay unique;
+//   then hits go through the same local top-k buffer / threshold publication
+//   as k_conj, and k_final selects the query's top-k.
+// Bounds are compared after inflating by 2^-17 relative, which covers any f32
+// summation-order difference for <= 16 clauses, so the pruning never drops a
+// true top-k doc: results equal the exhaustive union.
 constexpr uint32_t kTileShift = kDisjTileShift;
 constexpr uint32_t kTile = 1u << kTileShift;   // docs per tile (LDS score array: 16 KB)
-constexpr uint32_t kRound = 1024;              // scan round: entries per workgroup pass
-constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one round of hits
+constexpr uint32_t kRound = 1024;              // postings / docs per pass
+constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
+constexpr uint32_t kPairs = 1024;              // (candidate, clause) rescoring pairs per pass
+constexpr uint32_t kMaxTiles = kDisjMaxGroup;  // tiles per work item
+constexpr uint32_t kMaxSeg = kMaxTiles * kMaxTerms;
 
 struct DisjShared {
-  float acc[kTile];
   alignas(16) uint64_t buf[kBufD];
-  uint32_t cand[kRound];
+  union {
+    float acc[kTile];                // E: exhaustive tile scores
+    struct {
+      uint64_t cand[kRound];         // P: (doc << 32) | (maybe-mask << 16) | (tile << 8) | clause
+      float cand_s[kRound];          // P: the source clause's score of each candidate
+      float cs[kPairs];              // P: per-(candidate, clause) term scores
+      uint32_t seg_start[kMaxSeg];   // P: prefix of the essential segments' lengths
+    } p;
+  } u;
   uint32_t hist[kHistBins];
   uint32_t scratch[8];
-  uint32_t t_lo[kMaxTerms], t_hi[kMaxTerms];
-  float t_ub[kMaxTerms];
-  uint32_t n_buf, n_cand, ess, tile_mode;
-  float ub_ne;
+  // R: per (tile, clause) ranges and bounds, index t * m + i
+  uint32_t r_lo[kMaxSeg], r_hi[kMaxSeg];
+  float r_ub[kMaxSeg];
+  uint32_t t_ess[kMaxTiles];         // essential-clause mask per tile
+  uint32_t t_mode[kMaxTiles];        // 0 skip, 1 exhaustive, 2 posting-driven
+  uint16_t seg_info[kMaxSeg];        // P: (tile << 4) | clause of each segment
+  // per-clause constants of the work item's query
+  uint32_t c_meta[kMaxTerms], c_dir[kMaxTerms], c_toff[kMaxTerms];
+  uint64_t c_base[kMaxTerms];
+  float c_wt[kMaxTerms], c_wn[kMaxTerms];
+  uint32_t max_s, n_seg, n_post;
+  uint32_t n_buf, n_cand;
   uint64_t thr;
 };
 
@@ -476,73 +497,22 @@ __device__ inline bool doc_alive(const DevIndex& ix, uint32_t d) {
   return !ix.alive || ((ix.alive[d >> 5] >> (d & 31)) & 1u);
 }
 
-// packed tf of term t in doc d (0: absent) -- one directory probe (k_conj's
-// search, one item)
-__device__ inline uint32_t probe_tf(const DevIndex& ix, uint32_t t, uint32_t d) {
-  const uint32_t meta = ix.tmeta[t];
-  const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu, dslot = meta >> 16;
-  if (dslot) return ix.dense[(size_t)(dslot - 1) * ix.n_docs + d];
-  const uint64_t bi = ix.off[t];
-  const uint32_t* __restrict__ di = ix.doc + bi;
-  const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[t];
-  const uint32_t b = d >> B;
-  uint32_t pos = dir[b];
-  const uint32_t hi = dir[b + 1];
-  for (uint32_t st = S; st > 0; --st) {
-    const uint32_t half = 1u << (st - 1);
-    const uint32_t idx = pos + half - 1;
-    if (idx < hi && di[idx] < d) pos += half;
-  }
-  return (pos < hi && di[pos] == d) ? ix.tf[bi + pos] : 0u;
-}
-
-// Wave-cooperative: postings of term t in docs [d0, d1) = positions [lo, hi)
-// of its list, and the largest bucket maximum over the buckets they live in.
-__device__ inline void tile_range(const DevIndex& ix, uint32_t t, uint32_t d0, uint32_t d1, uint32_t& lo,
-                                  uint32_t& hi, float& ub) {
-  const uint32_t lane = lane_id();
-  const uint32_t meta = ix.tmeta[t];
-  const uint32_t B = meta & 0xFFu;
-  const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[t];
-  const float* __restrict__ bm = ix.bmax + ix.dir_off[t];
-  float mx = 0.0f;
-  if (B <= kTileShift) {
-    // the tile is a whole number of buckets
-    const uint32_t b0 = d0 >> B, b1 = ((d1 - 1) >> B) + 1;
-    lo = dir[b0];
-    hi = dir[b1];
-    for (uint32_t b = b0 + lane; b < b1; b += 64) mx = fmaxf(mx, bm[b]);
-  } else {
-    // one bucket holds the tile: count its postings below d0 and below d1
-    const uint32_t b = d0 >> B;
-    const uint32_t p0 = dir[b], p1 = dir[b + 1];
-    const uint32_t* __restrict__ di = ix.doc + ix.off[t];
-    uint32_t below0 = 0, below1 = 0;
-    for (uint32_t p = p0; p < p1; p += 64) {
-      const uint32_t x = p + lane < p1 ? di[p + lane] : 0xFFFFFFFFu;
-      below0 += (uint32_t)__popcll(__ballot(x < d0));
-      below1 += (uint32_t)__popcll(__ballot(x < d1));
+// Keep the threshold fresh: truncate the local buffer to K when it passes
+// `limit`, then publish the local k-th key and read back the best published.
+__device__ inline void disj_truncate(DisjShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr, bool publish) {
+  const uint32_t n = sh.n_buf;
+  __syncthreads();  // every thread has read n before anyone appends again
+  uint64_t T = 0;
+  if (n > limit) T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+  if (threadIdx.x == 0) {
+    uint64_t mine = T > sh.thr ? T : sh.thr;
+    if (publish) {
+      const uint64_t old = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)mine);
+      mine = old > mine ? old : mine;
     }
-    lo = p0 + below0;
-    hi = p0 + below1;
-    mx = bm[b];
+    sh.thr = mine;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  ub = lo == hi ? 0.0f : mx;
-}
-
-// Append u32 `v` (when keep) to an LDS list, one LDS atomic per wave.
-__device__ inline void wave_append_u32(bool keep, uint32_t v, uint32_t* list, uint32_t* count, uint32_t cap) {
-  const uint32_t lane = lane_id();
-  const unsigned long long bal = __ballot(keep);
-  const uint32_t nw = (uint32_t)__popcll(bal);
-  if (!nw) return;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(count, nw);
-  base = (uint32_t)__shfl((int)base, 0, 64);
-  const uint32_t at = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-  if (keep && at < cap) list[at] = v;
+  __syncthreads();
 }
 
 #ifndef FG_DISJ_WAVES
@@ -551,7 +521,7 @@ __device__ inline void wave_append_u32(bool keep, uint32_t v, uint32_t* list, ui
 
 __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, DevPlan pl) {
   __shared__ DisjShared sh;
-  const uint32_t tid = threadIdx.x, wv = wave_id();
+  const uint32_t tid = threadIdx.x;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
   const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
@@ -561,166 +531,360 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
   const uint32_t m = pl.q_m[q];
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
-  unsigned long long* gthr = reinterpret_cast<unsigned long long*>(&pl.thresh[q]);
+  uint64_t* gthr = &pl.thresh[q];
+#ifdef FG_DIAG
+  const uint64_t dg_t0 = FG_NOW();
+  uint64_t dg_mode[3] = {0, 0, 0}, dg_post = 0, dg_cand = 0, dg_trunc = 0, dg_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph = dg_t0;
+#define FG_PHASE(slot) do { const uint64_t n_ = FG_NOW(); dg_ph[slot] += n_ - ph; ph = n_; } while (0)
+#else
+#define FG_PHASE(slot) do { } while (0)
+#endif
   if (tid == 0) {
     sh.n_buf = 0;
-    sh.thr = atomicMax(gthr, 0ull);
+    const uint64_t t0 = pl.q_thr0[q];
+    const uint64_t g = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)t0);
+    sh.thr = g > t0 ? g : t0;
+  }
+  if (tid < m) {
+    const uint32_t t = terms[tid];
+    sh.c_meta[tid] = ix.tmeta[t];
+    sh.c_dir[tid] = ix.dir_off[t];
+    sh.c_toff[tid] = ix.toff[t];
+    sh.c_base[tid] = ix.off[t];
+    sh.c_wt[tid] = ix.w_text[t];
+    sh.c_wn[tid] = ix.w_name[t];
   }
   __syncthreads();
+  if (tid == 0) {
+    uint32_t ms = 0;
+    for (uint32_t i = 0; i < m; ++i) ms = max(ms, (sh.c_meta[i] >> 8) & 0xFFu);
+    sh.max_s = ms;
+  }
 
-  for (uint32_t tt = 0; tt < ntile; ++tt) {
-    const uint32_t d0 = (tile0 + tt) << kTileShift;
-    const uint32_t d1 = min(d0 + kTile, ix.n_docs);
-    // 1. per-clause ranges and bounds (wave w: clauses w, w+4, ...)
-    for (uint32_t i = wv; i < m; i += kThreads / 64) {
-      uint32_t lo, hi;
-      float ub;
-      tile_range(ix, terms[i], d0, d1, lo, hi, ub);
-      if (lane_id() == 0) {
-        sh.t_lo[i] = lo;
-        sh.t_hi[i] = hi;
-        sh.t_ub[i] = ub;
+  // ---- R: ranges and bounds of every (tile, clause) pair, one thread per pair
+  const uint32_t npair = ntile * m;
+  for (uint32_t p = tid; p < npair; p += kThreads) {
+    const uint32_t t = p / m, i = p - t * m;
+    const uint32_t tile = tile0 + t;
+    const uint32_t d0 = tile << kTileShift, d1 = min(d0 + kTile, ix.n_docs);
+    const uint32_t meta = sh.c_meta[i], B = meta & 0xFFu;
+    const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[i];
+    uint32_t lo, hi;
+    float ub;
+    if (B <= kTileShift) {
+      lo = dir[d0 >> B];
+      hi = dir[((d1 - 1) >> B) + 1];
+      ub = sh.c_toff[i] != kInvalid ? ix.tmax[sh.c_toff[i] + tile] : 0.0f;
+    } else {
+      // one bucket holds the tile: branchless searches for d0 and d1 inside it
+      const uint32_t b = d0 >> B;
+      const uint32_t p0 = dir[b], p1 = dir[b + 1];
+      const uint32_t* __restrict__ di = ix.doc + sh.c_base[i];
+      const uint32_t S = (meta >> 8) & 0xFFu;
+      uint32_t a = p0, c = p0;
+      for (uint32_t st = S; st > 0; --st) {
+        const uint32_t half = 1u << (st - 1);
+        const uint32_t ia = a + half - 1, ic = c + half - 1;
+        if (ia < p1 && di[ia] < d0) a += half;
+        if (ic < p1 && di[ic] < d1) c += half;
       }
+      if (a < p1 && di[a] < d0) ++a;
+      if (c < p1 && di[c] < d1) ++c;
+      lo = a;
+      hi = c;
+      ub = ix.bmax[sh.c_dir[i] + b];
     }
-    __syncthreads();
-    // 2. MaxScore split (one thread; m <= 16)
-    if (tid == 0) {
-      const uint64_t thr = sh.thr;
-      uint32_t ord[kMaxTerms];
-      for (uint32_t i = 0; i < m; ++i) {
-        uint32_t j = i;
-        while (j > 0 && sh.t_ub[ord[j - 1]] > sh.t_ub[i]) { ord[j] = ord[j - 1]; --j; }
-        ord[j] = i;
-      }
-      float s = 0.0f;
-      uint32_t P = 0;
-#ifdef FG_DISJ_NOPRUNE
-      for (; P < 0; ++P) {
-#else
-      for (; P < m; ++P) {
-#endif
-        const float s2 = s + sh.t_ub[ord[P]];
-        if (make_key(inflate_bound(s2), d0) >= thr) break;
-        s = s2;
-      }
-      uint32_t ess = 0, any = 0;
-      for (uint32_t j = P; j < m; ++j) {
-        ess |= 1u << ord[j];
-        any |= sh.t_hi[ord[j]] > sh.t_lo[ord[j]] ? 1u : 0u;
-      }
-      sh.ess = ess;
-      sh.ub_ne = s;
-      sh.tile_mode = (P == m || !any) ? 0u : (P == 0 ? 1u : 2u);  // 0 skip, 1 exact, 2 filter + rescore
-#if defined(FG_DISJ_DBG) && FG_DISJ_DBG == 2
-      if (P == m && m > 0) { sh.tile_mode = 1u; sh.ess = (1u << m) - 1u; }
-#endif
+    sh.r_lo[p] = lo;
+    sh.r_hi[p] = hi;
+    sh.r_ub[p] = lo < hi ? ub : 0.0f;
+  }
+  __syncthreads();
+  FG_PHASE(0);
+
+  // ---- S: MaxScore split per tile (one thread per tile)
+  if (tid < ntile) {
+    const uint32_t t = tid;
+    const uint32_t d0 = (tile0 + t) << kTileShift;
+    const uint64_t thr = sh.thr;
+    const float* ub = sh.r_ub + t * m;
+    uint32_t ord[kMaxTerms];
+    for (uint32_t i = 0; i < m; ++i) {
+      uint32_t j = i;
+      const float v = ub[i];
+      while (j > 0 && ub[ord[j - 1]] > v) { ord[j] = ord[j - 1]; --j; }
+      ord[j] = i;
     }
-    __syncthreads();
-    const uint32_t mode = sh.tile_mode;
-    if (mode == 0) continue;  // uniform across the workgroup
-    const uint32_t ess = sh.ess;
-    // 3. scatter-add the essential clauses, clause by clause
-    for (uint32_t i = tid; i < kTile; i += kThreads) sh.acc[i] = 0.0f;
+    float s = 0.0f;
+    uint32_t P = 0;
+    for (; P < m; ++P) {
+      const float s2 = s + ub[ord[P]];
+      if (make_key(inflate_bound(s2), d0) >= thr) break;
+      s = s2;
+    }
+    uint32_t ess = 0, any = 0;
+    for (uint32_t j = P; j < m; ++j) {
+      ess |= 1u << ord[j];
+      any |= sh.r_hi[t * m + ord[j]] > sh.r_lo[t * m + ord[j]] ? 1u : 0u;
+    }
+    sh.t_ess[t] = ess;
+    sh.t_mode[t] = (P == m || !any) ? 0u : (P == 0 ? 1u : 2u);
+  }
+  __syncthreads();
+  FG_PHASE(1);
+#ifdef FG_DIAG
+  if (tid == 0)
+    for (uint32_t t = 0; t < ntile; ++t) {
+      dg_mode[sh.t_mode[t]]++;
+      for (uint32_t i = 0; i < m; ++i)
+        if (sh.t_mode[t] && ((sh.t_ess[t] >> i) & 1u)) dg_post += sh.r_hi[t * m + i] - sh.r_lo[t * m + i];
+    }
+#endif
+
+  // ---- E: exhaustive tiles (every clause essential), clause-ordered LDS accumulation
+  for (uint32_t t = 0; t < ntile; ++t) {
+    if (sh.t_mode[t] != 1u) continue;  // uniform
+    const uint32_t d0 = (tile0 + t) << kTileShift;
+    const uint32_t span = min(d0 + kTile, ix.n_docs) - d0;
+    for (uint32_t x = tid; x < kTile; x += kThreads) sh.u.acc[x] = 0.0f;
     __syncthreads();
     for (uint32_t i = 0; i < m; ++i) {
-      if (!((ess >> i) & 1u)) continue;
-      const uint32_t t = terms[i];
-      const uint64_t bi = ix.off[t];
-      const float wt = ix.w_text[t], wn = ix.w_name[t];
-      const uint32_t lo = sh.t_lo[i], hi = sh.t_hi[i];
+      const uint64_t bi = sh.c_base[i];
+      const float wt = sh.c_wt[i], wn = sh.c_wn[i];
+      const uint32_t lo = sh.r_lo[t * m + i], hi = sh.r_hi[t * m + i];
       for (uint32_t p0 = lo; p0 < hi; p0 += 4 * kThreads) {
-        uint32_t dd[4], tf[4];
+        uint32_t dd[4], tf[4], fn[4];
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
           const uint32_t p = p0 + j * kThreads + tid;
           dd[j] = p < hi ? ix.doc[bi + p] : kInvalid;
           tf[j] = p < hi ? ix.tf[bi + p] : 0u;
         }
-        uint32_t fn[4];
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) fn[j] = dd[j] != kInvalid ? load_fn(ix, dd[j]) : 0u;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
-          if (dd[j] != kInvalid) sh.acc[dd[j] - d0] += term_score(tf[j], fn[j], wt, wn, ix.cache);
+          if (dd[j] != kInvalid) sh.u.acc[dd[j] - d0] += term_score(tf[j], fn[j], wt, wn, ix.cache);
       }
       __syncthreads();
     }
-    // 4./5. hits (exact) or candidates (filter + rescore) in rounds of kRound docs
-    const float ub_ne = sh.ub_ne;
-    const uint32_t span = d1 - d0;
     for (uint32_t r0 = 0; r0 < span; r0 += kRound) {
       const uint64_t thr = sh.thr;
-      if (mode == 1) {
 #pragma unroll
-        for (uint32_t j = 0; j < kRound / kThreads; ++j) {
-          const uint32_t i = r0 + j * kThreads + tid;
-          const float sc = i < span ? sh.acc[i] : 0.0f;
-          uint64_t key = 0;
-          bool keep = sc > 0.0f && doc_alive(ix, d0 + i);
-          if (keep) {
-            key = make_key(sc, d0 + i);
-            keep = key >= thr;
-          }
-          wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
+      for (uint32_t j = 0; j < kRound / kThreads; ++j) {
+        const uint32_t x = r0 + j * kThreads + tid;
+        const float sc = x < span ? sh.u.acc[x] : 0.0f;
+        uint64_t key = 0;
+        bool keep = sc > 0.0f && doc_alive(ix, d0 + x);
+        if (keep) {
+          key = make_key(sc, d0 + x);
+          keep = key >= thr;
         }
-      } else {
-        if (tid == 0) sh.n_cand = 0;
-        __syncthreads();
-#pragma unroll
-        for (uint32_t j = 0; j < kRound / kThreads; ++j) {
-          const uint32_t i = r0 + j * kThreads + tid;
-          const float sc = i < span ? sh.acc[i] : 0.0f;
-#if defined(FG_DISJ_DBG) && FG_DISJ_DBG == 1
-          const bool keep = sc > 0.0f && doc_alive(ix, d0 + i);
-#else
-          const bool keep = sc > 0.0f && make_key(inflate_bound(sc + ub_ne), d0 + i) >= thr && doc_alive(ix, d0 + i);
-#endif
-          wave_append_u32(keep, d0 + i, sh.cand, &sh.n_cand, kRound);
-        }
-        __syncthreads();
-        const uint32_t nc = sh.n_cand;
-        for (uint32_t c0 = 0; c0 < nc; c0 += kThreads) {
-          const uint32_t c = c0 + tid;
-          uint64_t key = 0;
-          bool keep = c < nc;
-          if (keep) {
-            const uint32_t d = sh.cand[c];
-            const uint32_t fnp = load_fn(ix, d);
-            float sc = 0.0f;
-            for (uint32_t i = 0; i < m; ++i) {
-              const uint32_t t = terms[i];
-              const uint32_t tfp = probe_tf(ix, t, d);
-              if (tfp) sc += term_score(tfp, fnp, ix.w_text[t], ix.w_name[t], ix.cache);
-            }
-            key = make_key(sc, d);
-            keep = key >= thr;
-          }
-          wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
-        }
+        wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
       }
       __syncthreads();
-      const uint32_t n = sh.n_buf;
-      __syncthreads();  // every thread has read n before the next round appends
-      if (n > kTrunc) {
-        const uint64_t T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
-        if (tid == 0 && T > sh.thr) sh.thr = T;
-        __syncthreads();
+#ifdef FG_DIAG
+      if (sh.n_buf > kTrunc) dg_trunc++;
+#endif
+      disj_truncate(sh, K, kTrunc, gthr, false);
+    }
+    disj_truncate(sh, K, K, gthr, true);
+  }
+  FG_PHASE(2);
+
+  // ---- P: posting-driven tiles: flat list of the essential clauses' segments
+  if (tid == 0) {
+    uint32_t ns = 0, np = 0;
+    for (uint32_t t = 0; t < ntile; ++t) {
+      if (sh.t_mode[t] != 2u) continue;
+      const uint32_t ess = sh.t_ess[t];
+      for (uint32_t i = 0; i < m; ++i) {
+        if (!((ess >> i) & 1u)) continue;
+        const uint32_t n = sh.r_hi[t * m + i] - sh.r_lo[t * m + i];
+        if (!n) continue;
+        sh.u.p.seg_start[ns] = np;
+        sh.seg_info[ns] = (uint16_t)((t << 4) | i);
+        ++ns;
+        np += n;
       }
     }
-    // publish the local k-th key, read the best published one
-    const uint32_t n = sh.n_buf;
-    uint64_t local_T = 0;
-    if (n > K) {
-      local_T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
-    }
-    if (tid == 0) {
-      const uint64_t mine = local_T > sh.thr ? local_T : sh.thr;
-      const uint64_t old = atomicMax(gthr, (unsigned long long)mine);
-      sh.thr = old > mine ? old : mine;
+    sh.n_seg = ns;
+    sh.n_post = np;
+  }
+  __syncthreads();
+  const uint32_t n_seg = sh.n_seg, n_post = sh.n_post;
+  FG_PHASE(3);
+  for (uint32_t e0 = 0; e0 < n_post; e0 += kRound) {
+    const uint64_t thr = sh.thr;
+    if (tid == 0) sh.n_cand = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kRound / kThreads; ++j) {
+      const uint32_t e = e0 + j * kThreads + tid;
+      bool keep = e < n_post;
+      uint64_t cv = 0;
+      float csrc = 0.0f;
+      if (keep) {
+        // segment of posting e: last seg_start <= e
+        uint32_t lo = 0, hi = n_seg;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sh.u.p.seg_start[mid] <= e) lo = mid; else hi = mid;
+        }
+        const uint32_t info = sh.seg_info[lo];
+        const uint32_t t = info >> 4, c = info & 15u;
+        const uint32_t pos = sh.r_lo[t * m + c] + (e - sh.u.p.seg_start[lo]);
+        const uint64_t bi = sh.c_base[c];
+        const uint32_t d = ix.doc[bi + pos];
+        const float sc = term_score(ix.tf[bi + pos], load_fn(ix, d), sh.c_wt[c], sh.c_wn[c], ix.cache);
+        // bound 1: the other clauses' tile bounds (LDS)
+        float ub = sc;
+        for (uint32_t i = 0; i < m; ++i)
+          if (i != c) ub += sh.r_ub[t * m + i];
+        keep = make_key(inflate_bound(ub), d) >= thr;
+        uint32_t maybe = 0;  // clauses whose bucket at d holds postings (the rest cannot match d)
+        if (keep) {
+          // bound 2: the other clauses' bucket maxima at d
+          float ub2 = sc;
+          for (uint32_t i = 0; i < m; ++i) {
+            if (i == c || sh.r_ub[t * m + i] == 0.0f) continue;
+            const float b = ix.bmax[sh.c_dir[i] + (d >> (sh.c_meta[i] & 0xFFu))];
+            ub2 += b;
+            maybe |= (b > 0.0f ? 1u : 0u) << i;
+          }
+          keep = make_key(inflate_bound(ub2), d) >= thr && doc_alive(ix, d);
+        }
+        cv = ((uint64_t)d << 32) | (maybe << 16) | (t << 8) | c;
+        csrc = sc;
+      }
+      const unsigned long long bal = __ballot(keep);
+      if (bal) {
+        const uint32_t nw = (uint32_t)__popcll(bal);
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(&sh.n_cand, nw);
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        const uint32_t at = base + (uint32_t)__popcll(bal & ((1ull << lane_id()) - 1ull));
+        if (keep) {
+          sh.u.p.cand[at] = cv;
+          sh.u.p.cand_s[at] = csrc;
+        }
+      }
     }
     __syncthreads();
+    FG_PHASE(4);
+    const uint32_t nc = sh.n_cand;
+#ifdef FG_DIAG
+    dg_cand += nc;
+#endif
+    // exact rescoring: every (candidate, clause) pair probed in parallel, four
+    // pairs per thread in lockstep so their directory loads overlap
+    const uint32_t Q = kPairs / m;
+    for (uint32_t c0 = 0; c0 < nc; c0 += Q) {
+      const uint32_t nq_ = min(Q, nc - c0), np = nq_ * m;
+      constexpr uint32_t R = kPairs / kThreads;
+      uint32_t pd[R], pc[R], tfv[R], pos[R], hi[R];
+#pragma unroll
+      for (uint32_t j = 0; j < R; ++j) {
+        const uint32_t p = j * kThreads + tid;
+        pc[j] = kInvalid;
+        pd[j] = 0;
+        tfv[j] = 0;
+        pos[j] = 0;
+        hi[j] = 0;
+        if (p < np) {
+          const uint64_t cv = sh.u.p.cand[c0 + p / m];
+          const uint32_t i = p % m;
+          pd[j] = (uint32_t)(cv >> 32);
+          // the source clause is known; a clause with an empty bucket at d cannot match
+          pc[j] = (i == ((uint32_t)cv & 0xFFu) || !(((uint32_t)cv >> 16 >> i) & 1u)) ? (0x80000000u | i) : i;
+        }
+        if (!(pc[j] & 0x80000000u)) {
+          const uint32_t meta = sh.c_meta[pc[j]];
+          const uint32_t slot = meta >> 16;
+          if (slot) {
+            tfv[j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
+            pc[j] |= 0x80000000u;  // resolved
+          } else {
+            const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[pc[j]];
+            const uint32_t b = pd[j] >> (meta & 0xFFu);
+            pos[j] = dir[b];
+            hi[j] = dir[b + 1];
+          }
+        }
+      }
+      for (uint32_t st = sh.max_s; st > 0; --st) {
+#pragma unroll
+        for (uint32_t j = 0; j < R; ++j) {
+          if (pc[j] & 0x80000000u) continue;  // invalid or dense
+          if (st > ((sh.c_meta[pc[j]] >> 8) & 0xFFu)) continue;
+          const uint32_t half = 1u << (st - 1);
+          const uint32_t idx = pos[j] + half - 1;
+          if (idx < hi[j] && ix.doc[sh.c_base[pc[j]] + idx] < pd[j]) pos[j] += half;
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < R; ++j) {
+        if (pc[j] & 0x80000000u) continue;
+        const uint64_t base = sh.c_base[pc[j]];
+        if (pos[j] < hi[j] && ix.doc[base + pos[j]] == pd[j]) tfv[j] = ix.tf[base + pos[j]];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < R; ++j) {
+        const uint32_t p = j * kThreads + tid;
+        if (p >= np) continue;
+        const uint32_t c = pc[j] & 0x7FFFFFFFu;
+        const uint64_t cv = sh.u.p.cand[c0 + p / m];
+        float v;
+        if (c == ((uint32_t)cv & 0xFFu)) v = sh.u.p.cand_s[c0 + p / m];
+        else v = tfv[j] ? term_score(tfv[j], load_fn(ix, pd[j]), sh.c_wt[c], sh.c_wn[c], ix.cache) : 0.0f;
+        sh.u.p.cs[p] = v;
+      }
+      __syncthreads();
+      for (uint32_t cc0 = 0; cc0 < nq_; cc0 += kThreads) {
+        const uint32_t cc = cc0 + tid;
+        uint64_t key = 0;
+        bool keep = cc < nq_;
+        if (keep) {
+          const uint64_t cv = sh.u.p.cand[c0 + cc];
+          const uint32_t t = ((uint32_t)cv >> 8) & 0xFFu, src = (uint32_t)cv & 0xFFu;
+          (void)t;
+          float sc = 0.0f;  // SumCombiner from 0.0 in clause order (+0.0 for a missing clause is exact)
+          uint32_t matched = 0;
+          for (uint32_t i = 0; i < m; ++i) {
+            const float v = sh.u.p.cs[cc * m + i];
+            sc += v;
+            matched |= (v > 0.0f ? 1u : 0u) << i;
+          }
+          // unique keys: keep the doc only from the first essential clause it matches
+          const uint32_t first = (uint32_t)__builtin_ctz(matched & sh.t_ess[t]);
+          key = make_key(sc, (uint32_t)(cv >> 32));
+          keep = first == src && key >= thr;
+        }
+        wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
+      }
+      __syncthreads();
+    }
+    FG_PHASE(5);
+#ifdef FG_DIAG
+    if (sh.n_buf > K) dg_trunc++;
+#endif
+    disj_truncate(sh, K, K, gthr, true);
+    FG_PHASE(6);
   }
   flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
+  FG_PHASE(7);
+#ifdef FG_DIAG
+  FG_STAMP(w, 0, dg_t0);
+  FG_STAMP(w, 1, FG_NOW());
+  FG_STAMP(w, 2, dg_mode[0]);
+  FG_STAMP(w, 3, dg_mode[1]);
+  FG_STAMP(w, 4, dg_mode[2]);
+  FG_STAMP(w, 5, dg_post);
+  FG_STAMP(w, 6, dg_cand);
+  FG_STAMP(w, 7, (dg_trunc << 32) | q);
+  for (uint32_t i = 0; i < 8; ++i) FG_STAMP(w, 8 + i, dg_ph[i]);
+#endif
+#undef FG_PHASE
 }
 
 // ---------------------------------------------------------------- k_final

@@ -34,6 +34,7 @@ FG_MAX_K = 1024
 FG_TERM_MISSING = 0xFFFFFFFF
 MODE_AND = 0
 MODE_OR = 1
+DIAG_PER_WG = 16  # fg_internal.h kDiagPerWg
 
 # every symbol include/fugu.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -326,10 +327,11 @@ class Plan:
     def diag(self):
         """Per-workgroup phase stamps of the last execute (FG_DIAG builds only)."""
         info = self.info()
-        n = 8 * (info.total_chunks + self.n_queries)
+        n = DIAG_PER_WG * (info.total_chunks + self.n_queries)
         out = np.zeros(n, np.uint64)
         _check(_lib.fg_plan_diag(self._h, _ptr(out, _u64p), n, None))
-        return out.reshape(-1, 8)[: info.total_chunks], out.reshape(-1, 8)[info.total_chunks:]
+        w = out.reshape(-1, DIAG_PER_WG)
+        return w[: info.total_chunks], w[info.total_chunks:]
 
     def close(self):
         if self._h:

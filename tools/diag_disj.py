@@ -1,0 +1,59 @@
+"""k_disj work breakdown from the -DFG_DIAG build: tile modes, postings, candidates.
+
+Run on the GPU box:  FUGU_LIB=fugu_amd/libfugu_diag.so python tools/diag_disj.py [--docs N] [--k K]
+Prints a JSON summary (totals over the 1024-query batch + per-WG time percentiles).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=10_000_000)
+    ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--mmin", type=int, default=2)
+    ap.add_argument("--mmax", type=int, default=5)
+    args = ap.parse_args()
+    from fugu_amd import native, synth
+    ctx = native.Context((0,))
+    corp = synth.corpus(args.docs, threads=16)
+    ix = native.Index.from_docs(ctx, corp.off, corp.tok, synth.VOCAB, threads=16)
+    q_off, terms = synth.queries(1024, args.mmin, args.mmax)
+    plan = ix.plan(q_off, terms, args.k, mode=native.MODE_OR)
+    for _ in range(2):
+        plan.execute()
+    plan.results()
+    plan.profile(True)
+    plan.execute()
+    plan.results()
+    ms, n = plan.kernel_ms()
+    wg, _ = plan.diag()
+    dt = (wg[:, 1].astype(np.int64) - wg[:, 0].astype(np.int64)) * 10e-3  # us
+    dfs = np.array([ix.df(int(t)) for t in terms], np.float64)
+    out = {
+        "k_disj_ms": round(ms[0] / max(n, 1), 3), "k_final_ms": round(ms[1] / max(n, 1), 3),
+        "work_items": int(len(wg)),
+        "tiles_skip": int(wg[:, 2].sum()), "tiles_exact": int(wg[:, 3].sum()), "tiles_filter": int(wg[:, 4].sum()),
+        "postings_scattered": int(wg[:, 5].sum()), "postings_total": int(dfs.sum()),
+        "candidates_probed": int(wg[:, 6].sum()), "truncations": int((wg[:, 7] >> 32).sum()),
+        "wg_us": {p: round(float(np.percentile(dt, p)), 1) for p in (50, 90, 99, 100)},
+        "wg_us_sum_ms": round(float(dt.sum()) * 1e-3, 1),
+        "phase_ms_sum_over_wgs": {nm: round(float(wg[:, 8 + i].sum()) * 1e-5, 1) for i, nm in enumerate(
+            ["ranges", "split", "zero+stage", "scatter", "filter", "rescore", "scan_rest", "publish"])},
+        "cand_per_query": [int(x) for x in np.percentile(plan.candidate_counts(), [50, 90, 100])],
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    t = time.time()
+    main()
+    print(f"[diag_disj] {time.time() - t:.1f}s", file=sys.stderr)
