@@ -63,6 +63,17 @@ __device__ inline float term_score(uint32_t tfp, uint32_t fnp, float wt, float w
   return s;
 }
 
+// Upper bounds are compared after inflating by 2^-17 relative: that covers any
+// f32 summation-order difference for <= 16 addends, so bound-based pruning
+// never drops a doc whose exactly-summed score reaches the threshold.
+__device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f; }  // 1 + 2^-17
+
+// Upper bound of term t's score in doc d: the tile maximum (4096-doc tiles)
+// when the term has one, else the maximum of d's directory bucket.
+__device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t toff, uint32_t dir_off, uint32_t d) {
+  return toff != 0xFFFFFFFFu ? ix.tmax[toff + (d >> kDisjTileShift)] : ix.bmax[dir_off + (d >> (meta & 0xFFu))];
+}
+
 __device__ inline uint32_t load_fn(const DevIndex& ix, uint32_t d) {
   uint32_t f = ix.fn_text[d];
   if (ix.has_name) f |= (uint32_t)ix.fn_name[d] << 8;
@@ -197,6 +208,9 @@ __device__ void bitonic_sort_desc(uint64_t* s, uint32_t P) {
 #ifndef FG_TRUNC
 #define FG_TRUNC 1024
 #endif
+#ifndef FG_CONJ_PRUNE
+#define FG_CONJ_PRUNE 0  // block-max pre-probe pruning: measured slower (2.65 -> 3.51 ms, tools/ab_variants.py)
+#endif
 #ifndef FG_WAVES
 #define FG_WAVES 4  // tools/ab_variants.py: 3 -> 4 waves/SIMD took k_conj 3.18 -> 2.58 ms
 #endif
@@ -314,6 +328,33 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       acc_r[j] = 0.0f;
       acc_o[j] = 0.0f;
     }
+#if FG_CONJ_PRUNE
+    // block-max pruning before any probe: lead score + the other terms' tile /
+    // bucket maxima at the doc must reach the query threshold
+    const uint64_t thr_c = sh.thr;
+    if (m > 1 && thr_c != 0) {
+      float ubs[kItems];
+#pragma unroll
+      for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
+        ubs[j] = 0.0f;
+        if (live & (1u << j)) {
+          fnp[j] = load_fn(ix, doc[j]);
+          ubs[j] = term_score(ix.tf[base0 + idx], fnp[j], wt0, wn0, ix.cache);
+        }
+      }
+      for (uint32_t i = 1; i < m; ++i) {
+        const uint32_t ti = terms[i];
+        const uint32_t meta = ix.tmeta[ti], toff = ix.toff[ti], doff = ix.dir_off[ti];
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+          if (live & (1u << j)) ubs[j] += term_bound(ix, meta, toff, doff, doc[j]);
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kItems; ++j)
+        if ((live & (1u << j)) && make_key(inflate_bound(ubs[j]), doc[j]) < thr_c) live &= ~(1u << j);
+    }
+#endif
 
     for (uint32_t i = 1; i < m; ++i) {
       if (!__any(live != 0)) break;  // wave-uniform early exit
@@ -490,8 +531,6 @@ struct DisjShared {
   uint32_t n_buf, n_cand;
   uint64_t thr;
 };
-
-__device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f; }  // 1 + 2^-17
 
 __device__ inline bool doc_alive(const DevIndex& ix, uint32_t d) {
   return !ix.alive || ((ix.alive[d >> 5] >> (d & 31)) & 1u);
