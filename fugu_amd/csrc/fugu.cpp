@@ -154,6 +154,7 @@ struct fg_index {
   uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0;
   uint32_t n_dense = 0;
   uint64_t tot[2] = {0, 0};
+  uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
   float avgdl[2] = {0, 0};
   float cache[512];
   std::vector<uint64_t> off;
@@ -215,8 +216,9 @@ int check_device(int dev) {
   return FG_OK;
 }
 
-// Stats, weights, skip index, upload.  Consumes hp.
-int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
+// Stats, weights, skip index, upload.  Consumes hp.  g: global statistics of
+// a doc-sharded namespace (NULL: the shard's own).
+int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, const fg_global_stats* g = nullptr) {
   auto ix = std::make_unique<fg_index>();
   ix->dev = dev;
   ix->mem.dev = dev;
@@ -224,19 +226,21 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out) {
   ix->n_terms = hp.n_terms;
   ix->has_name = hp.has_name;
   ix->n_postings = hp.off[hp.n_terms];
-  ix->tot[0] = hp.tot[0];
-  ix->tot[1] = hp.tot[1];
-  const uint64_t N = hp.n_docs;
+  ix->tot[0] = g ? g->tot_tokens[0] : hp.tot[0];
+  ix->tot[1] = g ? g->tot_tokens[1] : hp.tot[1];
+  const uint64_t N = hp.n_docs;           // docs of this shard (array sizes)
+  const uint64_t Ns = g ? g->n_docs : N;  // N of the statistics
+  ix->n_stats = Ns;
   for (int f = 0; f < 2; ++f) {
-    ix->avgdl[f] = (float)hp.tot[f] / (float)N;  // total_num_tokens as f32 / N as f32
+    ix->avgdl[f] = (float)ix->tot[f] / (float)Ns;  // total_num_tokens as f32 / N as f32
     bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
   }
   const uint32_t V = hp.n_terms;
   ix->w_text.resize(V);
   ix->w_name.resize(V);
   for (uint32_t t = 0; t < V; ++t) {
-    ix->w_text[t] = bm25_weight(hp.df_text[t], N);
-    ix->w_name[t] = bm25_weight(hp.df_name[t], N);
+    ix->w_text[t] = bm25_weight(g ? g->df_text[t] : hp.df_text[t], Ns);
+    ix->w_name[t] = bm25_weight(g ? (g->df_name ? g->df_name[t] : 0u) : hp.df_name[t], Ns);
   }
   // doc -> position bucket directory (fg_internal.h DevIndex): bucket width
   // 2^B_t docs with B_t the largest shift keeping ~32 postings per bucket
@@ -451,8 +455,64 @@ int fg_ctx_destroy(fg_ctx* ctx) {
 }
 
 int fg_index_build_from_docs(fg_ctx* ctx, int dev, const fg_docs_input* in, fg_index** out) {
+  return fg_index_build_from_docs_global(ctx, dev, in, nullptr, out);
+}
+
+int fg_docs_stats(const fg_docs_input* in, uint32_t* df_text, uint32_t* df_name, uint64_t* tot_tokens2) {
+  if (!in || !df_text || !df_name || !tot_tokens2 || !in->text_off || (!in->text_tok && in->text_off[in->n_docs] > 0))
+    return fail(FG_EINVAL, "bad arguments");
+  const uint32_t N = in->n_docs, V = in->n_terms;
+  const bool has_name_in = in->name_off && in->name_tok;
+  const int T = hw_threads(in->threads);
+  std::vector<std::vector<uint32_t>> dft(T), dfn(T);
+  std::vector<uint64_t> tt(T, 0), tn(T, 0);
+  std::atomic<bool> bad{false};
+  parallel_ranges(N, T, [&](int t, uint32_t b, uint32_t e) {
+    dft[t].assign(V, 0);
+    dfn[t].assign(V, 0);
+    std::vector<uint32_t> scratch;
+    std::vector<std::pair<uint32_t, uint32_t>> runs;
+    for (uint32_t d = b; d < e; ++d) {
+      const uint64_t lt = in->text_off[d + 1] - in->text_off[d];
+      tt[t] += lt;
+      doc_runs(in->text_tok + in->text_off[d], lt, scratch, runs);
+      for (auto& r : runs) {
+        if (r.first >= V) { bad = true; return; }
+        dft[t][r.first]++;
+      }
+      if (has_name_in) {
+        const uint64_t ln = in->name_off[d + 1] - in->name_off[d];
+        tn[t] += ln;
+        doc_runs(in->name_tok + in->name_off[d], ln, scratch, runs);
+        for (auto& r : runs) {
+          if (r.first >= V) { bad = true; return; }
+          dfn[t][r.first]++;
+        }
+      }
+    }
+  });
+  if (bad) return fail(FG_EINVAL, "token id >= n_terms");
+  std::fill(df_text, df_text + V, 0u);
+  std::fill(df_name, df_name + V, 0u);
+  tot_tokens2[0] = tot_tokens2[1] = 0;
+  for (int t = 0; t < T; ++t) {
+    if (dft[t].empty()) continue;
+    for (uint32_t v = 0; v < V; ++v) {
+      df_text[v] += dft[t][v];
+      df_name[v] += dfn[t][v];
+    }
+    tot_tokens2[0] += tt[t];
+    tot_tokens2[1] += tn[t];
+  }
+  return FG_OK;
+}
+
+int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g,
+                                    fg_index** out) {
   if (!ctx || !in || !out || !in->text_off || (!in->text_tok && in->text_off[in->n_docs] > 0))
     return fail(FG_EINVAL, "bad arguments");
+  if (g && (!g->df_text || g->n_docs < in->n_docs || g->n_docs >= 0x7FFFFFFFull))
+    return fail(FG_EINVAL, "bad global statistics");
   if (in->n_docs == 0) return fail(FG_EINVAL, "empty index (n_docs == 0)");
   if (in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs must be < 2^31 (tantivy DocId)");
   if (std::find(ctx->devs.begin(), ctx->devs.end(), dev) == ctx->devs.end())
@@ -555,7 +615,11 @@ int fg_index_build_from_docs(fg_ctx* ctx, int dev, const fg_docs_input* in, fg_i
     for (uint32_t d = 0; d < N; ++d)
       if (!in->deleted[d]) hp.alive[d >> 5] |= 1u << (d & 31);
   }
-  return finish_index(dev, hp, in->keep_host_postings != 0, out);
+  if (g)
+    for (uint32_t t = 0; t < V; ++t)
+      if (g->df_text[t] < hp.df_text[t] || (g->df_name ? g->df_name[t] : 0u) < hp.df_name[t])
+        return fail(FG_EINVAL, "global df of term %u is below this shard's", t);
+  return finish_index(dev, hp, in->keep_host_postings != 0, out, g);
 }
 
 int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out) {
@@ -638,8 +702,8 @@ int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_nam
     if (w_text) *w_text = ix->w_text[term];
     if (w_name) *w_name = ix->w_name[term];
   } else {
-    if (w_text) *w_text = bm25_weight(0, ix->n_docs);
-    if (w_name) *w_name = bm25_weight(0, ix->n_docs);
+    if (w_text) *w_text = bm25_weight(0, ix->n_stats);
+    if (w_name) *w_name = bm25_weight(0, ix->n_stats);
   }
   if (cache512) std::memcpy(cache512, ix->cache, sizeof ix->cache);
   return FG_OK;

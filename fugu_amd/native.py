@@ -44,6 +44,7 @@ EXPORTS = (
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_merge_shards", "fg_bytes_model",
+    "fg_docs_stats", "fg_index_build_from_docs_global",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -72,6 +73,10 @@ class IndexInput(C.Structure):
     _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("term_off", _u64p), ("doc", _u32p),
                 ("tf_text", _u16p), ("tf_name", _u16p), ("fn_text", _u8p), ("fn_name", _u8p),
                 ("tot_tokens", C.c_uint64 * 2), ("deleted", _u8p)]
+
+
+class GlobalStats(C.Structure):
+    _fields_ = [("n_docs", C.c_uint64), ("tot_tokens", C.c_uint64 * 2), ("df_text", _u32p), ("df_name", _u32p)]
 
 
 class QueryBatch(C.Structure):
@@ -103,6 +108,9 @@ _sig("fg_last_error", C.c_char_p)
 _sig("fg_version", C.c_char_p)
 _sig("fg_index_build_from_docs", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(_p))
 _sig("fg_index_build", C.c_int, _p, C.c_int, C.POINTER(IndexInput), C.POINTER(_p))
+_sig("fg_docs_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u32p, _u64p)
+_sig("fg_index_build_from_docs_global", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(GlobalStats),
+     C.POINTER(_p))
 _sig("fg_index_retain", C.c_int, _p)
 _sig("fg_index_release", C.c_int, _p)
 _sig("fg_index_stats_get", C.c_int, _p, C.POINTER(IndexStats))
@@ -201,6 +209,43 @@ def _u32(a):
     return np.ascontiguousarray(a, dtype=np.uint32)
 
 
+def _docs_input(text_off, text_tok, n_terms, name_off=None, name_tok=None, deleted=None, threads=0,
+                keep_host=True):
+    text_off = _u64(text_off)
+    text_tok = _u32(text_tok)
+    name_off = None if name_off is None else _u64(name_off)
+    name_tok = None if name_tok is None else _u32(name_tok)
+    deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint8)
+    n_docs = len(text_off) - 1
+    inp = DocsInput(n_docs, n_terms, _ptr(text_off, _u64p), _ptr(text_tok, _u32p), _ptr(name_off, _u64p),
+                    _ptr(name_tok, _u32p), _ptr(deleted, _u8p), threads, 1 if keep_host else 0)
+    return (text_off, text_tok, name_off, name_tok, deleted), inp
+
+
+@dataclass
+class ShardStats:
+    """BM25 statistics of a (shard of a) namespace: summed across shards by one all-reduce."""
+    n_docs: int
+    tot_tokens: tuple
+    df_text: np.ndarray
+    df_name: np.ndarray
+
+    def __add__(self, o: "ShardStats") -> "ShardStats":
+        return ShardStats(self.n_docs + o.n_docs, tuple(a + b for a, b in zip(self.tot_tokens, o.tot_tokens)),
+                          self.df_text + o.df_text, self.df_name + o.df_name)
+
+
+def docs_stats(text_off, text_tok, n_terms: int, name_off=None, name_tok=None, threads: int = 0) -> ShardStats:
+    """fg_docs_stats: a shard's local statistics (host only, no device)."""
+    keep, inp = _docs_input(text_off, text_tok, n_terms, name_off, name_tok, None, threads, False)
+    dft = np.zeros(n_terms, np.uint32)
+    dfn = np.zeros(n_terms, np.uint32)
+    tot = np.zeros(2, np.uint64)
+    _check(_lib.fg_docs_stats(C.byref(inp), _ptr(dft, _u32p), _ptr(dfn, _u32p), _ptr(tot, _u64p)))
+    del keep
+    return ShardStats(int(inp.n_docs), (int(tot[0]), int(tot[1])), dft, dfn)
+
+
 class Index:
     """An immutable device snapshot of one namespace's docs index."""
 
@@ -209,18 +254,22 @@ class Index:
 
     @classmethod
     def from_docs(cls, ctx: Context, text_off, text_tok, n_terms: int, name_off=None, name_tok=None,
-                  deleted=None, device: int | None = None, threads: int = 0, keep_host: bool = True):
-        text_off = _u64(text_off)
-        text_tok = _u32(text_tok)
-        name_off = None if name_off is None else _u64(name_off)
-        name_tok = None if name_tok is None else _u32(name_tok)
-        deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint8)
-        n_docs = len(text_off) - 1
-        inp = DocsInput(n_docs, n_terms, _ptr(text_off, _u64p), _ptr(text_tok, _u32p), _ptr(name_off, _u64p),
-                        _ptr(name_tok, _u32p), _ptr(deleted, _u8p), threads, 1 if keep_host else 0)
+                  deleted=None, device: int | None = None, threads: int = 0, keep_host: bool = True,
+                  global_stats: "ShardStats | None" = None):
+        """Build a snapshot; `global_stats` (a doc-sharded namespace's summed
+        ShardStats) makes the BM25 statistics global while the postings stay local."""
+        keep, inp = _docs_input(text_off, text_tok, n_terms, name_off, name_tok, deleted, threads, keep_host)
         h = _p()
         dev = ctx.devices[0] if device is None else device
-        _check(_lib.fg_index_build_from_docs(ctx.handle, dev, C.byref(inp), C.byref(h)))
+        if global_stats is None:
+            _check(_lib.fg_index_build_from_docs(ctx.handle, dev, C.byref(inp), C.byref(h)))
+        else:
+            g = global_stats
+            dft, dfn = _u32(g.df_text), _u32(g.df_name)
+            gs = GlobalStats(int(g.n_docs), (C.c_uint64 * 2)(*[int(x) for x in g.tot_tokens]), _ptr(dft, _u32p),
+                             _ptr(dfn, _u32p))
+            _check(_lib.fg_index_build_from_docs_global(ctx.handle, dev, C.byref(inp), C.byref(gs), C.byref(h)))
+        del keep
         return cls(h)
 
     @property

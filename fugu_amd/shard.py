@@ -54,3 +54,33 @@ def merge_on_device(s: torch.Tensor, d: torch.Tensor, c: torch.Tensor, nq: int, 
     native.merge_shards(world, nq, k, s.data_ptr(), d.data_ptr(), c.data_ptr(), out_s.data_ptr(), out_d.data_ptr(),
                         out_sh.data_ptr(), out_n.data_ptr(), st)
     return out_s, out_d, out_sh, out_n
+
+
+# ---- doc-sharded namespace ------------------------
+def allreduce_stats(local, group=None, device=None):
+    """Sum a shard's BM25 statistics over the group: ONE all-reduce of
+    [n_docs, tot_text, tot_name, df_text[V], df_name[V]] as int64 (RCCL when the
+    group is "nccl": pass the rank's cuda device).  Returns native.ShardStats of
+    the whole namespace, identical on every rank."""
+    import numpy as np
+
+    from .native import ShardStats
+    V = len(local.df_text)
+    buf = np.empty(3 + 2 * V, np.int64)
+    buf[0] = local.n_docs
+    buf[1:3] = local.tot_tokens
+    buf[3:3 + V] = local.df_text
+    buf[3 + V:] = local.df_name
+    t = torch.from_numpy(buf)
+    if device is not None:
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    out = t.cpu().numpy()
+    return ShardStats(int(out[0]), (int(out[1]), int(out[2])), out[3:3 + V].astype(np.uint32),
+                      out[3 + V:].astype(np.uint32))
+
+
+def shard_ranges(n_docs: int, world: int):
+    """Contiguous doc-id ranges [b, e) of the shards (tantivy segments)."""
+    step = (n_docs + world - 1) // world
+    return [(min(r * step, n_docs), min((r + 1) * step, n_docs)) for r in range(world)]

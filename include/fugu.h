@@ -97,6 +97,28 @@ typedef struct fg_index_input {
 } fg_index_input;
 int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out);
 
+/* ---- doc-sharded namespace --------------------- */
+/* One namespace split into contiguous doc-id ranges, one shard per GPU, each
+ * scoring with the namespace's GLOBAL statistics -- exactly tantivy's segment
+ * model, where Bm25Weight reads N, total_num_tokens and doc_freq summed over
+ * all segments (core/searcher.rs Bm25StatisticsProvider) while each segment
+ * runs its own postings.  A shard computes its local statistics with
+ * fg_docs_stats, the ranks sum them (one all-reduce), and every shard builds
+ * with the sums.  Merging the shard top-k lists by (score desc, shard asc,
+ * doc asc) with fg_merge_shards then equals (score desc, global doc asc). */
+typedef struct fg_global_stats {
+  uint64_t n_docs;           /* N over all shards, deleted docs included */
+  uint64_t tot_tokens[2];    /* total_num_tokens(text), (name) over all shards */
+  const uint32_t* df_text;   /* [n_terms] doc_freq in `text` over all shards */
+  const uint32_t* df_name;   /* [n_terms] doc_freq in `name`, or NULL (all 0) */
+} fg_global_stats;
+/* Local statistics of one shard (host only, no device): df per term and field
+ * ([n_terms] each, caller-owned) and the two token totals. */
+int fg_docs_stats(const fg_docs_input* in, uint32_t* df_text, uint32_t* df_name, uint64_t* tot_tokens2);
+/* fg_index_build_from_docs scored with global statistics (g may be NULL = local). */
+int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g,
+                                    fg_index** out);
+
 int fg_index_retain(fg_index* ix);
 int fg_index_release(fg_index* ix);
 

@@ -191,3 +191,69 @@ def test_merge_shards_matches_numpy(native):
         assert np.array_equal(os_.cpu().numpy().reshape(nq, k)[q, :m], es[q, :m])
         assert np.array_equal(od.cpu().numpy().view(np.uint32).reshape(nq, k)[q, :m], ed[q, :m])
         assert np.array_equal(osh.cpu().numpy().reshape(nq, k)[q, :m], esh[q, :m])
+
+
+# ---------------------------------------------------------------- doc-sharded namespace
+def _device_merge(native, sc, dc, nn, k):
+    import torch
+    S, nq, _ = sc.shape
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32) if a.dtype == np.uint32
+                                   else np.ascontiguousarray(a)).to(dev)
+    ts, td, tn = t(sc), t(dc), t(nn)
+    os_ = torch.zeros(nq * k, dtype=torch.float32, device=dev)
+    od = torch.zeros(nq * k, dtype=torch.int32, device=dev)
+    osh = torch.zeros(nq * k, dtype=torch.int32, device=dev)
+    on = torch.zeros(nq, dtype=torch.int32, device=dev)
+    native.merge_shards(S, nq, k, ts.data_ptr(), td.data_ptr(), tn.data_ptr(), os_.data_ptr(), od.data_ptr(),
+                        osh.data_ptr(), on.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return (os_.cpu().numpy().reshape(nq, k), od.cpu().numpy().view(np.uint32).reshape(nq, k),
+            osh.cpu().numpy().reshape(nq, k), on.cpu().numpy())
+
+
+@pytest.mark.parametrize("m_min,m_max,k,mode", [(1, 2, 100, 0), (2, 4, 1000, 1), (3, 3, 100, 0)])
+def test_doc_sharded_namespace_equals_single_index(native, ctx, corpus_1m, gpu_1m, m_min, m_max, k, mode):
+    """Three contiguous doc-range shards scored with the summed (global) statistics
+    and merged by (score desc, shard asc, doc asc) give the single index's top-k:
+    tantivy's multi-segment search.  Exact for OR and <= 2-term AND; a 3-term AND
+    sums in each shard's own cost order, as tantivy does per segment, so there the
+    scores are checked to 1e-6 relative and doc ids up to near-tie swaps."""
+    from fugu_amd.shard import shard_ranges
+    c = corpus_1m
+    V = 1 << 20
+    ranges = shard_ranges(len(c.off) - 1, 3)
+    parts = []
+    for b, e in ranges:
+        off = c.off[b:e + 1] - c.off[b]
+        parts.append((b, off, c.tok[c.off[b]:c.off[e]]))
+    local = [native.docs_stats(off, tok, V, threads=16) for _, off, tok in parts]
+    g = local[0] + local[1] + local[2]
+    full = native.docs_stats(c.off, c.tok, V, threads=16)
+    assert g.n_docs == full.n_docs and g.tot_tokens == full.tot_tokens and np.array_equal(g.df_text, full.df_text)
+    shards = [native.Index.from_docs(ctx, off, tok, V, threads=16, global_stats=g) for _, off, tok in parts]
+    from fugu_amd import synth
+    q_off, terms = synth.queries(256, m_min, m_max, seed_q=11)
+    nq = len(q_off) - 1
+    res = [ix.search_batch(q_off, terms, k, mode=mode) for ix in shards]
+    sc = np.stack([r[0] for r in res])
+    dc = np.stack([r[1] for r in res])
+    nn = np.stack([r[2] for r in res])
+    ms, md, msh, mn = _device_merge(native, sc, dc, nn, k)
+    base = np.array([b for b, _, _ in parts], np.uint32)
+    gdoc = md + base[msh]
+    s1, d1, n1 = gpu_1m.search_batch(q_off, terms, k, mode=mode)
+    assert np.array_equal(mn, n1)
+    exact = mode == 1 or m_max <= 2
+    for i in range(nq):
+        m = int(n1[i])
+        if exact:
+            assert np.array_equal(gdoc[i, :m], d1[i, :m]), i
+            assert np.array_equal(ms[i, :m], s1[i, :m]), i
+        else:
+            rel = np.abs(ms[i, :m].astype(np.float64) - s1[i, :m]) / np.maximum(s1[i, :m], 1e-30)
+            assert (rel <= 1e-6).all(), (i, rel.max())
+            bad = np.nonzero(gdoc[i, :m] != d1[i, :m])[0]
+            for j in bad:  # only swaps between scores equal to ~1 ulp
+                near = np.abs(s1[i, :m].astype(np.float64) - s1[i, j]) <= 1e-6 * s1[i, j]
+                assert gdoc[i, j] in d1[i, :m][near], (i, j)

@@ -94,3 +94,53 @@ def test_two_rank_fanout_matches_direct_merge():
                        for r in range(world) for i in range(int(per[r][2][q]))], key=lambda x: (-x[0], x[1], x[2]))[:k]
         assert mn[q] == len(rows)
         assert [(int(msh[q, i]), int(md[q, i])) for i in range(mn[q])] == [(r[1], r[2]) for r in rows]
+
+
+def _stats_worker(rank, world, port, outq):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fugu_amd import native, synth
+    from fugu_amd.shard import allreduce_stats, shard_ranges
+    c = synth.corpus(6000, 1 << 16)
+    b, e = shard_ranges(6000, world)[rank]
+    off = c.off[b:e + 1] - c.off[b]
+    tok = c.tok[c.off[b]:c.off[e]]
+    g = allreduce_stats(native.docs_stats(off, tok, 1 << 16))
+    if rank == 0:
+        outq.put((g.n_docs, g.tot_tokens, g.df_text, g.df_name))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_global_stats_allreduce():
+    """Doc-sharded namespace: the summed shard statistics equal the whole corpus's."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, world, port, outq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    got = None
+    for _ in range(240):
+        try:
+            got = outq.get(timeout=1)
+            break
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, "a rank failed"
+    assert got is not None
+    n, tot, dft, dfn = got
+    from fugu_amd import native, synth
+    c = synth.corpus(6000, 1 << 16)
+    full = native.docs_stats(c.off, c.tok, 1 << 16)
+    assert n == full.n_docs and tot == full.tot_tokens
+    assert np.array_equal(dft, full.df_text) and np.array_equal(dfn, full.df_name)
