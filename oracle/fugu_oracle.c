@@ -98,18 +98,24 @@ typedef struct {
   uint32_t* last;    /* skip list: last doc of each 128-doc block */
 } Postings;
 
+/* Field slots: 0 = text, 1 = name (TEXT, "default" analyzer), 2 = facet
+ * (schemas.rs:20 add_facet_field("facet", INDEXED|STORED): IndexRecordOption
+ * Basic, so tf = 1; no fieldnorms, so tantivy reads FieldNormReader::constant(
+ * max_doc, 1) = id 1; total_num_tokens counts every FacetTokenizer token). */
+#define OR_FIELDS 3
+#define OR_FACET 2
 typedef struct or_index {
-  uint32_t n_docs, n_terms;
+  uint32_t n_docs, n_terms, n_fterms;
   int has_name;
-  Postings* fld[2];         /* [0]=text, [1]=name, each [n_terms] */
-  uint32_t* store_doc[2];
-  uint32_t* store_tf[2];
-  uint32_t* store_last[2];
-  uint8_t* fn[2];           /* fieldnorm ids [n_docs] */
-  uint8_t* deleted;         /* nullable [n_docs] */
-  uint64_t tot[2];          /* total_num_tokens per field (deleted docs included) */
-  float avgdl[2];
-  float cache[2][256];
+  Postings* fld[OR_FIELDS];   /* [0]=text, [1]=name: [n_terms]; [2]=facet: [n_fterms] */
+  uint32_t* store_doc[OR_FIELDS];
+  uint32_t* store_tf[OR_FIELDS];
+  uint32_t* store_last[OR_FIELDS];
+  uint8_t* fn[OR_FIELDS];     /* fieldnorm ids [n_docs] (facet: constant 1) */
+  uint8_t* deleted;           /* nullable [n_docs] */
+  uint64_t tot[OR_FIELDS];    /* total_num_tokens per field (deleted docs included) */
+  float avgdl[OR_FIELDS];
+  float cache[OR_FIELDS][256];
 } or_index;
 
 typedef struct {
@@ -156,8 +162,8 @@ static void* build_worker(void* arg) {
   return NULL;
 }
 
-static int build_field(or_index* ix, int f, const uint64_t* off, const uint32_t* tok, int threads) {
-  uint32_t nt = ix->n_terms, nd = ix->n_docs;
+static int build_field(or_index* ix, int f, const uint64_t* off, const uint32_t* tok, int threads, uint32_t nt) {
+  uint32_t nd = ix->n_docs;
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
   BuildJob* jobs = (BuildJob*)calloc((size_t)threads, sizeof(BuildJob));
@@ -221,7 +227,7 @@ static int build_field(or_index* ix, int f, const uint64_t* off, const uint32_t*
 
 void or_index_free(or_index* ix) {
   if (!ix) return;
-  for (int f = 0; f < 2; ++f) {
+  for (int f = 0; f < OR_FIELDS; ++f) {
     free(ix->fld[f]); free(ix->store_doc[f]); free(ix->store_tf[f]); free(ix->store_last[f]); free(ix->fn[f]);
   }
   free(ix->deleted);
@@ -241,9 +247,9 @@ or_index* or_index_build(uint32_t n_docs, uint32_t n_terms, const uint64_t* text
   ix->n_docs = n_docs; ix->n_terms = n_terms;
   static const uint64_t zero_off_dummy = 0;
   (void)zero_off_dummy;
-  if (build_field(ix, 0, text_off, text_tok, threads)) { or_index_free(ix); return NULL; }
+  if (build_field(ix, 0, text_off, text_tok, threads, n_terms)) { or_index_free(ix); return NULL; }
   if (name_off && name_tok) {
-    if (build_field(ix, 1, name_off, name_tok, threads)) { or_index_free(ix); return NULL; }
+    if (build_field(ix, 1, name_off, name_tok, threads, n_terms)) { or_index_free(ix); return NULL; }
     ix->has_name = 1;
   } else {
     /* empty name field: every doc has fieldnorm 0, no postings */
@@ -262,7 +268,30 @@ or_index* or_index_build(uint32_t n_docs, uint32_t n_terms, const uint64_t* text
   return ix;
 }
 
-uint32_t or_df(const or_index* ix, int field, uint32_t term) { return term < ix->n_terms ? ix->fld[field][term].n : 0; }
+/* Facets of each doc as FacetTokenizer output (facet/facet_tokenizer.rs: the
+ * root, then every ancestor, then the facet itself, for each stored facet
+ * value; duplicates kept -- they count in total_num_tokens, not in df).
+ * fugu indexes them through build_full_document -> add_facets_to_document
+ * (src/db/document.rs:175-178, 310-330). */
+int or_index_set_facets(or_index* ix, uint32_t n_fterms, const uint64_t* facet_off, const uint32_t* facet_tok,
+                        int threads) {
+  if (!ix || !facet_off || ix->fld[OR_FACET]) return -1;
+  if (build_field(ix, OR_FACET, facet_off, facet_tok, threads, n_fterms)) return -1;
+  ix->n_fterms = n_fterms;
+  /* IndexRecordOption::Basic: term_freq() = 1; no fieldnorms: constant id 1 */
+  uint64_t np = 0;
+  for (uint32_t t = 0; t < n_fterms; ++t) np += ix->fld[OR_FACET][t].n;
+  for (uint64_t p = 0; p < np; ++p) ix->store_tf[OR_FACET][p] = 1;
+  memset(ix->fn[OR_FACET], 1, ix->n_docs ? ix->n_docs : 1);
+  ix->avgdl[OR_FACET] = (float)ix->tot[OR_FACET] / (float)ix->n_docs;
+  or_bm25_cache(ix->avgdl[OR_FACET], ix->cache[OR_FACET]);
+  return 0;
+}
+
+uint32_t or_df(const or_index* ix, int field, uint32_t term) {
+  uint32_t nt = field == OR_FACET ? ix->n_fterms : ix->n_terms;
+  return term < nt && ix->fld[field] ? ix->fld[field][term].n : 0;
+}
 uint64_t or_total_tokens(const or_index* ix, int field) { return ix->tot[field]; }
 float or_avgdl(const or_index* ix, int field) { return ix->avgdl[field]; }
 void or_cache(const or_index* ix, int field, float* out) { memcpy(out, ix->cache[field], sizeof(float) * 256); }
@@ -502,10 +531,217 @@ int or_search(const or_index* ix, const uint32_t* terms, uint32_t m, int mode, u
   return (int)topn_finish(&top, out_score, out_doc);
 }
 
+/* ---------------------------------------------------------------- filtered search */
+/*
+ * Dataset::search with facet filters (src/db/search.rs:129-150):
+ *   base_query = Bool[Must(text_query), Must(facet_query)]   text and filters
+ *              = facet_query                                  empty text, filters
+ *              = AllQuery                                     empty text, no filters
+ * facet_query = build_facet_query (:221-293): Should over the exact facet
+ * terms (new_multiterms_query), then one Should TermQuery per prefix filter;
+ * the caller passes that flat clause list (exact terms first, then prefixes).
+ * A union scores 0.0 + the matching clauses in clause order (SumCombiner);
+ * an Intersection of two children scores left + right (+ 0.0 for no others),
+ * which is commutative, so the order the children run in does not matter.
+ * AllScorer scores 1.0 (query/all_query.rs).  Scorers are generic cursors here.
+ */
+typedef struct Cur {
+  uint32_t (*doc)(struct Cur*);
+  uint32_t (*advance)(struct Cur*);
+  uint32_t (*seek)(struct Cur*, uint32_t);
+  float (*score)(struct Cur*);
+  uint64_t cost;
+} Cur;
+
+/* text AND over >= 2 terms: Intersection of the per-term unions */
+typedef struct { Cur c; UnionCur* ds[OR_MAX_TERMS]; uint32_t n, d; } AndCur;
+static uint32_t and_doc(Cur* c) { return ((AndCur*)c)->d; }
+static uint32_t and_advance(Cur* c) { AndCur* a = (AndCur*)c; return a->d = isect_advance(a->ds, a->n); }
+static uint32_t and_seek(Cur* c, uint32_t t) {
+  AndCur* a = (AndCur*)c;
+  if (a->d >= t) return a->d;
+  uc_seek(a->ds[0], t);
+  return a->d = go_to_first_doc(a->ds, a->n);
+}
+static float and_score(Cur* c) { AndCur* a = (AndCur*)c; return isect_score(a->ds, a->n); }
+
+/* one text term: the field union itself */
+typedef struct { Cur c; UnionCur* u; } OneCur;
+static uint32_t one_doc(Cur* c) { return ((OneCur*)c)->u->doc; }
+static uint32_t one_advance(Cur* c) { return uc_advance(((OneCur*)c)->u); }
+static uint32_t one_seek(Cur* c, uint32_t t) { return uc_seek(((OneCur*)c)->u, t); }
+static float one_score(Cur* c) { return uc_score(((OneCur*)c)->u); }
+
+/* text OR: union of the per-term unions, SumCombiner in clause order */
+typedef struct { Cur c; UnionCur* u; uint32_t n, d; } OrCur;
+static uint32_t or_min(OrCur* o) {
+  uint32_t d = OR_TERMINATED;
+  for (uint32_t i = 0; i < o->n; ++i) d = min_u32(d, o->u[i].doc);
+  return o->d = d;
+}
+static uint32_t orc_doc(Cur* c) { return ((OrCur*)c)->d; }
+static uint32_t orc_advance(Cur* c) {
+  OrCur* o = (OrCur*)c;
+  for (uint32_t i = 0; i < o->n; ++i) if (o->u[i].doc == o->d) uc_advance(&o->u[i]);
+  return or_min(o);
+}
+static uint32_t orc_seek(Cur* c, uint32_t t) {
+  OrCur* o = (OrCur*)c;
+  if (o->d >= t) return o->d;
+  for (uint32_t i = 0; i < o->n; ++i) uc_seek(&o->u[i], t);
+  return or_min(o);
+}
+static float orc_score(Cur* c) {
+  OrCur* o = (OrCur*)c;
+  float s = 0.0f;
+  for (uint32_t i = 0; i < o->n; ++i) if (o->u[i].doc == o->d) s += uc_score(&o->u[i]);
+  return s;
+}
+
+/* facet_query: union of facet TermScorers (tf 1, fieldnorm id 1), clause order */
+#define OR_MAX_FACETS 64
+typedef struct { Cur c; TermCur t[OR_MAX_FACETS]; uint32_t n, d; } FacetCur;
+static uint32_t fc_min(FacetCur* f) {
+  uint32_t d = OR_TERMINATED;
+  for (uint32_t i = 0; i < f->n; ++i) d = min_u32(d, tc_doc(&f->t[i]));
+  return f->d = d;
+}
+static uint32_t fc_doc(Cur* c) { return ((FacetCur*)c)->d; }
+static uint32_t fc_advance(Cur* c) {
+  FacetCur* f = (FacetCur*)c;
+  for (uint32_t i = 0; i < f->n; ++i) if (tc_doc(&f->t[i]) == f->d) tc_advance(&f->t[i]);
+  return fc_min(f);
+}
+static uint32_t fc_seek(Cur* c, uint32_t t) {
+  FacetCur* f = (FacetCur*)c;
+  if (f->d >= t) return f->d;
+  for (uint32_t i = 0; i < f->n; ++i) tc_seek(&f->t[i], t);
+  return fc_min(f);
+}
+static float fc_score(Cur* c) {
+  FacetCur* f = (FacetCur*)c;
+  float s = 0.0f;
+  for (uint32_t i = 0; i < f->n; ++i) if (tc_doc(&f->t[i]) == f->d) s += tc_score(&f->t[i]);
+  return s;
+}
+
+/* AllQuery: every doc, score 1.0 */
+typedef struct { Cur c; uint32_t d, n; } AllCur;
+static uint32_t all_doc(Cur* c) { return ((AllCur*)c)->d; }
+static uint32_t all_advance(Cur* c) {
+  AllCur* a = (AllCur*)c;
+  a->d = a->d + 1 < a->n ? a->d + 1 : OR_TERMINATED;
+  return a->d;
+}
+static uint32_t all_seek(Cur* c, uint32_t t) {
+  AllCur* a = (AllCur*)c;
+  if (a->d >= t) return a->d;
+  a->d = t < a->n ? t : OR_TERMINATED;
+  return a->d;
+}
+static float all_score(Cur* c) { (void)c; return 1.0f; }
+
+/*
+ * terms/m/mode: the text query (m = 0: empty text); fterms/nf: the facet
+ * clauses (facet term ids, ids >= n_fterms match nothing; nf = 0: no filter).
+ * Returns hits written (<= k) or -1 on bad arguments.
+ */
+int or_search_ex(const or_index* ix, const uint32_t* terms, uint32_t m, int mode, const uint32_t* fterms, uint32_t nf,
+                 uint32_t k, float* out_score, uint32_t* out_doc) {
+  if (k < 1 || m > OR_MAX_TERMS || nf > OR_MAX_FACETS) return -1;
+  if (nf == 0 && m > 0) return or_search(ix, terms, m, mode, k, out_score, out_doc);
+  UnionCur uc[OR_MAX_TERMS];
+  Child ch[OR_MAX_TERMS];
+  AndCur ac; OneCur oc; OrCur orc; FacetCur fc; AllCur al;
+  Cur* text = NULL;
+  for (uint32_t i = 0; i < m; ++i) {
+    uc_init(&uc[i], ix, terms[i]);
+    ch[i].c = &uc[i]; ch[i].cost = uc[i].cost; ch[i].qpos = i;
+  }
+  if (m == 0) {
+    text = NULL;
+  } else if (mode == 0 && m == 1) {
+    oc.u = &uc[0];
+    oc.c = (Cur){one_doc, one_advance, one_seek, one_score, uc[0].cost};
+    text = &oc.c;
+  } else if (mode == 0) {
+    qsort(ch, m, sizeof(Child), child_cmp);
+    for (uint32_t i = 0; i < m; ++i) ac.ds[i] = ch[i].c;
+    ac.n = m;
+    ac.d = go_to_first_doc(ac.ds, m);
+    ac.c = (Cur){and_doc, and_advance, and_seek, and_score, ac.ds[0]->cost};
+    text = &ac.c;
+  } else {
+    orc.u = uc; orc.n = m;
+    uint64_t cost = 0;
+    for (uint32_t i = 0; i < m; ++i) cost += uc[i].cost;
+    or_min(&orc);
+    orc.c = (Cur){orc_doc, orc_advance, orc_seek, orc_score, cost};
+    text = &orc.c;
+  }
+  Cur* filt = NULL;
+  if (nf > 0) {
+    static const Postings empty = {0, NULL, NULL, NULL};
+    uint64_t cost = 0;
+    for (uint32_t i = 0; i < nf; ++i) {
+      const Postings* p = (ix->fld[OR_FACET] && fterms[i] < ix->n_fterms) ? &ix->fld[OR_FACET][fterms[i]] : &empty;
+      fc.t[i].p = p;
+      fc.t[i].cur = 0;
+      fc.t[i].weight = or_term_weight(p->n, ix->n_docs);
+      fc.t[i].cache = ix->cache[OR_FACET];
+      fc.t[i].fn = ix->fn[OR_FACET];
+      cost += p->n;
+    }
+    fc.n = nf;
+    fc_min(&fc);
+    fc.c = (Cur){fc_doc, fc_advance, fc_seek, fc_score, cost};
+    filt = &fc.c;
+  } else {
+    al.n = ix->n_docs;
+    al.d = ix->n_docs ? 0 : OR_TERMINATED;
+    al.c = (Cur){all_doc, all_advance, all_seek, all_score, ix->n_docs};
+    filt = &al.c; /* m == 0 here: the query is AllQuery itself */
+  }
+  TopN top;
+  topn_init(&top, k);
+  float thr = -3.40282347e+38f;
+  if (!text) {
+    for (uint32_t d = filt->doc(filt); d != OR_TERMINATED; d = filt->advance(filt)) {
+      float s = filt->score(filt);
+      if (s > thr) thr = collect(&top, ix, d, s);
+    }
+  } else {
+    /* Intersection of (text, facet): children by cost (stable), leapfrog */
+    Cur* left = text->cost <= filt->cost ? text : filt;
+    Cur* right = left == text ? filt : text;
+    uint32_t cand = left->doc(left) > right->doc(right) ? left->doc(left) : right->doc(right);
+    for (;;) {
+      uint32_t a = left->seek(left, cand);
+      uint32_t b = right->seek(right, a);
+      if (b == a) { cand = a; break; }
+      cand = b;
+    }
+    while (cand != OR_TERMINATED) {
+      float s = left->score(left) + right->score(right) + 0.0f;
+      if (s > thr) thr = collect(&top, ix, cand, s);
+      cand = left->advance(left);
+      if (cand == OR_TERMINATED) break;
+      for (;;) {
+        uint32_t r = right->seek(right, cand);
+        if (r == cand) break;
+        cand = left->seek(left, r);
+        if (cand == OR_TERMINATED) break;
+      }
+    }
+  }
+  return (int)topn_finish(&top, out_score, out_doc);
+}
+
 /* ---------------------------------------------------------------- batch (CPU baseline) */
 typedef struct {
   const or_index* ix;
   const uint32_t* q_off; const uint32_t* q_terms;
+  const uint32_t* f_off; const uint32_t* f_terms; /* nullable: no facet filters */
   uint32_t nq; int mode; uint32_t k;
   float* out_score; uint32_t* out_doc; uint32_t* out_n;
   double* lat_ns;
@@ -525,8 +761,11 @@ static void* batch_worker(void* arg) {
     uint32_t q = __atomic_fetch_add(&c->next, 1u, __ATOMIC_RELAXED);
     if (q >= c->nq) break;
     double t0 = now_ns();
-    int n = or_search(c->ix, c->q_terms + c->q_off[q], c->q_off[q + 1] - c->q_off[q], c->mode, c->k,
-                      c->out_score + (size_t)q * c->k, c->out_doc + (size_t)q * c->k);
+    int n = c->f_off ? or_search_ex(c->ix, c->q_terms + c->q_off[q], c->q_off[q + 1] - c->q_off[q], c->mode,
+                                    c->f_terms + c->f_off[q], c->f_off[q + 1] - c->f_off[q], c->k,
+                                    c->out_score + (size_t)q * c->k, c->out_doc + (size_t)q * c->k)
+                     : or_search(c->ix, c->q_terms + c->q_off[q], c->q_off[q + 1] - c->q_off[q], c->mode, c->k,
+                                 c->out_score + (size_t)q * c->k, c->out_doc + (size_t)q * c->k);
     double t1 = now_ns();
     c->out_n[q] = n < 0 ? 0 : (uint32_t)n;
     if (c->lat_ns) c->lat_ns[q] = t1 - t0;
@@ -536,11 +775,13 @@ static void* batch_worker(void* arg) {
 
 /* Each thread runs whole queries (a tokio worker per request, tantivy's
  * single-threaded executor).  Returns the wall time in seconds. */
-double or_search_batch(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, uint32_t nq, int mode,
-                       uint32_t k, float* out_score, uint32_t* out_doc, uint32_t* out_n, double* lat_ns, int threads) {
+double or_search_batch_ex(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, const uint32_t* f_off,
+                          const uint32_t* f_terms, uint32_t nq, int mode, uint32_t k, float* out_score,
+                          uint32_t* out_doc, uint32_t* out_n, double* lat_ns, int threads) {
   BatchCtx c;
   memset(&c, 0, sizeof c);
   c.ix = ix; c.q_off = q_off; c.q_terms = q_terms; c.nq = nq; c.mode = mode; c.k = k;
+  c.f_off = f_off; c.f_terms = f_terms;
   c.out_score = out_score; c.out_doc = out_doc; c.out_n = out_n; c.lat_ns = lat_ns; c.next = 0;
   if (threads < 1) threads = 1;
   if (threads > 512) threads = 512;
@@ -551,6 +792,11 @@ double or_search_batch(const or_index* ix, const uint32_t* q_off, const uint32_t
   double t1 = now_ns();
   free(th);
   return (t1 - t0) * 1e-9;
+}
+
+double or_search_batch(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, uint32_t nq, int mode,
+                       uint32_t k, float* out_score, uint32_t* out_doc, uint32_t* out_n, double* lat_ns, int threads) {
+  return or_search_batch_ex(ix, q_off, q_terms, NULL, NULL, nq, mode, k, out_score, out_doc, out_n, lat_ns, threads);
 }
 
 /* ---------------------------------------------------------------- bytes model */

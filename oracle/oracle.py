@@ -46,11 +46,18 @@ _lib.or_search.restype = C.c_int
 _lib.or_search.argtypes = [_p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p]
 _lib.or_search_batch.restype = C.c_double
 _lib.or_search_batch.argtypes = [_p, _p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p, _p, _p, C.c_int]
+_lib.or_index_set_facets.restype = C.c_int
+_lib.or_index_set_facets.argtypes = [_p, C.c_uint32, _p, _p, C.c_int]
+_lib.or_search_ex.restype = C.c_int
+_lib.or_search_ex.argtypes = [_p, _p, C.c_uint32, C.c_int, _p, C.c_uint32, C.c_uint32, _p, _p]
+_lib.or_search_batch_ex.restype = C.c_double
+_lib.or_search_batch_ex.argtypes = [_p, _p, _p, _p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p, _p, _p, C.c_int]
 _lib.or_bytes_model.restype = C.c_int
 _lib.or_bytes_model.argtypes = [_p, _p, C.c_uint32, C.c_uint32, _p]
 
 AND = 0
 OR = 1
+FACET = 2  # field slot of the facet field (or_df / or_total_tokens / or_avgdl)
 
 
 def fieldnorm_table():
@@ -79,7 +86,7 @@ def bm25_cache(avgdl: float):
 
 class OracleIndex:
     def __init__(self, n_terms: int, text_off, text_tok, name_off=None, name_tok=None, deleted=None,
-                 threads: int = 1):
+                 threads: int = 1, facet_off=None, facet_tok=None, n_fterms: int = 0):
         self._keep = [np.ascontiguousarray(text_off, np.uint64), np.ascontiguousarray(text_tok, np.uint32)]
         n_docs = len(self._keep[0]) - 1
         no = nt = dl = None
@@ -95,6 +102,12 @@ class OracleIndex:
                                       None if dl is None else dl.ctypes.data, threads)
         if not self._h:
             raise MemoryError("oracle index build failed")
+        if facet_off is not None:
+            fo = np.ascontiguousarray(facet_off, np.uint64)
+            ft = np.ascontiguousarray(facet_tok, np.uint32)
+            self._keep += [fo, ft]
+            if _lib.or_index_set_facets(self._h, n_fterms, fo.ctypes.data, ft.ctypes.data, threads) != 0:
+                raise ValueError("oracle facet build failed")
         self.n_docs = n_docs
         self.n_terms = n_terms
 
@@ -115,25 +128,37 @@ class OracleIndex:
     def fieldnorm_id(self, doc: int, field: int = 0) -> int:
         return int(_lib.or_fieldnorm_id_of(self._h, field, doc))
 
-    def search(self, terms, k: int, mode: int = AND):
+    def search(self, terms, k: int, mode: int = AND, fterms=None):
+        """fterms: facet clauses (None: no filter); empty `terms` = empty text query."""
         t = np.ascontiguousarray(terms, np.uint32)
         score = np.zeros(k, np.float32)
         doc = np.zeros(k, np.uint32)
-        n = _lib.or_search(self._h, t.ctypes.data, len(t), mode, k, score.ctypes.data, doc.ctypes.data)
+        if fterms is None and len(t) > 0:
+            n = _lib.or_search(self._h, t.ctypes.data, len(t), mode, k, score.ctypes.data, doc.ctypes.data)
+        else:
+            f = np.ascontiguousarray(fterms if fterms is not None else [], np.uint32)
+            n = _lib.or_search_ex(self._h, t.ctypes.data, len(t), mode, f.ctypes.data, len(f), k,
+                                  score.ctypes.data, doc.ctypes.data)
         if n < 0:
             raise ValueError("oracle rejected the query")
         return score[:n].copy(), doc[:n].copy()
 
-    def search_batch(self, q_off, q_terms, k: int, mode: int = AND, threads: int = 1, latencies: bool = False):
+    def search_batch(self, q_off, q_terms, k: int, mode: int = AND, threads: int = 1, latencies: bool = False,
+                     f_off=None, f_terms=None):
         q_off = np.ascontiguousarray(q_off, np.uint32)
         q_terms = np.ascontiguousarray(q_terms, np.uint32)
+        if f_off is not None:
+            f_off = np.ascontiguousarray(f_off, np.uint32)
+            f_terms = np.ascontiguousarray(f_terms, np.uint32)
         nq = len(q_off) - 1
         score = np.zeros(nq * k, np.float32)
         doc = np.zeros(nq * k, np.uint32)
         n = np.zeros(nq, np.uint32)
         lat = np.zeros(nq, np.float64) if latencies else None
-        wall = _lib.or_search_batch(self._h, q_off.ctypes.data, q_terms.ctypes.data, nq, mode, k, score.ctypes.data,
-                                    doc.ctypes.data, n.ctypes.data, None if lat is None else lat.ctypes.data, threads)
+        wall = _lib.or_search_batch_ex(self._h, q_off.ctypes.data, q_terms.ctypes.data,
+                                       None if f_off is None else f_off.ctypes.data,
+                                       None if f_off is None else f_terms.ctypes.data, nq, mode, k, score.ctypes.data,
+                                       doc.ctypes.data, n.ctypes.data, None if lat is None else lat.ctypes.data, threads)
         return score.reshape(nq, k), doc.reshape(nq, k), n, wall, lat
 
     def bytes_model(self, terms, k: int):

@@ -47,6 +47,14 @@ def golden_corpus(fx, use_c_synth=True):
     return c["n_docs"], c["vocab"], off, tok, no, nt, dl
 
 
+def golden_facets(fx):
+    """(facet_off, facet_tok, n_fterms) of a fixture with facets, else Nones."""
+    if "facet_tokens" not in fx:
+        return None, None, 0
+    off, tok = tokens_to_csr(fx["facet_tokens"])
+    return off, tok, len(fx["facet_vocab"])
+
+
 def hits_of(scores, docs):
     return [[int(d), int(np.float32(s).view(np.uint32))] for s, d in zip(scores, docs)]
 

@@ -23,6 +23,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
+import facet_ref as fr  # noqa: E402
 import synth_ref as sr  # noqa: E402
 
 _libm = ctypes.CDLL(ctypes.util.find_library("m"))
@@ -94,10 +95,25 @@ class Field:
 
 
 class Index:
-    def __init__(self, n_docs, text, name=None, deleted=None):
+    def __init__(self, n_docs, text, name=None, deleted=None, facets=None):
         self.n = n_docs
         self.f = [Field(n_docs, *text), Field(n_docs, *(name if name else (None, None)))]
         self.deleted = deleted
+        # facet field (schemas.rs:20, Basic record option, no fieldnorms): facets[d] =
+        # FacetTokenizer token ids of doc d, duplicates included (total_num_tokens)
+        self.fpost = {}
+        ftot = 0
+        for d, toks in enumerate(facets or []):
+            ftot += len(toks)
+            for t in toks:
+                self.fpost.setdefault(t, set()).add(d)
+        self.fc1 = cache(F(ftot) / F(n_docs))[1]  # FieldNormReader::constant(max_doc, 1) -> id 1
+
+    def facet_clause(self, t, d):
+        docs = self.fpost.get(t, set())
+        if d not in docs:
+            return None
+        return weight(len(docs), self.n) * (F(1.0) / (F(1.0) + self.fc1))  # tf = 1
 
     def term_score(self, t, d):
         s = F(0.0)
@@ -115,7 +131,9 @@ class Index:
     def cost(self, t):
         return self.f[0].df(t) + self.f[1].df(t)
 
-    def search(self, terms, k, mode):
+    def search(self, terms, k, mode, fterms=None):
+        if fterms or not terms:
+            return self.search_filtered(terms, k, mode, fterms or [])
         if mode == "and":
             order = sorted(range(len(terms)), key=lambda i: (self.cost(terms[i]), i))
             ts = [terms[i] for i in order]
@@ -143,6 +161,47 @@ class Index:
             hits = [h for h in hits if not self.deleted[h[1]]]
         hits.sort(key=lambda h: (-float(h[0]), h[1]))
         return [[int(d), int(np.float32(s).view(np.uint32))] for s, d in hits[:k]]
+
+
+    def search_filtered(self, terms, k, mode, fterms):
+        """Bool[Must(text), Must(facet union)], the facet union alone, or AllQuery
+        (src/db/search.rs:129-150); a union sums its matching clauses from 0.0
+        in clause order, an Intersection of two children is left + right."""
+        text = None
+        if terms:
+            text = dict(self._all_hits(terms, mode))
+        hits = []
+        cand = range(self.n) if text is None else sorted(text)
+        for d in cand:
+            if fterms:
+                fs = F(0.0)
+                any_ = False
+                for t in fterms:
+                    v = self.facet_clause(t, d)
+                    if v is not None:
+                        fs = fs + v
+                        any_ = True
+                if not any_:
+                    continue
+                s = fs if text is None else text[d] + fs
+            else:
+                s = F(1.0)  # AllQuery (text is None here)
+            hits.append((s, d))
+        if self.deleted is not None:
+            hits = [h for h in hits if not self.deleted[h[1]]]
+        hits.sort(key=lambda h: (-float(h[0]), h[1]))
+        return [[int(d), int(np.float32(s).view(np.uint32))] for s, d in hits[:k]]
+
+    def _all_hits(self, terms, mode):
+        # every text match with its score, deletions not applied
+        keep, self.deleted = self.deleted, None
+        try:
+            out = []
+            for d, b in Index.search(self, terms, 1 << 40, mode):
+                out.append((d, F(np.uint32(b).view(np.float32))))
+            return out
+        finally:
+            self.deleted = keep
 
 
 def write(name, obj):
@@ -227,9 +286,64 @@ def edge():
     })
 
 
+MISSING = 0xFFFFFFFF
+
+
+def facets_set(fname, n_docs, vocab, seeds, facet_seed):
+    """Facet filters: text AND / OR + facet clauses, facet-only
+    queries (empty text) and AllQuery, on a corpus with names and deletions."""
+    off, tok = sr.corpus(n_docs, vocab, 1.0, seeds[0], seeds[1])
+    name_cfg = {"vocab": 1 << 9, "seed": 4243}
+    del_cfg = {"seed": 78}
+    name = sr.names(n_docs, **name_cfg)
+    deleted = sr.deleted_mask(n_docs, **del_cfg)
+    paths = sr.facet_paths(n_docs, facet_seed)
+    fvocab, ftoks = {}, []
+    for plist in paths:
+        ids = []
+        for p in plist:
+            enc = fr.from_text(fr.normalize(p))
+            for t in fr.tokens(enc):
+                ids.append(fvocab.setdefault(t, len(fvocab)))
+        ftoks.append(ids)
+    ix = Index(n_docs, (off, tok), name, deleted, ftoks)
+    nfv = len(fvocab)
+    queries = []
+    qo, qt = sr.queries(160, 1, 3, 1 << 9, 1.0, 31)
+    for i in range(160):
+        terms = qt[qo[i]:qo[i + 1]].tolist()
+        h = int(sr.h2(97, i))
+        nfc = 1 + h % 3
+        fterms = [int(sr.h3(98, i, j) % np.uint64(nfv)) for j in range(nfc)]
+        if h % 17 == 0:
+            fterms.append(MISSING)
+        if h % 23 == 0:
+            fterms.append(fterms[0])  # the same facet twice: two clauses
+        kind = (h >> 8) % 8
+        if kind < 4:
+            mode = "and"
+        elif kind < 6:
+            mode = "or" if len(terms) > 1 else "and"
+        else:
+            mode, terms = "and", []  # facet-only (empty text query)
+        k = [10, 10, 100, 1][(h >> 12) % 4]
+        queries.append({"terms": terms, "fterms": fterms, "mode": mode, "k": k,
+                        "hits": ix.search(terms, k, mode, fterms)})
+    for k in (1, 10, 300):
+        queries.append({"terms": [], "fterms": [], "mode": "and", "k": k, "hits": ix.search([], k, "and", [])})
+    write(fname, {
+        "corpus": {"kind": "synth", "n_docs": n_docs, "vocab": vocab, "s": 1.0, "seed_l": seeds[0],
+                   "seed_t": seeds[1], "name": name_cfg, "deleted": del_cfg, "facet_seed": facet_seed},
+        "facet_vocab": list(fvocab),
+        "facet_tokens": ftoks,
+        "queries": queries,
+    })
+
+
 def main():
     kat()
     edge()
+    facets_set("facets_2k.json", 2_000, 1 << 12, (0x5EED3, 101), 555)
     seeds = (0x5EED1, 20250808)
     # config-1 scale (10k docs): 2-term AND (C1), 3-term AND (C2/C3 shape), mixed 1-5, OR
     synth_set("synth_10k.json", 10_000, 1 << 20, 1.0, seeds,

@@ -101,3 +101,32 @@ def names(n_docs: int, vocab: int, seed: int, max_len: int = 3, s: float = 1.0, 
 def deleted_mask(n_docs: int, seed: int, every: int = 7):
     d = np.arange(n_docs, dtype=np.uint64)
     return ((h2(seed, d) % np.uint64(every)) == 0).astype(np.uint8)
+
+
+def facet_paths(n_docs: int, seed: int):
+    """Explicit `facets` of golden corpora (ObjectRecord.facets, src/object.rs:14-16):
+    a namespace facet, data-type / org hierarchy facets, a repeated metadata
+    tag (duplicate tokens), an escaped slash, the root facet, and docs with none."""
+    out = []
+    types = ["doc", "email", "chat", "page"]
+    for d in range(n_docs):
+        h = int(h2(seed, d))
+        if h % 8 == 0:
+            out.append([])
+            continue
+        ns = f"ns{(h >> 3) % 3}"
+        f = [f"/namespace/{ns}"]
+        if (h >> 5) % 10 < 7:
+            f.append(f"/namespace/{ns}/data/{types[(h >> 9) % 4]}")
+        if (h >> 12) % 10 < 4:
+            f.append("/metadata/tags")
+            if (h >> 16) % 2:
+                f.append("/metadata/tags")
+        if (h >> 20) % 10 < 3:
+            f.append(f"org/acme/team{(h >> 24) % 5}/proj{(h >> 28) % 7}")  # no leading '/': normalized
+        if (h >> 32) % 50 == 0:
+            f.append("/a\\/b/c")
+        if (h >> 40) % 100 == 0:
+            f.append("/")
+        out.append(f)
+    return out

@@ -9,7 +9,7 @@ Bit-exact: doc ids and f32 score bits.
 import numpy as np
 import pytest
 
-from conftest import golden_corpus, hits_of, load_golden, tokens_to_csr
+from conftest import golden_corpus, golden_facets, hits_of, load_golden, tokens_to_csr
 from oracle import oracle as orc
 
 
@@ -95,3 +95,27 @@ def test_bytes_model_definition():
     assert b == min(bm, bs) + 1 * 2 + 8 * 2
     bm, bs, b, isz = ix.bytes_model([1], 100)
     assert b == 8 * 3 + 8 * 3 and isz == 3
+
+
+def test_facets_golden():
+    """Facet filters, facet-only queries and AllQuery vs the numpy restatement."""
+    fx = load_golden("facets_2k.json")
+    n, nt, off, tok, no, ntk, dl = golden_corpus(fx)
+    fo, ft, nf = golden_facets(fx)
+    ix = orc.OracleIndex(nt, off, tok, no, ntk, dl, threads=4, facet_off=fo, facet_tok=ft, n_fterms=nf)
+    assert ix.total_tokens(orc.FACET) == len(ft)
+    bad = []
+    for q in fx["queries"]:
+        s, d = ix.search(q["terms"], q["k"], _mode(q["mode"]), q["fterms"])
+        if hits_of(s, d) != q["hits"]:
+            bad.append((q["terms"], q["fterms"]))
+    assert not bad, bad
+    # the batch entry point agrees with single queries
+    qs = [q for q in fx["queries"] if q["mode"] == "and" and q["k"] == 10]
+    q_off = np.cumsum([0] + [len(q["terms"]) for q in qs]).astype(np.uint32)
+    q_terms = np.array([t for q in qs for t in q["terms"]], np.uint32)
+    f_off = np.cumsum([0] + [len(q["fterms"]) for q in qs]).astype(np.uint32)
+    f_terms = np.array([t for q in qs for t in q["fterms"]], np.uint32)
+    sc, dc, cnt, _, _ = ix.search_batch(q_off, q_terms, 10, threads=3, f_off=f_off, f_terms=f_terms)
+    for i, q in enumerate(qs):
+        assert hits_of(sc[i, :cnt[i]], dc[i, :cnt[i]]) == q["hits"]
