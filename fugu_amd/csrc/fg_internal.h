@@ -32,6 +32,10 @@ constexpr uint32_t kDisjMaxGroup = 32;    // ... at most this many tiles per wor
 constexpr uint32_t kNumTopK = 4;          // per-term K-th best scores kept for these K
 constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 100, 1000};
 
+constexpr uint32_t kMaxFacetClauses = 8;  // facet clauses per query (FG_MAX_FACET_CLAUSES)
+constexpr uint32_t kFmaskChunk = 8192;    // facet postings per k_fmask workgroup
+constexpr uint32_t kScanMaxGroup = 32;    // k_scan: at most this many 4096-doc tiles per work item
+
 constexpr uint32_t kModeAnd = 0;
 constexpr uint32_t kModeOr = 1;
 
@@ -63,10 +67,39 @@ struct DevIndex {
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
   const uint32_t* toff;      // [V] first tmax entry of each term, or 0xFFFFFFFF (bucket >= tile: use bmax)
+  const uint32_t* fdoc;      // [PF] facet postings (doc ids, ascending), CSR by facet term
+  const uint64_t* foff;      // [VF+1]
   uint32_t n_docs;
   uint32_t n_terms;
   uint32_t has_name;
+  uint32_t n_fterms;
 };
+
+// Facet filters of a planned batch (DevPlan).  Every distinct clause list
+// (filter) gets a doc-indexed mask in HBM built by k_fmask from the facet
+// postings: 2^shift bits per doc (shift 0..3, >= the filter's clause count),
+// bit i set when the doc holds clause i's facet term.  f_tab[f*256 + bits] is
+// the facet union's score for that set of matching clauses, summed on the
+// host in clause order from 0.0 (SumCombiner), so the kernels add one f32.
+struct DevFilters {
+  uint32_t n_filters;
+  uint32_t n_chunks;            // k_fmask workgroups
+  const uint32_t* q_filter;     // [nq] filter of each query, 0xFFFFFFFF = none
+  const uint32_t* f_shift;      // [n_filters] log2(bits per doc)
+  const uint64_t* f_woff;       // [n_filters] first mask word
+  const float* f_tab;           // [n_filters * 256]
+  const float* f_max;           // [n_filters] largest f_tab entry (upper bound of the facet score)
+  const uint32_t* ch_filter;    // [n_chunks] k_fmask chunk -> filter
+  const uint32_t* ch_clause;    // [n_chunks] clause index in the filter
+  const uint32_t* ch_term;      // [n_chunks] facet term
+  const uint32_t* ch_start;     // [n_chunks] first posting of the chunk within the term's list
+  uint32_t* fmask;              // workspace, zeroed per run
+};
+
+__host__ __device__ inline uint32_t filter_bits(const uint32_t* mask, uint32_t shift, uint32_t d) {
+  const uint32_t bit = d << shift;  // fits: the plan rejects n_docs << shift > 2^32
+  return (mask[bit >> 5] >> (bit & 31)) & ((1u << (1u << shift)) - 1u);
+}
 
 // Device view of one planned batch.  Work items (query, 2048-candidate chunk
 // of the query's lead list) are ordered as a doc sweep across the batch:
@@ -90,6 +123,9 @@ struct DevPlan {
   uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list
   uint64_t* cand_keys;          // [cand_off[nq]] per-query candidate lists
   uint64_t* diag;               // diagnostic builds only (-DFG_DIAG): per-workgroup stamps
+  uint32_t n_scan;              // k_scan work items (queries with no text terms), after the total_chunks
+                                // k_conj / k_disj items in work_q / work_c / work_n
+  DevFilters f;
 };
 
 constexpr uint32_t kDiagPerWg = 16;  // u64 stamps per workgroup in diagnostic builds
@@ -112,6 +148,8 @@ __host__ __device__ inline uint32_t key_doc(uint64_t k) { return 0xFFFFFFFFu - (
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
+hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
+hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,

@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -128,6 +129,12 @@ struct HostPostings {
   std::vector<uint32_t> alive;    // bitset, empty when no deletes
   uint64_t tot[2] = {0, 0};
   bool has_name = false;
+  // facet field: postings (docs only: IndexRecordOption::Basic) per facet term
+  uint32_t n_fterms = 0;
+  std::vector<uint64_t> foff{0};  // [VF+1]
+  std::vector<uint32_t> fdoc;
+  std::vector<uint32_t> df_facet;
+  uint64_t tot_f = 0;             // total_num_tokens(facet), duplicates included
 };
 
 struct DevAllocs {
@@ -163,13 +170,20 @@ struct fg_index {
   std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
   std::vector<float> w_text, w_name;
   std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model
+  // facet field (FG_FIELD_FACET)
+  uint32_t n_fterms = 0;
+  uint64_t tot_f = 0;
+  float avgdl_f = 0.0f, cache_f1 = 0.0f;
+  std::vector<uint64_t> foff;
+  std::vector<uint32_t> df_facet, ffirst, flast;
+  std::vector<float> fscore;    // a facet clause's score in a doc holding the term (tf 1, fieldnorm id 1)
   fg::DevIndex d{};
   DevAllocs mem;
 };
 
 struct fg_plan {
   fg_index* ix = nullptr;
-  uint32_t nq = 0, k = 0, total_chunks = 0;
+  uint32_t nq = 0, k = 0, total_chunks = 0, n_scan = 0;
   int mode = FG_MODE_AND;
   fg::DevPlan d{};
   float* own_score = nullptr;
@@ -352,6 +366,35 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
                     }
                   });
   ix->n_dense = (uint32_t)dense_terms.size();
+  // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
+  // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
+  const uint32_t VF = hp.n_fterms;
+  ix->n_fterms = VF;
+  ix->tot_f = g ? g->tot_facet_tokens : hp.tot_f;
+  if (g && VF) {
+    if (!g->df_facet) return fail(FG_EINVAL, "global statistics lack df_facet for a faceted shard");
+    ix->df_facet.assign(g->df_facet, g->df_facet + VF);
+    for (uint32_t t = 0; t < VF; ++t)
+      if (ix->df_facet[t] < hp.df_facet[t]) return fail(FG_EINVAL, "global facet df of term %u is below this shard's", t);
+  } else {
+    ix->df_facet = hp.df_facet;
+  }
+  ix->fscore.assign(VF, 0.0f);
+  if (ix->tot_f > 0) {
+    float cf[256];
+    ix->avgdl_f = (float)ix->tot_f / (float)Ns;
+    bm25_cache(ix->avgdl_f, cf);
+    ix->cache_f1 = cf[1];
+    for (uint32_t t = 0; t < VF; ++t)
+      ix->fscore[t] = bm25_weight(ix->df_facet[t], Ns) * (1.0f / (1.0f + ix->cache_f1));
+  }
+  ix->ffirst.assign(VF, 0);
+  ix->flast.assign(VF, 0);
+  for (uint32_t t = 0; t < VF; ++t)
+    if (hp.foff[t + 1] > hp.foff[t]) {
+      ix->ffirst[t] = hp.fdoc[hp.foff[t]];
+      ix->flast[t] = hp.fdoc[hp.foff[t + 1] - 1];
+    }
   HIPCHK(hipSetDevice(dev));
   uint64_t bytes = 0;
   int rc;
@@ -379,8 +422,14 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   if ((rc = dev_upload(ix->mem, hp.fn_name.data(), hp.fn_name.size(), &d_fnn, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
   if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
+  uint32_t* d_fdoc;
+  uint64_t* d_foff;
+  if ((rc = dev_upload(ix->mem, hp.fdoc.data(), hp.fdoc.size(), &d_fdoc, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, hp.foff.data(), hp.foff.size(), &d_foff, &bytes))) return rc;
   ix->d = fg::DevIndex{d_doc, d_tf, d_off, d_dir, d_dir_off, d_tmeta, d_dense, d_wt, d_wn, d_fnt, d_fnn, d_alive,
-                       d_cache, d_bmax, d_tmax, d_toff, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u};
+                       d_cache, d_bmax, d_tmax, d_toff, d_fdoc, d_foff, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u,
+                       VF};
+  ix->foff = std::move(hp.foff);
   // per-term doc span (disjunctive plans skip the tiles outside it)
   ix->first_doc.assign(V, 0);
   ix->last_doc.assign(V, 0);
@@ -412,6 +461,67 @@ inline void doc_runs(const uint32_t* tok, uint64_t len, std::vector<uint32_t>& s
     runs.emplace_back(scratch[i], (uint32_t)(j - i));
     i = j;
   }
+}
+
+// Facet postings from per-doc FacetTokenizer tokens (fg_docs_input): each doc
+// once per distinct token (df), every token counted in total_num_tokens.
+int build_facets(const fg_docs_input* in, HostPostings& hp, int T) {
+  hp.n_fterms = 0;
+  hp.foff.assign(1, 0);
+  hp.fdoc.clear();
+  hp.df_facet.clear();
+  hp.tot_f = 0;
+  if (!in->facet_off) return FG_OK;
+  const uint32_t N = in->n_docs, VF = in->n_facet_terms;
+  if (in->facet_off[0] != 0 || (!in->facet_tok && in->facet_off[N] > 0))
+    return fail(FG_EINVAL, "bad facet token arrays");
+  for (uint32_t d = 0; d < N; ++d)
+    if (in->facet_off[d + 1] < in->facet_off[d]) return fail(FG_EINVAL, "facet_off not monotone at doc %u", d);
+  hp.n_fterms = VF;
+  hp.tot_f = in->facet_off[N];
+  std::vector<std::vector<uint32_t>> cnt(T);
+  std::atomic<bool> bad{false};
+  auto runs = [&](uint32_t d, std::vector<uint32_t>& sc) {
+    sc.assign(in->facet_tok + in->facet_off[d], in->facet_tok + in->facet_off[d + 1]);
+    std::sort(sc.begin(), sc.end());
+    sc.erase(std::unique(sc.begin(), sc.end()), sc.end());
+  };
+  parallel_ranges(N, T, [&](int t, uint32_t b, uint32_t e) {
+    cnt[t].assign(VF, 0);
+    std::vector<uint32_t> sc;
+    for (uint32_t d = b; d < e; ++d) {
+      runs(d, sc);
+      for (uint32_t x : sc) {
+        if (x >= VF) { bad = true; return; }
+        cnt[t][x]++;
+      }
+    }
+  });
+  if (bad) return fail(FG_EINVAL, "facet token id >= n_facet_terms");
+  std::vector<std::vector<uint64_t>> cur(T);
+  hp.foff.assign(VF + 1, 0);
+  hp.df_facet.assign(VF, 0);
+  uint64_t acc = 0;
+  for (int t = 0; t < T; ++t) cur[t].assign(VF, 0);
+  for (uint32_t x = 0; x < VF; ++x) {
+    hp.foff[x] = acc;
+    for (int t = 0; t < T; ++t) {
+      if (cnt[t].empty()) continue;
+      cur[t][x] = acc;
+      acc += cnt[t][x];
+      hp.df_facet[x] += cnt[t][x];
+    }
+  }
+  hp.foff[VF] = acc;
+  hp.fdoc.resize(acc);
+  parallel_ranges(N, T, [&](int t, uint32_t b, uint32_t e) {
+    std::vector<uint32_t> sc;
+    for (uint32_t d = b; d < e; ++d) {
+      runs(d, sc);
+      for (uint32_t x : sc) hp.fdoc[cur[t][x]++] = d;
+    }
+  });
+  return FG_OK;
 }
 
 }  // namespace
@@ -504,6 +614,15 @@ int fg_docs_stats(const fg_docs_input* in, uint32_t* df_text, uint32_t* df_name,
     tot_tokens2[0] += tt[t];
     tot_tokens2[1] += tn[t];
   }
+  return FG_OK;
+}
+
+int fg_docs_facet_stats(const fg_docs_input* in, uint32_t* df_facet, uint64_t* tot_facet) {
+  if (!in || !tot_facet || (in->facet_off && in->n_facet_terms && !df_facet)) return fail(FG_EINVAL, "bad arguments");
+  HostPostings hp;
+  if (int rc = build_facets(in, hp, hw_threads(in->threads))) return rc;
+  if (hp.n_fterms) std::copy(hp.df_facet.begin(), hp.df_facet.end(), df_facet);
+  *tot_facet = hp.tot_f;
   return FG_OK;
 }
 
@@ -619,6 +738,7 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
     for (uint32_t t = 0; t < V; ++t)
       if (g->df_text[t] < hp.df_text[t] || (g->df_name ? g->df_name[t] : 0u) < hp.df_name[t])
         return fail(FG_EINVAL, "global df of term %u is below this shard's", t);
+  if (int rc = build_facets(in, hp, T)) return rc;
   return finish_index(dev, hp, in->keep_host_postings != 0, out, g);
 }
 
@@ -659,6 +779,22 @@ int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** ou
     for (uint32_t d = 0; d < N; ++d)
       if (!in->deleted[d]) hp.alive[d >> 5] |= 1u << (d & 31);
   }
+  if (in->facet_term_off) {
+    const uint32_t VF = in->n_facet_terms;
+    hp.n_fterms = VF;
+    hp.foff.assign(in->facet_term_off, in->facet_term_off + VF + 1);
+    if (hp.foff[0] != 0 || (!in->facet_doc && hp.foff[VF] > 0)) return fail(FG_EINVAL, "bad facet postings");
+    hp.fdoc.assign(in->facet_doc, in->facet_doc + hp.foff[VF]);
+    hp.df_facet.assign(VF, 0);
+    for (uint32_t t = 0; t < VF; ++t) {
+      if (hp.foff[t + 1] < hp.foff[t]) return fail(FG_EINVAL, "facet_term_off not monotone at %u", t);
+      for (uint64_t p = hp.foff[t]; p < hp.foff[t + 1]; ++p)
+        if (hp.fdoc[p] >= N || (p > hp.foff[t] && hp.fdoc[p] <= hp.fdoc[p - 1]))
+          return fail(FG_EINVAL, "facet postings of term %u not strictly ascending / in range", t);
+      hp.df_facet[t] = (uint32_t)(hp.foff[t + 1] - hp.foff[t]);
+    }
+    hp.tot_f = in->tot_facet_tokens;
+  }
   return finish_index(dev, hp, true, out);
 }
 
@@ -686,10 +822,13 @@ int fg_index_stats_get(const fg_index* ix, fg_index_stats* o) {
   o->avgdl[1] = ix->avgdl[1];
   o->has_name = ix->has_name;
   o->device = ix->dev;
+  o->n_facet_terms = ix->n_fterms;
+  o->tot_facet_tokens = ix->tot_f;
   return FG_OK;
 }
 
 uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term) {
+  if (ix && field == FG_FIELD_FACET) return term < ix->n_fterms ? ix->df_facet[term] : 0;
   if (!ix || term >= ix->n_terms) return 0;
   if (field == FG_FIELD_TEXT) return ix->df_text[term];
   if (field == FG_FIELD_NAME) return ix->df_name[term];
@@ -712,26 +851,108 @@ int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_nam
 // ---------------------------------------------------------------- planning
 int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out) {
   if (!ix || !q || !out || (q->n_queries && (!q->q_off || !q->terms))) return fail(FG_EINVAL, "bad arguments");
+  if (q->f_off && q->n_queries && !q->f_terms) return fail(FG_EINVAL, "f_off without f_terms");
   if (k < 1) return fail(FG_EINVAL, "k must be >= 1 (TopDocs::with_limit asserts limit >= 1)");
   if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k=%u > FG_MAX_K=%d", k, FG_MAX_K);
   if (q->mode != FG_MODE_AND && q->mode != FG_MODE_OR) return fail(FG_EINVAL, "bad mode %d", q->mode);
   const uint32_t nq = q->n_queries;
+  const uint64_t N = ix->n_docs;
   const bool disj = q->mode == FG_MODE_OR;
   std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), nchunk(nq);
   std::vector<uint64_t> thr0(nq, 0);
-  uint64_t chunks = 0;
+
+  // ---- facet filters: one mask per distinct clause list (fg_internal.h DevFilters)
+  std::vector<uint32_t> q_filter(nq, 0xFFFFFFFFu);
+  std::vector<std::vector<uint32_t>> flist;
+  std::vector<uint8_t> q_nomatch(nq, 0);  // the filter matches no doc: no work items
+  if (q->f_off) {
+    std::map<std::vector<uint32_t>, uint32_t> fid;
+    for (uint32_t i = 0; i < nq; ++i) {
+      const uint32_t b = q->f_off[i], e = q->f_off[i + 1];
+      if (e < b) return fail(FG_EINVAL, "f_off not monotone at query %u", i);
+      if (e == b) continue;
+      if (e - b > fg::kMaxFacetClauses)
+        return fail(FG_EUNSUPPORTED, "query %u has %u facet clauses (> %u)", i, e - b, fg::kMaxFacetClauses);
+      std::vector<uint32_t> c(q->f_terms + b, q->f_terms + e);
+      bool any = false;
+      for (uint32_t t : c) any |= t < ix->n_fterms && ix->df_facet[t] > 0;
+      if (!any) { q_nomatch[i] = 1; continue; }
+      auto it = fid.find(c);
+      if (it == fid.end()) {
+        it = fid.emplace(c, (uint32_t)flist.size()).first;
+        flist.push_back(std::move(c));
+      }
+      q_filter[i] = it->second;
+    }
+  }
+  const uint32_t nf = (uint32_t)flist.size();
+  std::vector<uint32_t> f_shift(nf);
+  std::vector<uint64_t> f_woff(nf + 1, 0);
+  std::vector<float> f_tab((size_t)nf * 256, 0.0f), f_max(nf, 0.0f);
+  std::vector<uint32_t> ch_f, ch_c, ch_t, ch_s;
+  std::vector<uint32_t> f_lo(nf, 0xFFFFFFFFu), f_hi(nf, 0);  // doc span of the filter's postings
+  for (uint32_t f = 0; f < nf; ++f) {
+    const std::vector<uint32_t>& c = flist[f];
+    const uint32_t n = (uint32_t)c.size();
+    const uint32_t sh = n <= 1 ? 0 : n <= 2 ? 1 : n <= 4 ? 2 : 3;
+    if ((N << sh) > (1ull << 32)) return fail(FG_EUNSUPPORTED, "facet mask of %u clauses too large for %llu docs", n,
+                                              (unsigned long long)N);
+    f_shift[f] = sh;
+    f_woff[f + 1] = f_woff[f] + ((((N << sh) + 31) / 32 + 63) & ~63ull);  // 256-B aligned masks
+    // union score of each set of matching clauses: 0.0 + s_i in clause order (SumCombiner)
+    for (uint32_t v = 0; v < (1u << n); ++v) {
+      float sc = 0.0f;
+      for (uint32_t i = 0; i < n; ++i)
+        if ((v >> i) & 1u) sc += c[i] < ix->n_fterms ? ix->fscore[c[i]] : 0.0f;
+      f_tab[(size_t)f * 256 + v] = sc;
+      f_max[f] = std::max(f_max[f], sc);
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t t = c[i];
+      if (t >= ix->n_fterms || ix->df_facet[t] == 0) continue;
+      f_lo[f] = std::min(f_lo[f], ix->ffirst[t]);
+      f_hi[f] = std::max(f_hi[f], ix->flast[t]);
+      const uint64_t df = ix->foff[t + 1] - ix->foff[t];
+      for (uint64_t st = 0; st < df; st += fg::kFmaskChunk) {
+        ch_f.push_back(f);
+        ch_c.push_back(i);
+        ch_t.push_back(t);
+        ch_s.push_back((uint32_t)st);
+      }
+    }
+  }
+  if (f_woff[nf] * 4 > (8ull << 30)) return fail(FG_EUNSUPPORTED, "facet masks of this batch exceed 8 GiB");
+  if (ch_f.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "facet postings of this batch too large");
+
   // work items: each query's chunks (AND) or doc tiles (OR) in ~kGroupsPerQuery
   // groups, ordered as a doc sweep across the batch (a group centred at doc
-  // fraction x runs with the other queries' groups near x), ties by query
+  // fraction x runs with the other queries' groups near x), ties by query.
+  // Queries without text terms (facet-only / AllQuery) scan doc tiles (k_scan).
   struct W { double key; uint32_t q, c, n; };
-  std::vector<W> items;
+  std::vector<W> items, scan;
   std::vector<uint32_t> ngroup(nq, 0);
   for (uint32_t i = 0; i < nq; ++i) {
     const uint32_t b = q->q_off[i], e = q->q_off[i + 1];
     if (e < b) return fail(FG_EINVAL, "q_off not monotone at query %u", i);
     const uint32_t m = e - b;
-    if (m == 0) return fail(FG_EUNSUPPORTED, "query %u is empty (AllQuery runs on the CPU path)", i);
     if (m > fg::kMaxTerms) return fail(FG_EUNSUPPORTED, "query %u has %u terms (> %u)", i, m, fg::kMaxTerms);
+    if (q_nomatch[i]) continue;  // the facet clauses match nothing: no hits
+    if (m == 0) {
+      // empty text query: the facet union alone, or AllQuery (src/db/search.rs:115-116, 131-137)
+      q_m[i] = 0;
+      const uint32_t f = q_filter[i];
+      const uint64_t dlo = f == 0xFFFFFFFFu ? 0 : f_lo[f], dhi = f == 0xFFFFFFFFu ? N - 1 : f_hi[f];
+      const uint32_t tlo = (uint32_t)(dlo >> fg::kDisjTileShift), thi = (uint32_t)(dhi >> fg::kDisjTileShift);
+      const uint32_t nt = thi - tlo + 1;
+      const uint32_t G = std::min<uint32_t>(fg::kScanMaxGroup,
+                                            std::max<uint32_t>(1, (nt + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
+      const uint32_t ng = (nt + G - 1) / G;
+      ngroup[i] = ng;
+      // the groups of all queries in doc order: the first groups publish the
+      // thresholds that let the later ones stop early
+      for (uint32_t g = 0; g < ng; ++g) scan.push_back(W{(double)g, i, tlo + g * G, std::min(G, nt - g * G)});
+      continue;
+    }
     if (disj) {
       // Should clauses in clause order (SumCombiner order); a clause on a term
       // absent from the snapshot matches nothing and is dropped
@@ -745,8 +966,14 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
       }
       q_m[i] = mm;
       if (!mm) continue;
-      // starting threshold: the best per-clause K'-th score for the smallest stored K' >= k
-      for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
+      if (q_filter[i] != 0xFFFFFFFFu) {
+        dlo = std::max(dlo, f_lo[q_filter[i]]);
+        dhi = std::min(dhi, f_hi[q_filter[i]]);
+        if (dlo > dhi) continue;  // the text and facet doc spans do not meet
+      }
+      // starting threshold: the best per-clause K'-th score for the smallest stored
+      // K' >= k (unfiltered only: a filter may remove a term's best docs)
+      for (uint32_t j = 0; j < fg::kNumTopK && q_filter[i] == 0xFFFFFFFFu; ++j) {
         if (fg::kTopKs[j] < k) continue;
         float v = 0.0f;
         for (uint32_t c = 0; c < mm; ++c)
@@ -785,9 +1012,8 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     const uint64_t df0 = missing ? 0 : ix->off[ts[0].term + 1] - ix->off[ts[0].term];
     lead[i] = (uint32_t)df0;
     nchunk[i] = (uint32_t)((df0 + fg::kChunk - 1) / fg::kChunk);
-    chunks += nchunk[i];
-    if (chunks > 0x7FFFFFFFull)
-      return fail(FG_EUNSUPPORTED, "batch too large (%llu work items)", (unsigned long long)chunks);
+    if (items.size() + nchunk[i] > 0x7FFFFFFFull)
+      return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", items.size());
     const uint32_t nch = nchunk[i];
     const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
     const uint32_t ng = (nch + G - 1) / G;
@@ -796,7 +1022,11 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
       items.push_back(W{(g + 0.5) / ng, i, g * G, std::min(G, nch - g * G)});
   }
   std::stable_sort(items.begin(), items.end(), [](const W& a, const W& b) { return a.key < b.key; });
-  chunks = items.size();  // from here on: work items
+  std::stable_sort(scan.begin(), scan.end(), [](const W& a, const W& b) { return a.key < b.key; });
+  const uint64_t n_main = items.size(), n_scan = scan.size();
+  const uint64_t chunks = n_main + n_scan;  // from here on: work items (k_conj / k_disj, then k_scan)
+  if (chunks > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%llu work items)", (unsigned long long)chunks);
+  items.insert(items.end(), scan.begin(), scan.end());
   std::vector<uint32_t> work_q(chunks), work_c(chunks), work_n(chunks);
   std::vector<uint64_t> cand_off(nq + 1, 0);
   for (uint64_t w = 0; w < chunks; ++w) {
@@ -812,14 +1042,17 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->k = k;
   p->mode = q->mode;
   p->total_chunks = (uint32_t)chunks;
+  p->n_scan = (uint32_t)n_scan;
   p->mem.dev = ix->dev;
-  // one allocation: [inputs | zeroed (thresh, cand_cnt) | candidates | outputs]
+  // one allocation: [inputs | zeroed (thresh, cand_cnt, facet masks) | candidates | outputs]
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t nch = ch_f.size();
   const size_t s_qm = al(4ull * nq), s_qt = al(4ull * nq * fg::kMaxTerms), s_lead = al(4ull * nq),
                s_wq = al(4ull * chunks), s_wc = al(4ull * chunks), s_wn = al(4ull * chunks),
-               s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq);
-  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0;
-  const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq);
+               s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq), s_qf = al(4ull * nq), s_fs = al(4ull * nf),
+               s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch);
+  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_qf + s_fs + s_fw + s_ft + s_fm + 4 * s_ch;
+  const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]);
   const size_t s_ck = al(8ull * cand_off[nq]);
   const size_t s_os = al(4ull * nq * k), s_od = al(4ull * nq * k), s_on = al(4ull * nq);
 #ifdef FG_DIAG
@@ -827,7 +1060,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
 #else
   const size_t s_dg = 0;
 #endif
-  const size_t total = s_in + s_thr + s_cc + s_ck + s_os + s_od + s_on + s_dg;
+  const size_t total = s_in + s_thr + s_cc + s_mask + s_ck + s_os + s_od + s_on + s_dg;
   HIPCHK(hipSetDevice(ix->dev));
   char* base = nullptr;
   if (hipMalloc((void**)&base, std::max<size_t>(total, 256)) != hipSuccess)
@@ -850,14 +1083,25 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.work_n = (const uint32_t*)put(work_n.data(), 4ull * chunks, s_wn);
   p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
   p->d.q_thr0 = (const uint64_t*)put(thr0.data(), 8ull * nq, s_t0);
+  p->d.f.q_filter = (const uint32_t*)put(q_filter.data(), 4ull * nq, s_qf);
+  p->d.f.f_shift = (const uint32_t*)put(f_shift.data(), 4ull * nf, s_fs);
+  p->d.f.f_woff = (const uint64_t*)put(f_woff.data(), 8ull * nf, s_fw);
+  p->d.f.f_tab = (const float*)put(f_tab.data(), 4ull * nf * 256, s_ft);
+  p->d.f.f_max = (const float*)put(f_max.data(), 4ull * nf, s_fm);
+  p->d.f.ch_filter = (const uint32_t*)put(ch_f.data(), 4ull * nch, s_ch);
+  p->d.f.ch_clause = (const uint32_t*)put(ch_c.data(), 4ull * nch, s_ch);
+  p->d.f.ch_term = (const uint32_t*)put(ch_t.data(), 4ull * nch, s_ch);
+  p->d.f.ch_start = (const uint32_t*)put(ch_s.data(), 4ull * nch, s_ch);
   HIPCHK(hipMemcpy(base, staging.data(), s_in, hipMemcpyHostToDevice));
   char* cur = base + s_in;
   p->zero_region = cur;
-  p->zero_bytes = s_thr + s_cc;
+  p->zero_bytes = s_thr + s_cc + s_mask;
   p->d.thresh = (uint64_t*)cur;
   cur += s_thr;
   p->d.cand_cnt = (uint32_t*)cur;
   cur += s_cc;
+  p->d.f.fmask = (uint32_t*)cur;
+  cur += s_mask;
   p->d.cand_keys = (uint64_t*)cur;
   cur += s_ck;
   p->own_score = (float*)cur;
@@ -869,9 +1113,12 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.diag = s_dg ? (uint64_t*)cur : nullptr;
   p->diag_words = s_dg / 8;
   p->d.n_queries = nq;
-  p->d.total_chunks = (uint32_t)chunks;
+  p->d.total_chunks = (uint32_t)n_main;
+  p->d.n_scan = (uint32_t)n_scan;
   p->d.k = k;
   p->d.mode = (uint32_t)q->mode;
+  p->d.f.n_filters = nf;
+  p->d.f.n_chunks = (uint32_t)nch;
   fg_index_retain(ix);
   p->ix = ix;
   *out = p.release();
@@ -891,8 +1138,10 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventRecord(ev[0], s));
   }
+  if (p->d.f.n_chunks) HIPCHK(fg::launch_fmask(p->ix->d, p->d, s));
   if (p->mode == FG_MODE_OR) HIPCHK(fg::launch_disj(p->ix->d, p->d, s));
   else HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
+  if (p->d.n_scan) HIPCHK(fg::launch_scan(p->ix->d, p->d, s));
   if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
   HIPCHK(fg::launch_final(p->d, os, od, on, s));
   if (p->profile) {

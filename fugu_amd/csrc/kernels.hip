@@ -300,6 +300,16 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   const uint32_t lead_df = pl.q_lead_df[q];
   const float wt0 = ix.w_text[t0], wn0 = ix.w_name[t0];
   unsigned long long* gthr = reinterpret_cast<unsigned long long*>(&pl.thresh[q]);
+  // facet filter (uniform per work item): Bool[Must(text), Must(facet union)]
+  const uint32_t fslot = pl.f.q_filter[q];
+  const uint32_t* fmask = nullptr;
+  uint32_t fshift = 0;
+  const float* ftab = nullptr;
+  if (fslot != kInvalid) {
+    fmask = pl.f.fmask + pl.f.f_woff[fslot];
+    fshift = pl.f.f_shift[fslot];
+    ftab = pl.f.f_tab + (size_t)fslot * 256;
+  }
   if (tid == 0) {
     sh.n_buf = 0;
     // returning atomic: served at the memory side, so it sees every other
@@ -327,6 +337,12 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       fnp[j] = kInvalid;
       acc_r[j] = 0.0f;
       acc_o[j] = 0.0f;
+    }
+    if (fmask) {
+      // the facet mask first: one L2-resident bit probe drops a candidate before any list probe
+#pragma unroll
+      for (uint32_t j = 0; j < kItems; ++j)
+        if ((live & (1u << j)) && !filter_bits(fmask, fshift, doc[j])) live &= ~(1u << j);
     }
 #if FG_CONJ_PRUNE
     // block-max pruning before any probe: lead score + the other terms' tile /
@@ -431,7 +447,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       if (keep) {
         const float s0 = term_score(tf0[j], fnp[j], wt0, wn0, ix.cache);
         // Intersection::score = left + right + (0.0 + others...); one term = the union itself
-        const float s = m == 1 ? s0 : (s0 + acc_r[j]) + acc_o[j];
+        float s = m == 1 ? s0 : (s0 + acc_r[j]) + acc_o[j];
+        // with a filter: Intersection(text, facet union) = text + facet (two children)
+        if (fmask) s = s + ftab[filter_bits(fmask, fshift, doc[j])];
         key = make_key(s, doc[j]);
         keep = key >= thr;
       }
@@ -571,6 +589,19 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
   uint64_t* gthr = &pl.thresh[q];
+  // facet filter: the union is intersected with the facet union, score = union + facet;
+  // every bound below adds the facet score's maximum fmax
+  const uint32_t fslot = pl.f.q_filter[q];
+  const uint32_t* fmask = nullptr;
+  uint32_t fshift = 0;
+  const float* ftab = nullptr;
+  float fmax = 0.0f;
+  if (fslot != kInvalid) {
+    fmask = pl.f.fmask + pl.f.f_woff[fslot];
+    fshift = pl.f.f_shift[fslot];
+    ftab = pl.f.f_tab + (size_t)fslot * 256;
+    fmax = pl.f.f_max[fslot];
+  }
 #ifdef FG_DIAG
   const uint64_t dg_t0 = FG_NOW();
   uint64_t dg_mode[3] = {0, 0, 0}, dg_post = 0, dg_cand = 0, dg_trunc = 0, dg_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -658,7 +689,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     uint32_t P = 0;
     for (; P < m; ++P) {
       const float s2 = s + ub[ord[P]];
-      if (make_key(inflate_bound(s2), d0) >= thr) break;
+      if (make_key(inflate_bound(s2 + fmax), d0) >= thr) break;
       s = s2;
     }
     uint32_t ess = 0, any = 0;
@@ -712,9 +743,14 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #pragma unroll
       for (uint32_t j = 0; j < kRound / kThreads; ++j) {
         const uint32_t x = r0 + j * kThreads + tid;
-        const float sc = x < span ? sh.u.acc[x] : 0.0f;
+        float sc = x < span ? sh.u.acc[x] : 0.0f;
         uint64_t key = 0;
         bool keep = sc > 0.0f && doc_alive(ix, d0 + x);
+        if (keep && fmask) {
+          const uint32_t fb = filter_bits(fmask, fshift, d0 + x);
+          keep = fb != 0;
+          sc = sc + ftab[fb];
+        }
         if (keep) {
           key = make_key(sc, d0 + x);
           keep = key >= thr;
@@ -776,15 +812,16 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
         const uint64_t bi = sh.c_base[c];
         const uint32_t d = ix.doc[bi + pos];
         const float sc = term_score(ix.tf[bi + pos], load_fn(ix, d), sh.c_wt[c], sh.c_wn[c], ix.cache);
-        // bound 1: the other clauses' tile bounds (LDS)
-        float ub = sc;
+        // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
+        float ub = sc + fmax;
         for (uint32_t i = 0; i < m; ++i)
           if (i != c) ub += sh.r_ub[t * m + i];
         keep = make_key(inflate_bound(ub), d) >= thr;
+        if (keep && fmask) keep = filter_bits(fmask, fshift, d) != 0;
         uint32_t maybe = 0;  // clauses whose bucket at d holds postings (the rest cannot match d)
         if (keep) {
           // bound 2: the other clauses' bucket maxima at d
-          float ub2 = sc;
+          float ub2 = sc + fmax;
           for (uint32_t i = 0; i < m; ++i) {
             if (i == c || sh.r_ub[t * m + i] == 0.0f) continue;
             const float b = ix.bmax[sh.c_dir[i] + (d >> (sh.c_meta[i] & 0xFFu))];
@@ -896,6 +933,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
           }
           // unique keys: keep the doc only from the first essential clause it matches
           const uint32_t first = (uint32_t)__builtin_ctz(matched & sh.t_ess[t]);
+          if (fmask) sc = sc + ftab[filter_bits(fmask, fshift, (uint32_t)(cv >> 32))];
           key = make_key(sc, (uint32_t)(cv >> 32));
           keep = first == src && key >= thr;
         }
@@ -926,6 +964,109 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #undef FG_PHASE
 }
 
+// ---------------------------------------------------------------- k_fmask
+// Facet masks of a batch's filters (DevFilters): one workgroup per 8192
+// postings of one (filter, clause) facet list sets clause bit i of every doc
+// in it.  Postings ascend, so the lanes of a wave mostly hit the same or
+// neighbouring mask words: the atomics coalesce in L2.
+__global__ __launch_bounds__(kThreads) void k_fmask(DevIndex ix, DevPlan pl) {
+  const uint32_t c = blockIdx.x;
+  const uint32_t f = pl.f.ch_filter[c], i = pl.f.ch_clause[c], t = pl.f.ch_term[c], st = pl.f.ch_start[c];
+  const uint64_t b0 = ix.foff[t];
+  const uint32_t n = (uint32_t)(ix.foff[t + 1] - b0);
+  const uint32_t end = min(n, st + kFmaskChunk);
+  const uint32_t sh = pl.f.f_shift[f];
+  uint32_t* mask = pl.f.fmask + pl.f.f_woff[f];
+  for (uint32_t p = st + threadIdx.x; p < end; p += kThreads) {
+    const uint32_t bit = (ix.fdoc[b0 + p] << sh) + i;
+    atomicOr(&mask[bit >> 5], 1u << (bit & 31));
+  }
+}
+
+// ---------------------------------------------------------------- k_scan
+// Queries without text terms (Dataset::search with an empty query,
+// src/db/search.rs:115-116, 129-150): the facet union alone -- score =
+// f_tab[bits] of the doc's matching clauses -- or AllQuery (every alive doc,
+// score 1.0, query/all_query.rs).  A work item scans <= 32 consecutive
+// 4096-doc tiles in doc order through the same local top-k buffer and
+// threshold publication as k_disj.  Keys fall with the doc id at equal score,
+// so once (max score, first doc of a tile) is below the threshold nothing
+// later in the item can enter the top-k and the item stops.
+struct ScanShared {
+  alignas(16) uint64_t buf[kBufD];
+  uint32_t hist[kHistBins];
+  uint32_t scratch[8];
+  uint32_t n_buf;
+  uint64_t thr;
+};
+
+__device__ inline void scan_truncate(ScanShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr, bool publish) {
+  const uint32_t n = sh.n_buf;
+  __syncthreads();
+  uint64_t T = 0;
+  if (n > limit) T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+  if (threadIdx.x == 0) {
+    uint64_t mine = T > sh.thr ? T : sh.thr;
+    if (publish) {
+      const uint64_t old = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)mine);
+      mine = old > mine ? old : mine;
+    }
+    sh.thr = mine;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kThreads) void k_scan(DevIndex ix, DevPlan pl) {
+  __shared__ ScanShared sh;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t w = pl.total_chunks + blockIdx.x;  // scan items follow the k_conj / k_disj items
+  const uint32_t q = pl.work_q[w];
+  const uint32_t tile0 = pl.work_c[w], ntile = pl.work_n[w];
+  const uint32_t K = pl.k;
+  uint64_t* gthr = &pl.thresh[q];
+  const uint32_t fslot = pl.f.q_filter[q];
+  const uint32_t* fmask = nullptr;
+  uint32_t fshift = 0;
+  const float* ftab = nullptr;
+  float smax = 1.0f;  // AllScorer
+  if (fslot != kInvalid) {
+    fmask = pl.f.fmask + pl.f.f_woff[fslot];
+    fshift = pl.f.f_shift[fslot];
+    ftab = pl.f.f_tab + (size_t)fslot * 256;
+    smax = pl.f.f_max[fslot];
+  }
+  if (tid == 0) {
+    sh.n_buf = 0;
+    sh.thr = atomicMax(reinterpret_cast<unsigned long long*>(gthr), 0ull);
+  }
+  __syncthreads();
+  for (uint32_t t = 0; t < ntile; ++t) {
+    const uint32_t d0 = (tile0 + t) << kTileShift;
+    if (d0 >= ix.n_docs || make_key(smax, d0) < sh.thr) break;  // uniform: sh.thr read after a barrier
+    const uint32_t d1 = min(d0 + kTile, ix.n_docs);
+    for (uint32_t r0 = d0; r0 < d1; r0 += kRound) {
+      const uint64_t thr = sh.thr;
+#pragma unroll
+      for (uint32_t j = 0; j < kRound / kThreads; ++j) {
+        const uint32_t d = r0 + j * kThreads + tid;
+        bool keep = d < d1 && doc_alive(ix, d);
+        float sc = 1.0f;
+        if (keep && fmask) {
+          const uint32_t fb = filter_bits(fmask, fshift, d);
+          keep = fb != 0;
+          sc = ftab[fb];
+        }
+        const uint64_t key = keep ? make_key(sc, d) : 0;
+        wave_append(keep && key >= thr, key, sh.buf, &sh.n_buf, kBufD);
+      }
+      __syncthreads();
+      scan_truncate(sh, K, kTrunc, gthr, false);
+    }
+    scan_truncate(sh, K, K, gthr, true);
+  }
+  flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
+}
+
 // ---------------------------------------------------------------- k_final
 // Dynamic LDS (80 KB: 2 workgroups per CU): candidate keys, the k winners,
 // the radix histogram.  Keeps 16-B alignment of the dynamic base (no static
@@ -945,7 +1086,7 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   FinalShared& sh = *reinterpret_cast<FinalShared*>(lds_raw);
   const uint32_t q = blockIdx.x, tid = threadIdx.x;
-  const uint32_t dq = pl.total_chunks + q;
+  const uint32_t dq = pl.total_chunks + pl.n_scan + q;
   (void)dq;
   FG_STAMP(dq, 0, FG_NOW());
   const uint32_t K = pl.k;
@@ -1054,6 +1195,18 @@ hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
 hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   if (pl.total_chunks == 0) return hipSuccess;
   k_disj<<<pl.total_chunks, kThreads, 0, s>>>(ix, pl);
+  return hipGetLastError();
+}
+
+hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
+  if (pl.f.n_chunks == 0) return hipSuccess;
+  k_fmask<<<pl.f.n_chunks, kThreads, 0, s>>>(ix, pl);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
+  if (pl.n_scan == 0) return hipSuccess;
+  k_scan<<<pl.n_scan, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 

@@ -30,10 +30,14 @@ FG_EOOM = -3
 FG_EHIP = -4
 FG_EUNSUPPORTED = -5
 FG_MAX_TERMS = 16
+FG_MAX_FACET_CLAUSES = 8
 FG_MAX_K = 1024
 FG_TERM_MISSING = 0xFFFFFFFF
 MODE_AND = 0
 MODE_OR = 1
+FIELD_TEXT = 0
+FIELD_NAME = 1
+FIELD_FACET = 2
 DIAG_PER_WG = 16  # fg_internal.h kDiagPerWg
 
 # every symbol include/fugu.h declares (checked by tests/test_abi.py)
@@ -44,7 +48,7 @@ EXPORTS = (
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_merge_shards", "fg_bytes_model",
-    "fg_docs_stats", "fg_index_build_from_docs_global",
+    "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -66,27 +70,32 @@ _f64p = C.POINTER(C.c_double)
 class DocsInput(C.Structure):
     _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("text_off", _u64p), ("text_tok", _u32p),
                 ("name_off", _u64p), ("name_tok", _u32p), ("deleted", _u8p), ("threads", C.c_int),
-                ("keep_host_postings", C.c_int)]
+                ("keep_host_postings", C.c_int), ("n_facet_terms", C.c_uint32), ("facet_off", _u64p),
+                ("facet_tok", _u32p)]
 
 
 class IndexInput(C.Structure):
     _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("term_off", _u64p), ("doc", _u32p),
                 ("tf_text", _u16p), ("tf_name", _u16p), ("fn_text", _u8p), ("fn_name", _u8p),
-                ("tot_tokens", C.c_uint64 * 2), ("deleted", _u8p)]
+                ("tot_tokens", C.c_uint64 * 2), ("deleted", _u8p), ("n_facet_terms", C.c_uint32),
+                ("facet_term_off", _u64p), ("facet_doc", _u32p), ("tot_facet_tokens", C.c_uint64)]
 
 
 class GlobalStats(C.Structure):
-    _fields_ = [("n_docs", C.c_uint64), ("tot_tokens", C.c_uint64 * 2), ("df_text", _u32p), ("df_name", _u32p)]
+    _fields_ = [("n_docs", C.c_uint64), ("tot_tokens", C.c_uint64 * 2), ("df_text", _u32p), ("df_name", _u32p),
+                ("df_facet", _u32p), ("tot_facet_tokens", C.c_uint64)]
 
 
 class QueryBatch(C.Structure):
-    _fields_ = [("n_queries", C.c_uint32), ("q_off", _u32p), ("terms", _u32p), ("mode", C.c_int)]
+    _fields_ = [("n_queries", C.c_uint32), ("q_off", _u32p), ("terms", _u32p), ("mode", C.c_int),
+                ("f_off", _u32p), ("f_terms", _u32p)]
 
 
 class IndexStats(C.Structure):
     _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("n_postings", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("tot_tokens", C.c_uint64 * 2), ("avgdl", C.c_float * 2),
-                ("has_name", C.c_int), ("device", C.c_int)]
+                ("has_name", C.c_int), ("device", C.c_int), ("n_facet_terms", C.c_uint32),
+                ("tot_facet_tokens", C.c_uint64)]
 
 
 class PlanInfo(C.Structure):
@@ -109,6 +118,7 @@ _sig("fg_version", C.c_char_p)
 _sig("fg_index_build_from_docs", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(_p))
 _sig("fg_index_build", C.c_int, _p, C.c_int, C.POINTER(IndexInput), C.POINTER(_p))
 _sig("fg_docs_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u32p, _u64p)
+_sig("fg_docs_facet_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u64p)
 _sig("fg_index_build_from_docs_global", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(GlobalStats),
      C.POINTER(_p))
 _sig("fg_index_retain", C.c_int, _p)
@@ -199,6 +209,8 @@ class Stats:
     avgdl: tuple
     has_name: bool
     device: int
+    n_facet_terms: int = 0
+    tot_facet_tokens: int = 0
 
 
 def _u64(a):
@@ -210,16 +222,22 @@ def _u32(a):
 
 
 def _docs_input(text_off, text_tok, n_terms, name_off=None, name_tok=None, deleted=None, threads=0,
-                keep_host=True):
+                keep_host=True, facets=None):
+    """facets: (facet_off, facet_tok, n_facet_terms) or None."""
     text_off = _u64(text_off)
     text_tok = _u32(text_tok)
     name_off = None if name_off is None else _u64(name_off)
     name_tok = None if name_tok is None else _u32(name_tok)
     deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint8)
+    fo = ft = None
+    nft = 0
+    if facets is not None:
+        fo, ft, nft = _u64(facets[0]), _u32(facets[1]), int(facets[2])
     n_docs = len(text_off) - 1
     inp = DocsInput(n_docs, n_terms, _ptr(text_off, _u64p), _ptr(text_tok, _u32p), _ptr(name_off, _u64p),
-                    _ptr(name_tok, _u32p), _ptr(deleted, _u8p), threads, 1 if keep_host else 0)
-    return (text_off, text_tok, name_off, name_tok, deleted), inp
+                    _ptr(name_tok, _u32p), _ptr(deleted, _u8p), threads, 1 if keep_host else 0, nft,
+                    _ptr(fo, _u64p), _ptr(ft, _u32p))
+    return (text_off, text_tok, name_off, name_tok, deleted, fo, ft), inp
 
 
 @dataclass
@@ -229,21 +247,33 @@ class ShardStats:
     tot_tokens: tuple
     df_text: np.ndarray
     df_name: np.ndarray
+    df_facet: "np.ndarray | None" = None
+    tot_facet_tokens: int = 0
 
     def __add__(self, o: "ShardStats") -> "ShardStats":
+        dff = None
+        if self.df_facet is not None or o.df_facet is not None:
+            dff = (self.df_facet if self.df_facet is not None else 0) + (o.df_facet if o.df_facet is not None else 0)
         return ShardStats(self.n_docs + o.n_docs, tuple(a + b for a, b in zip(self.tot_tokens, o.tot_tokens)),
-                          self.df_text + o.df_text, self.df_name + o.df_name)
+                          self.df_text + o.df_text, self.df_name + o.df_name, dff,
+                          self.tot_facet_tokens + o.tot_facet_tokens)
 
 
-def docs_stats(text_off, text_tok, n_terms: int, name_off=None, name_tok=None, threads: int = 0) -> ShardStats:
-    """fg_docs_stats: a shard's local statistics (host only, no device)."""
-    keep, inp = _docs_input(text_off, text_tok, n_terms, name_off, name_tok, None, threads, False)
+def docs_stats(text_off, text_tok, n_terms: int, name_off=None, name_tok=None, threads: int = 0,
+               facets=None) -> ShardStats:
+    """fg_docs_stats (+ fg_docs_facet_stats): a shard's local statistics (host only, no device)."""
+    keep, inp = _docs_input(text_off, text_tok, n_terms, name_off, name_tok, None, threads, False, facets)
     dft = np.zeros(n_terms, np.uint32)
     dfn = np.zeros(n_terms, np.uint32)
     tot = np.zeros(2, np.uint64)
     _check(_lib.fg_docs_stats(C.byref(inp), _ptr(dft, _u32p), _ptr(dfn, _u32p), _ptr(tot, _u64p)))
+    dff = None
+    totf = C.c_uint64(0)
+    if facets is not None:
+        dff = np.zeros(max(int(facets[2]), 1), np.uint32)[: int(facets[2])]
+        _check(_lib.fg_docs_facet_stats(C.byref(inp), _ptr(dff, _u32p), C.byref(totf)))
     del keep
-    return ShardStats(int(inp.n_docs), (int(tot[0]), int(tot[1])), dft, dfn)
+    return ShardStats(int(inp.n_docs), (int(tot[0]), int(tot[1])), dft, dfn, dff, int(totf.value))
 
 
 class Index:
@@ -255,10 +285,12 @@ class Index:
     @classmethod
     def from_docs(cls, ctx: Context, text_off, text_tok, n_terms: int, name_off=None, name_tok=None,
                   deleted=None, device: int | None = None, threads: int = 0, keep_host: bool = True,
-                  global_stats: "ShardStats | None" = None):
+                  global_stats: "ShardStats | None" = None, facets=None):
         """Build a snapshot; `global_stats` (a doc-sharded namespace's summed
-        ShardStats) makes the BM25 statistics global while the postings stay local."""
-        keep, inp = _docs_input(text_off, text_tok, n_terms, name_off, name_tok, deleted, threads, keep_host)
+        ShardStats) makes the BM25 statistics global while the postings stay local.
+        `facets` = (facet_off, facet_tok, n_facet_terms): FacetTokenizer tokens per doc."""
+        keep, inp = _docs_input(text_off, text_tok, n_terms, name_off, name_tok, deleted, threads, keep_host,
+                                facets)
         h = _p()
         dev = ctx.devices[0] if device is None else device
         if global_stats is None:
@@ -266,8 +298,9 @@ class Index:
         else:
             g = global_stats
             dft, dfn = _u32(g.df_text), _u32(g.df_name)
+            dff = None if g.df_facet is None else _u32(g.df_facet)
             gs = GlobalStats(int(g.n_docs), (C.c_uint64 * 2)(*[int(x) for x in g.tot_tokens]), _ptr(dft, _u32p),
-                             _ptr(dfn, _u32p))
+                             _ptr(dfn, _u32p), _ptr(dff, _u32p), int(g.tot_facet_tokens))
             _check(_lib.fg_index_build_from_docs_global(ctx.handle, dev, C.byref(inp), C.byref(gs), C.byref(h)))
         del keep
         return cls(h)
@@ -280,7 +313,7 @@ class Index:
         s = IndexStats()
         _check(_lib.fg_index_stats_get(self._h, C.byref(s)))
         return Stats(s.n_docs, s.n_terms, s.n_postings, s.device_bytes, tuple(s.tot_tokens), tuple(s.avgdl),
-                     bool(s.has_name), s.device)
+                     bool(s.has_name), s.device, s.n_facet_terms, s.tot_facet_tokens)
 
     def df(self, term: int, field: int = -1) -> int:
         return int(_lib.fg_index_df(self._h, field, term))
@@ -291,14 +324,17 @@ class Index:
         _check(_lib.fg_index_bm25(self._h, term, C.byref(wt), C.byref(wn), _ptr(cache, _f32p)))
         return wt.value, wn.value, cache
 
-    def plan(self, q_off, terms, k: int, mode: int = MODE_AND) -> "Plan":
-        return Plan(self, q_off, terms, k, mode)
+    def plan(self, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None) -> "Plan":
+        return Plan(self, q_off, terms, k, mode, f_off, f_terms)
 
-    def search_batch(self, q_off, terms, k: int, mode: int = MODE_AND):
+    def search_batch(self, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None):
+        """f_off / f_terms: per-query facet clauses (facet term ids), or None."""
         q_off = _u32(q_off)
         terms = _u32(terms)
         nq = len(q_off) - 1
-        qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode)
+        f_off = None if f_off is None else _u32(f_off)
+        f_terms = None if f_off is None else _u32(f_terms)
+        qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode, _ptr(f_off, _u32p), _ptr(f_terms, _u32p))
         score = np.zeros(nq * k, np.float32)
         doc = np.zeros(nq * k, np.uint32)
         n = np.zeros(nq, np.uint32)
@@ -329,12 +365,15 @@ class Index:
 class Plan:
     """A batch planned on the host and resident in HBM (fg_plan_create)."""
 
-    def __init__(self, index: Index, q_off, terms, k: int, mode: int = MODE_AND):
+    def __init__(self, index: Index, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None):
         self._q_off = _u32(q_off)
         self._terms = _u32(terms)
+        self._f_off = None if f_off is None else _u32(f_off)
+        self._f_terms = None if f_off is None else _u32(f_terms)
         self.n_queries = len(self._q_off) - 1
         self.k = k
-        qb = QueryBatch(self.n_queries, _ptr(self._q_off, _u32p), _ptr(self._terms, _u32p), mode)
+        qb = QueryBatch(self.n_queries, _ptr(self._q_off, _u32p), _ptr(self._terms, _u32p), mode,
+                        _ptr(self._f_off, _u32p), _ptr(self._f_terms, _u32p))
         h = _p()
         _check(_lib.fg_plan_create(index.handle, C.byref(qb), k, C.byref(h)))
         self._h = h
@@ -362,7 +401,7 @@ class Plan:
         _check(_lib.fg_plan_profile(self._h, 1 if enable else 0))
 
     def kernel_ms(self):
-        """(summed ms of k_conj, k_final over the profiled executes, executes)."""
+        """(summed ms of (k_fmask + k_conj/k_disj + k_scan, k_final) over the profiled executes, executes)."""
         ms = np.zeros(2, np.float64)
         n = C.c_uint32(0)
         _check(_lib.fg_plan_kernel_ms(self._h, _ptr(ms, _f64p), C.byref(n)))

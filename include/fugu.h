@@ -36,6 +36,7 @@ extern "C" {
 #define FG_EUNSUPPORTED (-5)  /* query outside the device subset: the host runs its CPU path */
 
 #define FG_MAX_TERMS 16        /* terms per query on the device path */
+#define FG_MAX_FACET_CLAUSES 8 /* facet filter clauses per query on the device path */
 #define FG_MAX_K 1024          /* largest k on the device path */
 #define FG_TERM_MISSING 0xFFFFFFFFu /* a query term absent from the term dictionary */
 
@@ -44,6 +45,7 @@ extern "C" {
 
 #define FG_FIELD_TEXT 0
 #define FG_FIELD_NAME 1
+#define FG_FIELD_FACET 2 /* the docs index's Facet field (src/db/schemas.rs:20) */
 
 typedef struct fg_ctx fg_ctx;
 typedef struct fg_index fg_index;
@@ -74,6 +76,14 @@ typedef struct fg_docs_input {
   const uint8_t* deleted;    /* [n_docs] 1 = deleted-not-merged, or NULL */
   int threads;               /* host threads for the inversion (<= 0: all) */
   int keep_host_postings;    /* keep a host copy (needed by fg_bytes_model) */
+  /* Facet field (add_facets_to_document, src/db/document.rs:310-330): per doc
+   * the FacetTokenizer tokens of its facets -- for each facet the root, every
+   * ancestor and the facet itself -- as ids < n_facet_terms of the host's
+   * facet dictionary (encoded facet paths).  Duplicates are kept: they count
+   * in total_num_tokens, not in doc_freq.  NULL = no facets. */
+  uint32_t n_facet_terms;
+  const uint64_t* facet_off; /* [n_docs+1] or NULL */
+  const uint32_t* facet_tok;
 } fg_docs_input;
 
 /* Replaces: Index::open_or_create + IndexWriter commit + Searcher snapshot
@@ -94,6 +104,11 @@ typedef struct fg_index_input {
   const uint8_t* fn_name;    /* [n_docs] */
   uint64_t tot_tokens[2];    /* total_num_tokens of text / name, deleted docs included */
   const uint8_t* deleted;    /* [n_docs] or NULL */
+  /* facet postings (doc ids, ascending) per facet term, or NULL */
+  uint32_t n_facet_terms;
+  const uint64_t* facet_term_off; /* [n_facet_terms+1] */
+  const uint32_t* facet_doc;
+  uint64_t tot_facet_tokens;      /* total_num_tokens of the facet field */
 } fg_index_input;
 int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out);
 
@@ -111,10 +126,14 @@ typedef struct fg_global_stats {
   uint64_t tot_tokens[2];    /* total_num_tokens(text), (name) over all shards */
   const uint32_t* df_text;   /* [n_terms] doc_freq in `text` over all shards */
   const uint32_t* df_name;   /* [n_terms] doc_freq in `name`, or NULL (all 0) */
+  const uint32_t* df_facet;  /* [n_facet_terms] doc_freq in `facet`, or NULL (no facets) */
+  uint64_t tot_facet_tokens; /* total_num_tokens(facet) over all shards */
 } fg_global_stats;
 /* Local statistics of one shard (host only, no device): df per term and field
  * ([n_terms] each, caller-owned) and the two token totals. */
 int fg_docs_stats(const fg_docs_input* in, uint32_t* df_text, uint32_t* df_name, uint64_t* tot_tokens2);
+/* ... and of its facet field: df_facet [n_facet_terms], *tot_facet. */
+int fg_docs_facet_stats(const fg_docs_input* in, uint32_t* df_facet, uint64_t* tot_facet);
 /* fg_index_build_from_docs scored with global statistics (g may be NULL = local). */
 int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g,
                                     fg_index** out);
@@ -131,10 +150,12 @@ typedef struct fg_index_stats {
   float avgdl[2];
   int has_name;
   int device;
+  uint32_t n_facet_terms;
+  uint64_t tot_facet_tokens;
 } fg_index_stats;
 int fg_index_stats_get(const fg_index* ix, fg_index_stats* out);
-/* doc_freq of `term` in `field` (tantivy Searcher::doc_freq), and the merged
- * (text U name) posting-list length when field < 0. */
+/* doc_freq of `term` in `field` (tantivy Searcher::doc_freq; FG_FIELD_FACET:
+ * a facet term), and the merged (text U name) posting-list length when field < 0. */
 uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term);
 /* Bm25Weight pieces the device uses, for host-side checks. */
 int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512);
@@ -145,12 +166,22 @@ typedef struct fg_query_batch {
   const uint32_t* q_off;  /* [n_queries+1] */
   const uint32_t* terms;  /* term ids in query order; FG_TERM_MISSING allowed */
   int mode;               /* FG_MODE_AND (Must clauses) or FG_MODE_OR (Should clauses, k_disj) */
+  /* Facet filters (Dataset::search, src/db/search.rs:129-150), or NULL: per
+   * query the flat Should clause list build_facet_query makes (:221-293) --
+   * the exact facet terms in filter order, then the prefix terms -- as facet
+   * term ids (FG_TERM_MISSING allowed: matches nothing), <= FG_MAX_FACET_CLAUSES.
+   *   text terms + clauses : Bool[Must(text query), Must(Should(clauses))],
+   *                          score = text score + facet union score;
+   *   no text  + clauses   : the facet union alone (empty query + filters);
+   *   no text, no clauses  : AllQuery (score 1.0 for every alive doc). */
+  const uint32_t* f_off;  /* [n_queries+1] */
+  const uint32_t* f_terms;
 } fg_query_batch;
 
 /* Plan a batch: host-side query planning (tantivy Weight creation: terms
  * ordered by cost, query/intersection.rs) and upload of the plan to HBM.
- * Returns FG_EUNSUPPORTED for queries outside the device subset (empty query
- * = AllQuery, > FG_MAX_TERMS terms, multi-term OR, k > FG_MAX_K). */
+ * Returns FG_EUNSUPPORTED for queries outside the device subset
+ * (> FG_MAX_TERMS terms, > FG_MAX_FACET_CLAUSES clauses, k > FG_MAX_K). */
 int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out);
 /* Run a planned batch on `stream` (hipStream_t, NULL = default stream).
  * Outputs are device pointers [n_queries*k], [n_queries*k], [n_queries]; NULL
@@ -166,7 +197,8 @@ typedef struct fg_plan_info {
 } fg_plan_info;
 int fg_plan_info_get(const fg_plan* p, fg_plan_info* out);
 /* Per-kernel HIP-event timing of every execute while enabled.  ms_out[2] =
- * summed device time of (k_conj, k_final); *n_out = executes.  Resets. */
+ * summed device time of (k_fmask + k_conj / k_disj + k_scan, k_final);
+ * *n_out = executes.  Resets. */
 int fg_plan_profile(fg_plan* p, int enable);
 int fg_plan_kernel_ms(fg_plan* p, double* ms_out, uint32_t* n_out);
 /* Diagnostics of the last execute: per-query candidate counts (cand_cnt

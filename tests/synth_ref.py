@@ -130,3 +130,47 @@ def facet_paths(n_docs: int, seed: int):
             f.append("/")
         out.append(f)
     return out
+
+
+def facet_vocab():
+    """Facet dictionary of facet_tokens(): encoded facet terms (U+0000 separators)."""
+    v = ["", "namespace"]
+    v += [f"namespace\x00ns{x}" for x in range(3)]
+    v += [f"namespace\x00ns{x}\x00data" for x in range(3)]
+    v += [f"namespace\x00ns{x}\x00data\x00{t}" for x in range(3) for t in ("doc", "email", "chat", "page")]
+    v += ["metadata", "metadata\x00tags", "org", "org\x00acme"]
+    v += [f"org\x00acme\x00team{a}" for a in range(5)]
+    v += [f"org\x00acme\x00team{a}\x00proj{b}" for a in range(5) for b in range(7)]
+    return v
+
+
+def facet_tokens(n_docs: int, seed: int):
+    """Vectorised FacetTokenizer output of facet_paths()-like facets at any scale
+    (ids into facet_vocab()): (facet_off, facet_tok, n_facet_terms)."""
+    d = np.arange(n_docs, dtype=np.uint64)
+    h = h2(seed, d)
+    u = lambda sh, m: ((h >> np.uint64(sh)) % np.uint64(m)).astype(np.int64)  # noqa: E731
+    none = u(0, 8) == 0
+    ns = u(3, 3)
+    has_type = u(5, 10) < 7
+    typ = u(9, 4)
+    tags = u(12, 10) < 4
+    tags2 = tags & (u(16, 2) == 1)
+    org = u(20, 10) < 3
+    team, proj = u(24, 5), u(28, 7)
+    slots = []  # (valid mask, token id) in FacetTokenizer order per facet
+    live = ~none
+    slots += [(live, 0), (live, 1), (live, 2 + ns)]                                 # /namespace/nsX
+    ht = live & has_type
+    slots += [(ht, 0), (ht, 1), (ht, 2 + ns), (ht, 5 + ns), (ht, 8 + 4 * ns + typ)]  # .../data/type
+    for m in (live & tags, live & tags2):
+        slots += [(m, 0), (m, 20), (m, 21)]                                          # /metadata/tags
+    og = live & org
+    slots += [(og, 0), (og, 22), (og, 23), (og, 24 + team), (og, 29 + 7 * team + proj)]
+    valid = np.stack([np.broadcast_to(np.asarray(m), (n_docs,)) for m, _ in slots], axis=1)
+    ids = np.stack([np.broadcast_to(np.asarray(t, np.int64), (n_docs,)) for _, t in slots], axis=1)
+    cnt = valid.sum(axis=1)
+    off = np.zeros(n_docs + 1, np.uint64)
+    off[1:] = np.cumsum(cnt)
+    tok = ids[valid].astype(np.uint32)
+    return off, tok, len(facet_vocab())

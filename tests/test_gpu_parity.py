@@ -8,7 +8,7 @@ contract.
 import numpy as np
 import pytest
 
-from conftest import golden_corpus, hits_of, load_golden, tokens_to_csr
+from conftest import golden_corpus, golden_facets, hits_of, load_golden, tokens_to_csr
 
 pytestmark = pytest.mark.gpu
 
@@ -90,8 +90,11 @@ def test_unsupported_and_invalid(native, ctx):
     fx = load_golden("kat_appendix_c.json")
     n, nt, off, tok, *_ = golden_corpus(fx)
     ix = native.Index.from_docs(ctx, off, tok, nt)
-    with pytest.raises(native.Unsupported):
-        ix.search_batch(np.array([0, 0], np.uint32), np.array([], np.uint32), 10)  # empty query = AllQuery
+    # empty query = AllQuery: every doc, score 1.0, doc ascending (k_scan)
+    s0, d0, n0 = ix.search_batch(np.array([0, 0], np.uint32), np.array([], np.uint32), 10)
+    assert n0[0] == 3 and d0[0, :3].tolist() == [0, 1, 2] and (s0[0, :3] == 1.0).all()
+    with pytest.raises(native.Unsupported):  # more facet clauses than the device subset
+        ix.search_batch(*batch([[0]]), 10, f_off=np.array([0, 9], np.uint32), f_terms=np.zeros(9, np.uint32))
     with pytest.raises(native.FuguError) as e:
         ix.search_batch(*batch([[0]]), 0)
     assert e.value.code == native.FG_EINVAL
@@ -257,3 +260,84 @@ def test_doc_sharded_namespace_equals_single_index(native, ctx, corpus_1m, gpu_1
             for j in bad:  # only swaps between scores equal to ~1 ulp
                 near = np.abs(s1[i, :m].astype(np.float64) - s1[i, j]) <= 1e-6 * s1[i, j]
                 assert gdoc[i, j] in d1[i, :m][near], (i, j)
+
+
+# ---------------------------------------------------------------- facet filters
+def _fbatch(fl):
+    f_off = np.cumsum([0] + [len(f) for f in fl]).astype(np.uint32)
+    f_terms = np.array([t for f in fl for t in f], np.uint32)
+    return f_off, f_terms
+
+
+def test_facets_golden(native, ctx):
+    """Facet clauses with text AND / OR, facet-only queries and AllQuery vs the
+    numpy restatement's fixture (names + deletions), bit-exact."""
+    fx = load_golden("facets_2k.json")
+    n, nt, off, tok, no, ntk, dl = golden_corpus(fx)
+    fo, ft, nf = golden_facets(fx)
+    ix = native.Index.from_docs(ctx, off, tok, nt, no, ntk, dl, facets=(fo, ft, nf))
+    st = ix.stats()
+    assert st.n_facet_terms == nf and st.tot_facet_tokens == len(ft)
+    by = {}
+    for q in fx["queries"]:
+        by.setdefault((q["k"], q["mode"]), []).append(q)
+    checked = 0
+    for (k, mode), qs in by.items():
+        q_off, terms = batch([q["terms"] for q in qs])
+        f_off, f_terms = _fbatch([q["fterms"] for q in qs])
+        s, d, cnt = ix.search_batch(q_off, terms, k, mode=native.MODE_OR if mode == "or" else native.MODE_AND,
+                                    f_off=f_off, f_terms=f_terms)
+        for i, q in enumerate(qs):
+            assert hits_of(s[i, :cnt[i]], d[i, :cnt[i]]) == q["hits"], (q["terms"], q["fterms"])
+            checked += 1
+    assert checked == len(fx["queries"])
+
+
+@pytest.fixture(scope="module")
+def facets_1m():
+    import synth_ref as sr
+    return sr.facet_tokens(1_000_000, 4242)
+
+
+@pytest.fixture(scope="module")
+def gpu_1m_facets(native, ctx, corpus_1m, facets_1m):
+    return native.Index.from_docs(ctx, corpus_1m.off, corpus_1m.tok, 1 << 20, threads=16, facets=facets_1m)
+
+
+@pytest.fixture(scope="module")
+def oracle_1m_facets(corpus_1m, facets_1m):
+    from oracle import oracle as orc
+    fo, ft, nf = facets_1m
+    return orc.OracleIndex(1 << 20, corpus_1m.off, corpus_1m.tok, threads=16, facet_off=fo, facet_tok=ft,
+                           n_fterms=nf)
+
+
+def _clauses(nq, ncl, nf, seed):
+    import synth_ref as sr
+    out = []
+    for i in range(nq):
+        c = [int(sr.h3(seed, i, j) % np.uint64(nf)) for j in range(ncl)]
+        if ncl and int(sr.h2(seed + 1, i)) % 13 == 0:
+            c[-1] = 0xFFFFFFFF  # a clause on a facet absent from the dictionary
+        out.append(c)
+    return out
+
+
+@pytest.mark.parametrize("m_min,m_max,k,mode,ncl", [(3, 3, 100, 0, 1), (1, 5, 10, 0, 3), (2, 4, 100, 1, 2),
+                                                    (0, 0, 100, 0, 1), (0, 0, 10, 0, 4), (0, 0, 100, 0, 0),
+                                                    (2, 3, 1000, 0, 8), (2, 3, 1000, 1, 5)])
+def test_facets_1m_vs_oracle(native, gpu_1m_facets, oracle_1m_facets, facets_1m, m_min, m_max, k, mode, ncl):
+    from fugu_amd import synth
+    nq = 256 if k <= 100 else 64
+    if m_max == 0:
+        q_off, terms = np.zeros(nq + 1, np.uint32), np.zeros(0, np.uint32)
+    else:
+        q_off, terms = synth.queries(nq, m_min, m_max, seed_q=23 + ncl)
+    f_off, f_terms = _fbatch(_clauses(nq, ncl, facets_1m[2], 900 + ncl))
+    s, d, n = gpu_1m_facets.search_batch(q_off, terms, k, mode=mode, f_off=f_off, f_terms=f_terms)
+    rs, rd, rn, _, _ = oracle_1m_facets.search_batch(q_off, terms, k, mode=mode, threads=16, f_off=f_off,
+                                                     f_terms=f_terms)
+    assert np.array_equal(n, rn)
+    for i in range(nq):
+        assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], (i, f_terms[f_off[i]:f_off[i + 1]].tolist()))
+    assert (n > 0).mean() > 0.3
