@@ -850,8 +850,10 @@ int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_nam
 
 // ---------------------------------------------------------------- planning
 int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out) {
-  if (!ix || !q || !out || (q->n_queries && (!q->q_off || !q->terms))) return fail(FG_EINVAL, "bad arguments");
-  if (q->f_off && q->n_queries && !q->f_terms) return fail(FG_EINVAL, "f_off without f_terms");
+  if (!ix || !q || !out || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
+  if (q->n_queries && q->q_off[q->n_queries] > q->q_off[0] && !q->terms) return fail(FG_EINVAL, "q_off without terms");
+  if (q->f_off && q->n_queries && q->f_off[q->n_queries] > q->f_off[0] && !q->f_terms)
+    return fail(FG_EINVAL, "f_off without f_terms");
   if (k < 1) return fail(FG_EINVAL, "k must be >= 1 (TopDocs::with_limit asserts limit >= 1)");
   if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k=%u > FG_MAX_K=%d", k, FG_MAX_K);
   if (q->mode != FG_MODE_AND && q->mode != FG_MODE_OR) return fail(FG_EINVAL, "bad mode %d", q->mode);

@@ -4,6 +4,7 @@
 // reference's Rust toolchain is absent.  Reference citations
 // are on each function.
 #include <algorithm>
+#include <cctype>
 #include <cinttypes>
 #include <cmath>
 #include <cstdio>
@@ -241,6 +242,225 @@ int copy_out(const std::string& s, char* out, size_t cap, size_t* len) {
   return FG_OK;
 }
 
+// ---------------------------------------------------------------- JSON (metadata)
+// ObjectRecord.metadata is Option<HashMap<String, serde_json::Value>>
+// (src/object.rs:11): enough of a JSON reader to walk it.  Object members keep
+// their input order (Rust's HashMap order is unspecified).
+struct JVal {
+  enum Kind { Null, Bool, Num, Str, Arr, Obj } kind = Null;
+  std::string str;                                   // Str
+  std::vector<JVal> arr;                             // Arr
+  std::vector<std::pair<std::string, JVal>> obj;     // Obj
+};
+
+struct JParser {
+  std::string_view s;
+  size_t i = 0;
+  int depth = 0;
+  void ws() { while (i < s.size() && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) ++i; }
+  bool lit(const char* w) {
+    size_t n = std::strlen(w);
+    if (s.substr(i, n) != w) return false;
+    i += n;
+    return true;
+  }
+  bool hex4(uint32_t& v) {
+    if (i + 4 > s.size()) return false;
+    v = 0;
+    for (int k = 0; k < 4; ++k) {
+      char c = s[i++];
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= c - '0';
+      else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+      else return false;
+    }
+    return true;
+  }
+  bool string(std::string& out) {
+    if (i >= s.size() || s[i] != '"') return false;
+    ++i;
+    out.clear();
+    while (i < s.size()) {
+      char c = s[i++];
+      if (c == '"') return true;
+      if ((unsigned char)c < 0x20) return false;
+      if (c != '\\') { out.push_back(c); continue; }
+      if (i >= s.size()) return false;
+      char e = s[i++];
+      switch (e) {
+        case '"': out.push_back('"'); break;
+        case '\\': out.push_back('\\'); break;
+        case '/': out.push_back('/'); break;
+        case 'b': out.push_back('\b'); break;
+        case 'f': out.push_back('\f'); break;
+        case 'n': out.push_back('\n'); break;
+        case 'r': out.push_back('\r'); break;
+        case 't': out.push_back('\t'); break;
+        case 'u': {
+          uint32_t cp;
+          if (!hex4(cp)) return false;
+          if (cp >= 0xD800 && cp < 0xDC00) {
+            uint32_t lo;
+            if (!(lit("\\u") && hex4(lo) && lo >= 0xDC00 && lo < 0xE000)) return false;
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          } else if (cp >= 0xDC00 && cp < 0xE000) {
+            return false;
+          }
+          utf8_put(out, cp);
+          break;
+        }
+        default: return false;
+      }
+    }
+    return false;
+  }
+  bool value(JVal& v) {
+    if (++depth > 128) return false;
+    ws();
+    bool ok = false;
+    if (i >= s.size()) ok = false;
+    else if (s[i] == '{') {
+      v.kind = JVal::Obj;
+      ++i;
+      ws();
+      if (i < s.size() && s[i] == '}') { ++i; ok = true; }
+      else
+        for (;;) {
+          ws();
+          std::string k;
+          JVal x;
+          if (!string(k)) break;
+          ws();
+          if (i >= s.size() || s[i] != ':') break;
+          ++i;
+          if (!value(x)) break;
+          // serde_json into a HashMap: a repeated key keeps the last value
+          auto it = std::find_if(v.obj.begin(), v.obj.end(), [&](auto& m) { return m.first == k; });
+          if (it != v.obj.end()) it->second = std::move(x); else v.obj.emplace_back(std::move(k), std::move(x));
+          ws();
+          if (i < s.size() && s[i] == ',') { ++i; continue; }
+          if (i < s.size() && s[i] == '}') { ++i; ok = true; }
+          break;
+        }
+    } else if (s[i] == '[') {
+      v.kind = JVal::Arr;
+      ++i;
+      ws();
+      if (i < s.size() && s[i] == ']') { ++i; ok = true; }
+      else
+        for (;;) {
+          JVal x;
+          if (!value(x)) break;
+          v.arr.push_back(std::move(x));
+          ws();
+          if (i < s.size() && s[i] == ',') { ++i; continue; }
+          if (i < s.size() && s[i] == ']') { ++i; ok = true; }
+          break;
+        }
+    } else if (s[i] == '"') {
+      v.kind = JVal::Str;
+      ok = string(v.str);
+    } else if (lit("null")) { v.kind = JVal::Null; ok = true; }
+    else if (lit("true") || lit("false")) { v.kind = JVal::Bool; ok = true; }
+    else {
+      size_t b = i;
+      if (i < s.size() && s[i] == '-') ++i;
+      while (i < s.size() && (std::isdigit((unsigned char)s[i]) || s[i] == '.' || s[i] == 'e' || s[i] == 'E' ||
+                              s[i] == '+' || s[i] == '-'))
+        ++i;
+      v.kind = JVal::Num;
+      ok = i > b && std::isdigit((unsigned char)s[i - 1]);
+    }
+    --depth;
+    return ok;
+  }
+};
+
+bool parse_json(std::string_view text, JVal& out) {
+  JParser p{text};
+  if (!p.value(out)) return false;
+  p.ws();
+  return p.i == text.size();
+}
+
+// ---------------------------------------------------------------- facets
+// Facet::from_text (tantivy schema/facet.rs): the path must start with '/';
+// '/' separates segments, stored as U+0000; '\' escapes the next char.
+bool facet_from_text(std::string_view path, std::string& enc) {
+  enc.clear();
+  if (path.empty() || path[0] != '/') return false;
+  bool escaped = false;
+  size_t last = 1;
+  for (size_t i = 1; i < path.size(); ++i) {
+    const char c = path[i];
+    if (escaped) {
+      escaped = false;
+    } else if (c == '\\') {
+      enc.append(path.substr(last, i - last));
+      last = i + 1;
+      escaped = true;
+    } else if (c == '/') {
+      enc.append(path.substr(last, i - last));
+      enc.push_back('\0');
+      last = i + 1;
+    }
+  }
+  enc.append(path.substr(last));
+  return true;
+}
+
+// FacetTokenizer (tokenizer/facet_tokenizer.rs): the root (empty), every
+// prefix ending before a separator after position 0, then the whole facet.
+void facet_tokens(const std::string& enc, std::vector<std::string>& out) {
+  out.clear();
+  out.emplace_back();
+  if (enc.empty()) return;
+  size_t cur = 0;
+  for (;;) {
+    const size_t nxt = enc.find('\0', cur + 1);
+    if (nxt == std::string::npos) {
+      out.push_back(enc);
+      return;
+    }
+    out.push_back(enc.substr(0, nxt));
+    cur = nxt;
+  }
+}
+
+// Facet's Display: '/' + segment per segment, '/' inside a segment as "\/"
+// (convert_doc_to_search_result, src/db/search.rs:563-578)
+std::string facet_display(const std::string& enc) {
+  std::string o;
+  size_t b = 0;
+  for (;;) {
+    const size_t e = enc.find('\0', b);
+    o.push_back('/');
+    for (char c : enc.substr(b, e == std::string::npos ? std::string::npos : e - b)) {
+      if (c == '/') o.push_back('\\');
+      o.push_back(c);
+    }
+    if (e == std::string::npos) return o;
+    b = e + 1;
+  }
+}
+
+std::string normalize_facet_path(std::string_view p) {  // src/db/search.rs:594-600
+  return !p.empty() && p[0] == '/' ? std::string(p) : "/" + std::string(p);
+}
+
+// create_metadata_facets (src/db/utils.rs:11-56): one facet per non-empty
+// string leaf, carrying only the top-level key (get_all_facet_paths takes
+// facet_path.first(), src/db/document.rs:297-306)
+void string_leaves(const JVal& v, size_t& n) {
+  switch (v.kind) {
+    case JVal::Obj: for (auto& m : v.obj) string_leaves(m.second, n); break;
+    case JVal::Arr: for (auto& x : v.arr) string_leaves(x, n); break;
+    case JVal::Str: n += v.str.empty() ? 0 : 1; break;
+    default: break;
+  }
+}
+
 // ---------------------------------------------------------------- datasets
 struct Doc {
   std::string id, text, name, metadata;
@@ -248,6 +468,8 @@ struct Doc {
   bool deleted = false;
   std::vector<uint32_t> text_tok, name_tok;
   std::vector<std::string> id_tokens;
+  std::vector<std::string> facets;   // stored facet values, encoded (Facet), in document order
+  std::vector<uint32_t> facet_tok;   // FacetTokenizer tokens of all of them (facet dictionary ids)
 };
 
 struct Snapshot {
@@ -261,6 +483,7 @@ struct Namespace {
   std::mutex committer;                                // serialises commits (snapshot order)
   std::vector<Doc> docs;                               // global doc id = insertion order
   std::unordered_map<std::string, uint32_t> dict;      // term dictionary (text and name tokens)
+  std::unordered_map<std::string, uint32_t> fdict;     // facet dictionary (encoded facet terms)
   std::unordered_map<std::string, std::vector<uint32_t>> by_id_token;
   std::shared_ptr<Snapshot> snap;                      // committed device snapshot
   std::shared_mutex snap_mu;
@@ -306,20 +529,74 @@ std::vector<uint32_t> intern(Namespace& ns, std::string_view text) {
   return ids;
 }
 
+// build_facet_query's clause list (src/db/search.rs:221-324) for the filters
+// Dataset::search keeps (:98-103: not both starting and ending with '*'):
+// parse_filters normalizes a path with a leading '/', "<path>/*" is a Prefix,
+// "<key>=<value>" an Equals on <key> (the value is dropped), anything else an
+// Equals.  Clauses: Facet::from_text of every Equals path (exact terms, one
+// Should group), then of every Prefix path (one Should TermQuery each).
+// *all_query: the filters are non-empty but no clause parsed (facet_query =
+// AllQuery).  Returns whether facet filtering applies at all.
+bool facet_clauses(const std::vector<std::string>& filters, std::vector<std::string>& clauses, bool* all_query) {
+  clauses.clear();
+  *all_query = false;
+  std::vector<std::string> keep;
+  for (auto& f : filters)
+    if (!(!f.empty() && f.front() == '*' && f.back() == '*')) keep.push_back(f);
+  if (keep.empty()) return false;
+  std::vector<std::string> exact, prefix;
+  for (auto& f : keep) {
+    const std::string n = normalize_facet_path(f);
+    std::string path;
+    bool is_prefix = false;
+    if (n.size() >= 2 && n.compare(n.size() - 2, 2, "/*") == 0) {
+      path = n.substr(0, n.size() - 2);
+      is_prefix = true;
+    } else if (n.find('=') != std::string::npos) {
+      path = n.substr(0, n.find('='));
+    } else {
+      path = n;
+    }
+    std::string enc;
+    if (!facet_from_text(path, enc)) continue;  // `if let Ok(facet) = Facet::from_text(..)`
+    (is_prefix ? prefix : exact).push_back(std::move(enc));
+  }
+  clauses = exact;
+  clauses.insert(clauses.end(), prefix.begin(), prefix.end());
+  *all_query = clauses.empty();
+  return true;
+}
+
+bool blank(std::string_view q) {
+  for (char c : q)
+    if (!(c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v')) return false;
+  return true;
+}
+
 // Dataset::search core: hits of the page in order, or an error code.
-int search_hits(fg_db* db, Namespace& ns, const char* query, uint32_t page, uint32_t per_page,
-                std::vector<fg_hit>& hits) {
+int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<std::string>& filters, uint32_t page,
+                uint32_t per_page, std::vector<fg_hit>& hits) {
+  (void)db;
   hits.clear();
   if (per_page == 0) return hfail(FG_EINVAL, "TopDocs::with_limit requires limit >= 1");
+  const std::string_view qv = query ? query : "";
   int mode = FG_MODE_AND;
   std::vector<std::string> terms;
   std::string why;
-  int rc = parse_query(query ? query : "", &mode, terms, why);
-  if (rc) return hfail(rc, "query outside the device subset: " + why);
+  const bool empty_text = blank(qv);  // query.trim().is_empty() -> AllQuery (src/db/search.rs:115-116)
+  if (!empty_text) {
+    int rc = parse_query(qv, &mode, terms, why);
+    if (rc) return hfail(rc, "query outside the device subset: " + why);
+  }
+  std::vector<std::string> clauses;
+  bool facet_all = false;
+  const bool filtered = facet_clauses(filters, clauses, &facet_all);
+  if (filtered && facet_all && !empty_text)
+    return hfail(FG_EUNSUPPORTED, "query outside the device subset: text query AND an AllQuery facet filter");
   const uint64_t offset = (uint64_t)page * per_page, limit = offset + per_page;
   if (limit > FG_MAX_K) return hfail(FG_EUNSUPPORTED, "offset + per_page > FG_MAX_K");
   std::shared_ptr<Snapshot> snap;
-  std::vector<uint32_t> ids;
+  std::vector<uint32_t> ids, fids;
   {
     std::shared_lock<std::shared_mutex> l(ns.snap_mu);
     snap = ns.snap;
@@ -331,6 +608,10 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, uint32_t page, uint
       auto it = ns.dict.find(t);
       ids.push_back(it == ns.dict.end() ? FG_TERM_MISSING : it->second);
     }
+    for (auto& c : clauses) {
+      auto it = ns.fdict.find(c);
+      fids.push_back(it == ns.fdict.end() ? FG_TERM_MISSING : it->second);
+    }
   }
   if (!snap) return FG_OK;  // nothing committed yet: no hits
   // terms added after the snapshot are unknown to it
@@ -338,15 +619,24 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, uint32_t page, uint
   fg_index_stats_get(snap->ix, &st);
   for (auto& t : ids)
     if (t != FG_TERM_MISSING && t >= st.n_terms) t = FG_TERM_MISSING;
+  for (auto& t : fids)
+    if (t != FG_TERM_MISSING && t >= st.n_facet_terms) t = FG_TERM_MISSING;
   const uint32_t q_off[2] = {0, (uint32_t)ids.size()};
-  fg_query_batch qb{1, q_off, ids.data(), mode};
+  const uint32_t f_off[2] = {0, (uint32_t)fids.size()};
+  fg_query_batch qb{1, q_off, ids.data(), mode, fids.empty() ? nullptr : f_off, fids.data()};
   std::vector<float> sc(limit);
   std::vector<uint32_t> dc(limit);
   uint32_t n = 0;
-  rc = fg_search_batch(snap->ix, &qb, (uint32_t)limit, sc.data(), dc.data(), &n);
+  int rc = fg_search_batch(snap->ix, &qb, (uint32_t)limit, sc.data(), dc.data(), &n);
   if (rc) return hfail(rc, fg_last_error());
   for (uint64_t i = offset; i < n; ++i) hits.push_back(fg_hit{sc[i], dc[i]});  // skip(offset).take(per_page)
   return FG_OK;
+}
+
+std::vector<std::string> filter_list(const char* const* filters, uint32_t n) {
+  std::vector<std::string> v;
+  for (uint32_t i = 0; i < n; ++i) v.emplace_back(filters && filters[i] ? filters[i] : "");
+  return v;
 }
 
 }  // namespace
@@ -405,22 +695,93 @@ int fg_db_namespaces_json(fg_db* db, char* out, size_t cap, size_t* len) {
   return copy_out(o, out, cap, len);
 }
 
-int fg_db_upsert(fg_db* db, const char* nsname, const char* id, const char* text, const char* name,
-                 const char* metadata_json) {
-  if (!db) return hfail(FG_EINVAL, "bad arguments");
+}  // extern "C"
+
+namespace {
+
+std::vector<uint32_t> intern_facet(Namespace& ns, const std::vector<std::string>& enc) {
+  std::vector<uint32_t> ids;
+  std::vector<std::string> toks;
+  for (auto& e : enc) {
+    facet_tokens(e, toks);
+    for (auto& t : toks) {
+      auto it = ns.fdict.find(t);
+      if (it == ns.fdict.end()) it = ns.fdict.emplace(t, (uint32_t)ns.fdict.size()).first;
+      ids.push_back(it->second);
+    }
+  }
+  return ids;
+}
+
+// NamedIndex::upsert of one ObjectRecord into the docs index
+// (src/db/document.rs:23-67, build_full_document :116-184).  name_override:
+// the legacy fg_db_upsert entry passes the `name` value directly.
+int upsert_record(fg_db* db, const char* nsname, const fg_object_record* r, const char* name_override,
+                  bool legacy) {
+  if (!db || !r) return hfail(FG_EINVAL, "bad arguments");
   auto ns = find_ns(db, nsname);
   if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
   // ObjectRecord::validate (src/object.rs:31-78)
-  const std::string sid = id ? id : "", stext = text ? text : "";
+  const std::string sid = r->id ? r->id : "", stext = r->text ? r->text : "";
   if (sid.empty()) return hfail(FG_EINVAL, "Object ID cannot be empty");
   if (sid.size() > 256) return hfail(FG_EINVAL, "Object ID too long (max 256 characters)");
   if (stext.empty()) return hfail(FG_EINVAL, "Object text cannot be empty");
   if (stext.size() > 10000) return hfail(FG_EINVAL, "Text too long (max 10000 characters)");
-  if (nsname) {
-    std::string_view n(nsname);
+  const char* rns = legacy ? nsname : r->namespace_;
+  if (rns) {
+    std::string_view n(rns);
     if (n.empty() || n.find('/') != std::string_view::npos || n.find(' ') != std::string_view::npos)
       return hfail(FG_EINVAL, "Invalid namespace format");
     if (n.size() > 128) return hfail(FG_EINVAL, "Namespace too long (max 128 characters)");
+  }
+  if (r->has_facets) {
+    if (r->n_facets > 100) return hfail(FG_EINVAL, "Too many facets (max 100 per object)");
+    for (uint32_t i = 0; i < r->n_facets; ++i) {
+      const size_t len = r->facets[i] ? std::strlen(r->facets[i]) : 0;
+      if (!len) return hfail(FG_EINVAL, "Facet at index " + std::to_string(i) + " cannot be empty");
+      if (len > 512) return hfail(FG_EINVAL, "Facet at index " + std::to_string(i) + " too long (max 512 characters)");
+    }
+  }
+  JVal meta;
+  const bool has_meta = r->metadata_json != nullptr;
+  if (has_meta && (!parse_json(r->metadata_json, meta) || meta.kind != JVal::Obj))
+    return hfail(FG_EINVAL, "metadata must be a JSON object");
+  Doc doc;
+  doc.id = sid;
+  doc.text = stext;
+  if (has_meta) doc.metadata = r->metadata_json;
+  if (name_override) {
+    doc.has_name = true;
+    doc.name = name_override;
+  } else if (has_meta) {
+    // metadata["name"] when it is a string (build_full_document, document.rs:131-139)
+    for (auto& m : meta.obj)
+      if (m.first == "name" && m.second.kind == JVal::Str) { doc.has_name = true; doc.name = m.second.str; }
+  }
+  // get_all_facet_paths (document.rs:277-309): explicit facets, else the
+  // namespace facets (object.rs:81-111) then the metadata facets
+  std::vector<std::string> paths;
+  if (r->has_facets) {
+    for (uint32_t i = 0; i < r->n_facets; ++i) paths.push_back(normalize_facet_path(r->facets[i]));
+  } else {
+    if (r->namespace_ && !legacy) {
+      const std::string base = std::string("/namespace/") + r->namespace_;
+      paths.push_back(base);
+      if (r->organization) paths.push_back(base + "/organization/" + r->organization);
+      if (r->conversation_id) paths.push_back(base + "/conversation/" + r->conversation_id);
+      if (r->data_type) paths.push_back(base + "/data/" + r->data_type);
+    }
+    if (has_meta)
+      for (auto& m : meta.obj) {
+        size_t n = 0;
+        string_leaves(m.second, n);
+        const std::string path = !m.first.empty() && m.first[0] == '/' ? m.first : "/metadata/" + m.first;
+        for (size_t j = 0; j < n; ++j) paths.push_back(path);
+      }
+  }
+  for (auto& pth : paths) {
+    std::string enc;
+    if (facet_from_text(pth, enc)) doc.facets.push_back(std::move(enc));  // add_facets_to_document skips failures
   }
   std::lock_guard<std::mutex> w(ns->writer);
   // w.delete_term(Term::from_field_text(id_field, &object.id)) (src/db/document.rs:38-42): the
@@ -429,19 +790,31 @@ int fg_db_upsert(fg_db* db, const char* nsname, const char* id, const char* text
   auto it = ns->by_id_token.find(sid);
   if (it != ns->by_id_token.end())
     for (uint32_t d : it->second) ns->docs[d].deleted = true;
-  Doc doc;
-  doc.id = sid;
-  doc.text = stext;
-  doc.has_name = name != nullptr;
-  if (name) doc.name = name;
-  if (metadata_json) doc.metadata = metadata_json;
   doc.text_tok = intern(*ns, doc.text);
   if (doc.has_name) doc.name_tok = intern(*ns, doc.name);
+  doc.facet_tok = intern_facet(*ns, doc.facets);
   analyze(doc.id, doc.id_tokens);
   const uint32_t d = (uint32_t)ns->docs.size();
   for (auto& t : doc.id_tokens) ns->by_id_token[t].push_back(d);
   ns->docs.push_back(std::move(doc));
   return FG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fg_db_upsert(fg_db* db, const char* nsname, const char* id, const char* text, const char* name,
+                 const char* metadata_json) {
+  fg_object_record r{};
+  r.id = id;
+  r.text = text;
+  r.metadata_json = metadata_json;
+  return upsert_record(db, nsname, &r, name, true);
+}
+
+int fg_db_upsert_record(fg_db* db, const char* nsname, const fg_object_record* rec) {
+  return upsert_record(db, nsname, rec, nullptr, false);
 }
 
 int fg_db_commit(fg_db* db, const char* nsname) {
@@ -456,16 +829,19 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   if (ns->docs.empty()) return FG_OK;
   const uint32_t N = (uint32_t)ns->docs.size();
   const uint32_t n_terms = std::max<uint32_t>(1, (uint32_t)ns->dict.size());
-  std::vector<uint64_t> toff(N + 1, 0), noff(N + 1, 0);
-  std::vector<uint32_t> ttok, ntok;
+  const uint32_t n_fterms = (uint32_t)ns->fdict.size();
+  std::vector<uint64_t> toff(N + 1, 0), noff(N + 1, 0), foff(N + 1, 0);
+  std::vector<uint32_t> ttok, ntok, ftok;
   std::vector<uint8_t> del(N, 0);
   bool any_name = false, any_del = false;
   for (uint32_t d = 0; d < N; ++d) {
     const Doc& doc = ns->docs[d];
     ttok.insert(ttok.end(), doc.text_tok.begin(), doc.text_tok.end());
     ntok.insert(ntok.end(), doc.name_tok.begin(), doc.name_tok.end());
+    ftok.insert(ftok.end(), doc.facet_tok.begin(), doc.facet_tok.end());
     toff[d + 1] = ttok.size();
     noff[d + 1] = ntok.size();
+    foff[d + 1] = ftok.size();
     any_name |= !doc.name_tok.empty();
     del[d] = doc.deleted ? 1 : 0;
     any_del |= doc.deleted;
@@ -481,6 +857,9 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   in.deleted = any_del ? del.data() : nullptr;
   in.threads = 0;
   in.keep_host_postings = 0;
+  in.n_facet_terms = n_fterms;
+  in.facet_off = n_fterms ? foff.data() : nullptr;
+  in.facet_tok = n_fterms ? ftok.data() : nullptr;
   fg_index* ix = nullptr;
   int rc = fg_index_build_from_docs(db->ctx, db->dev, &in, &ix);
   if (rc) return hfail(rc, fg_last_error());
@@ -502,7 +881,12 @@ int fg_db_add_file(fg_db* db, const char* ns, const char* name, const char* body
   std::string meta = "{\"name\":";
   json_str(meta, name);
   meta += "}";
-  int rc = fg_db_upsert(db, ns, name, body, name, meta.c_str());
+  fg_object_record r{};
+  r.id = name;
+  r.text = body;
+  r.metadata_json = meta.c_str();
+  r.namespace_ = ns;
+  int rc = fg_db_upsert_record(db, ns, &r);
   if (rc) return rc;
   return fg_db_commit(db, ns);
 }
@@ -518,23 +902,30 @@ int fg_db_doc_count(fg_db* db, const char* nsname, uint64_t* total, uint64_t* al
   return FG_OK;
 }
 
-int fg_db_search(fg_db* db, const char* nsname, const char* query, uint32_t page, uint32_t per_page, fg_hit* out,
-                 uint32_t cap, uint32_t* n_out) {
+int fg_db_search_ex(fg_db* db, const char* nsname, const char* query, const char* const* filters, uint32_t n_filters,
+                    uint32_t page, uint32_t per_page, fg_hit* out, uint32_t cap, uint32_t* n_out) {
   if (!db || !n_out) return hfail(FG_EINVAL, "bad arguments");
   auto ns = find_ns(db, nsname);
   if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
   std::vector<fg_hit> hits;
-  int rc = search_hits(db, *ns, query, page, per_page, hits);
+  int rc = search_hits(db, *ns, query, filter_list(filters, n_filters), page, per_page, hits);
   if (rc) return rc;
   *n_out = (uint32_t)std::min<size_t>(hits.size(), cap);
   if (out) std::copy(hits.begin(), hits.begin() + *n_out, out);
   return FG_OK;
 }
 
-int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t page, uint32_t per_page,
-                      int include_text, int shape, char* out, size_t cap, size_t* len) {
+int fg_db_search(fg_db* db, const char* nsname, const char* query, uint32_t page, uint32_t per_page, fg_hit* out,
+                 uint32_t cap, uint32_t* n_out) {
+  return fg_db_search_ex(db, nsname, query, nullptr, 0, page, per_page, out, cap, n_out);
+}
+
+int fg_db_search_json_ex(fg_db* db, const char* nsname, const char* query, const char* const* filters,
+                         uint32_t n_filters, uint32_t page, uint32_t per_page, int include_text, int shape, char* out,
+                         size_t cap, size_t* len) {
   if (!db) return hfail(FG_EINVAL, "bad arguments");
   const std::string q = query ? query : "";
+  const std::vector<std::string> fl = filter_list(filters, n_filters);
   // perform_search (src/server/handlers/search.rs:350-402): namespace lookup, then
   // per_page 0 or > 100 -> 20; the POST /search shape has no clamp (:183)
   auto ns = find_ns(db, nsname);
@@ -547,7 +938,7 @@ int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t
   }
   if (shape == FG_SHAPE_GET_SEARCH && (per_page == 0 || per_page > 100)) per_page = 20;
   std::vector<fg_hit> hits;
-  int rc = search_hits(db, *ns, q.c_str(), page, per_page, hits);
+  int rc = search_hits(db, *ns, q.c_str(), fl, page, per_page, hits);
   if (rc) {
     std::string o = "{\"error\":";
     json_str(o, std::string("Search failed: ") + fg_last_error());
@@ -561,7 +952,7 @@ int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t
     for (size_t i = 0; i < hits.size(); ++i) {
       const Doc& d = ns->docs[hits[i].doc];
       if (i) res.push_back(',');
-      // FuguSearchResult {id, score, text, metadata, facets} (src/db/search.rs:20-27)
+      // FuguSearchResult {id, score, text, metadata, facets} (src/db/search.rs:20-27, 534-590)
       res += "{\"id\":";
       json_str(res, d.id);
       res += ",\"score\":";
@@ -572,7 +963,18 @@ int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t
       }
       res += ",\"metadata\":";
       res += d.metadata.empty() ? "null" : d.metadata;
-      res += ",\"facets\":null}";
+      res += ",\"facets\":";
+      if (d.facets.empty()) {
+        res += "null";
+      } else {
+        res.push_back('[');
+        for (size_t j = 0; j < d.facets.size(); ++j) {
+          if (j) res.push_back(',');
+          json_str(res, facet_display(d.facets[j]));
+        }
+        res.push_back(']');
+      }
+      res += "}";
     }
   }
   res += "]";
@@ -582,7 +984,12 @@ int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t
     // search_endpoint (src/server/handlers/search.rs:184-195)
     o = "{\"status\":\"success\",\"query\":";
     json_str(o, q);
-    o += ",\"filters\":[]";
+    o += ",\"filters\":[";
+    for (size_t j = 0; j < fl.size(); ++j) {
+      if (j) o.push_back(',');
+      json_str(o, fl[j]);
+    }
+    o += "]";
     snprintf(num, sizeof num, ",\"page\":%u,\"per_page\":%u,\"total\":%zu", page, per_page, hits.size());
     o += num;
     o += ",\"results\":" + res + "}";
@@ -596,6 +1003,64 @@ int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t
     o += "}";
   }
   return copy_out(o, out, cap, len);
+}
+
+int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t page, uint32_t per_page,
+                      int include_text, int shape, char* out, size_t cap, size_t* len) {
+  return fg_db_search_json_ex(db, nsname, query, nullptr, 0, page, per_page, include_text, shape, out, cap, len);
+}
+
+int fg_db_doc_facets(fg_db* db, const char* nsname, uint32_t doc, char* out, size_t cap, size_t* len) {
+  if (!db) return hfail(FG_EINVAL, "bad arguments");
+  auto ns = find_ns(db, nsname);
+  if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
+  std::lock_guard<std::mutex> w(ns->writer);
+  if (doc >= ns->docs.size()) return hfail(FG_EINVAL, "doc out of range");
+  std::string o;
+  for (size_t j = 0; j < ns->docs[doc].facets.size(); ++j) {
+    if (j) o.push_back('\n');
+    o += facet_display(ns->docs[doc].facets[j]);
+  }
+  return copy_out(o, out, cap, len);
+}
+
+int fg_facet_tokens(const char* path, char* out, size_t cap, size_t* len) {
+  if (!path) return hfail(FG_EINVAL, "bad arguments");
+  std::string enc;
+  if (!facet_from_text(path, enc)) return hfail(FG_EINVAL, "Facet::from_text: path must start with '/'");
+  std::vector<std::string> toks;
+  facet_tokens(enc, toks);
+  std::string o;
+  for (size_t i = 0; i < toks.size(); ++i) {
+    if (i) o.push_back('\n');
+    o += toks[i];  // U+0000 separators kept: read *len bytes
+  }
+  if (len) *len = o.size();
+  if (!out) return FG_OK;
+  if (cap < o.size() + 1) return hfail(FG_EINVAL, "output buffer too small");
+  std::memcpy(out, o.data(), o.size());
+  out[o.size()] = 0;
+  return FG_OK;
+}
+
+int fg_facet_clauses(const char* const* filters, uint32_t n_filters, int* applies, int* all_query, char* out,
+                     size_t cap, size_t* len) {
+  if (!applies || !all_query) return hfail(FG_EINVAL, "bad arguments");
+  std::vector<std::string> cl;
+  bool all = false;
+  *applies = facet_clauses(filter_list(filters, n_filters), cl, &all) ? 1 : 0;
+  *all_query = all ? 1 : 0;
+  std::string o;
+  for (size_t i = 0; i < cl.size(); ++i) {
+    if (i) o.push_back('\n');
+    o += cl[i];
+  }
+  if (len) *len = o.size();
+  if (!out) return FG_OK;
+  if (cap < o.size() + 1) return hfail(FG_EINVAL, "output buffer too small");
+  std::memcpy(out, o.data(), o.size());
+  out[o.size()] = 0;
+  return FG_OK;
 }
 
 int fg_analyze(const char* text, char* out, size_t cap, size_t* len) {

@@ -25,6 +25,8 @@ HOST_EXPORTS = (
     "fg_db_create", "fg_db_destroy", "fg_db_namespace_create", "fg_db_namespace_delete",
     "fg_db_namespaces_json", "fg_db_upsert", "fg_db_commit", "fg_db_add_file", "fg_db_doc_count",
     "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query",
+    "fg_db_upsert_record", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
+    "fg_facet_clauses",
 )
 
 _lib = native.lib()
@@ -35,6 +37,12 @@ _sz = C.c_size_t
 
 class Hit(C.Structure):
     _fields_ = [("score", C.c_float), ("doc", C.c_uint32)]
+
+
+class _Record(C.Structure):
+    _fields_ = [("id", _s), ("text", _s), ("metadata_json", _s), ("namespace_", _s), ("organization", _s),
+                ("conversation_id", _s), ("data_type", _s), ("facets", C.POINTER(_s)), ("n_facets", C.c_uint32),
+                ("has_facets", C.c_int)]
 
 
 def _sig(name, *args):
@@ -54,6 +62,14 @@ _sig("fg_db_add_file", _p, _s, _s, _s)
 _sig("fg_db_doc_count", _p, _s, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
 _sig("fg_db_search", _p, _s, _s, C.c_uint32, C.c_uint32, C.POINTER(Hit), C.c_uint32, C.POINTER(C.c_uint32))
 _sig("fg_db_search_json", _p, _s, _s, C.c_uint32, C.c_uint32, C.c_int, C.c_int, _s, _sz, C.POINTER(_sz))
+_sig("fg_db_upsert_record", _p, _s, C.POINTER(_Record))
+_sig("fg_db_search_ex", _p, _s, _s, C.POINTER(_s), C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(Hit), C.c_uint32,
+     C.POINTER(C.c_uint32))
+_sig("fg_db_search_json_ex", _p, _s, _s, C.POINTER(_s), C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, _s,
+     _sz, C.POINTER(_sz))
+_sig("fg_db_doc_facets", _p, _s, C.c_uint32, _s, _sz, C.POINTER(_sz))
+_sig("fg_facet_tokens", _s, _s, _sz, C.POINTER(_sz))
+_sig("fg_facet_clauses", C.POINTER(_s), C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
 _sig("fg_analyze", _s, _s, _sz, C.POINTER(_sz))
 _sig("fg_parse_query", _s, C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
 
@@ -91,6 +107,27 @@ def _string_call(fn, *args, cap: int = 1 << 16) -> str:
         return buf.raw[:n.value].decode()
 
 
+def _strs(items):
+    """(char** array, keep-alive) for a list of str."""
+    items = list(items or [])
+    arr = (_s * max(1, len(items)))(*[x.encode() for x in items])
+    return arr, len(items)
+
+
+def facet_tokens(path: str) -> list:
+    """FacetTokenizer tokens of Facet::from_text(path) (encoded, U+0000 separators)."""
+    out = _string_call(_lib.fg_facet_tokens, path.encode())
+    return out.split("\n")
+
+
+def facet_clauses(filters):
+    """(applies, all_query, clauses) of build_facet_query for `filters`."""
+    arr, n = _strs(filters)
+    a, al = C.c_int(0), C.c_int(0)
+    out = _string_call(_lib.fg_facet_clauses, arr, n, C.byref(a), C.byref(al))
+    return bool(a.value), bool(al.value), (out.split("\n") if (a.value and not al.value) else [])
+
+
 def analyze(text: str) -> list:
     """The "default" analyzer: SimpleTokenizer -> RemoveLongFilter(40) -> LowerCaser."""
     out = _string_call(_lib.fg_analyze, text.encode())
@@ -106,11 +143,16 @@ def parse_query(query: str):
 
 @dataclass
 class ObjectRecord:
-    """src/object.rs: id, text, optional namespace, optional metadata (JSON object)."""
+    """src/object.rs:8-27: id, text, metadata (JSON object), namespace, explicit
+    facets, and the organization / conversation / data-type namespace facets."""
     id: str
     text: str
     namespace: Optional[str] = None
     metadata: Optional[dict] = None
+    facets: Optional[list] = None
+    organization: Optional[str] = None
+    conversation_id: Optional[str] = None
+    data_type: Optional[str] = None
 
 
 class Database:
@@ -149,13 +191,21 @@ class Database:
 
     # -- ingest (NamedIndex::upsert, src/db/document.rs) --
     def upsert(self, obj: ObjectRecord, namespace: Optional[str] = None):
+        """Into `namespace` (default: obj.namespace, else the default namespace).  A record
+        without its own namespace carries the target one, as POST /add/{namespace} does
+        (ObjectRecord.namespace = namespace, cli.rs:392-397)."""
         ns = namespace if namespace is not None else obj.namespace
-        name = None
-        if obj.metadata is not None and isinstance(obj.metadata.get("name"), str):
-            name = obj.metadata["name"]
+        rec_ns = obj.namespace if obj.namespace is not None else namespace
         meta = json.dumps(obj.metadata, separators=(",", ":"), ensure_ascii=False) if obj.metadata is not None \
             else None
-        _check(_lib.fg_db_upsert(self._h, _b(ns), _b(obj.id), _b(obj.text), _b(name), _b(meta)))
+        farr, nf = _strs(obj.facets)
+        r = _Record(_b(obj.id), _b(obj.text), _b(meta), _b(rec_ns), _b(obj.organization),
+                    _b(obj.conversation_id), _b(obj.data_type), farr, nf, 1 if obj.facets is not None else 0)
+        _check(_lib.fg_db_upsert_record(self._h, _b(ns), C.byref(r)))
+
+    def doc_facets(self, namespace: Optional[str], doc: int) -> list:
+        out = _string_call(_lib.fg_db_doc_facets, self._h, _b(namespace), doc)
+        return out.split("\n") if out else []
 
     def commit(self, namespace: Optional[str] = None):
         _check(_lib.fg_db_commit(self._h, _b(namespace)))
@@ -169,15 +219,17 @@ class Database:
         return t.value, a.value
 
     # -- search (Dataset::search / perform_search) --
-    def search(self, namespace: Optional[str], query: str, page: int = 0, per_page: int = 20):
+    def search(self, namespace: Optional[str], query: str, page: int = 0, per_page: int = 20, filters=None):
         """[(score, doc)] of one page; doc = global insertion-order id."""
         out = (Hit * max(1, per_page))()
         n = C.c_uint32(0)
-        _check(_lib.fg_db_search(self._h, _b(namespace), query.encode(), page, per_page, out, max(1, per_page),
-                                 C.byref(n)))
+        farr, nf = _strs(filters)
+        _check(_lib.fg_db_search_ex(self._h, _b(namespace), query.encode(), farr, nf, page, per_page, out,
+                                    max(1, per_page), C.byref(n)))
         return [(out[i].score, out[i].doc) for i in range(n.value)]
 
     def search_json(self, namespace: Optional[str], query: str, page: int = 0, per_page: int = 20,
-                    include_text: bool = False, shape: int = SHAPE_GET_SEARCH) -> str:
-        return _string_call(_lib.fg_db_search_json, self._h, _b(namespace), query.encode(), page, per_page,
-                            int(include_text), shape)
+                    include_text: bool = False, shape: int = SHAPE_GET_SEARCH, filters=None) -> str:
+        farr, nf = _strs(filters)
+        return _string_call(_lib.fg_db_search_json_ex, self._h, _b(namespace), query.encode(), farr, nf, page,
+                            per_page, int(include_text), shape)

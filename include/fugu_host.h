@@ -7,16 +7,19 @@
  *   fg_db_*            DatasetManager (src/db/config.rs:91-331): namespace
  *                      registry; create/delete are the routes the CLI speaks
  *                      but the server lacks (cli.rs:241-243, 280-282)
- *   fg_db_upsert       NamedIndex::upsert for the docs index
- *                      (src/db/document.rs:23-67, build_full_document :116-139):
+ *   fg_db_upsert_record NamedIndex::upsert for the docs index
+ *                      (src/db/document.rs:23-67, build_full_document :116-184):
  *                      ObjectRecord::validate (src/object.rs:31-78), delete by
- *                      the RAW id term, index `text` and metadata["name"]
+ *                      the RAW id term, index `text`, metadata["name"] and the
+ *                      facets (get_all_facet_paths, document.rs:277-309)
+ *   fg_db_upsert       the same with `name` given directly (no namespace facets)
  *   fg_db_commit       IndexWriter::commit + reader reload: rebuilds the
  *                      namespace's immutable device snapshot (fg_index)
  *   fg_db_add_file     POST /add/{namespace} (cli.rs:392-397, types.rs:71-75)
- *   fg_db_search       Dataset::search (src/db/search.rs:74-218): QueryParser
- *                      over [text, name], TopDocs::with_limit(offset+per_page)
- *                      on the GPU, doc fetch, skip(offset).take(per_page)
+ *   fg_db_search_ex    Dataset::search (src/db/search.rs:74-218): QueryParser
+ *                      over [text, name], facet filters (build_facet_query,
+ *                      :221-324), TopDocs::with_limit(offset+per_page) on the
+ *                      GPU, doc fetch, skip(offset).take(per_page)
  *   fg_db_search_json  perform_search (src/server/handlers/search.rs:350-402)
  *                      + the response shapes of the GET /search, POST /search
  *                      and POST /search/{namespace} handlers (Appendix B)
@@ -24,9 +27,11 @@
  *                      RemoveLongFilter(40) -> LowerCaser)
  *   fg_parse_query     the QueryParser subset the device runs
  *
- * Queries outside the device subset (phrases, field:, -, boosts, empty =
- * AllQuery, facet filters) return FG_EUNSUPPORTED: the
+ * Queries outside the device subset (phrases, field:, -, boosts, a text
+ * query with filters that parse to no facet term) return FG_EUNSUPPORTED: the
  * reference host then runs tantivy; this library never answers them on the CPU.
+ * Empty queries (AllQuery), facet-only queries and text + facet filters run
+ * on the device.
  */
 #ifndef FUGU_HOST_H
 #define FUGU_HOST_H
@@ -55,6 +60,20 @@ int fg_db_namespace_delete(fg_db* db, const char* name);
 /* {"status":"success","namespaces":[...]} (handlers/namespaces.rs:24-30), names sorted */
 int fg_db_namespaces_json(fg_db* db, char* out, size_t cap, size_t* len);
 
+/* ObjectRecord (src/object.rs:8-27) as the upsert routes receive it. */
+typedef struct fg_object_record {
+  const char* id;
+  const char* text;
+  const char* metadata_json;    /* a JSON object, or NULL (metadata: None) */
+  const char* namespace_;       /* ObjectRecord.namespace, or NULL */
+  const char* organization;     /* or NULL */
+  const char* conversation_id;  /* or NULL */
+  const char* data_type;        /* or NULL */
+  const char* const* facets;    /* ObjectRecord.facets: n_facets paths when has_facets */
+  uint32_t n_facets;
+  int has_facets;               /* Some(facets) (even empty) vs None */
+} fg_object_record;
+int fg_db_upsert_record(fg_db* db, const char* ns, const fg_object_record* rec);
 int fg_db_upsert(fg_db* db, const char* ns, const char* id, const char* text, const char* name,
                  const char* metadata_json);
 int fg_db_commit(fg_db* db, const char* ns);
@@ -66,17 +85,33 @@ typedef struct fg_hit {
   float score;
   uint32_t doc; /* global doc id in the namespace (insertion order) */
 } fg_hit;
-/* Dataset::search: hits of page `page` (per_page each), *n_out <= per_page. */
+/* Dataset::search: hits of page `page` (per_page each), *n_out <= per_page.
+ * filters: the request's `filters` strings (FuguSearchQuery / JsonQueryRequest). */
+int fg_db_search_ex(fg_db* db, const char* ns, const char* query, const char* const* filters, uint32_t n_filters,
+                    uint32_t page, uint32_t per_page, fg_hit* out, uint32_t cap, uint32_t* n_out);
 int fg_db_search(fg_db* db, const char* ns, const char* query, uint32_t page, uint32_t per_page, fg_hit* out,
                  uint32_t cap, uint32_t* n_out);
 /* perform_search + handler response JSON (per_page clamp 1..100 else 20). */
+int fg_db_search_json_ex(fg_db* db, const char* ns, const char* query, const char* const* filters,
+                         uint32_t n_filters, uint32_t page, uint32_t per_page, int include_text, int shape, char* out,
+                         size_t cap, size_t* len);
 int fg_db_search_json(fg_db* db, const char* ns, const char* query, uint32_t page, uint32_t per_page,
                       int include_text, int shape, char* out, size_t cap, size_t* len);
+/* Stored facets of doc `doc` as Facet Display strings, '\n'-separated. */
+int fg_db_doc_facets(fg_db* db, const char* ns, uint32_t doc, char* out, size_t cap, size_t* len);
 
 /* Analyzer / parser exposed for tests: tokens separated by '\n'. */
 int fg_analyze(const char* text, char* out, size_t cap, size_t* len);
 /* mode (FG_MODE_AND / FG_MODE_OR) and the analyzed terms ('\n'-separated). */
 int fg_parse_query(const char* query, int* mode, char* out, size_t cap, size_t* len);
+/* FacetTokenizer tokens of Facet::from_text(path), '\n'-separated; the
+ * encoded facets keep their U+0000 separators, so read *len bytes. */
+int fg_facet_tokens(const char* path, char* out, size_t cap, size_t* len);
+/* build_facet_query's clause list for `filters` (encoded facet terms,
+ * '\n'-separated, *len bytes); *applies = some filter survives the wildcard
+ * split; *all_query = none parsed into a term (facet_query = AllQuery). */
+int fg_facet_clauses(const char* const* filters, uint32_t n_filters, int* applies, int* all_query, char* out,
+                     size_t cap, size_t* len);
 
 #ifdef __cplusplus
 }

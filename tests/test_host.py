@@ -194,6 +194,103 @@ def test_commit_needs_a_device_and_search_before_commit_is_empty(db):
         d.search(None, "hello", page=1000, per_page=100)  # offset + per_page > FG_MAX_K
 
 
+# ------------------------------------------------------------------ facets
+def string_leaves(v):
+    if isinstance(v, dict):
+        return sum(string_leaves(x) for x in v.values())
+    if isinstance(v, list):
+        return sum(string_leaves(x) for x in v)
+    return 1 if isinstance(v, str) and v else 0
+
+
+def py_facet_paths(meta, namespace=None, facets=None, org=None, conv=None, dtype=None):
+    """get_all_facet_paths (src/db/document.rs:277-309) restated, as Facet Display strings."""
+    import facet_ref as fr
+    if facets is not None:
+        paths = [fr.normalize(f) for f in facets]
+    else:
+        paths = []
+        if namespace is not None:
+            paths.append(f"/namespace/{namespace}")
+            if org is not None:
+                paths.append(f"/namespace/{namespace}/organization/{org}")
+            if conv is not None:
+                paths.append(f"/namespace/{namespace}/conversation/{conv}")
+            if dtype is not None:
+                paths.append(f"/namespace/{namespace}/data/{dtype}")
+        for k, v in (meta or {}).items():
+            p = k if k.startswith("/") else f"/metadata/{k}"
+            paths += [p] * string_leaves(v)
+    return [fr.display(fr.from_text(p)) for p in paths]
+
+
+FACET_PATHS = ["/a/b", "/", "/a//b", "//b", "/a\\/b/c", "/a/", "/namespace/x/data/email", "/x\\\\y", "/é/日本"]
+
+
+def test_facet_tokenizer_matches_restatement(db):
+    import facet_ref as fr
+    for p in FACET_PATHS:
+        assert db.facet_tokens(p) == fr.tokens(fr.from_text(p)), p
+    with pytest.raises(db.native.FuguError):
+        db.facet_tokens("a/b")  # Facet::from_text needs a leading '/'
+    # the golden facet corpus: every doc's tokens through the C++ tokenizer
+    import synth_ref as sr
+    from conftest import load_golden
+    fx = load_golden("facets_2k.json")
+    vocab = fx["facet_vocab"]
+    for d, paths in enumerate(sr.facet_paths(200, fx["corpus"]["facet_seed"])):
+        toks = [t for p in paths for t in db.facet_tokens(fr.normalize(p))]
+        assert toks == [vocab[i] for i in fx["facet_tokens"][d]], d
+
+
+def test_facet_filter_clauses(db):
+    """parse_filters + build_facet_query (src/db/search.rs:221-324) and the
+    wildcard split of Dataset::search (:89-103)."""
+    fc = db.facet_clauses
+    assert fc([]) == (False, False, [])
+    assert fc(["a/b"]) == (True, False, ["a\x00b"])
+    assert fc(["/a/b/*"]) == (True, False, ["a\x00b"])          # Prefix: the path itself (ancestors are indexed)
+    assert fc(["ns=foo"]) == (True, False, ["ns"])               # key=value: Equals on the key, value dropped
+    assert fc(["/a/*", "b", "c=d"]) == (True, False, ["b", "c", "a"])  # exact terms first, then prefixes
+    assert fc(["*x*"]) == (False, False, [])                      # wildcard: dropped (never post-filtered)
+    assert fc(["*", "*a*", "k"]) == (True, False, ["k"])
+    assert fc(["/*"]) == (True, True, [])                         # prefix "" fails Facet::from_text -> AllQuery
+    assert fc(["=x"]) == (True, False, [""])                      # "/=x" -> key "/" -> the root facet
+    assert fc(["a\\/b"]) == (True, False, ["a/b"])
+
+
+def test_upsert_facets(db):
+    d = db.Database()
+    d.create_namespace("n1")
+    d.upsert(db.ObjectRecord("e1", "x", facets=["a/b", "/c//d", "/e\\/f"]), "n1")
+    d.upsert(db.ObjectRecord("e2", "x", facets=[]), "n1")       # Some([]): no fallback facets
+    d.upsert(db.ObjectRecord("e3", "x", namespace="n1", organization="acme", conversation_id="c7",
+                             data_type="chat", metadata={"name": "N", "tags": ["t1", "", "t2", 5],
+                                                         "nested": {"a": {"b": "v"}, "c": 1}, "/raw": "v",
+                                                         "empty": "", "flag": True}))
+    d.upsert(db.ObjectRecord("e4", "x", metadata={"n": None}))  # into the default namespace: no namespace facet
+    assert d.doc_facets("n1", 0) == ["/a/b", "/c//d", "/e\\/f"]
+    assert d.doc_facets("n1", 1) == []
+    assert d.doc_facets("n1", 2) == ["/namespace/n1", "/namespace/n1/organization/acme",
+                                     "/namespace/n1/conversation/c7", "/namespace/n1/data/chat", "/metadata/name",
+                                     "/metadata/tags", "/metadata/tags", "/metadata/nested", "/raw"]
+    assert d.doc_facets(None, 0) == []
+    meta = {"name": "N", "tags": ["t1", "", "t2", 5], "nested": {"a": {"b": "v"}, "c": 1}, "/raw": "v", "empty": "",
+            "flag": True}
+    assert d.doc_facets("n1", 2) == py_facet_paths(meta, "n1", org="acme", conv="c7", dtype="chat")
+    bad = [(db.ObjectRecord("x", "t", facets=["f"] * 101), "Too many facets (max 100 per object)"),
+           (db.ObjectRecord("x", "t", facets=["a", ""]), "Facet at index 1 cannot be empty"),
+           (db.ObjectRecord("x", "t", facets=["a" * 513]), "Facet at index 0 too long (max 512 characters)"),
+           (db.ObjectRecord("x", "t", namespace="a b"), "Invalid namespace format"),
+           (db.ObjectRecord("x", "t", namespace="n" * 129), "Namespace too long (max 128 characters)")]
+    for rec, msg in bad:
+        with pytest.raises(db.native.FuguError) as e:
+            d.upsert(rec, "n1")
+        assert msg in str(e.value)
+    d.upsert(db.ObjectRecord("x", "t", facets=["f"] * 100), "n1")
+    d.upsert(db.ObjectRecord("x", "t", facets=["a" * 512]), "n1")
+
+
 # ------------------------------------------------------------------ end to end on the device
 WORDS = ["Alpha", "beta", "Gamma", "delta", "épsilon", "ZETA", "eta", "théta", "iota", "kappa", "lambda", "mu",
          "nu", "xi", "omicron", "pi", "rho", "sigma", "tau", "upsilon", "phi", "chi", "psi", "omega", "日本",
@@ -270,7 +367,8 @@ def test_db_end_to_end_vs_oracle(db):
         for h, (doc, bits) in zip(r["results"], want):
             assert h["id"] == recs[doc][0] and h["text"] == recs[doc][1]
             assert np.float32(h["score"]).view(np.uint32) == bits
-            assert h["metadata"] == recs[doc][2] and h["facets"] is None
+            assert h["metadata"] == recs[doc][2]
+            assert h["facets"] == (py_facet_paths(recs[doc][2], "docs") or None)
     assert checked > 100
     r = json.loads(d.search_json("docs", WORDS[1], 0, 3))
     assert all("text" not in h for h in r["results"])
@@ -289,3 +387,86 @@ def test_db_end_to_end_vs_oracle(db):
     assert len(got) == 1 and got[0][1] == len(recs)
     r = json.loads(d.search_json("docs", "brandnewword", shape=db.SHAPE_POST_SEARCH))
     assert r["results"][0]["id"] == "notes.txt" and r["results"][0]["metadata"] == {"name": "notes.txt"}
+    assert r["results"][0]["facets"] == ["/namespace/docs", "/metadata/name"]
+
+
+def facet_corpus(seed, n):
+    rng = random.Random(seed)
+    recs = []
+    for i in range(n):
+        words = [rng.choice(WORDS[:rng.randint(3, len(WORDS))]) for _ in range(rng.randint(1, 30))]
+        text = " ".join(words)
+        kind = rng.random()
+        rec = dict(id=f"doc{i}", text=text)
+        if kind < 0.3:
+            rec["facets"] = [rng.choice(["/lang/en", "/lang/de", "lang/fr", "/topic/a/b", "/topic/a/c", "/x\\/y"])
+                             for _ in range(rng.randint(0, 3))]
+        elif kind < 0.8:
+            rec["organization"] = rng.choice(["acme", "initech", None])
+            rec["data_type"] = rng.choice(["email", "chat", None])
+            rec["metadata"] = {"tags": [rng.choice(["t1", "t2", ""]) for _ in range(rng.randint(0, 3))]} \
+                if rng.random() < 0.5 else None
+        recs.append(rec)
+    return recs
+
+
+@pytest.mark.gpu
+def test_db_facet_filters_end_to_end_vs_oracle(db):
+    """Upserts with explicit / namespace / metadata facets, then filtered,
+    facet-only and empty-query searches through Dataset::search on the device,
+    against the oracle on facet tokens restated in Python."""
+    import facet_ref as fr
+    from conftest import tokens_to_csr
+    from fugu_amd import native
+    from oracle import oracle as orc
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("fx")
+    recs = facet_corpus(5, 1500)
+    for r in recs:
+        d.upsert(db.ObjectRecord(r["id"], r["text"], metadata=r.get("metadata"), facets=r.get("facets"),
+                                 organization=r.get("organization"), data_type=r.get("data_type")), "fx")
+    d.commit("fx")
+    dic, fdic, text, ftoks = {}, {}, [], []
+    for r in recs:
+        text.append([dic.setdefault(t, len(dic)) for t in py_analyze(r["text"])])
+        paths = py_facet_paths(r.get("metadata"), "fx", r.get("facets"), r.get("organization"), None,
+                               r.get("data_type"))
+        ftoks.append([fdic.setdefault(t, len(fdic)) for p in paths for t in fr.tokens(fr.from_text(p))])
+    to, tt = tokens_to_csr(text)
+    fo, ft = tokens_to_csr(ftoks)
+    ix = orc.OracleIndex(len(dic), to, tt, facet_off=fo, facet_tok=ft, n_fterms=len(fdic))
+    filters_pool = [["lang/en"], ["/lang/*"], ["/topic/a/*", "lang/de"], ["namespace/fx/organization/acme"],
+                    ["/namespace/fx/data/*", "*chat*"], ["metadata=tags"], ["/nope"], ["/x\\/y", "/lang/fr"],
+                    ["/"], ["*w*"]]
+    rng = random.Random(3)
+    checked = 0
+    for qi in range(80):
+        filters = rng.choice(filters_pool)
+        if qi % 4 == 0:
+            q, terms, mode = "", [], 0
+        else:
+            ws = [rng.choice(WORDS) for _ in range(rng.randint(1, 3))]
+            q = " AND ".join(ws) if rng.random() < 0.6 else " ".join(ws)
+            mode = 0 if (len(ws) == 1 or " AND " in q) else 1
+            terms = [dic.get(py_analyze(w)[0], native.FG_TERM_MISSING) for w in ws]
+        page, per_page = rng.randint(0, 2), rng.choice([5, 10, 20])
+        applies, all_q, cl = db.facet_clauses(filters)
+        fterms = [fdic.get(c, native.FG_TERM_MISSING) for c in cl] if applies and not all_q else None
+        got = d.search("fx", q, page, per_page, filters=filters)
+        s, dd = ix.search(np.array(terms, np.uint32), (page + 1) * per_page, mode=mode, fterms=fterms)
+        want = hits_of(s, dd)[page * per_page:]
+        assert hits_of([g[0] for g in got], [g[1] for g in got]) == want, (q, filters)
+        checked += len(want)
+        r = json.loads(d.search_json("fx", q, page, per_page, shape=db.SHAPE_POST_SEARCH, filters=filters))
+        assert r["filters"] == filters and r["total"] == len(want)
+        for h, (doc, bits) in zip(r["results"], want):
+            rc = recs[doc]
+            assert h["id"] == rc["id"] and np.float32(h["score"]).view(np.uint32) == bits
+            assert h["facets"] == (py_facet_paths(rc.get("metadata"), "fx", rc.get("facets"), rc.get("organization"),
+                                                  None, rc.get("data_type")) or None)
+    assert checked > 300
+    with pytest.raises(native.Unsupported):  # text AND an AllQuery facet filter
+        d.search("fx", "alpha", filters=["/*"])
