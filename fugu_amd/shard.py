@@ -59,25 +59,32 @@ def merge_on_device(s: torch.Tensor, d: torch.Tensor, c: torch.Tensor, nq: int, 
 # ---- doc-sharded namespace ------------------------
 def allreduce_stats(local, group=None, device=None):
     """Sum a shard's BM25 statistics over the group: ONE all-reduce of
-    [n_docs, tot_text, tot_name, df_text[V], df_name[V]] as int64 (RCCL when the
-    group is "nccl": pass the rank's cuda device).  Returns native.ShardStats of
-    the whole namespace, identical on every rank."""
+    [n_docs, tot_text, tot_name, tot_facet, df_text[V], df_name[V], df_facet[VF]]
+    as int64 (RCCL when the group is "nccl": pass the rank's cuda device).
+    Every rank must pass the same vocabularies (one term / facet dictionary per
+    namespace).  Returns native.ShardStats of the whole namespace, identical on
+    every rank."""
     import numpy as np
 
     from .native import ShardStats
     V = len(local.df_text)
-    buf = np.empty(3 + 2 * V, np.int64)
+    VF = 0 if local.df_facet is None else len(local.df_facet)
+    buf = np.empty(4 + 2 * V + VF, np.int64)
     buf[0] = local.n_docs
     buf[1:3] = local.tot_tokens
-    buf[3:3 + V] = local.df_text
-    buf[3 + V:] = local.df_name
+    buf[3] = local.tot_facet_tokens
+    buf[4:4 + V] = local.df_text
+    buf[4 + V:4 + 2 * V] = local.df_name
+    if VF:
+        buf[4 + 2 * V:] = local.df_facet
     t = torch.from_numpy(buf)
     if device is not None:
         t = t.to(device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     out = t.cpu().numpy()
-    return ShardStats(int(out[0]), (int(out[1]), int(out[2])), out[3:3 + V].astype(np.uint32),
-                      out[3 + V:].astype(np.uint32))
+    dff = out[4 + 2 * V:].astype(np.uint32) if local.df_facet is not None else None
+    return ShardStats(int(out[0]), (int(out[1]), int(out[2])), out[4:4 + V].astype(np.uint32),
+                      out[4 + V:4 + 2 * V].astype(np.uint32), dff, int(out[3]))
 
 
 def shard_ranges(n_docs: int, world: int):

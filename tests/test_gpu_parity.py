@@ -341,3 +341,39 @@ def test_facets_1m_vs_oracle(native, gpu_1m_facets, oracle_1m_facets, facets_1m,
     for i in range(nq):
         assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], (i, f_terms[f_off[i]:f_off[i + 1]].tolist()))
     assert (n > 0).mean() > 0.3
+
+
+@pytest.mark.parametrize("m_min,m_max,mode,ncl", [(1, 2, 0, 1), (0, 0, 0, 2), (2, 3, 1, 2)])
+def test_doc_sharded_facets_equal_single_index(native, ctx, corpus_1m, facets_1m, gpu_1m_facets, m_min, m_max,
+                                               mode, ncl):
+    """Doc-range shards with GLOBAL facet statistics (fg_docs_facet_stats summed)
+    answer filtered / facet-only queries exactly like the single index."""
+    from fugu_amd import synth
+    from fugu_amd.shard import shard_ranges
+    c = corpus_1m
+    fo, ft, nf = facets_1m
+    V, k = 1 << 20, 100
+    ranges = shard_ranges(len(c.off) - 1, 3)
+    parts = [(b, c.off[b:e + 1] - c.off[b], c.tok[c.off[b]:c.off[e]], (fo[b:e + 1] - fo[b], ft[fo[b]:fo[e]], nf))
+             for b, e in ranges]
+    local = [native.docs_stats(off, tok, V, threads=16, facets=fc) for _, off, tok, fc in parts]
+    g = local[0] + local[1] + local[2]
+    shards = [native.Index.from_docs(ctx, off, tok, V, threads=16, global_stats=g, facets=fc)
+              for _, off, tok, fc in parts]
+    nq = 128
+    if m_max == 0:
+        q_off, terms = np.zeros(nq + 1, np.uint32), np.zeros(0, np.uint32)
+    else:
+        q_off, terms = synth.queries(nq, m_min, m_max, seed_q=41)
+    f_off, f_terms = _fbatch(_clauses(nq, ncl, nf, 700 + ncl))
+    res = [ix.search_batch(q_off, terms, k, mode=mode, f_off=f_off, f_terms=f_terms) for ix in shards]
+    sc, dc, nn = (np.stack([r[j] for r in res]) for j in range(3))
+    ms, md, msh, mn = _device_merge(native, sc, dc, nn, k)
+    base = np.array([p[0] for p in parts], np.uint32)
+    gdoc = md + base[msh]
+    s1, d1, n1 = gpu_1m_facets.search_batch(q_off, terms, k, mode=mode, f_off=f_off, f_terms=f_terms)
+    assert np.array_equal(mn, n1)
+    for i in range(nq):
+        m = int(n1[i])
+        assert np.array_equal(gdoc[i, :m], d1[i, :m]), i
+        assert np.array_equal(ms[i, :m], s1[i, :m]), i

@@ -101,15 +101,19 @@ def _stats_worker(rank, world, port, outq):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fugu_amd import native, synth
     from fugu_amd.shard import allreduce_stats, shard_ranges
     c = synth.corpus(6000, 1 << 16)
     b, e = shard_ranges(6000, world)[rank]
     off = c.off[b:e + 1] - c.off[b]
     tok = c.tok[c.off[b]:c.off[e]]
-    g = allreduce_stats(native.docs_stats(off, tok, 1 << 16))
+    import synth_ref as sr
+    fo, ft, nf = sr.facet_tokens(6000, 31)
+    facets = (fo[b:e + 1] - fo[b], ft[fo[b]:fo[e]], nf)
+    g = allreduce_stats(native.docs_stats(off, tok, 1 << 16, facets=facets))
     if rank == 0:
-        outq.put((g.n_docs, g.tot_tokens, g.df_text, g.df_name))
+        outq.put((g.n_docs, g.tot_tokens, g.df_text, g.df_name, g.df_facet, g.tot_facet_tokens))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -138,9 +142,11 @@ def test_two_rank_global_stats_allreduce():
             p.kill()
         assert p.exitcode == 0, "a rank failed"
     assert got is not None
-    n, tot, dft, dfn = got
+    n, tot, dft, dfn, dff, totf = got
     from fugu_amd import native, synth
+    import synth_ref as sr
     c = synth.corpus(6000, 1 << 16)
-    full = native.docs_stats(c.off, c.tok, 1 << 16)
+    full = native.docs_stats(c.off, c.tok, 1 << 16, facets=sr.facet_tokens(6000, 31))
     assert n == full.n_docs and tot == full.tot_tokens
     assert np.array_equal(dft, full.df_text) and np.array_equal(dfn, full.df_name)
+    assert np.array_equal(dff, full.df_facet) and totf == full.tot_facet_tokens > 0
