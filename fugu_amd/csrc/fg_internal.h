@@ -41,29 +41,28 @@ constexpr uint32_t kModeOr = 1;
 
 // Device view of one namespace snapshot (all pointers device-resident).
 //
-// Per term t the postings are doc[off[t] .. off[t+1]) (ascending) with tf[]
-// alongside, and a doc -> position directory: bucket b covers docs
+// Per term t the postings are doc[off[t] .. off[t+1]) (ascending) with psc[]
+// (the posting's BM25 term score) alongside, and a doc -> position directory: bucket b covers docs
 // [b << B_t, (b+1) << B_t) and dir[dir_off[t] + b] = first position in the
 // list with doc >= b << B_t (the last entry is df_t).  B_t is chosen so a
 // bucket holds ~32 postings (one 128-B line of doc ids); a probe is one
 // directory load and a <= S_t step search inside one or two lines.  Terms that
 // occur in >= 1/8 of the docs (and only in `text`) additionally get a dense
-// doc-indexed u16 tf table: a probe into them is one coalesced 2-B load.
+// doc-indexed f32 score table: a probe into them is one 4-B load.
 struct DevIndex {
   const uint32_t* doc;       // [P] doc ids, CSR by term, ascending within a term
-  const uint32_t* tf;        // [P] packed: lo16 = tf in `text`, hi16 = tf in `name`
+  const float* psc;          // [P] the posting's term score: Should(text:t, name:t) in the doc, i.e.
+                             //     0.0 + w_text*(tf/(tf+cache[fn])) + w_name*(...), computed at snapshot
+                             //     build in tantivy's f32 operation order (a snapshot's BM25 statistics
+                             //     are fixed, so this is the value tantivy computes at query time)
   const uint64_t* off;       // [V+1] posting offsets
   const uint32_t* dir;       // [D] bucket directory (positions within the list)
   const uint32_t* dir_off;   // [V] first directory entry of each term
   const uint32_t* tmeta;     // [V] bits 0-7 = B_t (bucket shift), bits 8-15 = S_t (search steps),
                              //     bits 16-31 = dense slot + 1 (0: no dense table)
-  const uint16_t* dense;     // [n_dense * N] doc-indexed tf_text of the densest terms (0 = absent)
-  const float* w_text;       // [V] idf(df_text)*(1+K1)
-  const float* w_name;       // [V] idf(df_name)*(1+K1)
-  const uint8_t* fn_text;    // [N] fieldnorm ids
-  const uint8_t* fn_name;    // [N] fieldnorm ids (all 0 when no `name` values)
+  const float* dense;        // [n_dense * N] doc-indexed term score of the densest terms (-1 = absent)
+  const float* tmaxs;        // [V] largest posting score of each term (MaxScore bound)
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
-  const float* cache;        // [512] bm25 tf cache: [0,256) text, [256,512) name
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
   const uint32_t* toff;      // [V] first tmax entry of each term, or 0xFFFFFFFF (bucket >= tile: use bmax)
@@ -118,6 +117,8 @@ struct DevPlan {
   const uint32_t* work_n;       // [total_chunks] chunks in the item's group (k_disj: tiles)
   const uint64_t* cand_off;     // [nq+1] candidate-list capacity offsets (work items of q * k)
   const uint64_t* q_thr0;       // [nq] starting threshold key (k_disj: per-term top-K bound), 0 = none
+  const float* q_ub;            // [nq * kMaxTerms] k_conj MaxScore bounds: q_ub[i] = sum over the query's
+                                //     terms j >= i (intersection order) of tmaxs, i >= 1
   // workspace, zeroed per run
   uint64_t* thresh;             // [nq] monotone lower bound on the k-th best key
   uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list

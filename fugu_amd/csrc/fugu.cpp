@@ -168,6 +168,7 @@ struct fg_index {
   std::vector<uint32_t> df_text, df_name;
   std::vector<uint32_t> first_doc, last_doc;
   std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
+  std::vector<float> tmaxs; // [V] largest posting score per term
   std::vector<float> w_text, w_name;
   std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model
   // facet field (FG_FIELD_FACET)
@@ -275,6 +276,14 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   // bucket score maxima (parallel to dir): the per-bucket upper bound the
   // disjunctive kernel prunes with (block-max WAND / MaxScore bounds)
   std::vector<float> bmax(nd, 0.0f);
+  // every posting's term score (DevIndex::psc) and each term's largest one
+  std::vector<float> psc;
+  try {
+    psc.resize(hp.doc.size());
+  } catch (...) {
+    return fail(FG_EOOM, "posting scores allocation failed");
+  }
+  std::vector<float> tmaxs(V, 0.0f);
   // per-term K-th best score over alive docs for K in kTopKs: a doc among a
   // term's top K scores at least that much in any disjunction containing the
   // term, so the query's K-th best is >= it (k_disj's starting threshold)
@@ -297,14 +306,16 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
         while (p < n && hp.doc[b0 + p] < lo) {
           const uint32_t d = hp.doc[b0 + p], tfp = hp.tf[b0 + p];
           const float v = term_score_host(tfp, hp.fn_text[d], has_name ? hp.fn_name[d] : 0, wt, wn, ix->cache);
+          psc[b0 + p] = v;
           mx = std::max(mx, v);
+          tmaxs[t] = std::max(tmaxs[t], v);
           if (hp.alive.empty() || ((hp.alive[d >> 5] >> (d & 31)) & 1u)) sc.push_back(v);
           ++p;
         }
         dt[b] = (uint32_t)p;
         if (b) {
           maxocc = std::max<uint32_t>(maxocc, dt[b] - dt[b - 1]);
-          bm[b - 1] = mx;
+          bm[b - 1] = dt[b] > dt[b - 1] ? mx : -0.0f;  // -0.0: empty bucket (a score may be +0.0)
         }
       }
       uint32_t S = 0;
@@ -350,9 +361,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     const uint64_t n = hp.off[t + 1] - hp.off[t];
     if (n * fg::kDenseDiv >= N && hp.df_name[t] == 0) dense_terms.push_back(t);
   }
-  std::vector<uint16_t> dense;
+  std::vector<float> dense;
   try {
-    dense.assign(dense_terms.size() * (size_t)N, 0);
+    dense.assign(dense_terms.size() * (size_t)N, -1.0f);  // -1: absent (a score is >= 0, and may be 0)
   } catch (...) {
     return fail(FG_EOOM, "dense tables (%zu terms) allocation failed", dense_terms.size());
   }
@@ -360,8 +371,8 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
                   [&](int, uint32_t a, uint32_t e) {
                     for (uint32_t s = a; s < e; ++s) {
                       const uint32_t t = dense_terms[s];
-                      uint16_t* row = dense.data() + (size_t)s * N;
-                      for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) row[hp.doc[p]] = (uint16_t)(hp.tf[p] & 0xFFFFu);
+                      float* row = dense.data() + (size_t)s * N;
+                      for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) row[hp.doc[p]] = psc[p];
                       tmeta[t] |= (s + 1) << 16;
                     }
                   });
@@ -398,13 +409,15 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   HIPCHK(hipSetDevice(dev));
   uint64_t bytes = 0;
   int rc;
-  uint16_t* d_dense = nullptr;
-  uint32_t *d_doc, *d_tf, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr, *d_toff;
+  float* d_dense = nullptr;
+  uint32_t *d_doc, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr, *d_toff;
   uint64_t* d_off;
-  float *d_wt, *d_wn, *d_cache, *d_bmax, *d_tmax;
-  uint8_t *d_fnt, *d_fnn;
+  float *d_psc, *d_tmaxs, *d_bmax, *d_tmax;
   if ((rc = dev_upload(ix->mem, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, hp.tf.data(), hp.tf.size(), &d_tf, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, psc.data(), psc.size(), &d_psc, &bytes))) return rc;
+  std::vector<float>().swap(psc);
+  std::vector<uint32_t>().swap(hp.tf);
+  if ((rc = dev_upload(ix->mem, tmaxs.data(), tmaxs.size(), &d_tmaxs, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.off.data(), hp.off.size(), &d_off, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, dir.data(), dir.size(), &d_dir, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, bmax.data(), bmax.size(), &d_bmax, &bytes))) return rc;
@@ -415,20 +428,15 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, dense.data(), dense.size(), &d_dense, &bytes))) return rc;
-  std::vector<uint16_t>().swap(dense);
-  if ((rc = dev_upload(ix->mem, ix->w_text.data(), V, &d_wt, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, ix->w_name.data(), V, &d_wn, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, hp.fn_text.data(), hp.fn_text.size(), &d_fnt, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, hp.fn_name.data(), hp.fn_name.size(), &d_fnn, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
+  std::vector<float>().swap(dense);
+  ix->tmaxs = std::move(tmaxs);
   if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
   uint32_t* d_fdoc;
   uint64_t* d_foff;
   if ((rc = dev_upload(ix->mem, hp.fdoc.data(), hp.fdoc.size(), &d_fdoc, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.foff.data(), hp.foff.size(), &d_foff, &bytes))) return rc;
-  ix->d = fg::DevIndex{d_doc, d_tf, d_off, d_dir, d_dir_off, d_tmeta, d_dense, d_wt, d_wn, d_fnt, d_fnn, d_alive,
-                       d_cache, d_bmax, d_tmax, d_toff, d_fdoc, d_foff, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u,
-                       VF};
+  ix->d = fg::DevIndex{d_doc, d_psc, d_off, d_dir, d_dir_off, d_tmeta, d_dense, d_tmaxs, d_alive, d_bmax, d_tmax,
+                       d_toff, d_fdoc, d_foff, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u, VF};
   ix->foff = std::move(hp.foff);
   // per-term doc span (disjunctive plans skip the tiles outside it)
   ix->first_doc.assign(V, 0);
@@ -862,6 +870,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   const bool disj = q->mode == FG_MODE_OR;
   std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), nchunk(nq);
   std::vector<uint64_t> thr0(nq, 0);
+  std::vector<float> q_ub((size_t)nq * fg::kMaxTerms, 0.0f);
 
   // ---- facet filters: one mask per distinct clause list (fg_internal.h DevFilters)
   std::vector<uint32_t> q_filter(nq, 0xFFFFFFFFu);
@@ -1011,6 +1020,15 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     std::stable_sort(ts, ts + m, [](const T& x, const T& y) { return x.cost < y.cost; });
     q_m[i] = m;
     for (uint32_t j = 0; j < m; ++j) q_terms[(size_t)i * fg::kMaxTerms + j] = missing ? 0 : ts[j].term;
+    // MaxScore suffix bounds of the probed lists (k_conj prunes a candidate once its
+    // partial score plus these cannot reach the query's threshold)
+    if (!missing) {
+      float acc = 0.0f;
+      for (uint32_t j = m; j-- > 1;) {
+        acc += ix->tmaxs[ts[j].term];
+        q_ub[(size_t)i * fg::kMaxTerms + j] = acc;
+      }
+    }
     const uint64_t df0 = missing ? 0 : ix->off[ts[0].term + 1] - ix->off[ts[0].term];
     lead[i] = (uint32_t)df0;
     nchunk[i] = (uint32_t)((df0 + fg::kChunk - 1) / fg::kChunk);
@@ -1051,9 +1069,11 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   const size_t nch = ch_f.size();
   const size_t s_qm = al(4ull * nq), s_qt = al(4ull * nq * fg::kMaxTerms), s_lead = al(4ull * nq),
                s_wq = al(4ull * chunks), s_wc = al(4ull * chunks), s_wn = al(4ull * chunks),
-               s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq), s_qf = al(4ull * nq), s_fs = al(4ull * nf),
+               s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq), s_ub = al(4ull * nq * fg::kMaxTerms),
+               s_qf = al(4ull * nq), s_fs = al(4ull * nf),
                s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch);
-  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_qf + s_fs + s_fw + s_ft + s_fm + 4 * s_ch;
+  const size_t s_in =
+      s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft + s_fm + 4 * s_ch;
   const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]);
   const size_t s_ck = al(8ull * cand_off[nq]);
   const size_t s_os = al(4ull * nq * k), s_od = al(4ull * nq * k), s_on = al(4ull * nq);
@@ -1085,6 +1105,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.work_n = (const uint32_t*)put(work_n.data(), 4ull * chunks, s_wn);
   p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
   p->d.q_thr0 = (const uint64_t*)put(thr0.data(), 8ull * nq, s_t0);
+  p->d.q_ub = (const float*)put(q_ub.data(), 4ull * nq * fg::kMaxTerms, s_ub);
   p->d.f.q_filter = (const uint32_t*)put(q_filter.data(), 4ull * nq, s_qf);
   p->d.f.f_shift = (const uint32_t*)put(f_shift.data(), 4ull * nf, s_fs);
   p->d.f.f_woff = (const uint64_t*)put(f_woff.data(), 8ull * nf, s_fw);

@@ -47,22 +47,6 @@ constexpr uint32_t kInvalid = 0xFFFFFFFFu;
 __device__ inline uint32_t lane_id() { return threadIdx.x & 63; }
 __device__ inline uint32_t wave_id() { return threadIdx.x >> 6; }
 
-// One query term's score for one doc: Should(text:t, name:t) under a
-// SumCombiner that starts at 0.0 (query/union, query/bm25.rs score()).
-__device__ inline float term_score(uint32_t tfp, uint32_t fnp, float wt, float wn, const float* cache) {
-  float s = 0.0f;
-  const uint32_t tt = tfp & 0xFFFFu, tn = tfp >> 16;
-  if (tt) {
-    const float tf = (float)tt;
-    s += wt * (tf / (tf + cache[fnp & 0xFFu]));
-  }
-  if (tn) {
-    const float tf = (float)tn;
-    s += wn * (tf / (tf + cache[256 + (fnp >> 8)]));
-  }
-  return s;
-}
-
 // Upper bounds are compared after inflating by 2^-17 relative: that covers any
 // f32 summation-order difference for <= 16 addends, so bound-based pruning
 // never drops a doc whose exactly-summed score reaches the threshold.
@@ -72,12 +56,6 @@ __device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f
 // when the term has one, else the maximum of d's directory bucket.
 __device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t toff, uint32_t dir_off, uint32_t d) {
   return toff != 0xFFFFFFFFu ? ix.tmax[toff + (d >> kDisjTileShift)] : ix.bmax[dir_off + (d >> (meta & 0xFFu))];
-}
-
-__device__ inline uint32_t load_fn(const DevIndex& ix, uint32_t d) {
-  uint32_t f = ix.fn_text[d];
-  if (ix.has_name) f |= (uint32_t)ix.fn_name[d] << 8;
-  return f;
 }
 
 // ---------------------------------------------------------------- workgroup helpers
@@ -208,9 +186,6 @@ __device__ void bitonic_sort_desc(uint64_t* s, uint32_t P) {
 #ifndef FG_TRUNC
 #define FG_TRUNC 1024
 #endif
-#ifndef FG_CONJ_PRUNE
-#define FG_CONJ_PRUNE 0  // block-max pre-probe pruning: measured slower (2.65 -> 3.51 ms, tools/ab_variants.py)
-#endif
 #ifndef FG_WAVES
 #define FG_WAVES 4  // tools/ab_variants.py: 3 -> 4 waves/SIMD took k_conj 3.18 -> 2.58 ms
 #endif
@@ -294,21 +269,23 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   const uint32_t c0 = pl.work_c[w], nc = pl.work_n[w];
   const uint32_t m = pl.q_m[q];
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
+  const float* qub = pl.q_ub + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
   const uint32_t t0 = terms[0];
   const uint64_t lead_base = ix.off[t0];
   const uint32_t lead_df = pl.q_lead_df[q];
-  const float wt0 = ix.w_text[t0], wn0 = ix.w_name[t0];
   unsigned long long* gthr = reinterpret_cast<unsigned long long*>(&pl.thresh[q]);
   // facet filter (uniform per work item): Bool[Must(text), Must(facet union)]
   const uint32_t fslot = pl.f.q_filter[q];
   const uint32_t* fmask = nullptr;
   uint32_t fshift = 0;
   const float* ftab = nullptr;
+  float fmax = 0.0f;
   if (fslot != kInvalid) {
     fmask = pl.f.fmask + pl.f.f_woff[fslot];
     fshift = pl.f.f_shift[fslot];
     ftab = pl.f.f_tab + (size_t)fslot * 256;
+    fmax = pl.f.f_max[fslot];
   }
   if (tid == 0) {
     sh.n_buf = 0;
@@ -325,52 +302,37 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     const uint32_t cnt = min(kChunk, lead_df - c * kChunk);
     uint64_t tp0 = FG_NOW();
     (void)tp0;
+    const uint64_t thr = sh.thr;
+    // MaxScore (uniform): once the query has a threshold, a candidate whose
+    // partial score plus the remaining lists' maxima cannot reach it is dropped
+    // before the next probe.  Bounds are inflated by 2^-17 (inflate_bound).
+    const bool prune = thr != 0 && m > 1;
     // lead candidates: item j of lane l = wv*512 + j*64 + l (coalesced per j)
-    uint32_t doc[kItems], fnp[kItems];
-    float acc_r[kItems], acc_o[kItems];
+    uint32_t doc[kItems];
+    float s0[kItems], acc_r[kItems], acc_o[kItems];
     uint32_t live = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
       const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
-      doc[j] = idx < cnt ? ix.doc[base0 + idx] : kInvalid;
-      live |= (idx < cnt ? 1u : 0u) << j;
-      fnp[j] = kInvalid;
+      const bool in = idx < cnt;
+      doc[j] = in ? ix.doc[base0 + idx] : kInvalid;
+      s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
+      live |= (in ? 1u : 0u) << j;
       acc_r[j] = 0.0f;
       acc_o[j] = 0.0f;
     }
     if (fmask) {
-      // the facet mask first: one L2-resident bit probe drops a candidate before any list probe
+      // the facet mask: one L2-resident bit probe drops a candidate before any list probe
 #pragma unroll
       for (uint32_t j = 0; j < kItems; ++j)
         if ((live & (1u << j)) && !filter_bits(fmask, fshift, doc[j])) live &= ~(1u << j);
     }
-#if FG_CONJ_PRUNE
-    // block-max pruning before any probe: lead score + the other terms' tile /
-    // bucket maxima at the doc must reach the query threshold
-    const uint64_t thr_c = sh.thr;
-    if (m > 1 && thr_c != 0) {
-      float ubs[kItems];
-#pragma unroll
-      for (uint32_t j = 0; j < kItems; ++j) {
-        const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
-        ubs[j] = 0.0f;
-        if (live & (1u << j)) {
-          fnp[j] = load_fn(ix, doc[j]);
-          ubs[j] = term_score(ix.tf[base0 + idx], fnp[j], wt0, wn0, ix.cache);
-        }
-      }
-      for (uint32_t i = 1; i < m; ++i) {
-        const uint32_t ti = terms[i];
-        const uint32_t meta = ix.tmeta[ti], toff = ix.toff[ti], doff = ix.dir_off[ti];
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j)
-          if (live & (1u << j)) ubs[j] += term_bound(ix, meta, toff, doff, doc[j]);
-      }
+    if (prune) {
+      const float ub = qub[1] + fmax;
 #pragma unroll
       for (uint32_t j = 0; j < kItems; ++j)
-        if ((live & (1u << j)) && make_key(inflate_bound(ubs[j]), doc[j]) < thr_c) live &= ~(1u << j);
+        if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + ub), doc[j]) < thr) live &= ~(1u << j);
     }
-#endif
 
     for (uint32_t i = 1; i < m; ++i) {
       if (!__any(live != 0)) break;  // wave-uniform early exit
@@ -378,13 +340,12 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       const uint64_t bi = ix.off[ti];
       const uint32_t meta = ix.tmeta[ti];
       const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu, dslot = meta >> 16;
-      const float wt = ix.w_text[ti], wn = ix.w_name[ti];
-      uint32_t tfv[kItems];
+      float sc[kItems];
       if (dslot) {
-        // dense term: doc-indexed tf table, one 2-B load per item (text-only term)
-        const uint16_t* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
+        // dense term: doc-indexed score table, one 4-B load per item (-1 = absent)
+        const float* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
 #pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) tfv[j] = (live & (1u << j)) ? dt[doc[j]] : 0u;
+        for (uint32_t j = 0; j < kItems; ++j) sc[j] = (live & (1u << j)) ? dt[doc[j]] : -1.0f;
       } else {
         const uint32_t* __restrict__ di = ix.doc + bi;
         const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[ti];
@@ -400,8 +361,8 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
             hi[j] = dir[b + 1];
           }
         }
-        for (uint32_t s = S; s > 0; --s) {
-          const uint32_t half = 1u << (s - 1);
+        for (uint32_t st = S; st > 0; --st) {
+          const uint32_t half = 1u << (st - 1);
 #pragma unroll
           for (uint32_t j = 0; j < kItems; ++j) {
             const uint32_t idx = pos[j] + half - 1;
@@ -410,44 +371,37 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
         }
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
-          tfv[j] = 0;
-          if ((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j]) tfv[j] = ix.tf[bi + pos[j]];
+          sc[j] = -1.0f;
+          if ((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j]) sc[j] = ix.psc[bi + pos[j]];
         }
       }
+      // Intersection::score = left + right + (0.0 + others...)
 #pragma unroll
       for (uint32_t j = 0; j < kItems; ++j) {
-        if (!tfv[j]) live &= ~(1u << j);
-        else if (fnp[j] == kInvalid) fnp[j] = load_fn(ix, doc[j]);
+        if (sc[j] < 0.0f) { live &= ~(1u << j); continue; }
+        if (i == 1) acc_r[j] = sc[j]; else acc_o[j] += sc[j];
       }
+      if (prune && i + 1 < m) {
+        const float ub = qub[i + 1] + fmax;
 #pragma unroll
-      for (uint32_t j = 0; j < kItems; ++j) {
-        if (!(live & (1u << j))) continue;
-        const float s = term_score(tfv[j], fnp[j], wt, wn, ix.cache);
-        if (i == 1) acc_r[j] = s; else acc_o[j] += s;
+        for (uint32_t j = 0; j < kItems; ++j)
+          if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + acc_r[j] + acc_o[j] + ub), doc[j]) < thr)
+            live &= ~(1u << j);
       }
     }
     uint64_t tp1 = FG_NOW();
     (void)tp1;
 
-    // survivors: lead-list score (loads first), tantivy's summation order,
-    // alive bitset, pruning threshold, append to the local top-k buffer
-    uint32_t tf0[kItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
-      const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
-      tf0[j] = (live & (1u << j)) ? ix.tf[base0 + idx] : 0u;
-      if ((live & (1u << j)) && fnp[j] == kInvalid) fnp[j] = load_fn(ix, doc[j]);
-      if ((live & (1u << j)) && ix.alive && !((ix.alive[doc[j] >> 5] >> (doc[j] & 31)) & 1u)) live &= ~(1u << j);
-    }
-    const uint64_t thr = sh.thr;
+    // survivors: tantivy's summation order, alive bitset, pruning threshold,
+    // append to the local top-k buffer
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
       bool keep = (live >> j) & 1u;
       uint64_t key = 0;
+      if (keep && ix.alive && !((ix.alive[doc[j] >> 5] >> (doc[j] & 31)) & 1u)) keep = false;
       if (keep) {
-        const float s0 = term_score(tf0[j], fnp[j], wt0, wn0, ix.cache);
-        // Intersection::score = left + right + (0.0 + others...); one term = the union itself
-        float s = m == 1 ? s0 : (s0 + acc_r[j]) + acc_o[j];
+        // one term = the union itself
+        float s = m == 1 ? s0[j] : (s0[j] + acc_r[j]) + acc_o[j];
         // with a filter: Intersection(text, facet union) = text + facet (two children)
         if (fmask) s = s + ftab[filter_bits(fmask, fshift, doc[j])];
         key = make_key(s, doc[j]);
@@ -525,7 +479,10 @@ constexpr uint32_t kMaxSeg = kMaxTiles * kMaxTerms;
 struct DisjShared {
   alignas(16) uint64_t buf[kBufD];
   union {
-    float acc[kTile];                // E: exhaustive tile scores
+    struct {
+      float acc[kTile];              // E: exhaustive tile scores
+      uint32_t hit[kTile / 32];      // E: docs matching any clause (a score may be 0)
+    } e;
     struct {
       uint64_t cand[kRound];         // P: (doc << 32) | (maybe-mask << 16) | (tile << 8) | clause
       float cand_s[kRound];          // P: the source clause's score of each candidate
@@ -544,7 +501,6 @@ struct DisjShared {
   // per-clause constants of the work item's query
   uint32_t c_meta[kMaxTerms], c_dir[kMaxTerms], c_toff[kMaxTerms];
   uint64_t c_base[kMaxTerms];
-  float c_wt[kMaxTerms], c_wn[kMaxTerms];
   uint32_t max_s, n_seg, n_post;
   uint32_t n_buf, n_cand;
   uint64_t thr;
@@ -622,8 +578,6 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     sh.c_dir[tid] = ix.dir_off[t];
     sh.c_toff[tid] = ix.toff[t];
     sh.c_base[tid] = ix.off[t];
-    sh.c_wt[tid] = ix.w_text[t];
-    sh.c_wn[tid] = ix.w_name[t];
   }
   __syncthreads();
   if (tid == 0) {
@@ -667,7 +621,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     }
     sh.r_lo[p] = lo;
     sh.r_hi[p] = hi;
-    sh.r_ub[p] = lo < hi ? ub : 0.0f;
+    sh.r_ub[p] = lo < hi ? ub : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
   }
   __syncthreads();
   FG_PHASE(0);
@@ -716,25 +670,28 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     if (sh.t_mode[t] != 1u) continue;  // uniform
     const uint32_t d0 = (tile0 + t) << kTileShift;
     const uint32_t span = min(d0 + kTile, ix.n_docs) - d0;
-    for (uint32_t x = tid; x < kTile; x += kThreads) sh.u.acc[x] = 0.0f;
+    for (uint32_t x = tid; x < kTile; x += kThreads) sh.u.e.acc[x] = 0.0f;
+    for (uint32_t x = tid; x < kTile / 32; x += kThreads) sh.u.e.hit[x] = 0u;
     __syncthreads();
     for (uint32_t i = 0; i < m; ++i) {
       const uint64_t bi = sh.c_base[i];
-      const float wt = sh.c_wt[i], wn = sh.c_wn[i];
       const uint32_t lo = sh.r_lo[t * m + i], hi = sh.r_hi[t * m + i];
       for (uint32_t p0 = lo; p0 < hi; p0 += 4 * kThreads) {
-        uint32_t dd[4], tf[4], fn[4];
+        uint32_t dd[4];
+        float ps[4];
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
           const uint32_t p = p0 + j * kThreads + tid;
           dd[j] = p < hi ? ix.doc[bi + p] : kInvalid;
-          tf[j] = p < hi ? ix.tf[bi + p] : 0u;
+          ps[j] = p < hi ? ix.psc[bi + p] : 0.0f;
         }
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) fn[j] = dd[j] != kInvalid ? load_fn(ix, dd[j]) : 0u;
-#pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
-          if (dd[j] != kInvalid) sh.u.acc[dd[j] - d0] += term_score(tf[j], fn[j], wt, wn, ix.cache);
+          if (dd[j] != kInvalid) {
+            const uint32_t x = dd[j] - d0;
+            sh.u.e.acc[x] += ps[j];
+            if (i == 0 || !((sh.u.e.hit[x >> 5] >> (x & 31)) & 1u)) atomicOr(&sh.u.e.hit[x >> 5], 1u << (x & 31));
+          }
       }
       __syncthreads();
     }
@@ -743,9 +700,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #pragma unroll
       for (uint32_t j = 0; j < kRound / kThreads; ++j) {
         const uint32_t x = r0 + j * kThreads + tid;
-        float sc = x < span ? sh.u.acc[x] : 0.0f;
+        float sc = x < span ? sh.u.e.acc[x] : 0.0f;
         uint64_t key = 0;
-        bool keep = sc > 0.0f && doc_alive(ix, d0 + x);
+        bool keep = x < span && ((sh.u.e.hit[x >> 5] >> (x & 31)) & 1u) && doc_alive(ix, d0 + x);
         if (keep && fmask) {
           const uint32_t fb = filter_bits(fmask, fshift, d0 + x);
           keep = fb != 0;
@@ -811,7 +768,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
         const uint32_t pos = sh.r_lo[t * m + c] + (e - sh.u.p.seg_start[lo]);
         const uint64_t bi = sh.c_base[c];
         const uint32_t d = ix.doc[bi + pos];
-        const float sc = term_score(ix.tf[bi + pos], load_fn(ix, d), sh.c_wt[c], sh.c_wn[c], ix.cache);
+        const float sc = ix.psc[bi + pos];
         // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
         float ub = sc + fmax;
         for (uint32_t i = 0; i < m; ++i)
@@ -823,10 +780,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
           // bound 2: the other clauses' bucket maxima at d
           float ub2 = sc + fmax;
           for (uint32_t i = 0; i < m; ++i) {
-            if (i == c || sh.r_ub[t * m + i] == 0.0f) continue;
+            if (i == c || signbit(sh.r_ub[t * m + i])) continue;
             const float b = ix.bmax[sh.c_dir[i] + (d >> (sh.c_meta[i] & 0xFFu))];
             ub2 += b;
-            maybe |= (b > 0.0f ? 1u : 0u) << i;
+            maybe |= (signbit(b) ? 0u : 1u) << i;  // bmax -0.0: empty bucket
           }
           keep = make_key(inflate_bound(ub2), d) >= thr && doc_alive(ix, d);
         }
@@ -858,13 +815,14 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     for (uint32_t c0 = 0; c0 < nc; c0 += Q) {
       const uint32_t nq_ = min(Q, nc - c0), np = nq_ * m;
       constexpr uint32_t R = kPairs / kThreads;
-      uint32_t pd[R], pc[R], tfv[R], pos[R], hi[R];
+      uint32_t pd[R], pc[R], pos[R], hi[R];
+      float pv[R];  // the clause's score at the candidate, -1 = absent
 #pragma unroll
       for (uint32_t j = 0; j < R; ++j) {
         const uint32_t p = j * kThreads + tid;
         pc[j] = kInvalid;
         pd[j] = 0;
-        tfv[j] = 0;
+        pv[j] = -1.0f;
         pos[j] = 0;
         hi[j] = 0;
         if (p < np) {
@@ -878,7 +836,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
           const uint32_t meta = sh.c_meta[pc[j]];
           const uint32_t slot = meta >> 16;
           if (slot) {
-            tfv[j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
+            pv[j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
             pc[j] |= 0x80000000u;  // resolved
           } else {
             const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[pc[j]];
@@ -902,7 +860,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       for (uint32_t j = 0; j < R; ++j) {
         if (pc[j] & 0x80000000u) continue;
         const uint64_t base = sh.c_base[pc[j]];
-        if (pos[j] < hi[j] && ix.doc[base + pos[j]] == pd[j]) tfv[j] = ix.tf[base + pos[j]];
+        if (pos[j] < hi[j] && ix.doc[base + pos[j]] == pd[j]) pv[j] = ix.psc[base + pos[j]];
       }
 #pragma unroll
       for (uint32_t j = 0; j < R; ++j) {
@@ -910,10 +868,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
         if (p >= np) continue;
         const uint32_t c = pc[j] & 0x7FFFFFFFu;
         const uint64_t cv = sh.u.p.cand[c0 + p / m];
-        float v;
-        if (c == ((uint32_t)cv & 0xFFu)) v = sh.u.p.cand_s[c0 + p / m];
-        else v = tfv[j] ? term_score(tfv[j], load_fn(ix, pd[j]), sh.c_wt[c], sh.c_wn[c], ix.cache) : 0.0f;
-        sh.u.p.cs[p] = v;
+        sh.u.p.cs[p] = c == ((uint32_t)cv & 0xFFu) ? sh.u.p.cand_s[c0 + p / m] : pv[j];
       }
       __syncthreads();
       for (uint32_t cc0 = 0; cc0 < nq_; cc0 += kThreads) {
@@ -924,12 +879,14 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
           const uint64_t cv = sh.u.p.cand[c0 + cc];
           const uint32_t t = ((uint32_t)cv >> 8) & 0xFFu, src = (uint32_t)cv & 0xFFu;
           (void)t;
-          float sc = 0.0f;  // SumCombiner from 0.0 in clause order (+0.0 for a missing clause is exact)
+          float sc = 0.0f;  // SumCombiner from 0.0 in clause order over the matching clauses
           uint32_t matched = 0;
           for (uint32_t i = 0; i < m; ++i) {
             const float v = sh.u.p.cs[cc * m + i];
-            sc += v;
-            matched |= (v > 0.0f ? 1u : 0u) << i;
+            if (v >= 0.0f) {
+              sc += v;
+              matched |= 1u << i;
+            }
           }
           // unique keys: keep the doc only from the first essential clause it matches
           const uint32_t first = (uint32_t)__builtin_ctz(matched & sh.t_ess[t]);
