@@ -151,8 +151,11 @@ def main():
         with open(pmc_file) as f:
             pmc = json.load(f)
         wl = pmc.get("workload", {})
-        if (not wl or (wl.get("n_docs") == args.docs and wl.get("batch") == nq and wl.get("k") == K
-                       and wl.get("terms") == (args.terms if not args.mixed else "1-5"))):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from lib_id import lib_id
+        same_build = pmc.get("lib_id") == lib_id()
+        if same_build and (not wl or (wl.get("n_docs") == args.docs and wl.get("batch") == nq and wl.get("k") == K
+                                      and wl.get("terms") == (args.terms if not args.mixed else "1-5"))):
             traffic = pmc.get("k_conj_hbm_bytes_per_launch")
 
     # ---- CPU baseline: the oracle (tantivy's algorithm restated in C) on host cores, rank 0, N=1 only

@@ -8,7 +8,10 @@
 namespace fg {
 
 constexpr uint32_t kBlock = 128;          // tantivy block size (bytes model only)
-constexpr uint32_t kBucketTarget = 32;    // directory: expected postings per bucket (one 128-B line)
+#ifndef FG_BUCKET
+#define FG_BUCKET 4  // tools/ab_variants.py: 32 -> 4 took k_conj 1.686 -> 1.591 ms, k_disj 22.8 -> 20.2 ms
+#endif
+constexpr uint32_t kBucketTarget = FG_BUCKET;  // directory: expected postings per bucket
 constexpr uint32_t kThreads = 256;        // 4 waves of 64 per workgroup
 #ifndef FG_ITEMS
 #define FG_ITEMS 8
@@ -45,7 +48,7 @@ constexpr uint32_t kModeOr = 1;
 // (the posting's BM25 term score) alongside, and a doc -> position directory: bucket b covers docs
 // [b << B_t, (b+1) << B_t) and dir[dir_off[t] + b] = first position in the
 // list with doc >= b << B_t (the last entry is df_t).  B_t is chosen so a
-// bucket holds ~32 postings (one 128-B line of doc ids); a probe is one
+// bucket holds ~kBucketTarget (4) postings; a probe is one
 // directory load and a <= S_t step search inside one or two lines.  Terms that
 // occur in >= 1/8 of the docs (and only in `text`) additionally get a dense
 // doc-indexed f32 score table: a probe into them is one 4-B load.

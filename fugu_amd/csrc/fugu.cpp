@@ -258,7 +258,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ix->w_name[t] = bm25_weight(g ? (g->df_name ? g->df_name[t] : 0u) : hp.df_name[t], Ns);
   }
   // doc -> position bucket directory (fg_internal.h DevIndex): bucket width
-  // 2^B_t docs with B_t the largest shift keeping ~32 postings per bucket
+  // 2^B_t docs with B_t the largest shift keeping ~kBucketTarget postings per bucket
   std::vector<uint32_t> dir_off(V), tmeta(V);
   uint64_t nd = 0;
   for (uint32_t t = 0; t < V; ++t) {
@@ -435,8 +435,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint64_t* d_foff;
   if ((rc = dev_upload(ix->mem, hp.fdoc.data(), hp.fdoc.size(), &d_fdoc, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.foff.data(), hp.foff.size(), &d_foff, &bytes))) return rc;
-  ix->d = fg::DevIndex{d_doc, d_psc, d_off, d_dir, d_dir_off, d_tmeta, d_dense, d_tmaxs, d_alive, d_bmax, d_tmax,
-                       d_toff, d_fdoc, d_foff, hp.n_docs, hp.n_terms, hp.has_name ? 1u : 0u, VF};
+  ix->d = fg::DevIndex{d_doc,  d_psc,  d_off,  d_dir,  d_dir_off, d_tmeta, d_dense,   d_tmaxs,
+                       d_alive, d_bmax, d_tmax, d_toff, d_fdoc,    d_foff,  hp.n_docs, hp.n_terms,
+                       hp.has_name ? 1u : 0u, VF};
   ix->foff = std::move(hp.foff);
   // per-term doc span (disjunctive plans skip the tiles outside it)
   ix->first_doc.assign(V, 0);

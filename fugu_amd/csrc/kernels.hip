@@ -2,20 +2,23 @@
 // posting-list intersection + BM25 + top-k.
 //
 // Pipeline per planned batch:
-//   k_conj   one workgroup per work item = (query, 2048-posting chunk of the
-//            query's lead list, the lowest-cost term).  Each lane holds 8 lead
-//            candidates.  The other lists are probed in tantivy's
-//            intersection order (query/intersection.rs: children sorted by
-//            cost) through the per-term doc -> position bucket directory: one
-//            directory load, then a fixed-step branchless search inside the
-//            bucket (~32 postings, one 128-B line), all 8 items in lockstep so
-//            their loads overlap.  Survivors are scored with tantivy's
-//            Bm25Weight f32 arithmetic in tantivy's summation order
-//            (query/bm25.rs, Intersection::score), compacted with ballot +
-//            popcount into LDS, and cut to the chunk's exact top-k by an LDS
-//            radix select over a 64-bit (score, ~doc) key.  The chunk's k-th
-//            key raises a per-query threshold (atomicMax) that later chunks
-//            use to drop hits before any selection.
+//   k_conj   one workgroup per work item = (query, group of 2048-posting
+//            chunks of the query's lead list, the lowest-cost term).  Each
+//            lane holds 8 lead candidates.  The other lists are probed in
+//            tantivy's intersection order (query/intersection.rs: children
+//            sorted by cost): a dense list through its doc-indexed score
+//            table, any other through the per-term doc -> position bucket
+//            directory (one directory load, then a branchless search inside
+//            the ~4-posting bucket), all 8 items in lockstep so their loads
+//            overlap.  Posting scores are precomputed at snapshot build with
+//            tantivy's Bm25Weight f32 arithmetic; before each probe a MaxScore
+//            bound (partial score + the remaining lists' maxima) drops
+//            candidates that cannot reach the query's threshold.  Survivors
+//            are summed in tantivy's order (Intersection::score), compacted
+//            with ballot + popcount into LDS, and cut to the work item's exact
+//            top-k by an LDS radix select over a 64-bit (score, ~doc) key.  The
+//            k-th key raises a per-query threshold (atomicMax) that later
+//            chunks use to prune.
 //   k_final  one workgroup per query: gathers the chunk hits >= the query's
 //            final threshold, exact top-k select + bitonic sort, writes
 //            (score, doc) in (score desc, doc asc) order
@@ -198,7 +201,21 @@ struct ConjShared {
   uint32_t scratch[8];
   uint32_t n_buf;
   uint64_t thr;
+#ifdef FG_DIAG
+  unsigned long long dgc[8];  // candidates alive at: load, after the first bound, after probe i (1..5)
+#endif
 };
+
+#ifdef FG_DIAG
+#define FG_COUNT(slot, mask)                                                            \
+  do {                                                                                  \
+    uint32_t c_ = 0;                                                                    \
+    _Pragma("unroll") for (uint32_t j_ = 0; j_ < kItems; ++j_) c_ += (uint32_t)__popcll(__ballot(((mask) >> j_) & 1u)); \
+    if (lane == 0 && (slot) < 8) atomicAdd(&sh.dgc[(slot)], (unsigned long long)c_);  \
+  } while (0)
+#else
+#define FG_COUNT(slot, mask) do { } while (0)
+#endif
 
 // Keep exactly the K largest of buf[0, n) at the front (n <= Cap); returns the K-th key.
 template <uint32_t Cap>
@@ -287,14 +304,22 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     ftab = pl.f.f_tab + (size_t)fslot * 256;
     fmax = pl.f.f_max[fslot];
   }
+  // Threshold exchange without a blocking round trip: thread 0's returning
+  // atomicMax (served at the memory side, so it sees every XCD's publications;
+  // a plain or sc1 load could hit a stale L2 line) is issued at the end of a
+  // chunk and its result folded in at the start of the next one, after that
+  // chunk's lead loads are in flight.  A stale threshold is still a valid lower
+  // bound of the query's k-th key (values only grow), so pruning stays exact.
+  uint64_t pend = 0;
   if (tid == 0) {
     sh.n_buf = 0;
-    // returning atomic: served at the memory side, so it sees every other
-    // XCD's atomicMax (a plain or sc1 load could hit a stale L2 line)
-    sh.thr = atomicMax(gthr, 0ull);
+    sh.thr = 0;
+    pend = atomicMax(gthr, 0ull);
   }
+#ifdef FG_DIAG
+  if (tid < 8) sh.dgc[tid] = 0;
+#endif
   uint64_t local_T = 0;
-  __syncthreads();
 
   for (uint32_t cc = 0; cc < nc; ++cc) {
     const uint32_t c = c0 + cc;
@@ -302,14 +327,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     const uint32_t cnt = min(kChunk, lead_df - c * kChunk);
     uint64_t tp0 = FG_NOW();
     (void)tp0;
-    const uint64_t thr = sh.thr;
-    // MaxScore (uniform): once the query has a threshold, a candidate whose
-    // partial score plus the remaining lists' maxima cannot reach it is dropped
-    // before the next probe.  Bounds are inflated by 2^-17 (inflate_bound).
-    const bool prune = thr != 0 && m > 1;
     // lead candidates: item j of lane l = wv*512 + j*64 + l (coalesced per j)
     uint32_t doc[kItems];
-    float s0[kItems], acc_r[kItems], acc_o[kItems];
+    float s0[kItems];
     uint32_t live = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
@@ -318,28 +338,44 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       doc[j] = in ? ix.doc[base0 + idx] : kInvalid;
       s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
       live |= (in ? 1u : 0u) << j;
-      acc_r[j] = 0.0f;
-      acc_o[j] = 0.0f;
     }
+    if (tid == 0 && pend > sh.thr) sh.thr = pend;
+    __syncthreads();
+    const uint64_t thr = sh.thr;
+    // MaxScore (uniform): once the query has a threshold, a candidate whose
+    // partial score plus the remaining lists' maxima cannot reach it is dropped
+    // before the next probe.  Bounds are inflated by 2^-17 (inflate_bound).
+    const bool prune = thr != 0 && m > 1;
     if (fmask) {
       // the facet mask: one L2-resident bit probe drops a candidate before any list probe
 #pragma unroll
       for (uint32_t j = 0; j < kItems; ++j)
         if ((live & (1u << j)) && !filter_bits(fmask, fshift, doc[j])) live &= ~(1u << j);
     }
+    FG_COUNT(0, live);
+    if (!prune) FG_COUNT(7, live);  // candidates of chunks that start with no threshold
     if (prune) {
       const float ub = qub[1] + fmax;
 #pragma unroll
       for (uint32_t j = 0; j < kItems; ++j)
         if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + ub), doc[j]) < thr) live &= ~(1u << j);
     }
+    FG_COUNT(1, live);
 
+    // every list probed in intersection order; a candidate whose partial score
+    // plus the remaining lists' maxima cannot reach the threshold is dropped
+    // before the next probe
+    float acc_r[kItems], acc_o[kItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; ++j) {
+      acc_r[j] = 0.0f;
+      acc_o[j] = 0.0f;
+    }
     for (uint32_t i = 1; i < m; ++i) {
       if (!__any(live != 0)) break;  // wave-uniform early exit
       const uint32_t ti = terms[i];
-      const uint64_t bi = ix.off[ti];
       const uint32_t meta = ix.tmeta[ti];
-      const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu, dslot = meta >> 16;
+      const uint32_t dslot = meta >> 16;
       float sc[kItems];
       if (dslot) {
         // dense term: doc-indexed score table, one 4-B load per item (-1 = absent)
@@ -347,6 +383,8 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) sc[j] = (live & (1u << j)) ? dt[doc[j]] : -1.0f;
       } else {
+        const uint64_t bi = ix.off[ti];
+        const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu;
         const uint32_t* __restrict__ di = ix.doc + bi;
         const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[ti];
         // bucket of each live item, then a branchless power-of-two search in it
@@ -388,6 +426,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
           if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + acc_r[j] + acc_o[j] + ub), doc[j]) < thr)
             live &= ~(1u << j);
       }
+      FG_COUNT(1 + i, live);
     }
     uint64_t tp1 = FG_NOW();
     (void)tp1;
@@ -419,13 +458,14 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
 #ifdef FG_DIAG
     t_probe += tp1 - tp0; t_keys += tp2 - tp1; t_sel += tp3 - tp2; n_app += n;
 #endif
-    // publish the local k-th key, read the best published one
+    // publish the local k-th key; its reply (the best published one) is read next chunk
     if (tid == 0) {
-      const uint64_t old = atomicMax(gthr, (unsigned long long)local_T);
-      sh.thr = old > local_T ? old : local_T;
+      if (local_T > sh.thr) sh.thr = local_T;
+      pend = atomicMax(gthr, (unsigned long long)local_T);
     }
-    __syncthreads();
   }
+  if (tid == 0 && pend > sh.thr) sh.thr = pend;
+  __syncthreads();
 
   // write the kept keys that still clear the freshest threshold
   const uint32_t total = flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
@@ -438,6 +478,10 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   FG_STAMP(w, 5, n_app);
   FG_STAMP(w, 6, ((uint64_t)nc << 40) | ((uint64_t)m << 32) | q);
   FG_STAMP(w, 7, total);
+#ifdef FG_DIAG
+  __syncthreads();
+  for (uint32_t i = 0; i < 8; ++i) FG_STAMP(w, 8 + i, sh.dgc[i]);
+#endif
 }
 
 // ---------------------------------------------------------------- k_disj

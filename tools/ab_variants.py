@@ -26,8 +26,11 @@ def child(args):
     corp = synth.corpus(args.docs, threads=16)
     ix = native.Index.from_docs(ctx, corp.off, corp.tok, synth.VOCAB, threads=16, keep_host=False)
     m_min, m_max = (1, 5) if args.mixed else (args.terms, args.terms)
+    mode = native.MODE_AND
+    if args.disj:  # config C5 shape: 2-5 bare terms (Should), k = 1000
+        m_min, m_max, mode = 2, 5, native.MODE_OR
     q_off, terms = synth.queries(args.batch, m_min, m_max)
-    plan = ix.plan(q_off, terms, args.k)
+    plan = ix.plan(q_off, terms, args.k, mode)
     for _ in range(2):
         plan.execute()
     plan.results()
@@ -54,6 +57,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--terms", type=int, default=3)
     ap.add_argument("--mixed", action="store_true")
+    ap.add_argument("--disj", action="store_true", help="OR queries (k_disj), use with --k 1000")
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
@@ -70,6 +74,8 @@ def main():
                    "--terms", str(args.terms), "--k", str(args.k), "--steps", str(args.steps)]
             if args.mixed:
                 cmd.append("--mixed")
+            if args.disj:
+                cmd.append("--disj")
             out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if out.returncode != 0:
                 print(json.dumps({"lib": lib, "error": out.stderr[-800:]}), flush=True)

@@ -56,6 +56,8 @@ def main():
             "select_us_sum": round(float(c_sel.sum() * us), 1),
             "appended_per_chunk": pct(conj[:, 5].astype(np.float64) / np.maximum(nchk, 1)),
             "written_total": int(conj[:, 7].sum()),
+            # candidates alive at: lead load, after the first MaxScore bound, after probe i
+            "alive_lead_b1_p1_p2_p3": [int(conj[:, 8 + i].sum()) for i in range(5)], "lead_unpruned": int(conj[:, 15].sum()),
         },
     }
     f_start, f_read, f_sel, f_end = (fin[:, i].astype(np.int64) for i in range(4))

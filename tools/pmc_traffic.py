@@ -29,7 +29,7 @@ def read_counters(d, counter):
 
 
 def short(name):
-    for k in ("k_conj", "k_filter", "k_final", "k_merge", "stream16", "stream4"):
+    for k in ("k_conj", "k_disj", "k_scan", "k_fmask", "k_final", "k_merge", "stream16", "stream4"):
         if k in name:
             return k
     return name[:40]
@@ -56,6 +56,11 @@ def main():
     kc = res["kernels"].get("k_conj")
     if kc:
         res["k_conj_hbm_bytes_per_launch"] = kc["fetch_bytes_corrected"] + kc["write_bytes"]
+    # the library the counters were taken on: bench.py only quotes this traffic
+    # for the same build (tools/lib_id.py)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from lib_id import lib_id
+    res["lib_id"] = lib_id()
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))

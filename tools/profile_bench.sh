@@ -11,7 +11,7 @@ TAG=${1:-r01}
 shift || true
 # --p50-queries 0: only the batch dispatches, so the trace's average k_conj
 # duration is the batch kernel the bench's roofline line is computed on
-ARGS="--steps 5 --warmup 1 --no-cpu --p50-queries 0 $*"
+ARGS="--steps 5 --warmup 1 --no-cpu --p50-queries 0 --no-extra $*"
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
