@@ -25,10 +25,20 @@ constexpr uint32_t kWaveSpan = kChunk / 4;       // 512 consecutive candidates p
 constexpr uint32_t kMaxTerms = 16;        // terms per query (FG_MAX_TERMS)
 constexpr uint32_t kMaxK = 1024;          // largest top-k the device select supports
 constexpr uint32_t kFinalCap = 8192;      // candidates kept in LDS by the final select
-constexpr uint32_t kDenseDiv = 8;         // terms in >= 1/8 of the docs also get a dense tf table
+#ifndef FG_DENSE_DIV
+#define FG_DENSE_DIV 8
+#endif
+#ifndef FG_DENSE_GIB
+#define FG_DENSE_GIB 64
+#endif
+constexpr uint32_t kDenseDiv = FG_DENSE_DIV;  // terms in >= 1/kDenseDiv of the docs get a dense score table
+constexpr uint64_t kDenseBudget = (uint64_t)FG_DENSE_GIB << 30;  // ... densest first, within this many bytes
 constexpr uint32_t kMaxDense = 4096;      // at most this many dense tables per index
 constexpr uint32_t kGroupsPerQuery = 64;  // a query's chunks are split into ~this many work items
-constexpr uint32_t kMaxGroup = 16;        // ... of at most this many chunks each
+#ifndef FG_MAXGROUP
+#define FG_MAXGROUP 16
+#endif
+constexpr uint32_t kMaxGroup = FG_MAXGROUP;  // ... of at most this many chunks each
 constexpr uint32_t kHistBins = 2048;      // 11-bit radix digits
 constexpr uint32_t kDisjTileShift = 12;   // k_disj: 4096-doc tiles
 constexpr uint32_t kDisjMaxGroup = 32;    // ... at most this many tiles per work item
@@ -155,6 +165,7 @@ hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s);
+hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

@@ -355,27 +355,28 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       }
     }
   });
-  // dense doc-indexed tf tables for the densest text-only terms
+  // dense doc-indexed score tables (DevIndex::dense) for the densest terms:
+  // df >= N / kDenseDiv, densest first (ties by term id), within kDenseBudget
+  // and a quarter of the device's free memory.  A table holds the posting
+  // scores psc[] (the text + name union), so name terms qualify too.  The
+  // tables are filled on the device from the uploaded postings (k_dense).
   std::vector<uint32_t> dense_terms;
-  for (uint32_t t = 0; t < V && dense_terms.size() < fg::kMaxDense; ++t) {
+  for (uint32_t t = 0; t < V; ++t) {
     const uint64_t n = hp.off[t + 1] - hp.off[t];
-    if (n * fg::kDenseDiv >= N && hp.df_name[t] == 0) dense_terms.push_back(t);
+    if (n > 0 && n * fg::kDenseDiv >= N) dense_terms.push_back(t);
   }
-  std::vector<float> dense;
-  try {
-    dense.assign(dense_terms.size() * (size_t)N, -1.0f);  // -1: absent (a score is >= 0, and may be 0)
-  } catch (...) {
-    return fail(FG_EOOM, "dense tables (%zu terms) allocation failed", dense_terms.size());
+  std::stable_sort(dense_terms.begin(), dense_terms.end(), [&](uint32_t a, uint32_t b) {
+    return hp.off[a + 1] - hp.off[a] > hp.off[b + 1] - hp.off[b];
+  });
+  {
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipSetDevice(dev));
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t budget = std::min<uint64_t>(fg::kDenseBudget, free_b / 4);
+    const uint64_t cap = std::min<uint64_t>(fg::kMaxDense, budget / (N * sizeof(float)));
+    if (dense_terms.size() > cap) dense_terms.resize(cap);
   }
-  parallel_ranges((uint32_t)dense_terms.size(), std::min<int>(hw_threads(0), (int)dense_terms.size()),
-                  [&](int, uint32_t a, uint32_t e) {
-                    for (uint32_t s = a; s < e; ++s) {
-                      const uint32_t t = dense_terms[s];
-                      float* row = dense.data() + (size_t)s * N;
-                      for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) row[hp.doc[p]] = psc[p];
-                      tmeta[t] |= (s + 1) << 16;
-                    }
-                  });
+  for (uint32_t s = 0; s < dense_terms.size(); ++s) tmeta[dense_terms[s]] |= (s + 1) << 16;
   ix->n_dense = (uint32_t)dense_terms.size();
   // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
   // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
@@ -427,8 +428,22 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   std::vector<float>().swap(tmax);
   if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, dense.data(), dense.size(), &d_dense, &bytes))) return rc;
-  std::vector<float>().swap(dense);
+  {
+    const size_t cnt = std::max<size_t>((size_t)N * dense_terms.size(), 4);
+    void* p = nullptr;
+    if (hipMalloc(&p, cnt * sizeof(float)) != hipSuccess)
+      return fail(FG_EOOM, "dense tables (%zu terms) hipMalloc failed", dense_terms.size());
+    ix->mem.ptrs.push_back(p);
+    bytes += cnt * sizeof(float);
+    d_dense = static_cast<float*>(p);
+    HIPCHK(hipMemsetD32(p, (int)0xBF800000u, cnt));  // -1.0f: absent (a score is >= 0, and may be 0)
+    for (uint32_t s = 0; s < dense_terms.size(); ++s) {
+      const uint32_t t = dense_terms[s];
+      HIPCHK(fg::launch_dense(d_doc, d_psc, hp.off[t], (uint32_t)(hp.off[t + 1] - hp.off[t]), d_dense + (size_t)s * N,
+                              nullptr));
+    }
+    HIPCHK(hipStreamSynchronize(nullptr));
+  }
   ix->tmaxs = std::move(tmaxs);
   if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
   uint32_t* d_fdoc;
