@@ -26,7 +26,7 @@ constexpr uint32_t kMaxTerms = 16;        // terms per query (FG_MAX_TERMS)
 constexpr uint32_t kMaxK = 1024;          // largest top-k the device select supports
 constexpr uint32_t kFinalCap = 8192;      // candidates kept in LDS by the final select
 #ifndef FG_DENSE_DIV
-#define FG_DENSE_DIV 8
+#define FG_DENSE_DIV 256  // tools/ab_variants.py sweep 8..512: DESIGN.md §3
 #endif
 #ifndef FG_DENSE_GIB
 #define FG_DENSE_GIB 64
