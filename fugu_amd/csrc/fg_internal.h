@@ -60,8 +60,8 @@ constexpr uint32_t kModeOr = 1;
 // list with doc >= b << B_t (the last entry is df_t).  B_t is chosen so a
 // bucket holds ~kBucketTarget (4) postings; a probe is one
 // directory load and a <= S_t step search inside one or two lines.  Terms that
-// occur in >= 1/8 of the docs (and only in `text`) additionally get a dense
-// doc-indexed f32 score table: a probe into them is one 4-B load.
+// occur in >= 1/kDenseDiv of the docs additionally get a dense doc-indexed f32
+// score table (densest first, within kDenseBudget): a probe is one 4-B load.
 struct DevIndex {
   const uint32_t* doc;       // [P] doc ids, CSR by term, ascending within a term
   const float* psc;          // [P] the posting's term score: Should(text:t, name:t) in the doc, i.e.
