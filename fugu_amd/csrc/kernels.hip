@@ -823,13 +823,17 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
         if (keep && fmask) keep = filter_bits(fmask, fshift, d) != 0;
         uint32_t maybe = 0;  // clauses whose bucket at d holds postings (the rest cannot match d)
         if (keep) {
-          // bound 2: the other clauses' bucket maxima at d
+          // bound 2: the other clauses at d -- the exact score from a dense
+          // table (-1.0: absent), else the bucket maximum (-0.0: empty bucket)
           float ub2 = sc + fmax;
           for (uint32_t i = 0; i < m; ++i) {
             if (i == c || signbit(sh.r_ub[t * m + i])) continue;
-            const float b = ix.bmax[sh.c_dir[i] + (d >> (sh.c_meta[i] & 0xFFu))];
+            const uint32_t meta = sh.c_meta[i], slot = meta >> 16;
+            const float b = slot ? ix.dense[(size_t)(slot - 1) * ix.n_docs + d]
+                                 : ix.bmax[sh.c_dir[i] + (d >> (meta & 0xFFu))];
+            if (signbit(b)) continue;  // clause i cannot match d
             ub2 += b;
-            maybe |= (signbit(b) ? 0u : 1u) << i;  // bmax -0.0: empty bucket
+            maybe |= 1u << i;
           }
           keep = make_key(inflate_bound(ub2), d) >= thr && doc_alive(ix, d);
         }
