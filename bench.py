@@ -31,6 +31,44 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def host_cores():
+    """The host CPU share this process may use (T = nproc on the box).
+    nproc honours OMP_NUM_THREADS (16 on the GPU box = its CPU share per GPU);
+    the affinity mask and the cgroup quota are reported beside it."""
+    import subprocess
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout.strip())
+    except Exception:
+        nproc = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    return {"nproc": nproc, "affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+            "cgroup_cpus": quota}
+
+
+def native_oracle():
+    """Compile the CPU baseline (oracle/fugu_oracle.c) for THIS host with
+    -march=native and point oracle.py at it; returns the flags."""
+    import subprocess
+    import tempfile
+    d = tempfile.mkdtemp(prefix="fugu_oracle_")
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", f"OUT={d}"],
+                       capture_output=True, text=True)
+    lib = os.path.join(d, "libfugu_oracle_native.so")
+    if r.returncode == 0 and os.path.exists(lib):
+        os.environ["FUGU_ORACLE_LIB"] = lib
+        from oracle import oracle as orc
+        return orc.NATIVE_FLAGS
+    log(f"[bench] native oracle build failed ({r.stderr[-300:]}); using the portable build")
+    return "-O3 -ffp-contract=off -march=x86-64-v2 (portable build: native compile failed)"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,7 +107,8 @@ def main():
 
     from fugu_amd import native, synth
 
-    threads = args.threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 8, 16)
+    cores = host_cores()
+    threads = args.threads or cores["nproc"]
     t0 = time.time()
     # namespace r: its own corpus (seeds offset by rank); rank 0 is the standard corpus
     corp = synth.corpus(args.docs, synth.VOCAB, 1.0, synth.SEED_L + rank, synth.SEED_T + rank, threads=threads)
@@ -137,15 +176,21 @@ def main():
         lat.append(time.perf_counter() - t1)
     p50_ms = float(np.median(lat) * 1e3) if lat else None
 
-    # ---- roofline of the dominant kernel (k_conj), SURVEY.md §8(d) algorithmic bytes
+    # ---- roofline of the dominant kernel (k_conj): algorithmic bytes at the HBM
+    # layout (fg_bytes_model_gpu: k_conj's exhaustive cascade) over
+    # its HIP-event time on the launch stream.  The SURVEY 8(d) tantivy byte
+    # model (1 KiB block decode per probed block) is reported beside it, labelled.
+    bmg = ix.bytes_model_gpu(q_off, terms, K)
+    alg_bytes = float(bmg[:, 3].sum())
     bm = ix.bytes_model(q_off, terms, K)
-    alg_bytes = float(bm[:, 2].sum())
+    cpu_model_bytes = float(bm[:, 2].sum())
     conj_ms = ms_k[0] / max(n_prof, 1)
     achieved = alg_bytes / (conj_ms * 1e-3) / 1e9
-    # HBM bytes per k_conj launch from rocprofv3 PMC (FETCH_SIZE x2 gfx950
-    # correction + WRITE_SIZE), collected by tools/profile_bench.sh on this
-    # exact workload and committed under profiles/ (profiles/latest.json)
-    traffic = None
+    # HBM bytes per k_conj launch from rocprofv3 PMC (FETCH_SIZE with the
+    # gather-calibrated gfx950 correction + WRITE_SIZE), collected by
+    # tools/profile_bench.sh on this exact workload and build, committed under
+    # profiles/ (profiles/latest.json)
+    traffic, pmc = None, {}
     pmc_file = os.environ.get("FUGU_PMC_BYTES") or os.path.join(ROOT, "profiles", "latest.json")
     if os.path.exists(pmc_file):
         with open(pmc_file) as f:
@@ -157,8 +202,13 @@ def main():
         if same_build and (not wl or (wl.get("n_docs") == args.docs and wl.get("batch") == nq and wl.get("k") == K
                                       and wl.get("terms") == (args.terms if not args.mixed else "1-5"))):
             traffic = pmc.get("k_conj_hbm_bytes_per_launch")
+        else:
+            log(f"[bench] {pmc_file} does not match this build/workload: roofline.traffic = null")
 
-    # ---- CPU baseline: the oracle (tantivy's algorithm restated in C) on host cores, rank 0, N=1 only
+    # ---- CPU baseline: the oracle (tantivy's algorithm restated in C, compiled
+    # -march=native on this host) on T = nproc host threads, each running whole
+    # queries (a tokio worker per request, tantivy's single-threaded executor),
+    # plus a T = 1 row; rank 0, N = 1 only, bounded samples of the same batch
     cpu = None
     parity = None
     ref = None
@@ -166,39 +216,45 @@ def main():
     d_gpu = out_d.cpu().numpy().view(np.uint32).reshape(nq, K)
     n_gpu = out_n.cpu().numpy()
     if rank == 0 and world == 1 and not args.no_cpu:
+        flags = native_oracle()
         from oracle import oracle as orc
         t0 = time.time()
         ref = orc.OracleIndex(synth.VOCAB, corp.off, corp.tok, threads=threads)
-        log(f"[bench] oracle index built in {time.time() - t0:.1f}s")
-        done, wall, lats = 0, 0.0, []
-        mism = 0
-        while done < nq and wall < args.cpu_seconds:
-            hi = min(nq, done + 128)
-            sub_off = (q_off[done:hi + 1] - q_off[done]).astype(np.uint32)
-            sub_terms = terms[q_off[done]:q_off[hi]]
-            rs, rd, rn, w, l = ref.search_batch(sub_off, sub_terms, K, threads=threads, latencies=True)
-            wall += w
-            lats.append(l)
-            for j in range(hi - done):
-                i = done + j
-                m = int(rn[j])
-                if (int(n_gpu[i]) != m or not np.array_equal(d_gpu[i, :m], rd[j, :m])
-                        or not np.allclose(s_gpu[i, :m], rs[j, :m], rtol=1e-5, atol=0)):
-                    mism += 1
-            done = hi
-        lat_all = np.concatenate(lats)
+        log(f"[bench] oracle index built in {time.time() - t0:.1f}s ({flags})")
+
+        def cpu_run(T, budget, step):
+            done, wall, lats, mism = 0, 0.0, [], 0
+            while done < nq and wall < budget:
+                hi = min(nq, done + step)
+                sub_off = (q_off[done:hi + 1] - q_off[done]).astype(np.uint32)
+                rs, rd, rn, w, l = ref.search_batch(sub_off, terms[q_off[done]:q_off[hi]], K, threads=T,
+                                                    latencies=True)
+                wall += w
+                lats.append(l)
+                for j in range(hi - done):
+                    i, m = done + j, int(rn[j])
+                    if (int(n_gpu[i]) != m or not np.array_equal(d_gpu[i, :m], rd[j, :m])
+                            or not np.allclose(s_gpu[i, :m], rs[j, :m], rtol=1e-5, atol=0)):
+                        mism += 1
+                done = hi
+            return done, wall, float(np.median(np.concatenate(lats))) * 1e-6, mism
+
+        done, wall, p50_cpu, mism = cpu_run(threads, args.cpu_seconds, 128)
+        d1, w1, p1, m1 = cpu_run(1, args.cpu_seconds / 4, 16)
         cpu = {"value": round(done / wall, 2), "unit": "queries/s", "cores": threads, "kind": "port",
                "sample": f"first {done} queries of the same 1024-query batch, {threads} threads x whole queries, "
                          f"warm in-RAM index (tantivy 0.24.1 algorithm restated in C: oracle/fugu_oracle.c)",
-               "p50_ms": round(float(np.median(lat_all)) * 1e-6, 4)}
-        parity = {"queries_checked": done, "mismatches": mism, "rule": "doc ids exact, scores rtol 1e-5"}
+               "p50_ms": round(p50_cpu, 4), "compile": f"gcc {flags}", "host": cores,
+               "t1": {"value": round(d1 / w1, 2), "unit": "queries/s", "cores": 1, "p50_ms": round(p1, 4),
+                      "sample": f"first {d1} queries of the batch, 1 thread"}}
+        parity = {"queries_checked": done, "mismatches": mism + m1, "rule": "doc ids exact, scores rtol 1e-5"}
 
     # ---- secondary workloads on the same index (rank 0, N=1): SURVEY §8(d) C3 and the
     # disjunctive C5 query shape (k_disj), each timed the same way and parity-sampled
     extra = None
     if rank == 0 and world == 1 and not args.no_extra:
         extra = {}
-        specs = [("C3_mixed_and", 1, 5, 100, native.MODE_AND), ("C5_or_top1000", 2, 5, 1000, native.MODE_OR)]
+        specs = [("C3_mixed_and", 1, 5, 100, native.MODE_AND), ("OR_top1000_10M", 2, 5, 1000, native.MODE_OR)]
         for name, a_min, a_max, kk, mode in specs:
             qo_all, qt_all = synth.queries(4096, a_min, a_max)
             qo = qo_all[: nq + 1].copy()
@@ -280,9 +336,19 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "k_conj", "kernel_ms": round(conj_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
-                "alg_model": "SURVEY.md 8(d) B(q): tantivy block-decode bytes (1 KiB per probed 128-posting block)",
+                "alg_model": "fg_bytes_model_gpu: k_conj's exhaustive cascade at the HBM layout (8 B per lead "
+                             "posting; per probe 4 B dense element, or 8 B bucket bounds + 4 B per search step + "
+                             "4 B compare + 4 B score on a hit; 8 B per kept key)",
+                "alg_bytes_split": {"lead": float(bmg[:, 0].sum()), "probe": float(bmg[:, 1].sum()),
+                                    "output": float(bmg[:, 2].sum())},
+                "traffic_over_alg": round(traffic / alg_bytes, 3) if traffic else None,
+                "traffic_source": pmc.get("source") if traffic else None,
                 "hbm_gbs_measured": (round(traffic / (conj_ms * 1e-3) / 1e9, 1) if traffic else None),
                 "hbm_frac_measured": (round(traffic / (conj_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None),
+                "cpu_model_bytes_per_launch": cpu_model_bytes,
+                "cpu_model": "SURVEY.md 8(d) B(q): tantivy's CPU walk (1 KiB block decode per probed 128-posting "
+                             "block); not bytes this layout reads",
+                "cpu_model_gbs": round(cpu_model_bytes / (conj_ms * 1e-3) / 1e9, 1),
             },
             "kernels_ms_per_step": {"k_conj": round(ms_k[0] / max(n_prof, 1), 4),
                                     "k_final": round(ms_k[1] / max(n_prof, 1), 4)},

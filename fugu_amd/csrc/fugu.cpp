@@ -153,6 +153,52 @@ struct fg_ctx {
   std::vector<int> devs;
 };
 
+// Plan workspaces of one index, recycled across batches (a server plans a new
+// batch every few ms; a hipMalloc/hipFree pair per batch would serialise the
+// device).  Buffers are reused when they fit a request within 2x; at most
+// kPoolKeep bytes stay cached.
+struct WsPool {
+  static constexpr size_t kPoolKeep = 1ull << 30;
+  std::mutex mu;
+  std::multimap<size_t, void*> free_bufs;
+  size_t cached = 0;
+  int dev = 0;
+  void* get(size_t bytes, size_t* got) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      auto it = free_bufs.lower_bound(bytes);
+      if (it != free_bufs.end() && it->first <= 2 * bytes) {
+        void* p = it->second;
+        *got = it->first;
+        cached -= it->first;
+        free_bufs.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    *got = bytes;
+    return p;
+  }
+  void put(void* p, size_t bytes) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (cached + bytes <= kPoolKeep) {
+        free_bufs.emplace(bytes, p);
+        cached += bytes;
+        return;
+      }
+    }
+    (void)hipSetDevice(dev);
+    (void)hipFree(p);
+  }
+  ~WsPool() {
+    if (free_bufs.empty()) return;
+    (void)hipSetDevice(dev);
+    for (auto& kv : free_bufs) (void)hipFree(kv.second);
+  }
+};
+
 struct fg_index {
   std::atomic<int> refs{1};
   int dev = 0;
@@ -170,7 +216,8 @@ struct fg_index {
   std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
   std::vector<float> tmaxs; // [V] largest posting score per term
   std::vector<float> w_text, w_name;
-  std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model
+  std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model / fg_bytes_model_gpu
+  std::vector<uint32_t> tmeta;  // host copy of DevIndex::tmeta (probe kind of each term)
   // facet field (FG_FIELD_FACET)
   uint32_t n_fterms = 0;
   uint64_t tot_f = 0;
@@ -180,6 +227,7 @@ struct fg_index {
   std::vector<float> fscore;    // a facet clause's score in a doc holding the term (tf 1, fieldnorm id 1)
   fg::DevIndex d{};
   DevAllocs mem;
+  WsPool pool;  // plan workspaces (destroyed before mem: declared after it)
 };
 
 struct fg_plan {
@@ -187,6 +235,8 @@ struct fg_plan {
   uint32_t nq = 0, k = 0, total_chunks = 0, n_scan = 0;
   int mode = FG_MODE_AND;
   fg::DevPlan d{};
+  void* ws = nullptr;  // workspace from ix->pool
+  size_t ws_got = 0;
   float* own_score = nullptr;
   uint32_t* own_doc = nullptr;
   uint32_t* own_n = nullptr;
@@ -202,8 +252,14 @@ struct fg_plan {
   uint32_t n_prof = 0;
   ~fg_plan() {
     for (hipEvent_t e : pending) (void)hipEventDestroy(e);
+    if (ws) {
+      // the workspace may still be read by this plan's last launch
+      if (last_stream_used) (void)hipStreamSynchronize(last_stream);
+      ix->pool.put(ws, ws_got);
+    }
     if (ix) fg_index_release(ix);
   }
+  bool last_stream_used = false;
 };
 
 namespace {
@@ -237,6 +293,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   auto ix = std::make_unique<fg_index>();
   ix->dev = dev;
   ix->mem.dev = dev;
+  ix->pool.dev = dev;
   ix->n_docs = hp.n_docs;
   ix->n_terms = hp.n_terms;
   ix->has_name = hp.has_name;
@@ -428,6 +485,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   std::vector<float>().swap(tmax);
   if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
+  ix->tmeta = tmeta;
   {
     const size_t cnt = std::max<size_t>((size_t)N * dense_terms.size(), 4);
     void* p = nullptr;
@@ -769,12 +827,17 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
 int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out) {
   if (!ctx || !in || !out || !in->term_off || !in->fn_text) return fail(FG_EINVAL, "bad arguments");
   if (in->n_docs == 0 || in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs out of range");
+  if (in->term_off[0] != 0) return fail(FG_EINVAL, "term_off[0] must be 0");
+  if (in->term_off[in->n_terms] > 0 && (!in->doc || (!in->tf_text && !in->tf_name)))
+    return fail(FG_EINVAL, "postings without doc ids or term frequencies");
   if (std::find(ctx->devs.begin(), ctx->devs.end(), dev) == ctx->devs.end())
     return fail(FG_EINVAL, "device %d not in context", dev);
   HostPostings hp;
   const uint32_t N = in->n_docs, V = in->n_terms;
   hp.n_docs = N;
   hp.n_terms = V;
+  for (uint32_t t = 0; t < V; ++t)
+    if (in->term_off[t + 1] < in->term_off[t]) return fail(FG_EINVAL, "term_off not monotone at %u", t);
   hp.off.assign(in->term_off, in->term_off + V + 1);
   const uint64_t P = hp.off[V];
   hp.doc.assign(in->doc, in->doc + P);
@@ -782,7 +845,6 @@ int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** ou
   hp.df_text.assign(V, 0);
   hp.df_name.assign(V, 0);
   for (uint32_t t = 0; t < V; ++t) {
-    if (hp.off[t + 1] < hp.off[t]) return fail(FG_EINVAL, "term_off not monotone at %u", t);
     for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) {
       uint32_t tt = in->tf_text ? in->tf_text[p] : 0, tn = in->tf_name ? in->tf_name[p] : 0;
       if (!tt && !tn) return fail(FG_EINVAL, "posting %llu has tf 0 in both fields", (unsigned long long)p);
@@ -1100,10 +1162,11 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
 #endif
   const size_t total = s_in + s_thr + s_cc + s_mask + s_ck + s_os + s_od + s_on + s_dg;
   HIPCHK(hipSetDevice(ix->dev));
-  char* base = nullptr;
-  if (hipMalloc((void**)&base, std::max<size_t>(total, 256)) != hipSuccess)
-    return fail(FG_EOOM, "plan workspace hipMalloc(%zu) failed", total);
-  p->mem.ptrs.push_back(base);
+  char* base = static_cast<char*>(ix->pool.get(std::max<size_t>(total, 256), &p->ws_got));
+  if (!base) return fail(FG_EOOM, "plan workspace hipMalloc(%zu) failed", total);
+  p->ws = base;
+  p->ix = ix;  // owns the workspace from here on (returned to ix->pool); retained below
+  fg_index_retain(ix);
   p->ws_bytes = total;
   std::vector<char> staging(s_in, 0);
   size_t o = 0;
@@ -1158,8 +1221,6 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.mode = (uint32_t)q->mode;
   p->d.f.n_filters = nf;
   p->d.f.n_chunks = (uint32_t)nch;
-  fg_index_retain(ix);
-  p->ix = ix;
   *out = p.release();
   return FG_OK;
 }
@@ -1188,17 +1249,20 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
     p->pending.insert(p->pending.end(), ev, ev + 3);
   }
   p->last_stream = s;
+  p->last_stream_used = true;
   return FG_OK;
 }
 
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n) {
   if (!p) return fail(FG_EINVAL, "NULL plan");
   HIPCHK(hipSetDevice(p->ix->dev));
-  HIPCHK(hipStreamSynchronize(p->last_stream));
+  // copies on the plan's stream (a per-thread stream under fg_search_batch), then wait for it
   const size_t nk = (size_t)p->nq * p->k;
-  if (out_score) HIPCHK(hipMemcpy(out_score, p->own_score, 4 * nk, hipMemcpyDeviceToHost));
-  if (out_doc) HIPCHK(hipMemcpy(out_doc, p->own_doc, 4 * nk, hipMemcpyDeviceToHost));
-  if (out_n) HIPCHK(hipMemcpy(out_n, p->own_n, 4ull * p->nq, hipMemcpyDeviceToHost));
+  hipStream_t s = p->last_stream;
+  if (out_score) HIPCHK(hipMemcpyAsync(out_score, p->own_score, 4 * nk, hipMemcpyDeviceToHost, s));
+  if (out_doc) HIPCHK(hipMemcpyAsync(out_doc, p->own_doc, 4 * nk, hipMemcpyDeviceToHost, s));
+  if (out_n) HIPCHK(hipMemcpyAsync(out_n, p->own_n, 4ull * p->nq, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   return FG_OK;
 }
 
@@ -1261,7 +1325,9 @@ int fg_search_batch(fg_index* ix, const fg_query_batch* q, uint32_t k, float* ou
   int rc = fg_plan_create(ix, q, k, &p);
   if (rc) return rc;
   std::unique_ptr<fg_plan> guard(p);
-  if ((rc = fg_plan_execute(p, nullptr, nullptr, nullptr, nullptr))) return rc;
+  // the calling thread's own stream: concurrent callers (tokio workers sharing
+  // one Arc<Dataset>, src/db/config.rs:93) run their batches side by side
+  if ((rc = fg_plan_execute(p, hipStreamPerThread, nullptr, nullptr, nullptr))) return rc;
   return fg_plan_results(p, out_score, out_doc, out_n);
 }
 
@@ -1328,6 +1394,95 @@ int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, doub
     o[2] = std::min(bmerge, bskip) + F * ns + 8.0 * std::min<double>(ns, k);
     o[3] = ns;
   }
+  return FG_OK;
+}
+
+// ---------------------------------------------------------------- bytes model at the device layout
+// The bytes k_conj's exhaustive cascade reads at this snapshot's HBM layout
+// (DESIGN.md §5): the roofline numerator.  The probes replay the kernel's
+// access sequence (kernels.hip k_conj) on the host copy of the postings.
+int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out) {
+  if (!ix || !q || !out || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
+  if (ix->h_doc.empty() && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
+  const uint32_t nq = q->n_queries;
+  std::atomic<bool> bad{false};
+  parallel_ranges(nq, nq >= 64 ? hw_threads(0) : 1, [&](int, uint32_t qb, uint32_t qe) {
+    std::vector<uint32_t> cand, next;
+    for (uint32_t i = qb; i < qe; ++i) {
+      double* o = out + 4ull * i;
+      o[0] = o[1] = o[2] = o[3] = 0.0;
+      const uint32_t b = q->q_off[i], m = q->q_off[i + 1] - b;
+      if (q->q_off[i + 1] < b || m > fg::kMaxTerms) { bad = true; return; }
+      if (m == 0) continue;
+      if (q->mode == FG_MODE_OR) {
+        // k_disj's exhaustive union: every posting (doc + score) of every clause once
+        for (uint32_t j = 0; j < m; ++j) {
+          const uint32_t t = q->terms[b + j];
+          if (t < ix->n_terms) o[0] += 8.0 * (double)(ix->off[t + 1] - ix->off[t]);
+        }
+        o[2] = 8.0 * k;
+        o[3] = o[0] + o[2];
+        continue;
+      }
+      // intersection order: cost = df_text + df_name, stable (fg_plan_create)
+      struct T { uint64_t cost; uint32_t term; };
+      T ts[fg::kMaxTerms];
+      bool missing = false;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t t = q->terms[b + j];
+        const uint64_t cost = t < ix->n_terms ? (uint64_t)ix->df_text[t] + ix->df_name[t] : 0;
+        missing |= cost == 0;
+        ts[j] = T{cost, t};
+      }
+      if (missing) continue;
+      std::stable_sort(ts, ts + m, [](const T& x, const T& y) { return x.cost < y.cost; });
+      const uint32_t t0 = ts[0].term;
+      const uint64_t df0 = ix->off[t0 + 1] - ix->off[t0];
+      o[0] = 8.0 * (double)df0;  // lead doc id + posting score
+      cand.assign(ix->h_doc.begin() + ix->off[t0], ix->h_doc.begin() + ix->off[t0 + 1]);
+      double probe = 0.0;
+      for (uint32_t j = 1; j < m && !cand.empty(); ++j) {
+        const uint32_t t = ts[j].term, meta = ix->tmeta[t];
+        const uint32_t* d = ix->h_doc.data() + ix->off[t];
+        const uint64_t n = ix->off[t + 1] - ix->off[t];
+        next.clear();
+        if (meta >> 16) {
+          // dense score table: one 4-B element per candidate
+          probe += 4.0 * (double)cand.size();
+          for (uint32_t x : cand)
+            if (std::binary_search(d, d + n, x)) next.push_back(x);
+        } else {
+          // bucket directory: the bucket's two bounds, the search steps inside it,
+          // the final compare and, on a hit, the posting score
+          const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu;
+          for (uint32_t x : cand) {
+            const uint64_t lo = (uint64_t)(x >> B) << B;
+            uint64_t pos = std::lower_bound(d, d + n, (uint32_t)std::min<uint64_t>(lo, 0xFFFFFFFFull)) - d;
+            const uint64_t hi = std::lower_bound(d + pos, d + n, (uint32_t)std::min<uint64_t>(lo + (1ull << B),
+                                                                                             0xFFFFFFFFull)) - d;
+            double words = 2.0;
+            for (uint32_t st = S; st > 0; --st) {
+              const uint64_t half = 1ull << (st - 1), idx = pos + half - 1;
+              if (idx < hi) {
+                words += 1.0;
+                if (d[idx] < x) pos += half;
+              }
+            }
+            if (pos < hi) {
+              words += 1.0;
+              if (d[pos] == x) { words += 1.0; next.push_back(x); }
+            }
+            probe += 4.0 * words;
+          }
+        }
+        cand.swap(next);
+      }
+      o[1] = probe;
+      o[2] = 8.0 * (double)std::min<size_t>(cand.size(), k);  // the work item's kept keys
+      o[3] = o[0] + o[1] + o[2];
+    }
+  });
+  if (bad) return fail(FG_EINVAL, "bad query batch");
   return FG_OK;
 }
 

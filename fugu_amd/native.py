@@ -47,7 +47,7 @@ EXPORTS = (
     "fg_index_stats_get", "fg_index_df", "fg_index_bm25",
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
-    "fg_search_batch", "fg_merge_shards", "fg_bytes_model",
+    "fg_search_batch", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats",
 )
 
@@ -137,6 +137,7 @@ _sig("fg_plan_destroy", C.c_int, _p)
 _sig("fg_search_batch", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f32p, _u32p, _u32p)
 _sig("fg_merge_shards", C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("fg_bytes_model", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f64p)
+_sig("fg_bytes_model_gpu", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f64p)
 
 
 class FuguError(RuntimeError):
@@ -305,6 +306,32 @@ class Index:
         del keep
         return cls(h)
 
+    @classmethod
+    def from_postings(cls, ctx: Context, n_docs: int, term_off, doc, tf_text, tf_name, fn_text, fn_name,
+                      tot_tokens, deleted=None, facets=None, device: int | None = None):
+        """fg_index_build: postings already inverted by the host (the entry the Rust
+        binding feeds from tantivy's segment readers).  `facets` =
+        (facet_term_off, facet_doc, n_facet_terms, tot_facet_tokens) or None."""
+        term_off = _u64(term_off)
+        doc = _u32(doc)
+        tf_text = None if tf_text is None else np.ascontiguousarray(tf_text, np.uint16)
+        tf_name = None if tf_name is None else np.ascontiguousarray(tf_name, np.uint16)
+        fn_text = np.ascontiguousarray(fn_text, np.uint8)
+        fn_name = None if fn_name is None else np.ascontiguousarray(fn_name, np.uint8)
+        deleted = None if deleted is None else np.ascontiguousarray(deleted, np.uint8)
+        fo = fd = None
+        nft, totf = 0, 0
+        if facets is not None:
+            fo, fd, nft, totf = _u64(facets[0]), _u32(facets[1]), int(facets[2]), int(facets[3])
+        inp = IndexInput(n_docs, len(term_off) - 1, _ptr(term_off, _u64p), _ptr(doc, _u32p), _ptr(tf_text, _u16p),
+                         _ptr(tf_name, _u16p), _ptr(fn_text, _u8p), _ptr(fn_name, _u8p),
+                         (C.c_uint64 * 2)(*[int(x) for x in tot_tokens]), _ptr(deleted, _u8p), nft,
+                         _ptr(fo, _u64p), _ptr(fd, _u32p), totf)
+        h = _p()
+        dev = ctx.devices[0] if device is None else device
+        _check(_lib.fg_index_build(ctx.handle, dev, C.byref(inp), C.byref(h)))
+        return cls(h)
+
     @property
     def handle(self):
         return self._h
@@ -348,6 +375,16 @@ class Index:
         qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode)
         out = np.zeros(4 * nq, np.float64)
         _check(_lib.fg_bytes_model(self._h, C.byref(qb), k, _ptr(out, _f64p)))
+        return out.reshape(nq, 4)
+
+    def bytes_model_gpu(self, q_off, terms, k: int, mode: int = MODE_AND):
+        """fg_bytes_model_gpu: per query {lead, probe, output, total} bytes at the HBM layout."""
+        q_off = _u32(q_off)
+        terms = _u32(terms)
+        nq = len(q_off) - 1
+        qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode)
+        out = np.zeros(4 * nq, np.float64)
+        _check(_lib.fg_bytes_model_gpu(self._h, C.byref(qb), k, _ptr(out, _f64p)))
         return out.reshape(nq, 4)
 
     def close(self):

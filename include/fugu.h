@@ -226,6 +226,16 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
 /* SURVEY.md §8(d) algorithmic bytes per query: out[4*i..] = {B_merge, B_skip,
  * B, |I|}.  Host analysis over the host posting copy (keep_host_postings). */
 int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);
+/* Algorithmic bytes at THIS snapshot's HBM layout (the roofline numerator,
+ * DESIGN.md §5): out[4*i..] = {lead, probe, output, total} bytes of query i.
+ * FG_MODE_AND replays k_conj's exhaustive cascade (no MaxScore pruning): 8 B
+ * per lead posting (doc id + posting score); then, in intersection order, one
+ * probe per candidate still alive -- 4 B on a dense score table, or on the
+ * bucket directory 8 B of bucket bounds + 4 B per search step + 4 B final
+ * compare + 4 B score on a hit; then 8 B per kept key (<= k).  FG_MODE_OR: 8 B
+ * per posting of every clause (exhaustive union) + 8 B * k.  Needs
+ * keep_host_postings. */
+int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);
 
 #ifdef __cplusplus
 }

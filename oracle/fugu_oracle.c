@@ -28,7 +28,10 @@
  * DESIGN.md): blocks hold raw u32 doc ids / tfs instead of bitpacked deltas,
  * which makes this baseline FASTER than tantivy, never slower.
  *
- * Build: oracle/Makefile (gcc -O3 -march=native -ffp-contract=off).
+ * Build: oracle/Makefile.  The portable test build uses -march=x86-64-v2 (the
+ * container that builds it is not the GPU box's CPU); bench.py's CPU baseline
+ * recompiles this file with -O3 -march=native -ffp-contract=off ON THE BOX
+ * (`make -C oracle native OUT=<dir>`) and loads that copy (FUGU_ORACLE_LIB).
  */
 #include <math.h>
 #include <pthread.h>

@@ -12,7 +12,10 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfugu_oracle.so")
+# FUGU_ORACLE_LIB: the -march=native build bench.py compiles on the box for the
+# CPU baseline (oracle/Makefile `native`); default: the portable test build
+LIB_PATH = os.environ.get("FUGU_ORACLE_LIB") or os.path.join(_HERE, "libfugu_oracle.so")
+NATIVE_FLAGS = "-O3 -std=c11 -fPIC -ffp-contract=off -D_GNU_SOURCE -march=native"
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} missing: run `make -C oracle`")
 _lib = C.CDLL(LIB_PATH)

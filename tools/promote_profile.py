@@ -2,7 +2,7 @@
 committed profiles/<round>/ and point profiles/latest.json at it (the per-launch
 k_conj HBM bytes bench.py quotes as roofline.traffic for the same build).
 
-  python tools/promote_profile.py <tag> <round>      e.g.  r01d r01
+  python tools/promote_profile.py <tag> <round>      e.g.  r02a r02
 """
 import glob
 import json
@@ -20,23 +20,26 @@ def main():
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "pmc.json"), os.path.join(dst, "pmc.json"))
-    for f in glob.glob(os.path.join(src, "calib", "**", "*counter_collection.csv"), recursive=True):
-        shutil.copy(f, os.path.join(dst, "calib_fetch_counter_collection.csv"))
+    for sub in ("calib_fetch", "calib_dram"):
+        for f in glob.glob(os.path.join(src, sub, "**", "*counter_collection.csv"), recursive=True):
+            shutil.copy(f, os.path.join(dst, f"{sub}_counter_collection.csv"))
     shutil.copy(os.path.join(src, "trace_bench.json"), os.path.join(dst, "bench_under_trace.json"))
     with open(os.path.join(src, "pmc.json")) as f:
         pmc = json.load(f)
     with open(os.path.join(src, "trace_bench.json")) as f:
         bench = json.loads(f.read().strip().splitlines()[-1])
     cfg = bench["config"]
+    kc = pmc["kernels"].get("k_conj", {})
     latest = {
         "source": f"profiles/{rnd}/pmc.json",
-        "command": f"bash tools/profile_bench.sh {tag}  (= rocprofv3 --kernel-trace --stats, then --pmc FETCH_SIZE / "
-                   "WRITE_SIZE passes of python3 bench.py --steps 5 --warmup 1 --no-cpu --p50-queries 0 --no-extra)",
+        "command": f"bash tools/profile_bench.sh {tag}  (= rocprofv3 --kernel-trace --stats, then separate --pmc passes "
+                   "(FETCH_SIZE / WRITE_SIZE / TCC_EA0_RDREQ_DRAM_32B + TCC_EA0_WRREQ_WRITE_DRAM_32B) of python3 "
+                   "bench.py --steps 5 --warmup 1 --no-cpu --p50-queries 0 --no-extra)",
         "workload": {"n_docs": cfg["n_docs"], "batch": cfg["batch"], "k": cfg["k"], "terms": cfg["terms"]},
         "lib_id": pmc.get("lib_id"),
-        "k_conj_hbm_bytes_per_launch": pmc["k_conj_hbm_bytes_per_launch"],
-        "fetch_correction": "FETCH_SIZE x2.0 (gfx950 reads 1/2 of streamed bytes; calibrated on a 1 GiB stream, "
-                            "4-B and 16-B lanes: profiles/%s/calib_fetch_counter_collection.csv)" % rnd,
+        "k_conj_hbm_bytes_per_launch": pmc.get("k_conj_hbm_bytes_per_launch"),
+        "hbm_source": kc.get("hbm_source"),
+        "calibration": pmc.get("calibration"),
     }
     with open(os.path.join(ROOT, "profiles", "latest.json"), "w") as f:
         json.dump(latest, f, indent=1)
