@@ -29,11 +29,20 @@ constexpr uint32_t kFinalCap = 8192;      // candidates kept in LDS by the final
 #define FG_DENSE_DIV 256  // tools/ab_variants.py sweep 8..512: DESIGN.md §3
 #endif
 #ifndef FG_DENSE_GIB
-#define FG_DENSE_GIB 64
+#define FG_DENSE_GIB 0    // f32 score tables: superseded by rank words; env FUGU_DENSE_GIB
 #endif
-constexpr uint32_t kDenseDiv = FG_DENSE_DIV;  // terms in >= 1/kDenseDiv of the docs get a dense score table
+#ifndef FG_RANK_DIV
+#define FG_RANK_DIV 16384
+#endif
+#ifndef FG_RANK_GIB
+#define FG_RANK_GIB 64    // env FUGU_RANK_GIB
+#endif
+constexpr uint32_t kDenseDiv = FG_DENSE_DIV;  // terms in >= 1/kDenseDiv of the docs may get a dense f32 score table
 constexpr uint64_t kDenseBudget = (uint64_t)FG_DENSE_GIB << 30;  // ... densest first, within this many bytes
-constexpr uint32_t kMaxDense = 4096;      // at most this many dense tables per index
+constexpr uint32_t kRankDiv = FG_RANK_DIV;    // terms in >= 1/kRankDiv of the docs may get rank words
+constexpr uint64_t kRankBudget = (uint64_t)FG_RANK_GIB << 30;    // ... densest first, within this many bytes
+constexpr uint32_t kMaxDense = 32767;     // slots per kind (tmeta bits 16-30)
+constexpr uint32_t kRankChunkWords = 2048;  // k_rank: words (65536 docs) per workgroup
 constexpr uint32_t kGroupsPerQuery = 64;  // a query's chunks are split into ~this many work items
 #ifndef FG_MAXGROUP
 #define FG_MAXGROUP 16
@@ -52,6 +61,11 @@ constexpr uint32_t kScanMaxGroup = 32;    // k_scan: at most this many 4096-doc 
 constexpr uint32_t kModeAnd = 0;
 constexpr uint32_t kModeOr = 1;
 
+// tmeta of a term: bits 0-7 = B_t (bucket shift), 8-15 = S_t (search steps),
+// 16-30 = dense slot + 1 (0: none), bit 31 = the slot's kind (1: rank words, 0: f32 table)
+__host__ __device__ inline uint32_t meta_slot(uint32_t meta) { return (meta >> 16) & 0x7FFFu; }
+__host__ __device__ inline bool meta_rank(uint32_t meta) { return (meta >> 31) != 0; }
+
 // Device view of one namespace snapshot (all pointers device-resident).
 //
 // Per term t the postings are doc[off[t] .. off[t+1]) (ascending) with psc[]
@@ -59,9 +73,16 @@ constexpr uint32_t kModeOr = 1;
 // [b << B_t, (b+1) << B_t) and dir[dir_off[t] + b] = first position in the
 // list with doc >= b << B_t (the last entry is df_t).  B_t is chosen so a
 // bucket holds ~kBucketTarget (4) postings; a probe is one
-// directory load and a <= S_t step search inside one or two lines.  Terms that
-// occur in >= 1/kDenseDiv of the docs additionally get a dense doc-indexed f32
-// score table (densest first, within kDenseBudget): a probe is one 4-B load.
+// directory load and a <= S_t step search inside one or two lines.  The
+// densest terms (within a byte budget) additionally get RANK WORDS: one u64 per
+// 32 docs, the low half the docs' presence bits, the high half the number of
+// the term's postings before the word's first doc.  A probe is one 8-B load; on
+// a hit the posting's position is rank + popcount(bits below the doc), and its
+// score one psc[] load.  Scattered single-dword probes each move a 128-B line
+// (profiles/r02_start: tools/calib_fetch gather_lines), and a line of rank words
+// covers 512 docs where a line of a doc-indexed f32 score table covers 32, so
+// the candidates of a long lead list share lines.  (f32 tables, a probe = one
+// 4-B load giving the score, remain available: FUGU_DENSE_GIB.)
 struct DevIndex {
   const uint32_t* doc;       // [P] doc ids, CSR by term, ascending within a term
   const float* psc;          // [P] the posting's term score: Should(text:t, name:t) in the doc, i.e.
@@ -71,9 +92,9 @@ struct DevIndex {
   const uint64_t* off;       // [V+1] posting offsets
   const uint32_t* dir;       // [D] bucket directory (positions within the list)
   const uint32_t* dir_off;   // [V] first directory entry of each term
-  const uint32_t* tmeta;     // [V] bits 0-7 = B_t (bucket shift), bits 8-15 = S_t (search steps),
-                             //     bits 16-31 = dense slot + 1 (0: no dense table)
-  const float* dense;        // [n_dense * N] doc-indexed term score of the densest terms (-1 = absent)
+  const uint32_t* tmeta;     // [V] meta_slot / meta_rank above
+  const float* dense;        // [n_dense * N] doc-indexed term score (-1 = absent), f32-kind slots
+  const uint64_t* rank;      // [n_rank * rank_words] rank words, rank-kind slots
   const float* tmaxs;        // [V] largest posting score of each term (MaxScore bound)
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
@@ -85,6 +106,7 @@ struct DevIndex {
   uint32_t n_terms;
   uint32_t has_name;
   uint32_t n_fterms;
+  uint32_t rank_words;       // words per rank-kind term: ceil(N / 32)
 };
 
 // Facet filters of a planned batch (DevPlan).  Every distinct clause list
@@ -166,6 +188,8 @@ hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s);
 hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s);
+hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
+                       uint32_t n_words, uint64_t* out, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

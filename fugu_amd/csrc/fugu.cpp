@@ -205,7 +205,7 @@ struct fg_index {
   uint32_t n_docs = 0, n_terms = 0;
   bool has_name = false;
   uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0;
-  uint32_t n_dense = 0;
+  uint32_t n_dense = 0, n_rank = 0;
   uint64_t tot[2] = {0, 0};
   uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
   float avgdl[2] = {0, 0};
@@ -412,29 +412,6 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       }
     }
   });
-  // dense doc-indexed score tables (DevIndex::dense) for the densest terms:
-  // df >= N / kDenseDiv, densest first (ties by term id), within kDenseBudget
-  // and a quarter of the device's free memory.  A table holds the posting
-  // scores psc[] (the text + name union), so name terms qualify too.  The
-  // tables are filled on the device from the uploaded postings (k_dense).
-  std::vector<uint32_t> dense_terms;
-  for (uint32_t t = 0; t < V; ++t) {
-    const uint64_t n = hp.off[t + 1] - hp.off[t];
-    if (n > 0 && n * fg::kDenseDiv >= N) dense_terms.push_back(t);
-  }
-  std::stable_sort(dense_terms.begin(), dense_terms.end(), [&](uint32_t a, uint32_t b) {
-    return hp.off[a + 1] - hp.off[a] > hp.off[b + 1] - hp.off[b];
-  });
-  {
-    size_t free_b = 0, total_b = 0;
-    HIPCHK(hipSetDevice(dev));
-    HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t budget = std::min<uint64_t>(fg::kDenseBudget, free_b / 4);
-    const uint64_t cap = std::min<uint64_t>(fg::kMaxDense, budget / (N * sizeof(float)));
-    if (dense_terms.size() > cap) dense_terms.resize(cap);
-  }
-  for (uint32_t s = 0; s < dense_terms.size(); ++s) tmeta[dense_terms[s]] |= (s + 1) << 16;
-  ix->n_dense = (uint32_t)dense_terms.size();
   // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
   // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
   const uint32_t VF = hp.n_fterms;
@@ -467,7 +444,6 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   HIPCHK(hipSetDevice(dev));
   uint64_t bytes = 0;
   int rc;
-  float* d_dense = nullptr;
   uint32_t *d_doc, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr, *d_toff;
   uint64_t* d_off;
   float *d_psc, *d_tmaxs, *d_bmax, *d_tmax;
@@ -484,33 +460,111 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   if ((rc = dev_upload(ix->mem, toff.data(), toff.size(), &d_toff, &bytes))) return rc;
   std::vector<float>().swap(tmax);
   if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
-  ix->tmeta = tmeta;
-  {
-    const size_t cnt = std::max<size_t>((size_t)N * dense_terms.size(), 4);
-    void* p = nullptr;
-    if (hipMalloc(&p, cnt * sizeof(float)) != hipSuccess)
-      return fail(FG_EOOM, "dense tables (%zu terms) hipMalloc failed", dense_terms.size());
-    ix->mem.ptrs.push_back(p);
-    bytes += cnt * sizeof(float);
-    d_dense = static_cast<float*>(p);
-    HIPCHK(hipMemsetD32(p, (int)0xBF800000u, cnt));  // -1.0f: absent (a score is >= 0, and may be 0)
-    for (uint32_t s = 0; s < dense_terms.size(); ++s) {
-      const uint32_t t = dense_terms[s];
-      HIPCHK(fg::launch_dense(d_doc, d_psc, hp.off[t], (uint32_t)(hp.off[t + 1] - hp.off[t]), d_dense + (size_t)s * N,
-                              nullptr));
+  // dense structures for the densest terms (fg_internal.h DevIndex), chosen
+  // AFTER the uploads above so the budgets see the memory actually left: f32
+  // score tables (df >= N / kDenseDiv, FUGU_DENSE_GIB) for the densest, then
+  // rank words (df >= N / kRankDiv, FUGU_RANK_GIB) for the next ones, densest
+  // first (ties by term id), each within its budget and a quarter of the free
+  // memory.  An allocation that fails is retried with half the terms (down to
+  // none), so a snapshot build never fails for want of optional structures.
+  // Both hold the union score psc[] (text + name), so name terms qualify too.
+  std::vector<uint32_t> by_df;
+  for (uint32_t t = 0; t < V; ++t)
+    if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * std::max(fg::kDenseDiv, fg::kRankDiv) >= N)
+      by_df.push_back(t);
+  std::stable_sort(by_df.begin(), by_df.end(), [&](uint32_t a, uint32_t b) {
+    return hp.off[a + 1] - hp.off[a] > hp.off[b + 1] - hp.off[b];
+  });
+  const uint32_t rank_words = (uint32_t)((N + 31) / 32);
+  std::vector<uint32_t> f32_terms, rank_terms;
+  float* d_dense = nullptr;
+  uint64_t* d_rank = nullptr;
+  auto env_gib = [](const char* name, uint64_t dflt) {
+    const char* v = getenv(name);
+    return v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : dflt;
+  };
+  // per_term bytes for each of terms, halving the term list while hipMalloc fails
+  auto alloc_slots = [&](std::vector<uint32_t>& terms, size_t per_term, void** out_p) -> int {
+    while (!terms.empty()) {
+      void* p = nullptr;
+      if (hipMalloc(&p, per_term * terms.size()) == hipSuccess) {
+        ix->mem.ptrs.push_back(p);
+        bytes += per_term * terms.size();
+        *out_p = p;
+        return FG_OK;
+      }
+      (void)hipGetLastError();
+      terms.resize(terms.size() / 2);
     }
+    return FG_OK;
+  };
+  {
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t b32 = std::min<uint64_t>(env_gib("FUGU_DENSE_GIB", fg::kDenseBudget), free_b / 4);
+    size_t i = 0;
+    for (; i < by_df.size() && f32_terms.size() < fg::kMaxDense; ++i) {
+      const uint32_t t = by_df[i];
+      if ((hp.off[t + 1] - hp.off[t]) * fg::kDenseDiv < N || (f32_terms.size() + 1) * N * 4ull > b32) break;
+      f32_terms.push_back(t);
+    }
+    void* p = nullptr;
+    if ((rc = alloc_slots(f32_terms, (size_t)N * 4, &p))) return rc;
+    d_dense = static_cast<float*>(p);
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t brk = std::min<uint64_t>(env_gib("FUGU_RANK_GIB", fg::kRankBudget), free_b / 4);
+    for (i = f32_terms.size(); i < by_df.size() && rank_terms.size() < fg::kMaxDense; ++i) {
+      const uint32_t t = by_df[i];
+      if ((hp.off[t + 1] - hp.off[t]) * fg::kRankDiv < N || (rank_terms.size() + 1) * rank_words * 8ull > brk) break;
+      rank_terms.push_back(t);
+    }
+    p = nullptr;
+    if ((rc = alloc_slots(rank_terms, (size_t)rank_words * 8, &p))) return rc;
+    d_rank = static_cast<uint64_t*>(p);
+  }
+  if (!f32_terms.empty()) {
+    HIPCHK(hipMemsetD32(d_dense, (int)0xBF800000u, (size_t)N * f32_terms.size()));  // -1.0f: absent
+    for (uint32_t s2 = 0; s2 < f32_terms.size(); ++s2) {
+      const uint32_t t = f32_terms[s2];
+      HIPCHK(fg::launch_dense(d_doc, d_psc, hp.off[t], (uint32_t)(hp.off[t + 1] - hp.off[t]),
+                              d_dense + (size_t)s2 * N, nullptr));
+      tmeta[t] |= (s2 + 1) << 16;
+    }
+  }
+  if (!rank_terms.empty()) {
+    // one k_rank launch for every rank term: per slot the term's posting range
+    std::vector<uint64_t> sb(rank_terms.size());
+    std::vector<uint32_t> sn(rank_terms.size());
+    for (uint32_t s2 = 0; s2 < rank_terms.size(); ++s2) {
+      const uint32_t t = rank_terms[s2];
+      sb[s2] = hp.off[t];
+      sn[s2] = (uint32_t)(hp.off[t + 1] - hp.off[t]);
+      tmeta[t] |= ((s2 + 1) << 16) | 0x80000000u;
+    }
+    DevAllocs tmp;
+    tmp.dev = dev;
+    uint64_t* d_sb;
+    uint32_t* d_sn;
+    uint64_t tb = 0;
+    if ((rc = dev_upload(tmp, sb.data(), sb.size(), &d_sb, &tb))) return rc;
+    if ((rc = dev_upload(tmp, sn.data(), sn.size(), &d_sn, &tb))) return rc;
+    HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
   }
+  HIPCHK(hipStreamSynchronize(nullptr));
+  ix->n_dense = (uint32_t)f32_terms.size();
+  ix->n_rank = (uint32_t)rank_terms.size();
+  if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
+  ix->tmeta = tmeta;
   ix->tmaxs = std::move(tmaxs);
   if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
   uint32_t* d_fdoc;
   uint64_t* d_foff;
   if ((rc = dev_upload(ix->mem, hp.fdoc.data(), hp.fdoc.size(), &d_fdoc, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, hp.foff.data(), hp.foff.size(), &d_foff, &bytes))) return rc;
-  ix->d = fg::DevIndex{d_doc,  d_psc,  d_off,  d_dir,  d_dir_off, d_tmeta, d_dense,   d_tmaxs,
-                       d_alive, d_bmax, d_tmax, d_toff, d_fdoc,    d_foff,  hp.n_docs, hp.n_terms,
-                       hp.has_name ? 1u : 0u, VF};
+  ix->d = fg::DevIndex{d_doc,   d_psc,  d_off,  d_dir,  d_dir_off, d_tmeta,   d_dense,    d_rank,
+                       d_tmaxs, d_alive, d_bmax, d_tmax, d_toff, d_fdoc,    d_foff,     hp.n_docs,
+                       hp.n_terms, hp.has_name ? 1u : 0u, VF, rank_words};
   ix->foff = std::move(hp.foff);
   // per-term doc span (disjunctive plans skip the tiles outside it)
   ix->first_doc.assign(V, 0);
@@ -910,6 +964,8 @@ int fg_index_stats_get(const fg_index* ix, fg_index_stats* o) {
   o->device = ix->dev;
   o->n_facet_terms = ix->n_fterms;
   o->tot_facet_tokens = ix->tot_f;
+  o->n_dense_f32 = ix->n_dense;
+  o->n_rank_terms = ix->n_rank;
   return FG_OK;
 }
 
@@ -1446,11 +1502,13 @@ int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, 
         const uint32_t* d = ix->h_doc.data() + ix->off[t];
         const uint64_t n = ix->off[t + 1] - ix->off[t];
         next.clear();
-        if (meta >> 16) {
-          // dense score table: one 4-B element per candidate
-          probe += 4.0 * (double)cand.size();
+        if (fg::meta_slot(meta)) {
+          // f32 score table: one 4-B element per candidate; rank words: one 8-B
+          // word per candidate + the 4-B posting score on a hit
           for (uint32_t x : cand)
             if (std::binary_search(d, d + n, x)) next.push_back(x);
+          probe += fg::meta_rank(meta) ? 8.0 * (double)cand.size() + 4.0 * (double)next.size()
+                                       : 4.0 * (double)cand.size();
         } else {
           // bucket directory: the bucket's two bounds, the search steps inside it,
           // the final compare and, on a hit, the posting score

@@ -55,6 +55,20 @@ __device__ inline uint32_t wave_id() { return threadIdx.x >> 6; }
 // never drops a doc whose exactly-summed score reaches the threshold.
 __device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f; }  // 1 + 2^-17
 
+// Term score at doc d through the term's dense structure (meta_slot != 0),
+// -1 = the term is absent from d.  Rank words: one 8-B load, and on a hit the
+// posting score at position rank + popcount(presence bits below d).
+__device__ inline float dense_score(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t d) {
+  const uint32_t slot = meta_slot(meta);
+  if (meta_rank(meta)) {
+    const uint64_t x = ix.rank[(size_t)(slot - 1) * ix.rank_words + (d >> 5)];
+    const uint32_t bits = (uint32_t)x, b = d & 31u;
+    if (!((bits >> b) & 1u)) return -1.0f;
+    return ix.psc[base + (uint32_t)(x >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))];
+  }
+  return ix.dense[(size_t)(slot - 1) * ix.n_docs + d];
+}
+
 // Upper bound of term t's score in doc d: the tile maximum (4096-doc tiles)
 // when the term has one, else the maximum of d's directory bucket.
 __device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t toff, uint32_t dir_off, uint32_t d) {
@@ -377,10 +391,23 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       if (!__any(live != 0)) break;  // wave-uniform early exit
       const uint32_t ti = terms[i];
       const uint32_t meta = ix.tmeta[ti];
-      const uint32_t dslot = meta >> 16;
+      const uint32_t dslot = meta_slot(meta);
       float sc[kItems];
-      if (dslot) {
-        // dense term: doc-indexed score table, one 4-B load per item (-1 = absent)
+      if (dslot && meta_rank(meta)) {
+        // rank words: presence + rank in one 8-B load per item (all items'
+        // loads in flight together), then the posting score of the hits
+        const uint64_t* __restrict__ rw = ix.rank + (size_t)(dslot - 1) * ix.rank_words;
+        const float* __restrict__ ps = ix.psc + ix.off[ti];
+        uint64_t x[kItems];
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> 5] : 0ull;
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+          const uint32_t bits = (uint32_t)x[j], b = doc[j] & 31u;
+          sc[j] = ((bits >> b) & 1u) ? ps[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))] : -1.0f;
+        }
+      } else if (dslot) {
+        // f32 score table: doc-indexed, one 4-B load per item (-1 = absent)
         const float* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) sc[j] = (live & (1u << j)) ? dt[doc[j]] : -1.0f;
@@ -828,9 +855,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
           float ub2 = sc + fmax;
           for (uint32_t i = 0; i < m; ++i) {
             if (i == c || signbit(sh.r_ub[t * m + i])) continue;
-            const uint32_t meta = sh.c_meta[i], slot = meta >> 16;
-            const float b = slot ? ix.dense[(size_t)(slot - 1) * ix.n_docs + d]
-                                 : ix.bmax[sh.c_dir[i] + (d >> (meta & 0xFFu))];
+            const uint32_t meta = sh.c_meta[i];
+            const float b = meta_slot(meta) ? dense_score(ix, meta, sh.c_base[i], d)
+                                            : ix.bmax[sh.c_dir[i] + (d >> (meta & 0xFFu))];
             if (signbit(b)) continue;  // clause i cannot match d
             ub2 += b;
             maybe |= 1u << i;
@@ -884,9 +911,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
         }
         if (!(pc[j] & 0x80000000u)) {
           const uint32_t meta = sh.c_meta[pc[j]];
-          const uint32_t slot = meta >> 16;
-          if (slot) {
-            pv[j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
+          if (meta_slot(meta)) {
+            pv[j] = dense_score(ix, meta, sh.c_base[pc[j]], pd[j]);
             pc[j] |= 0x80000000u;  // resolved
           } else {
             const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[pc[j]];
@@ -1240,6 +1266,65 @@ __global__ __launch_bounds__(kThreads) void k_dense(const uint32_t* __restrict__
                                                     uint64_t base, uint32_t n, float* __restrict__ row) {
   for (uint32_t p = blockIdx.x * kThreads + threadIdx.x; p < n; p += gridDim.x * kThreads)
     row[doc[base + p]] = psc[base + p];
+}
+
+// Snapshot build: the rank words of every rank-kind term (fg_internal.h
+// DevIndex::rank) in one launch.  One workgroup per (term slot, 2048 words =
+// 65536 docs): two binary searches locate the chunk's postings, their presence
+// bits are set in LDS, and a workgroup prefix sum of the words' popcounts gives
+// each word's rank.
+__global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ doc_all,
+                                                   const uint64_t* __restrict__ slot_base,
+                                                   const uint32_t* __restrict__ slot_n, uint32_t chunks_per_slot,
+                                                   uint32_t n_words, uint64_t* __restrict__ out_all) {
+  __shared__ uint32_t bits[kRankChunkWords];
+  __shared__ uint32_t scratch[8];
+  __shared__ uint32_t range[2];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t slot = blockIdx.x / chunks_per_slot, chunk = blockIdx.x - slot * chunks_per_slot;
+  const uint32_t* __restrict__ doc = doc_all + slot_base[slot];
+  const uint32_t n = slot_n[slot];
+  uint64_t* __restrict__ out = out_all + (size_t)slot * n_words;
+  const uint32_t w0 = chunk * kRankChunkWords;
+  if (tid < 2) {
+    const uint64_t target = ((uint64_t)w0 + (tid ? kRankChunkWords : 0u)) << 5;
+    uint32_t lo = 0, hi = n;  // first posting with doc >= target
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1);
+      if ((uint64_t)doc[mid] < target) lo = mid + 1; else hi = mid;
+    }
+    range[tid] = lo;
+  }
+  for (uint32_t i = tid; i < kRankChunkWords; i += kThreads) bits[i] = 0u;
+  __syncthreads();
+  for (uint32_t p = range[0] + tid; p < range[1]; p += kThreads) {
+    const uint32_t d = doc[p];
+    atomicOr(&bits[(d >> 5) - w0], 1u << (d & 31u));
+  }
+  __syncthreads();
+  constexpr uint32_t R = kRankChunkWords / kThreads;
+  uint32_t c[R], sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < R; ++i) {
+    c[i] = (uint32_t)__popc(bits[tid * R + i]);
+    sum += c[i];
+  }
+  uint32_t r = range[0] + block_exclusive_scan(sum, scratch);
+#pragma unroll
+  for (uint32_t i = 0; i < R; ++i) {
+    const uint32_t w = w0 + tid * R + i;
+    if (w < n_words) out[w] = (uint64_t)bits[tid * R + i] | ((uint64_t)r << 32);
+    r += c[i];
+  }
+}
+
+hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
+                       uint32_t n_words, uint64_t* out, hipStream_t s) {
+  if (n_words == 0 || n_slots == 0) return hipSuccess;
+  const uint32_t cps = (n_words + kRankChunkWords - 1) / kRankChunkWords;
+  if ((uint64_t)cps * n_slots > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  k_rank<<<cps * n_slots, kThreads, 0, s>>>(doc, slot_base, slot_n, cps, n_words, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s) {

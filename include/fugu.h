@@ -152,6 +152,8 @@ typedef struct fg_index_stats {
   int device;
   uint32_t n_facet_terms;
   uint64_t tot_facet_tokens;
+  uint32_t n_dense_f32;      /* terms with an f32 score table */
+  uint32_t n_rank_terms;     /* terms with rank words */
 } fg_index_stats;
 int fg_index_stats_get(const fg_index* ix, fg_index_stats* out);
 /* doc_freq of `term` in `field` (tantivy Searcher::doc_freq; FG_FIELD_FACET:
@@ -230,9 +232,10 @@ int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, doub
  * DESIGN.md §5): out[4*i..] = {lead, probe, output, total} bytes of query i.
  * FG_MODE_AND replays k_conj's exhaustive cascade (no MaxScore pruning): 8 B
  * per lead posting (doc id + posting score); then, in intersection order, one
- * probe per candidate still alive -- 4 B on a dense score table, or on the
- * bucket directory 8 B of bucket bounds + 4 B per search step + 4 B final
- * compare + 4 B score on a hit; then 8 B per kept key (<= k).  FG_MODE_OR: 8 B
+ * probe per candidate still alive -- 8 B rank word + 4 B score on a hit, or
+ * 4 B on an f32 score table, or on the bucket directory 8 B of bucket bounds +
+ * 4 B per search step + 4 B final compare + 4 B score on a hit; then 8 B per
+ * kept key (<= k).  FG_MODE_OR: 8 B
  * per posting of every clause (exhaustive union) + 8 B * k.  Needs
  * keep_host_postings. */
 int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);
