@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -101,6 +102,23 @@ float term_score_host(uint32_t tfp, uint32_t fn_t, uint32_t fn_n, float wt, floa
   return s;
 }
 
+// FUGU_BUILD_TRACE=1: per-phase wall time of a snapshot build on stderr
+struct BuildTrace {
+  bool on = false;
+  std::chrono::steady_clock::time_point t;
+  void start() {
+    on = getenv("FUGU_BUILD_TRACE") != nullptr;
+    t = std::chrono::steady_clock::now();
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[fg build] %-24s %9.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+thread_local BuildTrace g_bt;
+
 template <class F>
 void parallel_ranges(uint32_t n, int threads, F&& f) {
   if (threads <= 1 || n < 1024) { f(0, 0u, n); return; }
@@ -113,8 +131,30 @@ void parallel_ranges(uint32_t n, int threads, F&& f) {
   for (auto& t : ts) t.join();
 }
 
+// Dynamic schedule over [0, n) in chunks of `grain` (per-term loops: Zipf term
+// ids put most postings in the first terms, so a static split leaves one
+// thread with nearly all the work).  f(thread, begin, end).
+template <class F>
+void parallel_dynamic(uint32_t n, int threads, uint32_t grain, F&& f) {
+  if (threads <= 1 || n <= grain) { f(0, 0u, n); return; }
+  std::atomic<uint64_t> next{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      for (;;) {
+        const uint64_t b = next.fetch_add(grain);
+        if (b >= n) break;
+        f(t, (uint32_t)b, (uint32_t)std::min<uint64_t>(n, b + grain));
+      }
+    });
+  for (auto& t : ts) t.join();
+}
+
 int hw_threads(int req) {
   if (req > 0) return std::min(req, 256);
+  // the process's CPU share where the launcher states it (16 per GPU on the box)
+  if (const char* e = getenv("OMP_NUM_THREADS"))
+    if (atoi(e) > 0) return std::min(atoi(e), 256);
   unsigned h = std::thread::hardware_concurrency();
   return (int)std::max(1u, std::min(h, 64u));
 }
@@ -314,6 +354,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ix->w_text[t] = bm25_weight(g ? g->df_text[t] : hp.df_text[t], Ns);
     ix->w_name[t] = bm25_weight(g ? (g->df_name ? g->df_name[t] : 0u) : hp.df_name[t], Ns);
   }
+  g_bt.mark("weights");
   // doc -> position bucket directory (fg_internal.h DevIndex): bucket width
   // 2^B_t docs with B_t the largest shift keeping ~kBucketTarget postings per bucket
   std::vector<uint32_t> dir_off(V), tmeta(V);
@@ -346,7 +387,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   // term, so the query's K-th best is >= it (k_disj's starting threshold)
   ix->ktop.assign((size_t)V * fg::kNumTopK, 0.0f);
   const bool has_name = hp.has_name;
-  parallel_ranges(V, hw_threads(0), [&](int, uint32_t tb, uint32_t te) {
+  parallel_dynamic(V, hw_threads(0), 1, [&](int, uint32_t tb, uint32_t te) {
     std::vector<float> sc;
     for (uint32_t t = tb; t < te; ++t) {
       const uint64_t b0 = hp.off[t], n = hp.off[t + 1] - b0;
@@ -387,6 +428,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       sc.clear();
     }
   });
+  g_bt.mark("dir + scores + ktop");
   // per-term tile maxima (4096-doc tiles of k_disj) for terms whose buckets are
   // no wider than a tile: one load gives a clause's bound over a tile
   std::vector<uint32_t> toff(V, 0xFFFFFFFFu);
@@ -399,7 +441,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       ntm += n_tiles;
     }
   std::vector<float> tmax(ntm, 0.0f);
-  parallel_ranges(V, hw_threads(0), [&](int, uint32_t tb, uint32_t te) {
+  parallel_dynamic(V, hw_threads(0), 256, [&](int, uint32_t tb, uint32_t te) {
     for (uint32_t t = tb; t < te; ++t) {
       if (toff[t] == 0xFFFFFFFFu) continue;
       const uint32_t B = tmeta[t] & 0xFFu;
@@ -412,6 +454,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       }
     }
   });
+  g_bt.mark("tile maxima");
   // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
   // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
   const uint32_t VF = hp.n_fterms;
@@ -447,6 +490,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint32_t *d_doc, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr, *d_toff;
   uint64_t* d_off;
   float *d_psc, *d_tmaxs, *d_bmax, *d_tmax;
+  g_bt.mark("facet weights");
   if ((rc = dev_upload(ix->mem, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
   if ((rc = dev_upload(ix->mem, psc.data(), psc.size(), &d_psc, &bytes))) return rc;
   std::vector<float>().swap(psc);
@@ -460,6 +504,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   if ((rc = dev_upload(ix->mem, toff.data(), toff.size(), &d_toff, &bytes))) return rc;
   std::vector<float>().swap(tmax);
   if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
+  g_bt.mark("upload");
   // dense structures for the densest terms (fg_internal.h DevIndex), chosen
   // AFTER the uploads above so the budgets see the memory actually left: f32
   // score tables (df >= N / kDenseDiv, FUGU_DENSE_GIB) for the densest, then
@@ -552,6 +597,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     HIPCHK(hipStreamSynchronize(nullptr));
   }
   HIPCHK(hipStreamSynchronize(nullptr));
+  g_bt.mark("dense + rank words");
   ix->n_dense = (uint32_t)f32_terms.size();
   ix->n_rank = (uint32_t)rank_terms.size();
   if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
@@ -580,6 +626,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->df_text = std::move(hp.df_text);
   ix->df_name = std::move(hp.df_name);
   if (keep_host) ix->h_doc = std::move(hp.doc);
+  g_bt.mark("tail");
   *out = ix.release();
   return FG_OK;
 }
@@ -772,6 +819,7 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
   if (in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs must be < 2^31 (tantivy DocId)");
   if (std::find(ctx->devs.begin(), ctx->devs.end(), dev) == ctx->devs.end())
     return fail(FG_EINVAL, "device %d not in context", dev);
+  g_bt.start();
   const uint32_t N = in->n_docs, V = in->n_terms;
   const bool has_name_in = in->name_off && in->name_tok;
   const int T = hw_threads(in->threads);
@@ -841,6 +889,7 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
   } catch (...) {
     return fail(FG_EOOM, "host postings (%llu) allocation failed", (unsigned long long)acc);
   }
+  g_bt.mark("pass 1 counts + offsets");
   // pass 2: fill (thread t's docs land after threads < t within each term)
   parallel_ranges(N, T, [&](int t, uint32_t b, uint32_t e) {
     std::vector<uint32_t> scratch;
@@ -874,7 +923,9 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
     for (uint32_t t = 0; t < V; ++t)
       if (g->df_text[t] < hp.df_text[t] || (g->df_name ? g->df_name[t] : 0u) < hp.df_name[t])
         return fail(FG_EINVAL, "global df of term %u is below this shard's", t);
+  g_bt.mark("pass 2 fill");
   if (int rc = build_facets(in, hp, T)) return rc;
+  g_bt.mark("facets");
   return finish_index(dev, hp, in->keep_host_postings != 0, out, g);
 }
 
