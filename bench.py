@@ -69,6 +69,191 @@ def native_oracle():
     return "-O3 -ffp-contract=off -march=x86-64-v2 (portable build: native compile failed)"
 
 
+def timed_steps(step, steps, warmup, torch):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
+    """End-to-end batch throughput: every step plans a DIFFERENT 1024-query batch
+    on the host (fg_plan_create: cost order, work items, H2D), executes it and
+    copies the hits back (D2H), with `workers` batches in flight on their own
+    streams so host planning overlaps the kernels of the other batches."""
+    import threading
+    batches = [synth.queries(nq, 3, 3, seed_q=1000 + i) for i in range(steps + workers)]
+    streams = [torch.cuda.Stream(dev) for _ in range(workers)]
+    plan_ms, errors = [], []
+
+    def work(w, idxs):
+        try:
+            for i in idxs:
+                t1 = time.perf_counter()
+                p = ix.plan(batches[i][0], batches[i][1], K)
+                plan_ms.append((time.perf_counter() - t1) * 1e3)
+                p.execute(streams[w].cuda_stream)
+                p.results()
+                p.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    def run(idxs_all):
+        th = [threading.Thread(target=work, args=(w, idxs_all[w::workers])) for w in range(workers)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    run(list(range(steps, steps + workers)))  # warm the workspace pool and the streams
+    plan_ms.clear()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(list(range(steps)))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if errors:
+        raise RuntimeError(errors[0])
+    return {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_batch": round(el * 1e3 / steps, 3),
+            "batches": steps, "batch": nq, "k": K, "workers": workers,
+            "plan_ms_per_batch_p50": round(float(np.median(plan_ms)), 3),
+            "note": "each step = a different 3-term AND batch: host planning + H2D + k_conj + k_final + D2H of the "
+                    "hits, pipelined over the workers' streams (planning overlaps other batches' kernels)"}
+
+
+def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads):
+    """C4 (BASELINE configs[3]) on one GPU: the 10M docs as 8 namespaces x
+    1.25M, each its own index and statistics; a step = one fan-out 3-term AND
+    top-100 batch on all 8 namespaces + the device merge of the 8 top-100 lists
+    (what each GPU of the 8-GPU run does for its namespace, then the RCCL
+    gather's merge)."""
+    from fugu_amd.shard import merge_on_device, shard_ranges
+    q_off, terms = synth.queries(nq, 3, 3)
+    ranges = shard_ranges(corp.n_docs, 8)
+    ixs, plans = [], []
+    t0 = time.time()
+    for b, e in ranges:
+        off = corp.off[b:e + 1] - corp.off[b]
+        ix = native.Index.from_docs(ctx, off, corp.tok[corp.off[b]:corp.off[e]], synth.VOCAB, threads=threads,
+                                    keep_host=False)
+        ixs.append(ix)
+        plans.append(ix.plan(q_off, terms, K))
+    build_s = time.time() - t0
+    gs = torch.empty((8, nq * K), dtype=torch.float32, device=dev)
+    gd = torch.empty((8, nq * K), dtype=torch.int32, device=dev)
+    gn = torch.empty((8, nq), dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        for r, p in enumerate(plans):
+            p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+        merge_on_device(gs, gd, gn, nq, K, st)
+
+    for p in plans:
+        p.profile(True)
+    el = timed_steps(step, steps, warmup, torch)
+    kms = [p.kernel_ms() for p in plans]
+    per_ns = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
+    del plans
+    for ix in ixs:
+        ix.close()
+    return {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
+            "batch": nq, "k": K, "terms": 3, "mode": "AND", "namespaces": 8, "docs_per_namespace": ranges[0][1],
+            "k_conj_ms_per_namespace": per_ns, "snapshot_build_s": round(build_s, 1),
+            "workload": "C4: 10M docs as 8 namespaces x 1.25M (own statistics each), fan-out 3-term AND top-100 "
+                        "on all 8 + device merge, all 8 namespaces on this one GPU",
+            "projected_8gpu": "each GPU runs one namespace: step ~ max(k_conj_ms_per_namespace) + k_final + gather"}
+
+
+def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_seconds, do_cpu):
+    """C5 (BASELINE configs[4]) on one GPU: 100M docs, Zipf s=1.1, as 8
+    contiguous doc shards scored with the GLOBAL statistics (tantivy's segment
+    model); a step = one 2-5-term OR top-1000 batch on all 8 shards + the device
+    merge by (score desc, shard asc, doc asc)."""
+    from fugu_amd.shard import merge_on_device, shard_ranges
+    K, N, S = 1000, 100_000_000, 1.1
+    t0 = time.time()
+    c = synth.corpus(N, synth.VOCAB, S, threads=threads)
+    ranges = shard_ranges(N, 8)
+    parts = [(c.off[b:e + 1] - c.off[b], c.tok[c.off[b]:c.off[e]]) for b, e in ranges]
+    g = None
+    for off, tok in parts:
+        x = native.docs_stats(off, tok, synth.VOCAB, threads=threads)
+        g = x if g is None else g + x
+    old = os.environ.get("FUGU_RANK_GIB")
+    os.environ["FUGU_RANK_GIB"] = "12"
+    try:
+        ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=False, global_stats=g)
+               for off, tok in parts]
+    finally:
+        if old is None:
+            os.environ.pop("FUGU_RANK_GIB")
+        else:
+            os.environ["FUGU_RANK_GIB"] = old
+    del parts
+    build_s = time.time() - t0
+    log(f"[bench] C5: 100M docs as 8 shards built in {build_s:.1f}s")
+    q_off, terms = synth.queries(nq, 2, 5)
+    plans = [ix.plan(q_off, terms, K, native.MODE_OR) for ix in ixs]
+    gs = torch.empty((8, nq * K), dtype=torch.float32, device=dev)
+    gd = torch.empty((8, nq * K), dtype=torch.int32, device=dev)
+    gn = torch.empty((8, nq), dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    merged = {}
+
+    def step():
+        for r, p in enumerate(plans):
+            p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+        merged["out"] = merge_on_device(gs, gd, gn, nq, K, st)
+
+    for p in plans:
+        p.profile(True)
+    el = timed_steps(step, steps, warmup, torch)
+    kms = [p.kernel_ms() for p in plans]
+    per_shard = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
+    ent = {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
+           "batch": nq, "k": K, "terms": "2-5", "mode": "OR", "n_docs": N, "zipf_s": S, "shards": 8,
+           "k_disj_ms_per_shard": per_shard, "snapshot_build_s": round(build_s, 1),
+           "workload": "C5: 100M docs s=1.1 as 8 doc shards with global BM25 statistics, 2-5-term OR top-1000 on "
+                       "all 8 + device merge, all 8 shards on this one GPU",
+           "projected_8gpu": "each GPU runs one shard: step ~ max(k_disj_ms_per_shard) + k_final + gather"}
+    del plans
+    for ix in ixs:
+        ix.close()
+    if do_cpu:
+        # CPU baseline + parity on a bounded sample: ONE 100M-doc oracle index
+        from oracle import oracle as orc
+        ms_, md, msh, mn = merged["out"]
+        base = np.array([b for b, _ in ranges], np.uint64)
+        ms_ = ms_.cpu().numpy().reshape(nq, K)
+        gdoc = md.cpu().numpy().view(np.uint32).reshape(nq, K).astype(np.uint64) + base[
+            msh.cpu().numpy().reshape(nq, K)]
+        mn = mn.cpu().numpy()
+        ref = orc.OracleIndex(synth.VOCAB, c.off, c.tok, threads=threads)
+        done, wall, mism = 0, 0.0, 0
+        while done < nq and wall < cpu_seconds:
+            hi = min(nq, done + threads)
+            so = (q_off[done:hi + 1] - q_off[done]).astype(np.uint32)
+            rs, rd, rn, w, _ = ref.search_batch(so, terms[q_off[done]:q_off[hi]], K, mode=orc.OR, threads=threads)
+            wall += w
+            for j in range(hi - done):
+                i, m = done + j, int(rn[j])
+                if (int(mn[i]) != m or not np.array_equal(gdoc[i, :m], rd[j, :m].astype(np.uint64))
+                        or not np.allclose(ms_[i, :m], rs[j, :m], rtol=1e-5, atol=0)):
+                    mism += 1
+            done = hi
+        ent["cpu_baseline"] = {"value": round(done / wall, 2), "unit": "queries/s", "cores": threads, "kind": "port",
+                               "sample": f"first {done} queries of the batch on ONE 100M-doc oracle index "
+                                         "(exhaustive union, SumCombiner)"}
+        ent["parity"] = {"queries_checked": done, "mismatches": mism}
+        del ref
+    return ent
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -84,8 +269,9 @@ def main():
     ap.add_argument("--p50-queries", type=int, default=200)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--no-extra", action="store_true",
-                    help="skip the secondary workloads (C3 mixed AND, disjunctive OR top-1000)")
+                    help="skip the secondary workloads (C3, OR top-1000, end-to-end, C4, C5)")
     ap.add_argument("--extra-steps", type=int, default=5)
+    ap.add_argument("--no-c5", action="store_true", help="skip the 100M-doc C5 secondary line")
     args = ap.parse_args()
 
     import torch
@@ -308,6 +494,22 @@ def main():
             extra[name] = ent
             log(f"[bench] {name}: {ent['value']} q/s, {ent['kernel']} {ent['kernel_ms']} ms")
             del pl2
+
+    # ---- end-to-end batches, then the fan-out configs C4 and C5 on this one GPU
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra["e2e_pipelined"] = e2e_pipeline(ix, native, synth, torch, dev, nq, K, 20, 2)
+        log(f"[bench] e2e pipelined: {extra['e2e_pipelined']['value']} q/s")
+    del plan
+    ix.close()
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra["C4_8ns_fanout"] = bench_c4(ctx, corp, native, synth, torch, dev, nq, K, args.extra_steps, 2, threads)
+        log(f"[bench] C4: {extra['C4_8ns_fanout']['value']} q/s")
+        if not args.no_c5:
+            ref = None
+            del corp
+            extra["C5_or_top1000_100M"] = bench_c5(ctx, native, synth, torch, dev, nq, args.extra_steps, 2, threads,
+                                                   args.cpu_seconds / 2, not args.no_cpu)
+            log(f"[bench] C5: {extra['C5_or_top1000_100M']['value']} q/s")
 
     if rank == 0:
         out = {

@@ -1301,7 +1301,10 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.f.ch_clause = (const uint32_t*)put(ch_c.data(), 4ull * nch, s_ch);
   p->d.f.ch_term = (const uint32_t*)put(ch_t.data(), 4ull * nch, s_ch);
   p->d.f.ch_start = (const uint32_t*)put(ch_s.data(), 4ull * nch, s_ch);
-  HIPCHK(hipMemcpy(base, staging.data(), s_in, hipMemcpyHostToDevice));
+  // on the planning thread's own stream: a plan built while another thread's
+  // batch runs does not serialise against it through the legacy null stream
+  HIPCHK(hipMemcpyAsync(base, staging.data(), s_in, hipMemcpyHostToDevice, hipStreamPerThread));
+  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
   char* cur = base + s_in;
   p->zero_region = cur;
   p->zero_bytes = s_thr + s_cc + s_mask;
