@@ -4,6 +4,7 @@
 // reference's Rust toolchain is absent.  Reference citations
 // are on each function.
 #include <algorithm>
+#include <cerrno>
 #include <cctype>
 #include <cinttypes>
 #include <cmath>
@@ -248,6 +249,8 @@ int copy_out(const std::string& s, char* out, size_t cap, size_t* len) {
 // their input order (Rust's HashMap order is unspecified).
 struct JVal {
   enum Kind { Null, Bool, Num, Str, Arr, Obj } kind = Null;
+  bool b = false;                                    // Bool
+  std::string num;                                   // Num: the literal
   std::string str;                                   // Str
   std::vector<JVal> arr;                             // Arr
   std::vector<std::pair<std::string, JVal>> obj;     // Obj
@@ -362,7 +365,8 @@ struct JParser {
       v.kind = JVal::Str;
       ok = string(v.str);
     } else if (lit("null")) { v.kind = JVal::Null; ok = true; }
-    else if (lit("true") || lit("false")) { v.kind = JVal::Bool; ok = true; }
+    else if (lit("true")) { v.kind = JVal::Bool; v.b = true; ok = true; }
+    else if (lit("false")) { v.kind = JVal::Bool; v.b = false; ok = true; }
     else {
       size_t b = i;
       if (i < s.size() && s[i] == '-') ++i;
@@ -370,6 +374,7 @@ struct JParser {
                               s[i] == '+' || s[i] == '-'))
         ++i;
       v.kind = JVal::Num;
+      v.num.assign(s.substr(b, i - b));
       ok = i > b && std::isdigit((unsigned char)s[i - 1]);
     }
     --depth;
@@ -382,6 +387,93 @@ bool parse_json(std::string_view text, JVal& out) {
   if (!p.value(out)) return false;
   p.ws();
   return p.i == text.size();
+}
+
+// serde_json's f64 output (ryu's shortest round-trip digits, ryu's layout:
+// 1e16 -> "1e16", 1e15 -> "1000000000000000.0", 1e-5 -> "1e-5", 1e-4 -> "0.0001").
+void json_f64(std::string& o, double v) {
+  if (v == 0.0) { o += std::signbit(v) ? "-0.0" : "0.0"; return; }
+  char b[48];
+  int p = 1;
+  for (; p <= 17; ++p) {
+    snprintf(b, sizeof b, "%.*e", p - 1, v);
+    if (strtod(b, nullptr) == v) break;
+  }
+  std::string m(b);
+  const size_t epos = m.find('e');
+  const int e10 = atoi(m.c_str() + epos + 1);
+  std::string digits;
+  for (size_t i = 0; i < epos; ++i)
+    if (std::isdigit((unsigned char)m[i])) digits.push_back(m[i]);
+  if (v < 0) o.push_back('-');
+  const int len = (int)digits.size(), kk = e10 + 1, k = kk - len;
+  if (k >= 0 && kk <= 16) {
+    o += digits;
+    o.append((size_t)k, '0');
+    o += ".0";
+  } else if (kk > 0 && kk <= 16) {
+    o += digits.substr(0, (size_t)kk) + "." + digits.substr((size_t)kk);
+  } else if (kk > -5 && kk <= 0) {
+    o += "0.";
+    o.append((size_t)-kk, '0');
+    o += digits;
+  } else {
+    o += digits.substr(0, 1);
+    if (len > 1) o += "." + digits.substr(1);
+    o += "e" + std::to_string(kk - 1);
+  }
+}
+
+// A number as serde_json re-serializes it (no arbitrary_precision): an integer
+// literal that fits u64 (or i64 when negative) stays an integer, "-0" and
+// everything else become f64.
+void json_num(std::string& o, const std::string& lit) {
+  const bool intlike = lit.find_first_of(".eE") == std::string::npos;
+  if (intlike) {
+    errno = 0;
+    if (lit[0] != '-') {
+      const unsigned long long u = strtoull(lit.c_str(), nullptr, 10);
+      if (errno == 0) { o += std::to_string(u); return; }
+    } else {
+      const long long x = strtoll(lit.c_str(), nullptr, 10);
+      if (errno == 0 && x != 0) { o += std::to_string(x); return; }
+    }
+  }
+  json_f64(o, strtod(lit.c_str(), nullptr));
+}
+
+// serde_json::Value serialization: without the preserve_order feature (the
+// reference's Cargo.lock builds serde_json 1.0.140 without indexmap) an object
+// is a BTreeMap, so its keys come out in byte order.
+void json_dump(std::string& o, const JVal& v) {
+  switch (v.kind) {
+    case JVal::Null: o += "null"; break;
+    case JVal::Bool: o += v.b ? "true" : "false"; break;
+    case JVal::Num: json_num(o, v.num); break;
+    case JVal::Str: json_str(o, v.str); break;
+    case JVal::Arr:
+      o.push_back('[');
+      for (size_t i = 0; i < v.arr.size(); ++i) {
+        if (i) o.push_back(',');
+        json_dump(o, v.arr[i]);
+      }
+      o.push_back(']');
+      break;
+    case JVal::Obj: {
+      std::vector<const std::pair<std::string, JVal>*> m;
+      for (auto& kv : v.obj) m.push_back(&kv);
+      std::sort(m.begin(), m.end(), [](auto* a, auto* b) { return a->first < b->first; });
+      o.push_back('{');
+      for (size_t i = 0; i < m.size(); ++i) {
+        if (i) o.push_back(',');
+        json_str(o, m[i]->first);
+        o.push_back(':');
+        json_dump(o, m[i]->second);
+      }
+      o.push_back('}');
+      break;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- facets
@@ -639,6 +731,153 @@ std::vector<std::string> filter_list(const char* const* filters, uint32_t n) {
   return v;
 }
 
+// urlencoding::decode: %XX escapes become bytes (a malformed escape stays as
+// it is); the result must be UTF-8, else "Invalid URL encoding in query"
+bool url_decode(std::string& q) {
+  auto hex = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
+  std::string o;
+  for (size_t i = 0; i < q.size(); ++i) {
+    if (q[i] == '%' && i + 2 < q.size() && hex(q[i + 1]) >= 0 && hex(q[i + 2]) >= 0) {
+      o.push_back((char)(hex(q[i + 1]) * 16 + hex(q[i + 2])));
+      i += 2;
+    } else {
+      o.push_back(q[i]);
+    }
+  }
+  // UTF-8 validation (Rust String::from_utf8)
+  for (size_t i = 0; i < o.size();) {
+    const unsigned char c = (unsigned char)o[i];
+    size_t n = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+    if (!n || i + n > o.size()) return false;
+    uint32_t cp = n == 1 ? c : c & (0x7F >> n);
+    for (size_t k = 1; k < n; ++k) {
+      const unsigned char x = (unsigned char)o[i + k];
+      if ((x >> 6) != 2) return false;
+      cp = (cp << 6) | (x & 0x3F);
+    }
+    if ((n == 2 && cp < 0x80) || (n == 3 && cp < 0x800) || (n == 4 && (cp < 0x10000 || cp > 0x10FFFF)) ||
+        (cp >= 0xD800 && cp < 0xE000))
+      return false;
+    i += n;
+  }
+  q.swap(o);
+  return true;
+}
+
+// The POST /search/json additions (src/server/handlers/search.rs:273-285).
+struct JsonExtras {
+  bool include_data = true, targeting = false;
+  std::string developer_message;  // empty: absent
+};
+
+// perform_search + the handlers' JSON (src/server/handlers/search.rs).  Every
+// response is a serde_json Value, so object keys come out in byte order
+// (BTreeMap: serde_json is built without preserve_order, Cargo.lock:4313-4322).
+//   post_search   search_endpoint (POST /search, :152-207): no per_page clamp,
+//                 text kept, {filters, page, per_page, query, results, status, total}
+//   otherwise     perform_search (:350-402) shapes {page, per_page, query, results,
+//                 total} (+ the POST /search/json extras), text stripped unless asked
+int search_json(fg_db* db, const char* nsname, const std::string& q, const std::vector<std::string>& fl,
+                uint32_t page, uint32_t per_page, bool include_text, bool post_search, const JsonExtras* ex,
+                char* out, size_t cap, size_t* len) {
+  auto ns = find_ns(db, nsname);
+  const std::string nsn = nsname ? nsname : "";
+  if (!ns) {
+    std::string o;
+    if (post_search && !nsname) {
+      o = "{\"error\":\"Default dataset not found\",\"status\":\"error\"}";
+    } else if (post_search) {
+      // POST /search/{namespace} (CLI contract cli.rs:352-355): the POST shape, scoped
+      o = "{\"error\":";
+      json_str(o, "Namespace '" + nsn + "' not found");
+      o += ",\"status\":\"error\"}";
+    } else {
+      o = "{\"error\":";
+      json_str(o, "Search failed: Namespace '" + nsn + "' not found");
+      o += "}";
+    }
+    copy_out(o, out, cap, len);
+    return hfail(FG_ENOTFOUND, "Namespace '" + nsn + "' not found");
+  }
+  if (!post_search && (per_page == 0 || per_page > 100)) per_page = 20;
+  std::vector<fg_hit> hits;
+  int rc = search_hits(db, *ns, q.c_str(), fl, page, per_page, hits);
+  if (rc) {
+    // perform_search wraps Dataset::search's error once, its handler again
+    std::string o = "{\"error\":";
+    json_str(o, std::string(post_search ? "Search failed: " : "Search failed: Search failed: ") + fg_last_error());
+    o += post_search ? ",\"status\":\"error\"}" : "}";
+    copy_out(o, out, cap, len);
+    return rc;
+  }
+  const bool with_text = post_search || include_text;
+  std::string res = "[";
+  {
+    std::lock_guard<std::mutex> w(ns->writer);
+    for (size_t i = 0; i < hits.size(); ++i) {
+      const Doc& d = ns->docs[hits[i].doc];
+      if (i) res.push_back(',');
+      // FuguSearchResult {id, score, text, metadata, facets} (src/db/search.rs:20-27, 534-590) as a Value
+      res += "{\"facets\":";
+      if (d.facets.empty()) {
+        res += "null";
+      } else {
+        res.push_back('[');
+        for (size_t j = 0; j < d.facets.size(); ++j) {
+          if (j) res.push_back(',');
+          json_str(res, facet_display(d.facets[j]));
+        }
+        res.push_back(']');
+      }
+      res += ",\"id\":";
+      json_str(res, d.id);
+      res += ",\"metadata\":";
+      res += d.metadata.empty() ? "null" : d.metadata;
+      res += ",\"score\":";
+      json_f32(res, hits[i].score);
+      if (with_text) {
+        res += ",\"text\":";
+        json_str(res, d.text);
+      }
+      res += "}";
+    }
+  }
+  res += "]";
+  std::string o = "{";
+  char num[64];
+  if (post_search) {
+    o += "\"filters\":[";
+    for (size_t j = 0; j < fl.size(); ++j) {
+      if (j) o.push_back(',');
+      json_str(o, fl[j]);
+    }
+    o += "],";
+  }
+  if (ex) {
+    if (!ex->developer_message.empty()) {
+      o += "\"developer_message\":";
+      json_str(o, ex->developer_message);
+      o += ",";
+    }
+    o += ex->include_data ? "\"includes_data_objects\":true," : "\"includes_data_objects\":false,";
+  }
+  snprintf(num, sizeof num, "\"page\":%u,\"per_page\":%u,\"query\":", page, per_page);
+  o += num;
+  json_str(o, q);
+  o += ",\"results\":" + res;
+  if (post_search) o += ",\"status\":\"success\"";
+  if (ex) o += ex->targeting ? ",\"targeting_conversations_or_organizations\":true"
+                             : ",\"targeting_conversations_or_organizations\":false";
+  snprintf(num, sizeof num, ",\"total\":%zu}", hits.size());
+  o += num;
+  return copy_out(o, out, cap, len);
+}
+
 }  // namespace
 
 extern "C" {
@@ -681,7 +920,8 @@ int fg_db_namespace_delete(fg_db* db, const char* name) {
 
 int fg_db_namespaces_json(fg_db* db, char* out, size_t cap, size_t* len) {
   if (!db) return hfail(FG_EINVAL, "bad arguments");
-  std::string o = "{\"status\":\"success\",\"namespaces\":[";
+  // json!({"status", "namespaces"}) is a serde_json Value: keys in byte order
+  std::string o = "{\"namespaces\":[";
   {
     std::shared_lock<std::shared_mutex> l(db->mu);
     bool first = true;
@@ -691,7 +931,7 @@ int fg_db_namespaces_json(fg_db* db, char* out, size_t cap, size_t* len) {
       json_str(o, kv.first);
     }
   }
-  o += "]}";
+  o += "],\"status\":\"success\"}";
   return copy_out(o, out, cap, len);
 }
 
@@ -749,7 +989,7 @@ int upsert_record(fg_db* db, const char* nsname, const fg_object_record* r, cons
   Doc doc;
   doc.id = sid;
   doc.text = stext;
-  if (has_meta) doc.metadata = r->metadata_json;
+  if (has_meta) json_dump(doc.metadata, meta);  // what the reference returns: serde_json::from_str(stored) re-serialized
   if (name_override) {
     doc.has_name = true;
     doc.name = name_override;
@@ -924,85 +1164,46 @@ int fg_db_search_json_ex(fg_db* db, const char* nsname, const char* query, const
                          uint32_t n_filters, uint32_t page, uint32_t per_page, int include_text, int shape, char* out,
                          size_t cap, size_t* len) {
   if (!db) return hfail(FG_EINVAL, "bad arguments");
-  const std::string q = query ? query : "";
+  if (shape != FG_SHAPE_GET_SEARCH && shape != FG_SHAPE_POST_SEARCH && shape != FG_SHAPE_GET_SEARCH_PATH)
+    return hfail(FG_EINVAL, "bad shape (POST /search/json: fg_db_search_json_post)");
+  std::string q = query ? query : "";
+  if (shape == FG_SHAPE_GET_SEARCH_PATH) {
+    // query_text_path (src/server/handlers/search.rs:79-139): the path component
+    // is URL-decoded; page 0, per_page 20
+    if (!url_decode(q)) {
+      copy_out("{\"error\":\"Invalid URL encoding in query\"}", out, cap, len);
+      return hfail(FG_EINVAL, "Invalid URL encoding in query");
+    }
+    page = 0;
+    per_page = 20;
+  }
+  return search_json(db, nsname, q, filter_list(filters, n_filters), page, per_page, include_text != 0,
+                     shape == FG_SHAPE_POST_SEARCH, nullptr, out, cap, len);
+}
+
+int fg_db_search_json_post(fg_db* db, const char* nsname, const char* query, const char* const* filters,
+                           uint32_t n_filters, int has_page, uint32_t page, uint32_t per_page, int url_text,
+                           int body_text, int url_include_data, int body_include_data, char* out, size_t cap,
+                           size_t* len) {
+  // query_json_post (src/server/handlers/search.rs:210-301)
+  if (!db) return hfail(FG_EINVAL, "bad arguments");
   const std::vector<std::string> fl = filter_list(filters, n_filters);
-  // perform_search (src/server/handlers/search.rs:350-402): namespace lookup, then
-  // per_page 0 or > 100 -> 20; the POST /search shape has no clamp (:183)
-  auto ns = find_ns(db, nsname);
-  if (!ns) {
-    std::string o = "{\"error\":";
-    json_str(o, std::string("Search failed: Namespace '") + (nsname ? nsname : "") + "' not found");
-    o += "}";
-    copy_out(o, out, cap, len);
-    return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
+  if (!has_page) { page = 0; per_page = 20; }
+  // text: the URL flag wins when set; a disagreeing body flag adds a developer_message
+  const bool include_text = url_text >= 0 ? url_text != 0 : body_text > 0;
+  JsonExtras ex;
+  if (url_text >= 0 && body_text >= 0 && (url_text != 0) != (body_text != 0))
+    ex.developer_message = "url and request body are set to different values; using url:true/false";
+  // is_targeting_conversations_or_organizations (handlers/utils.rs:4-14)
+  ex.targeting = false;
+  for (auto& f : fl) {
+    const std::string n = !f.empty() && f[0] == '/' ? f : "/" + f;
+    if (n.find("/conversation") != std::string::npos || n.find("/organization") != std::string::npos) ex.targeting = true;
   }
-  if (shape == FG_SHAPE_GET_SEARCH && (per_page == 0 || per_page > 100)) per_page = 20;
-  std::vector<fg_hit> hits;
-  int rc = search_hits(db, *ns, q.c_str(), fl, page, per_page, hits);
-  if (rc) {
-    std::string o = "{\"error\":";
-    json_str(o, std::string("Search failed: ") + fg_last_error());
-    o += "}";
-    copy_out(o, out, cap, len);
-    return rc;
-  }
-  std::string res = "[";
-  {
-    std::lock_guard<std::mutex> w(ns->writer);
-    for (size_t i = 0; i < hits.size(); ++i) {
-      const Doc& d = ns->docs[hits[i].doc];
-      if (i) res.push_back(',');
-      // FuguSearchResult {id, score, text, metadata, facets} (src/db/search.rs:20-27, 534-590)
-      res += "{\"id\":";
-      json_str(res, d.id);
-      res += ",\"score\":";
-      json_f32(res, hits[i].score);
-      if (include_text) {
-        res += ",\"text\":";
-        json_str(res, d.text);
-      }
-      res += ",\"metadata\":";
-      res += d.metadata.empty() ? "null" : d.metadata;
-      res += ",\"facets\":";
-      if (d.facets.empty()) {
-        res += "null";
-      } else {
-        res.push_back('[');
-        for (size_t j = 0; j < d.facets.size(); ++j) {
-          if (j) res.push_back(',');
-          json_str(res, facet_display(d.facets[j]));
-        }
-        res.push_back(']');
-      }
-      res += "}";
-    }
-  }
-  res += "]";
-  std::string o;
-  char num[64];
-  if (shape == FG_SHAPE_POST_SEARCH) {
-    // search_endpoint (src/server/handlers/search.rs:184-195)
-    o = "{\"status\":\"success\",\"query\":";
-    json_str(o, q);
-    o += ",\"filters\":[";
-    for (size_t j = 0; j < fl.size(); ++j) {
-      if (j) o.push_back(',');
-      json_str(o, fl[j]);
-    }
-    o += "]";
-    snprintf(num, sizeof num, ",\"page\":%u,\"per_page\":%u,\"total\":%zu", page, per_page, hits.size());
-    o += num;
-    o += ",\"results\":" + res + "}";
-  } else {
-    // SearchResponse {results, total, page, per_page, query} (server/types.rs)
-    o = "{\"results\":" + res;
-    snprintf(num, sizeof num, ",\"total\":%zu,\"page\":%u,\"per_page\":%u", hits.size(), page, per_page);
-    o += num;
-    o += ",\"query\":";
-    json_str(o, q);
-    o += "}";
-  }
-  return copy_out(o, out, cap, len);
+  // include_data: body, else URL, else !targeting
+  ex.include_data = body_include_data >= 0 ? body_include_data != 0
+                    : url_include_data >= 0 ? url_include_data != 0 : !ex.targeting;
+  return search_json(db, nsname, query ? query : "", fl, page, per_page, include_text, false, &ex, out, cap, len);
 }
 
 int fg_db_search_json(fg_db* db, const char* nsname, const char* query, uint32_t page, uint32_t per_page,

@@ -19,6 +19,7 @@ FG_ENOTFOUND = -6
 FG_EEXIST = -7
 SHAPE_GET_SEARCH = 0
 SHAPE_POST_SEARCH = 1
+SHAPE_GET_SEARCH_PATH = 2
 
 # every symbol include/fugu_host.h declares (checked by tests/test_abi.py)
 HOST_EXPORTS = (
@@ -26,7 +27,7 @@ HOST_EXPORTS = (
     "fg_db_namespaces_json", "fg_db_upsert", "fg_db_commit", "fg_db_add_file", "fg_db_doc_count",
     "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query",
     "fg_db_upsert_record", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
-    "fg_facet_clauses",
+    "fg_facet_clauses", "fg_db_search_json_post",
 )
 
 _lib = native.lib()
@@ -67,6 +68,8 @@ _sig("fg_db_search_ex", _p, _s, _s, C.POINTER(_s), C.c_uint32, C.c_uint32, C.c_u
      C.POINTER(C.c_uint32))
 _sig("fg_db_search_json_ex", _p, _s, _s, C.POINTER(_s), C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, _s,
      _sz, C.POINTER(_sz))
+_sig("fg_db_search_json_post", _p, _s, _s, C.POINTER(_s), C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
+     C.c_int, C.c_int, C.c_int, _s, _sz, C.POINTER(_sz))
 _sig("fg_db_doc_facets", _p, _s, C.c_uint32, _s, _sz, C.POINTER(_sz))
 _sig("fg_facet_tokens", _s, _s, _sz, C.POINTER(_sz))
 _sig("fg_facet_clauses", C.POINTER(_s), C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
@@ -103,7 +106,11 @@ def _string_call(fn, *args, cap: int = 1 << 16) -> str:
         if rc == native.FG_EINVAL and n.value + 1 > cap:
             cap = n.value + 1
             continue
-        _check(rc)
+        try:
+            _check(rc)
+        except native.FuguError as e:
+            e.body = buf.raw[:n.value].decode(errors="replace")  # the handler's error JSON, when one was written
+            raise
         return buf.raw[:n.value].decode()
 
 
@@ -227,6 +234,17 @@ class Database:
         _check(_lib.fg_db_search_ex(self._h, _b(namespace), query.encode(), farr, nf, page, per_page, out,
                                     max(1, per_page), C.byref(n)))
         return [(out[i].score, out[i].doc) for i in range(n.value)]
+
+    def search_json_post(self, namespace: Optional[str], query: str, filters=None, page: Optional[tuple] = None,
+                         url_text: Optional[bool] = None, body_text: Optional[bool] = None,
+                         url_include_data: Optional[bool] = None, body_include_data: Optional[bool] = None) -> str:
+        """POST /search/json: page = (page, per_page) or None (no `page` object)."""
+        tri = lambda b: -1 if b is None else int(bool(b))  # noqa: E731
+        farr, nf = _strs(filters)
+        pg, pp = page if page is not None else (0, 20)
+        return _string_call(_lib.fg_db_search_json_post, self._h, _b(namespace), query.encode(), farr, nf,
+                            int(page is not None), pg, pp, tri(url_text), tri(body_text), tri(url_include_data),
+                            tri(body_include_data))
 
     def search_json(self, namespace: Optional[str], query: str, page: int = 0, per_page: int = 20,
                     include_text: bool = False, shape: int = SHAPE_GET_SEARCH, filters=None) -> str:

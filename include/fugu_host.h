@@ -48,8 +48,15 @@ typedef struct fg_db fg_db;
 #define FG_EEXIST (-7)    /* namespace already exists */
 
 /* Response shapes. */
-#define FG_SHAPE_GET_SEARCH 0  /* GET /search, GET /search/{q}: SearchResponse, text stripped unless asked */
-#define FG_SHAPE_POST_SEARCH 1 /* POST /search, POST /search/{namespace}: status/query/filters/page/... */
+/* Every response is a serde_json Value in the reference, so object keys come out
+ * in byte order (serde_json without preserve_order, Cargo.lock:4313-4322), and
+ * stored metadata is re-serialized the same way (sorted keys, serde numbers). */
+#define FG_SHAPE_GET_SEARCH 0  /* GET /search: {page, per_page, query, results, total}, text stripped unless asked */
+#define FG_SHAPE_POST_SEARCH 1 /* POST /search, POST /search/{namespace}: {filters, page, per_page, query,
+                                * results, status, total}, text kept, no per_page clamp */
+#define FG_SHAPE_GET_SEARCH_PATH 2 /* GET /search/{query} (handlers/search.rs:79-139): `query` is the URL-encoded
+                                    * path component (decoded here; bad UTF-8 -> 400 "Invalid URL encoding in
+                                    * query", FG_EINVAL); page 0, per_page 20 */
 
 /* ctx may be NULL: the registry, upserts and doc store then work on the host
  * alone and fg_db_commit fails with FG_ENODEV (CPU tests of the host logic). */
@@ -57,7 +64,7 @@ int fg_db_create(fg_ctx* ctx, int dev, const char* default_namespace, fg_db** ou
 int fg_db_destroy(fg_db* db);
 int fg_db_namespace_create(fg_db* db, const char* name);
 int fg_db_namespace_delete(fg_db* db, const char* name);
-/* {"status":"success","namespaces":[...]} (handlers/namespaces.rs:24-30), names sorted */
+/* {"namespaces":[...],"status":"success"} (handlers/namespaces.rs:24-30), names sorted */
 int fg_db_namespaces_json(fg_db* db, char* out, size_t cap, size_t* len);
 
 /* ObjectRecord (src/object.rs:8-27) as the upsert routes receive it. */
@@ -97,6 +104,17 @@ int fg_db_search_json_ex(fg_db* db, const char* ns, const char* query, const cha
                          size_t cap, size_t* len);
 int fg_db_search_json(fg_db* db, const char* ns, const char* query, uint32_t page, uint32_t per_page,
                       int include_text, int shape, char* out, size_t cap, size_t* len);
+/* POST /search/json (query_json_post, handlers/search.rs:210-301): the
+ * JsonQueryRequest fields and the ?text= / ?include_data= URL flags, each flag
+ * tri-state (-1 absent, 0 false, 1 true); has_page = 0 means no `page` object
+ * (page 0, per_page 20).  Text: the URL flag wins, a disagreeing body flag adds
+ * "developer_message"; "includes_data_objects" = body flag, else URL flag, else
+ * not targeting; "targeting_conversations_or_organizations" = a filter
+ * containing /conversation or /organization (handlers/utils.rs:4-14). */
+int fg_db_search_json_post(fg_db* db, const char* ns, const char* query, const char* const* filters,
+                           uint32_t n_filters, int has_page, uint32_t page, uint32_t per_page, int url_text,
+                           int body_text, int url_include_data, int body_include_data, char* out, size_t cap,
+                           size_t* len);
 /* Stored facets of doc `doc` as Facet Display strings, '\n'-separated. */
 int fg_db_doc_facets(fg_db* db, const char* ns, uint32_t doc, char* out, size_t cap, size_t* len);
 

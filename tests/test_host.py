@@ -194,6 +194,54 @@ def test_commit_needs_a_device_and_search_before_commit_is_empty(db):
         d.search(None, "hello", page=1000, per_page=100)  # offset + per_page > FG_MAX_K
 
 
+def test_response_shapes_byte_exact(db):
+    """The handlers build serde_json Values (json!, to_value): serde_json without
+    preserve_order (reference Cargo.lock:4313-4322) keeps object keys in byte
+    order, so the bytes below are what the reference server writes."""
+    d = db.Database()
+    d.create_namespace("ns1")
+    assert d.search_json(None, "hello", 0, 0) == '{"page":0,"per_page":20,"query":"hello","results":[],"total":0}'
+    assert d.search_json(None, "hello", 2, 5, shape=db.SHAPE_POST_SEARCH, filters=["/a/b"]) == \
+        '{"filters":["/a/b"],"page":2,"per_page":5,"query":"hello","results":[],"status":"success","total":0}'
+    assert d.namespaces_json() == '{"namespaces":["fugu_db","ns1"],"status":"success"}'
+    # GET /search/{query}: URL-decoded path component, page 0, per_page 20 whatever is passed
+    assert d.search_json("ns1", "hello%20w%C3%B6rld", 3, 7, shape=db.SHAPE_GET_SEARCH_PATH) == \
+        '{"page":0,"per_page":20,"query":"hello w\u00f6rld","results":[],"total":0}'
+    with pytest.raises(db.native.FuguError) as e:
+        d.search_json("ns1", "bad%ffutf8", shape=db.SHAPE_GET_SEARCH_PATH)
+    assert e.value.code == db.native.FG_EINVAL and e.value.body == '{"error":"Invalid URL encoding in query"}'
+    # errors
+    with pytest.raises(db.NotFound) as e:
+        d.search_json("nope", "x")
+    assert e.value.body == '{"error":"Search failed: Namespace \'nope\' not found"}'
+    with pytest.raises(db.NotFound) as e:
+        d.search_json("nope", "x", shape=db.SHAPE_POST_SEARCH)
+    assert e.value.body == '{"error":"Namespace \'nope\' not found","status":"error"}'
+    with pytest.raises(db.native.Unsupported) as e:
+        d.search_json("ns1", "a -b")
+    assert e.value.body.startswith('{"error":"Search failed: Search failed: query outside the device subset')
+
+
+def test_post_search_json_flags(db):
+    """query_json_post (handlers/search.rs:210-301): text flag resolution,
+    developer_message, includes_data_objects, targeting_conversations_or_organizations."""
+    d = db.Database()
+    r = d.search_json_post(None, "hello")
+    assert r == ('{"includes_data_objects":true,"page":0,"per_page":20,"query":"hello","results":[],'
+                 '"targeting_conversations_or_organizations":false,"total":0}')
+    r = json.loads(d.search_json_post(None, "hello", url_text=True, body_text=False, page=(1, 500)))
+    assert r["developer_message"] == "url and request body are set to different values; using url:true/false"
+    assert (r["page"], r["per_page"]) == (1, 20)  # perform_search clamp
+    assert "developer_message" not in json.loads(d.search_json_post(None, "h", url_text=True, body_text=True))
+    assert "developer_message" not in json.loads(d.search_json_post(None, "h", body_text=False))
+    r = json.loads(d.search_json_post(None, "h", filters=["organization/acme"]))
+    assert r["targeting_conversations_or_organizations"] is True and r["includes_data_objects"] is False
+    r = json.loads(d.search_json_post(None, "h", filters=["/x/conversation/1"], url_include_data=True))
+    assert r["targeting_conversations_or_organizations"] is True and r["includes_data_objects"] is True
+    r = json.loads(d.search_json_post(None, "h", filters=["/x"], url_include_data=True, body_include_data=False))
+    assert r["targeting_conversations_or_organizations"] is False and r["includes_data_objects"] is False
+
+
 # ------------------------------------------------------------------ facets (SURVEY §8f-3)
 def string_leaves(v):
     if isinstance(v, dict):
@@ -470,3 +518,39 @@ def test_db_facet_filters_end_to_end_vs_oracle(db):
     assert checked > 300
     with pytest.raises(native.Unsupported):  # text AND an AllQuery facet filter
         d.search("fx", "alpha", filters=["/*"])
+
+
+@pytest.mark.gpu
+def test_json_shapes_with_hits_and_canonical_metadata(db):
+    """Hits through every handler shape, byte-exact: serde_json re-serializes the
+    stored metadata (from_str -> Value: sorted keys, serde number forms) and
+    every response object has its keys in byte order."""
+    from fugu_amd import native
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    raw = ('{"z": 1, "a": {"y": 2.50, "b": 1e16, "c": -0, "d": 1.0E-5, "g": 1e-6, "e": 18446744073709551616, '
+           '"f": [true, null, "s\\u00e9"]}, "m": -12, "name": "N1"}')
+    assert db._lib.fg_db_upsert(d._h, None, b"d1", b"alpha beta", None, raw.encode()) == 0
+    d.upsert(db.ObjectRecord("d2", "alpha gamma", facets=["/t/x"]))
+    d.commit()
+    canon = ('{"a":{"b":1e16,"c":-0.0,"d":0.00001,"e":1.8446744073709552e19,"f":[true,null,"sé"],'
+             '"g":1e-6,"y":2.5},"m":-12,"name":"N1","z":1}')
+    hits = d.search(None, "alpha", 0, 10)
+    assert [h[1] for h in hits] == [0, 1] or [h[1] for h in hits] == [1, 0]
+    out = d.search_json(None, "alpha", 0, 10, include_text=True)
+    r = json.loads(out)
+    by = {x["id"]: x for x in r["results"]}
+    assert canon in out
+    assert list(by["d1"].keys()) == ["facets", "id", "metadata", "score", "text"]
+    assert by["d2"]["facets"] == ["/t/x"] and by["d2"]["metadata"] is None
+    assert list(r.keys()) == ["page", "per_page", "query", "results", "total"]
+    assert "text" not in json.loads(d.search_json(None, "alpha", 0, 10))["results"][0]
+    p = json.loads(d.search_json_post(None, "alpha", filters=["/t/x"], url_text=True))
+    assert list(p.keys()) == ["includes_data_objects", "page", "per_page", "query", "results",
+                              "targeting_conversations_or_organizations", "total"]
+    assert [x["id"] for x in p["results"]] == ["d2"] and "text" in p["results"][0]
+    s = json.loads(d.search_json(None, "alpha", 0, 10, shape=db.SHAPE_POST_SEARCH))
+    assert list(s.keys()) == ["filters", "page", "per_page", "query", "results", "status", "total"]
+    assert all("text" in x for x in s["results"])
+    g = json.loads(d.search_json(None, "alpha%20gamma", 5, 5, shape=db.SHAPE_GET_SEARCH_PATH))
+    assert g["query"] == "alpha gamma" and (g["page"], g["per_page"]) == (0, 20) and g["results"][0]["id"] == "d2"
