@@ -272,6 +272,8 @@ def main():
                     help="skip the secondary workloads (C3, OR top-1000, end-to-end, C4, C5)")
     ap.add_argument("--extra-steps", type=int, default=5)
     ap.add_argument("--no-c5", action="store_true", help="skip the 100M-doc C5 secondary line")
+    ap.add_argument("--disj", action="store_true",
+                    help="headline batch = 2-5-term OR (k_disj; profiling runs, pass --k 1000 --no-cpu)")
     args = ap.parse_args()
 
     import torch
@@ -306,13 +308,16 @@ def main():
     log(f"[bench] index: {st.n_postings} postings, {st.device_bytes / 2**30:.2f} GiB in HBM, built in "
         f"{time.time() - t0:.1f}s")
 
-    m_min, m_max = (1, 5) if args.mixed else (args.terms, args.terms)
+    m_min, m_max = (1, 5) if args.mixed else (2, 5) if args.disj else (args.terms, args.terms)
+    qmode = native.MODE_OR if args.disj else native.MODE_AND
+    kname = "k_disj" if args.disj else "k_conj"
+    wl_terms = "1-5" if args.mixed else "2-5 OR" if args.disj else args.terms
     q_off_all, terms_all = synth.queries(4096, m_min, m_max)
     nq = args.batch
     q_off = q_off_all[: nq + 1].copy()
     terms = terms_all[: q_off[-1]].copy()
     K = args.k
-    plan = ix.plan(q_off, terms, K)
+    plan = ix.plan(q_off, terms, K, qmode)
     info = plan.info()
     log(f"[bench] plan: {info.total_chunks} work items, workspace {info.workspace_bytes / 2**20:.1f} MiB")
 
@@ -366,10 +371,10 @@ def main():
     # layout (fg_bytes_model_gpu: k_conj's exhaustive cascade) over
     # its HIP-event time on the launch stream.  The SURVEY 8(d) tantivy byte
     # model (1 KiB block decode per probed block) is reported beside it, labelled.
-    bmg = ix.bytes_model_gpu(q_off, terms, K)
+    bmg = ix.bytes_model_gpu(q_off, terms, K, qmode)
     alg_bytes = float(bmg[:, 3].sum())
-    bm = ix.bytes_model(q_off, terms, K)
-    cpu_model_bytes = float(bm[:, 2].sum())
+    # (FG_MODE_OR: the exhaustive union is both models)
+    cpu_model_bytes = alg_bytes if args.disj else float(ix.bytes_model(q_off, terms, K)[:, 2].sum())
     conj_ms = ms_k[0] / max(n_prof, 1)
     achieved = alg_bytes / (conj_ms * 1e-3) / 1e9
     # HBM bytes per k_conj launch from rocprofv3 PMC (FETCH_SIZE with the
@@ -386,8 +391,8 @@ def main():
         from lib_id import lib_id
         same_build = pmc.get("lib_id") == lib_id()
         if same_build and (not wl or (wl.get("n_docs") == args.docs and wl.get("batch") == nq and wl.get("k") == K
-                                      and wl.get("terms") == (args.terms if not args.mixed else "1-5"))):
-            traffic = pmc.get("k_conj_hbm_bytes_per_launch")
+                                      and wl.get("terms") == wl_terms)):
+            traffic = pmc.get(f"{kname}_hbm_bytes_per_launch")
         else:
             log(f"[bench] {pmc_file} does not match this build/workload: roofline.traffic = null")
 
@@ -526,17 +531,18 @@ def main():
             "dtype": "u32+f32",
             "data": "synthetic",
             "config": {
-                "workload": (f"{'C3 mixed 1-5' if args.mixed else str(args.terms) + '-term'} AND, BM25 top-{K}, "
+                "workload": (f"{'C3 mixed 1-5' if args.mixed else '2-5-term OR' if args.disj else str(args.terms) + '-term'}"
+                             f"{'' if args.disj else ' AND'}, BM25 top-{K}, "
                              f"{args.docs // 1_000_000}M-doc Zipf s=1.0 corpus per namespace, batch {nq}"),
                 "n_docs": args.docs, "vocab": synth.VOCAB, "batch": nq, "k": K,
-                "terms": "1-5" if args.mixed else args.terms, "namespaces": world,
+                "terms": wl_terms, "namespaces": world,
                 "parallelism": f"namespace-shard x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
             },
             "p50_ms": round(p50_ms, 4) if p50_ms is not None else None,
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_conj", "kernel_ms": round(conj_ms, 4),
+                "kernel": kname, "kernel_ms": round(conj_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
                 "alg_model": "fg_bytes_model_gpu: k_conj's exhaustive cascade at the HBM layout (8 B per lead "
                              "posting; per probe 4 B dense element, or 8 B bucket bounds + 4 B per search step + "
@@ -552,7 +558,7 @@ def main():
                              "block); not bytes this layout reads",
                 "cpu_model_gbs": round(cpu_model_bytes / (conj_ms * 1e-3) / 1e9, 1),
             },
-            "kernels_ms_per_step": {"k_conj": round(ms_k[0] / max(n_prof, 1), 4),
+            "kernels_ms_per_step": {kname: round(ms_k[0] / max(n_prof, 1), 4),
                                     "k_final": round(ms_k[1] / max(n_prof, 1), 4)},
             "cpu_baseline": cpu,
             "parity": parity,

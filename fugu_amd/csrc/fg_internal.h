@@ -181,6 +181,38 @@ __host__ __device__ inline float key_score(uint64_t k) {
 }
 __host__ __device__ inline uint32_t key_doc(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
 
+// Snapshot scoring on the device (k_score / k_bucket / k_ktop): every posting's
+// BM25 term score from its term frequencies and the doc's fieldnorm ids with
+// the snapshot's statistics, then the bounds the kernels prune with.  Run at
+// build and again by fg_index_rescore when a commit changes the statistics.
+// Work is split into chunks of one term: k_score over postings, k_bucket over
+// directory buckets; ch_* arrays are the chunk tables.
+constexpr uint32_t kScoreChunk = 2048;   // postings per k_score workgroup
+constexpr uint32_t kBucketChunk = 2048;  // buckets per k_bucket workgroup
+struct ScoreJob {
+  const uint32_t* doc;
+  const uint32_t* tfp;        // [P] tf_text | tf_name << 16
+  const uint8_t* fn_text;     // [N] fieldnorm ids
+  const uint8_t* fn_name;     // [N] or nullptr
+  const uint64_t* off;        // [V+1]
+  const uint32_t* dir;
+  const uint32_t* dir_off;
+  const uint32_t* tmeta;
+  const uint32_t* toff;       // [V] tile-maxima offset or 0xFFFFFFFF
+  const uint32_t* alive;      // bitset or nullptr
+  const float* w_text;        // [V] idf * (1 + K1)
+  const float* w_name;        // [V]
+  const float* cache;         // [512] K1 * ((1 - B) + B * TABLE[id] / avgdl), text then name
+  float* psc;                 // [P] out
+  float* bmax;                // [D] out
+  uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
+  uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
+  float* ktop;                // [V * kNumTopK] out (zeroed first)
+  const uint32_t* ch_term;    // chunk tables
+  const uint32_t* ch_first;
+  const uint32_t* kt_terms;   // k_ktop: terms with df >= kTopKs[1]
+};
+
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
@@ -190,6 +222,9 @@ hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, 
 hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s);
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
                        uint32_t n_words, uint64_t* out, hipStream_t s);
+hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
+hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);
+hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

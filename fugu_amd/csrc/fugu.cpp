@@ -244,27 +244,39 @@ struct fg_index {
   int dev = 0;
   uint32_t n_docs = 0, n_terms = 0;
   bool has_name = false;
-  uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0;
+  uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0, tile_entries = 0;
   uint32_t n_dense = 0, n_rank = 0;
+  // ---- statistics and scoring (this snapshot's own)
   uint64_t tot[2] = {0, 0};
   uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
   float avgdl[2] = {0, 0};
   float cache[512];
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> df_text, df_name;
-  std::vector<uint32_t> first_doc, last_doc;
   std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
   std::vector<float> tmaxs; // [V] largest posting score per term
   std::vector<float> w_text, w_name;
-  std::vector<uint32_t> h_doc;  // optional host copy for fg_bytes_model / fg_bytes_model_gpu
+  // ---- structure (independent of the statistics; shared with rescored snapshots)
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> df_text, df_name;  // this snapshot's own postings (tantivy's per-segment cost order)
+  std::vector<uint32_t> first_doc, last_doc;
+  std::shared_ptr<const std::vector<uint32_t>> h_doc;  // optional host copy for fg_bytes_model(_gpu)
   std::vector<uint32_t> tmeta;  // host copy of DevIndex::tmeta (probe kind of each term)
+  uint64_t tot_local[2] = {0, 0};
   // facet field (FG_FIELD_FACET)
   uint32_t n_fterms = 0;
-  uint64_t tot_f = 0;
+  uint64_t tot_f = 0, tot_f_local = 0;
   float avgdl_f = 0.0f, cache_f1 = 0.0f;
   std::vector<uint64_t> foff;
-  std::vector<uint32_t> df_facet, ffirst, flast;
+  std::vector<uint32_t> df_facet, df_facet_local, ffirst, flast;
   std::vector<float> fscore;    // a facet clause's score in a doc holding the term (tf 1, fieldnorm id 1)
+  // device: structure arrays (smem, shared) and the scoring tables (mem)
+  std::shared_ptr<DevAllocs> smem;
+  uint64_t struct_bytes = 0;
+  const uint32_t* d_tfp = nullptr;
+  const uint8_t* d_fn_text = nullptr;
+  const uint8_t* d_fn_name = nullptr;
+  const uint32_t *d_sc_term = nullptr, *d_sc_first = nullptr, *d_bk_term = nullptr, *d_bk_first = nullptr,
+                 *d_kt_terms = nullptr;
+  uint32_t n_sc = 0, n_bk = 0, n_kt = 0;
   fg::DevIndex d{};
   DevAllocs mem;
   WsPool pool;  // plan workspaces (destroyed before mem: declared after it)
@@ -327,34 +339,186 @@ int check_device(int dev) {
   return FG_OK;
 }
 
-// Stats, weights, skip index, upload.  Consumes hp.  g: global statistics of
-// a doc-sharded namespace (NULL: the shard's own).
+// ---------------------------------------------------------------- snapshot scoring
+// The statistics-dependent half of a snapshot: BM25 weights and tf cache (host,
+// tantivy's f32 order with the host libm), then on the device every posting's
+// score (k_score), the bucket / term / tile maxima (k_bucket) and the per-term
+// K-th best alive scores (k_ktop), optional f32 score tables, the alive
+// bitset.  `df_t`/`df_n`/`df_f`: the statistics' doc frequencies (global for a
+// doc-sharded namespace).  Structure arrays must be in ix->d already.
+int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_t* df_t, const uint32_t* df_n,
+                const std::vector<uint32_t>& alive, uint64_t tot_f, const uint32_t* df_f) {
+  const uint32_t V = ix->n_terms;
+  const uint64_t N = ix->n_docs;
+  ix->n_stats = Ns;
+  ix->tot[0] = tot2[0];
+  ix->tot[1] = tot2[1];
+  for (int f = 0; f < 2; ++f) {
+    ix->avgdl[f] = (float)ix->tot[f] / (float)Ns;  // total_num_tokens as f32 / N as f32
+    bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
+  }
+  ix->w_text.resize(V);
+  ix->w_name.resize(V);
+  for (uint32_t t = 0; t < V; ++t) {
+    ix->w_text[t] = bm25_weight(df_t[t], Ns);
+    ix->w_name[t] = bm25_weight(df_n ? df_n[t] : 0u, Ns);
+  }
+  // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
+  // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
+  const uint32_t VF = ix->n_fterms;
+  ix->tot_f = tot_f;
+  ix->df_facet.assign(df_f, df_f + VF);
+  ix->fscore.assign(VF, 0.0f);
+  if (ix->tot_f > 0) {
+    float cf[256];
+    ix->avgdl_f = (float)ix->tot_f / (float)Ns;
+    bm25_cache(ix->avgdl_f, cf);
+    ix->cache_f1 = cf[1];
+    for (uint32_t t = 0; t < VF; ++t) ix->fscore[t] = bm25_weight(ix->df_facet[t], Ns) * (1.0f / (1.0f + ix->cache_f1));
+  }
+  g_bt.mark("weights");
+  HIPCHK(hipSetDevice(ix->dev));
+  uint64_t bytes = 0;
+  int rc;
+  float *d_wt, *d_wn, *d_cache, *d_psc, *d_bmax, *d_ktop;
+  uint32_t *d_alive = nullptr, *d_tmaxs, *d_tmax;
+  if ((rc = dev_upload(ix->mem, ix->w_text.data(), V, &d_wt, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, ix->w_name.data(), V, &d_wn, &bytes))) return rc;
+  if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
+  if (!alive.empty() && (rc = dev_upload(ix->mem, alive.data(), alive.size(), &d_alive, &bytes))) return rc;
+  auto dev_alloc = [&](size_t n_bytes, void** p) -> int {
+    if (hipMalloc(p, std::max<size_t>(n_bytes, 16)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", n_bytes);
+    ix->mem.ptrs.push_back(*p);
+    bytes += std::max<size_t>(n_bytes, 16);
+    return FG_OK;
+  };
+  void* p;
+  if ((rc = dev_alloc(4ull * ix->n_postings, &p))) return rc;
+  d_psc = static_cast<float*>(p);
+  if ((rc = dev_alloc(4ull * ix->dir_entries, &p))) return rc;
+  d_bmax = static_cast<float*>(p);
+  if ((rc = dev_alloc(4ull * V, &p))) return rc;
+  d_tmaxs = static_cast<uint32_t*>(p);
+  if ((rc = dev_alloc(4ull * ix->tile_entries, &p))) return rc;
+  d_tmax = static_cast<uint32_t*>(p);
+  if ((rc = dev_alloc(4ull * V * fg::kNumTopK, &p))) return rc;
+  d_ktop = static_cast<float*>(p);
+  HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, nullptr));
+  HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), nullptr));
+  HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, nullptr));
+  fg::ScoreJob j{};
+  j.doc = ix->d.doc;
+  j.tfp = ix->d_tfp;
+  j.fn_text = ix->d_fn_text;
+  j.fn_name = ix->has_name ? ix->d_fn_name : nullptr;
+  j.off = ix->d.off;
+  j.dir = ix->d.dir;
+  j.dir_off = ix->d.dir_off;
+  j.tmeta = ix->d.tmeta;
+  j.toff = ix->d.toff;
+  j.alive = d_alive;
+  j.w_text = d_wt;
+  j.w_name = d_wn;
+  j.cache = d_cache;
+  j.psc = d_psc;
+  j.bmax = d_bmax;
+  j.tmaxs = d_tmaxs;
+  j.tmax = d_tmax;
+  j.ktop = d_ktop;
+  j.ch_term = ix->d_sc_term;
+  j.ch_first = ix->d_sc_first;
+  HIPCHK(fg::launch_score(j, ix->n_sc, nullptr));
+  j.ch_term = ix->d_bk_term;
+  j.ch_first = ix->d_bk_first;
+  HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, nullptr));
+  j.kt_terms = ix->d_kt_terms;
+  HIPCHK(fg::launch_ktop(j, ix->n_kt, nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));
+  ix->tmaxs.resize(V);
+  ix->ktop.resize((size_t)V * fg::kNumTopK);
+  HIPCHK(hipMemcpy(ix->tmaxs.data(), d_tmaxs, 4ull * V, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ix->ktop.data(), d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost));
+  g_bt.mark("device scoring");
+  // f32 score tables (FUGU_DENSE_GIB, default none: rank words serve the dense
+  // terms) for the densest terms without rank words, filled from the new scores
+  std::vector<uint32_t> f32_terms;
+  float* d_dense = nullptr;
+  {
+    const char* v = getenv("FUGU_DENSE_GIB");
+    const uint64_t want = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kDenseBudget;
+    if (want > 0) {
+      size_t free_b = 0, total_b = 0;
+      HIPCHK(hipMemGetInfo(&free_b, &total_b));
+      const uint64_t b32 = std::min<uint64_t>(want, free_b / 4);
+      std::vector<uint32_t> by_df;
+      for (uint32_t t = 0; t < V; ++t)
+        if (!fg::meta_slot(ix->tmeta[t]) && (ix->off[t + 1] - ix->off[t]) * fg::kDenseDiv >= N) by_df.push_back(t);
+      std::stable_sort(by_df.begin(), by_df.end(), [&](uint32_t a, uint32_t b) {
+        return ix->off[a + 1] - ix->off[a] > ix->off[b + 1] - ix->off[b];
+      });
+      for (uint32_t t : by_df) {
+        if ((f32_terms.size() + 1) * N * 4ull > b32 || f32_terms.size() >= fg::kMaxDense) break;
+        f32_terms.push_back(t);
+      }
+      while (!f32_terms.empty()) {
+        void* q = nullptr;
+        if (hipMalloc(&q, N * 4ull * f32_terms.size()) == hipSuccess) {
+          ix->mem.ptrs.push_back(q);
+          bytes += N * 4ull * f32_terms.size();
+          d_dense = static_cast<float*>(q);
+          break;
+        }
+        (void)hipGetLastError();
+        f32_terms.resize(f32_terms.size() / 2);
+      }
+    }
+  }
+  std::vector<uint32_t> tmeta = ix->tmeta;
+  if (!f32_terms.empty()) {
+    HIPCHK(hipMemsetD32(d_dense, (int)0xBF800000u, N * f32_terms.size()));  // -1.0f: absent
+    for (uint32_t s2 = 0; s2 < f32_terms.size(); ++s2) {
+      const uint32_t t = f32_terms[s2];
+      HIPCHK(fg::launch_dense(ix->d.doc, d_psc, ix->off[t], (uint32_t)(ix->off[t + 1] - ix->off[t]),
+                              d_dense + (size_t)s2 * N, nullptr));
+      tmeta[t] |= (s2 + 1) << 16;  // f32 kind (bit 31 clear)
+    }
+    HIPCHK(hipStreamSynchronize(nullptr));
+    uint32_t* d_tm;
+    if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tm, &bytes))) return rc;
+    ix->d.tmeta = d_tm;
+    ix->tmeta = tmeta;
+  }
+  ix->n_dense = (uint32_t)f32_terms.size();
+  ix->d.psc = d_psc;
+  ix->d.bmax = d_bmax;
+  ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
+  ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
+  ix->d.alive = d_alive;
+  ix->d.dense = d_dense;
+  ix->device_bytes = ix->struct_bytes + bytes;
+  return FG_OK;
+}
+
+// The statistics-independent half of a snapshot (postings, tf, fieldnorm ids,
+// bucket directory, rank words, facet postings, chunk tables) is uploaded into
+// ix->smem, then score_index computes the rest.  Consumes hp.  g: global
+// statistics of a doc-sharded namespace (NULL: the shard's own).
 int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, const fg_global_stats* g = nullptr) {
   auto ix = std::make_unique<fg_index>();
   ix->dev = dev;
   ix->mem.dev = dev;
   ix->pool.dev = dev;
+  ix->smem = std::make_shared<DevAllocs>();
+  ix->smem->dev = dev;
   ix->n_docs = hp.n_docs;
   ix->n_terms = hp.n_terms;
   ix->has_name = hp.has_name;
   ix->n_postings = hp.off[hp.n_terms];
-  ix->tot[0] = g ? g->tot_tokens[0] : hp.tot[0];
-  ix->tot[1] = g ? g->tot_tokens[1] : hp.tot[1];
-  const uint64_t N = hp.n_docs;           // docs of this shard (array sizes)
-  const uint64_t Ns = g ? g->n_docs : N;  // N of the statistics
-  ix->n_stats = Ns;
-  for (int f = 0; f < 2; ++f) {
-    ix->avgdl[f] = (float)ix->tot[f] / (float)Ns;  // total_num_tokens as f32 / N as f32
-    bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
-  }
+  ix->tot_local[0] = hp.tot[0];
+  ix->tot_local[1] = hp.tot[1];
+  const uint64_t N = hp.n_docs;  // docs of this shard (array sizes)
   const uint32_t V = hp.n_terms;
-  ix->w_text.resize(V);
-  ix->w_name.resize(V);
-  for (uint32_t t = 0; t < V; ++t) {
-    ix->w_text[t] = bm25_weight(g ? g->df_text[t] : hp.df_text[t], Ns);
-    ix->w_name[t] = bm25_weight(g ? (g->df_name ? g->df_name[t] : 0u) : hp.df_name[t], Ns);
-  }
-  g_bt.mark("weights");
+  if (g && g->df_name == nullptr && hp.has_name) return fail(FG_EINVAL, "global statistics lack df_name for a shard with names");
   // doc -> position bucket directory (fg_internal.h DevIndex): bucket width
   // 2^B_t docs with B_t the largest shift keeping ~kBucketTarget postings per bucket
   std::vector<uint32_t> dir_off(V), tmeta(V);
@@ -371,64 +535,27 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     nd += nbk + 1;
   }
   std::vector<uint32_t> dir(nd);
-  // bucket score maxima (parallel to dir): the per-bucket upper bound the
-  // disjunctive kernel prunes with (block-max WAND / MaxScore bounds)
-  std::vector<float> bmax(nd, 0.0f);
-  // every posting's term score (DevIndex::psc) and each term's largest one
-  std::vector<float> psc;
-  try {
-    psc.resize(hp.doc.size());
-  } catch (...) {
-    return fail(FG_EOOM, "posting scores allocation failed");
-  }
-  std::vector<float> tmaxs(V, 0.0f);
-  // per-term K-th best score over alive docs for K in kTopKs: a doc among a
-  // term's top K scores at least that much in any disjunction containing the
-  // term, so the query's K-th best is >= it (k_disj's starting threshold)
-  ix->ktop.assign((size_t)V * fg::kNumTopK, 0.0f);
-  const bool has_name = hp.has_name;
   parallel_dynamic(V, hw_threads(0), 1, [&](int, uint32_t tb, uint32_t te) {
-    std::vector<float> sc;
     for (uint32_t t = tb; t < te; ++t) {
       const uint64_t b0 = hp.off[t], n = hp.off[t + 1] - b0;
       const uint32_t B = tmeta[t];
       const uint64_t nbk = ((N - 1) >> B) + 1;
       uint32_t* dt = dir.data() + dir_off[t];
-      float* bm = bmax.data() + dir_off[t];
-      const float wt = ix->w_text[t], wn = ix->w_name[t];
       uint64_t p = 0;
       uint32_t maxocc = 0;
       for (uint64_t b = 0; b <= nbk; ++b) {
         const uint64_t lo = b << B;
-        float mx = 0.0f;
-        while (p < n && hp.doc[b0 + p] < lo) {
-          const uint32_t d = hp.doc[b0 + p], tfp = hp.tf[b0 + p];
-          const float v = term_score_host(tfp, hp.fn_text[d], has_name ? hp.fn_name[d] : 0, wt, wn, ix->cache);
-          psc[b0 + p] = v;
-          mx = std::max(mx, v);
-          tmaxs[t] = std::max(tmaxs[t], v);
-          if (hp.alive.empty() || ((hp.alive[d >> 5] >> (d & 31)) & 1u)) sc.push_back(v);
-          ++p;
-        }
+        const uint64_t p0 = p;
+        while (p < n && hp.doc[b0 + p] < lo) ++p;
         dt[b] = (uint32_t)p;
-        if (b) {
-          maxocc = std::max<uint32_t>(maxocc, dt[b] - dt[b - 1]);
-          bm[b - 1] = dt[b] > dt[b - 1] ? mx : -0.0f;  // -0.0: empty bucket (a score may be +0.0)
-        }
+        if (b) maxocc = std::max<uint32_t>(maxocc, (uint32_t)(p - p0));
       }
       uint32_t S = 0;
       while ((1ull << S) <= maxocc) ++S;  // 2^S > largest bucket
       tmeta[t] = B | (S << 8);
-      for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
-        const uint32_t K = fg::kTopKs[j];
-        if (sc.size() < K) break;
-        std::nth_element(sc.begin(), sc.begin() + (K - 1), sc.end(), std::greater<float>());
-        ix->ktop[(size_t)t * fg::kNumTopK + j] = sc[K - 1];
-      }
-      sc.clear();
     }
   });
-  g_bt.mark("dir + scores + ktop");
+  g_bt.mark("directory");
   // per-term tile maxima (4096-doc tiles of k_disj) for terms whose buckets are
   // no wider than a tile: one load gives a clause's bound over a tile
   std::vector<uint32_t> toff(V, 0xFFFFFFFFu);
@@ -440,140 +567,81 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       toff[t] = (uint32_t)ntm;
       ntm += n_tiles;
     }
-  std::vector<float> tmax(ntm, 0.0f);
-  parallel_dynamic(V, hw_threads(0), 256, [&](int, uint32_t tb, uint32_t te) {
-    for (uint32_t t = tb; t < te; ++t) {
-      if (toff[t] == 0xFFFFFFFFu) continue;
-      const uint32_t B = tmeta[t] & 0xFFu;
-      const uint64_t nbk = ((N - 1) >> B) + 1;
-      const float* bm = bmax.data() + dir_off[t];
-      float* tm = tmax.data() + toff[t];
-      for (uint64_t b = 0; b < nbk; ++b) {
-        const uint64_t tile = (b << B) >> fg::kDisjTileShift;
-        tm[tile] = std::max(tm[tile], bm[b]);
-      }
-    }
-  });
-  g_bt.mark("tile maxima");
-  // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
-  // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
-  const uint32_t VF = hp.n_fterms;
-  ix->n_fterms = VF;
-  ix->tot_f = g ? g->tot_facet_tokens : hp.tot_f;
-  if (g && VF) {
-    if (!g->df_facet) return fail(FG_EINVAL, "global statistics lack df_facet for a faceted shard");
-    ix->df_facet.assign(g->df_facet, g->df_facet + VF);
-    for (uint32_t t = 0; t < VF; ++t)
-      if (ix->df_facet[t] < hp.df_facet[t]) return fail(FG_EINVAL, "global facet df of term %u is below this shard's", t);
-  } else {
-    ix->df_facet = hp.df_facet;
+  ix->dir_entries = nd;
+  ix->tile_entries = ntm;
+  // chunk tables of the scoring kernels: (term, first posting) per <= kScoreChunk
+  // postings, (term, first bucket) per <= kBucketChunk buckets, terms with postings
+  std::vector<uint32_t> sc_t, sc_f, bk_t, bk_f, kt;
+  for (uint32_t t = 0; t < V; ++t) {
+    const uint64_t n = hp.off[t + 1] - hp.off[t];
+    if (!n) continue;
+    for (uint64_t f = 0; f < n; f += fg::kScoreChunk) { sc_t.push_back(t); sc_f.push_back((uint32_t)f); }
+    const uint64_t nbk = ((N - 1) >> (tmeta[t] & 0xFFu)) + 1;
+    for (uint64_t f = 0; f < nbk; f += fg::kBucketChunk) { bk_t.push_back(t); bk_f.push_back((uint32_t)f); }
+    kt.push_back(t);
   }
-  ix->fscore.assign(VF, 0.0f);
-  if (ix->tot_f > 0) {
-    float cf[256];
-    ix->avgdl_f = (float)ix->tot_f / (float)Ns;
-    bm25_cache(ix->avgdl_f, cf);
-    ix->cache_f1 = cf[1];
-    for (uint32_t t = 0; t < VF; ++t)
-      ix->fscore[t] = bm25_weight(ix->df_facet[t], Ns) * (1.0f / (1.0f + ix->cache_f1));
-  }
-  ix->ffirst.assign(VF, 0);
-  ix->flast.assign(VF, 0);
-  for (uint32_t t = 0; t < VF; ++t)
-    if (hp.foff[t + 1] > hp.foff[t]) {
-      ix->ffirst[t] = hp.fdoc[hp.foff[t]];
-      ix->flast[t] = hp.fdoc[hp.foff[t + 1] - 1];
-    }
+  if (sc_t.size() > 0x7FFFFFFFull || bk_t.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "index too large");
   HIPCHK(hipSetDevice(dev));
-  uint64_t bytes = 0;
+  DevAllocs& sm = *ix->smem;
+  uint64_t& bytes = ix->struct_bytes;
   int rc;
-  uint32_t *d_doc, *d_dir, *d_dir_off, *d_tmeta, *d_alive = nullptr, *d_toff;
-  uint64_t* d_off;
-  float *d_psc, *d_tmaxs, *d_bmax, *d_tmax;
-  g_bt.mark("facet weights");
-  if ((rc = dev_upload(ix->mem, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, psc.data(), psc.size(), &d_psc, &bytes))) return rc;
-  std::vector<float>().swap(psc);
+  uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_fdoc;
+  uint8_t *d_fnt, *d_fnn = nullptr;
+  uint64_t *d_off, *d_foff;
+  uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt;
+  if ((rc = dev_upload(sm, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
+  if ((rc = dev_upload(sm, hp.tf.data(), hp.tf.size(), &d_tfp, &bytes))) return rc;
   std::vector<uint32_t>().swap(hp.tf);
-  if ((rc = dev_upload(ix->mem, tmaxs.data(), tmaxs.size(), &d_tmaxs, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, hp.off.data(), hp.off.size(), &d_off, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, dir.data(), dir.size(), &d_dir, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, bmax.data(), bmax.size(), &d_bmax, &bytes))) return rc;
-  std::vector<float>().swap(bmax);
-  if ((rc = dev_upload(ix->mem, tmax.data(), tmax.size(), &d_tmax, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, toff.data(), toff.size(), &d_toff, &bytes))) return rc;
-  std::vector<float>().swap(tmax);
-  if ((rc = dev_upload(ix->mem, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
+  if ((rc = dev_upload(sm, hp.fn_text.data(), hp.fn_text.size(), &d_fnt, &bytes))) return rc;
+  if (hp.has_name && (rc = dev_upload(sm, hp.fn_name.data(), hp.fn_name.size(), &d_fnn, &bytes))) return rc;
+  if ((rc = dev_upload(sm, hp.off.data(), hp.off.size(), &d_off, &bytes))) return rc;
+  if ((rc = dev_upload(sm, dir.data(), dir.size(), &d_dir, &bytes))) return rc;
+  std::vector<uint32_t>().swap(dir);
+  if ((rc = dev_upload(sm, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
+  if ((rc = dev_upload(sm, toff.data(), toff.size(), &d_toff, &bytes))) return rc;
+  if ((rc = dev_upload(sm, hp.fdoc.data(), hp.fdoc.size(), &d_fdoc, &bytes))) return rc;
+  if ((rc = dev_upload(sm, hp.foff.data(), hp.foff.size(), &d_foff, &bytes))) return rc;
+  if ((rc = dev_upload(sm, sc_t.data(), sc_t.size(), &d_sct, &bytes))) return rc;
+  if ((rc = dev_upload(sm, sc_f.data(), sc_f.size(), &d_scf, &bytes))) return rc;
+  if ((rc = dev_upload(sm, bk_t.data(), bk_t.size(), &d_bkt, &bytes))) return rc;
+  if ((rc = dev_upload(sm, bk_f.data(), bk_f.size(), &d_bkf, &bytes))) return rc;
+  if ((rc = dev_upload(sm, kt.data(), kt.size(), &d_kt, &bytes))) return rc;
   g_bt.mark("upload");
-  // dense structures for the densest terms (fg_internal.h DevIndex), chosen
-  // AFTER the uploads above so the budgets see the memory actually left: f32
-  // score tables (df >= N / kDenseDiv, FUGU_DENSE_GIB) for the densest, then
-  // rank words (df >= N / kRankDiv, FUGU_RANK_GIB) for the next ones, densest
-  // first (ties by term id), each within its budget and a quarter of the free
-  // memory.  An allocation that fails is retried with half the terms (down to
-  // none), so a snapshot build never fails for want of optional structures.
-  // Both hold the union score psc[] (text + name), so name terms qualify too.
+  // rank words for the densest terms (fg_internal.h DevIndex), chosen AFTER the
+  // uploads above so the budget sees the memory actually left: df >= N /
+  // kRankDiv, densest first (ties by term id), within FUGU_RANK_GIB and a
+  // quarter of the free memory; a failed allocation is retried with half the
+  // terms (down to none), so a build never fails for want of them.  They hang
+  // on doc ids only, so rescored snapshots share them.
   std::vector<uint32_t> by_df;
   for (uint32_t t = 0; t < V; ++t)
-    if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * std::max(fg::kDenseDiv, fg::kRankDiv) >= N)
-      by_df.push_back(t);
+    if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * fg::kRankDiv >= N) by_df.push_back(t);
   std::stable_sort(by_df.begin(), by_df.end(), [&](uint32_t a, uint32_t b) {
     return hp.off[a + 1] - hp.off[a] > hp.off[b + 1] - hp.off[b];
   });
   const uint32_t rank_words = (uint32_t)((N + 31) / 32);
-  std::vector<uint32_t> f32_terms, rank_terms;
-  float* d_dense = nullptr;
+  std::vector<uint32_t> rank_terms;
   uint64_t* d_rank = nullptr;
-  auto env_gib = [](const char* name, uint64_t dflt) {
-    const char* v = getenv(name);
-    return v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : dflt;
-  };
-  // per_term bytes for each of terms, halving the term list while hipMalloc fails
-  auto alloc_slots = [&](std::vector<uint32_t>& terms, size_t per_term, void** out_p) -> int {
-    while (!terms.empty()) {
-      void* p = nullptr;
-      if (hipMalloc(&p, per_term * terms.size()) == hipSuccess) {
-        ix->mem.ptrs.push_back(p);
-        bytes += per_term * terms.size();
-        *out_p = p;
-        return FG_OK;
-      }
-      (void)hipGetLastError();
-      terms.resize(terms.size() / 2);
-    }
-    return FG_OK;
-  };
   {
+    const char* v = getenv("FUGU_RANK_GIB");
+    const uint64_t want = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kRankBudget;
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t b32 = std::min<uint64_t>(env_gib("FUGU_DENSE_GIB", fg::kDenseBudget), free_b / 4);
-    size_t i = 0;
-    for (; i < by_df.size() && f32_terms.size() < fg::kMaxDense; ++i) {
-      const uint32_t t = by_df[i];
-      if ((hp.off[t + 1] - hp.off[t]) * fg::kDenseDiv < N || (f32_terms.size() + 1) * N * 4ull > b32) break;
-      f32_terms.push_back(t);
-    }
-    void* p = nullptr;
-    if ((rc = alloc_slots(f32_terms, (size_t)N * 4, &p))) return rc;
-    d_dense = static_cast<float*>(p);
-    HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t brk = std::min<uint64_t>(env_gib("FUGU_RANK_GIB", fg::kRankBudget), free_b / 4);
-    for (i = f32_terms.size(); i < by_df.size() && rank_terms.size() < fg::kMaxDense; ++i) {
-      const uint32_t t = by_df[i];
-      if ((hp.off[t + 1] - hp.off[t]) * fg::kRankDiv < N || (rank_terms.size() + 1) * rank_words * 8ull > brk) break;
+    const uint64_t brk = std::min<uint64_t>(want, free_b / 4);
+    for (uint32_t t : by_df) {
+      if ((rank_terms.size() + 1) * rank_words * 8ull > brk || rank_terms.size() >= fg::kMaxDense) break;
       rank_terms.push_back(t);
     }
-    p = nullptr;
-    if ((rc = alloc_slots(rank_terms, (size_t)rank_words * 8, &p))) return rc;
-    d_rank = static_cast<uint64_t*>(p);
-  }
-  if (!f32_terms.empty()) {
-    HIPCHK(hipMemsetD32(d_dense, (int)0xBF800000u, (size_t)N * f32_terms.size()));  // -1.0f: absent
-    for (uint32_t s2 = 0; s2 < f32_terms.size(); ++s2) {
-      const uint32_t t = f32_terms[s2];
-      HIPCHK(fg::launch_dense(d_doc, d_psc, hp.off[t], (uint32_t)(hp.off[t + 1] - hp.off[t]),
-                              d_dense + (size_t)s2 * N, nullptr));
-      tmeta[t] |= (s2 + 1) << 16;
+    while (!rank_terms.empty()) {
+      void* q = nullptr;
+      if (hipMalloc(&q, rank_words * 8ull * rank_terms.size()) == hipSuccess) {
+        sm.ptrs.push_back(q);
+        bytes += rank_words * 8ull * rank_terms.size();
+        d_rank = static_cast<uint64_t*>(q);
+        break;
+      }
+      (void)hipGetLastError();
+      rank_terms.resize(rank_terms.size() / 2);
     }
   }
   if (!rank_terms.empty()) {
@@ -596,36 +664,69 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
   }
-  HIPCHK(hipStreamSynchronize(nullptr));
-  g_bt.mark("dense + rank words");
-  ix->n_dense = (uint32_t)f32_terms.size();
   ix->n_rank = (uint32_t)rank_terms.size();
-  if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
+  if ((rc = dev_upload(sm, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
   ix->tmeta = tmeta;
-  ix->tmaxs = std::move(tmaxs);
-  if (!hp.alive.empty() && (rc = dev_upload(ix->mem, hp.alive.data(), hp.alive.size(), &d_alive, &bytes))) return rc;
-  uint32_t* d_fdoc;
-  uint64_t* d_foff;
-  if ((rc = dev_upload(ix->mem, hp.fdoc.data(), hp.fdoc.size(), &d_fdoc, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, hp.foff.data(), hp.foff.size(), &d_foff, &bytes))) return rc;
-  ix->d = fg::DevIndex{d_doc,   d_psc,  d_off,  d_dir,  d_dir_off, d_tmeta,   d_dense,    d_rank,
-                       d_tmaxs, d_alive, d_bmax, d_tmax, d_toff, d_fdoc,    d_foff,     hp.n_docs,
-                       hp.n_terms, hp.has_name ? 1u : 0u, VF, rank_words};
-  ix->foff = std::move(hp.foff);
-  // per-term doc span (disjunctive plans skip the tiles outside it)
-  ix->first_doc.assign(V, 0);
-  ix->last_doc.assign(V, 0);
-  for (uint32_t t = 0; t < V; ++t)
-    if (hp.off[t + 1] > hp.off[t]) {
-      ix->first_doc[t] = hp.doc[hp.off[t]];
-      ix->last_doc[t] = hp.doc[hp.off[t + 1] - 1];
-    }
-  ix->dir_entries = nd;
-  ix->device_bytes = bytes;
+  g_bt.mark("rank words");
+  ix->d_tfp = d_tfp;
+  ix->d_fn_text = d_fnt;
+  ix->d_fn_name = d_fnn;
+  ix->d_sc_term = d_sct;
+  ix->d_sc_first = d_scf;
+  ix->d_bk_term = d_bkt;
+  ix->d_bk_first = d_bkf;
+  ix->d_kt_terms = d_kt;
+  ix->n_sc = (uint32_t)sc_t.size();
+  ix->n_bk = (uint32_t)bk_t.size();
+  ix->n_kt = (uint32_t)kt.size();
+  ix->d.doc = d_doc;
+  ix->d.off = d_off;
+  ix->d.dir = d_dir;
+  ix->d.dir_off = d_dir_off;
+  ix->d.tmeta = d_tmeta;
+  ix->d.rank = d_rank;
+  ix->d.toff = d_toff;
+  ix->d.fdoc = d_fdoc;
+  ix->d.foff = d_foff;
+  ix->d.n_docs = hp.n_docs;
+  ix->d.n_terms = hp.n_terms;
+  ix->d.has_name = hp.has_name ? 1u : 0u;
+  ix->d.n_fterms = hp.n_fterms;
+  ix->d.rank_words = rank_words;
+  // host bookkeeping of the structure
   ix->off = std::move(hp.off);
   ix->df_text = std::move(hp.df_text);
   ix->df_name = std::move(hp.df_name);
-  if (keep_host) ix->h_doc = std::move(hp.doc);
+  ix->first_doc.assign(V, 0);
+  ix->last_doc.assign(V, 0);
+  for (uint32_t t = 0; t < V; ++t)
+    if (ix->off[t + 1] > ix->off[t]) {
+      ix->first_doc[t] = hp.doc[ix->off[t]];
+      ix->last_doc[t] = hp.doc[ix->off[t + 1] - 1];
+    }
+  if (keep_host) ix->h_doc = std::make_shared<const std::vector<uint32_t>>(std::move(hp.doc));
+  const uint32_t VF = hp.n_fterms;
+  ix->n_fterms = VF;
+  ix->df_facet_local = hp.df_facet;
+  ix->tot_f_local = hp.tot_f;
+  ix->ffirst.assign(VF, 0);
+  ix->flast.assign(VF, 0);
+  for (uint32_t t = 0; t < VF; ++t)
+    if (hp.foff[t + 1] > hp.foff[t]) {
+      ix->ffirst[t] = hp.fdoc[hp.foff[t]];
+      ix->flast[t] = hp.fdoc[hp.foff[t + 1] - 1];
+    }
+  ix->foff = std::move(hp.foff);
+  // statistics: the shard's own, or the namespace's global ones
+  if (g && VF && !g->df_facet) return fail(FG_EINVAL, "global statistics lack df_facet for a faceted shard");
+  if (g && VF)
+    for (uint32_t t = 0; t < VF; ++t)
+      if (g->df_facet[t] < ix->df_facet_local[t]) return fail(FG_EINVAL, "global facet df of term %u is below this shard's", t);
+  const uint64_t tot_local[2] = {ix->tot_local[0], ix->tot_local[1]};
+  if ((rc = score_index(ix.get(), g ? g->n_docs : N, g ? g->tot_tokens : tot_local,
+                        g ? g->df_text : ix->df_text.data(), g ? g->df_name : ix->df_name.data(), hp.alive,
+                        g ? g->tot_facet_tokens : ix->tot_f_local, g && VF ? g->df_facet : ix->df_facet_local.data())))
+    return rc;
   g_bt.mark("tail");
   *out = ix.release();
   return FG_OK;
@@ -987,6 +1088,84 @@ int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** ou
     hp.tot_f = in->tot_facet_tokens;
   }
   return finish_index(dev, hp, true, out);
+}
+
+int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out) {
+  if (!base || !g || !out || !g->df_text) return fail(FG_EINVAL, "bad arguments");
+  const uint32_t N = base->n_docs, V = base->n_terms, VF = base->n_fterms;
+  if (g->n_docs < N || g->n_docs >= 0x7FFFFFFFull) return fail(FG_EINVAL, "bad global statistics");
+  if (base->has_name && !g->df_name) return fail(FG_EINVAL, "global statistics lack df_name for a snapshot with names");
+  if (VF && !g->df_facet) return fail(FG_EINVAL, "global statistics lack df_facet for a faceted snapshot");
+  for (uint32_t t = 0; t < V; ++t)
+    if (g->df_text[t] < base->df_text[t] || (g->df_name ? g->df_name[t] : 0u) < base->df_name[t])
+      return fail(FG_EINVAL, "global df of term %u is below this snapshot's", t);
+  for (uint32_t t = 0; t < VF; ++t)
+    if (g->df_facet[t] < base->df_facet_local[t]) return fail(FG_EINVAL, "global facet df of term %u is below this snapshot's", t);
+  g_bt.start();
+  auto ix = std::make_unique<fg_index>();
+  ix->dev = base->dev;
+  ix->mem.dev = base->dev;
+  ix->pool.dev = base->dev;
+  // the structure: shared device arrays, copied host bookkeeping
+  ix->smem = base->smem;
+  ix->struct_bytes = base->struct_bytes;
+  ix->n_docs = N;
+  ix->n_terms = V;
+  ix->has_name = base->has_name;
+  ix->n_postings = base->n_postings;
+  ix->dir_entries = base->dir_entries;
+  ix->tile_entries = base->tile_entries;
+  ix->n_rank = base->n_rank;
+  ix->off = base->off;
+  ix->df_text = base->df_text;
+  ix->df_name = base->df_name;
+  ix->first_doc = base->first_doc;
+  ix->last_doc = base->last_doc;
+  ix->h_doc = base->h_doc;
+  ix->tot_local[0] = base->tot_local[0];
+  ix->tot_local[1] = base->tot_local[1];
+  // f32 score tables belong to the scoring: drop base's slots of that kind
+  ix->tmeta = base->tmeta;
+  bool f32_slots = false;
+  for (auto& m : ix->tmeta)
+    if (fg::meta_slot(m) && !fg::meta_rank(m)) { m &= 0xFFFFu; f32_slots = true; }
+  ix->n_fterms = VF;
+  ix->tot_f_local = base->tot_f_local;
+  ix->foff = base->foff;
+  ix->df_facet_local = base->df_facet_local;
+  ix->ffirst = base->ffirst;
+  ix->flast = base->flast;
+  ix->d_tfp = base->d_tfp;
+  ix->d_fn_text = base->d_fn_text;
+  ix->d_fn_name = base->d_fn_name;
+  ix->d_sc_term = base->d_sc_term;
+  ix->d_sc_first = base->d_sc_first;
+  ix->d_bk_term = base->d_bk_term;
+  ix->d_bk_first = base->d_bk_first;
+  ix->d_kt_terms = base->d_kt_terms;
+  ix->n_sc = base->n_sc;
+  ix->n_bk = base->n_bk;
+  ix->n_kt = base->n_kt;
+  ix->d = base->d;
+  int rc;
+  if (f32_slots) {
+    HIPCHK(hipSetDevice(ix->dev));
+    uint32_t* d_tm;
+    uint64_t b = 0;
+    if ((rc = dev_upload(ix->mem, ix->tmeta.data(), ix->tmeta.size(), &d_tm, &b))) return rc;
+    ix->d.tmeta = d_tm;
+  }
+  std::vector<uint32_t> alive;
+  if (deleted) {
+    alive.assign((N + 31) / 32, 0);
+    for (uint32_t d = 0; d < N; ++d)
+      if (!deleted[d]) alive[d >> 5] |= 1u << (d & 31);
+  }
+  if ((rc = score_index(ix.get(), g->n_docs, g->tot_tokens, g->df_text, g->df_name, alive, g->tot_facet_tokens,
+                        VF ? g->df_facet : nullptr)))
+    return rc;
+  *out = ix.release();
+  return FG_OK;
 }
 
 int fg_index_retain(fg_index* ix) {
@@ -1454,7 +1633,7 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
 // ---------------------------------------------------------------- bytes model
 int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out) {
   if (!ix || !q || !out) return fail(FG_EINVAL, "bad arguments");
-  if (ix->h_doc.empty() && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
+  if (!ix->h_doc && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
   const double F = ix->has_name ? 2.0 : 1.0;
   std::vector<uint32_t> S;
   for (uint32_t i = 0; i < q->n_queries; ++i) {
@@ -1480,9 +1659,9 @@ int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, doub
     double bmerge = 0;
     for (auto& l : ls) bmerge += 8.0 * (double)l.n;
     double bskip = 8.0 * (double)ls[0].n;
-    S.assign(ix->h_doc.begin() + ls[0].off, ix->h_doc.begin() + ls[0].off + ls[0].n);
+    S.assign(ix->h_doc->begin() + ls[0].off, ix->h_doc->begin() + ls[0].off + ls[0].n);
     for (size_t t = 1; t < ls.size(); ++t) {
-      const uint32_t* d = ix->h_doc.data() + ls[t].off;
+      const uint32_t* d = ix->h_doc->data() + ls[t].off;
       const uint64_t n = ls[t].n;
       uint64_t blocks = 0, lb = 0;
       int64_t last_block = -1;
@@ -1513,7 +1692,7 @@ int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, doub
 // access sequence (kernels.hip k_conj) on the host copy of the postings.
 int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out) {
   if (!ix || !q || !out || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
-  if (ix->h_doc.empty() && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
+  if (!ix->h_doc && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
   const uint32_t nq = q->n_queries;
   std::atomic<bool> bad{false};
   parallel_ranges(nq, nq >= 64 ? hw_threads(0) : 1, [&](int, uint32_t qb, uint32_t qe) {
@@ -1549,11 +1728,11 @@ int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, 
       const uint32_t t0 = ts[0].term;
       const uint64_t df0 = ix->off[t0 + 1] - ix->off[t0];
       o[0] = 8.0 * (double)df0;  // lead doc id + posting score
-      cand.assign(ix->h_doc.begin() + ix->off[t0], ix->h_doc.begin() + ix->off[t0 + 1]);
+      cand.assign(ix->h_doc->begin() + ix->off[t0], ix->h_doc->begin() + ix->off[t0 + 1]);
       double probe = 0.0;
       for (uint32_t j = 1; j < m && !cand.empty(); ++j) {
         const uint32_t t = ts[j].term, meta = ix->tmeta[t];
-        const uint32_t* d = ix->h_doc.data() + ix->off[t];
+        const uint32_t* d = ix->h_doc->data() + ix->off[t];
         const uint64_t n = ix->off[t + 1] - ix->off[t];
         next.clear();
         if (fg::meta_slot(meta)) {

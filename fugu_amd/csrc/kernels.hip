@@ -548,6 +548,7 @@ constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
 constexpr uint32_t kPairs = 1024;              // (candidate, clause) rescoring pairs per pass
 constexpr uint32_t kMaxTiles = kDisjMaxGroup;  // tiles per work item
 constexpr uint32_t kMaxSeg = kMaxTiles * kMaxTerms;
+static_assert(kMaxSeg <= 2 * kThreads, "k_disj segment list: two (tile, clause) pairs per thread");
 
 struct DisjShared {
   alignas(16) uint64_t buf[kBufD];
@@ -797,24 +798,36 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
   }
   FG_PHASE(2);
 
-  // ---- P: posting-driven tiles: flat list of the essential clauses' segments
-  if (tid == 0) {
-    uint32_t ns = 0, np = 0;
-    for (uint32_t t = 0; t < ntile; ++t) {
-      if (sh.t_mode[t] != 2u) continue;
-      const uint32_t ess = sh.t_ess[t];
-      for (uint32_t i = 0; i < m; ++i) {
-        if (!((ess >> i) & 1u)) continue;
-        const uint32_t n = sh.r_hi[t * m + i] - sh.r_lo[t * m + i];
-        if (!n) continue;
-        sh.u.p.seg_start[ns] = np;
-        sh.seg_info[ns] = (uint16_t)((t << 4) | i);
-        ++ns;
-        np += n;
+  // ---- P: posting-driven tiles: flat list of the essential clauses' segments,
+  // (tile, clause) pairs in order, compacted by two workgroup prefix sums
+  {
+    uint32_t len[2], cnt = 0, tot = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {
+      const uint32_t p = 2 * tid + r;
+      len[r] = 0;
+      if (p < npair) {
+        const uint32_t t = p / m, i = p - t * m;
+        if (sh.t_mode[t] == 2u && ((sh.t_ess[t] >> i) & 1u)) len[r] = sh.r_hi[p] - sh.r_lo[p];
       }
+      cnt += len[r] ? 1u : 0u;
+      tot += len[r];
     }
-    sh.n_seg = ns;
-    sh.n_post = np;
+    uint32_t sb = block_exclusive_scan(cnt, sh.scratch);
+    uint32_t pb = block_exclusive_scan(tot, sh.scratch);
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {
+      if (!len[r]) continue;
+      const uint32_t p = 2 * tid + r, t = p / m, i = p - t * m;
+      sh.u.p.seg_start[sb] = pb;
+      sh.seg_info[sb] = (uint16_t)((t << 4) | i);
+      ++sb;
+      pb += len[r];
+    }
+    if (tid == kThreads - 1) {
+      sh.n_seg = sb;
+      sh.n_post = pb;
+    }
   }
   __syncthreads();
   const uint32_t n_seg = sh.n_seg, n_post = sh.n_post;
@@ -823,13 +836,21 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     const uint64_t thr = sh.thr;
     if (tid == 0) sh.n_cand = 0;
     __syncthreads();
+    // the J postings of a thread go through every step in lockstep, so their
+    // loads (the posting, then each clause's rank word and score) overlap
+    constexpr uint32_t J = kRound / kThreads;
+    uint32_t pd[J], pt[J], pcl[J], ess[J];
+    float ps[J];
+    bool pk[J];
 #pragma unroll
-    for (uint32_t j = 0; j < kRound / kThreads; ++j) {
+    for (uint32_t j = 0; j < J; ++j) {
       const uint32_t e = e0 + j * kThreads + tid;
-      bool keep = e < n_post;
-      uint64_t cv = 0;
-      float csrc = 0.0f;
-      if (keep) {
+      pk[j] = e < n_post;
+      pd[j] = 0;
+      pt[j] = 0;
+      pcl[j] = 0;
+      ps[j] = 0.0f;
+      if (pk[j]) {
         // segment of posting e: last seg_start <= e
         uint32_t lo = 0, hi = n_seg;
         while (hi - lo > 1) {
@@ -837,36 +858,96 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
           if (sh.u.p.seg_start[mid] <= e) lo = mid; else hi = mid;
         }
         const uint32_t info = sh.seg_info[lo];
-        const uint32_t t = info >> 4, c = info & 15u;
-        const uint32_t pos = sh.r_lo[t * m + c] + (e - sh.u.p.seg_start[lo]);
-        const uint64_t bi = sh.c_base[c];
-        const uint32_t d = ix.doc[bi + pos];
-        const float sc = ix.psc[bi + pos];
-        // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
-        float ub = sc + fmax;
-        for (uint32_t i = 0; i < m; ++i)
-          if (i != c) ub += sh.r_ub[t * m + i];
-        keep = make_key(inflate_bound(ub), d) >= thr;
-        if (keep && fmask) keep = filter_bits(fmask, fshift, d) != 0;
-        uint32_t maybe = 0;  // clauses whose bucket at d holds postings (the rest cannot match d)
-        if (keep) {
-          // bound 2: the other clauses at d -- the exact score from a dense
-          // table (-1.0: absent), else the bucket maximum (-0.0: empty bucket)
-          float ub2 = sc + fmax;
-          for (uint32_t i = 0; i < m; ++i) {
-            if (i == c || signbit(sh.r_ub[t * m + i])) continue;
-            const uint32_t meta = sh.c_meta[i];
-            const float b = meta_slot(meta) ? dense_score(ix, meta, sh.c_base[i], d)
-                                            : ix.bmax[sh.c_dir[i] + (d >> (meta & 0xFFu))];
-            if (signbit(b)) continue;  // clause i cannot match d
-            ub2 += b;
-            maybe |= 1u << i;
-          }
-          keep = make_key(inflate_bound(ub2), d) >= thr && doc_alive(ix, d);
-        }
-        cv = ((uint64_t)d << 32) | (maybe << 16) | (t << 8) | c;
-        csrc = sc;
+        pt[j] = info >> 4;
+        pcl[j] = info & 15u;
+        const uint64_t at = sh.c_base[pcl[j]] + sh.r_lo[pt[j] * m + pcl[j]] + (e - sh.u.p.seg_start[lo]);
+        pd[j] = ix.doc[at];
+        ps[j] = ix.psc[at];
       }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < J; ++j) {
+      ess[j] = 0;
+      if (!pk[j]) continue;
+      // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
+      float ub = ps[j] + fmax;
+      for (uint32_t i = 0; i < m; ++i)
+        if (i != pcl[j]) ub += sh.r_ub[pt[j] * m + i];
+      pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
+      if (pk[j] && fmask) pk[j] = filter_bits(fmask, fshift, pd[j]) != 0;
+      ess[j] = sh.t_ess[pt[j]];
+    }
+    // bound 2: every clause at d in clause order -- the exact score from a dense
+    // structure (-1.0: absent), else the bucket maximum (-0.0: empty bucket).
+    // When every other clause is dense (or has no posting in the tile) the sum
+    // IS the doc's exact SumCombiner score (0.0 + s_i in clause order over the
+    // matching clauses): the doc is a hit right here and skips the rescoring.
+    float sum[J];
+    uint32_t maybe[J];  // clauses whose structure at d says they may match (the rest cannot)
+    bool exact[J];
+#pragma unroll
+    for (uint32_t j = 0; j < J; ++j) {
+      sum[j] = 0.0f;
+      maybe[j] = 0;
+      exact[j] = true;
+    }
+    for (uint32_t i = 0; i < m; ++i) {
+      const uint32_t meta = sh.c_meta[i];
+      const uint32_t slot = meta_slot(meta);
+      const bool rank = slot && meta_rank(meta);
+      bool need[J];
+      uint64_t x[J];
+      float v[J];
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        need[j] = pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i]);
+        x[j] = 0;
+        v[j] = -1.0f;
+        if (need[j]) {
+          if (rank) x[j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
+          else if (slot) v[j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
+          else v[j] = ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))];
+        }
+      }
+      if (rank) {
+        const float* __restrict__ sp = ix.psc + sh.c_base[i];
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+          const uint32_t bits = (uint32_t)x[j], bt = pd[j] & 31u;
+          if (need[j] && ((bits >> bt) & 1u))
+            v[j] = sp[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))];
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        if (!pk[j]) continue;
+        float b = ps[j];
+        if (i != pcl[j]) {
+          if (!need[j]) continue;
+          b = v[j];
+          exact[j] = exact[j] && slot != 0;
+          if (signbit(b)) continue;  // clause i cannot match d
+          maybe[j] |= 1u << i;
+        }
+        sum[j] += b;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < J; ++j) {
+      bool keep = false, direct = false;
+      uint64_t dkey = 0;
+      if (pk[j]) {
+        if (exact[j]) {
+          // unique keys: the doc is kept only from the first essential clause it matches
+          const uint32_t first = (uint32_t)__builtin_ctz((maybe[j] | (1u << pcl[j])) & ess[j]);
+          const float s2 = fmask ? sum[j] + ftab[filter_bits(fmask, fshift, pd[j])] : sum[j];
+          dkey = make_key(s2, pd[j]);
+          direct = first == pcl[j] && dkey >= thr && doc_alive(ix, pd[j]);
+        } else {
+          keep = make_key(inflate_bound(sum[j] + fmax), pd[j]) >= thr && doc_alive(ix, pd[j]);
+        }
+      }
+      wave_append(direct, dkey, sh.buf, &sh.n_buf, kBufD);
       const unsigned long long bal = __ballot(keep);
       if (bal) {
         const uint32_t nw = (uint32_t)__popcll(bal);
@@ -875,8 +956,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
         base = (uint32_t)__shfl((int)base, 0, 64);
         const uint32_t at = base + (uint32_t)__popcll(bal & ((1ull << lane_id()) - 1ull));
         if (keep) {
-          sh.u.p.cand[at] = cv;
-          sh.u.p.cand_s[at] = csrc;
+          sh.u.p.cand[at] = ((uint64_t)pd[j] << 32) | (maybe[j] << 16) | (pt[j] << 8) | pcl[j];
+          sh.u.p.cand_s[at] = ps[j];
         }
       }
     }
@@ -1324,6 +1405,143 @@ hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uin
   const uint32_t cps = (n_words + kRankChunkWords - 1) / kRankChunkWords;
   if ((uint64_t)cps * n_slots > 0x7FFFFFFFull) return hipErrorInvalidValue;
   k_rank<<<cps * n_slots, kThreads, 0, s>>>(doc, slot_base, slot_n, cps, n_words, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- snapshot scoring
+// Bm25Weight::score in tantivy's f32 operation order (query/bm25.rs:
+// weight * (tf / (tf + cache[fieldnorm_id]))) for each field of the union
+// Should(text:t, name:t), summed from 0.0 (SumCombiner).  -ffp-contract=off and
+// IEEE f32 division: bit-identical to the oracle's host arithmetic.
+__device__ inline float posting_score(uint32_t tfp, uint32_t fn_t, uint32_t fn_n, float wt, float wn,
+                                      const float* cache) {
+  float s = 0.0f;
+  const uint32_t tt = tfp & 0xFFFFu, tn = tfp >> 16;
+  if (tt) {
+    const float tf = (float)tt;
+    s += wt * (tf / (tf + cache[fn_t]));
+  }
+  if (tn) {
+    const float tf = (float)tn;
+    s += wn * (tf / (tf + cache[256 + fn_n]));
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
+  __shared__ float cache[512];
+  for (uint32_t i = threadIdx.x; i < 512; i += kThreads) cache[i] = j.cache[i];
+  __syncthreads();
+  const uint32_t t = j.ch_term[blockIdx.x], first = j.ch_first[blockIdx.x];
+  const uint64_t b = j.off[t];
+  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
+  const uint32_t end = min(n, first + kScoreChunk);
+  const float wt = j.w_text[t], wn = j.w_name[t];
+  for (uint32_t p = first + threadIdx.x; p < end; p += kThreads) {
+    const uint32_t d = j.doc[b + p];
+    j.psc[b + p] = posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache);
+  }
+}
+
+// Bucket maxima (-0.0: empty bucket, a score may be +0.0), the term maxima and
+// the 4096-doc tile maxima (terms whose buckets are no wider than a tile).
+// Scores are >= 0, so their f32 bits order like the values (atomicMax on u32).
+__global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs) {
+  const uint32_t t = j.ch_term[blockIdx.x], first = j.ch_first[blockIdx.x];
+  const uint32_t meta = j.tmeta[t], B = meta & 0xFFu;
+  const uint32_t nbk = (uint32_t)(((uint64_t)(n_docs - 1) >> B) + 1);
+  const uint32_t end = min(nbk, first + kBucketChunk);
+  const uint32_t* dir = j.dir + j.dir_off[t];
+  const float* ps = j.psc + j.off[t];
+  const uint32_t to = j.toff[t];
+  uint32_t tm = 0;
+  for (uint32_t bk = first + threadIdx.x; bk < end; bk += kThreads) {
+    const uint32_t lo = dir[bk], hi = dir[bk + 1];
+    float mx = -0.0f;
+    if (hi > lo) {
+      mx = 0.0f;
+      for (uint32_t p = lo; p < hi; ++p) mx = fmaxf(mx, ps[p]);
+      const uint32_t bits = __float_as_uint(mx);
+      tm = max(tm, bits);
+      if (to != 0xFFFFFFFFu) atomicMax(&j.tmax[to + (uint32_t)(((uint64_t)bk << B) >> kDisjTileShift)], bits);
+    }
+    j.bmax[j.dir_off[t] + bk] = mx;
+  }
+  // one atomic per wave for the term maximum
+  for (int o = 32; o > 0; o >>= 1) tm = max(tm, (uint32_t)__shfl_xor((int)tm, o, 64));
+  if ((threadIdx.x & 63) == 0 && tm) atomicMax(&j.tmaxs[t], tm);
+}
+
+// Per term the K-th best score over its ALIVE postings for K in kTopKs (0 when
+// fewer): a doc among a term's top K scores at least that much in any
+// disjunction containing the term, so the query's K-th best is >= it (k_disj's
+// starting threshold).  One workgroup per term with postings; exact select
+// over unique (score, doc) keys.
+__global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
+  __shared__ uint32_t hist[kHistBins];
+  __shared__ uint32_t scratch[8];
+  __shared__ uint32_t red[2];  // alive postings, smallest alive score (bits)
+  const uint32_t t = j.kt_terms[blockIdx.x];
+  const uint64_t b = j.off[t];
+  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
+  auto alive = [&](uint32_t d) { return !j.alive || ((j.alive[d >> 5] >> (d & 31u)) & 1u); };
+  if (threadIdx.x == 0) {
+    red[0] = 0;
+    red[1] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  uint32_t c = 0, mx = 0, mn = 0xFFFFFFFFu;
+  for (uint32_t p = threadIdx.x; p < n; p += kThreads) {
+    if (!alive(j.doc[b + p])) continue;
+    const uint32_t bits = __float_as_uint(j.psc[b + p]);
+    ++c;
+    mx = max(mx, bits);
+    mn = min(mn, bits);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += (uint32_t)__shfl_xor((int)c, o, 64);
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&red[0], c);
+    atomicMin(&red[1], mn);
+    if (c) atomicMax(reinterpret_cast<uint32_t*>(&j.ktop[(size_t)t * kNumTopK]), mx);  // K = 1: the maximum
+  }
+  __syncthreads();
+  const uint32_t na = red[0];
+  for (uint32_t kk = 1; kk < kNumTopK; ++kk) {
+    const uint32_t K = kTopKs[kk];
+    if (na < K) break;  // uniform
+    if (na == K) {      // every alive key is in: the minimum
+      if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = __uint_as_float(red[1]);
+      continue;
+    }
+    const uint64_t T = select_kth(K, hist, scratch, [&](auto&& f) {
+      for (uint32_t p = threadIdx.x; p < n; p += kThreads) {
+        const uint32_t d = j.doc[b + p];
+        if (alive(d)) f(make_key(j.psc[b + p], d));
+      }
+    });
+    if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = key_score(T);
+  }
+}
+
+hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s) {
+  if (!n_chunks) return hipSuccess;
+  k_score<<<n_chunks, kThreads, 0, s>>>(j);
+  return hipGetLastError();
+}
+
+hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s) {
+  if (!n_chunks) return hipSuccess;
+  k_bucket<<<n_chunks, kThreads, 0, s>>>(j, n_docs);
+  return hipGetLastError();
+}
+
+hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, hipStream_t s) {
+  if (!n_terms) return hipSuccess;
+  k_ktop<<<n_terms, kThreads, 0, s>>>(j);
   return hipGetLastError();
 }
 

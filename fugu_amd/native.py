@@ -48,7 +48,7 @@ EXPORTS = (
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
-    "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats",
+    "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -121,6 +121,7 @@ _sig("fg_docs_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u32p, _u64p)
 _sig("fg_docs_facet_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u64p)
 _sig("fg_index_build_from_docs_global", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(GlobalStats),
      C.POINTER(_p))
+_sig("fg_index_rescore", C.c_int, _p, C.POINTER(GlobalStats), _u8p, C.POINTER(_p))
 _sig("fg_index_retain", C.c_int, _p)
 _sig("fg_index_release", C.c_int, _p)
 _sig("fg_index_stats_get", C.c_int, _p, C.POINTER(IndexStats))
@@ -333,6 +334,18 @@ class Index:
         dev = ctx.devices[0] if device is None else device
         _check(_lib.fg_index_build(ctx.handle, dev, C.byref(inp), C.byref(h)))
         return cls(h)
+
+    def rescore(self, global_stats: "ShardStats", deleted=None) -> "Index":
+        """fg_index_rescore: this snapshot's structure scored with other statistics."""
+        g = global_stats
+        dft, dfn = _u32(g.df_text), _u32(g.df_name)
+        dff = None if g.df_facet is None else _u32(g.df_facet)
+        gs = GlobalStats(int(g.n_docs), (C.c_uint64 * 2)(*[int(x) for x in g.tot_tokens]), _ptr(dft, _u32p),
+                         _ptr(dfn, _u32p), _ptr(dff, _u32p), int(g.tot_facet_tokens))
+        dl = None if deleted is None else np.ascontiguousarray(deleted, np.uint8)
+        h = _p()
+        _check(_lib.fg_index_rescore(self._h, C.byref(gs), _ptr(dl, _u8p), C.byref(h)))
+        return Index(h)
 
     @property
     def handle(self):

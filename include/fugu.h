@@ -138,6 +138,17 @@ int fg_docs_facet_stats(const fg_docs_input* in, uint32_t* df_facet, uint64_t* t
 int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g,
                                     fg_index** out);
 
+/* A new snapshot of `base` scored with other statistics: after a commit added
+ * docs elsewhere in the namespace (a new segment) or deleted some.  tantivy's
+ * Bm25Weight reads the Searcher's statistics at query time, so every segment
+ * scores with the namespace's current N, df and token totals
+ * (core/searcher.rs Bm25StatisticsProvider; one segment per commit,
+ * src/db/document.rs:65).  The postings, directory and rank words stay shared
+ * with `base` (no host inversion, no upload); the posting scores, bounds and
+ * the alive bitset are recomputed on the device.  `deleted` [n_docs of base]
+ * or NULL (none).  g must cover base's own doc frequencies. */
+int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out);
+
 int fg_index_retain(fg_index* ix);
 int fg_index_release(fg_index* ix);
 

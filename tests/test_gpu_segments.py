@@ -1,0 +1,109 @@
+"""Snapshots scored on the device and rescored with new statistics
+(fg_index_rescore): tantivy's commit model, where a commit adds a segment
+(reference src/db/document.rs:65) and every segment is then scored with the
+namespace's new N / df / token totals (Bm25StatisticsProvider).  A rescored
+snapshot must answer exactly like a snapshot built from scratch with the same
+statistics; segments merged by (score desc, segment asc, doc asc) must answer
+like the single index.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from fugu_amd import native as nat
+    if nat.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    return nat
+
+
+@pytest.fixture(scope="module")
+def ctx(native):
+    return native.Context((0,))
+
+
+@pytest.fixture(scope="module")
+def parts():
+    from fugu_amd import synth
+    c = synth.corpus(1_000_000)
+    cut = 800_000
+    a = (c.off[:cut + 1].copy(), c.tok[:c.off[cut]])
+    b = (c.off[cut:] - c.off[cut], c.tok[c.off[cut]:])
+    return c, cut, a, b
+
+
+def same(x, y, what):
+    sx, dx, nx = x
+    sy, dy, ny = y
+    assert np.array_equal(nx, ny), what
+    for i in range(len(nx)):
+        m = int(nx[i])
+        assert np.array_equal(dx[i, :m], dy[i, :m]), (what, i)
+        assert np.array_equal(sx[i, :m].view(np.uint32), sy[i, :m].view(np.uint32)), (what, i)
+
+
+@pytest.mark.parametrize("with_deletes", [False, True])
+def test_rescore_equals_build_with_global_stats(native, ctx, parts, with_deletes):
+    from fugu_amd import synth
+    c, cut, (ao, at), (bo, bt) = parts
+    V = synth.VOCAB
+    g = native.docs_stats(ao, at, V, threads=16) + native.docs_stats(bo, bt, V, threads=16)
+    dl = None
+    if with_deletes:
+        dl = (np.arange(cut) % 7 == 3).astype(np.uint8)
+    local = native.Index.from_docs(ctx, ao, at, V, threads=16, deleted=dl)
+    fresh = native.Index.from_docs(ctx, ao, at, V, threads=16, deleted=dl, global_stats=g)
+    re = local.rescore(g, deleted=dl)
+    sl, sf, sr = local.stats(), fresh.stats(), re.stats()
+    assert sr.avgdl == sf.avgdl and sr.avgdl != sl.avgdl
+    for t in (0, 5, 99, 1000, 20000):
+        assert re.bm25(t)[:2] == fresh.bm25(t)[:2]
+    for (m0, m1, k, mode) in [(3, 3, 100, native.MODE_AND), (1, 5, 10, native.MODE_AND),
+                              (2, 5, 1000, native.MODE_OR), (2, 3, 1, native.MODE_OR)]:
+        q_off, terms = synth.queries(256, m0, m1, seed_q=77)
+        same(re.search_batch(q_off, terms, k, mode=mode), fresh.search_batch(q_off, terms, k, mode=mode),
+             (m0, m1, k, mode))
+
+
+def test_rescore_twice_and_segment_merge_equals_single_index(native, ctx, parts):
+    """Commit 1 builds segment A with A's statistics; commit 2 adds segment B and
+    rescores A with the statistics of A + B; the two segments merged on the
+    device give the single index's results (OR exactly, 2-term AND exactly)."""
+    import torch
+
+    from fugu_amd import synth
+    from fugu_amd.shard import merge_on_device
+    c, cut, (ao, at), (bo, bt) = parts
+    V = synth.VOCAB
+    seg_a = native.Index.from_docs(ctx, ao, at, V, threads=16)
+    g = native.docs_stats(ao, at, V, threads=16) + native.docs_stats(bo, bt, V, threads=16)
+    seg_a2 = seg_a.rescore(g)
+    seg_a3 = seg_a2.rescore(g)  # a rescored snapshot rescored again keeps the shared structure
+    seg_b = native.Index.from_docs(ctx, bo, bt, V, threads=16, global_stats=g)
+    single = native.Index.from_docs(ctx, c.off, c.tok, V, threads=16)
+    seg_a.close()
+    seg_a2.close()
+    dev = torch.device("cuda:0")
+    for (m0, m1, k, mode) in [(2, 5, 1000, native.MODE_OR), (2, 2, 100, native.MODE_AND)]:
+        q_off, terms = synth.queries(256, m0, m1, seed_q=91)
+        nq = len(q_off) - 1
+        res = [seg_a3.search_batch(q_off, terms, k, mode=mode), seg_b.search_batch(q_off, terms, k, mode=mode)]
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32) if a.dtype == np.uint32  # noqa: E731
+                                       else np.ascontiguousarray(a)).to(dev)
+        ms, md, msh, mn = merge_on_device(t(np.stack([r[0] for r in res]).reshape(2, -1)),
+                                          t(np.stack([r[1] for r in res]).reshape(2, -1)),
+                                          t(np.stack([r[2] for r in res])), nq, k)
+        torch.cuda.synchronize()
+        md = md.cpu().numpy().view(np.uint32).reshape(nq, k)
+        msh = msh.cpu().numpy().reshape(nq, k)
+        s1, d1, n1 = single.search_batch(q_off, terms, k, mode=mode)
+        assert np.array_equal(mn.cpu().numpy(), n1)
+        ms = ms.cpu().numpy().reshape(nq, k)
+        for i in range(nq):
+            m = int(n1[i])  # entries past the hit count are not written
+            gdoc = md[i, :m] + np.array([0, cut], np.uint32)[msh[i, :m]]
+            assert np.array_equal(gdoc, d1[i, :m]), (mode, i)
+            assert np.array_equal(ms[i, :m], s1[i, :m]), (mode, i)
