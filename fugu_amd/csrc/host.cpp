@@ -564,10 +564,21 @@ struct Doc {
   std::vector<uint32_t> facet_tok;   // FacetTokenizer tokens of all of them (facet dictionary ids)
 };
 
-struct Snapshot {
+// A committed view of a namespace: tantivy's segments, one per commit
+// (src/db/document.rs:65) until kMaxSegments, then merged into one (the merge
+// policy's job).  Every segment scores with the namespace-wide statistics.
+struct Segment {
   fg_index* ix = nullptr;
-  ~Snapshot() { if (ix) fg_index_release(ix); }
+  uint32_t base = 0, n = 0;  // global doc ids [base, base + n)
 };
+struct Snapshot {
+  std::vector<Segment> segs;
+  ~Snapshot() {
+    for (auto& s : segs)
+      if (s.ix) fg_index_release(s.ix);
+  }
+};
+constexpr size_t kMaxSegments = 8;
 
 struct Namespace {
   std::string name;
@@ -580,6 +591,11 @@ struct Namespace {
   std::shared_ptr<Snapshot> snap;                      // committed device snapshot
   std::shared_mutex snap_mu;
   size_t committed_docs = 0;
+  // BM25 statistics of the committed docs, deleted ones included (tantivy's
+  // Searcher counts them until a merge): N, token totals, doc frequencies.
+  // Updated with each commit's new docs only.
+  uint64_t st_tot[2] = {0, 0}, st_tot_f = 0;
+  std::vector<uint32_t> st_df_text, st_df_name, st_df_facet;
 };
 
 }  // namespace
@@ -706,22 +722,36 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
     }
   }
   if (!snap) return FG_OK;  // nothing committed yet: no hits
-  // terms added after the snapshot are unknown to it
-  fg_index_stats st;
-  fg_index_stats_get(snap->ix, &st);
-  for (auto& t : ids)
-    if (t != FG_TERM_MISSING && t >= st.n_terms) t = FG_TERM_MISSING;
-  for (auto& t : fids)
-    if (t != FG_TERM_MISSING && t >= st.n_facet_terms) t = FG_TERM_MISSING;
-  const uint32_t q_off[2] = {0, (uint32_t)ids.size()};
-  const uint32_t f_off[2] = {0, (uint32_t)fids.size()};
-  fg_query_batch qb{1, q_off, ids.data(), mode, fids.empty() ? nullptr : f_off, fids.data()};
+  // every segment answers the query (TopDocs::with_limit(offset + per_page) per
+  // segment), then merge_fruits: (score desc, segment asc, doc asc) = (score
+  // desc, global doc asc), since segments hold ascending doc-id ranges
+  struct H { float s; uint32_t seg, doc; };
+  std::vector<H> all;
   std::vector<float> sc(limit);
   std::vector<uint32_t> dc(limit);
-  uint32_t n = 0;
-  int rc = fg_search_batch(snap->ix, &qb, (uint32_t)limit, sc.data(), dc.data(), &n);
-  if (rc) return hfail(rc, fg_last_error());
-  for (uint64_t i = offset; i < n; ++i) hits.push_back(fg_hit{sc[i], dc[i]});  // skip(offset).take(per_page)
+  for (uint32_t si = 0; si < snap->segs.size(); ++si) {
+    const Segment& seg = snap->segs[si];
+    // terms interned after a segment was built are unknown to it
+    fg_index_stats st;
+    fg_index_stats_get(seg.ix, &st);
+    std::vector<uint32_t> sid = ids, sfid = fids;
+    for (auto& t : sid)
+      if (t != FG_TERM_MISSING && t >= st.n_terms) t = FG_TERM_MISSING;
+    for (auto& t : sfid)
+      if (t != FG_TERM_MISSING && t >= st.n_facet_terms) t = FG_TERM_MISSING;
+    const uint32_t q_off[2] = {0, (uint32_t)sid.size()};
+    const uint32_t f_off[2] = {0, (uint32_t)sfid.size()};
+    fg_query_batch qb{1, q_off, sid.data(), mode, sfid.empty() ? nullptr : f_off, sfid.data()};
+    uint32_t n = 0;
+    int rc = fg_search_batch(seg.ix, &qb, (uint32_t)limit, sc.data(), dc.data(), &n);
+    if (rc) return hfail(rc, fg_last_error());
+    for (uint32_t i = 0; i < n; ++i) all.push_back(H{sc[i], si, seg.base + dc[i]});
+  }
+  std::stable_sort(all.begin(), all.end(), [](const H& a, const H& b) {
+    return a.s != b.s ? a.s > b.s : a.doc < b.doc;
+  });
+  const uint64_t n = std::min<uint64_t>(all.size(), limit);
+  for (uint64_t i = offset; i < n; ++i) hits.push_back(fg_hit{all[i].s, all[i].doc});  // skip(offset).take(per_page)
   return FG_OK;
 }
 
@@ -1058,53 +1088,108 @@ int fg_db_upsert_record(fg_db* db, const char* nsname, const fg_object_record* r
 }
 
 int fg_db_commit(fg_db* db, const char* nsname) {
+  // IndexWriter::commit (src/db/document.rs:65): the docs upserted since the
+  // last commit become a new segment; the namespace statistics change, so the
+  // older segments are rescored on the device (fg_index_rescore: their postings
+  // stay where they are) and pick up the new deletions; past kMaxSegments all
+  // docs are rebuilt into one segment (the merge policy).  Readers keep the
+  // snapshot they hold (refcounted).
   if (!db) return hfail(FG_EINVAL, "bad arguments");
   auto ns = find_ns(db, nsname);
   if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
   if (!db->ctx) return hfail(FG_ENODEV, "fg_db created without a device context");
   std::lock_guard<std::mutex> c(ns->committer);
-  // gather under the writer lock, build the device snapshot outside it so
-  // searches (doc fetch) and upserts are not blocked by the upload
+  std::shared_ptr<Snapshot> cur;
+  {
+    std::shared_lock<std::shared_mutex> l(ns->snap_mu);
+    cur = ns->snap;
+  }
+  // gather under the writer lock, build outside it so searches (doc fetch) and
+  // upserts are not blocked by the device work
   std::unique_lock<std::mutex> w(ns->writer);
-  if (ns->docs.empty()) return FG_OK;
   const uint32_t N = (uint32_t)ns->docs.size();
+  const uint32_t old = (uint32_t)ns->committed_docs;
+  if (N == 0 || (N == old && cur)) return FG_OK;
+  const bool merge = !cur || cur->segs.size() + 1 > kMaxSegments;
+  const uint32_t from = merge ? 0 : old;  // docs of the segment to build
   const uint32_t n_terms = std::max<uint32_t>(1, (uint32_t)ns->dict.size());
   const uint32_t n_fterms = (uint32_t)ns->fdict.size();
-  std::vector<uint64_t> toff(N + 1, 0), noff(N + 1, 0), foff(N + 1, 0);
+  std::vector<uint64_t> toff(N - from + 1, 0), noff(N - from + 1, 0), foff(N - from + 1, 0);
   std::vector<uint32_t> ttok, ntok, ftok;
   std::vector<uint8_t> del(N, 0);
   bool any_name = false, any_del = false;
   for (uint32_t d = 0; d < N; ++d) {
     const Doc& doc = ns->docs[d];
+    del[d] = doc.deleted ? 1 : 0;
+    any_del |= doc.deleted;
+    if (d < from) continue;
     ttok.insert(ttok.end(), doc.text_tok.begin(), doc.text_tok.end());
     ntok.insert(ntok.end(), doc.name_tok.begin(), doc.name_tok.end());
     ftok.insert(ftok.end(), doc.facet_tok.begin(), doc.facet_tok.end());
-    toff[d + 1] = ttok.size();
-    noff[d + 1] = ntok.size();
-    foff[d + 1] = ftok.size();
+    toff[d - from + 1] = ttok.size();
+    noff[d - from + 1] = ntok.size();
+    foff[d - from + 1] = ftok.size();
     any_name |= !doc.name_tok.empty();
-    del[d] = doc.deleted ? 1 : 0;
-    any_del |= doc.deleted;
   }
+  for (uint32_t d = 0; d < from && !any_name; ++d) any_name |= !ns->docs[d].name_tok.empty();
   w.unlock();
+  // namespace statistics += the new docs [old, N) (distinct terms per doc per field)
+  ns->st_df_text.resize(n_terms, 0);
+  ns->st_df_name.resize(n_terms, 0);
+  ns->st_df_facet.resize(n_fterms, 0);
+  {
+    std::lock_guard<std::mutex> w2(ns->writer);
+    std::vector<uint32_t> sc;
+    auto distinct = [&](const std::vector<uint32_t>& v, std::vector<uint32_t>& df) {
+      sc = v;
+      std::sort(sc.begin(), sc.end());
+      sc.erase(std::unique(sc.begin(), sc.end()), sc.end());
+      for (uint32_t t : sc) df[t]++;
+    };
+    for (uint32_t d = old; d < N; ++d) {
+      const Doc& doc = ns->docs[d];
+      ns->st_tot[0] += doc.text_tok.size();
+      ns->st_tot[1] += doc.name_tok.size();
+      ns->st_tot_f += doc.facet_tok.size();
+      distinct(doc.text_tok, ns->st_df_text);
+      distinct(doc.name_tok, ns->st_df_name);
+      distinct(doc.facet_tok, ns->st_df_facet);
+    }
+  }
+  fg_global_stats g{};
+  g.n_docs = N;
+  g.tot_tokens[0] = ns->st_tot[0];
+  g.tot_tokens[1] = ns->st_tot[1];
+  g.df_text = ns->st_df_text.data();
+  g.df_name = ns->st_df_name.data();
+  g.df_facet = n_fterms ? ns->st_df_facet.data() : nullptr;
+  g.tot_facet_tokens = ns->st_tot_f;
   fg_docs_input in{};
-  in.n_docs = N;
+  in.n_docs = N - from;
   in.n_terms = n_terms;
   in.text_off = toff.data();
   in.text_tok = ttok.data();
   in.name_off = any_name ? noff.data() : nullptr;
   in.name_tok = any_name ? ntok.data() : nullptr;
-  in.deleted = any_del ? del.data() : nullptr;
+  in.deleted = any_del ? del.data() + from : nullptr;
   in.threads = 0;
   in.keep_host_postings = 0;
   in.n_facet_terms = n_fterms;
   in.facet_off = n_fterms ? foff.data() : nullptr;
   in.facet_tok = n_fterms ? ftok.data() : nullptr;
-  fg_index* ix = nullptr;
-  int rc = fg_index_build_from_docs(db->ctx, db->dev, &in, &ix);
-  if (rc) return hfail(rc, fg_last_error());
   auto snap = std::make_shared<Snapshot>();
-  snap->ix = ix;
+  if (!merge) {
+    for (const Segment& s0 : cur->segs) {
+      fg_index* re = nullptr;
+      int rc = fg_index_rescore(s0.ix, &g, any_del ? del.data() + s0.base : nullptr, &re);
+      if (rc) return hfail(rc, fg_last_error());
+      snap->segs.push_back(Segment{re, s0.base, s0.n});
+    }
+  }
+  fg_index* ix = nullptr;
+  int rc = fg_index_build_from_docs_global(db->ctx, db->dev, &in, &g, &ix);
+  if (rc) return hfail(rc, fg_last_error());
+  snap->segs.push_back(Segment{ix, from, N - from});
   {
     std::unique_lock<std::shared_mutex> l(ns->snap_mu);  // readers keep the old snapshot (refcount)
     ns->snap = snap;

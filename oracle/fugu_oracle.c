@@ -534,6 +534,59 @@ int or_search(const or_index* ix, const uint32_t* terms, uint32_t m, int mode, u
   return (int)topn_finish(&top, out_score, out_doc);
 }
 
+/* Postings of `p` with doc < d (lower bound). */
+static uint32_t post_lb(const Postings* p, uint32_t d) {
+  uint32_t lo = 0, hi = p->n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (p->doc[mid] < d) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+/*
+ * or_search over a multi-segment index: one segment per commit
+ * (src/db/document.rs:65), seg[0..nseg] = the segments' doc-id boundaries.
+ * Every segment runs its own scorer with the index-wide statistics
+ * (Bm25StatisticsProvider of the Searcher), and BooleanWeight orders the
+ * intersection's children by the SEGMENT's cost (its own doc_freq), so a
+ * conjunction of >= 3 terms sums its scores in each segment's own order.  One
+ * TopN collects all segments (merge_fruits of per-segment top-k gives the same
+ * top-k: a later segment's doc loses every tie by DocAddress).  Disjunctions
+ * and single terms do not depend on the segmentation.
+ */
+int or_search_seg(const or_index* ix, const uint32_t* terms, uint32_t m, int mode, uint32_t k, const uint32_t* seg,
+                  uint32_t nseg, float* out_score, uint32_t* out_doc) {
+  if (mode != 0 || m < 2 || nseg < 1) return or_search(ix, terms, m, mode, k, out_score, out_doc);
+  if (k < 1 || m > OR_MAX_TERMS) return -1;
+  UnionCur cur[OR_MAX_TERMS];
+  Child ch[OR_MAX_TERMS];
+  UnionCur* ds[OR_MAX_TERMS];
+  TopN top;
+  topn_init(&top, k);
+  float thr = -3.40282347e+38f;
+  for (uint32_t s = 0; s < nseg; ++s) {
+    const uint32_t lo = seg[s], hi = seg[s + 1];
+    if (lo >= hi) continue;
+    for (uint32_t i = 0; i < m; ++i) {
+      uc_init(&cur[i], ix, terms[i]);
+      uint64_t cost = 0;
+      for (int f = 0; f < 2; ++f) cost += post_lb(cur[i].f[f].p, hi) - post_lb(cur[i].f[f].p, lo);
+      ch[i].c = &cur[i]; ch[i].cost = cost; ch[i].qpos = i;
+      uc_seek(&cur[i], lo);
+    }
+    qsort(ch, m, sizeof(Child), child_cmp);
+    for (uint32_t i = 0; i < m; ++i) ds[i] = ch[i].c;
+    uint32_t d = go_to_first_doc(ds, m);
+    while (d < hi) {
+      float sc = isect_score(ds, m);
+      if (sc > thr) thr = collect(&top, ix, d, sc);
+      d = isect_advance(ds, m);
+    }
+  }
+  return (int)topn_finish(&top, out_score, out_doc);
+}
+
 /* ---------------------------------------------------------------- filtered search */
 /*
  * Dataset::search with facet filters (src/db/search.rs:129-150):

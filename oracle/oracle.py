@@ -55,6 +55,8 @@ _lib.or_search_ex.restype = C.c_int
 _lib.or_search_ex.argtypes = [_p, _p, C.c_uint32, C.c_int, _p, C.c_uint32, C.c_uint32, _p, _p]
 _lib.or_search_batch_ex.restype = C.c_double
 _lib.or_search_batch_ex.argtypes = [_p, _p, _p, _p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p, _p, _p, C.c_int]
+_lib.or_search_seg.restype = C.c_int
+_lib.or_search_seg.argtypes = [_p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, C.c_uint32, _p, _p]
 _lib.or_bytes_model.restype = C.c_int
 _lib.or_bytes_model.argtypes = [_p, _p, C.c_uint32, C.c_uint32, _p]
 
@@ -142,6 +144,18 @@ class OracleIndex:
             f = np.ascontiguousarray(fterms if fterms is not None else [], np.uint32)
             n = _lib.or_search_ex(self._h, t.ctypes.data, len(t), mode, f.ctypes.data, len(f), k,
                                   score.ctypes.data, doc.ctypes.data)
+        if n < 0:
+            raise ValueError("oracle rejected the query")
+        return score[:n].copy(), doc[:n].copy()
+
+    def search_segments(self, terms, k: int, seg_bounds, mode: int = AND):
+        """or_search_seg: the index as segments [seg_bounds[i], seg_bounds[i+1]) (one per commit)."""
+        t = np.ascontiguousarray(terms, np.uint32)
+        sb = np.ascontiguousarray(seg_bounds, np.uint32)
+        score = np.zeros(k, np.float32)
+        doc = np.zeros(k, np.uint32)
+        n = _lib.or_search_seg(self._h, t.ctypes.data, len(t), mode, k, sb.ctypes.data, len(sb) - 1,
+                               score.ctypes.data, doc.ctypes.data)
         if n < 0:
             raise ValueError("oracle rejected the query")
         return score[:n].copy(), doc[:n].copy()

@@ -554,3 +554,43 @@ def test_json_shapes_with_hits_and_canonical_metadata(db):
     assert all("text" in x for x in s["results"])
     g = json.loads(d.search_json(None, "alpha%20gamma", 5, 5, shape=db.SHAPE_GET_SEARCH_PATH))
     assert g["query"] == "alpha gamma" and (g["page"], g["per_page"]) == (0, 20) and g["results"][0]["id"] == "d2"
+
+
+@pytest.mark.gpu
+def test_db_incremental_commits_segments_vs_oracle(db):
+    """A commit per 200 upserts: each commit adds a segment and rescores the
+    older ones with the new statistics (fg_index_rescore); the ninth merges all
+    into one segment.  After every commit the paged AND / OR results equal the
+    oracle run over the same segments (per-segment intersection order,
+    namespace-wide statistics), bit for bit."""
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("inc")
+    recs = build_corpus(11, 2400)
+    bounds = [0]  # segment boundaries of the model (mirror of the host's merge policy)
+    rng = random.Random(5)
+    checked = 0
+    for c in range(0, len(recs), 200):
+        for rid, t, meta in recs[c:c + 200]:
+            d.upsert(db.ObjectRecord(rid, t, metadata=meta), "inc")
+        d.commit("inc")
+        n = c + 200
+        bounds = [0, n] if len(bounds) - 1 + 1 > 8 else bounds + [n]
+        ix, dic = oracle_of(recs[:n])
+        for _ in range(12):
+            m = rng.randint(1, 4)
+            ws = [rng.choice(WORDS) for _ in range(m)]
+            q = ws[0] if m == 1 else (" AND ".join(ws) if rng.random() < 0.6 else " ".join(ws))
+            mode = 1 if (m > 1 and " AND " not in q) else 0
+            page, per_page = rng.randint(0, 2), rng.choice([5, 10, 20])
+            got = d.search("inc", q, page, per_page)
+            terms = [dic.get(t, native.FG_TERM_MISSING) for t in (py_analyze(w)[0] for w in ws)]
+            s, dd = ix.search_segments(np.array(terms, np.uint32), (page + 1) * per_page, bounds, mode=mode)
+            want = hits_of(s, dd)[page * per_page:]
+            assert hits_of([g[0] for g in got], [g[1] for g in got]) == want, (n, q, bounds)
+            checked += len(want)
+        assert d.doc_count("inc")[0] == n
+    assert checked > 300
