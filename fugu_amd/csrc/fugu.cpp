@@ -1031,7 +1031,14 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
 }
 
 int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out) {
+  return fg_index_build_global(ctx, dev, in, nullptr, out);
+}
+
+int fg_index_build_global(fg_ctx* ctx, int dev, const fg_index_input* in, const fg_global_stats* g, fg_index** out) {
   if (!ctx || !in || !out || !in->term_off || !in->fn_text) return fail(FG_EINVAL, "bad arguments");
+  if (g && (!g->df_text || g->n_docs < in->n_docs || g->n_docs >= 0x7FFFFFFFull))
+    return fail(FG_EINVAL, "bad global statistics");
+  g_bt.start();
   if (in->n_docs == 0 || in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs out of range");
   if (in->term_off[0] != 0) return fail(FG_EINVAL, "term_off[0] must be 0");
   if (in->term_off[in->n_terms] > 0 && (!in->doc || (!in->tf_text && !in->tf_name)))
@@ -1087,7 +1094,11 @@ int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** ou
     }
     hp.tot_f = in->tot_facet_tokens;
   }
-  return finish_index(dev, hp, true, out);
+  if (g)
+    for (uint32_t t = 0; t < V; ++t)
+      if (g->df_text[t] < hp.df_text[t] || (g->df_name ? g->df_name[t] : 0u) < hp.df_name[t])
+        return fail(FG_EINVAL, "global df of term %u is below this segment's", t);
+  return finish_index(dev, hp, true, out, g);
 }
 
 int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out) {

@@ -48,7 +48,7 @@ EXPORTS = (
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
-    "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore",
+    "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -117,6 +117,7 @@ _sig("fg_last_error", C.c_char_p)
 _sig("fg_version", C.c_char_p)
 _sig("fg_index_build_from_docs", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(_p))
 _sig("fg_index_build", C.c_int, _p, C.c_int, C.POINTER(IndexInput), C.POINTER(_p))
+_sig("fg_index_build_global", C.c_int, _p, C.c_int, C.POINTER(IndexInput), C.POINTER(GlobalStats), C.POINTER(_p))
 _sig("fg_docs_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u32p, _u64p)
 _sig("fg_docs_facet_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u64p)
 _sig("fg_index_build_from_docs_global", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(GlobalStats),
@@ -263,6 +264,15 @@ class ShardStats:
                           self.tot_facet_tokens + o.tot_facet_tokens)
 
 
+def _global_stats(g: "ShardStats"):
+    """(GlobalStats struct, arrays it points into) of summed ShardStats."""
+    dft, dfn = _u32(g.df_text), _u32(g.df_name)
+    dff = None if g.df_facet is None else _u32(g.df_facet)
+    gs = GlobalStats(int(g.n_docs), (C.c_uint64 * 2)(*[int(x) for x in g.tot_tokens]), _ptr(dft, _u32p),
+                     _ptr(dfn, _u32p), _ptr(dff, _u32p), int(g.tot_facet_tokens))
+    return gs, (dft, dfn, dff)
+
+
 def docs_stats(text_off, text_tok, n_terms: int, name_off=None, name_tok=None, threads: int = 0,
                facets=None) -> ShardStats:
     """fg_docs_stats (+ fg_docs_facet_stats): a shard's local statistics (host only, no device)."""
@@ -311,7 +321,8 @@ class Index:
 
     @classmethod
     def from_postings(cls, ctx: Context, n_docs: int, term_off, doc, tf_text, tf_name, fn_text, fn_name,
-                      tot_tokens, deleted=None, facets=None, device: int | None = None):
+                      tot_tokens, deleted=None, facets=None, device: int | None = None,
+                      global_stats: "ShardStats | None" = None):
         """fg_index_build: postings already inverted by the host (the entry the Rust
         binding feeds from tantivy's segment readers).  `facets` =
         (facet_term_off, facet_doc, n_facet_terms, tot_facet_tokens) or None."""
@@ -332,7 +343,12 @@ class Index:
                          _ptr(fo, _u64p), _ptr(fd, _u32p), totf)
         h = _p()
         dev = ctx.devices[0] if device is None else device
-        _check(_lib.fg_index_build(ctx.handle, dev, C.byref(inp), C.byref(h)))
+        if global_stats is None:
+            _check(_lib.fg_index_build(ctx.handle, dev, C.byref(inp), C.byref(h)))
+        else:
+            gs, keep = _global_stats(global_stats)
+            _check(_lib.fg_index_build_global(ctx.handle, dev, C.byref(inp), C.byref(gs), C.byref(h)))
+            del keep
         return cls(h)
 
     def rescore(self, global_stats: "ShardStats", deleted=None) -> "Index":

@@ -111,6 +111,10 @@ typedef struct fg_index_input {
   uint64_t tot_facet_tokens;      /* total_num_tokens of the facet field */
 } fg_index_input;
 int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** out);
+/* ... one segment of a namespace scored with the namespace's statistics g
+ * (below): the per-segment build a tantivy host makes for each new segment. */
+typedef struct fg_global_stats fg_global_stats;
+int fg_index_build_global(fg_ctx* ctx, int dev, const fg_index_input* in, const fg_global_stats* g, fg_index** out);
 
 /* ---- doc-sharded namespace --------------------- */
 /* One namespace split into contiguous doc-id ranges, one shard per GPU, each
@@ -121,14 +125,14 @@ int fg_index_build(fg_ctx* ctx, int dev, const fg_index_input* in, fg_index** ou
  * fg_docs_stats, the ranks sum them (one all-reduce), and every shard builds
  * with the sums.  Merging the shard top-k lists by (score desc, shard asc,
  * doc asc) with fg_merge_shards then equals (score desc, global doc asc). */
-typedef struct fg_global_stats {
+struct fg_global_stats {
   uint64_t n_docs;           /* N over all shards, deleted docs included */
   uint64_t tot_tokens[2];    /* total_num_tokens(text), (name) over all shards */
   const uint32_t* df_text;   /* [n_terms] doc_freq in `text` over all shards */
   const uint32_t* df_name;   /* [n_terms] doc_freq in `name`, or NULL (all 0) */
   const uint32_t* df_facet;  /* [n_facet_terms] doc_freq in `facet`, or NULL (no facets) */
   uint64_t tot_facet_tokens; /* total_num_tokens(facet) over all shards */
-} fg_global_stats;
+};
 /* Local statistics of one shard (host only, no device): df per term and field
  * ([n_terms] each, caller-owned) and the two token totals. */
 int fg_docs_stats(const fg_docs_input* in, uint32_t* df_text, uint32_t* df_name, uint64_t* tot_tokens2);

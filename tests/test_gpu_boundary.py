@@ -100,8 +100,7 @@ def test_index_build_from_postings_equals_from_docs(native, ctx, fixture):
         q_off, terms = synth.queries(64, m0, m1, max_rank=min(nt, 1 << 14), seed_q=31)
         kw = {}
         if facets is not None:
-            f_off = np.arange(65, dtype=np.uint32) % 2 * 0  # every other query filtered below
-            fl = [[int(i % nf)] if i % 2 else [] for i in range(64)]
+            fl = [[int(i % nf)] if i % 2 else [] for i in range(64)]  # every other query filtered
             f_off = np.cumsum([0] + [len(x) for x in fl]).astype(np.uint32)
             kw = dict(f_off=f_off, f_terms=np.array([x for f in fl for x in f], np.uint32))
         same_results(a.search_batch(q_off, terms, k, mode=mode, **kw), b.search_batch(q_off, terms, k, mode=mode, **kw))
@@ -197,3 +196,24 @@ def test_concurrent_searches_and_commit(native, ctx):
         rs, rd = ref2.search([vocab[a], vocab[b]], 20)
         assert [g[1] for g in got] == rd.tolist()
         assert np.allclose([g[0] for g in got], rs, rtol=1e-5, atol=0)
+
+
+def test_index_build_global_postings_segment(native, ctx):
+    """fg_index_build_global: one segment's host-inverted postings scored with
+    the namespace's statistics equal fg_index_build_from_docs_global's snapshot
+    of the same docs (the per-segment build of a tantivy host)."""
+    from fugu_amd import synth
+    fx = load_golden("synth_names_2k.json")
+    n, nt, off, tok, no, ntk, dl = golden_corpus(fx)
+    cut = 1200  # segment = docs [cut, n); the namespace = all n docs
+    so, st = off[cut:] - off[cut], tok[off[cut]:]
+    sno, snt = no[cut:] - no[cut], ntk[no[cut]:]
+    g = native.docs_stats(off, tok, nt, no, ntk)
+    a = native.Index.from_docs(ctx, so, st, nt, sno, snt, dl[cut:], global_stats=g)
+    term_off, doc, tf_t, tf_n, fn_t, fn_n, tot, _ = invert(n - cut, nt, so, st, sno, snt)
+    b = native.Index.from_postings(ctx, n - cut, term_off, doc, tf_t, tf_n, fn_t, fn_n, tot, deleted=dl[cut:],
+                                   global_stats=g)
+    assert a.stats().avgdl == b.stats().avgdl
+    for (m0, m1, k, mode) in [(1, 3, 10, native.MODE_AND), (2, 5, 50, native.MODE_OR)]:
+        q_off, terms = synth.queries(64, m0, m1, max_rank=min(nt, 1 << 14), seed_q=33)
+        same_results(a.search_batch(q_off, terms, k, mode=mode), b.search_batch(q_off, terms, k, mode=mode))
