@@ -50,9 +50,11 @@ constexpr uint32_t kInvalid = 0xFFFFFFFFu;
 __device__ inline uint32_t lane_id() { return threadIdx.x & 63; }
 __device__ inline uint32_t wave_id() { return threadIdx.x >> 6; }
 
-// Upper bounds are compared after inflating by 2^-17 relative: that covers any
-// f32 summation-order difference for <= 16 addends, so bound-based pruning
-// never drops a doc whose exactly-summed score reaches the threshold.
+// Upper bounds are compared after inflating by 2^-17 relative: a bound sums at
+// most 16 clauses plus the facet maximum (17 non-negative addends), whose f32
+// summation-order error is below 2 * 17 * 2^-24 < 2^-18 relative, so
+// bound-based pruning never drops a doc whose exactly-summed score reaches the
+// threshold.
 __device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f; }  // 1 + 2^-17
 
 // Term score at doc d through the term's dense structure (meta_slot != 0),
@@ -539,8 +541,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
 //   then hits go through the same local top-k buffer / threshold publication
 //   as k_conj, and k_final selects the query's top-k.
 // Bounds are compared after inflating by 2^-17 relative, which covers any f32
-// summation-order difference for <= 16 clauses, so the pruning never drops a
-// true top-k doc: results equal the exhaustive union.
+// summation-order difference of <= 16 clauses plus the facet maximum
+// (inflate_bound), so the pruning never drops a true top-k doc: results equal
+// the exhaustive union.
 constexpr uint32_t kTileShift = kDisjTileShift;
 constexpr uint32_t kTile = 1u << kTileShift;   // docs per tile (LDS score array: 16 KB)
 constexpr uint32_t kRound = 1024;              // postings / docs per pass

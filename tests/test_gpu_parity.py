@@ -377,3 +377,37 @@ def test_doc_sharded_facets_equal_single_index(native, ctx, corpus_1m, facets_1m
         m = int(n1[i])
         assert np.array_equal(gdoc[i, :m], d1[i, :m]), i
         assert np.array_equal(ms[i, :m], s1[i, :m]), i
+
+
+def test_or_top1000_near_ties_all_dense_with_facet_filter(native, ctx):
+    """k_disj's bound 2 is the exact score when every clause is dense,
+    so pruning at the top-k boundary rests on inflate_bound alone.  A corpus of
+    few distinct documents repeated thousands of times puts long runs of EQUAL
+    scores across the k = 1000 boundary; every term is dense (rank words) and a
+    facet filter keeps part of the docs.  Results must equal the oracle's: the
+    lowest doc ids win each tie."""
+    from oracle import oracle as orc
+    rng = np.random.default_rng(17)
+    shapes = [[0, 1, 2], [0, 1], [1, 2, 2], [0, 2], [3, 0, 1, 2], [1], [2, 3], [0, 0, 1]]
+    docs = [shapes[int(rng.integers(0, len(shapes)))] for _ in range(12000)]
+    off = np.cumsum([0] + [len(d) for d in docs]).astype(np.uint64)
+    tok = np.array([t for d in docs for t in d], np.uint32)
+    facet_tok = [[0, 1] if i % 3 else [0, 2] for i in range(len(docs))]  # two facet values + the root
+    fo = np.cumsum([0] + [len(f) for f in facet_tok]).astype(np.uint64)
+    ft = np.array([t for f in facet_tok for t in f], np.uint32)
+    ix = native.Index.from_docs(ctx, off, tok, 4, facets=(fo, ft, 3))
+    assert ix.stats().n_rank_terms == 4  # every term has rank words
+    ref = orc.OracleIndex(4, off, tok, facet_off=fo, facet_tok=ft, n_fterms=3)
+    qs = [[0, 1, 2], [1, 2], [0, 3], [2, 1, 0, 3]]
+    q_off = np.cumsum([0] + [len(q) for q in qs]).astype(np.uint32)
+    terms = np.array([t for q in qs for t in q], np.uint32)
+    for fl in ([[1]] * 4, [[2, 1]] * 4, [[]] * 4):
+        f_off = np.cumsum([0] + [len(f) for f in fl]).astype(np.uint32)
+        f_terms = np.array([t for f in fl for t in f], np.uint32)
+        s, d, n = ix.search_batch(q_off, terms, 1000, mode=native.MODE_OR, f_off=f_off, f_terms=f_terms)
+        rs, rd, rn, _, _ = ref.search_batch(q_off, terms, 1000, mode=orc.OR, f_off=f_off, f_terms=f_terms)
+        assert np.array_equal(n, rn)
+        for i in range(len(qs)):
+            assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], (fl[i], qs[i]))
+            # the boundary sits inside a run of equal scores
+            assert n[i] == 1000 and s[i, 999] == s[i, 998]
