@@ -24,7 +24,11 @@ constexpr uint32_t kChunk = kThreads * kItems;   // 2048 lead candidates per wor
 constexpr uint32_t kWaveSpan = kChunk / 4;       // 512 consecutive candidates per wave
 constexpr uint32_t kMaxTerms = 16;        // terms per query (FG_MAX_TERMS)
 constexpr uint32_t kMaxK = 1024;          // largest top-k the device select supports
-constexpr uint32_t kFinalCap = 8192;      // candidates kept in LDS by the final select
+#ifndef FG_FINALCAP
+#define FG_FINALCAP 4096  // tools/ab_variants.py: 8192 -> 4096 took k_final 0.132 -> 0.083 ms (5 WGs per CU), OR k=1000 0.99 -> 0.75
+#endif
+constexpr uint32_t kFinalCap = FG_FINALCAP;  // candidates kept in LDS by the final select (>= kMaxK)
+static_assert(FG_FINALCAP >= 1024, "the final sort runs in place for up to kMaxK keys");
 #ifndef FG_DENSE_DIV
 #define FG_DENSE_DIV 256  // tools/ab_variants.py sweep 8..512: DESIGN.md §3
 #endif
@@ -210,7 +214,7 @@ struct ScoreJob {
   float* ktop;                // [V * kNumTopK] out (zeroed first)
   const uint32_t* ch_term;    // chunk tables
   const uint32_t* ch_first;
-  const uint32_t* kt_terms;   // k_ktop: terms with df >= kTopKs[1]
+  const uint32_t* kt_terms;   // k_ktop: terms with postings
 };
 
 // kernels.hip entry points (host-callable launchers)
