@@ -302,6 +302,7 @@ def main():
                     help="skip the secondary workloads (C3, OR top-1000, end-to-end, C4, C5)")
     ap.add_argument("--extra-steps", type=int, default=5)
     ap.add_argument("--no-c5", action="store_true", help="skip the 100M-doc C5 secondary line")
+    ap.add_argument("--e2e-workers", type=int, default=4, help="batches in flight in the end-to-end line")
     ap.add_argument("--disj", action="store_true",
                     help="headline batch = 2-5-term OR (k_disj; profiling runs, pass --k 1000 --no-cpu)")
     args = ap.parse_args()
@@ -532,7 +533,7 @@ def main():
 
     # ---- end-to-end batches, then the fan-out configs C4 and C5 on this one GPU
     if rank == 0 and world == 1 and not args.no_extra:
-        extra["e2e_pipelined"] = e2e_pipeline(ix, native, synth, torch, dev, nq, K, 20, 2)
+        extra["e2e_pipelined"] = e2e_pipeline(ix, native, synth, torch, dev, nq, K, 24, args.e2e_workers)
         log(f"[bench] e2e pipelined: {extra['e2e_pipelined']['value']} q/s")
     if rank == 0 and world == 1 and not args.no_extra:
         extra["commit_10M"] = commit_latency(ctx, ix, corp, native, synth, threads)

@@ -550,6 +550,10 @@ constexpr uint32_t kRound = 1024;              // postings / docs per pass
 constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
 constexpr uint32_t kPairs = 1024;              // (candidate, clause) rescoring pairs per pass
 constexpr uint32_t kMaxTiles = kDisjMaxGroup;  // tiles per work item
+#ifndef FG_EXHMIN
+#define FG_EXHMIN 1024
+#endif
+constexpr uint32_t kExhaustiveMin = FG_EXHMIN;  // all-essential tiles with fewer postings go posting-driven
 constexpr uint32_t kMaxSeg = kMaxTiles * kMaxTerms;
 static_assert(kMaxSeg <= 2 * kThreads, "k_disj segment list: two (tile, clause) pairs per thread");
 
@@ -723,13 +727,16 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       if (make_key(inflate_bound(s2 + fmax), d0) >= thr) break;
       s = s2;
     }
-    uint32_t ess = 0, any = 0;
+    uint32_t ess = 0, any = 0, npost = 0;
     for (uint32_t j = P; j < m; ++j) {
       ess |= 1u << ord[j];
       any |= sh.r_hi[t * m + ord[j]] > sh.r_lo[t * m + ord[j]] ? 1u : 0u;
+      npost += sh.r_hi[t * m + ord[j]] - sh.r_lo[t * m + ord[j]];
     }
     sh.t_ess[t] = ess;
-    sh.t_mode[t] = (P == m || !any) ? 0u : (P == 0 ? 1u : 2u);
+    // every clause essential: the exhaustive LDS pass costs the whole tile
+    // (4096 docs), the posting-driven one its postings; take the cheaper
+    sh.t_mode[t] = (P == m || !any) ? 0u : (P == 0 && npost >= kExhaustiveMin ? 1u : 2u);
   }
   __syncthreads();
   FG_PHASE(1);
@@ -894,45 +901,63 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       maybe[j] = 0;
       exact[j] = true;
     }
-    for (uint32_t i = 0; i < m; ++i) {
-      const uint32_t meta = sh.c_meta[i];
-      const uint32_t slot = meta_slot(meta);
-      const bool rank = slot && meta_rank(meta);
-      bool need[J];
-      uint64_t x[J];
-      float v[J];
+    // clauses in groups of G: the rank words of a group's clauses for all J
+    // postings are loaded together, then their scores -- two round trips per
+    // group instead of two per clause; sums still run in clause order
+    constexpr uint32_t G = 4;
+    for (uint32_t i0 = 0; i0 < m; i0 += G) {
+      uint64_t x[G][J];
+      float v[G][J];
+      uint32_t need = 0;  // bit g * J + j
 #pragma unroll
-      for (uint32_t j = 0; j < J; ++j) {
-        need[j] = pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i]);
-        x[j] = 0;
-        v[j] = -1.0f;
-        if (need[j]) {
-          if (rank) x[j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
-          else if (slot) v[j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
-          else v[j] = ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))];
+      for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t i = i0 + g;
+        const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
+        const uint32_t slot = meta_slot(meta);
+        const bool rank = slot && meta_rank(meta);
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+          x[g][j] = 0;
+          v[g][j] = -1.0f;
+          if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
+            need |= 1u << (g * J + j);
+            if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
+            else if (slot) v[g][j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
+            else v[g][j] = ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))];
+          }
         }
       }
-      if (rank) {
+#pragma unroll
+      for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t i = i0 + g;
+        const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
+        if (!(meta_slot(meta) && meta_rank(meta))) continue;
         const float* __restrict__ sp = ix.psc + sh.c_base[i];
 #pragma unroll
         for (uint32_t j = 0; j < J; ++j) {
-          const uint32_t bits = (uint32_t)x[j], bt = pd[j] & 31u;
-          if (need[j] && ((bits >> bt) & 1u))
-            v[j] = sp[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))];
+          const uint32_t bits = (uint32_t)x[g][j], bt = pd[j] & 31u;
+          if (((need >> (g * J + j)) & 1u) && ((bits >> bt) & 1u))
+            v[g][j] = sp[(uint32_t)(x[g][j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))];
         }
       }
 #pragma unroll
-      for (uint32_t j = 0; j < J; ++j) {
-        if (!pk[j]) continue;
-        float b = ps[j];
-        if (i != pcl[j]) {
-          if (!need[j]) continue;
-          b = v[j];
-          exact[j] = exact[j] && slot != 0;
-          if (signbit(b)) continue;  // clause i cannot match d
-          maybe[j] |= 1u << i;
+      for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t i = i0 + g;
+        if (i >= m) break;
+        const uint32_t slot = meta_slot(sh.c_meta[i]);
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+          if (!pk[j]) continue;
+          float b = ps[j];
+          if (i != pcl[j]) {
+            if (!((need >> (g * J + j)) & 1u)) continue;
+            b = v[g][j];
+            exact[j] = exact[j] && slot != 0;
+            if (signbit(b)) continue;  // clause i cannot match d
+            maybe[j] |= 1u << i;
+          }
+          sum[j] += b;
         }
-        sum[j] += b;
       }
     }
 #pragma unroll
