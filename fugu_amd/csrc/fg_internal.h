@@ -104,6 +104,9 @@ struct DevIndex {
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
   const uint32_t* toff;      // [V] first tmax entry of each term, or 0xFFFFFFFF (bucket >= tile: use bmax)
+  const float* cmax;         // [score chunks] largest posting score of each kChunk-posting chunk of a
+                             //     list (block-max: k_conj skips a lead chunk that cannot reach the threshold)
+  const uint32_t* coff;      // [V] index of each term's first chunk in cmax
   const uint32_t* fdoc;      // [PF] facet postings (doc ids, ascending), CSR by facet term
   const uint64_t* foff;      // [VF+1]
   uint32_t n_docs;
@@ -163,6 +166,7 @@ struct DevPlan {
   uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list
   uint64_t* cand_keys;          // [cand_off[nq]] per-query candidate lists
   uint64_t* diag;               // diagnostic builds only (-DFG_DIAG): per-workgroup stamps
+  uint32_t n_single;            // k_conj: the first n_single work items belong to single-list queries
   uint32_t n_scan;              // k_scan work items (queries with no text terms), after the total_chunks
                                 // k_conj / k_disj items in work_q / work_c / work_n
   DevFilters f;
@@ -193,6 +197,7 @@ __host__ __device__ inline uint32_t key_doc(uint64_t k) { return 0xFFFFFFFFu - (
 // directory buckets; ch_* arrays are the chunk tables.
 constexpr uint32_t kScoreChunk = 2048;   // postings per k_score workgroup
 constexpr uint32_t kBucketChunk = 2048;  // buckets per k_bucket workgroup
+static_assert(kScoreChunk == kChunk, "DevIndex::cmax: a k_score chunk is a k_conj lead chunk");
 struct ScoreJob {
   const uint32_t* doc;
   const uint32_t* tfp;        // [P] tf_text | tf_name << 16
@@ -212,6 +217,7 @@ struct ScoreJob {
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
+  float* cmax;                // [score chunks] out: the largest score of each k_score chunk
   const uint32_t* ch_term;    // chunk tables
   const uint32_t* ch_first;
   const uint32_t* kt_terms;   // k_ktop: terms with postings

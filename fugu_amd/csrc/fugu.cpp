@@ -403,6 +403,8 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   d_tmax = static_cast<uint32_t*>(p);
   if ((rc = dev_alloc(4ull * V * fg::kNumTopK, &p))) return rc;
   d_ktop = static_cast<float*>(p);
+  if ((rc = dev_alloc(4ull * ix->n_sc, &p))) return rc;
+  float* d_cmax = static_cast<float*>(p);
   HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, nullptr));
   HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), nullptr));
   HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, nullptr));
@@ -425,6 +427,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.tmaxs = d_tmaxs;
   j.tmax = d_tmax;
   j.ktop = d_ktop;
+  j.cmax = d_cmax;
   j.ch_term = ix->d_sc_term;
   j.ch_first = ix->d_sc_first;
   HIPCHK(fg::launch_score(j, ix->n_sc, nullptr));
@@ -493,6 +496,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
+  ix->d.cmax = d_cmax;
   ix->d.alive = d_alive;
   ix->d.dense = d_dense;
   ix->device_bytes = ix->struct_bytes + bytes;
@@ -571,9 +575,10 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->tile_entries = ntm;
   // chunk tables of the scoring kernels: (term, first posting) per <= kScoreChunk
   // postings, (term, first bucket) per <= kBucketChunk buckets, terms with postings
-  std::vector<uint32_t> sc_t, sc_f, bk_t, bk_f, kt;
+  std::vector<uint32_t> sc_t, sc_f, bk_t, bk_f, kt, coff(V);
   for (uint32_t t = 0; t < V; ++t) {
     const uint64_t n = hp.off[t + 1] - hp.off[t];
+    coff[t] = (uint32_t)sc_t.size();  // the term's first score chunk (DevIndex::cmax)
     if (!n) continue;
     for (uint64_t f = 0; f < n; f += fg::kScoreChunk) { sc_t.push_back(t); sc_f.push_back((uint32_t)f); }
     const uint64_t nbk = ((N - 1) >> (tmeta[t] & 0xFFu)) + 1;
@@ -588,7 +593,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_fdoc;
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
-  uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt;
+  uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt, *d_coff;
   if ((rc = dev_upload(sm, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
   if ((rc = dev_upload(sm, hp.tf.data(), hp.tf.size(), &d_tfp, &bytes))) return rc;
   std::vector<uint32_t>().swap(hp.tf);
@@ -606,6 +611,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   if ((rc = dev_upload(sm, bk_t.data(), bk_t.size(), &d_bkt, &bytes))) return rc;
   if ((rc = dev_upload(sm, bk_f.data(), bk_f.size(), &d_bkf, &bytes))) return rc;
   if ((rc = dev_upload(sm, kt.data(), kt.size(), &d_kt, &bytes))) return rc;
+  if ((rc = dev_upload(sm, coff.data(), coff.size(), &d_coff, &bytes))) return rc;
   g_bt.mark("upload");
   // rank words for the densest terms (fg_internal.h DevIndex), chosen AFTER the
   // uploads above so the budget sees the memory actually left: df >= N /
@@ -686,6 +692,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d.tmeta = d_tmeta;
   ix->d.rank = d_rank;
   ix->d.toff = d_toff;
+  ix->d.coff = d_coff;
   ix->d.fdoc = d_fdoc;
   ix->d.foff = d_foff;
   ix->d.n_docs = hp.n_docs;
@@ -1404,6 +1411,16 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
         q_ub[(size_t)i * fg::kMaxTerms + j] = acc;
       }
     }
+    // one list: its K'-th best alive score (the smallest stored K' >= k) bounds
+    // the query's k-th best from below, so k_conj starts from that threshold and
+    // skips the lead chunks whose block-max cannot reach it (the block-max
+    // pruning tantivy's TopDocs runs on a single TermScorer: block_wand_single_scorer)
+    for (uint32_t j = 0; j < fg::kNumTopK && !missing && m == 1 && q_filter[i] == 0xFFFFFFFFu; ++j) {
+      if (fg::kTopKs[j] < k) continue;
+      const float v = ix->ktop[(size_t)ts[0].term * fg::kNumTopK + j];
+      if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
+      break;
+    }
     const uint64_t df0 = missing ? 0 : ix->off[ts[0].term + 1] - ix->off[ts[0].term];
     lead[i] = (uint32_t)df0;
     nchunk[i] = (uint32_t)((df0 + fg::kChunk - 1) / fg::kChunk);
@@ -1416,7 +1433,13 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     for (uint32_t g = 0; g < ng; ++g)
       items.push_back(W{(g + 0.5) / ng, i, g * G, std::min(G, nch - g * G)});
   }
-  std::stable_sort(items.begin(), items.end(), [](const W& a, const W& b) { return a.key < b.key; });
+  // AND: single-list queries' items first (their own k_conj launch), each part in sweep order
+  auto single = [&](const W& x) { return !disj && q_m[x.q] == 1; };
+  std::stable_sort(items.begin(), items.end(), [&](const W& a, const W& b) {
+    return single(a) != single(b) ? single(a) : a.key < b.key;
+  });
+  uint64_t n_single = 0;
+  for (const W& x : items) n_single += single(x) ? 1 : 0;
   std::stable_sort(scan.begin(), scan.end(), [](const W& a, const W& b) { return a.key < b.key; });
   const uint64_t n_main = items.size(), n_scan = scan.size();
   const uint64_t chunks = n_main + n_scan;  // from here on: work items (k_conj / k_disj, then k_scan)
@@ -1517,6 +1540,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.n_queries = nq;
   p->d.total_chunks = (uint32_t)n_main;
   p->d.n_scan = (uint32_t)n_scan;
+  p->d.n_single = (uint32_t)n_single;
   p->d.k = k;
   p->d.mode = (uint32_t)q->mode;
   p->d.f.n_filters = nf;

@@ -286,6 +286,11 @@ __device__ uint32_t flush_candidates(const DevPlan& pl, uint32_t q, const uint64
 
 // FG_WAVES: minimum waves per SIMD the register allocation must allow (the
 // kernel is bound by memory latency, so occupancy is its main lever)
+// kSingle: the instantiation for single-list queries runs work items
+// [0, n_single) (no probes; block-max chunk skipping), the general one
+// [n_single, total_chunks); separate launches keep the general kernel's
+// register allocation.
+template <bool kSingle>
 __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPlan pl) {
   __shared__ ConjShared sh;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -294,13 +299,14 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   // doc sweep, so its L2 holds one doc window of the hot lists.
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
   const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const uint32_t w = (kSingle ? 0u : pl.n_single) +
+                     (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 
   uint64_t t_start = FG_NOW(), t_probe = 0, t_keys = 0, t_sel = 0, n_app = 0;
   (void)t_start; (void)t_probe; (void)t_keys; (void)t_sel; (void)n_app;
   const uint32_t q = pl.work_q[w];
   const uint32_t c0 = pl.work_c[w], nc = pl.work_n[w];
-  const uint32_t m = pl.q_m[q];
+  const uint32_t m = kSingle ? 1u : pl.q_m[q];
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const float* qub = pl.q_ub + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
@@ -326,23 +332,31 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   // chunk and its result folded in at the start of the next one, after that
   // chunk's lead loads are in flight.  A stale threshold is still a valid lower
   // bound of the query's k-th key (values only grow), so pruning stays exact.
+  // the plan's starting threshold (single-list queries: the term's K'-th best score)
+  const uint64_t thr0 = pl.q_thr0[q];
   uint64_t pend = 0;
   if (tid == 0) {
     sh.n_buf = 0;
-    sh.thr = 0;
-    pend = atomicMax(gthr, 0ull);
+    sh.thr = thr0;
+    pend = atomicMax(gthr, (unsigned long long)thr0);
   }
 #ifdef FG_DIAG
   if (tid < 8) sh.dgc[tid] = 0;
 #endif
   uint64_t local_T = 0;
+  // block-max skip (single lists): a chunk whose largest score (+ the facet
+  // maximum) cannot reach the threshold is not loaded.  thr_k is the threshold
+  // as every thread last saw it (uniform), so the skip is uniform too.
+  const float* __restrict__ cmax = ix.cmax + ix.coff[t0];
+  uint64_t thr_k = thr0;
 
   for (uint32_t cc = 0; cc < nc; ++cc) {
     const uint32_t c = c0 + cc;
+    uint64_t tp0 = FG_NOW(), tp1 = tp0;
+    (void)tp0; (void)tp1;
+    if (!kSingle || make_key(inflate_bound(cmax[c] + fmax), 0u) >= thr_k) {
     const uint64_t base0 = lead_base + (uint64_t)c * kChunk;
     const uint32_t cnt = min(kChunk, lead_df - c * kChunk);
-    uint64_t tp0 = FG_NOW();
-    (void)tp0;
     // lead candidates: item j of lane l = wv*512 + j*64 + l (coalesced per j)
     uint32_t doc[kItems];
     float s0[kItems];
@@ -360,6 +374,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     if (tid == 0 && pend > sh.thr) sh.thr = pend;
     __syncthreads();
     const uint64_t thr = sh.thr;
+    thr_k = thr;
     // MaxScore (uniform): once the query has a threshold, a candidate whose
     // partial score plus the remaining lists' maxima cannot reach it is dropped
     // before the next probe.  Bounds are inflated by 2^-17 (inflate_bound).
@@ -371,6 +386,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
         if ((live & (1u << j)) && !filter_bits(fmask, fshift, doc[j])) live &= ~(1u << j);
     }
     FG_COUNT(0, live);
+#ifdef FG_DIAG
+    const uint32_t live0 = live;
+#endif
     if (!prune) FG_COUNT(7, live);  // candidates of chunks that start with no threshold
     if (prune) {
       const float ub = qub[1] + fmax;
@@ -379,6 +397,26 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
         if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + ub), doc[j]) < thr) live &= ~(1u << j);
     }
     FG_COUNT(1, live);
+#ifdef FG_DIAG
+    {
+      // block-max headroom: rows (wave, item j = 64 consecutive lead postings)
+      // with loaded candidates, rows the first bound prunes whole (slot 6), and
+      // chunks it prunes whole (slot 4); slots 4-6 then no longer count probes
+      uint32_t rows = 0, dead = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kItems; ++j) {
+        const bool l0 = __ballot((live0 >> j) & 1u) != 0, l1 = __ballot((live >> j) & 1u) != 0;
+        rows += l0 ? 1u : 0u;
+        dead += (l0 && !l1) ? 1u : 0u;
+      }
+      if (lane == 0) {
+        atomicAdd(&sh.dgc[5], (unsigned long long)rows);
+        atomicAdd(&sh.dgc[6], (unsigned long long)dead);
+      }
+      const int any_live = __syncthreads_or(live != 0), any_loaded = __syncthreads_or(live0 != 0);
+      if (tid == 0 && any_loaded && !any_live) sh.dgc[4] += 1;
+    }
+#endif
 
     // every list probed in intersection order; a candidate whose partial score
     // plus the remaining lists' maxima cannot reach the threshold is dropped
@@ -457,10 +495,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
           if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + acc_r[j] + acc_o[j] + ub), doc[j]) < thr)
             live &= ~(1u << j);
       }
-      FG_COUNT(1 + i, live);
+      if (i <= 2) FG_COUNT(1 + i, live);
     }
-    uint64_t tp1 = FG_NOW();
-    (void)tp1;
+    tp1 = FG_NOW();
 
     // survivors: tantivy's summation order, alive bitset, pruning threshold,
     // append to the local top-k buffer
@@ -479,11 +516,15 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       }
       wave_append(keep, key, sh.buf, &sh.n_buf, kBuf);
     }
+    }  // block-max skip
     __syncthreads();
     const uint32_t n = sh.n_buf;
     uint64_t tp2 = FG_NOW();
     (void)tp2;
-    if (n > kTrunc || (cc + 1 == nc && n > K)) local_T = truncate_topk(sh, n, K);
+    if (n > kTrunc || (cc + 1 == nc && n > K)) {
+      local_T = truncate_topk(sh, n, K);
+      if (local_T > thr_k) thr_k = local_T;
+    }
     uint64_t tp3 = FG_NOW();
     (void)tp3;
 #ifdef FG_DIAG
@@ -1329,8 +1370,12 @@ __global__ __launch_bounds__(kThreads) void k_merge(uint32_t n_shards, uint32_t 
 }  // namespace
 
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
-  if (pl.total_chunks == 0) return hipSuccess;
-  k_conj<<<pl.total_chunks, kThreads, 0, s>>>(ix, pl);
+  if (pl.n_single) {
+    k_conj<true><<<pl.n_single, kThreads, 0, s>>>(ix, pl);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (pl.total_chunks > pl.n_single) k_conj<false><<<pl.total_chunks - pl.n_single, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 
@@ -1465,9 +1510,22 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
   const uint32_t n = (uint32_t)(j.off[t + 1] - b);
   const uint32_t end = min(n, first + kScoreChunk);
   const float wt = j.w_text[t], wn = j.w_name[t];
+  float mx = 0.0f;
   for (uint32_t p = first + threadIdx.x; p < end; p += kThreads) {
     const uint32_t d = j.doc[b + p];
-    j.psc[b + p] = posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache);
+    const float v = posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache);
+    j.psc[b + p] = v;
+    mx = fmaxf(mx, v);
+  }
+  // the chunk's block-max (scores >= 0)
+  __shared__ float wmax[kThreads / 64];
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = wmax[0];
+    for (uint32_t w = 1; w < kThreads / 64; ++w) m = fmaxf(m, wmax[w]);
+    j.cmax[blockIdx.x] = m;
   }
 }
 

@@ -411,3 +411,31 @@ def test_or_top1000_near_ties_all_dense_with_facet_filter(native, ctx):
             assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], (fl[i], qs[i]))
             # the boundary sits inside a run of equal scores
             assert n[i] == 1000 and s[i, 999] == s[i, 998]
+
+
+@pytest.mark.parametrize("k", [1, 10, 37, 100, 1000, 1024])
+def test_single_list_block_max_vs_oracle(native, ctx, gpu_1m, oracle_1m, k):
+    """Single-term AND queries start from the term's K'-th best alive score and
+    skip lead chunks by their block-max (k_conj, DevIndex::cmax): the top-k
+    must still equal the oracle's, for stored K' (1/10/100/1000), k between
+    them and k above the largest, on frequent and rare terms, with and
+    without deletions."""
+    from fugu_amd import synth
+    from oracle import oracle as orc
+    terms = np.array(list(range(0, 40)) + list(range(1000, 1040, 2)) + [60000, 300000], np.uint32)
+    q_off = np.arange(len(terms) + 1, dtype=np.uint32)
+    s, d, n = gpu_1m.search_batch(q_off, terms, k)
+    rs, rd, rn, _, _ = oracle_1m.search_batch(q_off, terms, k, threads=16)
+    assert np.array_equal(n, rn)
+    for i in range(len(terms)):
+        assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], (k, int(terms[i])))
+    # deletions: the K'-th best counts alive postings only
+    c = synth.corpus(300_000)
+    dl = (np.arange(300_000) % 3 == 1).astype(np.uint8)
+    gi = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, deleted=dl)
+    oi = orc.OracleIndex(synth.VOCAB, c.off, c.tok, deleted=dl, threads=16)
+    s, d, n = gi.search_batch(q_off, terms, k)
+    rs, rd, rn, _, _ = oi.search_batch(q_off, terms, k, threads=16)
+    assert np.array_equal(n, rn)
+    for i in range(len(terms)):
+        assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], ("deletes", k, int(terms[i])))

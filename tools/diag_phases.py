@@ -57,7 +57,10 @@ def main():
             "appended_per_chunk": pct(conj[:, 5].astype(np.float64) / np.maximum(nchk, 1)),
             "written_total": int(conj[:, 7].sum()),
             # candidates alive at: lead load, after the first MaxScore bound, after probe i
-            "alive_lead_b1_p1_p2_p3": [int(conj[:, 8 + i].sum()) for i in range(5)], "lead_unpruned": int(conj[:, 15].sum()),
+            "alive_lead_b1_p1_p2": [int(conj[:, 8 + i].sum()) for i in range(4)], "lead_unpruned": int(conj[:, 15].sum()),
+            # block-max headroom: 64-posting rows / whole chunks the first bound prunes entirely
+            "rows_loaded": int(conj[:, 13].sum()), "rows_pruned_by_b1": int(conj[:, 14].sum()),
+            "chunks_pruned_by_b1": int(conj[:, 12].sum()),
         },
     }
     f_start, f_read, f_sel, f_end = (fin[:, i].astype(np.int64) for i in range(4))
