@@ -205,11 +205,29 @@ __device__ void bitonic_sort_desc(uint64_t* s, uint32_t P) {
 #ifndef FG_TRUNC
 #define FG_TRUNC 1024
 #endif
+#ifndef FG_MAXPROBE
+#define FG_MAXPROBE kMaxTerms  // timing experiments only (tools/ab_variants.py): lists probed per query
+#endif
 #ifndef FG_WAVES
 #define FG_WAVES 4  // tools/ab_variants.py: 3 -> 4 waves/SIMD took k_conj 3.18 -> 2.58 ms
 #endif
 constexpr uint32_t kTrunc = FG_TRUNC;           // truncate the local buffer past this (>= kMaxK)
 constexpr uint32_t kBuf = kTrunc + kChunk;       // kept keys (<= kTrunc) + one chunk of hits
+// Deferred probes (queries of >= 3 unfiltered lists): the candidates that pass
+// the second list wait in an LDS queue, and the remaining lists are probed for
+// the whole queue at once (flush_deferred) instead of per chunk for the few
+// lanes still alive.  The queue fills the LDS left at 4 workgroups per CU.
+#ifndef FG_DEFER
+#define FG_DEFER 896
+#endif
+constexpr uint32_t kDeferCap = FG_DEFER;                                // entries (doc << 32 | partial score)
+#ifndef FG_DEFER_FLUSH
+#define FG_DEFER_FLUSH (FG_DEFER / 2)
+#endif
+constexpr uint32_t kDeferFlush = FG_DEFER_FLUSH;                        // flush once this full at a chunk end
+constexpr uint32_t kDeferR = kDeferCap ? (kDeferCap + kThreads - 1) / kThreads : 1;  // entries per thread in a flush
+constexpr uint64_t kDeferNone = ~0ull;                                  // a reserved slot left empty
+static_assert(kTrunc + kDeferCap <= kBuf, "a flush after truncation must fit the key buffer");
 
 struct ConjShared {
   alignas(16) uint64_t buf[kBuf];
@@ -217,6 +235,8 @@ struct ConjShared {
   uint32_t scratch[8];
   uint32_t n_buf;
   uint64_t thr;
+  uint64_t dq[kDeferCap > 0 ? kDeferCap : 1];  // deferred candidates
+  uint32_t n_dq;                               // slots reserved (may pass kDeferCap: the rest went inline)
 #ifdef FG_DIAG
   unsigned long long dgc[8];  // candidates alive at: load, after the first bound, after probe i (1..5)
 #endif
@@ -284,6 +304,112 @@ __device__ uint32_t flush_candidates(const DevPlan& pl, uint32_t q, const uint64
   return total;
 }
 
+// Term ti's score at the doc of each live item (-1: the term is absent from
+// it), through the term's rank words, its f32 score table or its bucket
+// directory; the N items' loads are in flight together.
+template <uint32_t N>
+__device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_t (&doc)[N], uint32_t live,
+                                  float (&sc)[N]) {
+  const uint32_t meta = ix.tmeta[ti];
+  const uint32_t dslot = meta_slot(meta);
+  if (dslot && meta_rank(meta)) {
+    // rank words: presence + rank in one 8-B load per item (all items'
+    // loads in flight together), then the posting score of the hits
+    const uint64_t* __restrict__ rw = ix.rank + (size_t)(dslot - 1) * ix.rank_words;
+    const float* __restrict__ ps = ix.psc + ix.off[ti];
+    uint64_t x[N];
+#pragma unroll
+    for (uint32_t j = 0; j < N; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> 5] : 0ull;
+#pragma unroll
+    for (uint32_t j = 0; j < N; ++j) {
+      const uint32_t bits = (uint32_t)x[j], b = doc[j] & 31u;
+      sc[j] = ((bits >> b) & 1u) ? ps[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))] : -1.0f;
+    }
+  } else if (dslot) {
+    // f32 score table: doc-indexed, one 4-B load per item (-1 = absent)
+    const float* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
+#pragma unroll
+    for (uint32_t j = 0; j < N; ++j) sc[j] = (live & (1u << j)) ? dt[doc[j]] : -1.0f;
+  } else {
+    const uint64_t bi = ix.off[ti];
+    const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu;
+    const uint32_t* __restrict__ di = ix.doc + bi;
+    const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[ti];
+    // bucket of each live item, then a branchless power-of-two search in it
+    uint32_t pos[N], hi[N];
+#pragma unroll
+    for (uint32_t j = 0; j < N; ++j) {
+      pos[j] = 0;
+      hi[j] = 0;
+      if (live & (1u << j)) {
+        const uint32_t b = doc[j] >> B;
+        pos[j] = dir[b];
+        hi[j] = dir[b + 1];
+      }
+    }
+    for (uint32_t st = S; st > 0; --st) {
+      const uint32_t half = 1u << (st - 1);
+#pragma unroll
+      for (uint32_t j = 0; j < N; ++j) {
+        const uint32_t idx = pos[j] + half - 1;
+        if ((live & (1u << j)) && idx < hi[j] && di[idx] < doc[j]) pos[j] += half;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < N; ++j) {
+      sc[j] = -1.0f;
+      if ((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j]) sc[j] = ix.psc[bi + pos[j]];
+    }
+  }
+}
+
+// Probe lists 2.. of the queue's nd deferred candidates (doc, left + right
+// score), in intersection order with the MaxScore bound after each, and append
+// the survivors' keys.  The sums are the ones the inline path forms:
+// (left + right) + (0.0 + s_2 + ...).  Unfiltered queries only (no facet term).
+__device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_t* terms, uint32_t m,
+                               const float* qub, uint64_t thr, uint32_t nd) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t doc[kDeferR], live = 0;
+  float s01[kDeferR], acc[kDeferR];
+#pragma unroll
+  for (uint32_t r = 0; r < kDeferR; ++r) {
+    const uint32_t i = r * kThreads + tid;
+    const uint64_t e = i < nd ? sh.dq[i] : kDeferNone;
+    doc[r] = (uint32_t)(e >> 32);
+    s01[r] = __uint_as_float((uint32_t)e);
+    acc[r] = 0.0f;
+    live |= (doc[r] != kInvalid ? 1u : 0u) << r;
+  }
+  for (uint32_t i = 2; i < min(m, (uint32_t)FG_MAXPROBE); ++i) {
+    if (!__any(live != 0)) break;
+    float sc[kDeferR];
+    probe_list<kDeferR>(ix, terms[i], doc, live, sc);
+#pragma unroll
+    for (uint32_t r = 0; r < kDeferR; ++r) {
+      if (sc[r] < 0.0f) live &= ~(1u << r);
+      else acc[r] += sc[r];
+    }
+    if (thr != 0 && i + 1 < m) {
+      const float ub = qub[i + 1];
+#pragma unroll
+      for (uint32_t r = 0; r < kDeferR; ++r)
+        if ((live & (1u << r)) && make_key(inflate_bound(s01[r] + acc[r] + ub), doc[r]) < thr) live &= ~(1u << r);
+    }
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kDeferR; ++r) {
+    bool keep = (live >> r) & 1u;
+    uint64_t key = 0;
+    if (keep && ix.alive && !((ix.alive[doc[r] >> 5] >> (doc[r] & 31)) & 1u)) keep = false;
+    if (keep) {
+      key = make_key(s01[r] + acc[r], doc[r]);
+      keep = key >= thr;
+    }
+    wave_append(keep, key, sh.buf, &sh.n_buf, kBuf);
+  }
+}
+
 // FG_WAVES: minimum waves per SIMD the register allocation must allow (the
 // kernel is bound by memory latency, so occupancy is its main lever)
 // kSingle: the instantiation for single-list queries runs work items
@@ -337,6 +463,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   uint64_t pend = 0;
   if (tid == 0) {
     sh.n_buf = 0;
+    sh.n_dq = 0;
     sh.thr = thr0;
     pend = atomicMax(gthr, (unsigned long long)thr0);
   }
@@ -349,6 +476,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   // as every thread last saw it (uniform), so the skip is uniform too.
   const float* __restrict__ cmax = ix.cmax + ix.coff[t0];
   uint64_t thr_k = thr0;
+  const bool defer = !kSingle && kDeferCap > 0 && m >= 3 && !fmask;
 
   for (uint32_t cc = 0; cc < nc; ++cc) {
     const uint32_t c = c0 + cc;
@@ -421,13 +549,11 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     // every list probed in intersection order; a candidate whose partial score
     // plus the remaining lists' maxima cannot reach the threshold is dropped
     // before the next probe
-    float acc_r[kItems], acc_o[kItems];
+    // after the first probe s0[j] holds left + right (the first two lists' sum)
+    float acc_o[kItems];
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
-      acc_r[j] = 0.0f;
-      acc_o[j] = 0.0f;
-    }
-    for (uint32_t i = 1; i < m; ++i) {
+    for (uint32_t j = 0; j < kItems; ++j) acc_o[j] = 0.0f;
+    for (uint32_t i = 1; i < min(m, (uint32_t)FG_MAXPROBE); ++i) {
       if (!__any(live != 0)) break;  // wave-uniform early exit
       const uint32_t ti = terms[i];
       const uint32_t meta = ix.tmeta[ti];
@@ -486,14 +612,41 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
 #pragma unroll
       for (uint32_t j = 0; j < kItems; ++j) {
         if (sc[j] < 0.0f) { live &= ~(1u << j); continue; }
-        if (i == 1) acc_r[j] = sc[j]; else acc_o[j] += sc[j];
+        if (i == 1) s0[j] = s0[j] + sc[j]; else acc_o[j] += sc[j];
       }
       if (prune && i + 1 < m) {
         const float ub = qub[i + 1] + fmax;
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
-          if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + acc_r[j] + acc_o[j] + ub), doc[j]) < thr)
+          if ((live & (1u << j)) && make_key(inflate_bound(s0[j] + acc_o[j] + ub), doc[j]) < thr)
             live &= ~(1u << j);
+      }
+      if (i == 1 && defer) {
+        // park this wave's survivors in the queue when they fit (slots reserved
+        // with one LDS atomic); a wave that does not fit probes on inline
+        uint32_t nw = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) nw += (uint32_t)__popcll(__ballot((live >> j) & 1u));
+        if (nw) {
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(&sh.n_dq, nw);
+          base = (uint32_t)__shfl((int)base, 0, 64);
+          if (base + nw <= kDeferCap) {
+            uint32_t at = base;
+#pragma unroll
+            for (uint32_t j = 0; j < kItems; ++j) {
+              const bool b = (live >> j) & 1u;
+              const unsigned long long bal = __ballot(b);
+              if (b)
+                sh.dq[at + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] =
+                    ((uint64_t)doc[j] << 32) | __float_as_uint(s0[j]);
+              at += (uint32_t)__popcll(bal);
+            }
+            live = 0;
+          } else {
+            for (uint32_t x = base + lane; x < kDeferCap; x += 64) sh.dq[x] = kDeferNone;  // the part that fit
+          }
+        }
       }
       if (i <= 2) FG_COUNT(1 + i, live);
     }
@@ -508,7 +661,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       if (keep && ix.alive && !((ix.alive[doc[j] >> 5] >> (doc[j] & 31)) & 1u)) keep = false;
       if (keep) {
         // one term = the union itself
-        float s = m == 1 ? s0[j] : (s0[j] + acc_r[j]) + acc_o[j];
+        float s = m == 1 ? s0[j] : s0[j] + acc_o[j];
         // with a filter: Intersection(text, facet union) = text + facet (two children)
         if (fmask) s = s + ftab[filter_bits(fmask, fshift, doc[j])];
         key = make_key(s, doc[j]);
@@ -518,9 +671,22 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     }
     }  // block-max skip
     __syncthreads();
-    const uint32_t n = sh.n_buf;
+    uint32_t n = sh.n_buf;
     uint64_t tp2 = FG_NOW();
     (void)tp2;
+    if (defer) {
+      const uint32_t nd = min(sh.n_dq, kDeferCap);
+      if (nd >= kDeferFlush || (cc + 1 == nc && nd > 0)) {
+        if (n > kTrunc) {  // room for the flush's keys
+          local_T = truncate_topk(sh, n, K);
+          if (local_T > thr_k) thr_k = local_T;
+        }
+        flush_deferred(ix, sh, terms, m, qub, thr_k, nd);
+        __syncthreads();
+        n = sh.n_buf;
+        if (tid == 0) sh.n_dq = 0;
+      }
+    }
     if (n > kTrunc || (cc + 1 == nc && n > K)) {
       local_T = truncate_topk(sh, n, K);
       if (local_T > thr_k) thr_k = local_T;
