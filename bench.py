@@ -580,7 +580,7 @@ def main():
                 "kernel": kname, "kernel_ms": round(conj_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
                 "alg_model": "fg_bytes_model_gpu: k_conj's exhaustive cascade at the HBM layout (8 B per lead "
-                             "posting; per probe 4 B dense element, or 8 B bucket bounds + 4 B per search step + "
+                             "posting; per probe 8 B rank word + 4 B score on a hit, or 8 B bucket bounds + 4 B per search step + "
                              "4 B compare + 4 B score on a hit; 8 B per kept key)",
                 "alg_bytes_split": {"lead": float(bmg[:, 0].sum()), "probe": float(bmg[:, 1].sum()),
                                     "output": float(bmg[:, 2].sum())},

@@ -52,7 +52,12 @@ constexpr uint32_t kGroupsPerQuery = 64;  // a query's chunks are split into ~th
 #define FG_MAXGROUP 16
 #endif
 constexpr uint32_t kMaxGroup = FG_MAXGROUP;  // ... of at most this many chunks each
-constexpr uint32_t kHistBins = 2048;      // 11-bit radix digits
+#ifndef FG_HIST_BITS
+#define FG_HIST_BITS 10  // tools/ab_variants.py: 11 -> 10 took k_conj 1.110 -> 1.082 ms (LDS 40.0 -> 35.9 KB, no spills)
+#endif
+constexpr uint32_t kHistBits = 11;                 // radix digit width of the LDS selects
+constexpr uint32_t kHistBins = 1u << kHistBits;
+constexpr uint32_t kConjHistBits = FG_HIST_BITS;   // ... k_conj's (its LDS sets its occupancy)
 constexpr uint32_t kDisjTileShift = 12;   // k_disj: 4096-doc tiles
 constexpr uint32_t kDisjMaxGroup = 32;    // ... at most this many tiles per work item
 constexpr uint32_t kNumTopK = 4;          // per-term K-th best scores kept for these K

@@ -111,10 +111,11 @@ __device__ inline void wave_append(bool keep, uint64_t key, uint64_t* list, uint
 
 // Exact k-th largest over a set of unique 64-bit keys (visited by `each`,
 // which calls its argument once per key): returns T with exactly K keys >= T.
-// 11-bit radix digits from the top; stops as soon as the digit holding the
+// Bits-wide radix digits from the top; stops as soon as the digit holding the
 // K-th key is taken whole.  Requires more than K keys.
-template <class Each>
+template <uint32_t Bits = kHistBits, class Each>
 __device__ uint64_t select_kth(uint32_t K, uint32_t* hist, uint32_t* scratch, Each each) {
+  constexpr uint32_t kBins = 1u << Bits;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   // Skip the bits every key shares (scores of one query cluster: the sign,
   // exponent and top mantissa bits are mostly equal).  Digits then start at
@@ -140,28 +141,30 @@ __device__ uint64_t select_kth(uint32_t K, uint32_t* hist, uint32_t* scratch, Ea
   uint64_t prefix = top >= 64 ? 0 : (kand & (~0ull << top));
   uint32_t need = K;
   while (top > 0) {
-    const int width = top < 11 ? top : 11;
+    const int width = top < (int)Bits ? top : (int)Bits;
     const int sh = top - width;
-    for (uint32_t i = tid; i < kHistBins; i += kThreads) hist[i] = 0;
+    for (uint32_t i = tid; i < kBins; i += kThreads) hist[i] = 0;
     __syncthreads();
     each([&](uint64_t k) {
       if (top >= 64 || (k >> top) == (prefix >> top)) atomicAdd(&hist[(uint32_t)(k >> sh) & ((1u << width) - 1)], 1u);
     });
     __syncthreads();
-    // thread t owns digits [2047-8t-7, 2047-8t] in descending order
-    uint32_t local[8], s = 0;
+    // thread t owns digits [bins-1-D*t-(D-1), bins-1-D*t] in descending order
+    constexpr uint32_t D = kBins / kThreads;
+    static_assert(D * kThreads == kBins, "whole digits per thread");
+    uint32_t local[D], s = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      local[i] = hist[kHistBins - 1 - (tid * 8 + i)];
+    for (uint32_t i = 0; i < D; ++i) {
+      local[i] = hist[kBins - 1 - (tid * D + i)];
       s += local[i];
     }
     const uint32_t before = block_exclusive_scan(s, scratch);
     if (before < need && before + s >= need) {
       uint32_t c = before;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (uint32_t i = 0; i < D; ++i) {
         if (c < need && c + local[i] >= need) {
-          scratch[4] = kHistBins - 1 - (tid * 8 + i);
+          scratch[4] = kBins - 1 - (tid * D + i);
           scratch[5] = need - c;
           scratch[6] = local[i];
         }
@@ -231,7 +234,7 @@ static_assert(kTrunc + kDeferCap <= kBuf, "a flush after truncation must fit the
 
 struct ConjShared {
   alignas(16) uint64_t buf[kBuf];
-  uint32_t hist[kHistBins];
+  uint32_t hist[1u << kConjHistBits];
   uint32_t scratch[8];
   uint32_t n_buf;
   uint64_t thr;
@@ -254,11 +257,11 @@ struct ConjShared {
 #endif
 
 // Keep exactly the K largest of buf[0, n) at the front (n <= Cap); returns the K-th key.
-template <uint32_t Cap>
+template <uint32_t Cap, uint32_t Bits = kHistBits>
 __device__ uint64_t truncate_keys(uint64_t* buf, uint32_t* n_buf, uint32_t* hist, uint32_t* scratch, uint32_t n,
                                   uint32_t K) {
   const uint32_t tid = threadIdx.x;
-  const uint64_t T = select_kth(K, hist, scratch, [&](auto&& f) {
+  const uint64_t T = select_kth<Bits>(K, hist, scratch, [&](auto&& f) {
     for (uint32_t i = tid; i < n; i += kThreads) f(buf[i]);
   });
   constexpr uint32_t R = Cap / kThreads;
@@ -278,7 +281,7 @@ __device__ uint64_t truncate_keys(uint64_t* buf, uint32_t* n_buf, uint32_t* hist
 }
 
 __device__ inline uint64_t truncate_topk(ConjShared& sh, uint32_t n, uint32_t K) {
-  return truncate_keys<kBuf>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+  return truncate_keys<kBuf, kConjHistBits>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
 }
 
 // Append the kept keys of buf[0, n) that clear `cur` to query q's candidate list.
