@@ -517,9 +517,6 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
         if ((live & (1u << j)) && !filter_bits(fmask, fshift, doc[j])) live &= ~(1u << j);
     }
     FG_COUNT(0, live);
-#ifdef FG_DIAG
-    const uint32_t live0 = live;
-#endif
     if (!prune) FG_COUNT(7, live);  // candidates of chunks that start with no threshold
     if (prune) {
       const float ub = qub[1] + fmax;
@@ -530,22 +527,24 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     FG_COUNT(1, live);
 #ifdef FG_DIAG
     {
-      // block-max headroom: rows (wave, item j = 64 consecutive lead postings)
-      // with loaded candidates, rows the first bound prunes whole (slot 6), and
-      // chunks it prunes whole (slot 4); slots 4-6 then no longer count probes
-      uint32_t rows = 0, dead = 0;
+      // tile-bound headroom (slot 6): candidates alive after the first bound
+      // that the other lists' 4096-doc tile maxima, in place of their global
+      // maxima, would drop; slots 4-6 then no longer count probes
+      uint32_t extra = 0;
+      if (prune) {
 #pragma unroll
-      for (uint32_t j = 0; j < kItems; ++j) {
-        const bool l0 = __ballot((live0 >> j) & 1u) != 0, l1 = __ballot((live >> j) & 1u) != 0;
-        rows += l0 ? 1u : 0u;
-        dead += (l0 && !l1) ? 1u : 0u;
+        for (uint32_t j = 0; j < kItems; ++j) {
+          if (!((live >> j) & 1u)) continue;
+          float ub = fmax;
+          for (uint32_t i = 1; i < m; ++i) {
+            const uint32_t t = terms[i], to = ix.toff[t];
+            ub += to != kInvalid ? ix.tmax[to + (doc[j] >> kDisjTileShift)] : ix.tmaxs[t];
+          }
+          if (make_key(inflate_bound(s0[j] + ub), doc[j]) < thr) ++extra;
+        }
       }
-      if (lane == 0) {
-        atomicAdd(&sh.dgc[5], (unsigned long long)rows);
-        atomicAdd(&sh.dgc[6], (unsigned long long)dead);
-      }
-      const int any_live = __syncthreads_or(live != 0), any_loaded = __syncthreads_or(live0 != 0);
-      if (tid == 0 && any_loaded && !any_live) sh.dgc[4] += 1;
+      for (int o = 32; o > 0; o >>= 1) extra += (uint32_t)__shfl_xor((int)extra, o, 64);
+      if (lane == 0) atomicAdd(&sh.dgc[6], (unsigned long long)extra);
     }
 #endif
 

@@ -58,9 +58,8 @@ def main():
             "written_total": int(conj[:, 7].sum()),
             # candidates alive at: lead load, after the first MaxScore bound, after probe i
             "alive_lead_b1_p1_p2": [int(conj[:, 8 + i].sum()) for i in range(4)], "lead_unpruned": int(conj[:, 15].sum()),
-            # block-max headroom: 64-posting rows / whole chunks the first bound prunes entirely
-            "rows_loaded": int(conj[:, 13].sum()), "rows_pruned_by_b1": int(conj[:, 14].sum()),
-            "chunks_pruned_by_b1": int(conj[:, 12].sum()),
+            # tile-bound headroom: candidates past the first bound that tile maxima would drop
+            "b1_extra_pruned_by_tile_maxima": int(conj[:, 14].sum()),
         },
     }
     f_start, f_read, f_sel, f_end = (fin[:, i].astype(np.int64) for i in range(4))
