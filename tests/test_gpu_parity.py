@@ -439,3 +439,40 @@ def test_single_list_block_max_vs_oracle(native, ctx, gpu_1m, oracle_1m, k):
     assert np.array_equal(n, rn)
     for i in range(len(terms)):
         assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], ("deletes", k, int(terms[i])))
+
+
+@pytest.mark.parametrize("env", [{"FUGU_RANK_GIB": "0"}, {"FUGU_RANK_GIB": "0.02"},
+                                 {"FUGU_RANK_GIB": "0", "FUGU_DENSE_GIB": "0.5"},
+                                 {"FUGU_RANK_GIB": "0.02", "FUGU_DENSE_GIB": "0.05"}],
+                         ids=["directory_only", "few_rank_terms", "f32_tables", "mixed_kinds"])
+def test_probe_structure_budgets_vs_oracle(native, ctx, corpus_1m, oracle_1m, env):
+    """Every probe kind gives the oracle's results: the bucket directory alone
+    (no rank words), a budget that fits only the densest terms' rank words, the
+    f32 score tables, and both dense kinds at once (fg_internal.h DevIndex)."""
+    import os
+    from fugu_amd import synth
+    old = {k: os.environ.get(k) for k in ("FUGU_RANK_GIB", "FUGU_DENSE_GIB")}
+    os.environ.update(env)
+    try:
+        ix = native.Index.from_docs(ctx, corpus_1m.off, corpus_1m.tok, 1 << 20, threads=16)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    st = ix.stats()
+    if env.get("FUGU_RANK_GIB") == "0":
+        assert st.n_rank_terms == 0
+    else:
+        assert 0 < st.n_rank_terms < 2000
+    assert (st.n_dense_f32 > 0) == ("FUGU_DENSE_GIB" in env)
+    for (m0, m1, k, mode) in [(3, 3, 100, native.MODE_AND), (1, 5, 1000, native.MODE_AND),
+                              (2, 4, 1000, native.MODE_OR)]:
+        q_off, terms = synth.queries(256, m0, m1, seed_q=55)
+        s, d, n = ix.search_batch(q_off, terms, k, mode=mode)
+        rs, rd, rn, _, _ = oracle_1m.search_batch(q_off, terms, k, mode=mode, threads=16)
+        assert np.array_equal(n, rn)
+        for i in range(len(q_off) - 1):
+            assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], (env, m0, m1, k, mode, i))
+    ix.close()

@@ -44,8 +44,16 @@ def main():
     dur = (c_end - c_start) * us
     t0 = c_start.min()
     nchk = (conj[:, 6] >> np.uint64(40)).astype(np.int64)
+    # occupancy over time: the tail where fewer than half of the resident
+    # workgroup slots (4 per CU x 256 CUs) are busy
+    ev = np.concatenate([np.stack([c_start, np.ones_like(c_start)], 1), np.stack([c_end, -np.ones_like(c_end)], 1)])
+    ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+    act = np.cumsum(ev[:, 1])
+    busy = np.nonzero(act >= 512)[0]
+    tail_us = float((c_end.max() - ev[busy[-1], 0]) * 1e-2) if len(busy) else None
     out = {
         "k_conj": {
+            "tail_us_below_half_slots": tail_us, "max_active_wgs": int(act.max()),
             "work_items": int(len(conj)),
             "chunks": int(nchk.sum()),
             "span_us": round(float((c_end.max() - t0) * us), 1),
