@@ -851,6 +851,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #ifdef FG_DIAG
   const uint64_t dg_t0 = FG_NOW();
   uint64_t dg_mode[3] = {0, 0, 0}, dg_post = 0, dg_cand = 0, dg_trunc = 0, dg_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg_b1 = 0;  // postings past bound 1 (this thread's)
   uint64_t ph = dg_t0;
 #define FG_PHASE(slot) do { const uint64_t n_ = FG_NOW(); dg_ph[slot] += n_ - ph; ph = n_; } while (0)
 #else
@@ -1095,6 +1096,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
       if (pk[j] && fmask) pk[j] = filter_bits(fmask, fshift, pd[j]) != 0;
       ess[j] = sh.t_ess[pt[j]];
+#ifdef FG_DIAG
+      dg_b1 += pk[j] ? 1u : 0u;
+#endif
     }
     // bound 2: every clause at d in clause order -- the exact score from a dense
     // structure (-1.0: absent), else the bucket maximum (-0.0: empty bucket).
@@ -1308,7 +1312,15 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
   FG_STAMP(w, 3, dg_mode[1]);
   FG_STAMP(w, 4, dg_mode[2]);
   FG_STAMP(w, 5, dg_post);
-  FG_STAMP(w, 6, dg_cand);
+  {
+    // postings past bound 1, summed over the workgroup (scratch is free after the flush)
+    __syncthreads();
+    if (tid == 0) sh.scratch[0] = 0;
+    __syncthreads();
+    atomicAdd(&sh.scratch[0], (uint32_t)dg_b1);
+    __syncthreads();
+    FG_STAMP(w, 6, ((uint64_t)sh.scratch[0] << 32) | (dg_cand & 0xFFFFFFFFull));
+  }
   FG_STAMP(w, 7, (dg_trunc << 32) | q);
   for (uint32_t i = 0; i < 8; ++i) FG_STAMP(w, 8 + i, dg_ph[i]);
 #endif

@@ -43,7 +43,8 @@ def main():
         "work_items": int(len(wg)),
         "tiles_skip": int(wg[:, 2].sum()), "tiles_exact": int(wg[:, 3].sum()), "tiles_filter": int(wg[:, 4].sum()),
         "postings_scattered": int(wg[:, 5].sum()), "postings_total": int(dfs.sum()),
-        "candidates_probed": int(wg[:, 6].sum()), "truncations": int((wg[:, 7] >> 32).sum()),
+        "candidates_probed": int((wg[:, 6] & np.uint64(0xFFFFFFFF)).sum()),
+        "postings_past_bound1": int((wg[:, 6] >> np.uint64(32)).sum()), "truncations": int((wg[:, 7] >> 32).sum()),
         "wg_us": {p: round(float(np.percentile(dt, p)), 1) for p in (50, 90, 99, 100)},
         "wg_us_sum_ms": round(float(dt.sum()) * 1e-3, 1),
         "phase_ms_sum_over_wgs": {nm: round(float(wg[:, 8 + i].sum()) * 1e-5, 1) for i, nm in enumerate(
