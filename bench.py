@@ -571,7 +571,9 @@ def main():
                              f"{args.docs // 1_000_000}M-doc Zipf s=1.0 corpus per namespace, batch {nq}"),
                 "n_docs": args.docs, "vocab": synth.VOCAB, "batch": nq, "k": K,
                 "terms": wl_terms, "namespaces": world,
-                "parallelism": f"namespace-shard x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
+                "parallelism": f"namespace-shard x{world}" + (
+                    (" + RCCL all-gather top-k" if backend == "nccl" else f" + {backend} all-gather top-k (rehearsal)")
+                    if world > 1 else ""),
             },
             "p50_ms": round(p50_ms, 4) if p50_ms is not None else None,
             "roofline": {
