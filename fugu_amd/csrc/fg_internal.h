@@ -47,9 +47,13 @@ constexpr uint32_t kRankDiv = FG_RANK_DIV;    // terms in >= 1/kRankDiv of the d
 constexpr uint64_t kRankBudget = (uint64_t)FG_RANK_GIB << 30;    // ... densest first, within this many bytes
 constexpr uint32_t kMaxDense = 32767;     // slots per kind (tmeta bits 16-30)
 constexpr uint32_t kRankChunkWords = 2048;  // k_rank: words (65536 docs) per workgroup
-constexpr uint32_t kGroupsPerQuery = 64;  // a query's chunks are split into ~this many work items
+constexpr uint32_t kGroupsPerQuery = 64;  // k_disj / k_scan: a query's doc tiles in ~this many work items
+#ifndef FG_GPQ
+#define FG_GPQ 16  // tools/ab_variants.py (ab_group*.log): 64 -> 16 with FG_MAXGROUP 16 -> 8: k_conj 1.08 -> 1.00 ms
+#endif
+constexpr uint32_t kConjGroupsPerQuery = FG_GPQ;  // k_conj: a query's lead chunks in ~this many work items
 #ifndef FG_MAXGROUP
-#define FG_MAXGROUP 16
+#define FG_MAXGROUP 8
 #endif
 constexpr uint32_t kMaxGroup = FG_MAXGROUP;  // ... of at most this many chunks each
 #ifndef FG_HIST_BITS

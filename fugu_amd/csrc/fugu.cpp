@@ -1427,7 +1427,8 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     if (items.size() + nchunk[i] > 0x7FFFFFFFull)
       return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", items.size());
     const uint32_t nch = nchunk[i];
-    const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
+    const uint32_t G = std::min<uint32_t>(
+        fg::kMaxGroup, std::max<uint32_t>(1, (nch + fg::kConjGroupsPerQuery - 1) / fg::kConjGroupsPerQuery));
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;
     for (uint32_t g = 0; g < ng; ++g)

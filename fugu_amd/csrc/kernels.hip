@@ -1456,12 +1456,23 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
   const uint64_t T0 = pl.thresh[q];
   const uint32_t cnt = pl.cand_cnt[q];
   const uint64_t* src = pl.cand_keys + pl.cand_off[q];
-  // every candidate of query q, f(key >= lb, key) with the whole workgroup converged
+  // every candidate of query q, f(key >= lb, key) with the whole workgroup
+  // converged; eight loads per thread in flight per round (the list is read
+  // once per pass and the passes are latency-bound)
   auto each_key = [&](uint64_t lb, auto&& f) {
-    for (uint32_t i0 = 0; i0 < cnt; i0 += kThreads) {
-      const uint32_t i = i0 + tid;
-      const uint64_t key = i < cnt ? src[i] : 0;
-      f(i < cnt && key >= lb, key);
+    constexpr uint32_t U = 8;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += U * kThreads) {
+      uint64_t key[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * kThreads + tid;
+        key[u] = i < cnt ? src[i] : 0;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * kThreads + tid;
+        f(i < cnt && key[u] >= lb, key[u]);
+      }
     }
   };
   if (tid == 0) { sh.n_keys = 0; sh.n_win = 0; }
