@@ -47,7 +47,10 @@ constexpr uint32_t kRankDiv = FG_RANK_DIV;    // terms in >= 1/kRankDiv of the d
 constexpr uint64_t kRankBudget = (uint64_t)FG_RANK_GIB << 30;    // ... densest first, within this many bytes
 constexpr uint32_t kMaxDense = 32767;     // slots per kind (tmeta bits 16-30)
 constexpr uint32_t kRankChunkWords = 2048;  // k_rank: words (65536 docs) per workgroup
-constexpr uint32_t kGroupsPerQuery = 64;  // k_disj / k_scan: a query's doc tiles in ~this many work items
+#ifndef FG_DISJ_GPQ
+#define FG_DISJ_GPQ 64
+#endif
+constexpr uint32_t kGroupsPerQuery = FG_DISJ_GPQ;  // k_disj / k_scan: a query's doc tiles in ~this many work items
 #ifndef FG_GPQ
 #define FG_GPQ 16  // tools/ab_variants.py (ab_group*.log): 64 -> 16 with FG_MAXGROUP 16 -> 8: k_conj 1.08 -> 1.00 ms
 #endif
@@ -63,7 +66,10 @@ constexpr uint32_t kHistBits = 11;                 // radix digit width of the L
 constexpr uint32_t kHistBins = 1u << kHistBits;
 constexpr uint32_t kConjHistBits = FG_HIST_BITS;   // ... k_conj's (its LDS sets its occupancy)
 constexpr uint32_t kDisjTileShift = 12;   // k_disj: 4096-doc tiles
-constexpr uint32_t kDisjMaxGroup = 32;    // ... at most this many tiles per work item
+#ifndef FG_DISJ_MAXGROUP
+#define FG_DISJ_MAXGROUP 32
+#endif
+constexpr uint32_t kDisjMaxGroup = FG_DISJ_MAXGROUP;  // ... at most this many tiles per work item
 constexpr uint32_t kNumTopK = 4;          // per-term K-th best scores kept for these K
 constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 100, 1000};
 
