@@ -1755,26 +1755,47 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
 // starting threshold).  One workgroup per term with postings; exact select
 // over unique (score, doc) keys.
 __global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
+  constexpr uint32_t KM = kTopKs[kNumTopK - 1];  // the largest K: its keys are kept in LDS
   __shared__ uint32_t hist[kHistBins];
   __shared__ uint32_t scratch[8];
   __shared__ uint32_t red[2];  // alive postings, smallest alive score (bits)
+  __shared__ uint64_t top[KM];
+  __shared__ uint32_t n_top;
   const uint32_t t = j.kt_terms[blockIdx.x];
   const uint64_t b = j.off[t];
   const uint32_t n = (uint32_t)(j.off[t + 1] - b);
   auto alive = [&](uint32_t d) { return !j.alive || ((j.alive[d >> 5] >> (d & 31u)) & 1u); };
+  // every posting as (valid && alive, key), U loads per thread in flight, the
+  // workgroup converged (callers may use wave-wide operations)
+  auto each_posting = [&](auto&& f) {
+    constexpr uint32_t U = 4;
+    for (uint32_t p0 = 0; p0 < n; p0 += U * kThreads) {
+      uint32_t d[U];
+      float s[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t p = p0 + u * kThreads + threadIdx.x;
+        d[u] = p < n ? j.doc[b + p] : 0xFFFFFFFFu;
+        s[u] = p < n ? j.psc[b + p] : 0.0f;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) f(d[u] != 0xFFFFFFFFu && alive(d[u]), s[u], d[u]);
+    }
+  };
   if (threadIdx.x == 0) {
     red[0] = 0;
     red[1] = 0xFFFFFFFFu;
+    n_top = 0;
   }
   __syncthreads();
   uint32_t c = 0, mx = 0, mn = 0xFFFFFFFFu;
-  for (uint32_t p = threadIdx.x; p < n; p += kThreads) {
-    if (!alive(j.doc[b + p])) continue;
-    const uint32_t bits = __float_as_uint(j.psc[b + p]);
+  each_posting([&](bool ok, float sv, uint32_t) {
+    if (!ok) return;
+    const uint32_t bits = __float_as_uint(sv);
     ++c;
     mx = max(mx, bits);
     mn = min(mn, bits);
-  }
+  });
   for (int o = 32; o > 0; o >>= 1) {
     c += (uint32_t)__shfl_xor((int)c, o, 64);
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
@@ -1787,20 +1808,35 @@ __global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
   }
   __syncthreads();
   const uint32_t na = red[0];
+  if (na < kTopKs[1]) return;  // uniform: only K = 1
+  // the KM best alive keys (all of them when there are no more) into LDS: one
+  // select over the whole list, the smaller K then select inside LDS
+  uint64_t T = 0;
+  if (na > KM) {
+    T = select_kth(KM, hist, scratch, [&](auto&& f) {
+      each_posting([&](bool ok, float sv, uint32_t d) { if (ok) f(make_key(sv, d)); });
+    });
+  }
+  each_posting([&](bool ok, float sv, uint32_t d) {
+    const uint64_t key = make_key(sv, d);
+    wave_append(ok && key >= T, key, top, &n_top, KM);
+  });
+  __syncthreads();
+  const uint32_t nt = min(na, KM);  // keys in top[] (unique: exactly KM are >= T)
   for (uint32_t kk = 1; kk < kNumTopK; ++kk) {
     const uint32_t K = kTopKs[kk];
-    if (na < K) break;  // uniform
-    if (na == K) {      // every alive key is in: the minimum
-      if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = __uint_as_float(red[1]);
-      continue;
+    if (nt < K) break;  // uniform
+    float v;
+    if (na == K) {
+      v = __uint_as_float(red[1]);  // every alive key is in: the minimum
+    } else if (K == KM) {
+      v = key_score(T);
+    } else {
+      v = key_score(select_kth(K, hist, scratch, [&](auto&& f) {
+        for (uint32_t i = threadIdx.x; i < nt; i += kThreads) f(top[i]);
+      }));
     }
-    const uint64_t T = select_kth(K, hist, scratch, [&](auto&& f) {
-      for (uint32_t p = threadIdx.x; p < n; p += kThreads) {
-        const uint32_t d = j.doc[b + p];
-        if (alive(d)) f(make_key(j.psc[b + p], d));
-      }
-    });
-    if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = key_score(T);
+    if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = v;
   }
 }
 
