@@ -328,6 +328,33 @@ int dev_upload(DevAllocs& m, const T* src, size_t n, T** out, uint64_t* bytes) {
   return FG_OK;
 }
 
+// Several host arrays into ONE device allocation (one hipMalloc instead of one
+// per array: a small segment's build is otherwise dominated by allocation).
+struct UploadBatch {
+  struct E { const void* src; size_t bytes; void** out; };
+  std::vector<E> es;
+  size_t total = 0;
+  template <class T>
+  void add(const T* src, size_t n, T** out) {
+    es.push_back(E{src, n * sizeof(T), reinterpret_cast<void**>(out)});
+    total += (std::max<size_t>(n * sizeof(T), 16) + 255) & ~size_t(255);
+  }
+  int commit(DevAllocs& m, uint64_t* bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(total, 256)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", total);
+    m.ptrs.push_back(p);
+    size_t o = 0;
+    for (const E& e : es) {
+      char* d = static_cast<char*>(p) + o;
+      if (e.bytes) HIPCHK(hipMemcpy(d, e.src, e.bytes, hipMemcpyHostToDevice));
+      *e.out = d;
+      o += (std::max<size_t>(e.bytes, 16) + 255) & ~size_t(255);
+    }
+    *bytes += total;
+    return FG_OK;
+  }
+};
+
 int check_device(int dev) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(FG_ENODEV, "no HIP device visible");
@@ -539,8 +566,22 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     nd += nbk + 1;
   }
   std::vector<uint32_t> dir(nd);
-  parallel_dynamic(V, hw_threads(0), 1, [&](int, uint32_t tb, uint32_t te) {
-    for (uint32_t t = tb; t < te; ++t) {
+  // term ranges of about equal work (postings + a per-term constant): a million
+  // mostly empty terms of a small segment cost one range grab per range, not
+  // one per term, and the densest terms still spread over the threads
+  std::vector<uint32_t> cuts{0};
+  {
+    const int nth = hw_threads(0);
+    const uint64_t tot = hp.off[V] + 64ull * V, step = std::max<uint64_t>(1, tot / (uint64_t)(nth * 16));
+    uint64_t acc = 0;
+    for (uint32_t t = 0; t < V; ++t) {
+      acc += (hp.off[t + 1] - hp.off[t]) + 64;
+      if (acc >= step) { cuts.push_back(t + 1); acc = 0; }
+    }
+    if (cuts.back() != V) cuts.push_back(V);
+  }
+  parallel_dynamic((uint32_t)cuts.size() - 1, hw_threads(0), 1, [&](int, uint32_t rb, uint32_t re) {
+    for (uint32_t t = cuts[rb]; t < cuts[re]; ++t) {
       const uint64_t b0 = hp.off[t], n = hp.off[t + 1] - b0;
       const uint32_t B = tmeta[t];
       const uint64_t nbk = ((N - 1) >> B) + 1;
@@ -594,24 +635,28 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
   uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt, *d_coff;
-  if ((rc = dev_upload(sm, hp.doc.data(), hp.doc.size(), &d_doc, &bytes))) return rc;
-  if ((rc = dev_upload(sm, hp.tf.data(), hp.tf.size(), &d_tfp, &bytes))) return rc;
+  {
+    UploadBatch ub;
+    ub.add(hp.doc.data(), hp.doc.size(), &d_doc);
+    ub.add(hp.tf.data(), hp.tf.size(), &d_tfp);
+    ub.add(hp.fn_text.data(), hp.fn_text.size(), &d_fnt);
+    if (hp.has_name) ub.add(hp.fn_name.data(), hp.fn_name.size(), &d_fnn);
+    ub.add(hp.off.data(), hp.off.size(), &d_off);
+    ub.add(dir.data(), dir.size(), &d_dir);
+    ub.add(dir_off.data(), dir_off.size(), &d_dir_off);
+    ub.add(toff.data(), toff.size(), &d_toff);
+    ub.add(hp.fdoc.data(), hp.fdoc.size(), &d_fdoc);
+    ub.add(hp.foff.data(), hp.foff.size(), &d_foff);
+    ub.add(sc_t.data(), sc_t.size(), &d_sct);
+    ub.add(sc_f.data(), sc_f.size(), &d_scf);
+    ub.add(bk_t.data(), bk_t.size(), &d_bkt);
+    ub.add(bk_f.data(), bk_f.size(), &d_bkf);
+    ub.add(kt.data(), kt.size(), &d_kt);
+    ub.add(coff.data(), coff.size(), &d_coff);
+    if ((rc = ub.commit(sm, &bytes))) return rc;
+  }
   std::vector<uint32_t>().swap(hp.tf);
-  if ((rc = dev_upload(sm, hp.fn_text.data(), hp.fn_text.size(), &d_fnt, &bytes))) return rc;
-  if (hp.has_name && (rc = dev_upload(sm, hp.fn_name.data(), hp.fn_name.size(), &d_fnn, &bytes))) return rc;
-  if ((rc = dev_upload(sm, hp.off.data(), hp.off.size(), &d_off, &bytes))) return rc;
-  if ((rc = dev_upload(sm, dir.data(), dir.size(), &d_dir, &bytes))) return rc;
   std::vector<uint32_t>().swap(dir);
-  if ((rc = dev_upload(sm, dir_off.data(), dir_off.size(), &d_dir_off, &bytes))) return rc;
-  if ((rc = dev_upload(sm, toff.data(), toff.size(), &d_toff, &bytes))) return rc;
-  if ((rc = dev_upload(sm, hp.fdoc.data(), hp.fdoc.size(), &d_fdoc, &bytes))) return rc;
-  if ((rc = dev_upload(sm, hp.foff.data(), hp.foff.size(), &d_foff, &bytes))) return rc;
-  if ((rc = dev_upload(sm, sc_t.data(), sc_t.size(), &d_sct, &bytes))) return rc;
-  if ((rc = dev_upload(sm, sc_f.data(), sc_f.size(), &d_scf, &bytes))) return rc;
-  if ((rc = dev_upload(sm, bk_t.data(), bk_t.size(), &d_bkt, &bytes))) return rc;
-  if ((rc = dev_upload(sm, bk_f.data(), bk_f.size(), &d_bkf, &bytes))) return rc;
-  if ((rc = dev_upload(sm, kt.data(), kt.size(), &d_kt, &bytes))) return rc;
-  if ((rc = dev_upload(sm, coff.data(), coff.size(), &d_coff, &bytes))) return rc;
   g_bt.mark("upload");
   // rank words for the densest terms (fg_internal.h DevIndex), chosen AFTER the
   // uploads above so the budget sees the memory actually left: df >= N /
