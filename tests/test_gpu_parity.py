@@ -152,8 +152,12 @@ def test_plan_reuse_profile_and_bytes_model(native, gpu_1m, oracle_1m):
     p.execute()
     p.execute()
     b = p.results()
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
+    # a replayed plan gives the same hits; slots past n[i] are unspecified
+    assert np.array_equal(a[2], b[2])
+    for i in range(len(a[2])):
+        m = int(a[2][i])
+        assert np.array_equal(a[0][i, :m], b[0][i, :m]) and np.array_equal(a[1][i, :m], b[1][i, :m]), (
+            i, m, np.nonzero(a[0][i, :m] != b[0][i, :m])[0][:8], np.nonzero(a[1][i, :m] != b[1][i, :m])[0][:8])
     ms, cnt = p.kernel_ms()
     assert cnt == 3 and ms[0] > 0
     bm = gpu_1m.bytes_model(q_off, terms, 100)
