@@ -155,6 +155,21 @@ def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
                     "hits, pipelined over the workers' streams (planning overlaps other batches' kernels)"}
 
 
+def merge_ms(gs, gd, gn, nq, K, torch, reps=20):
+    """Device time of one fg_merge_shards call on the gathered lists (torch's
+    current stream, where merge_on_device launches it)."""
+    from fugu_amd.shard import merge_on_device
+    st = torch.cuda.current_stream(gs.device)
+    merge_on_device(gs, gd, gn, nq, K, st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        merge_on_device(gs, gd, gn, nq, K, st.cuda_stream)
+    e1.record(st)
+    e1.synchronize()
+    return round(e0.elapsed_time(e1) / reps, 4)
+
+
 def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads):
     """C4 (BASELINE configs[3]) on one GPU: the 10M docs as 8 namespaces x
     1.25M, each its own index and statistics; a step = one fan-out 3-term AND
@@ -188,12 +203,13 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
     el = timed_steps(step, steps, warmup, torch)
     kms = [p.kernel_ms() for p in plans]
     per_ns = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
+    mms = merge_ms(gs, gd, gn, nq, K, torch)
     del plans
     for ix in ixs:
         ix.close()
     return {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
             "batch": nq, "k": K, "terms": 3, "mode": "AND", "namespaces": 8, "docs_per_namespace": ranges[0][1],
-            "k_conj_ms_per_namespace": per_ns, "snapshot_build_s": round(build_s, 1),
+            "k_conj_ms_per_namespace": per_ns, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
             "workload": "C4: 10M docs as 8 namespaces x 1.25M (own statistics each), fan-out 3-term AND top-100 "
                         "on all 8 + device merge, all 8 namespaces on this one GPU",
             "projected_8gpu": "each GPU runs one namespace: step ~ max(k_conj_ms_per_namespace) + k_final + gather"}
@@ -245,9 +261,10 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     el = timed_steps(step, steps, warmup, torch)
     kms = [p.kernel_ms() for p in plans]
     per_shard = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
+    mms = merge_ms(gs, gd, gn, nq, K, torch)
     ent = {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
            "batch": nq, "k": K, "terms": "2-5", "mode": "OR", "n_docs": N, "zipf_s": S, "shards": 8,
-           "k_disj_ms_per_shard": per_shard, "snapshot_build_s": round(build_s, 1),
+           "k_disj_ms_per_shard": per_shard, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
            "workload": "C5: 100M docs s=1.1 as 8 doc shards with global BM25 statistics, 2-5-term OR top-1000 on "
                        "all 8 + device merge, all 8 shards on this one GPU",
            "projected_8gpu": "each GPU runs one shard: step ~ max(k_disj_ms_per_shard) + k_final + gather"}

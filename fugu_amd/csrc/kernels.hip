@@ -1524,8 +1524,78 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
 
 // ---------------------------------------------------------------- k_merge
 // Cross-shard merge of per-shard top-k lists (each in key order) into the
-// global top-k by (score desc, shard asc, doc asc): one lane per query walks
-// the n_shards heads (n_shards <= 64).
+// global top-k by (score desc, shard asc, doc asc).
+//
+// k_merge_rank: one workgroup per query.  The shards' scores go to LDS; every
+// entry (s, i) then finds its output position directly,
+//   pos = i + #{s' < s: score >= sc} + #{s' > s: score > sc},
+// by one binary search per other shard (the lists are score-descending, and
+// within a shard equal scores are already doc-ascending), and writes itself
+// when pos < k.  No serial walk: every entry of every shard in parallel.
+constexpr uint32_t kMergeCap = 12288;  // scores per query held in LDS (48 KB)
+
+__device__ inline uint32_t count_ge(const float* l, uint32_t c, float x) {  // l descending
+  uint32_t lo = 0, hi = c;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (l[mid] >= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ inline uint32_t count_gt(const float* l, uint32_t c, float x) {
+  uint32_t lo = 0, hi = c;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (l[mid] > x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kThreads) void k_merge_rank(uint32_t n_shards, uint32_t nq, uint32_t k,
+                                                          const float* __restrict__ score,
+                                                          const uint32_t* __restrict__ doc,
+                                                          const uint32_t* __restrict__ n, float* __restrict__ out_score,
+                                                          uint32_t* __restrict__ out_doc,
+                                                          uint32_t* __restrict__ out_shard,
+                                                          uint32_t* __restrict__ out_n) {
+  __shared__ float ls[kMergeCap];
+  __shared__ uint32_t cnt[65], off[65];
+  const uint32_t q = blockIdx.x, tid = threadIdx.x;
+  if (tid < n_shards) cnt[tid] = min(n[(size_t)tid * nq + q], k);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t o = 0;
+    for (uint32_t s = 0; s < n_shards; ++s) { off[s] = o; o += cnt[s]; }
+    off[n_shards] = o;
+  }
+  __syncthreads();
+  const uint32_t total = off[n_shards];
+  for (uint32_t s = 0; s < n_shards; ++s) {
+    const float* src = score + ((size_t)s * nq + q) * k;
+    for (uint32_t i = tid; i < cnt[s]; i += kThreads) ls[off[s] + i] = src[i];
+  }
+  __syncthreads();
+  for (uint32_t e = tid; e < total; e += kThreads) {
+    uint32_t s = 0;
+    while (off[s + 1] <= e) ++s;
+    const uint32_t i = e - off[s];
+    const float sc = ls[e];
+    uint32_t pos = i;
+    for (uint32_t t = 0; t < n_shards && pos < k; ++t) {
+      if (t == s) continue;
+      pos += t < s ? count_ge(ls + off[t], cnt[t], sc) : count_gt(ls + off[t], cnt[t], sc);
+    }
+    if (pos < k) {
+      out_score[(size_t)q * k + pos] = sc;
+      out_doc[(size_t)q * k + pos] = doc[((size_t)s * nq + q) * k + i];
+      if (out_shard) out_shard[(size_t)q * k + pos] = s;
+    }
+  }
+  if (tid == 0) out_n[q] = min(total, k);
+}
+
+// k_merge: the serial form (one lane per query walks the n_shards heads) for
+// merges whose lists do not fit k_merge_rank's LDS (n_shards x k > kMergeCap).
 __global__ __launch_bounds__(kThreads) void k_merge(uint32_t n_shards, uint32_t nq, uint32_t k,
                                                      const float* __restrict__ score, const uint32_t* __restrict__ doc,
                                                      const uint32_t* __restrict__ n, float* __restrict__ out_score,
@@ -1869,6 +1939,11 @@ hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s) {
   if (n_queries == 0) return hipSuccess;
+  if ((uint64_t)n_shards * k <= kMergeCap) {
+    k_merge_rank<<<n_queries, kThreads, 0, s>>>(n_shards, n_queries, k, score, doc, n, out_score, out_doc, out_shard,
+                                                 out_n);
+    return hipGetLastError();
+  }
   k_merge<<<(n_queries + kThreads - 1) / kThreads, kThreads, 0, s>>>(n_shards, n_queries, k, score, doc, n,
                                                                      out_score, out_doc, out_shard, out_n);
   return hipGetLastError();

@@ -168,11 +168,14 @@ def test_plan_reuse_profile_and_bytes_model(native, gpu_1m, oracle_1m):
     assert (a[2] == np.minimum(bm[:, 3], 100)).all()
 
 
-def test_merge_shards_matches_numpy(native):
+@pytest.mark.parametrize("S,nq,k,levels", [(4, 64, 10, 50), (8, 256, 100, 400), (8, 64, 1000, 6), (3, 32, 1000, 2000),
+                                           (64, 16, 300, 40), (1, 8, 100, 10)])
+def test_merge_shards_matches_numpy(native, S, nq, k, levels):
+    """k_merge_rank (parallel ranks, S x k <= 12288) and the serial k_merge
+    (64 x 300) vs the numpy merge, with heavy cross-shard score ties."""
     import torch
-    rng = np.random.default_rng(5)
-    S, nq, k = 4, 64, 10
-    sc = np.sort(rng.integers(0, 50, (S, nq, k)).astype(np.float32) / 8, axis=2)[:, :, ::-1].copy()
+    rng = np.random.default_rng(5 + S + k)
+    sc = np.sort(rng.integers(0, levels, (S, nq, k)).astype(np.float32) / 8, axis=2)[:, :, ::-1].copy()
     dc = rng.integers(0, 1000, (S, nq, k)).astype(np.uint32)
     # within a shard, equal scores must already be doc-ascending
     for s in range(S):
