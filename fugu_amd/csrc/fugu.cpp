@@ -305,8 +305,12 @@ struct fg_plan {
   ~fg_plan() {
     for (hipEvent_t e : pending) (void)hipEventDestroy(e);
     if (ws) {
-      // the workspace may still be read by this plan's last launch
-      if (last_stream_used) (void)hipStreamSynchronize(last_stream);
+      // the workspace may still be read by this plan's last launch (a per-thread
+      // stream handle resolves on the current device: select the plan's first)
+      if (last_stream_used) {
+        (void)hipSetDevice(ix->dev);
+        (void)hipStreamSynchronize(last_stream);
+      }
       ix->pool.put(ws, ws_got);
     }
     if (ix) fg_index_release(ix);
@@ -1708,6 +1712,113 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
     return fail(FG_EINVAL, "bad arguments");
   HIPCHK(fg::launch_merge(n_shards, n_queries, k, d_score, d_doc, d_n, d_out_score, d_out_doc, d_out_shard, d_out_n,
                           static_cast<hipStream_t>(stream)));
+  return FG_OK;
+}
+
+// One batch over several shards / segments / namespaces of one logical index
+// (SURVEY.md §8b fg_search_sharded, §8e): every shard is planned on its own
+// host thread, executed on its own device's per-thread stream, its top-k lists
+// copied over xGMI (hipMemcpyPeerAsync) to the first shard's device unless they
+// are already there, and merged there by k_merge_rank into (score desc, shard
+// asc, doc asc) -- tantivy's merge_fruits over DocAddress (segment_ord, doc).
+int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
+                      float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
+  if (!shards || n_shards == 0 || n_shards > 64 || !q || k == 0 || !out_score || !out_doc || !out_n)
+    return fail(FG_EINVAL, "bad arguments");
+  for (uint32_t s = 0; s < n_shards; ++s) {
+    if (!shards[s]) return fail(FG_EINVAL, "NULL shard");
+    if (ctx && std::find(ctx->devs.begin(), ctx->devs.end(), shards[s]->dev) == ctx->devs.end())
+      return fail(FG_EINVAL, "a shard lives on a device outside the context");
+  }
+  const uint32_t nq = q->n_queries;
+  if (nq == 0) return FG_OK;
+  // ---- plan every shard (host work: cost order, work items, plan upload)
+  std::vector<std::unique_ptr<fg_plan>> plans(n_shards);
+  std::vector<int> rcs(n_shards, FG_OK);
+  std::vector<std::string> errs(n_shards);
+  auto plan_range = [&](uint32_t a, uint32_t b) {
+    for (uint32_t s = a; s < b; ++s) {
+      fg_plan* p = nullptr;
+      rcs[s] = fg_plan_create(shards[s], q, k, &p);
+      plans[s].reset(p);
+      if (rcs[s]) errs[s] = fg_last_error();
+    }
+  };
+  // (a thread per shard group pays off only for batches; a single query plans inline)
+  const uint32_t nt = nq >= 64 ? std::min<uint32_t>(n_shards, 8) : 1;
+  if (nt > 1) {
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < nt; ++t)
+      th.emplace_back(plan_range, t * n_shards / nt, (t + 1) * n_shards / nt);
+    for (auto& x : th) x.join();
+  } else {
+    plan_range(0, n_shards);
+  }
+  for (uint32_t s = 0; s < n_shards; ++s)
+    if (rcs[s]) return fail(rcs[s], "shard %u: %s", s, errs[s].c_str());
+  // ---- gathered lists + merged output on the first shard's device (its pool)
+  const int dev0 = shards[0]->dev;
+  const size_t nk = (size_t)nq * k;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t g_s = al(4 * nk * n_shards), g_n = al(4ull * nq * n_shards), o_k = al(4 * nk), o_n = al(4ull * nq);
+  const size_t total = 2 * g_s + g_n + 3 * o_k + o_n;
+  size_t got = 0;
+  HIPCHK(hipSetDevice(dev0));
+  char* base = static_cast<char*>(shards[0]->pool.get(total, &got));
+  if (!base) return fail(FG_EOOM, "hipMalloc of the shard merge buffers failed");
+  // returned to the pool once every device's per-thread stream has drained
+  // (an early error return may leave launches or peer copies in flight)
+  struct Back {
+    fg_index* const* sh; uint32_t ns; void* p; size_t n;
+    ~Back() {
+      for (uint32_t s = 0; s < ns; ++s) {
+        (void)hipSetDevice(sh[s]->dev);
+        (void)hipStreamSynchronize(hipStreamPerThread);
+      }
+      sh[0]->pool.put(p, n);
+    }
+  } back{shards, n_shards, base, got};
+  float* gs = reinterpret_cast<float*>(base);
+  uint32_t* gd = reinterpret_cast<uint32_t*>(base + g_s);
+  uint32_t* gn = reinterpret_cast<uint32_t*>(base + 2 * g_s);
+  float* ms = reinterpret_cast<float*>(base + 2 * g_s + g_n);
+  uint32_t* md = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + o_k);
+  uint32_t* msh = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 2 * o_k);
+  uint32_t* mn = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 3 * o_k);
+  // ---- execute: shards on dev0 write straight into the gathered lists (same
+  // per-thread stream as the merge); the others copy theirs over xGMI and the
+  // merge stream waits for their events
+  std::vector<hipEvent_t> evs;
+  struct EvGuard {
+    std::vector<hipEvent_t>& v;
+    ~EvGuard() { for (hipEvent_t e : v) (void)hipEventDestroy(e); }
+  } evg{evs};
+  for (uint32_t s = 0; s < n_shards; ++s) {
+    fg_plan* p = plans[s].get();
+    const int d = shards[s]->dev;
+    if (d == dev0) {
+      int rc = fg_plan_execute(p, hipStreamPerThread, gs + s * nk, gd + s * nk, gn + (size_t)s * nq);
+      if (rc) return rc;
+      continue;
+    }
+    int rc = fg_plan_execute(p, hipStreamPerThread, nullptr, nullptr, nullptr);  // sets device d
+    if (rc) return rc;
+    HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score, d, 4 * nk, hipStreamPerThread));
+    HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc, d, 4 * nk, hipStreamPerThread));
+    HIPCHK(hipMemcpyPeerAsync(gn + (size_t)s * nq, dev0, p->own_n, d, 4ull * nq, hipStreamPerThread));
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    evs.push_back(e);
+    HIPCHK(hipEventRecord(e, hipStreamPerThread));
+  }
+  HIPCHK(hipSetDevice(dev0));
+  for (hipEvent_t e : evs) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
+  HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
+  if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(out_n, mn, 4ull * nq, hipMemcpyDeviceToHost, hipStreamPerThread));
+  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
   return FG_OK;
 }
 

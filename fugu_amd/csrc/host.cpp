@@ -723,35 +723,23 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
   }
   if (!snap) return FG_OK;  // nothing committed yet: no hits
   // every segment answers the query (TopDocs::with_limit(offset + per_page) per
-  // segment), then merge_fruits: (score desc, segment asc, doc asc) = (score
-  // desc, global doc asc), since segments hold ascending doc-id ranges
-  struct H { float s; uint32_t seg, doc; };
-  std::vector<H> all;
+  // segment), then merge_fruits on the device: (score desc, segment asc, doc
+  // asc) = (score desc, global doc asc), since segments hold ascending doc-id
+  // ranges.  Terms interned after a segment was built (ids >= its n_terms)
+  // match nothing there.
+  std::vector<fg_index*> segs;
+  for (const Segment& seg : snap->segs) segs.push_back(seg.ix);
+  const uint32_t q_off[2] = {0, (uint32_t)ids.size()};
+  const uint32_t f_off[2] = {0, (uint32_t)fids.size()};
+  fg_query_batch qb{1, q_off, ids.data(), mode, fids.empty() ? nullptr : f_off, fids.data()};
   std::vector<float> sc(limit);
-  std::vector<uint32_t> dc(limit);
-  for (uint32_t si = 0; si < snap->segs.size(); ++si) {
-    const Segment& seg = snap->segs[si];
-    // terms interned after a segment was built are unknown to it
-    fg_index_stats st;
-    fg_index_stats_get(seg.ix, &st);
-    std::vector<uint32_t> sid = ids, sfid = fids;
-    for (auto& t : sid)
-      if (t != FG_TERM_MISSING && t >= st.n_terms) t = FG_TERM_MISSING;
-    for (auto& t : sfid)
-      if (t != FG_TERM_MISSING && t >= st.n_facet_terms) t = FG_TERM_MISSING;
-    const uint32_t q_off[2] = {0, (uint32_t)sid.size()};
-    const uint32_t f_off[2] = {0, (uint32_t)sfid.size()};
-    fg_query_batch qb{1, q_off, sid.data(), mode, sfid.empty() ? nullptr : f_off, sfid.data()};
-    uint32_t n = 0;
-    int rc = fg_search_batch(seg.ix, &qb, (uint32_t)limit, sc.data(), dc.data(), &n);
-    if (rc) return hfail(rc, fg_last_error());
-    for (uint32_t i = 0; i < n; ++i) all.push_back(H{sc[i], si, seg.base + dc[i]});
-  }
-  std::stable_sort(all.begin(), all.end(), [](const H& a, const H& b) {
-    return a.s != b.s ? a.s > b.s : a.doc < b.doc;
-  });
-  const uint64_t n = std::min<uint64_t>(all.size(), limit);
-  for (uint64_t i = offset; i < n; ++i) hits.push_back(fg_hit{all[i].s, all[i].doc});  // skip(offset).take(per_page)
+  std::vector<uint32_t> dc(limit), sh(limit);
+  uint32_t n = 0;
+  int rc = fg_search_sharded(nullptr, segs.data(), (uint32_t)segs.size(), &qb, (uint32_t)limit, sc.data(), dc.data(),
+                             sh.data(), &n);
+  if (rc) return hfail(rc, fg_last_error());
+  for (uint64_t i = offset; i < n; ++i)  // skip(offset).take(per_page)
+    hits.push_back(fg_hit{sc[i], snap->segs[sh[i]].base + dc[i]});
   return FG_OK;
 }
 

@@ -47,7 +47,7 @@ EXPORTS = (
     "fg_index_stats_get", "fg_index_df", "fg_index_bm25",
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
-    "fg_search_batch", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
+    "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
 )
 
@@ -137,6 +137,8 @@ _sig("fg_plan_kernel_ms", C.c_int, _p, _f64p, _u32p)
 _sig("fg_plan_diag", C.c_int, _p, _u64p, C.c_size_t, _u32p)
 _sig("fg_plan_destroy", C.c_int, _p)
 _sig("fg_search_batch", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f32p, _u32p, _u32p)
+_sig("fg_search_sharded", C.c_int, _p, C.POINTER(_p), C.c_uint32, C.POINTER(QueryBatch), C.c_uint32, _f32p, _u32p,
+     _u32p, _u32p)
 _sig("fg_merge_shards", C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("fg_bytes_model", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f64p)
 _sig("fg_bytes_model_gpu", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f64p)
@@ -499,6 +501,26 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+def search_sharded(indexes, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None, ctx=None):
+    """fg_search_sharded: one batch over several shard / segment / namespace
+    indexes, merged on the first one's device by (score desc, shard asc, doc
+    asc).  Returns (score [nq,k], doc [nq,k], shard [nq,k], n [nq])."""
+    q_off = _u32(q_off)
+    terms = _u32(terms)
+    nq = len(q_off) - 1
+    f_off = None if f_off is None else _u32(f_off)
+    f_terms = None if f_off is None else _u32(f_terms)
+    qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode, _ptr(f_off, _u32p), _ptr(f_terms, _u32p))
+    hs = (_p * len(indexes))(*[ix._h for ix in indexes])
+    score = np.zeros(nq * k, np.float32)
+    doc = np.zeros(nq * k, np.uint32)
+    shard = np.zeros(nq * k, np.uint32)
+    n = np.zeros(nq, np.uint32)
+    _check(_lib.fg_search_sharded(ctx._h if ctx is not None else None, hs, len(indexes), C.byref(qb), k,
+                                  _ptr(score, _f32p), _ptr(doc, _u32p), _ptr(shard, _u32p), _ptr(n, _u32p)))
+    return score.reshape(nq, k), doc.reshape(nq, k), shard.reshape(nq, k), n
 
 
 def merge_shards(n_shards: int, n_queries: int, k: int, d_score: int, d_doc: int, d_n: int, d_out_score: int,

@@ -240,6 +240,22 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
                     const uint32_t* d_n, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_shard,
                     uint32_t* d_out_n, void* stream);
 
+/* One batch over the shards of one logical index (SURVEY.md §8b
+ * fg_search_sharded, §8e): the segments of a namespace (tantivy's per-commit
+ * segments, src/db/document.rs:65, searched and merged by
+ * searcher.search(.., TopDocs), src/db/search.rs:162), the doc shards of a
+ * namespace built with global statistics, or several namespaces of a fan-out
+ * query.  The shards share one term / facet dictionary; a term id >= a shard's
+ * n_terms matches nothing there.  Each shard runs on its own device (one
+ * process driving the node's GPUs; shards on the same device run back to back),
+ * its per-shard top-k is copied over xGMI to shards[0]'s device and merged there
+ * into (score desc, shard asc, doc asc) -- merge_fruits over (segment_ord, doc).
+ * Host outputs [n_queries*k] (out_shard may be NULL) and out_n [n_queries].
+ * ctx, when given, must hold every shard's device.  Thread-safe like
+ * fg_search_batch (the calling thread's per-thread streams). */
+int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
+                      float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n);
+
 /* SURVEY.md §8(d) algorithmic bytes per query: out[4*i..] = {B_merge, B_skip,
  * B, |I|}.  Host analysis over the host posting copy (keep_host_postings). */
 int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);

@@ -22,7 +22,7 @@ def header_functions(header="fugu.h"):
 def test_header_declares_the_abi():
     fns = header_functions()
     for f in ["fg_ctx_create", "fg_index_build_from_docs", "fg_index_build", "fg_plan_create", "fg_plan_execute",
-              "fg_search_batch", "fg_merge_shards", "fg_last_error", "fg_bytes_model"]:
+              "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_last_error", "fg_bytes_model"]:
         assert f in fns
 
 
@@ -65,6 +65,7 @@ def test_null_arguments_are_rejected():
     assert lib.fg_plan_create(None, None, 10, None) == native.FG_EINVAL
     assert lib.fg_index_stats_get(None, None) == native.FG_EINVAL
     assert lib.fg_merge_shards(0, 1, 1, None, None, None, None, None, None, None, None) == native.FG_EINVAL
+    assert lib.fg_search_sharded(None, None, 0, None, 10, None, None, None, None) == native.FG_EINVAL
     assert native.lib().fg_last_error()
 
 
