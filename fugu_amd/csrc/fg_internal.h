@@ -65,7 +65,10 @@ constexpr uint32_t kMaxGroup = FG_MAXGROUP;  // ... of at most this many chunks 
 constexpr uint32_t kHistBits = 11;                 // radix digit width of the LDS selects
 constexpr uint32_t kHistBins = 1u << kHistBits;
 constexpr uint32_t kConjHistBits = FG_HIST_BITS;   // ... k_conj's (its LDS sets its occupancy)
-constexpr uint32_t kDisjTileShift = 12;   // k_disj: 4096-doc tiles
+#ifndef FG_TILE_SHIFT
+#define FG_TILE_SHIFT 12
+#endif
+constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
 #endif
