@@ -155,6 +155,21 @@ def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
                     "hits, pipelined over the workers' streams (planning overlaps other batches' kernels)"}
 
 
+def fanout(plans, gs, gd, gn, streams, torch, dev):
+    """One fan-out step's shard executes: every shard's plan on its own stream
+    (the shards are independent, so one shard's tail overlaps the next one's
+    start), joined back into torch's current stream before the merge."""
+    main = torch.cuda.current_stream(dev)
+    ev = torch.cuda.Event()
+    ev.record(main)
+    for r, p in enumerate(plans):
+        s = streams[r % len(streams)]
+        s.wait_event(ev)
+        p.execute(s.cuda_stream, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+    for s in streams:
+        main.wait_stream(s)
+
+
 def merge_ms(gs, gd, gn, nq, K, torch, reps=20):
     """Device time of one fg_merge_shards call on the gathered lists (torch's
     current stream, where merge_on_device launches it)."""
@@ -193,16 +208,27 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
     gn = torch.empty((8, nq), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
 
-    def step():
+    streams = [torch.cuda.Stream(dev) for _ in range(8)]
+
+    def step_seq():
         for r, p in enumerate(plans):
             p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
         merge_on_device(gs, gd, gn, nq, K, st)
 
+    def step():
+        fanout(plans, gs, gd, gn, streams, torch, dev)
+        merge_on_device(gs, gd, gn, nq, K, st)
+
+    # per-namespace kernel times from back-to-back launches; the step itself
+    # runs the 8 namespaces on 8 streams
     for p in plans:
         p.profile(True)
-    el = timed_steps(step, steps, warmup, torch)
+    el_seq = timed_steps(step_seq, steps, warmup, torch)
     kms = [p.kernel_ms() for p in plans]
     per_ns = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
+    for p in plans:
+        p.profile(False)
+    el = timed_steps(step, steps, warmup, torch)
     mms = merge_ms(gs, gd, gn, nq, K, torch)
     del plans
     for ix in ixs:
@@ -210,6 +236,7 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
     return {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
             "batch": nq, "k": K, "terms": 3, "mode": "AND", "namespaces": 8, "docs_per_namespace": ranges[0][1],
             "k_conj_ms_per_namespace": per_ns, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
+            "streams": 8, "ms_per_step_one_stream": round(el_seq * 1e3 / steps, 4),
             "workload": "C4: 10M docs as 8 namespaces x 1.25M (own statistics each), fan-out 3-term AND top-100 "
                         "on all 8 + device merge, all 8 namespaces on this one GPU",
             "projected_8gpu": "each GPU runs one namespace: step ~ max(k_conj_ms_per_namespace) + k_final + gather"}
@@ -251,6 +278,8 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     st = torch.cuda.current_stream(dev).cuda_stream
     merged = {}
 
+    # back to back on one stream: a shard's k_disj fills the GPU by itself
+    # (8 streams measured 110.5 -> 112.6 ms per step)
     def step():
         for r, p in enumerate(plans):
             p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
