@@ -230,6 +230,22 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
         p.profile(False)
     el = timed_steps(step, steps, warmup, torch)
     mms = merge_ms(gs, gd, gn, nq, K, torch)
+    # the same fan-out through the ABI call a host makes: fg_search_sharded
+    # (host batch in, merged host hits out: 8 plans, 8 executes, merge, D2H)
+    ms_, md, msh, mn = merge_on_device(gs, gd, gn, nq, K, st)
+    torch.cuda.synchronize()
+    native.search_sharded(ixs, q_off, terms, K)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        s2, d2, sh2, n2 = native.search_sharded(ixs, q_off, terms, K)
+    sharded_ms = (time.perf_counter() - t0) * 1e3 / steps
+    mn = mn.cpu().numpy()
+    same = bool(np.array_equal(n2, mn))
+    ms_, md, msh = (x.cpu().numpy().reshape(nq, K) for x in (ms_, md, msh))
+    for i in range(nq):
+        m = int(mn[i])
+        same = same and np.array_equal(s2[i, :m], ms_[i, :m]) and np.array_equal(
+            d2[i, :m], md[i, :m].view(np.uint32)) and np.array_equal(sh2[i, :m], msh[i, :m].astype(np.uint32))
     del plans
     for ix in ixs:
         ix.close()
@@ -237,6 +253,10 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
             "batch": nq, "k": K, "terms": 3, "mode": "AND", "namespaces": 8, "docs_per_namespace": ranges[0][1],
             "k_conj_ms_per_namespace": per_ns, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
             "streams": 8, "ms_per_step_one_stream": round(el_seq * 1e3 / steps, 4),
+            "fg_search_sharded": {"value": round(nq / sharded_ms * 1e3, 1), "ms_per_batch": round(sharded_ms, 4),
+                                  "same_hits_as_step": same,
+                                  "note": "one synchronous ABI call per batch: host planning of 8 namespaces, "
+                                          "executes on side streams, device merge, D2H"},
             "workload": "C4: 10M docs as 8 namespaces x 1.25M (own statistics each), fan-out 3-term AND top-100 "
                         "on all 8 + device merge, all 8 namespaces on this one GPU",
             "projected_8gpu": "each GPU runs one namespace: step ~ max(k_conj_ms_per_namespace) + k_final + gather"}

@@ -1715,12 +1715,35 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
   return FG_OK;
 }
 
+// Side streams of fg_search_sharded, per device, created once and shared by
+// every caller (a stream takes work from any thread; each call orders its own
+// work with events)
+static constexpr uint32_t kSideStreams = 8;
+static hipStream_t side_stream(int dev, uint32_t i) {
+  static std::mutex mu;
+  static std::map<int, std::vector<hipStream_t>> pool;
+  std::lock_guard<std::mutex> l(mu);
+  auto& v = pool[dev];
+  while (v.size() <= i) {
+    hipStream_t st = nullptr;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+      return nullptr;
+    v.push_back(st);
+  }
+  return v[i];
+}
+
 // One batch over several shards / segments / namespaces of one logical index
-// (SURVEY.md §8b fg_search_sharded, §8e): every shard is planned on its own
-// host thread, executed on its own device's per-thread stream, its top-k lists
-// copied over xGMI (hipMemcpyPeerAsync) to the first shard's device unless they
-// are already there, and merged there by k_merge_rank into (score desc, shard
-// asc, doc asc) -- tantivy's merge_fruits over DocAddress (segment_ord, doc).
+// (SURVEY.md §8b fg_search_sharded, §8e).  Every shard's top-k lists land in
+// gathered buffers on the first shard's device -- directly, or over xGMI
+// (hipMemcpyPeerAsync) from the shard's own device -- and k_merge_rank merges
+// them there into (score desc, shard asc, doc asc): tantivy's merge_fruits over
+// DocAddress (segment_ord, doc).
+//   batch (>= 64 queries, > 1 shard): one host thread per shard plans it and
+//     launches it at once on a side stream of its device, so later shards are
+//     planned while earlier ones run and a device's shards overlap each other;
+//   otherwise (a single query: the host mirror's segment fan-out) everything
+//     runs inline on the calling thread's per-thread streams.
 int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
                       float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
   if (!shards || n_shards == 0 || n_shards > 64 || !q || k == 0 || !out_score || !out_doc || !out_n)
@@ -1732,30 +1755,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   }
   const uint32_t nq = q->n_queries;
   if (nq == 0) return FG_OK;
-  // ---- plan every shard (host work: cost order, work items, plan upload)
-  std::vector<std::unique_ptr<fg_plan>> plans(n_shards);
-  std::vector<int> rcs(n_shards, FG_OK);
-  std::vector<std::string> errs(n_shards);
-  auto plan_range = [&](uint32_t a, uint32_t b) {
-    for (uint32_t s = a; s < b; ++s) {
-      fg_plan* p = nullptr;
-      rcs[s] = fg_plan_create(shards[s], q, k, &p);
-      plans[s].reset(p);
-      if (rcs[s]) errs[s] = fg_last_error();
-    }
-  };
-  // (a thread per shard group pays off only for batches; a single query plans inline)
-  const uint32_t nt = nq >= 64 ? std::min<uint32_t>(n_shards, 8) : 1;
-  if (nt > 1) {
-    std::vector<std::thread> th;
-    for (uint32_t t = 0; t < nt; ++t)
-      th.emplace_back(plan_range, t * n_shards / nt, (t + 1) * n_shards / nt);
-    for (auto& x : th) x.join();
-  } else {
-    plan_range(0, n_shards);
-  }
-  for (uint32_t s = 0; s < n_shards; ++s)
-    if (rcs[s]) return fail(rcs[s], "shard %u: %s", s, errs[s].c_str());
+  if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k > FG_MAX_K");
   // ---- gathered lists + merged output on the first shard's device (its pool)
   const int dev0 = shards[0]->dev;
   const size_t nk = (size_t)nq * k;
@@ -1766,18 +1766,6 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   HIPCHK(hipSetDevice(dev0));
   char* base = static_cast<char*>(shards[0]->pool.get(total, &got));
   if (!base) return fail(FG_EOOM, "hipMalloc of the shard merge buffers failed");
-  // returned to the pool once every device's per-thread stream has drained
-  // (an early error return may leave launches or peer copies in flight)
-  struct Back {
-    fg_index* const* sh; uint32_t ns; void* p; size_t n;
-    ~Back() {
-      for (uint32_t s = 0; s < ns; ++s) {
-        (void)hipSetDevice(sh[s]->dev);
-        (void)hipStreamSynchronize(hipStreamPerThread);
-      }
-      sh[0]->pool.put(p, n);
-    }
-  } back{shards, n_shards, base, got};
   float* gs = reinterpret_cast<float*>(base);
   uint32_t* gd = reinterpret_cast<uint32_t*>(base + g_s);
   uint32_t* gn = reinterpret_cast<uint32_t*>(base + 2 * g_s);
@@ -1785,34 +1773,71 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   uint32_t* md = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + o_k);
   uint32_t* msh = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 2 * o_k);
   uint32_t* mn = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 3 * o_k);
-  // ---- execute: shards on dev0 write straight into the gathered lists (same
-  // per-thread stream as the merge); the others copy theirs over xGMI and the
-  // merge stream waits for their events
-  std::vector<hipEvent_t> evs;
-  struct EvGuard {
-    std::vector<hipEvent_t>& v;
-    ~EvGuard() { for (hipEvent_t e : v) (void)hipEventDestroy(e); }
-  } evg{evs};
-  for (uint32_t s = 0; s < n_shards; ++s) {
-    fg_plan* p = plans[s].get();
-    const int d = shards[s]->dev;
-    if (d == dev0) {
-      int rc = fg_plan_execute(p, hipStreamPerThread, gs + s * nk, gd + s * nk, gn + (size_t)s * nq);
-      if (rc) return rc;
-      continue;
+  // per shard: its plan, the stream it ran on, the event the merge waits for
+  const bool threaded = nq >= 64 && n_shards > 1;
+  std::vector<std::unique_ptr<fg_plan>> plans(n_shards);
+  std::vector<hipStream_t> sst(n_shards, nullptr);
+  std::vector<hipEvent_t> evs(n_shards, nullptr);
+  std::vector<int> rcs(n_shards, FG_OK);
+  std::vector<std::string> errs(n_shards);
+  // teardown (also on error returns): every stream drained, then the events,
+  // the plans (their destructors sync their own streams) and the buffers
+  struct Back {
+    fg_index* const* sh; uint32_t ns; void* p; size_t n;
+    std::vector<hipStream_t>& st; std::vector<hipEvent_t>& ev;
+    ~Back() {
+      for (uint32_t s = 0; s < ns; ++s) {
+        (void)hipSetDevice(sh[s]->dev);
+        (void)hipStreamSynchronize(st[s] ? st[s] : hipStreamPerThread);
+        if (ev[s]) (void)hipEventDestroy(ev[s]);
+      }
+      sh[0]->pool.put(p, n);
     }
-    int rc = fg_plan_execute(p, hipStreamPerThread, nullptr, nullptr, nullptr);  // sets device d
+  } back{shards, n_shards, base, got, sst, evs};
+  if (threaded)
+    for (uint32_t s = 0, nth = 0; s < n_shards; ++s, nth = 0) {
+      for (uint32_t t = 0; t < s; ++t) nth += shards[t]->dev == shards[s]->dev ? 1u : 0u;
+      if (!(sst[s] = side_stream(shards[s]->dev, nth % kSideStreams))) return fail(FG_EHIP, "side stream creation failed");
+    }
+  auto run = [&](uint32_t s) -> int {  // plan, launch, move the lists to dev0, record the event
+    fg_plan* p = nullptr;
+    int rc = fg_plan_create(shards[s], q, k, &p);
     if (rc) return rc;
-    HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score, d, 4 * nk, hipStreamPerThread));
-    HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc, d, 4 * nk, hipStreamPerThread));
-    HIPCHK(hipMemcpyPeerAsync(gn + (size_t)s * nq, dev0, p->own_n, d, 4ull * nq, hipStreamPerThread));
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    evs.push_back(e);
-    HIPCHK(hipEventRecord(e, hipStreamPerThread));
+    plans[s].reset(p);
+    const int d = shards[s]->dev;
+    hipStream_t st = sst[s] ? sst[s] : hipStreamPerThread;
+    const bool local = d == dev0;
+    rc = local ? fg_plan_execute(p, st, gs + s * nk, gd + s * nk, gn + (size_t)s * nq)
+               : fg_plan_execute(p, st, nullptr, nullptr, nullptr);  // selects device d
+    if (rc) return rc;
+    if (!local) {
+      HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score, d, 4 * nk, st));
+      HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc, d, 4 * nk, st));
+      HIPCHK(hipMemcpyPeerAsync(gn + (size_t)s * nq, dev0, p->own_n, d, 4ull * nq, st));
+    }
+    if (threaded || !local) {
+      HIPCHK(hipEventCreateWithFlags(&evs[s], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(evs[s], st));
+    }
+    return FG_OK;
+  };
+  if (threaded) {
+    std::vector<std::thread> th;
+    for (uint32_t s = 0; s < n_shards; ++s)
+      th.emplace_back([&, s] {
+        rcs[s] = run(s);
+        if (rcs[s]) errs[s] = fg_last_error();
+      });
+    for (auto& x : th) x.join();
+  } else {
+    for (uint32_t s = 0; s < n_shards; ++s)
+      if ((rcs[s] = run(s))) errs[s] = fg_last_error();
   }
+  for (uint32_t s = 0; s < n_shards; ++s)
+    if (rcs[s]) return fail(rcs[s], "shard %u: %s", s, errs[s].c_str());
   HIPCHK(hipSetDevice(dev0));
-  for (hipEvent_t e : evs) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
+  for (hipEvent_t e : evs)
+    if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
   HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
   HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
   HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
