@@ -213,7 +213,7 @@ __host__ __device__ inline uint32_t key_doc(uint64_t k) { return 0xFFFFFFFFu - (
 // build and again by fg_index_rescore when a commit changes the statistics.
 // Work is split into chunks of one term: k_score over postings, k_bucket over
 // directory buckets; ch_* arrays are the chunk tables.
-constexpr uint32_t kScoreChunk = 2048;   // postings per k_score workgroup
+constexpr uint32_t kScoreChunk = kChunk;  // postings per k_score workgroup (= a k_conj lead chunk: cmax)
 constexpr uint32_t kBucketChunk = 2048;  // buckets per k_bucket workgroup
 static_assert(kScoreChunk == kChunk, "DevIndex::cmax: a k_score chunk is a k_conj lead chunk");
 struct ScoreJob {

@@ -1434,10 +1434,14 @@ __global__ __launch_bounds__(kThreads) void k_scan(DevIndex ix, DevPlan pl) {
 // Dynamic LDS (80 KB: 2 workgroups per CU): candidate keys, the k winners,
 // the radix histogram.  Keeps 16-B alignment of the dynamic base (no static
 // __shared__ in this kernel: cdna_hip_programming.md Guideline 17).
+#ifndef FG_FINAL_HBITS
+#define FG_FINAL_HBITS 11
+#endif
+constexpr uint32_t kFinalHistBits = FG_FINAL_HBITS;  // k_final's radix digits (its LDS sets its occupancy)
 struct FinalShared {
   uint64_t keys[kFinalCap];
   uint64_t win[kMaxK];
-  uint32_t hist[kHistBins];
+  uint32_t hist[1u << kFinalHistBits];
   uint32_t scratch[8];
   uint32_t n_keys;
   uint32_t n_win;
@@ -1489,12 +1493,12 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
     // exact k-th key (in LDS, or straight from HBM when the list overflowed), then the K winners
     uint64_t T;
     if (nk > kFinalCap) {
-      T = select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
+      T = select_kth<kFinalHistBits>(K, sh.hist, sh.scratch, [&](auto&& f) {
         each_key(T0, [&](bool keep, uint64_t key) { if (keep) f(key); });
       });
       each_key(T, [&](bool keep, uint64_t key) { wave_append(keep, key, sh.win, &sh.n_win, kMaxK); });
     } else {
-      T = select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
+      T = select_kth<kFinalHistBits>(K, sh.hist, sh.scratch, [&](auto&& f) {
         for (uint32_t i = tid; i < nk; i += kThreads) f(sh.keys[i]);
       });
       for (uint32_t i0 = 0; i0 < nk; i0 += kThreads) {
