@@ -239,6 +239,56 @@ struct WsPool {
   }
 };
 
+// Pinned host buffers of one index: plan uploads and result copies go through
+// them (a pageable copy is staged by the runtime and synchronises on the way),
+// which takes ~tens of us off a batch-of-one search.
+struct PinnedPool {
+  static constexpr size_t kKeep = 64ull << 20;
+  std::mutex mu;
+  std::multimap<size_t, void*> free_bufs;
+  size_t cached = 0;
+  void* get(size_t bytes, size_t* got) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      auto it = free_bufs.lower_bound(bytes);
+      if (it != free_bufs.end() && it->first <= 4 * bytes + 65536) {
+        void* p = it->second;
+        *got = it->first;
+        cached -= it->first;
+        free_bufs.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    const size_t n = std::max<size_t>(bytes, 4096);
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    *got = n;
+    return p;
+  }
+  void put(void* p, size_t bytes) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (cached + bytes <= kKeep) {
+        free_bufs.emplace(bytes, p);
+        cached += bytes;
+        return;
+      }
+    }
+    (void)hipHostFree(p);
+  }
+  ~PinnedPool() {
+    for (auto& kv : free_bufs) (void)hipHostFree(kv.second);
+  }
+};
+// a pinned buffer of the pool for one scope
+struct PinnedLease {
+  PinnedPool& pool;
+  void* p = nullptr;
+  size_t n = 0;
+  PinnedLease(PinnedPool& pl, size_t bytes) : pool(pl) { p = pool.get(bytes, &n); }
+  ~PinnedLease() { if (p) pool.put(p, n); }
+};
+
 struct fg_index {
   std::atomic<int> refs{1};
   int dev = 0;
@@ -280,6 +330,7 @@ struct fg_index {
   fg::DevIndex d{};
   DevAllocs mem;
   WsPool pool;  // plan workspaces (destroyed before mem: declared after it)
+  PinnedPool pinned;  // host staging of plan uploads and result copies
 };
 
 struct fg_plan {
@@ -1476,8 +1527,12 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
     if (items.size() + nchunk[i] > 0x7FFFFFFFull)
       return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", items.size());
     const uint32_t nch = nchunk[i];
-    const uint32_t G = std::min<uint32_t>(
-        fg::kMaxGroup, std::max<uint32_t>(1, (nch + fg::kConjGroupsPerQuery - 1) / fg::kConjGroupsPerQuery));
+    // items per query: ~kConjGroupsPerQuery in a full batch; a small batch (a
+    // batch of one: the p50 latency) spreads a query over up to 64 items so its
+    // chunks run side by side instead of up to kMaxGroup in a row, while its
+    // k_final still reads at most 64 x k candidates
+    const uint32_t per_q = std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u)));
+    const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + per_q - 1) / per_q));
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;
     for (uint32_t g = 0; g < ng; ++g)
@@ -1538,10 +1593,16 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->ix = ix;  // owns the workspace from here on (returned to ix->pool); retained below
   fg_index_retain(ix);
   p->ws_bytes = total;
-  std::vector<char> staging(s_in, 0);
+  PinnedLease pin(ix->pinned, s_in);
+  std::vector<char> staging_pageable;  // only if the pinned allocation failed
+  char* staging = static_cast<char*>(pin.p);
+  if (!staging) {
+    staging_pageable.assign(s_in, 0);
+    staging = staging_pageable.data();
+  }
   size_t o = 0;
   auto put = [&](const void* src, size_t bytes, size_t slot) {
-    if (bytes) std::memcpy(staging.data() + o, src, bytes);
+    if (bytes) std::memcpy(staging + o, src, bytes);
     void* dptr = base + o;
     o += slot;
     return dptr;
@@ -1566,7 +1627,7 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.f.ch_start = (const uint32_t*)put(ch_s.data(), 4ull * nch, s_ch);
   // on the planning thread's own stream: a plan built while another thread's
   // batch runs does not serialise against it through the legacy null stream
-  HIPCHK(hipMemcpyAsync(base, staging.data(), s_in, hipMemcpyHostToDevice, hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(base, staging, s_in, hipMemcpyHostToDevice, hipStreamPerThread));
   HIPCHK(hipStreamSynchronize(hipStreamPerThread));
   char* cur = base + s_in;
   p->zero_region = cur;
@@ -1633,6 +1694,22 @@ int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* o
   // copies on the plan's stream (a per-thread stream under fg_search_batch), then wait for it
   const size_t nk = (size_t)p->nq * p->k;
   hipStream_t s = p->last_stream;
+  // own_score, own_doc, own_n are consecutive in the workspace: one D2H into a
+  // pinned buffer, then host copies (small batches: the batch-of-one latency)
+  const char* first = reinterpret_cast<const char*>(p->own_score);
+  const size_t span = reinterpret_cast<const char*>(p->own_n) + 4ull * p->nq - first;
+  if (span <= (4ull << 20)) {
+    PinnedLease pin(p->ix->pinned, span);
+    if (pin.p) {
+      HIPCHK(hipMemcpyAsync(pin.p, first, span, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      const char* h = static_cast<const char*>(pin.p);
+      if (out_score) std::memcpy(out_score, h, 4 * nk);
+      if (out_doc) std::memcpy(out_doc, h + (reinterpret_cast<const char*>(p->own_doc) - first), 4 * nk);
+      if (out_n) std::memcpy(out_n, h + (reinterpret_cast<const char*>(p->own_n) - first), 4ull * p->nq);
+      return FG_OK;
+    }
+  }
   if (out_score) HIPCHK(hipMemcpyAsync(out_score, p->own_score, 4 * nk, hipMemcpyDeviceToHost, s));
   if (out_doc) HIPCHK(hipMemcpyAsync(out_doc, p->own_doc, 4 * nk, hipMemcpyDeviceToHost, s));
   if (out_n) HIPCHK(hipMemcpyAsync(out_n, p->own_n, 4ull * p->nq, hipMemcpyDeviceToHost, s));

@@ -142,6 +142,22 @@ def test_zipf_1m_vs_oracle(native, gpu_1m, oracle_1m, m_min, m_max, k, mode):
     assert (n > 0).mean() > 0.5
 
 
+@pytest.mark.parametrize("batch", [1, 8])
+def test_small_batches_vs_oracle(native, gpu_1m, oracle_1m, batch):
+    """Batches of one and of eight (the latency path: a query spread over up to
+    64 work items) give the batch results."""
+    from fugu_amd import synth
+    q_off, terms = synth.queries(64, 1, 5, seed_q=21)
+    rs, rd, rn, _, _ = oracle_1m.search_batch(q_off, terms, 100, threads=16)
+    for b0 in range(0, 64, batch):
+        a, b = int(q_off[b0]), int(q_off[b0 + batch])
+        sub = (q_off[b0:b0 + batch + 1] - q_off[b0]).astype(np.uint32)
+        s, d, n = gpu_1m.search_batch(sub, terms[a:b], 100)
+        for j in range(batch):
+            i = b0 + j
+            assert_same(s[j], d[j], n[j], rs[i, :rn[i]], rd[i, :rn[i]], (batch, i))
+
+
 def test_plan_reuse_profile_and_bytes_model(native, gpu_1m, oracle_1m):
     from fugu_amd import synth
     q_off, terms = synth.queries(256, 3, 3)
