@@ -355,6 +355,10 @@ struct fg_plan {
   uint32_t n_prof = 0;
   ~fg_plan() {
     for (hipEvent_t e : pending) (void)hipEventDestroy(e);
+    if (pin) {  // an upload nothing waited for yet (created without sync, never executed)
+      (void)hipSetDevice(ix->dev);
+      (void)hipStreamSynchronize(hipStreamPerThread);
+    }
     if (ws) {
       // the workspace may still be read by this plan's last launch (a per-thread
       // stream handle resolves on the current device: select the plan's first)
@@ -362,11 +366,15 @@ struct fg_plan {
         (void)hipSetDevice(ix->dev);
         (void)hipStreamSynchronize(last_stream);
       }
+      if (pin) ix->pinned.put(pin, pin_n);
       ix->pool.put(ws, ws_got);
     }
     if (ix) fg_index_release(ix);
   }
   bool last_stream_used = false;
+  bool zeroed = false;        // the zero region arrived zeroed with the upload: the first execute skips its memset
+  void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
+  size_t pin_n = 0;
 };
 
 namespace {
@@ -1339,7 +1347,16 @@ int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_nam
 }
 
 // ---------------------------------------------------------------- planning
+static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync);
+
 int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out) {
+  return plan_create(ix, q, k, out, true);
+}
+
+// sync = false (fg_search_batch): the upload stays in flight on the calling
+// thread's per-thread stream, where the plan's execute is queued behind it;
+// the pinned staging is returned when the plan is destroyed
+static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync) {
   if (!ix || !q || !out || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
   if (q->n_queries && q->q_off[q->n_queries] > q->q_off[0] && !q->terms) return fail(FG_EINVAL, "q_off without terms");
   if (q->f_off && q->n_queries && q->f_off[q->n_queries] > q->f_off[0] && !q->f_terms)
@@ -1593,12 +1610,18 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->ix = ix;  // owns the workspace from here on (returned to ix->pool); retained below
   fg_index_retain(ix);
   p->ws_bytes = total;
-  PinnedLease pin(ix->pinned, s_in);
+  // a small zero region (thresholds, candidate counts, facet masks) travels
+  // zeroed with the upload, so the first execute needs no memset
+  const size_t s_zero = s_thr + s_cc + s_mask;
+  const size_t s_up = s_in + (s_zero <= (64u << 10) ? s_zero : 0);
+  PinnedLease pin(ix->pinned, s_up);
   std::vector<char> staging_pageable;  // only if the pinned allocation failed
   char* staging = static_cast<char*>(pin.p);
   if (!staging) {
-    staging_pageable.assign(s_in, 0);
+    staging_pageable.assign(s_up, 0);
     staging = staging_pageable.data();
+  } else if (s_up > s_in) {
+    std::memset(staging + s_in, 0, s_up - s_in);
   }
   size_t o = 0;
   auto put = [&](const void* src, size_t bytes, size_t slot) {
@@ -1627,8 +1650,15 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
   p->d.f.ch_start = (const uint32_t*)put(ch_s.data(), 4ull * nch, s_ch);
   // on the planning thread's own stream: a plan built while another thread's
   // batch runs does not serialise against it through the legacy null stream
-  HIPCHK(hipMemcpyAsync(base, staging, s_in, hipMemcpyHostToDevice, hipStreamPerThread));
-  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, hipStreamPerThread));
+  p->zeroed = s_up > s_in;
+  if (sync || !pin.p) {
+    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+  } else {
+    p->pin = pin.p;  // the plan returns it (after a sync) when destroyed
+    p->pin_n = pin.n;
+    pin.p = nullptr;
+  }
   char* cur = base + s_in;
   p->zero_region = cur;
   p->zero_bytes = s_thr + s_cc + s_mask;
@@ -1667,7 +1697,8 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
   float* os = d_out_score ? d_out_score : p->own_score;
   uint32_t* od = d_out_doc ? d_out_doc : p->own_doc;
   uint32_t* on = d_out_n ? d_out_n : p->own_n;
-  HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
+  if (p->zeroed) p->zeroed = false;  // the first execute after the upload
+  else HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
   hipEvent_t ev[3] = {};
   if (p->profile) {
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
@@ -1773,7 +1804,7 @@ int fg_plan_destroy(fg_plan* p) {
 int fg_search_batch(fg_index* ix, const fg_query_batch* q, uint32_t k, float* out_score, uint32_t* out_doc,
                     uint32_t* out_n) {
   fg_plan* p = nullptr;
-  int rc = fg_plan_create(ix, q, k, &p);
+  int rc = plan_create(ix, q, k, &p, false);  // execute is queued behind the upload on the same stream
   if (rc) return rc;
   std::unique_ptr<fg_plan> guard(p);
   // the calling thread's own stream: concurrent callers (tokio workers sharing
