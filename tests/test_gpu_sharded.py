@@ -94,6 +94,41 @@ def test_namespaces_fanout_equals_numpy_merge(native, ctx):
             assert np.array_equal(sh[i, :m], esh[i, :m]), (mode, i)
 
 
+def test_sharded_concurrent_callers(native, ctx):
+    """Four host threads issue fan-out batches over the same namespaces at once
+    (the side streams are shared by every caller; each call orders its own work
+    with events): every call returns the single-caller result."""
+    import threading
+
+    from fugu_amd import synth
+    V = synth.VOCAB
+    nss = [synth.corpus(100_000, V, 1.0, synth.SEED_L + 10 + r, synth.SEED_T + 10 + r) for r in range(3)]
+    ixs = [native.Index.from_docs(ctx, c.off, c.tok, V, threads=16, keep_host=False) for c in nss]
+    batches = [synth.queries(128, 1, 4, seed_q=40 + t) for t in range(4)]
+    want = [native.search_sharded(ixs, qo, qt, 100) for qo, qt in batches]
+    errors = []
+
+    def worker(t):
+        try:
+            for _ in range(5):
+                got = native.search_sharded(ixs, *batches[t], 100)
+                n = want[t][3]
+                assert np.array_equal(got[3], n)
+                for i in range(len(n)):
+                    m = int(n[i])
+                    for a, b in zip(got[:3], want[t][:3]):
+                        assert np.array_equal(a[i, :m], b[i, :m]), (t, i)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errors, errors[:3]
+
+
 def test_sharded_terms_outside_a_shard_and_errors(native, ctx):
     """A shard built before a term was interned (smaller n_terms) matches nothing
     for it; bad arguments are rejected before any launch."""
