@@ -243,7 +243,7 @@ struct WsPool {
 // them (a pageable copy is staged by the runtime and synchronises on the way),
 // which takes ~tens of us off a batch-of-one search.
 struct PinnedPool {
-  static constexpr size_t kKeep = 64ull << 20;
+  static constexpr size_t kKeep = 16ull << 20;
   std::mutex mu;
   std::multimap<size_t, void*> free_bufs;
   size_t cached = 0;
