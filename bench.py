@@ -368,8 +368,9 @@ def main():
                     help="skip the secondary workloads (C3, OR top-1000, end-to-end, C4, C5)")
     ap.add_argument("--extra-steps", type=int, default=5)
     ap.add_argument("--no-c5", action="store_true", help="skip the 100M-doc C5 secondary line")
-    ap.add_argument("--e2e-workers", type=int, default=8,
-                    help="batches in flight in the end-to-end line (tools/e2e_workers.py: 2 -> 570K, 4 -> 713K, 8 -> 780K q/s)")
+    ap.add_argument("--e2e-workers", type=int, default=4,
+                    help="batches in flight in the end-to-end line (tools/e2e_workers.py with the radix planner: "
+                         "1 -> 697K, 2 -> 816K, 4 -> 934K, 8 -> 868K q/s)")
     ap.add_argument("--disj", action="store_true",
                     help="headline batch = 2-5-term OR (k_disj; profiling runs, pass --k 1000 --no-cpu)")
     args = ap.parse_args()

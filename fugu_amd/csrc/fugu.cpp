@@ -1555,11 +1555,30 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
     for (uint32_t g = 0; g < ng; ++g)
       items.push_back(W{(g + 0.5) / ng, i, g * G, std::min(G, nch - g * G)});
   }
-  // AND: single-list queries' items first (their own k_conj launch), each part in sweep order
+  // AND: single-list queries' items first (their own k_conj launch), each part in sweep order.
+  // A stable LSD radix sort on (not single, key quantized to 31 bits): the order
+  // is a scheduling choice only (every order gives the same hits), and it takes
+  // a fraction of a comparison sort's host time on a 20K-item batch.
   auto single = [&](const W& x) { return !disj && q_m[x.q] == 1; };
-  std::stable_sort(items.begin(), items.end(), [&](const W& a, const W& b) {
-    return single(a) != single(b) ? single(a) : a.key < b.key;
-  });
+  {
+    const size_t n = items.size();
+    std::vector<uint64_t> a(n), b(n);  // (sort key << 32) | item index
+    for (size_t x = 0; x < n; ++x) {
+      const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
+      const uint32_t rk = (single(items[x]) ? 0u : 0x80000000u) | (uint32_t)(kk * 2147483647.0);
+      a[x] = ((uint64_t)rk << 32) | (uint64_t)x;
+    }
+    for (int sh = 32; sh < 64; sh += 11) {
+      uint32_t cnt[2049] = {0};
+      for (size_t x = 0; x < n; ++x) cnt[((a[x] >> sh) & 2047u) + 1]++;
+      for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
+      for (size_t x = 0; x < n; ++x) b[cnt[(a[x] >> sh) & 2047u]++] = a[x];
+      a.swap(b);
+    }
+    std::vector<W> sorted(n);
+    for (size_t x = 0; x < n; ++x) sorted[x] = items[(uint32_t)a[x]];
+    items.swap(sorted);
+  }
   uint64_t n_single = 0;
   for (const W& x : items) n_single += single(x) ? 1 : 0;
   std::stable_sort(scan.begin(), scan.end(), [](const W& a, const W& b) { return a.key < b.key; });
