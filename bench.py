@@ -465,6 +465,7 @@ def main():
         ix.search_batch(one_off, terms[a:b], K)
         lat.append(time.perf_counter() - t1)
     p50_ms = float(np.median(lat) * 1e3) if lat else None
+    tail_ms = {f"p{q}": round(float(np.percentile(lat, q) * 1e3), 4) for q in (90, 99)} if lat else None
 
     # ---- roofline of the dominant kernel (k_conj): algorithmic bytes at the HBM
     # layout (fg_bytes_model_gpu: k_conj's exhaustive cascade) over
@@ -643,6 +644,7 @@ def main():
                     if world > 1 else ""),
             },
             "p50_ms": round(p50_ms, 4) if p50_ms is not None else None,
+            "latency_ms": tail_ms,  # batch-of-one p90 / p99 beside p50 (same sample)
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
