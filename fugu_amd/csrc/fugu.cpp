@@ -8,6 +8,7 @@
 // on the host, in that operation order with the host libm, so the device only
 // multiplies/divides precomputed f32 values (bit-identical to the CPU path).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -150,13 +151,36 @@ void parallel_dynamic(uint32_t n, int threads, uint32_t grain, F&& f) {
   for (auto& t : ts) t.join();
 }
 
+// Host threads for snapshot builds and planning: FUGU_THREADS when set; else
+// OMP_NUM_THREADS when it states a share above one (16 per GPU on the box; a
+// launcher's default of 1 -- torchrun sets it for every rank -- is not a CPU
+// share and is ignored); else the CPUs this process may run on (affinity,
+// capped by the cgroup quota), at most 64.
 int hw_threads(int req) {
   if (req > 0) return std::min(req, 256);
-  // the process's CPU share where the launcher states it (16 per GPU on the box)
-  if (const char* e = getenv("OMP_NUM_THREADS"))
-    if (atoi(e) > 0) return std::min(atoi(e), 256);
-  unsigned h = std::thread::hardware_concurrency();
-  return (int)std::max(1u, std::min(h, 64u));
+  static const int n = [] {
+    int t = 0;
+    if (const char* e = getenv("FUGU_THREADS")) t = atoi(e);
+    if (t <= 0)
+      if (const char* e = getenv("OMP_NUM_THREADS"))
+        if (atoi(e) > 1) t = atoi(e);
+    if (t <= 0) {
+      cpu_set_t cs;
+      t = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : (int)std::thread::hardware_concurrency();
+      if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long per = 0;
+        if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+          t = std::min<long long>(t, std::max<long long>(1, atoll(q) / per));
+        fclose(f);
+      }
+      t = std::min(t, 64);
+    }
+    t = std::max(1, std::min(t, 256));
+    if (getenv("FUGU_BUILD_TRACE")) fprintf(stderr, "[fg build] host threads: %d\n", t);
+    return t;
+  }();
+  return n;
 }
 
 // Host-side postings before upload (merged text U name per term).
@@ -191,6 +215,7 @@ struct DevAllocs {
 
 struct fg_ctx {
   std::vector<int> devs;
+  std::vector<std::pair<int, int>> peers;  // (a, b): a reaches b's memory directly
 };
 
 // Plan workspaces of one index, recycled across batches (a server plans a new
@@ -216,7 +241,17 @@ struct WsPool {
       }
     }
     void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      // the cached workspaces may be what the device lacks: free them, retry once
+      (void)hipGetLastError();
+      {
+        std::lock_guard<std::mutex> l(mu);
+        for (auto& kv : free_bufs) (void)hipFree(kv.second);
+        free_bufs.clear();
+        cached = 0;
+      }
+      if (hipMalloc(&p, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    }
     *got = bytes;
     return p;
   }
@@ -954,6 +989,22 @@ int fg_ctx_create(int ndev, const int* devs, fg_ctx** out) {
     int rc = check_device(d);
     if (rc) return rc;
   }
+  // fg_search_sharded moves each shard's top-k to the first shard's device
+  // with hipMemcpyPeerAsync: direct xGMI transfers need peer access enabled
+  // between every pair of the context's devices (already-enabled is fine)
+  for (int a : c->devs)
+    for (int b : c->devs) {
+      if (a == b) continue;
+      int can = 0;
+      HIPCHK(hipDeviceCanAccessPeer(&can, a, b));
+      if (!can) return fail(FG_ENODEV, "device %d cannot access device %d over xGMI", a, b);
+      HIPCHK(hipSetDevice(a));
+      const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        return fail(FG_EHIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", a, b, hipGetErrorString(e));
+      (void)hipGetLastError();
+      c->peers.emplace_back(a, b);
+    }
   *out = c.release();
   return FG_OK;
 }
@@ -1918,6 +1969,11 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
         (void)hipStreamSynchronize(st[s] ? st[s] : hipStreamPerThread);
         if (ev[s]) (void)hipEventDestroy(ev[s]);
       }
+      // the merge and its copies run on the first device's per-thread stream:
+      // drained before the buffers go back to the pool (an error return may
+      // leave them in flight)
+      (void)hipSetDevice(sh[0]->dev);
+      (void)hipStreamSynchronize(hipStreamPerThread);
       sh[0]->pool.put(p, n);
     }
   } back{shards, n_shards, base, got, sst, evs};

@@ -569,7 +569,9 @@ struct Doc {
 // policy's job).  Every segment scores with the namespace-wide statistics.
 struct Segment {
   fg_index* ix = nullptr;
-  uint32_t base = 0, n = 0;  // global doc ids [base, base + n)
+  uint32_t base = 0, n = 0;  // global doc ids [base, base + n) ...
+  std::shared_ptr<const std::vector<uint32_t>> gid;  // ... or, for a merged segment, gid[local doc]
+  uint32_t global(uint32_t d) const { return gid ? (*gid)[d] : base + d; }
 };
 struct Snapshot {
   std::vector<Segment> segs;
@@ -591,10 +593,11 @@ struct Namespace {
   std::shared_ptr<Snapshot> snap;                      // committed device snapshot
   std::shared_mutex snap_mu;
   size_t committed_docs = 0;
-  // BM25 statistics of the committed docs, deleted ones included (tantivy's
-  // Searcher counts them until a merge): N, token totals, doc frequencies.
-  // Updated with each commit's new docs only.
-  uint64_t st_tot[2] = {0, 0}, st_tot_f = 0;
+  // BM25 statistics of the committed segments, deleted docs included (tantivy's
+  // Searcher counts them until a merge drops them): N, token totals, doc
+  // frequencies.  Updated with each commit's new docs only; recomputed from the
+  // alive docs when segments merge.
+  uint64_t st_n = 0, st_tot[2] = {0, 0}, st_tot_f = 0;
   std::vector<uint32_t> st_df_text, st_df_name, st_df_facet;
 };
 
@@ -739,7 +742,7 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
                              sh.data(), &n);
   if (rc) return hfail(rc, fg_last_error());
   for (uint64_t i = offset; i < n; ++i)  // skip(offset).take(per_page)
-    hits.push_back(fg_hit{sc[i], snap->segs[sh[i]].base + dc[i]});
+    hits.push_back(fg_hit{sc[i], snap->segs[sh[i]].global(dc[i])});
   return FG_OK;
 }
 
@@ -1079,9 +1082,12 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   // IndexWriter::commit (src/db/document.rs:65): the docs upserted since the
   // last commit become a new segment; the namespace statistics change, so the
   // older segments are rescored on the device (fg_index_rescore: their postings
-  // stay where they are) and pick up the new deletions; past kMaxSegments all
-  // docs are rebuilt into one segment (the merge policy).  Readers keep the
-  // snapshot they hold (refcounted).
+  // stay where they are) and pick up the new deletions.  Past kMaxSegments the
+  // alive docs are rebuilt into one segment (the merge policy): like a tantivy
+  // merge, it drops the deleted docs, so N, df and token totals are recomputed
+  // from the alive docs, and the merged segment keeps their global order.
+  // Readers keep the snapshot they hold (refcounted).  The namespace's
+  // statistics and snapshot change together, only when every step succeeded.
   if (!db) return hfail(FG_EINVAL, "bad arguments");
   auto ns = find_ns(db, nsname);
   if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
@@ -1099,67 +1105,77 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   const uint32_t old = (uint32_t)ns->committed_docs;
   if (N == 0 || (N == old && cur)) return FG_OK;
   const bool merge = !cur || cur->segs.size() + 1 > kMaxSegments;
-  const uint32_t from = merge ? 0 : old;  // docs of the segment to build
+  // docs of the segment to build (global ids): the new ones, or every alive one on a merge
+  // (the first commit keeps its deleted docs: no merge has dropped them yet)
+  std::vector<uint32_t> build_ids;
+  for (uint32_t d = merge ? 0 : old; d < N; ++d)
+    if (!cur || !merge || !ns->docs[d].deleted) build_ids.push_back(d);
+  const uint32_t nb = (uint32_t)build_ids.size();
   const uint32_t n_terms = std::max<uint32_t>(1, (uint32_t)ns->dict.size());
   const uint32_t n_fterms = (uint32_t)ns->fdict.size();
-  std::vector<uint64_t> toff(N - from + 1, 0), noff(N - from + 1, 0), foff(N - from + 1, 0);
+  std::vector<uint64_t> toff(nb + 1, 0), noff(nb + 1, 0), foff(nb + 1, 0);
   std::vector<uint32_t> ttok, ntok, ftok;
-  std::vector<uint8_t> del(N, 0);
+  std::vector<uint8_t> del(N, 0), bdel(nb, 0);
   bool any_name = false, any_del = false;
   for (uint32_t d = 0; d < N; ++d) {
-    const Doc& doc = ns->docs[d];
-    del[d] = doc.deleted ? 1 : 0;
-    any_del |= doc.deleted;
-    if (d < from) continue;
+    del[d] = ns->docs[d].deleted ? 1 : 0;
+    any_del |= ns->docs[d].deleted;
+  }
+  // statistics after this commit, in local copies
+  uint64_t st_n = merge ? 0 : ns->st_n, st_tot[2] = {merge ? 0 : ns->st_tot[0], merge ? 0 : ns->st_tot[1]};
+  uint64_t st_tot_f = merge ? 0 : ns->st_tot_f;
+  std::vector<uint32_t> df_t, df_n, df_f;
+  if (!merge) { df_t = ns->st_df_text; df_n = ns->st_df_name; df_f = ns->st_df_facet; }
+  df_t.resize(n_terms, 0);
+  df_n.resize(n_terms, 0);
+  df_f.resize(n_fterms, 0);
+  std::vector<uint32_t> sc;
+  auto distinct = [&](const std::vector<uint32_t>& v, std::vector<uint32_t>& df) {
+    sc = v;
+    std::sort(sc.begin(), sc.end());
+    sc.erase(std::unique(sc.begin(), sc.end()), sc.end());
+    for (uint32_t t : sc) df[t]++;
+  };
+  bool built_del = false;
+  for (uint32_t i = 0; i < nb; ++i) {
+    const Doc& doc = ns->docs[build_ids[i]];
     ttok.insert(ttok.end(), doc.text_tok.begin(), doc.text_tok.end());
     ntok.insert(ntok.end(), doc.name_tok.begin(), doc.name_tok.end());
     ftok.insert(ftok.end(), doc.facet_tok.begin(), doc.facet_tok.end());
-    toff[d - from + 1] = ttok.size();
-    noff[d - from + 1] = ntok.size();
-    foff[d - from + 1] = ftok.size();
+    toff[i + 1] = ttok.size();
+    noff[i + 1] = ntok.size();
+    foff[i + 1] = ftok.size();
     any_name |= !doc.name_tok.empty();
+    bdel[i] = doc.deleted ? 1 : 0;
+    built_del |= doc.deleted;
+    // namespace statistics += this segment's docs (distinct terms per doc per field)
+    st_n++;
+    st_tot[0] += doc.text_tok.size();
+    st_tot[1] += doc.name_tok.size();
+    st_tot_f += doc.facet_tok.size();
+    distinct(doc.text_tok, df_t);
+    distinct(doc.name_tok, df_n);
+    distinct(doc.facet_tok, df_f);
   }
-  for (uint32_t d = 0; d < from && !any_name; ++d) any_name |= !ns->docs[d].name_tok.empty();
+  if (!merge)
+    for (uint32_t d = 0; d < old && !any_name; ++d) any_name |= !ns->docs[d].name_tok.empty();
   w.unlock();
-  // namespace statistics += the new docs [old, N) (distinct terms per doc per field)
-  ns->st_df_text.resize(n_terms, 0);
-  ns->st_df_name.resize(n_terms, 0);
-  ns->st_df_facet.resize(n_fterms, 0);
-  {
-    std::lock_guard<std::mutex> w2(ns->writer);
-    std::vector<uint32_t> sc;
-    auto distinct = [&](const std::vector<uint32_t>& v, std::vector<uint32_t>& df) {
-      sc = v;
-      std::sort(sc.begin(), sc.end());
-      sc.erase(std::unique(sc.begin(), sc.end()), sc.end());
-      for (uint32_t t : sc) df[t]++;
-    };
-    for (uint32_t d = old; d < N; ++d) {
-      const Doc& doc = ns->docs[d];
-      ns->st_tot[0] += doc.text_tok.size();
-      ns->st_tot[1] += doc.name_tok.size();
-      ns->st_tot_f += doc.facet_tok.size();
-      distinct(doc.text_tok, ns->st_df_text);
-      distinct(doc.name_tok, ns->st_df_name);
-      distinct(doc.facet_tok, ns->st_df_facet);
-    }
-  }
   fg_global_stats g{};
-  g.n_docs = N;
-  g.tot_tokens[0] = ns->st_tot[0];
-  g.tot_tokens[1] = ns->st_tot[1];
-  g.df_text = ns->st_df_text.data();
-  g.df_name = ns->st_df_name.data();
-  g.df_facet = n_fterms ? ns->st_df_facet.data() : nullptr;
-  g.tot_facet_tokens = ns->st_tot_f;
+  g.n_docs = st_n;
+  g.tot_tokens[0] = st_tot[0];
+  g.tot_tokens[1] = st_tot[1];
+  g.df_text = df_t.data();
+  g.df_name = df_n.data();
+  g.df_facet = n_fterms ? df_f.data() : nullptr;
+  g.tot_facet_tokens = st_tot_f;
   fg_docs_input in{};
-  in.n_docs = N - from;
+  in.n_docs = nb;
   in.n_terms = n_terms;
   in.text_off = toff.data();
   in.text_tok = ttok.data();
   in.name_off = any_name ? noff.data() : nullptr;
   in.name_tok = any_name ? ntok.data() : nullptr;
-  in.deleted = any_del ? del.data() + from : nullptr;
+  in.deleted = built_del ? bdel.data() : nullptr;
   in.threads = 0;
   in.keep_host_postings = 0;
   in.n_facet_terms = n_fterms;
@@ -1167,21 +1183,38 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   in.facet_tok = n_fterms ? ftok.data() : nullptr;
   auto snap = std::make_shared<Snapshot>();
   if (!merge) {
+    std::vector<uint8_t> sdel;
     for (const Segment& s0 : cur->segs) {
+      // this segment's deleted flags in its own doc order
+      sdel.assign(s0.n, 0);
+      bool sany = false;
+      for (uint32_t d = 0; d < s0.n; ++d) sany |= (sdel[d] = del[s0.global(d)]) != 0;
       fg_index* re = nullptr;
-      int rc = fg_index_rescore(s0.ix, &g, any_del ? del.data() + s0.base : nullptr, &re);
-      if (rc) return hfail(rc, fg_last_error());
-      snap->segs.push_back(Segment{re, s0.base, s0.n});
+      int rc = fg_index_rescore(s0.ix, &g, sany ? sdel.data() : nullptr, &re);
+      if (rc) return hfail(rc, fg_last_error());  // snap releases the rescored ones
+      snap->segs.push_back(Segment{re, s0.base, s0.n, s0.gid});
     }
   }
+  if (const char* f = getenv("FUGU_FAULT_INJECT"))  // tests only: a commit whose device build fails
+    if (std::strcmp(f, "commit_build") == 0) return hfail(FG_EHIP, "injected fault: segment build");
   fg_index* ix = nullptr;
   int rc = fg_index_build_from_docs_global(db->ctx, db->dev, &in, &g, &ix);
   if (rc) return hfail(rc, fg_last_error());
-  snap->segs.push_back(Segment{ix, from, N - from});
+  Segment ns_seg{ix, merge ? 0u : old, nb, nullptr};
+  if (merge && nb != N) ns_seg.gid = std::make_shared<const std::vector<uint32_t>>(std::move(build_ids));
+  snap->segs.push_back(std::move(ns_seg));
   {
+    std::lock_guard<std::mutex> w2(ns->writer);  // the statistics are read under the writer lock
     std::unique_lock<std::shared_mutex> l(ns->snap_mu);  // readers keep the old snapshot (refcount)
     ns->snap = snap;
     ns->committed_docs = N;
+    ns->st_n = st_n;
+    ns->st_tot[0] = st_tot[0];
+    ns->st_tot[1] = st_tot[1];
+    ns->st_tot_f = st_tot_f;
+    ns->st_df_text.swap(df_t);
+    ns->st_df_name.swap(df_n);
+    ns->st_df_facet.swap(df_f);
   }
   return FG_OK;
 }

@@ -359,26 +359,39 @@ def build_corpus(seed, n):
     return recs
 
 
-def oracle_of(recs):
-    """Token-id CSR + deleted mask restated in Python from the reference semantics."""
-    from oracle import oracle as orc
-    dic, text, name, ids, deleted = {}, [], [], [], []
-
-    def intern(s):
-        return [dic.setdefault(t, len(dic)) for t in py_analyze(s)]
-    for rid, t, meta in recs:
+def deleted_of(recs):
+    """Upsert semantics (src/db/document.rs:38-42): a record deletes every earlier
+    doc whose tokenized id holds the RAW new id as a token."""
+    ids, deleted = [], []
+    for rid, _, _ in recs:
         for j, toks in enumerate(ids):
             if rid in toks:
                 deleted[j] = 1
+        ids.append(py_analyze(rid))
+        deleted.append(0)
+    return deleted
+
+
+def oracle_of(recs, keep=None):
+    """Token-id CSR + deleted mask restated in Python from the reference semantics.
+    keep: the global ids of the docs the index holds (a merge dropped the rest),
+    in order; None = all of them."""
+    from oracle import oracle as orc
+    deleted = deleted_of(recs)
+    keep = list(range(len(recs))) if keep is None else keep
+    dic, text, name = {}, [], []
+
+    def intern(s):
+        return [dic.setdefault(t, len(dic)) for t in py_analyze(s)]
+    for g in keep:
+        _, t, meta = recs[g]
         text.append(intern(t))
         nm = meta.get("name") if meta else None
         name.append(intern(nm) if isinstance(nm, str) else [])
-        ids.append(py_analyze(rid))
-        deleted.append(0)
     from conftest import tokens_to_csr
     to, tt = tokens_to_csr(text)
     no, nt = tokens_to_csr(name)
-    ix = orc.OracleIndex(max(1, len(dic)), to, tt, no, nt, np.array(deleted, np.uint8))
+    ix = orc.OracleIndex(max(1, len(dic)), to, tt, no, nt, np.array([deleted[g] for g in keep], np.uint8))
     return ix, dic
 
 
@@ -560,9 +573,10 @@ def test_json_shapes_with_hits_and_canonical_metadata(db):
 def test_db_incremental_commits_segments_vs_oracle(db):
     """A commit per 200 upserts: each commit adds a segment and rescores the
     older ones with the new statistics (fg_index_rescore); the ninth merges all
-    into one segment.  After every commit the paged AND / OR results equal the
-    oracle run over the same segments (per-segment intersection order,
-    namespace-wide statistics), bit for bit."""
+    into one segment that, like a tantivy merge, drops the deleted docs (N, df
+    and token totals then count the alive docs only).  After every commit the
+    paged AND / OR results equal the oracle run over the same segments
+    (per-segment intersection order, namespace-wide statistics), bit for bit."""
     from fugu_amd import native
     if native.device_count() == 0:
         pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
@@ -570,16 +584,23 @@ def test_db_incremental_commits_segments_vs_oracle(db):
     d = db.Database(ctx)
     d.create_namespace("inc")
     recs = build_corpus(11, 2400)
-    bounds = [0]  # segment boundaries of the model (mirror of the host's merge policy)
+    segs = []  # the model's segments: global doc ids each (mirror of the host's merge policy)
     rng = random.Random(5)
-    checked = 0
+    checked = merged_dropped = 0
     for c in range(0, len(recs), 200):
         for rid, t, meta in recs[c:c + 200]:
             d.upsert(db.ObjectRecord(rid, t, metadata=meta), "inc")
         d.commit("inc")
         n = c + 200
-        bounds = [0, n] if len(bounds) - 1 + 1 > 8 else bounds + [n]
-        ix, dic = oracle_of(recs[:n])
+        if len(segs) + 1 > 8:
+            dele = deleted_of(recs[:n])
+            segs = [[g for g in range(n) if not dele[g]]]
+            merged_dropped = n - len(segs[0])
+        else:
+            segs.append(list(range(c, n)))
+        keep = [g for sg in segs for g in sg]
+        bounds = list(np.cumsum([0] + [len(sg) for sg in segs]))
+        ix, dic = oracle_of(recs[:n], keep)
         for _ in range(12):
             m = rng.randint(1, 4)
             ws = [rng.choice(WORDS) for _ in range(m)]
@@ -589,8 +610,46 @@ def test_db_incremental_commits_segments_vs_oracle(db):
             got = d.search("inc", q, page, per_page)
             terms = [dic.get(t, native.FG_TERM_MISSING) for t in (py_analyze(w)[0] for w in ws)]
             s, dd = ix.search_segments(np.array(terms, np.uint32), (page + 1) * per_page, bounds, mode=mode)
-            want = hits_of(s, dd)[page * per_page:]
+            want = [(keep[doc], bits) for doc, bits in hits_of(s, dd)[page * per_page:]]
             assert hits_of([g[0] for g in got], [g[1] for g in got]) == want, (n, q, bounds)
             checked += len(want)
         assert d.doc_count("inc")[0] == n
-    assert checked > 300
+    assert checked > 300 and merged_dropped > 0
+
+
+@pytest.mark.gpu
+def test_db_failed_commit_leaves_statistics_unchanged(db, monkeypatch):
+    """A commit whose device build fails (injected) changes nothing: the next
+    commit counts the same docs once, so scores equal the oracle's."""
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("ft")
+    recs = build_corpus(17, 900)
+    for rid, t, meta in recs[:300]:
+        d.upsert(db.ObjectRecord(rid, t, metadata=meta), "ft")
+    d.commit("ft")
+    for rid, t, meta in recs[300:600]:
+        d.upsert(db.ObjectRecord(rid, t, metadata=meta), "ft")
+    monkeypatch.setenv("FUGU_FAULT_INJECT", "commit_build")
+    with pytest.raises(native.FuguError):
+        d.commit("ft")
+    with pytest.raises(native.FuguError):
+        d.commit("ft")
+    monkeypatch.delenv("FUGU_FAULT_INJECT")
+    d.commit("ft")
+    ix, dic = oracle_of(recs[:600])
+    rng = random.Random(8)
+    checked = 0
+    for _ in range(30):
+        ws = [rng.choice(WORDS) for _ in range(rng.randint(1, 3))]
+        q = " AND ".join(ws) if rng.random() < 0.5 else " ".join(ws)
+        mode = 1 if (len(ws) > 1 and " AND " not in q) else 0
+        got = d.search("ft", q, 0, 20)
+        terms = [dic.get(py_analyze(w)[0], native.FG_TERM_MISSING) for w in ws]
+        s, dd = ix.search_segments(np.array(terms, np.uint32), 20, [0, 300, 600], mode=mode)
+        assert hits_of([g[0] for g in got], [g[1] for g in got]) == hits_of(s, dd), q
+        checked += len(got)
+    assert checked > 50
