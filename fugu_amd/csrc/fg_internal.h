@@ -73,6 +73,10 @@ constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #define FG_DISJ_MAXGROUP 32
 #endif
 constexpr uint32_t kDisjMaxGroup = FG_DISJ_MAXGROUP;  // ... at most this many tiles per work item
+#ifndef FG_EXHMIN
+#define FG_EXHMIN 1024
+#endif
+constexpr uint32_t kExhaustiveMin = FG_EXHMIN;  // k_disj: all-essential tiles with fewer postings go posting-driven
 constexpr uint32_t kNumTopK = 4;          // per-term K-th best scores kept for these K
 constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 100, 1000};
 
@@ -82,6 +86,21 @@ constexpr uint32_t kScanMaxGroup = 32;    // k_scan: at most this many 4096-doc 
 
 constexpr uint32_t kModeAnd = 0;
 constexpr uint32_t kModeOr = 1;
+
+// Per-query running-threshold histograms (DevPlan::hist): every work item adds
+// the exact scores of the hits it keeps; the largest bin edge with at least k
+// counted docs at or above it is a lower bound of the query's k-th best score
+// across ALL the query's work items (and across the shards of a linked group).
+constexpr uint32_t kQBins = 512;
+
+// DevPlan::q_m packing: bits 0-7 terms in q_terms, 8-15 Must clauses (k_conj
+// queries; 0 for k_disj queries), 16-23 MustNot clauses.  q_terms holds, per
+// query, k_conj: [Must (cost order)][MustNot][Should (clause order)];
+// k_disj: [Should (clause order)][MustNot].
+__host__ __device__ inline uint32_t qm_terms(uint32_t qm) { return qm & 0xFFu; }
+__host__ __device__ inline uint32_t qm_must(uint32_t qm) { return (qm >> 8) & 0xFFu; }
+__host__ __device__ inline uint32_t qm_not(uint32_t qm) { return (qm >> 16) & 0xFFu; }
+__host__ __device__ inline uint32_t qm_pack(uint32_t m, uint32_t nm, uint32_t nx) { return m | (nm << 8) | (nx << 16); }
 
 // tmeta of a term: bits 0-7 = B_t (bucket shift), 8-15 = S_t (search steps),
 // 16-30 = dense slot + 1 (0: none), bit 31 = the slot's kind (1: rank words, 0: f32 table)
@@ -166,11 +185,11 @@ __host__ __device__ inline uint32_t filter_bits(const uint32_t* mask, uint32_t s
 // segments of hot posting lists they probe are shared through L2 / MALL.
 struct DevPlan {
   uint32_t n_queries;
-  uint32_t total_chunks;
+  uint32_t total_chunks;        // k_conj items [0, n_conj) then k_disj items [n_conj, total_chunks)
   uint32_t k;
-  uint32_t mode;
-  const uint32_t* q_m;          // [nq] terms per query
-  const uint32_t* q_terms;      // [nq * kMaxTerms] term ids, intersection (cost) order
+  uint32_t n_conj;
+  const uint32_t* q_m;          // [nq] packed term counts (qm_terms / qm_must / qm_not)
+  const uint32_t* q_terms;      // [nq * kMaxTerms] term ids (layout: qm_pack above)
   const uint32_t* q_lead_df;    // [nq] length of the lead list (0 => empty result)
   const uint32_t* work_q;       // [total_chunks] query of each work item (sweep order)
   const uint32_t* work_c;       // [total_chunks] first chunk of the item's group (k_disj: first tile)
@@ -179,8 +198,12 @@ struct DevPlan {
   const uint64_t* q_thr0;       // [nq] starting threshold key (k_disj: per-term top-K bound), 0 = none
   const float* q_ub;            // [nq * kMaxTerms] k_conj MaxScore bounds: q_ub[i] = sum over the query's
                                 //     terms j >= i (intersection order) of tmaxs, i >= 1
-  // workspace, zeroed per run
-  uint64_t* thresh;             // [nq] monotone lower bound on the k-th best key
+  const uint32_t* q_hlo;        // [nq] f32 bits of the histogram's bin 0 lower edge
+  const uint32_t* q_hsh;        // [nq] bin width: 2^q_hsh f32 ulps
+  // workspace, zeroed per run (thresh and hist may be a linked group's shared ones)
+  uint64_t* thresh;             // [nq] monotone lower bound on the k-th best key (published score-only)
+  uint32_t* hist;               // [nq * kQBins] counted hits per score bin
+  uint64_t pub_mask;            // thresholds published as key & pub_mask: ~0 exact, or score-only (linked)
   uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list
   uint64_t* cand_keys;          // [cand_off[nq]] per-query candidate lists
   uint64_t* diag;               // diagnostic builds only (-DFG_DIAG): per-workgroup stamps

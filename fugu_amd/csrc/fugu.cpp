@@ -103,6 +103,14 @@ float term_score_host(uint32_t tfp, uint32_t fn_t, uint32_t fn_n, float wt, floa
   return s;
 }
 
+// Bin width (2^shift f32 ulps) of a query score histogram spanning the f32
+// bit patterns [lo, hi] in fewer than kQBins bins (DevPlan::hist).
+uint32_t bin_shift(uint32_t lo, uint32_t hi) {
+  uint32_t sh = 0;
+  while (sh < 31 && ((uint64_t)(hi - lo) >> sh) >= fg::kQBins - 1) ++sh;
+  return sh;
+}
+
 // FUGU_BUILD_TRACE=1: per-phase wall time of a snapshot build on stderr
 struct BuildTrace {
   bool on = false;
@@ -407,6 +415,7 @@ struct fg_plan {
     if (ix) fg_index_release(ix);
   }
   bool last_stream_used = false;
+  std::vector<uint32_t> h_lo, h_hi;  // per query: f32 bits spanned by its score histogram (fg_plan_link)
   bool zeroed = false;        // the zero region arrived zeroed with the upload: the first execute skips its memset
   void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
   size_t pin_n = 0;
@@ -1014,6 +1023,12 @@ int fg_ctx_destroy(fg_ctx* ctx) {
   return FG_OK;
 }
 
+int fg_ctx_peer_access(const fg_ctx* ctx, int a, int b, int* enabled) {
+  if (!ctx || !enabled) return fail(FG_EINVAL, "bad arguments");
+  *enabled = std::find(ctx->peers.begin(), ctx->peers.end(), std::make_pair(a, b)) != ctx->peers.end() ? 1 : 0;
+  return FG_OK;
+}
+
 int fg_index_build_from_docs(fg_ctx* ctx, int dev, const fg_docs_input* in, fg_index** out) {
   return fg_index_build_from_docs_global(ctx, dev, in, nullptr, out);
 }
@@ -1485,19 +1500,37 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   if (f_woff[nf] * 4 > (8ull << 30)) return fail(FG_EUNSUPPORTED, "facet masks of this batch exceed 8 GiB");
   if (ch_f.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "facet postings of this batch too large");
 
-  // work items: each query's chunks (AND) or doc tiles (OR) in ~kGroupsPerQuery
-  // groups, ordered as a doc sweep across the batch (a group centred at doc
-  // fraction x runs with the other queries' groups near x), ties by query.
-  // Queries without text terms (facet-only / AllQuery) scan doc tiles (k_scan).
+  // work items: each query's chunks (Must-driven: k_conj) or doc tiles (Should
+  // only: k_disj) in ~kGroupsPerQuery groups, ordered as a doc sweep across the
+  // batch (a group centred at doc fraction x runs with the other queries'
+  // groups near x), ties by query.  Queries without text terms (facet-only /
+  // AllQuery) scan doc tiles (k_scan).  Per-term occurs (q->occur) make a
+  // query Must-driven when it has a Must clause (RequiredOptionalScorer over
+  // its Shoulds), a union of its Shoulds otherwise; MustNot clauses exclude.
   struct W { double key; uint32_t q, c, n; };
-  std::vector<W> items, scan;
-  std::vector<uint32_t> ngroup(nq, 0);
+  std::vector<W> citems, ditems, scan;
+  std::vector<uint32_t> ngroup(nq, 0), q_hlo(nq, 0x3F800000u), q_hhi(nq, 0x3F800000u), q_hsh(nq, 31);
+  auto present = [&](uint32_t t) { return t < ix->n_terms && ix->off[t + 1] > ix->off[t]; };
+  // histogram bins of query i: bin 0 at the starting threshold (or ub / 256), the
+  // top bin at the query's largest possible score ub; ~kQBins bins between
+  auto set_bins = [&](uint32_t i, float ub) {
+    const float lo = thr0[i] ? fg::key_score(thr0[i]) : ub / 256.0f;
+    uint32_t lb, hb;
+    std::memcpy(&lb, &lo, 4);
+    std::memcpy(&hb, &ub, 4);
+    lb = std::max<uint32_t>(lb, 1);
+    hb = std::max(hb, lb);
+    q_hlo[i] = lb;
+    q_hhi[i] = hb;
+    q_hsh[i] = bin_shift(lb, hb);
+  };
   for (uint32_t i = 0; i < nq; ++i) {
     const uint32_t b = q->q_off[i], e = q->q_off[i + 1];
     if (e < b) return fail(FG_EINVAL, "q_off not monotone at query %u", i);
     const uint32_t m = e - b;
     if (m > fg::kMaxTerms) return fail(FG_EUNSUPPORTED, "query %u has %u terms (> %u)", i, m, fg::kMaxTerms);
     if (q_nomatch[i]) continue;  // the facet clauses match nothing: no hits
+    const float fmx = q_filter[i] == 0xFFFFFFFFu ? 0.0f : f_max[q_filter[i]];
     if (m == 0) {
       // empty text query: the facet union alone, or AllQuery (src/db/search.rs:115-116, 131-137)
       q_m[i] = 0;
@@ -1514,34 +1547,58 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
       for (uint32_t g = 0; g < ng; ++g) scan.push_back(W{(double)g, i, tlo + g * G, std::min(G, nt - g * G)});
       continue;
     }
-    if (disj) {
-      // Should clauses in clause order (SumCombiner order); a clause on a term
-      // absent from the snapshot matches nothing and is dropped
-      uint32_t mm = 0, dlo = 0xFFFFFFFFu, dhi = 0;
-      for (uint32_t j = 0; j < m; ++j) {
-        const uint32_t t = q->terms[b + j];
-        if (t >= ix->n_terms || ix->off[t + 1] == ix->off[t]) continue;
-        q_terms[(size_t)i * fg::kMaxTerms + mm++] = t;
-        dlo = std::min(dlo, ix->first_doc[t]);
-        dhi = std::max(dhi, ix->last_doc[t]);
+    // the query's clauses by occur; a Should or MustNot clause on a term the
+    // snapshot lacks matches nothing and is dropped; a missing Must empties it
+    uint32_t tm[fg::kMaxTerms], ts_[fg::kMaxTerms], tx[fg::kMaxTerms];
+    uint32_t nm = 0, ns = 0, nx = 0;
+    bool must_missing = false;
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint32_t t = q->terms[b + j];
+      const uint8_t oc = q->occur ? q->occur[b + j] : (disj ? FG_OCCUR_SHOULD : FG_OCCUR_MUST);
+      if (oc > FG_OCCUR_MUST_NOT) return fail(FG_EINVAL, "query %u: bad occur %u", i, (unsigned)oc);
+      if (oc == FG_OCCUR_MUST) {
+        tm[nm++] = t;
+        must_missing |= !present(t);
+      } else if (present(t)) {
+        (oc == FG_OCCUR_SHOULD ? ts_[ns++] : tx[nx++]) = t;
       }
-      q_m[i] = mm;
-      if (!mm) continue;
+    }
+    // one positive clause: the union of one Should IS that clause, so it runs
+    // Must-driven (k_conj's single-list and exclusion paths); same docs, same score
+    if (nm == 0 && ns == 1) {
+      tm[nm++] = ts_[0];
+      ns = 0;
+    }
+    uint32_t* qt = q_terms.data() + (size_t)i * fg::kMaxTerms;
+    if (nm == 0) {
+      if (ns == 0) continue;  // no positive clause: EmptyScorer, no hits
+      // Should clauses in clause order (SumCombiner order), then the MustNots
+      uint32_t dlo = 0xFFFFFFFFu, dhi = 0;
+      for (uint32_t j = 0; j < ns; ++j) {
+        qt[j] = ts_[j];
+        dlo = std::min(dlo, ix->first_doc[ts_[j]]);
+        dhi = std::max(dhi, ix->last_doc[ts_[j]]);
+      }
+      for (uint32_t j = 0; j < nx; ++j) qt[ns + j] = tx[j];
+      q_m[i] = fg::qm_pack(ns + nx, 0, nx);
       if (q_filter[i] != 0xFFFFFFFFu) {
         dlo = std::max(dlo, f_lo[q_filter[i]]);
         dhi = std::min(dhi, f_hi[q_filter[i]]);
         if (dlo > dhi) continue;  // the text and facet doc spans do not meet
       }
       // starting threshold: the best per-clause K'-th score for the smallest stored
-      // K' >= k (unfiltered only: a filter may remove a term's best docs)
-      for (uint32_t j = 0; j < fg::kNumTopK && q_filter[i] == 0xFFFFFFFFu; ++j) {
+      // K' >= k (unfiltered and unexcluded only: a filter or an exclusion may
+      // remove a term's best docs)
+      for (uint32_t j = 0; j < fg::kNumTopK && q_filter[i] == 0xFFFFFFFFu && nx == 0; ++j) {
         if (fg::kTopKs[j] < k) continue;
         float v = 0.0f;
-        for (uint32_t c = 0; c < mm; ++c)
-          v = std::max(v, ix->ktop[(size_t)q_terms[(size_t)i * fg::kMaxTerms + c] * fg::kNumTopK + j]);
+        for (uint32_t c = 0; c < ns; ++c) v = std::max(v, ix->ktop[(size_t)qt[c] * fg::kNumTopK + j]);
         if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
         break;
       }
+      float ub = fmx;
+      for (uint32_t c = 0; c < ns; ++c) ub += ix->tmaxs[qt[c]];
+      set_bins(i, ub);
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
       const uint32_t G = std::min<uint32_t>(fg::kDisjMaxGroup,
@@ -1551,31 +1608,30 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
       for (uint32_t g = 0; g < ng; ++g) {
         const uint32_t t0 = tlo + g * G, n = std::min(G, nt - g * G);
         const double mid = ((double)t0 + 0.5 * n) * (double)(1u << fg::kDisjTileShift) / (double)ix->n_docs;
-        items.push_back(W{mid, i, t0, n});
+        ditems.push_back(W{mid, i, t0, n});
       }
-      if (items.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", items.size());
+      if (ditems.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", ditems.size());
       continue;
     }
-    // tantivy intersect_scorers: children sorted by cost (union cost = df_text + df_name), stable
+    if (must_missing) continue;  // a Must clause matches nothing: no hits
+    // tantivy intersect_scorers: the Must children sorted by cost (union cost =
+    // df_text + df_name), stable; then the MustNots, then the Shoulds in clause order
     struct T { uint64_t cost; uint32_t pos, term; };
-    T ts[fg::kMaxTerms];
-    bool missing = false;
-    for (uint32_t j = 0; j < m; ++j) {
-      const uint32_t t = q->terms[b + j];
-      uint64_t cost = 0;
-      if (t >= ix->n_terms) missing = true; else cost = (uint64_t)ix->df_text[t] + ix->df_name[t];
-      if (cost == 0) missing = true;
-      ts[j] = T{cost, j, t};
-    }
-    std::stable_sort(ts, ts + m, [](const T& x, const T& y) { return x.cost < y.cost; });
-    q_m[i] = m;
-    for (uint32_t j = 0; j < m; ++j) q_terms[(size_t)i * fg::kMaxTerms + j] = missing ? 0 : ts[j].term;
+    T tc[fg::kMaxTerms];
+    for (uint32_t j = 0; j < nm; ++j) tc[j] = T{(uint64_t)ix->df_text[tm[j]] + ix->df_name[tm[j]], j, tm[j]};
+    std::stable_sort(tc, tc + nm, [](const T& x, const T& y) { return x.cost < y.cost; });
+    for (uint32_t j = 0; j < nm; ++j) qt[j] = tc[j].term;
+    for (uint32_t j = 0; j < nx; ++j) qt[nm + j] = tx[j];
+    for (uint32_t j = 0; j < ns; ++j) qt[nm + nx + j] = ts_[j];
+    const uint32_t mt = nm + nx + ns;
+    q_m[i] = fg::qm_pack(mt, nm, nx);
     // MaxScore suffix bounds of the probed lists (k_conj prunes a candidate once its
-    // partial score plus these cannot reach the query's threshold)
-    if (!missing) {
+    // partial score plus these cannot reach the query's threshold): the Must and
+    // Should maxima from position j on (MustNots add nothing)
+    {
       float acc = 0.0f;
-      for (uint32_t j = m; j-- > 1;) {
-        acc += ix->tmaxs[ts[j].term];
+      for (uint32_t j = mt; j-- > 1;) {
+        if (j < nm || j >= nm + nx) acc += ix->tmaxs[qt[j]];
         q_ub[(size_t)i * fg::kMaxTerms + j] = acc;
       }
     }
@@ -1583,17 +1639,23 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
     // the query's k-th best from below, so k_conj starts from that threshold and
     // skips the lead chunks whose block-max cannot reach it (the block-max
     // pruning tantivy's TopDocs runs on a single TermScorer: block_wand_single_scorer)
-    for (uint32_t j = 0; j < fg::kNumTopK && !missing && m == 1 && q_filter[i] == 0xFFFFFFFFu; ++j) {
+    for (uint32_t j = 0; j < fg::kNumTopK && mt == 1 && q_filter[i] == 0xFFFFFFFFu; ++j) {
       if (fg::kTopKs[j] < k) continue;
-      const float v = ix->ktop[(size_t)ts[0].term * fg::kNumTopK + j];
+      const float v = ix->ktop[(size_t)qt[0] * fg::kNumTopK + j];
       if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
       break;
     }
-    const uint64_t df0 = missing ? 0 : ix->off[ts[0].term + 1] - ix->off[ts[0].term];
+    {
+      float ub = fmx + ix->tmaxs[qt[0]];
+      for (uint32_t j = 1; j < mt; ++j)
+        if (j < nm || j >= nm + nx) ub += ix->tmaxs[qt[j]];
+      set_bins(i, ub);
+    }
+    const uint64_t df0 = ix->off[qt[0] + 1] - ix->off[qt[0]];
     lead[i] = (uint32_t)df0;
     nchunk[i] = (uint32_t)((df0 + fg::kChunk - 1) / fg::kChunk);
-    if (items.size() + nchunk[i] > 0x7FFFFFFFull)
-      return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", items.size());
+    if (citems.size() + nchunk[i] > 0x7FFFFFFFull)
+      return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", citems.size());
     const uint32_t nch = nchunk[i];
     // items per query: ~kConjGroupsPerQuery in a full batch; a small batch (a
     // batch of one: the p50 latency) spreads a query over up to 64 items so its
@@ -1604,34 +1666,42 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;
     for (uint32_t g = 0; g < ng; ++g)
-      items.push_back(W{(g + 0.5) / ng, i, g * G, std::min(G, nch - g * G)});
+      citems.push_back(W{(g + 0.5) / ng, i, g * G, std::min(G, nch - g * G)});
   }
-  // AND: single-list queries' items first (their own k_conj launch), each part in sweep order.
-  // A stable LSD radix sort on (not single, key quantized to 31 bits): the order
-  // is a scheduling choice only (every order gives the same hits), and it takes
-  // a fraction of a comparison sort's host time on a 20K-item batch.
-  auto single = [&](const W& x) { return !disj && q_m[x.q] == 1; };
-  {
+  // k_conj: single-list queries' items first (their own k_conj launch), each part
+  // in sweep order; k_disj: sweep order.  A stable LSD radix sort on (not single,
+  // key quantized to 31 bits): the order is a scheduling choice only (every
+  // order gives the same hits), and it takes a fraction of a comparison sort's
+  // host time on a 20K-item batch.
+  auto single = [&](const W& x) { return q_m[x.q] == fg::qm_pack(1, 1, 0); };
+  auto radix = [&](std::vector<W>& items, bool conj) {
     const size_t n = items.size();
-    std::vector<uint64_t> a(n), b(n);  // (sort key << 32) | item index
+    std::vector<uint64_t> a(n), bb(n);  // (sort key << 32) | item index
     for (size_t x = 0; x < n; ++x) {
       const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
-      const uint32_t rk = (single(items[x]) ? 0u : 0x80000000u) | (uint32_t)(kk * 2147483647.0);
+      const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | (uint32_t)(kk * 2147483647.0);
       a[x] = ((uint64_t)rk << 32) | (uint64_t)x;
     }
     for (int sh = 32; sh < 64; sh += 11) {
       uint32_t cnt[2049] = {0};
       for (size_t x = 0; x < n; ++x) cnt[((a[x] >> sh) & 2047u) + 1]++;
       for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
-      for (size_t x = 0; x < n; ++x) b[cnt[(a[x] >> sh) & 2047u]++] = a[x];
-      a.swap(b);
+      for (size_t x = 0; x < n; ++x) bb[cnt[(a[x] >> sh) & 2047u]++] = a[x];
+      a.swap(bb);
     }
     std::vector<W> sorted(n);
     for (size_t x = 0; x < n; ++x) sorted[x] = items[(uint32_t)a[x]];
     items.swap(sorted);
-  }
+  };
+  radix(citems, true);
+  radix(ditems, false);
+  std::vector<W> items;
+  items.reserve(citems.size() + ditems.size() + scan.size());
+  items.insert(items.end(), citems.begin(), citems.end());
+  const uint64_t n_conj = citems.size();
+  items.insert(items.end(), ditems.begin(), ditems.end());
   uint64_t n_single = 0;
-  for (const W& x : items) n_single += single(x) ? 1 : 0;
+  for (const W& x : citems) n_single += single(x) ? 1 : 0;
   std::stable_sort(scan.begin(), scan.end(), [](const W& a, const W& b) { return a.key < b.key; });
   const uint64_t n_main = items.size(), n_scan = scan.size();
   const uint64_t chunks = n_main + n_scan;  // from here on: work items (k_conj / k_disj, then k_scan)
@@ -1661,10 +1731,14 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
                s_wq = al(4ull * chunks), s_wc = al(4ull * chunks), s_wn = al(4ull * chunks),
                s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq), s_ub = al(4ull * nq * fg::kMaxTerms),
                s_qf = al(4ull * nq), s_fs = al(4ull * nf),
-               s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch);
-  const size_t s_in =
-      s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft + s_fm + 4 * s_ch;
-  const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]);
+               s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch),
+               s_hb = al(4ull * nq);
+  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft +
+                      s_fm + 4 * s_ch + 2 * s_hb;
+  // score histograms only for the queries of k_disj work items (k_conj keeps
+  // its per-item thresholds)
+  const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]),
+               s_hist = al(4ull * nq * fg::kQBins);
   const size_t s_ck = al(8ull * cand_off[nq]);
   const size_t s_os = al(4ull * nq * k), s_od = al(4ull * nq * k), s_on = al(4ull * nq);
 #ifdef FG_DIAG
@@ -1672,7 +1746,7 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
 #else
   const size_t s_dg = 0;
 #endif
-  const size_t total = s_in + s_thr + s_cc + s_mask + s_ck + s_os + s_od + s_on + s_dg;
+  const size_t total = s_in + s_thr + s_cc + s_mask + s_hist + s_ck + s_os + s_od + s_on + s_dg;
   HIPCHK(hipSetDevice(ix->dev));
   char* base = static_cast<char*>(ix->pool.get(std::max<size_t>(total, 256), &p->ws_got));
   if (!base) return fail(FG_EOOM, "plan workspace hipMalloc(%zu) failed", total);
@@ -1682,7 +1756,7 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   p->ws_bytes = total;
   // a small zero region (thresholds, candidate counts, facet masks) travels
   // zeroed with the upload, so the first execute needs no memset
-  const size_t s_zero = s_thr + s_cc + s_mask;
+  const size_t s_zero = s_thr + s_cc + s_mask + s_hist;
   const size_t s_up = s_in + (s_zero <= (64u << 10) ? s_zero : 0);
   PinnedLease pin(ix->pinned, s_up);
   std::vector<char> staging_pageable;  // only if the pinned allocation failed
@@ -1718,6 +1792,8 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   p->d.f.ch_clause = (const uint32_t*)put(ch_c.data(), 4ull * nch, s_ch);
   p->d.f.ch_term = (const uint32_t*)put(ch_t.data(), 4ull * nch, s_ch);
   p->d.f.ch_start = (const uint32_t*)put(ch_s.data(), 4ull * nch, s_ch);
+  p->d.q_hlo = (const uint32_t*)put(q_hlo.data(), 4ull * nq, s_hb);
+  p->d.q_hsh = (const uint32_t*)put(q_hsh.data(), 4ull * nq, s_hb);
   // on the planning thread's own stream: a plan built while another thread's
   // batch runs does not serialise against it through the legacy null stream
   HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, hipStreamPerThread));
@@ -1731,13 +1807,15 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   }
   char* cur = base + s_in;
   p->zero_region = cur;
-  p->zero_bytes = s_thr + s_cc + s_mask;
+  p->zero_bytes = s_zero;
   p->d.thresh = (uint64_t*)cur;
   cur += s_thr;
   p->d.cand_cnt = (uint32_t*)cur;
   cur += s_cc;
   p->d.f.fmask = (uint32_t*)cur;
   cur += s_mask;
+  p->d.hist = (uint32_t*)cur;
+  cur += s_hist;
   p->d.cand_keys = (uint64_t*)cur;
   cur += s_ck;
   p->own_score = (float*)cur;
@@ -1750,10 +1828,13 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   p->diag_words = s_dg / 8;
   p->d.n_queries = nq;
   p->d.total_chunks = (uint32_t)n_main;
+  p->d.n_conj = (uint32_t)n_conj;
   p->d.n_scan = (uint32_t)n_scan;
   p->d.n_single = (uint32_t)n_single;
   p->d.k = k;
-  p->d.mode = (uint32_t)q->mode;
+  p->d.pub_mask = ~0ull;
+  p->h_lo.swap(q_hlo);
+  p->h_hi.swap(q_hhi);
   p->d.f.n_filters = nf;
   p->d.f.n_chunks = (uint32_t)nch;
   *out = p.release();
@@ -1775,8 +1856,8 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
     HIPCHK(hipEventRecord(ev[0], s));
   }
   if (p->d.f.n_chunks) HIPCHK(fg::launch_fmask(p->ix->d, p->d, s));
-  if (p->mode == FG_MODE_OR) HIPCHK(fg::launch_disj(p->ix->d, p->d, s));
-  else HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
+  if (p->d.n_conj) HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
+  if (p->d.total_chunks > p->d.n_conj) HIPCHK(fg::launch_disj(p->ix->d, p->d, s));
   if (p->d.n_scan) HIPCHK(fg::launch_scan(p->ix->d, p->d, s));
   if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
   HIPCHK(fg::launch_final(p->d, os, od, on, s));
@@ -1868,6 +1949,44 @@ int fg_plan_diag(fg_plan* p, uint64_t* out, size_t n_words, uint32_t* cand_cnt) 
 
 int fg_plan_destroy(fg_plan* p) {
   delete p;
+  return FG_OK;
+}
+
+// One per-query threshold word and score histogram for plans of one batch on
+// one device (fugu.h).  Every plan's bins are re-drawn over the union of the
+// plans' score spans, so a bin means the same scores in every plan.
+int fg_plan_link(fg_plan* const* plans, uint32_t n) {
+  if (!plans || n == 0) return fail(FG_EINVAL, "bad arguments");
+  fg_plan* o = plans[0];
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!plans[i]) return fail(FG_EINVAL, "NULL plan");
+    if (plans[i]->nq != o->nq || plans[i]->k != o->k) return fail(FG_EINVAL, "linked plans differ in batch or k");
+    if (plans[i]->ix->dev != o->ix->dev) return fail(FG_EINVAL, "linked plans live on different devices");
+  }
+  const uint32_t nq = o->nq;
+  std::vector<uint32_t> lo(nq, 0), sh(nq, 0);
+  for (uint32_t q = 0; q < nq; ++q) {
+    uint32_t l = 0, h = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      l = std::max(l, plans[i]->h_lo[q]);
+      h = std::max(h, plans[i]->h_hi[q]);
+    }
+    h = std::max(h, l);
+    lo[q] = l;
+    sh[q] = bin_shift(l, h);
+  }
+  HIPCHK(hipSetDevice(o->ix->dev));
+  for (uint32_t i = 0; i < n; ++i) {
+    fg_plan* p = plans[i];
+    if (nq) {
+      HIPCHK(hipMemcpy(const_cast<uint32_t*>(p->d.q_hlo), lo.data(), 4ull * nq, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(const_cast<uint32_t*>(p->d.q_hsh), sh.data(), 4ull * nq, hipMemcpyHostToDevice));
+    }
+    p->h_lo = lo;
+    p->d.thresh = o->d.thresh;
+    p->d.hist = o->d.hist;
+    p->d.pub_mask = 0xFFFFFFFF00000000ull;  // score-only
+  }
   return FG_OK;
 }
 
@@ -1982,16 +2101,69 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       for (uint32_t t = 0; t < s; ++t) nth += shards[t]->dev == shards[s]->dev ? 1u : 0u;
       if (!(sst[s] = side_stream(shards[s]->dev, nth % kSideStreams))) return fail(FG_EHIP, "side stream creation failed");
     }
-  auto run = [&](uint32_t s) -> int {  // plan, launch, move the lists to dev0, record the event
+  // 1. plan every shard (one host thread per shard for a batch)
+  auto plan = [&](uint32_t s) -> int {
     fg_plan* p = nullptr;
     int rc = fg_plan_create(shards[s], q, k, &p);
     if (rc) return rc;
     plans[s].reset(p);
+    return FG_OK;
+  };
+  auto each = [&](auto&& f) {
+    if (threaded) {
+      std::vector<std::thread> th;
+      for (uint32_t s = 0; s < n_shards; ++s)
+        th.emplace_back([&, s] {
+          rcs[s] = f(s);
+          if (rcs[s]) errs[s] = fg_last_error();
+        });
+      for (auto& x : th) x.join();
+    } else {
+      for (uint32_t s = 0; s < n_shards; ++s)
+        if ((rcs[s] = f(s))) errs[s] = fg_last_error();
+    }
+    for (uint32_t s = 0; s < n_shards; ++s)
+      if (rcs[s]) return fail(rcs[s], "shard %u: %s", s, errs[s].c_str());
+    return FG_OK;
+  };
+  if (int rc = each(plan)) return rc;
+  // 2. the shards of one device share per-query thresholds (fg_plan_link): the
+  // merge keeps the k best across shards, so a shard need not keep a doc below
+  // the k-th best score any shard has found.  The shared state is zeroed once,
+  // before any of the device's shards runs.
+  std::vector<hipEvent_t> zev;
+  struct ZevBack {
+    std::vector<hipEvent_t>& v;
+    ~ZevBack() { for (hipEvent_t e : v) (void)hipEventDestroy(e); }
+  } zback{zev};
+  std::vector<int> owner(n_shards, -1);
+  for (uint32_t s = 0; s < n_shards; ++s) {
+    if (owner[s] >= 0) continue;
+    std::vector<fg_plan*> grp{plans[s].get()};
+    owner[s] = (int)s;
+    for (uint32_t t = s + 1; t < n_shards; ++t)
+      if (shards[t]->dev == shards[s]->dev) { grp.push_back(plans[t].get()); owner[t] = (int)s; }
+    if (grp.size() < 2) continue;
+    if (int rc = fg_plan_link(grp.data(), (uint32_t)grp.size())) return rc;
+    fg_plan* o = plans[s].get();
+    HIPCHK(hipSetDevice(shards[s]->dev));
+    HIPCHK(hipMemsetAsync(o->zero_region, 0, o->zero_bytes, hipStreamPerThread));
+    o->zeroed = true;  // its execute skips the memset (it would wipe what the others share)
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    zev.push_back(e);
+    HIPCHK(hipEventRecord(e, hipStreamPerThread));
+    for (uint32_t t = s; t < n_shards; ++t)
+      if (owner[t] == (int)s && sst[t]) HIPCHK(hipStreamWaitEvent(sst[t], e, 0));
+  }
+  // 3. launch each shard, move its lists to dev0, record the event the merge waits for
+  auto run = [&](uint32_t s) -> int {
+    fg_plan* p = plans[s].get();
     const int d = shards[s]->dev;
     hipStream_t st = sst[s] ? sst[s] : hipStreamPerThread;
     const bool local = d == dev0;
-    rc = local ? fg_plan_execute(p, st, gs + s * nk, gd + s * nk, gn + (size_t)s * nq)
-               : fg_plan_execute(p, st, nullptr, nullptr, nullptr);  // selects device d
+    int rc = local ? fg_plan_execute(p, st, gs + s * nk, gd + s * nk, gn + (size_t)s * nq)
+                   : fg_plan_execute(p, st, nullptr, nullptr, nullptr);  // selects device d
     if (rc) return rc;
     if (!local) {
       HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score, d, 4 * nk, st));
@@ -2004,20 +2176,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     }
     return FG_OK;
   };
-  if (threaded) {
-    std::vector<std::thread> th;
-    for (uint32_t s = 0; s < n_shards; ++s)
-      th.emplace_back([&, s] {
-        rcs[s] = run(s);
-        if (rcs[s]) errs[s] = fg_last_error();
-      });
-    for (auto& x : th) x.join();
-  } else {
-    for (uint32_t s = 0; s < n_shards; ++s)
-      if ((rcs[s] = run(s))) errs[s] = fg_last_error();
-  }
-  for (uint32_t s = 0; s < n_shards; ++s)
-    if (rcs[s]) return fail(rcs[s], "shard %u: %s", s, errs[s].c_str());
+  if (int rc = each(run)) return rc;
   HIPCHK(hipSetDevice(dev0));
   for (hipEvent_t e : evs)
     if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
@@ -2171,6 +2330,138 @@ int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, 
       o[1] = probe;
       o[2] = 8.0 * (double)std::min<size_t>(cand.size(), k);  // the work item's kept keys
       o[3] = o[0] + o[1] + o[2];
+    }
+  });
+  if (bad) return fail(FG_EINVAL, "bad query batch");
+  return FG_OK;
+}
+
+// ---------------------------------------------------------------- OR bytes model at the device layout
+// k_disj's MaxScore with the pruning threshold fixed at thr[i] (the query's
+// final k-th best score: no exact MaxScore run can prune harder), replayed on
+// the host over this snapshot's layout:
+//   stream: per (tile, clause) 8 B of directory bounds + 4 B tile maximum; per
+//           essential posting of a posting-driven tile 8 B (doc + score); per
+//           posting of an exhaustive tile 8 B;
+//   probe : per posting past bound 1 (the other clauses' tile maxima), for every
+//           other clause with postings in the tile its rank word (8 B) or its
+//           bucket maximum (4 B); per posting past the presence bound 4 B per
+//           present rank clause's posting score; per candidate a non-dense
+//           clause's directory probe (8 B bounds + 4 B per search step + 4 B)
+//           and score (4 B on a hit);
+//   output: 8 B per kept key (<= k).
+int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, const float* thr, double* out) {
+  if (!ix || !q || !out || !thr || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
+  if (!ix->h_doc && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
+  std::vector<float> psc(ix->n_postings);
+  HIPCHK(hipSetDevice(ix->dev));
+  if (ix->n_postings) HIPCHK(hipMemcpy(psc.data(), ix->d.psc, 4ull * ix->n_postings, hipMemcpyDeviceToHost));
+  const uint32_t nq = q->n_queries, N = ix->n_docs;
+  const uint32_t TS = fg::kDisjTileShift, nt = (N + (1u << TS) - 1) >> TS;
+  const uint32_t* hd = ix->h_doc ? ix->h_doc->data() : nullptr;
+  std::atomic<bool> bad{false};
+  parallel_dynamic(nq, hw_threads(0), 1, [&](int, uint32_t qb, uint32_t qe) {
+    std::vector<float> tmx;
+    std::vector<uint32_t> tcnt;
+    std::vector<uint64_t> pres;  // presence bitmaps, one per clause
+    for (uint32_t i = qb; i < qe; ++i) {
+      double* o = out + 4ull * i;
+      o[0] = o[1] = o[2] = o[3] = 0.0;
+      const uint32_t b = q->q_off[i], e = q->q_off[i + 1];
+      if (e < b || e - b > fg::kMaxTerms) { bad = true; return; }
+      uint32_t t[fg::kMaxTerms], m = 0;
+      for (uint32_t j = b; j < e; ++j) {
+        const uint8_t oc = q->occur ? q->occur[j] : FG_OCCUR_SHOULD;
+        const uint32_t tt = q->terms[j];
+        if (oc == FG_OCCUR_SHOULD && tt < ix->n_terms && ix->off[tt + 1] > ix->off[tt]) t[m++] = tt;
+      }
+      if (!m) continue;
+      tmx.assign((size_t)nt * m, 0.0f);
+      tcnt.assign((size_t)nt * m, 0);
+      pres.assign((size_t)m * ((N + 63) / 64), 0);
+      for (uint32_t c = 0; c < m; ++c)
+        for (uint64_t p = ix->off[t[c]]; p < ix->off[t[c] + 1]; ++p) {
+          const uint32_t d = hd[p], ti = d >> TS;
+          tmx[(size_t)ti * m + c] = std::max(tmx[(size_t)ti * m + c], psc[p]);
+          tcnt[(size_t)ti * m + c]++;
+          pres[(size_t)c * ((N + 63) / 64) + (d >> 6)] |= 1ull << (d & 63);
+        }
+      const float th = thr[i];
+      const uint64_t thk = fg::make_key(th, 0xFFFFFFFFu);
+      double stream = 0, probe = 0;
+      std::vector<uint64_t> cur(m);
+      for (uint32_t c = 0; c < m; ++c) cur[c] = ix->off[t[c]];
+      for (uint32_t ti = 0; ti < nt; ++ti) {
+        float ub[fg::kMaxTerms];
+        uint32_t ord[fg::kMaxTerms], np = 0;
+        for (uint32_t c = 0; c < m; ++c) {
+          ub[c] = tcnt[(size_t)ti * m + c] ? tmx[(size_t)ti * m + c] : 0.0f;
+          np += tcnt[(size_t)ti * m + c];
+          uint32_t j = c;
+          while (j > 0 && ub[ord[j - 1]] > ub[c]) { ord[j] = ord[j - 1]; --j; }
+          ord[j] = c;
+        }
+        stream += 12.0 * m;  // R: directory bounds + tile maximum per clause
+        float sacc = 0.0f;
+        uint32_t P = 0;
+        for (; P < m; ++P) {
+          const float s2 = sacc + ub[ord[P]];
+          if (fg::make_key(s2 * 1.00000762939453125f, 0u) >= thk) break;
+          sacc = s2;
+        }
+        uint32_t ess = 0, npe = 0;
+        for (uint32_t j = P; j < m; ++j) {
+          ess |= 1u << ord[j];
+          npe += tcnt[(size_t)ti * m + ord[j]];
+        }
+        if (P == m || npe == 0) {
+          for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
+          continue;
+        }
+        if (P == 0 && np >= fg::kExhaustiveMin) {  // every clause essential: exhaustive LDS tile
+          stream += 8.0 * np;
+          for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
+          continue;
+        }
+        float ubsum = 0.0f;
+        for (uint32_t c = 0; c < m; ++c) ubsum += ub[c];
+        for (uint32_t c = 0; c < m; ++c) {
+          const uint64_t p0 = cur[c], p1 = p0 + tcnt[(size_t)ti * m + c];
+          cur[c] = p1;
+          if (!((ess >> c) & 1u)) continue;
+          for (uint64_t p = p0; p < p1; ++p) {
+            stream += 8.0;
+            const uint32_t d = hd[p];
+            if (fg::make_key((psc[p] + (ubsum - ub[c])) * 1.00000762939453125f, d) < thk) continue;
+            float pb = psc[p];
+            bool all_dense = true;
+            for (uint32_t c2 = 0; c2 < m; ++c2) {
+              if (c2 == c || !tcnt[(size_t)ti * m + c2]) continue;
+              const uint32_t meta = ix->tmeta[t[c2]];
+              const bool rank = fg::meta_slot(meta) && fg::meta_rank(meta);
+              const bool here = (pres[(size_t)c2 * ((N + 63) / 64) + (d >> 6)] >> (d & 63)) & 1ull;
+              probe += rank ? 8.0 : 4.0;
+              all_dense = all_dense && fg::meta_slot(meta);
+              if (here) pb += ub[c2];
+            }
+            if (fg::make_key(pb * 1.00000762939453125f, d) < thk) continue;
+            for (uint32_t c2 = 0; c2 < m; ++c2) {
+              if (c2 == c || !tcnt[(size_t)ti * m + c2]) continue;
+              const uint32_t meta = ix->tmeta[t[c2]];
+              const bool here = (pres[(size_t)c2 * ((N + 63) / 64) + (d >> 6)] >> (d & 63)) & 1ull;
+              if (fg::meta_slot(meta) && fg::meta_rank(meta)) probe += here ? 4.0 : 0.0;
+              else if (!all_dense && !fg::meta_slot(meta)) {
+                const uint32_t S = (meta >> 8) & 0xFFu;
+                probe += 8.0 + 4.0 * S + 4.0 + (here ? 4.0 : 0.0);
+              }
+            }
+          }
+        }
+      }
+      o[0] = stream;
+      o[1] = probe;
+      o[2] = 8.0 * k;
+      o[3] = stream + probe + o[2];
     }
   });
   if (bad) return fail(FG_EINVAL, "bad query batch");

@@ -131,13 +131,15 @@ void analyze(std::string_view s, std::vector<std::string>& out) {
 
 // ---------------------------------------------------------------- query parser subset
 // QueryParser::for_index(index, [text, name]).parse_query (src/db/search.rs:108-127)
-// restricted to what the device runs:
-//   `t1 t2 ...`                 default conjunction Should  -> FG_MODE_OR
-//   `t1 AND t2 AND ...`, `+t1 +t2`                          -> FG_MODE_AND
-//   `t1`                                                    -> single term
+// restricted to what the device runs (tantivy-query-grammar 0.24: the default
+// conjunction is Should, `+` Must, `-` MustNot, binary AND / OR):
+//   `t1 t2 -t3 +t4 ...`   each term's occur by its prefix (bare = Should)
+//   `t1 AND t2 AND ...`   every term Must
+//   `t1 OR t2 OR ...`     every term Should (the same query as `t1 t2 ...`)
 // Every term must analyze to exactly one token (more = PhraseQuery).  Anything
-// else is FG_EUNSUPPORTED (the reference host runs tantivy).  An empty query is
-// AllQuery (src/db/search.rs:115-116): unsupported on the device.
+// else (mixed AND / OR, parentheses, field:, phrases, boosts, ranges, a query
+// of MustNot clauses only) is FG_EUNSUPPORTED: the reference host runs tantivy.
+// An empty query is AllQuery (src/db/search.rs:115-116), handled by the caller.
 bool is_special(char c) {
   switch (c) {
     case '+': case '-': case '(': case ')': case '[': case ']': case '{': case '}': case '"': case ':':
@@ -149,8 +151,9 @@ bool is_special(char c) {
   }
 }
 
-int parse_query(std::string_view q, int* mode, std::vector<std::string>& terms, std::string& why) {
+int parse_query(std::string_view q, std::vector<std::string>& terms, std::vector<uint8_t>& occur, std::string& why) {
   terms.clear();
+  occur.clear();
   std::vector<std::string_view> words;
   size_t i = 0;
   while (i < q.size()) {
@@ -160,29 +163,32 @@ int parse_query(std::string_view q, int* mode, std::vector<std::string>& terms, 
     if (i > s) words.push_back(q.substr(s, i - s));
   }
   if (words.empty()) { why = "empty query (AllQuery)"; return FG_EUNSUPPORTED; }
-  std::vector<std::string_view> raw;
-  bool and_form = words.size() >= 3 && words.size() % 2 == 1;
-  for (size_t w = 1; and_form && w < words.size(); w += 2) and_form = words[w] == "AND";
-  bool plus_form = true;
-  for (auto w : words) plus_form = plus_form && w.size() > 1 && w[0] == '+';
-  if (and_form) {
-    *mode = FG_MODE_AND;
-    for (size_t w = 0; w < words.size(); w += 2) raw.push_back(words[w]);
-  } else if (plus_form) {
-    *mode = FG_MODE_AND;
-    for (auto w : words) raw.push_back(w.substr(1));
+  std::vector<std::pair<std::string_view, uint8_t>> raw;
+  auto binary_form = [&](std::string_view op) {
+    bool ok = words.size() >= 3 && words.size() % 2 == 1;
+    for (size_t w = 1; ok && w < words.size(); w += 2) ok = words[w] == op;
+    return ok;
+  };
+  if (binary_form("AND") || binary_form("OR")) {
+    const uint8_t oc = words[1] == "AND" ? FG_OCCUR_MUST : FG_OCCUR_SHOULD;
+    for (size_t w = 0; w < words.size(); w += 2) raw.emplace_back(words[w], oc);
   } else {
-    *mode = words.size() == 1 ? FG_MODE_AND : FG_MODE_OR;
-    raw = words;
+    for (auto w : words) {
+      if (w.size() > 1 && (w[0] == '+' || w[0] == '-'))
+        raw.emplace_back(w.substr(1), w[0] == '+' ? FG_OCCUR_MUST : FG_OCCUR_MUST_NOT);
+      else
+        raw.emplace_back(w, FG_OCCUR_SHOULD);
+    }
   }
-  for (auto w : raw) {
+  bool positive = false;
+  for (auto& [w, oc] : raw) {
     if (w == "AND" || w == "OR" || w == "NOT" || w == "IN" || w == "TO") {
       why = "operator outside the supported forms";
       return FG_EUNSUPPORTED;
     }
     for (char c : w)
       if (is_special(c)) {
-        why = "query syntax beyond bare/+/AND terms";
+        why = "query syntax beyond bare/+/-/AND/OR terms";
         return FG_EUNSUPPORTED;
       }
     std::vector<std::string> toks;
@@ -192,8 +198,24 @@ int parse_query(std::string_view q, int* mode, std::vector<std::string>& terms, 
       return FG_EUNSUPPORTED;
     }
     terms.push_back(std::move(toks[0]));
+    occur.push_back(oc);
+    positive |= oc != FG_OCCUR_MUST_NOT;
+  }
+  if (!positive) {
+    why = "MustNot clauses only";
+    return FG_EUNSUPPORTED;
   }
   return FG_OK;
+}
+
+// FG_MODE_AND / FG_MODE_OR when every clause is Must / Should, else FG_MODE_MIXED
+int mode_of(const std::vector<uint8_t>& occur) {
+  bool all_m = true, all_s = true;
+  for (uint8_t o : occur) {
+    all_m = all_m && o == FG_OCCUR_MUST;
+    all_s = all_s && o == FG_OCCUR_SHOULD;
+  }
+  return occur.size() == 1 ? FG_MODE_AND : all_m ? FG_MODE_AND : all_s ? FG_MODE_OR : FG_MODE_MIXED;
 }
 
 // ---------------------------------------------------------------- JSON helpers
@@ -691,12 +713,12 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
   hits.clear();
   if (per_page == 0) return hfail(FG_EINVAL, "TopDocs::with_limit requires limit >= 1");
   const std::string_view qv = query ? query : "";
-  int mode = FG_MODE_AND;
   std::vector<std::string> terms;
+  std::vector<uint8_t> occur;
   std::string why;
   const bool empty_text = blank(qv);  // query.trim().is_empty() -> AllQuery (src/db/search.rs:115-116)
   if (!empty_text) {
-    int rc = parse_query(qv, &mode, terms, why);
+    int rc = parse_query(qv, terms, occur, why);
     if (rc) return hfail(rc, "query outside the device subset: " + why);
   }
   std::vector<std::string> clauses;
@@ -734,7 +756,7 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
   for (const Segment& seg : snap->segs) segs.push_back(seg.ix);
   const uint32_t q_off[2] = {0, (uint32_t)ids.size()};
   const uint32_t f_off[2] = {0, (uint32_t)fids.size()};
-  fg_query_batch qb{1, q_off, ids.data(), mode, fids.empty() ? nullptr : f_off, fids.data()};
+  fg_query_batch qb{1, q_off, ids.data(), FG_MODE_AND, fids.empty() ? nullptr : f_off, fids.data(), occur.data()};
   std::vector<float> sc(limit);
   std::vector<uint32_t> dc(limit), sh(limit);
   uint32_t n = 0;
@@ -1385,12 +1407,31 @@ int fg_analyze(const char* text, char* out, size_t cap, size_t* len) {
 int fg_parse_query(const char* query, int* mode, char* out, size_t cap, size_t* len) {
   if (!query || !mode) return hfail(FG_EINVAL, "bad arguments");
   std::vector<std::string> terms;
+  std::vector<uint8_t> occur;
   std::string why;
-  int rc = parse_query(query, mode, terms, why);
+  int rc = parse_query(query, terms, occur, why);
+  if (rc) return hfail(rc, why);
+  *mode = mode_of(occur);
+  std::string o;
+  for (size_t i = 0; i < terms.size(); ++i) {
+    if (i) o.push_back('\n');
+    o += terms[i];
+  }
+  return copy_out(o, out, cap, len);
+}
+
+int fg_parse_query_occur(const char* query, char* out, size_t cap, size_t* len) {
+  if (!query) return hfail(FG_EINVAL, "bad arguments");
+  std::vector<std::string> terms;
+  std::vector<uint8_t> occur;
+  std::string why;
+  int rc = parse_query(query, terms, occur, why);
   if (rc) return hfail(rc, why);
   std::string o;
   for (size_t i = 0; i < terms.size(); ++i) {
     if (i) o.push_back('\n');
+    o.push_back((char)('0' + occur[i]));
+    o.push_back(':');
     o += terms[i];
   }
   return copy_out(o, out, cap, len);

@@ -77,6 +77,35 @@ __device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t t
   return toff != 0xFFFFFFFFu ? ix.tmax[toff + (d >> kDisjTileShift)] : ix.bmax[dir_off + (d >> (meta & 0xFFu))];
 }
 
+// Does term (meta, postings at base, directory at dir_off) hold doc d?  (MustNot probes)
+__device__ inline bool term_has_doc(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t dir_off, uint32_t d) {
+  const uint32_t slot = meta_slot(meta);
+  if (slot && meta_rank(meta)) return (ix.rank[(size_t)(slot - 1) * ix.rank_words + (d >> 5)] >> (d & 31u)) & 1ull;
+  if (slot) return ix.dense[(size_t)(slot - 1) * ix.n_docs + d] >= 0.0f;
+  const uint32_t* __restrict__ dir = ix.dir + dir_off;
+  const uint32_t b = d >> (meta & 0xFFu);
+  uint32_t lo = dir[b], hi = dir[b + 1];
+  const uint32_t* __restrict__ di = ix.doc + base;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (di[mid] < d) lo = mid + 1; else hi = mid;
+  }
+  return lo < dir[b + 1] && di[lo] == d;
+}
+
+// DevPlan::pub_mask: a linked group's shared thresholds are published
+// score-only (the lowest key with the score), so a doc of another shard or
+// namespace with an equal score is never pruned (the merge breaks ties by
+// shard); an unlinked plan publishes exact keys.
+
+// Histogram bin of a hit key for query bins (lo, sh), or kQBins (not counted:
+// below bin 0's edge).
+__device__ inline uint32_t qbin(uint64_t key, uint32_t lo, uint32_t sh) {
+  const uint32_t bits = (uint32_t)(key >> 32);
+  if (bits < lo) return kQBins;
+  return min((bits - lo) >> sh, kQBins - 1);
+}
+
 // ---------------------------------------------------------------- workgroup helpers
 // Exclusive prefix over the workgroup of one u32 per thread (256 threads).
 __device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* scratch /*[4]*/) {
@@ -94,6 +123,26 @@ __device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* scratch /*
   for (uint32_t i = 0; i < kThreads / 64; ++i) base += i < w ? scratch[i] : 0u;
   __syncthreads();
   return base + incl - v;
+}
+
+// The running threshold of query q from its score histogram: the lower edge of
+// the highest bin b with >= K counted docs in bins >= b (score-only key), or 0.
+// Relaxed agent-scope loads (sc1): the bins only grow, so a stale bin can only
+// lower the threshold.  Workgroup-uniform result; scratch[0..6] used.
+__device__ uint64_t hist_threshold(const uint32_t* gh, uint32_t K, uint32_t lo, uint32_t sh, uint32_t* scratch) {
+  static_assert(kQBins == 2 * kThreads, "two bins per thread");
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = kQBins - 1 - 2 * tid, b1 = b0 - 1;  // descending
+  const uint32_t v0 = __hip_atomic_load(gh + b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t v1 = __hip_atomic_load(gh + b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) scratch[5] = kQBins;
+  const uint32_t before = block_exclusive_scan(v0 + v1, scratch);
+  if (before < K && before + v0 >= K) scratch[5] = b0;
+  else if (before + v0 < K && before + v0 + v1 >= K) scratch[5] = b1;
+  __syncthreads();
+  const uint32_t b = scratch[5];
+  __syncthreads();
+  return b < kQBins ? (uint64_t)(lo + (b << sh)) << 32 : 0ull;
 }
 
 // Append `key` (when keep) to an LDS list through one LDS atomic per wave.
@@ -435,7 +484,11 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   (void)t_start; (void)t_probe; (void)t_keys; (void)t_sel; (void)n_app;
   const uint32_t q = pl.work_q[w];
   const uint32_t c0 = pl.work_c[w], nc = pl.work_n[w];
-  const uint32_t m = kSingle ? 1u : pl.q_m[q];
+  // terms: [Must (cost order)][MustNot][Should]; a query with Should clauses is
+  // Must-driven (RequiredOptionalScorer): the Shoulds only add score
+  const uint32_t qmv = kSingle ? qm_pack(1, 1, 0) : pl.q_m[q];
+  const uint32_t m = qm_terms(qmv), nm = qm_must(qmv), nmx = nm + qm_not(qmv);
+  const bool has_opt = m > nmx;
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const float* qub = pl.q_ub + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
@@ -479,7 +532,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   // as every thread last saw it (uniform), so the skip is uniform too.
   const float* __restrict__ cmax = ix.cmax + ix.coff[t0];
   uint64_t thr_k = thr0;
-  const bool defer = !kSingle && kDeferCap > 0 && m >= 3 && !fmask;
+  const bool defer = !kSingle && kDeferCap > 0 && m >= 3 && nm == m && !fmask;  // pure conjunctions
 
   for (uint32_t cc = 0; cc < nc; ++cc) {
     const uint32_t c = c0 + cc;
@@ -551,12 +604,22 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     // every list probed in intersection order; a candidate whose partial score
     // plus the remaining lists' maxima cannot reach the threshold is dropped
     // before the next probe
-    // after the first probe s0[j] holds left + right (the first two lists' sum)
+    // after the first probe s0[j] holds left + right (the first two lists' sum);
+    // then the MustNot lists drop the docs they hold; before the first Should
+    // list s0[j] takes the whole required score and acc_o[j] restarts as the
+    // optional union's sum (0.0 + s_a + ... in clause order)
     float acc_o[kItems];
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) acc_o[j] = 0.0f;
     for (uint32_t i = 1; i < min(m, (uint32_t)FG_MAXPROBE); ++i) {
       if (!__any(live != 0)) break;  // wave-uniform early exit
+      if (i == nmx && nm > 1) {
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+          s0[j] = s0[j] + acc_o[j];
+          acc_o[j] = 0.0f;
+        }
+      }
       const uint32_t ti = terms[i];
       const uint32_t meta = ix.tmeta[ti];
       const uint32_t dslot = meta_slot(meta);
@@ -611,10 +674,20 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
         }
       }
       // Intersection::score = left + right + (0.0 + others...)
+      if (i < nm) {
 #pragma unroll
-      for (uint32_t j = 0; j < kItems; ++j) {
-        if (sc[j] < 0.0f) { live &= ~(1u << j); continue; }
-        if (i == 1) s0[j] = s0[j] + sc[j]; else acc_o[j] += sc[j];
+        for (uint32_t j = 0; j < kItems; ++j) {
+          if (sc[j] < 0.0f) { live &= ~(1u << j); continue; }
+          if (i == 1) s0[j] = s0[j] + sc[j]; else acc_o[j] += sc[j];
+        }
+      } else if (i < nmx) {
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+          if (sc[j] >= 0.0f) live &= ~(1u << j);  // Exclude
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+          if (sc[j] >= 0.0f) acc_o[j] += sc[j];  // RequiredOptionalScorer's optional union
       }
       if (prune && i + 1 < m) {
         const float ub = qub[i + 1] + fmax;
@@ -662,8 +735,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       uint64_t key = 0;
       if (keep && ix.alive && !((ix.alive[doc[j] >> 5] >> (doc[j] & 31)) & 1u)) keep = false;
       if (keep) {
-        // one term = the union itself
-        float s = m == 1 ? s0[j] : s0[j] + acc_o[j];
+        // one Must term = the union itself; with Shoulds s0 = req, acc_o = opt:
+        // (0.0 + req) + opt
+        float s = (nm == 1 && !has_opt) ? s0[j] : s0[j] + acc_o[j];
         // with a filter: Intersection(text, facet union) = text + facet (two children)
         if (fmask) s = s + ftab[filter_bits(fmask, fshift, doc[j])];
         key = make_key(s, doc[j]);
@@ -701,7 +775,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     // publish the local k-th key; its reply (the best published one) is read next chunk
     if (tid == 0) {
       if (local_T > sh.thr) sh.thr = local_T;
-      pend = atomicMax(gthr, (unsigned long long)local_T);
+      pend = atomicMax(gthr, (unsigned long long)(local_T & pl.pub_mask));
     }
   }
   if (tid == 0 && pend > sh.thr) sh.thr = pend;
@@ -759,10 +833,6 @@ constexpr uint32_t kRound = 1024;              // postings / docs per pass
 constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
 constexpr uint32_t kPairs = 1024;              // (candidate, clause) rescoring pairs per pass
 constexpr uint32_t kMaxTiles = kDisjMaxGroup;  // tiles per work item
-#ifndef FG_EXHMIN
-#define FG_EXHMIN 1024
-#endif
-constexpr uint32_t kExhaustiveMin = FG_EXHMIN;  // all-essential tiles with fewer postings go posting-driven
 constexpr uint32_t kMaxSeg = kMaxTiles * kMaxTerms;
 static_assert(kMaxSeg <= 2 * kThreads, "k_disj segment list: two (tile, clause) pairs per thread");
 
@@ -793,27 +863,102 @@ struct DisjShared {
   uint64_t c_base[kMaxTerms];
   uint32_t max_s, n_seg, n_post;
   uint32_t n_buf, n_cand;
+  uint32_t n_cnt;                    // buf[0, n_cnt) are counted in the query's histogram
   uint64_t thr;
+  uint32_t lh[kQBins];               // hits per score bin not yet added to the global histogram
 };
 
 __device__ inline bool doc_alive(const DevIndex& ix, uint32_t d) {
   return !ix.alive || ((ix.alive[d >> 5] >> (d & 31)) & 1u);
 }
 
-// Keep the threshold fresh: truncate the local buffer to K when it passes
-// `limit`, then publish the local k-th key and read back the best published.
-__device__ inline void disj_truncate(DisjShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr, bool publish) {
-  const uint32_t n = sh.n_buf;
+// The query's score histogram (DevPlan::hist) and its bin geometry.
+struct QHist {
+  uint32_t* gh;
+  uint32_t lo, sh;
+  uint64_t pub;      // DevPlan::pub_mask
+  uint32_t m, mq;    // MustNot clauses: c_meta[m, mq)
+};
+
+// A query's work items run about one after another (the items are ordered as
+// a doc sweep across the batch, ~one per query in flight), so the global
+// histogram is read when an item starts and added to when it ends;
+// FG_HIST_EVERY_PUBLISH=1 also does both at every publication (A/B builds).
+#ifndef FG_HIST_EVERY_PUBLISH
+#define FG_HIST_EVERY_PUBLISH 0
+#endif
+#ifndef FG_DISJ_HIST
+#define FG_DISJ_HIST 1      // A/B: 0 = no running-threshold histogram reads
+#endif
+#ifndef FG_DISJ_PREFETCH
+#define FG_DISJ_PREFETCH 0  // A/B: 1 = load the next pass's postings during this pass's gathers
+#endif
+#ifndef FG_DISJ_PRESENCE
+#define FG_DISJ_PRESENCE 0  // A/B (ab_disj_presence.log): 1 = presence bound before the score gathers, slower
+#endif
+
+// Add the LDS bins to the query's global histogram and clear them.
+__device__ inline void hist_add(uint32_t* lh, uint32_t* gh) {
+  for (uint32_t b = threadIdx.x; b < kQBins; b += kThreads) {
+    const uint32_t c = lh[b];
+    if (c) {
+      atomicAdd(&gh[b], c);
+      lh[b] = 0;
+    }
+  }
+}
+
+// Keep the threshold fresh: drop the keys appended since the last call whose
+// doc a MustNot clause holds (Exclude: the hit loops never probe them), count
+// the rest into the LDS bins, truncate the local buffer to K when it passes
+// `limit`; when publishing, add the LDS bins to the query's histogram, read
+// back its running threshold, and exchange the threshold with the query's
+// (possibly shared) threshold word.
+__device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr,
+                                     bool publish, const QHist& hq, uint64_t& pend) {
+  uint32_t n = sh.n_buf;
   __syncthreads();  // every thread has read n before anyone appends again
+  if (hq.mq > hq.m) {
+    constexpr uint32_t R = kBufD / kThreads;
+    uint64_t v[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = sh.n_cnt + r * kThreads + threadIdx.x;
+      v[r] = i < n ? sh.buf[i] : 0ull;
+      if (v[r]) {
+        const uint32_t d = key_doc(v[r]);
+        for (uint32_t c = hq.m; c < hq.mq; ++c)
+          if (term_has_doc(ix, sh.c_meta[c], sh.c_base[c], sh.c_dir[c], d)) { v[r] = 0; break; }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sh.n_buf = sh.n_cnt;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) wave_append(v[r] != 0, v[r], sh.buf, &sh.n_buf, kBufD);
+    __syncthreads();
+    n = sh.n_buf;
+  }
+  for (uint32_t i = sh.n_cnt + threadIdx.x; i < n; i += kThreads) {
+    const uint32_t b = qbin(sh.buf[i], hq.lo, hq.sh);
+    if (b < kQBins) atomicAdd(&sh.lh[b], 1u);
+  }
+  __syncthreads();
   uint64_t T = 0;
   if (n > limit) T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+  uint64_t H = 0;
+  if (publish && FG_HIST_EVERY_PUBLISH) {
+    hist_add(sh.lh, hq.gh);
+    H = hist_threshold(hq.gh, K, hq.lo, hq.sh, sh.scratch);
+  }
   if (threadIdx.x == 0) {
     uint64_t mine = T > sh.thr ? T : sh.thr;
-    if (publish) {
-      const uint64_t old = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)mine);
-      mine = old > mine ? old : mine;
-    }
+    mine = H > mine ? H : mine;
+    // the exchange does not wait: the returned best is folded in when the
+    // next pass starts (pend), after that pass's posting loads are in flight
+    if (publish) pend = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)(mine & hq.pub));
     sh.thr = mine;
+    sh.n_cnt = sh.n_buf;
   }
   __syncthreads();
 }
@@ -827,14 +972,19 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
   const uint32_t tid = threadIdx.x;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
   const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const uint32_t w = pl.n_conj + (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 
   const uint32_t q = pl.work_q[w];
   const uint32_t tile0 = pl.work_c[w], ntile = pl.work_n[w];
-  const uint32_t m = pl.q_m[q];
+  // terms: [Should clauses (clause order)][MustNot]; m = the Should clauses
+  const uint32_t qmv = pl.q_m[q];
+  const uint32_t mq = qm_terms(qmv), m = mq - qm_not(qmv);
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
   uint64_t* gthr = &pl.thresh[q];
+  const QHist hq{pl.hist + (size_t)q * kQBins, pl.q_hlo[q], pl.q_hsh[q], pl.pub_mask, m, mq};
+  uint64_t pend = 0;  // thread 0: the last threshold exchange's reply, not yet folded in
+
   // facet filter: the union is intersected with the facet union, score = union + facet;
   // every bound below adds the facet score's maximum fmax
   const uint32_t fslot = pl.f.q_filter[q];
@@ -859,11 +1009,13 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #endif
   if (tid == 0) {
     sh.n_buf = 0;
+    sh.n_cnt = 0;
     const uint64_t t0 = pl.q_thr0[q];
     const uint64_t g = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)t0);
     sh.thr = g > t0 ? g : t0;
   }
-  if (tid < m) {
+  for (uint32_t b = tid; b < kQBins; b += kThreads) sh.lh[b] = 0;
+  if (tid < mq) {
     const uint32_t t = terms[tid];
     sh.c_meta[tid] = ix.tmeta[t];
     sh.c_dir[tid] = ix.dir_off[t];
@@ -913,6 +1065,11 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     sh.r_lo[p] = lo;
     sh.r_hi[p] = hi;
     sh.r_ub[p] = lo < hi ? ub : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
+  }
+  {
+    // the query's running threshold (every work item's counted hits so far)
+    const uint64_t H = FG_DISJ_HIST ? hist_threshold(hq.gh, K, hq.lo, hq.sh, sh.scratch) : 0ull;
+    if (tid == 0 && H > sh.thr) sh.thr = H;
   }
   __syncthreads();
   FG_PHASE(0);
@@ -989,6 +1146,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       }
       __syncthreads();
     }
+    if (tid == 0 && pend > sh.thr) sh.thr = pend;
+    __syncthreads();
     for (uint32_t r0 = 0; r0 < span; r0 += kRound) {
       const uint64_t thr = sh.thr;
 #pragma unroll
@@ -1012,9 +1171,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #ifdef FG_DIAG
       if (sh.n_buf > kTrunc) dg_trunc++;
 #endif
-      disj_truncate(sh, K, kTrunc, gthr, false);
+      disj_truncate(ix, sh, K, kTrunc, gthr, false, hq, pend);
     }
-    disj_truncate(sh, K, K, gthr, true);
+    disj_truncate(ix, sh, K, K, gthr, true, hq, pend);
   }
   FG_PHASE(2);
 
@@ -1052,13 +1211,40 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
   __syncthreads();
   const uint32_t n_seg = sh.n_seg, n_post = sh.n_post;
   FG_PHASE(3);
+  // the J postings of a thread go through every step in lockstep, so their
+  // loads (the posting, then each clause's rank word and score) overlap
+  constexpr uint32_t J = kRound / kThreads;
+  // posting e of the flat list: its (tile, clause) segment (the last
+  // seg_start <= e, binary search in LDS) and its position in the postings
+  auto locate = [&](uint32_t e, uint32_t& t, uint32_t& c) -> uint64_t {
+    uint32_t lo = 0, hi = n_seg;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sh.u.p.seg_start[mid] <= e) lo = mid; else hi = mid;
+    }
+    const uint32_t info = sh.seg_info[lo];
+    t = info >> 4;
+    c = info & 15u;
+    return sh.c_base[c] + sh.r_lo[t * m + c] + (e - sh.u.p.seg_start[lo]);
+  };
+#if FG_DISJ_PREFETCH
+  // the next pass's postings are loaded while this pass gathers (bound 2)
+  uint32_t npd[J];
+  float nps[J];
+#pragma unroll
+  for (uint32_t j = 0; j < J; ++j) {
+    const uint32_t e = j * kThreads + tid;
+    uint32_t t, c;
+    npd[j] = 0;
+    nps[j] = 0.0f;
+    if (e < n_post) {
+      const uint64_t at = locate(e, t, c);
+      npd[j] = ix.doc[at];
+      nps[j] = ix.psc[at];
+    }
+  }
+#endif
   for (uint32_t e0 = 0; e0 < n_post; e0 += kRound) {
-    const uint64_t thr = sh.thr;
-    if (tid == 0) sh.n_cand = 0;
-    __syncthreads();
-    // the J postings of a thread go through every step in lockstep, so their
-    // loads (the posting, then each clause's rank word and score) overlap
-    constexpr uint32_t J = kRound / kThreads;
     uint32_t pd[J], pt[J], pcl[J], ess[J];
     float ps[J];
     bool pk[J];
@@ -1071,20 +1257,24 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       pcl[j] = 0;
       ps[j] = 0.0f;
       if (pk[j]) {
-        // segment of posting e: last seg_start <= e
-        uint32_t lo = 0, hi = n_seg;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (sh.u.p.seg_start[mid] <= e) lo = mid; else hi = mid;
-        }
-        const uint32_t info = sh.seg_info[lo];
-        pt[j] = info >> 4;
-        pcl[j] = info & 15u;
-        const uint64_t at = sh.c_base[pcl[j]] + sh.r_lo[pt[j] * m + pcl[j]] + (e - sh.u.p.seg_start[lo]);
+        const uint64_t at = locate(e, pt[j], pcl[j]);
+#if FG_DISJ_PREFETCH
+        (void)at;
+        pd[j] = npd[j];
+        ps[j] = nps[j];
+#else
         pd[j] = ix.doc[at];
         ps[j] = ix.psc[at];
+#endif
       }
     }
+    // with this pass's posting loads in flight: the last exchange's reply
+    if (tid == 0) {
+      sh.n_cand = 0;
+      if (pend > sh.thr) sh.thr = pend;
+    }
+    __syncthreads();
+    const uint64_t thr = sh.thr;
 #pragma unroll
     for (uint32_t j = 0; j < J; ++j) {
       ess[j] = 0;
@@ -1100,10 +1290,28 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       dg_b1 += pk[j] ? 1u : 0u;
 #endif
     }
-    // bound 2: every clause at d in clause order -- the exact score from a dense
-    // structure (-1.0: absent), else the bucket maximum (-0.0: empty bucket).
-    // When every other clause is dense (or has no posting in the tile) the sum
-    // IS the doc's exact SumCombiner score (0.0 + s_i in clause order over the
+#if FG_DISJ_PREFETCH
+#pragma unroll
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t e = e0 + kRound + j * kThreads + tid;
+      if (e < n_post) {
+        uint32_t t, c;
+        const uint64_t at = locate(e, t, c);
+        npd[j] = ix.doc[at];
+        nps[j] = ix.psc[at];
+      }
+    }
+#endif
+    // bound 2: every other clause at d, in two steps per group of G clauses.
+    //  (a) presence: its rank word (presence bits + rank), its f32 table score or
+    //      its bucket maximum (-0.0: empty bucket), the loads of all J postings
+    //      in flight together; a clause the doc lacks adds 0 to the bound, one
+    //      it holds its tile bound (rank words) / exact table score / bucket
+    //      maximum, the clauses of later groups their tile bounds; a posting
+    //      whose bound cannot reach the threshold stops before any score gather;
+    //  (b) the survivors' posting scores of the clauses present by rank word.
+    // When every other clause is dense (or has no posting in the tile) the
+    // clause-order sum IS the doc's exact SumCombiner score (0.0 + s_i over the
     // matching clauses): the doc is a hit right here and skips the rescoring.
     float sum[J];
     uint32_t maybe[J];  // clauses whose structure at d says they may match (the rest cannot)
@@ -1114,32 +1322,71 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       maybe[j] = 0;
       exact[j] = true;
     }
-    // clauses in groups of G: the rank words of a group's clauses for all J
-    // postings are loaded together, then their scores -- two round trips per
-    // group instead of two per clause; sums still run in clause order
     constexpr uint32_t G = 4;
+    constexpr uint32_t kAbsent = 0xBF800000u;  // -1.0f: the clause is not on the doc
     for (uint32_t i0 = 0; i0 < m; i0 += G) {
-      uint64_t x[G][J];
-      float v[G][J];
+      // y[g][j]: a rank clause's posting position (< 2^31) or kAbsent; an f32
+      // table clause's score (-1.0: absent); a directory clause's bucket
+      // maximum (-0.0: empty bucket) -- one word per (clause, posting) once the
+      // loads (all G x J in flight together) have landed
+      uint32_t y[G][J];
       uint32_t need = 0;  // bit g * J + j
+      {
+        uint64_t x[G][J];
 #pragma unroll
-      for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t i = i0 + g;
-        const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
-        const uint32_t slot = meta_slot(meta);
-        const bool rank = slot && meta_rank(meta);
+        for (uint32_t g = 0; g < G; ++g) {
+          const uint32_t i = i0 + g;
+          const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
+          const uint32_t slot = meta_slot(meta);
+          const bool rank = slot && meta_rank(meta);
 #pragma unroll
-        for (uint32_t j = 0; j < J; ++j) {
-          x[g][j] = 0;
-          v[g][j] = -1.0f;
-          if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
-            need |= 1u << (g * J + j);
-            if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
-            else if (slot) v[g][j] = ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]];
-            else v[g][j] = ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))];
+          for (uint32_t j = 0; j < J; ++j) {
+            x[g][j] = kAbsent;
+            if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
+              need |= 1u << (g * J + j);
+              if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
+              else if (slot) x[g][j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
+              else x[g][j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
+            }
+          }
+        }
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+          const uint32_t i = i0 + g;
+          const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
+          const bool rank = meta_slot(meta) && meta_rank(meta);
+#pragma unroll
+          for (uint32_t j = 0; j < J; ++j) {
+            const uint32_t bits = (uint32_t)x[g][j], bt = pd[j] & 31u;
+            if (!rank || !((need >> (g * J + j)) & 1u)) y[g][j] = (uint32_t)x[g][j];
+            else y[g][j] = ((bits >> bt) & 1u) ? (uint32_t)(x[g][j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))
+                                               : kAbsent;
           }
         }
       }
+      // (a) the presence bound: the earlier groups' clause-order sum (exact
+      // scores or bucket maxima), the own posting's score if not in it yet, this
+      // group's presence contributions, the later groups' tile bounds
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        if (!FG_DISJ_PRESENCE || !pk[j]) continue;
+        float b = sum[j] + fmax;
+        if (pcl[j] >= i0) b += ps[j];
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+          if (!((need >> (g * J + j)) & 1u)) continue;
+          const uint32_t i = i0 + g, meta = sh.c_meta[i];
+          if (meta_slot(meta) && meta_rank(meta)) {
+            if (y[g][j] < 0x80000000u) b += sh.r_ub[pt[j] * m + i];
+          } else if (!signbit(__uint_as_float(y[g][j]))) {
+            b += __uint_as_float(y[g][j]);
+          }
+        }
+        for (uint32_t i = i0 + G; i < m; ++i)
+          if (i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) b += sh.r_ub[pt[j] * m + i];
+        pk[j] = make_key(inflate_bound(b), pd[j]) >= thr;
+      }
+      // (b) the posting scores of the present rank clauses, survivors only
 #pragma unroll
       for (uint32_t g = 0; g < G; ++g) {
         const uint32_t i = i0 + g;
@@ -1147,12 +1394,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
         if (!(meta_slot(meta) && meta_rank(meta))) continue;
         const float* __restrict__ sp = ix.psc + sh.c_base[i];
 #pragma unroll
-        for (uint32_t j = 0; j < J; ++j) {
-          const uint32_t bits = (uint32_t)x[g][j], bt = pd[j] & 31u;
-          if (((need >> (g * J + j)) & 1u) && ((bits >> bt) & 1u))
-            v[g][j] = sp[(uint32_t)(x[g][j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))];
-        }
+        for (uint32_t j = 0; j < J; ++j)
+          if (pk[j] && ((need >> (g * J + j)) & 1u) && y[g][j] < 0x80000000u) y[g][j] = __float_as_uint(sp[y[g][j]]);
       }
+      // the clause-order sum (the own clause: the streamed posting's score)
 #pragma unroll
       for (uint32_t g = 0; g < G; ++g) {
         const uint32_t i = i0 + g;
@@ -1164,7 +1409,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
           float b = ps[j];
           if (i != pcl[j]) {
             if (!((need >> (g * J + j)) & 1u)) continue;
-            b = v[g][j];
+            b = __uint_as_float(y[g][j]);
             exact[j] = exact[j] && slot != 0;
             if (signbit(b)) continue;  // clause i cannot match d
             maybe[j] |= 1u << i;
@@ -1300,9 +1545,14 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #ifdef FG_DIAG
     if (sh.n_buf > K) dg_trunc++;
 #endif
-    disj_truncate(sh, K, K, gthr, true);
+    disj_truncate(ix, sh, K, K, gthr, true, hq, pend);
     FG_PHASE(6);
   }
+  // the item's counted hits join the query's histogram (every key was counted
+  // by the last disj_truncate)
+  hist_add(sh.lh, hq.gh);
+  if (tid == 0 && pend > sh.thr) sh.thr = pend;
+  __syncthreads();
   flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
   FG_PHASE(7);
 #ifdef FG_DIAG
@@ -1363,7 +1613,8 @@ struct ScanShared {
   uint64_t thr;
 };
 
-__device__ inline void scan_truncate(ScanShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr, bool publish) {
+__device__ inline void scan_truncate(ScanShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr, bool publish,
+                                     uint64_t pub) {
   const uint32_t n = sh.n_buf;
   __syncthreads();
   uint64_t T = 0;
@@ -1371,7 +1622,7 @@ __device__ inline void scan_truncate(ScanShared& sh, uint32_t K, uint32_t limit,
   if (threadIdx.x == 0) {
     uint64_t mine = T > sh.thr ? T : sh.thr;
     if (publish) {
-      const uint64_t old = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)mine);
+      const uint64_t old = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)(mine & pub));
       mine = old > mine ? old : mine;
     }
     sh.thr = mine;
@@ -1423,9 +1674,9 @@ __global__ __launch_bounds__(kThreads) void k_scan(DevIndex ix, DevPlan pl) {
         wave_append(keep && key >= thr, key, sh.buf, &sh.n_buf, kBufD);
       }
       __syncthreads();
-      scan_truncate(sh, K, kTrunc, gthr, false);
+      scan_truncate(sh, K, kTrunc, gthr, false, pl.pub_mask);
     }
-    scan_truncate(sh, K, K, gthr, true);
+    scan_truncate(sh, K, K, gthr, true, pl.pub_mask);
   }
   flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
 }
@@ -1640,13 +1891,13 @@ hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (pl.total_chunks > pl.n_single) k_conj<false><<<pl.total_chunks - pl.n_single, kThreads, 0, s>>>(ix, pl);
+  if (pl.n_conj > pl.n_single) k_conj<false><<<pl.n_conj - pl.n_single, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 
 hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
-  if (pl.total_chunks == 0) return hipSuccess;
-  k_disj<<<pl.total_chunks, kThreads, 0, s>>>(ix, pl);
+  if (pl.total_chunks <= pl.n_conj) return hipSuccess;
+  k_disj<<<pl.total_chunks - pl.n_conj, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 

@@ -25,7 +25,7 @@ SHAPE_GET_SEARCH_PATH = 2
 HOST_EXPORTS = (
     "fg_db_create", "fg_db_destroy", "fg_db_namespace_create", "fg_db_namespace_delete",
     "fg_db_namespaces_json", "fg_db_upsert", "fg_db_commit", "fg_db_add_file", "fg_db_doc_count",
-    "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query",
+    "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query", "fg_parse_query_occur",
     "fg_db_upsert_record", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
     "fg_facet_clauses", "fg_db_search_json_post",
 )
@@ -75,6 +75,7 @@ _sig("fg_facet_tokens", _s, _s, _sz, C.POINTER(_sz))
 _sig("fg_facet_clauses", C.POINTER(_s), C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
 _sig("fg_analyze", _s, _s, _sz, C.POINTER(_sz))
 _sig("fg_parse_query", _s, C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
+_sig("fg_parse_query_occur", _s, _s, _sz, C.POINTER(_sz))
 
 
 class NotFound(native.FuguError):
@@ -141,11 +142,21 @@ def analyze(text: str) -> list:
     return out.split("\n") if out else []
 
 
+MODE_MIXED = 2
+
+
 def parse_query(query: str):
-    """(mode, terms) for the QueryParser subset the device runs; Unsupported otherwise."""
+    """(mode, terms) for the QueryParser subset the device runs; Unsupported otherwise.
+    mode: native.MODE_AND / MODE_OR when every clause is Must / Should, else MODE_MIXED."""
     mode = C.c_int(0)
     out = _string_call(_lib.fg_parse_query, query.encode(), C.byref(mode))
     return mode.value, out.split("\n")
+
+
+def parse_query_occur(query: str):
+    """[(occur, term)] with occur native.OCCUR_MUST / OCCUR_SHOULD / OCCUR_MUST_NOT."""
+    out = _string_call(_lib.fg_parse_query_occur, query.encode())
+    return [(int(x[0]), x[2:]) for x in out.split("\n")]
 
 
 @dataclass

@@ -35,6 +35,9 @@ FG_MAX_K = 1024
 FG_TERM_MISSING = 0xFFFFFFFF
 MODE_AND = 0
 MODE_OR = 1
+OCCUR_MUST = 0
+OCCUR_SHOULD = 1
+OCCUR_MUST_NOT = 2
 FIELD_TEXT = 0
 FIELD_NAME = 1
 FIELD_FACET = 2
@@ -49,6 +52,7 @@ EXPORTS = (
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
+    "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -88,7 +92,7 @@ class GlobalStats(C.Structure):
 
 class QueryBatch(C.Structure):
     _fields_ = [("n_queries", C.c_uint32), ("q_off", _u32p), ("terms", _u32p), ("mode", C.c_int),
-                ("f_off", _u32p), ("f_terms", _u32p)]
+                ("f_off", _u32p), ("f_terms", _u32p), ("occur", _u8p)]
 
 
 class IndexStats(C.Structure):
@@ -113,6 +117,9 @@ def _sig(name, res, *args):
 _sig("fg_device_count", C.c_int, C.POINTER(C.c_int))
 _sig("fg_ctx_create", C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(_p))
 _sig("fg_ctx_destroy", C.c_int, _p)
+_sig("fg_ctx_peer_access", C.c_int, _p, C.c_int, C.c_int, C.POINTER(C.c_int))
+_sig("fg_plan_link", C.c_int, C.POINTER(_p), C.c_uint32)
+_sig("fg_bytes_model_or", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f32p, _f64p)
 _sig("fg_last_error", C.c_char_p)
 _sig("fg_version", C.c_char_p)
 _sig("fg_index_build_from_docs", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(_p))
@@ -192,6 +199,12 @@ class Context:
     def handle(self):
         return self._h
 
+    def peer_access(self, a: int, b: int) -> bool:
+        """fg_ctx_peer_access: direct access from device a to device b enabled."""
+        e = C.c_int(0)
+        _check(_lib.fg_ctx_peer_access(self._h, a, b, C.byref(e)))
+        return bool(e.value)
+
     def close(self):
         if self._h:
             _lib.fg_ctx_destroy(self._h)
@@ -226,6 +239,20 @@ def _u64(a):
 
 def _u32(a):
     return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _batch(q_off, terms, mode, f_off=None, f_terms=None, occur=None):
+    """(QueryBatch, arrays it points into); occur: per-term OCCUR_* or None."""
+    q_off = _u32(q_off)
+    terms = _u32(terms)
+    f_off = None if f_off is None else _u32(f_off)
+    f_terms = None if f_off is None else _u32(f_terms)
+    occur = None if occur is None else np.ascontiguousarray(occur, np.uint8)
+    if occur is not None and len(occur) != len(terms):
+        raise ValueError("occur must parallel terms")
+    qb = QueryBatch(len(q_off) - 1, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode, _ptr(f_off, _u32p),
+                    _ptr(f_terms, _u32p), _ptr(occur, _u8p))
+    return qb, (q_off, terms, f_off, f_terms, occur)
 
 
 def _docs_input(text_off, text_tok, n_terms, name_off=None, name_tok=None, deleted=None, threads=0,
@@ -384,17 +411,14 @@ class Index:
         _check(_lib.fg_index_bm25(self._h, term, C.byref(wt), C.byref(wn), _ptr(cache, _f32p)))
         return wt.value, wn.value, cache
 
-    def plan(self, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None) -> "Plan":
-        return Plan(self, q_off, terms, k, mode, f_off, f_terms)
+    def plan(self, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None, occur=None) -> "Plan":
+        return Plan(self, q_off, terms, k, mode, f_off, f_terms, occur)
 
-    def search_batch(self, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None):
-        """f_off / f_terms: per-query facet clauses (facet term ids), or None."""
-        q_off = _u32(q_off)
-        terms = _u32(terms)
-        nq = len(q_off) - 1
-        f_off = None if f_off is None else _u32(f_off)
-        f_terms = None if f_off is None else _u32(f_terms)
-        qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode, _ptr(f_off, _u32p), _ptr(f_terms, _u32p))
+    def search_batch(self, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None, occur=None):
+        """f_off / f_terms: per-query facet clauses (facet term ids), or None;
+        occur: per-term OCCUR_MUST / SHOULD / MUST_NOT (None: `mode`)."""
+        qb, keep = _batch(q_off, terms, mode, f_off, f_terms, occur)
+        nq = qb.n_queries
         score = np.zeros(nq * k, np.float32)
         doc = np.zeros(nq * k, np.uint32)
         n = np.zeros(nq, np.uint32)
@@ -409,6 +433,16 @@ class Index:
         out = np.zeros(4 * nq, np.float64)
         _check(_lib.fg_bytes_model(self._h, C.byref(qb), k, _ptr(out, _f64p)))
         return out.reshape(nq, 4)
+
+    def bytes_model_or(self, q_off, terms, k: int, thr, occur=None):
+        """fg_bytes_model_or: per query {stream, probe, output, total} bytes of k_disj's
+        MaxScore at the device layout with the pruning threshold fixed at `thr` (the
+        query's final k-th best score: the least any exact MaxScore reads)."""
+        qb, keep = _batch(q_off, terms, MODE_OR, occur=occur)
+        t = np.ascontiguousarray(thr, np.float32)
+        out = np.zeros(4 * qb.n_queries, np.float64)
+        _check(_lib.fg_bytes_model_or(self._h, C.byref(qb), k, _ptr(t, _f32p), _ptr(out, _f64p)))
+        return out.reshape(qb.n_queries, 4)
 
     def bytes_model_gpu(self, q_off, terms, k: int, mode: int = MODE_AND):
         """fg_bytes_model_gpu: per query {lead, probe, output, total} bytes at the HBM layout."""
@@ -435,15 +469,11 @@ class Index:
 class Plan:
     """A batch planned on the host and resident in HBM (fg_plan_create)."""
 
-    def __init__(self, index: Index, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None):
-        self._q_off = _u32(q_off)
-        self._terms = _u32(terms)
-        self._f_off = None if f_off is None else _u32(f_off)
-        self._f_terms = None if f_off is None else _u32(f_terms)
-        self.n_queries = len(self._q_off) - 1
+    def __init__(self, index: Index, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None,
+                 occur=None):
+        qb, self._keep = _batch(q_off, terms, mode, f_off, f_terms, occur)
+        self.n_queries = qb.n_queries
         self.k = k
-        qb = QueryBatch(self.n_queries, _ptr(self._q_off, _u32p), _ptr(self._terms, _u32p), mode,
-                        _ptr(self._f_off, _u32p), _ptr(self._f_terms, _u32p))
         h = _p()
         _check(_lib.fg_plan_create(index.handle, C.byref(qb), k, C.byref(h)))
         self._h = h
@@ -503,16 +533,20 @@ class Plan:
             pass
 
 
-def search_sharded(indexes, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None, ctx=None):
+def link_plans(plans):
+    """fg_plan_link: plans of one batch on one device share per-query pruning
+    thresholds; execute plans[0] first in every round, destroy it last."""
+    hs = (_p * len(plans))(*[p._h for p in plans])
+    _check(_lib.fg_plan_link(hs, len(plans)))
+
+
+def search_sharded(indexes, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None, ctx=None,
+                   occur=None):
     """fg_search_sharded: one batch over several shard / segment / namespace
     indexes, merged on the first one's device by (score desc, shard asc, doc
     asc).  Returns (score [nq,k], doc [nq,k], shard [nq,k], n [nq])."""
-    q_off = _u32(q_off)
-    terms = _u32(terms)
-    nq = len(q_off) - 1
-    f_off = None if f_off is None else _u32(f_off)
-    f_terms = None if f_off is None else _u32(f_terms)
-    qb = QueryBatch(nq, _ptr(q_off, _u32p), _ptr(terms, _u32p), mode, _ptr(f_off, _u32p), _ptr(f_terms, _u32p))
+    qb, keep = _batch(q_off, terms, mode, f_off, f_terms, occur)
+    nq = qb.n_queries
     hs = (_p * len(indexes))(*[ix._h for ix in indexes])
     score = np.zeros(nq * k, np.float32)
     doc = np.zeros(nq * k, np.uint32)

@@ -43,6 +43,13 @@ extern "C" {
 #define FG_MODE_AND 0 /* `t1 AND t2 ...` / `+t1 +t2`: Must clauses (src/db/search.rs:112 parser) */
 #define FG_MODE_OR 1  /* `t1 t2 ...`: the parser's default Should conjunction */
 
+/* Per-term occur (tantivy Occur) of fg_query_batch.occur: `+t` / `t AND u` Must,
+ * bare `t` / `t OR u` Should, `-t` MustNot (query parser over [text, name],
+ * src/db/search.rs:108-127; scoring: SURVEY.md Appendix A.6). */
+#define FG_OCCUR_MUST 0
+#define FG_OCCUR_SHOULD 1
+#define FG_OCCUR_MUST_NOT 2
+
 #define FG_FIELD_TEXT 0
 #define FG_FIELD_NAME 1
 #define FG_FIELD_FACET 2 /* the docs index's Facet field (src/db/schemas.rs:20) */
@@ -57,6 +64,9 @@ typedef struct fg_plan fg_plan;
 int fg_device_count(int* out);
 int fg_ctx_create(int ndev, const int* devs, fg_ctx** out);
 int fg_ctx_destroy(fg_ctx* ctx);
+/* *enabled = 1 when fg_ctx_create enabled direct (xGMI) access from device a
+ * to device b's memory (every ordered pair of the context's devices). */
+int fg_ctx_peer_access(const fg_ctx* ctx, int a, int b, int* enabled);
 const char* fg_last_error(void);
 const char* fg_version(void);
 
@@ -182,7 +192,7 @@ typedef struct fg_query_batch {
   uint32_t n_queries;
   const uint32_t* q_off;  /* [n_queries+1] */
   const uint32_t* terms;  /* term ids in query order; FG_TERM_MISSING allowed */
-  int mode;               /* FG_MODE_AND (Must clauses) or FG_MODE_OR (Should clauses, k_disj) */
+  int mode;               /* FG_MODE_AND (Must clauses) or FG_MODE_OR (Should clauses), when occur is NULL */
   /* Facet filters (Dataset::search, src/db/search.rs:129-150), or NULL: per
    * query the flat Should clause list build_facet_query makes (:221-293) --
    * the exact facet terms in filter order, then the prefix terms -- as facet
@@ -193,6 +203,12 @@ typedef struct fg_query_batch {
    *   no text, no clauses  : AllQuery (score 1.0 for every alive doc). */
   const uint32_t* f_off;  /* [n_queries+1] */
   const uint32_t* f_terms;
+  /* Per-term occurs parallel to `terms` (FG_OCCUR_*), or NULL (every term is
+   * `mode`'s).  tantivy BooleanWeight semantics per query: with a Must clause
+   * the Musts intersect and the Shoulds only add score (RequiredOptionalScorer:
+   * (0.0 + must score) + Should union); without one the Shoulds' union; MustNot
+   * clauses exclude; no Must and no Should: no hits.  A batch may mix shapes. */
+  const uint8_t* occur;
 } fg_query_batch;
 
 /* Plan a batch: host-side query planning (tantivy Weight creation: terms
@@ -204,6 +220,15 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
  * Outputs are device pointers [n_queries*k], [n_queries*k], [n_queries]; NULL
  * outputs use the plan's own buffers.  Asynchronous. */
 int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_n);
+/* Link plans of ONE query batch and k on one device (the shards, segments or
+ * namespaces one merged result is drawn from) so they prune with one shared
+ * per-query threshold and score histogram: a doc below the k-th best score
+ * any of them has found cannot enter the merged top-k.  Thresholds are then
+ * shared score-only (a doc tied with the k-th score is kept: the merge breaks
+ * ties by shard).  plans[0] owns the shared state and zeroes it when executed:
+ * execute plans[0] first in every round and the others after it on the same
+ * stream (or ordered after it); destroy plans[0] last. */
+int fg_plan_link(fg_plan* const* plans, uint32_t n);
 /* Copy the plan's own result buffers to host (synchronises the plan's stream). */
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n);
 typedef struct fg_plan_info {
@@ -270,6 +295,16 @@ int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, doub
  * per posting of every clause (exhaustive union) + 8 B * k.  Needs
  * keep_host_postings. */
 int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);
+/* Algorithmic bytes of k_disj (Should clauses) at THIS layout
+ * with the MaxScore threshold fixed at thr_score[i], the query's final k-th
+ * best score (the least any exact MaxScore pass reads): out[4*i..] = {stream,
+ * probe, output, total} bytes.  Per (tile, clause) 12 B of bounds; per
+ * essential posting 8 B (every posting of an all-essential tile: 8 B); per
+ * posting past the tile bound, each other clause's rank word (8 B) or bucket
+ * maximum (4 B); per posting past the presence bound each present rank
+ * clause's score (4 B) and each other clause's directory probe; 8 B * k.
+ * Reads the posting scores back from the device; needs keep_host_postings. */
+int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, const float* thr_score, double* out);
 
 #ifdef __cplusplus
 }

@@ -120,8 +120,13 @@ int fg_db_doc_facets(fg_db* db, const char* ns, uint32_t doc, char* out, size_t 
 
 /* Analyzer / parser exposed for tests: tokens separated by '\n'. */
 int fg_analyze(const char* text, char* out, size_t cap, size_t* len);
-/* mode (FG_MODE_AND / FG_MODE_OR) and the analyzed terms ('\n'-separated). */
+/* mode (FG_MODE_AND / FG_MODE_OR: every clause Must / Should; FG_MODE_MIXED
+ * otherwise) and the analyzed terms ('\n'-separated). */
+#define FG_MODE_MIXED 2
 int fg_parse_query(const char* query, int* mode, char* out, size_t cap, size_t* len);
+/* The terms with their occurs: one line per term, "<o>:<term>", o = FG_OCCUR_*
+ * ('0' Must, '1' Should, '2' MustNot). */
+int fg_parse_query_occur(const char* query, char* out, size_t cap, size_t* len);
 /* FacetTokenizer tokens of Facet::from_text(path), '\n'-separated; the
  * encoded facets keep their U+0000 separators, so read *len bytes. */
 int fg_facet_tokens(const char* path, char* out, size_t cap, size_t* len);

@@ -793,10 +793,227 @@ int or_search_ex(const or_index* ix, const uint32_t* terms, uint32_t m, int mode
   return (int)topn_finish(&top, out_score, out_doc);
 }
 
+/* ---------------------------------------------------------------- occurs: Must / Should / MustNot */
+/*
+ * The parser's BooleanQuery with per-clause occurs (src/db/search.rs:108-127:
+ * `+a b -c`, `a OR b`, `a AND b`), each clause the per-term field union
+ * Should(text:t, name:t).  tantivy 0.24.1 query/boolean_query/boolean_weight.rs
+ * complex_scorer:
+ *   Must clauses     -> the clause itself when one, else Intersection (children
+ *                       by cost, leapfrog), score left + right + others;
+ *   Should + Must    -> RequiredOptionalScorer (query/reqopt_scorer.rs): the
+ *                       Must scorer drives; SumCombiner from 0.0 adds the
+ *                       required score, then the optional union's score when it
+ *                       is on the doc;
+ *   Should only      -> the union (SumCombiner, clause order);
+ *   MustNot          -> Exclude (query/exclude.rs) of the positive scorer by the
+ *                       union of the excluded clauses; scores unchanged;
+ *   no Must/Should   -> EmptyScorer (no hits).
+ * The positive query then meets the facet filter as before (two-child
+ * Intersection, text + facet).  Segments (seg != NULL): each runs its own
+ * scorers over its doc range, the Must children ordered by the SEGMENT's cost
+ * (BooleanWeight per SegmentReader), collected into one TopN.
+ */
+#define OR_OCC_MUST 0
+#define OR_OCC_SHOULD 1
+#define OR_OCC_MUST_NOT 2
+
+typedef struct { Cur c; Cur* req; Cur* opt; } ReqOptCur;
+static uint32_t ro_doc(Cur* c) { ReqOptCur* r = (ReqOptCur*)c; return r->req->doc(r->req); }
+static uint32_t ro_advance(Cur* c) { ReqOptCur* r = (ReqOptCur*)c; return r->req->advance(r->req); }
+static uint32_t ro_seek(Cur* c, uint32_t t) { ReqOptCur* r = (ReqOptCur*)c; return r->req->seek(r->req, t); }
+static float ro_score(Cur* c) {
+  ReqOptCur* r = (ReqOptCur*)c;
+  float s = 0.0f;
+  s += r->req->score(r->req);
+  const uint32_t d = r->req->doc(r->req);
+  if (r->opt && r->opt->doc(r->opt) <= d && r->opt->seek(r->opt, d) == d) s += r->opt->score(r->opt);
+  return s;
+}
+
+typedef struct { Cur c; Cur* pos; Cur* ex; uint32_t d; } ExclCur;
+static uint32_t ex_skip(ExclCur* e, uint32_t d) {
+  while (d != OR_TERMINATED) {
+    const uint32_t x = e->ex->doc(e->ex);
+    if (x > d || e->ex->seek(e->ex, d) != d) break;  /* accept: not in the excluded set */
+    d = e->pos->advance(e->pos);
+  }
+  return e->d = d;
+}
+static uint32_t exc_doc(Cur* c) { return ((ExclCur*)c)->d; }
+static uint32_t exc_advance(Cur* c) { ExclCur* e = (ExclCur*)c; return ex_skip(e, e->pos->advance(e->pos)); }
+static uint32_t exc_seek(Cur* c, uint32_t t) {
+  ExclCur* e = (ExclCur*)c;
+  if (e->d >= t) return e->d;
+  return ex_skip(e, e->pos->seek(e->pos, t));
+}
+static float exc_score(Cur* c) { ExclCur* e = (ExclCur*)c; return e->pos->score(e->pos); }
+
+typedef struct {
+  UnionCur um[OR_MAX_TERMS], us[OR_MAX_TERMS], ux[OR_MAX_TERMS];
+  Child ch[OR_MAX_TERMS];
+  AndCur ac; OneCur oc, so; OrCur sor, xor_; ReqOptCur ro; ExclCur ex;
+  FacetCur fc; AllCur al;
+} QueryCurs;
+
+/* The text cursor of one query over docs [lo, hi) (all cursors at or past lo),
+ * or NULL: *empty = 1 when the query matches nothing, 0 when the text is empty
+ * (m == 0: the facet union or AllQuery alone). */
+static Cur* build_text(QueryCurs* Q, const or_index* ix, const uint32_t* terms, const uint8_t* occur, uint32_t m,
+                       uint32_t lo, uint32_t hi, int* empty) {
+  uint32_t nm = 0, ns = 0, nx = 0;
+  *empty = 0;
+  if (m == 0) return NULL;
+  for (uint32_t i = 0; i < m; ++i) {
+    UnionCur* u = occur[i] == OR_OCC_MUST ? &Q->um[nm++] : occur[i] == OR_OCC_SHOULD ? &Q->us[ns++] : &Q->ux[nx++];
+    uc_init(u, ix, terms[i]);
+    uc_seek(u, lo);
+  }
+  if (nm == 0 && ns == 0) { *empty = 1; return NULL; }
+  Cur* req = NULL;
+  if (nm == 1) {
+    Q->oc.u = &Q->um[0];
+    Q->oc.c = (Cur){one_doc, one_advance, one_seek, one_score, Q->um[0].cost};
+    req = &Q->oc.c;
+  } else if (nm > 1) {
+    for (uint32_t i = 0; i < nm; ++i) {
+      uint64_t cost = Q->um[i].cost;
+      if (lo != 0 || hi != ix->n_docs) { /* the segment's own doc_freq */
+        cost = 0;
+        for (int f = 0; f < 2; ++f) cost += post_lb(Q->um[i].f[f].p, hi) - post_lb(Q->um[i].f[f].p, lo);
+      }
+      Q->ch[i].c = &Q->um[i]; Q->ch[i].cost = cost; Q->ch[i].qpos = i;
+    }
+    qsort(Q->ch, nm, sizeof(Child), child_cmp);
+    for (uint32_t i = 0; i < nm; ++i) Q->ac.ds[i] = Q->ch[i].c;
+    Q->ac.n = nm;
+    Q->ac.d = go_to_first_doc(Q->ac.ds, nm);
+    Q->ac.c = (Cur){and_doc, and_advance, and_seek, and_score, Q->ac.ds[0]->cost};
+    req = &Q->ac.c;
+  }
+  Cur* opt = NULL;
+  if (ns > 0) {
+    Q->sor.u = Q->us; Q->sor.n = ns;
+    uint64_t cost = 0;
+    for (uint32_t i = 0; i < ns; ++i) cost += Q->us[i].cost;
+    or_min(&Q->sor);
+    Q->sor.c = (Cur){orc_doc, orc_advance, orc_seek, orc_score, cost};
+    opt = &Q->sor.c;
+  }
+  Cur* pos;
+  if (req && opt) {
+    Q->ro.req = req; Q->ro.opt = opt;
+    Q->ro.c = (Cur){ro_doc, ro_advance, ro_seek, ro_score, req->cost};
+    pos = &Q->ro.c;
+  } else {
+    pos = req ? req : opt;
+  }
+  if (nx == 0) return pos;
+  Q->xor_.u = Q->ux; Q->xor_.n = nx;
+  or_min(&Q->xor_);
+  Q->xor_.c = (Cur){orc_doc, orc_advance, orc_seek, orc_score, 0};
+  Q->ex.pos = pos; Q->ex.ex = &Q->xor_.c;
+  Q->ex.c = (Cur){exc_doc, exc_advance, exc_seek, exc_score, pos->cost};
+  ex_skip(&Q->ex, pos->doc(pos));
+  return &Q->ex.c;
+}
+
+static void run_range(const or_index* ix, const uint32_t* terms, const uint8_t* occur, uint32_t m,
+                      const uint32_t* fterms, uint32_t nf, int filtered, uint32_t lo, uint32_t hi, TopN* top,
+                      float* thr) {
+  QueryCurs* Q = (QueryCurs*)malloc(sizeof(QueryCurs));
+  int empty = 0;
+  Cur* text = build_text(Q, ix, terms, occur, m, lo, hi, &empty);
+  Cur* filt = NULL;
+  if (!empty && filtered) {
+    static const Postings emptyp = {0, NULL, NULL, NULL};
+    uint64_t cost = 0;
+    for (uint32_t i = 0; i < nf; ++i) {
+      const Postings* p = (ix->fld[OR_FACET] && fterms[i] < ix->n_fterms) ? &ix->fld[OR_FACET][fterms[i]] : &emptyp;
+      Q->fc.t[i].p = p;
+      Q->fc.t[i].cur = 0;
+      Q->fc.t[i].weight = or_term_weight(p->n, ix->n_docs);
+      Q->fc.t[i].cache = ix->cache[OR_FACET];
+      Q->fc.t[i].fn = ix->fn[OR_FACET];
+      cost += p->n;
+    }
+    Q->fc.n = nf;
+    fc_min(&Q->fc);
+    Q->fc.c = (Cur){fc_doc, fc_advance, fc_seek, fc_score, cost};
+    filt = &Q->fc.c;
+    filt->seek(filt, lo);
+  } else if (!empty && !text) {
+    Q->al.n = ix->n_docs;
+    Q->al.d = lo < ix->n_docs ? lo : OR_TERMINATED;
+    Q->al.c = (Cur){all_doc, all_advance, all_seek, all_score, ix->n_docs};
+    filt = &Q->al.c; /* m == 0, no filter: AllQuery */
+  }
+  if (empty) { free(Q); return; }
+  if (!filt) {
+    for (uint32_t d = text->doc(text); d < hi; d = text->advance(text)) {
+      float s = text->score(text);
+      if (s > *thr) *thr = collect(top, ix, d, s);
+    }
+  } else if (!text) {
+    for (uint32_t d = filt->doc(filt); d < hi; d = filt->advance(filt)) {
+      float s = filt->score(filt);
+      if (s > *thr) *thr = collect(top, ix, d, s);
+    }
+  } else {
+    /* Intersection of (text, facet): children by cost (stable), leapfrog */
+    Cur* left = text->cost <= filt->cost ? text : filt;
+    Cur* right = left == text ? filt : text;
+    uint32_t cand = left->doc(left) > right->doc(right) ? left->doc(left) : right->doc(right);
+    for (;;) {
+      uint32_t a = left->seek(left, cand);
+      uint32_t b = right->seek(right, a);
+      if (b == a) { cand = a; break; }
+      cand = b;
+    }
+    while (cand < hi) {
+      float s = left->score(left) + right->score(right) + 0.0f;
+      if (s > *thr) *thr = collect(top, ix, cand, s);
+      cand = left->advance(left);
+      if (cand == OR_TERMINATED) break;
+      for (;;) {
+        uint32_t r = right->seek(right, cand);
+        if (r == cand) break;
+        cand = left->seek(left, r);
+        if (cand == OR_TERMINATED) break;
+      }
+    }
+  }
+  free(Q);
+}
+
+/*
+ * The general entry: terms[m] with occur[m] (OR_OCC_*); fterms[nf] with
+ * filtered != 0 = the facet clauses; seg[nseg+1] = segment doc-id bounds, or
+ * NULL (one segment).  Returns hits written (<= k), or -1 on bad arguments.
+ */
+int or_search_q(const or_index* ix, const uint32_t* terms, const uint8_t* occur, uint32_t m, const uint32_t* fterms,
+                uint32_t nf, int filtered, const uint32_t* seg, uint32_t nseg, uint32_t k, float* out_score,
+                uint32_t* out_doc) {
+  if (k < 1 || m > OR_MAX_TERMS || nf > OR_MAX_FACETS || (m && !occur)) return -1;
+  for (uint32_t i = 0; i < m; ++i)
+    if (occur[i] > OR_OCC_MUST_NOT) return -1;
+  TopN top;
+  topn_init(&top, k);
+  float thr = -3.40282347e+38f;
+  if (!seg) {
+    run_range(ix, terms, occur, m, fterms, nf, filtered, 0, ix->n_docs, &top, &thr);
+  } else {
+    for (uint32_t s = 0; s < nseg; ++s)
+      if (seg[s] < seg[s + 1]) run_range(ix, terms, occur, m, fterms, nf, filtered, seg[s], seg[s + 1], &top, &thr);
+  }
+  return (int)topn_finish(&top, out_score, out_doc);
+}
+
 /* ---------------------------------------------------------------- batch (CPU baseline) */
 typedef struct {
   const or_index* ix;
   const uint32_t* q_off; const uint32_t* q_terms;
+  const uint8_t* q_occur; /* nullable: every term is `mode`'s occur */
   const uint32_t* f_off; const uint32_t* f_terms; /* nullable: no facet filters */
   uint32_t nq; int mode; uint32_t k;
   float* out_score; uint32_t* out_doc; uint32_t* out_n;
@@ -817,7 +1034,11 @@ static void* batch_worker(void* arg) {
     uint32_t q = __atomic_fetch_add(&c->next, 1u, __ATOMIC_RELAXED);
     if (q >= c->nq) break;
     double t0 = now_ns();
-    int n = c->f_off ? or_search_ex(c->ix, c->q_terms + c->q_off[q], c->q_off[q + 1] - c->q_off[q], c->mode,
+    int n = c->q_occur ? or_search_q(c->ix, c->q_terms + c->q_off[q], c->q_occur + c->q_off[q],
+                                     c->q_off[q + 1] - c->q_off[q], c->f_off ? c->f_terms + c->f_off[q] : NULL,
+                                     c->f_off ? c->f_off[q + 1] - c->f_off[q] : 0, c->f_off != NULL, NULL, 0, c->k,
+                                     c->out_score + (size_t)q * c->k, c->out_doc + (size_t)q * c->k)
+            : c->f_off ? or_search_ex(c->ix, c->q_terms + c->q_off[q], c->q_off[q + 1] - c->q_off[q], c->mode,
                                     c->f_terms + c->f_off[q], c->f_off[q + 1] - c->f_off[q], c->k,
                                     c->out_score + (size_t)q * c->k, c->out_doc + (size_t)q * c->k)
                      : or_search(c->ix, c->q_terms + c->q_off[q], c->q_off[q + 1] - c->q_off[q], c->mode, c->k,
@@ -831,12 +1052,12 @@ static void* batch_worker(void* arg) {
 
 /* Each thread runs whole queries (a tokio worker per request, tantivy's
  * single-threaded executor).  Returns the wall time in seconds. */
-double or_search_batch_ex(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, const uint32_t* f_off,
-                          const uint32_t* f_terms, uint32_t nq, int mode, uint32_t k, float* out_score,
-                          uint32_t* out_doc, uint32_t* out_n, double* lat_ns, int threads) {
+double or_search_batch_q(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, const uint8_t* q_occur,
+                         const uint32_t* f_off, const uint32_t* f_terms, uint32_t nq, int mode, uint32_t k,
+                         float* out_score, uint32_t* out_doc, uint32_t* out_n, double* lat_ns, int threads) {
   BatchCtx c;
   memset(&c, 0, sizeof c);
-  c.ix = ix; c.q_off = q_off; c.q_terms = q_terms; c.nq = nq; c.mode = mode; c.k = k;
+  c.ix = ix; c.q_off = q_off; c.q_terms = q_terms; c.q_occur = q_occur; c.nq = nq; c.mode = mode; c.k = k;
   c.f_off = f_off; c.f_terms = f_terms;
   c.out_score = out_score; c.out_doc = out_doc; c.out_n = out_n; c.lat_ns = lat_ns; c.next = 0;
   if (threads < 1) threads = 1;
@@ -848,6 +1069,13 @@ double or_search_batch_ex(const or_index* ix, const uint32_t* q_off, const uint3
   double t1 = now_ns();
   free(th);
   return (t1 - t0) * 1e-9;
+}
+
+double or_search_batch_ex(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, const uint32_t* f_off,
+                          const uint32_t* f_terms, uint32_t nq, int mode, uint32_t k, float* out_score,
+                          uint32_t* out_doc, uint32_t* out_n, double* lat_ns, int threads) {
+  return or_search_batch_q(ix, q_off, q_terms, NULL, f_off, f_terms, nq, mode, k, out_score, out_doc, out_n, lat_ns,
+                           threads);
 }
 
 double or_search_batch(const or_index* ix, const uint32_t* q_off, const uint32_t* q_terms, uint32_t nq, int mode,

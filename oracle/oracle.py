@@ -57,12 +57,20 @@ _lib.or_search_batch_ex.restype = C.c_double
 _lib.or_search_batch_ex.argtypes = [_p, _p, _p, _p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p, _p, _p, C.c_int]
 _lib.or_search_seg.restype = C.c_int
 _lib.or_search_seg.argtypes = [_p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, C.c_uint32, _p, _p]
+_lib.or_search_q.restype = C.c_int
+_lib.or_search_q.argtypes = [_p, _p, _p, C.c_uint32, _p, C.c_uint32, C.c_int, _p, C.c_uint32, C.c_uint32, _p, _p]
+_lib.or_search_batch_q.restype = C.c_double
+_lib.or_search_batch_q.argtypes = [_p, _p, _p, _p, _p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p, _p, _p, C.c_int]
 _lib.or_bytes_model.restype = C.c_int
 _lib.or_bytes_model.argtypes = [_p, _p, C.c_uint32, C.c_uint32, _p]
 
 AND = 0
 OR = 1
-FACET = 2  # field slot of the facet field (or_df / or_total_tokens / or_avgdl)
+FACET = 2
+# clause occurs (tantivy Occur; query/boolean_query): per term of a query
+MUST = 0
+SHOULD = 1
+MUST_NOT = 2  # field slot of the facet field (or_df / or_total_tokens / or_avgdl)
 
 
 def fieldnorm_table():
@@ -133,9 +141,24 @@ class OracleIndex:
     def fieldnorm_id(self, doc: int, field: int = 0) -> int:
         return int(_lib.or_fieldnorm_id_of(self._h, field, doc))
 
-    def search(self, terms, k: int, mode: int = AND, fterms=None):
-        """fterms: facet clauses (None: no filter); empty `terms` = empty text query."""
+    def search(self, terms, k: int, mode: int = AND, fterms=None, occur=None, seg_bounds=None):
+        """fterms: facet clauses (None: no filter); empty `terms` = empty text query.
+        occur: per-term MUST / SHOULD / MUST_NOT (None: every term is `mode`'s);
+        seg_bounds: segment doc-id bounds (None: one segment)."""
         t = np.ascontiguousarray(terms, np.uint32)
+        if occur is not None or seg_bounds is not None:
+            oc = np.ascontiguousarray(occur if occur is not None else [MUST if mode == AND else SHOULD] * len(t),
+                                      np.uint8)
+            f = np.ascontiguousarray(fterms if fterms is not None else [], np.uint32)
+            sb = None if seg_bounds is None else np.ascontiguousarray(seg_bounds, np.uint32)
+            score = np.zeros(k, np.float32)
+            doc = np.zeros(k, np.uint32)
+            n = _lib.or_search_q(self._h, t.ctypes.data, oc.ctypes.data, len(t), f.ctypes.data, len(f),
+                                 1 if fterms is not None else 0, None if sb is None else sb.ctypes.data,
+                                 0 if sb is None else len(sb) - 1, k, score.ctypes.data, doc.ctypes.data)
+            if n < 0:
+                raise ValueError("oracle rejected the query")
+            return score[:n].copy(), doc[:n].copy()
         score = np.zeros(k, np.float32)
         doc = np.zeros(k, np.uint32)
         if fterms is None and len(t) > 0:
@@ -161,9 +184,11 @@ class OracleIndex:
         return score[:n].copy(), doc[:n].copy()
 
     def search_batch(self, q_off, q_terms, k: int, mode: int = AND, threads: int = 1, latencies: bool = False,
-                     f_off=None, f_terms=None):
+                     f_off=None, f_terms=None, occur=None):
+        """occur: per-term MUST / SHOULD / MUST_NOT parallel to q_terms (None: `mode`)."""
         q_off = np.ascontiguousarray(q_off, np.uint32)
         q_terms = np.ascontiguousarray(q_terms, np.uint32)
+        oc = None if occur is None else np.ascontiguousarray(occur, np.uint8)
         if f_off is not None:
             f_off = np.ascontiguousarray(f_off, np.uint32)
             f_terms = np.ascontiguousarray(f_terms, np.uint32)
@@ -172,7 +197,8 @@ class OracleIndex:
         doc = np.zeros(nq * k, np.uint32)
         n = np.zeros(nq, np.uint32)
         lat = np.zeros(nq, np.float64) if latencies else None
-        wall = _lib.or_search_batch_ex(self._h, q_off.ctypes.data, q_terms.ctypes.data,
+        wall = _lib.or_search_batch_q(self._h, q_off.ctypes.data, q_terms.ctypes.data,
+                                       None if oc is None else oc.ctypes.data,
                                        None if f_off is None else f_off.ctypes.data,
                                        None if f_off is None else f_terms.ctypes.data, nq, mode, k, score.ctypes.data,
                                        doc.ctypes.data, n.ctypes.data, None if lat is None else lat.ctypes.data, threads)

@@ -163,6 +163,50 @@ class Index:
         return [[int(d), int(np.float32(s).view(np.uint32))] for s, d in hits[:k]]
 
 
+    def search_occ(self, terms, occur, k):
+        """BooleanQuery with per-clause occurs (query/boolean_query/boolean_weight.rs
+        complex_scorer): Must -> the clause / Intersection (cost order, left + right
+        + others); Should with Must -> RequiredOptionalScorer: (0.0 + req) + the
+        Should union when it is on the doc; Should alone -> the union from 0.0 in
+        clause order; MustNot -> Exclude; neither Must nor Should -> no hits."""
+        M = [t for t, o in zip(terms, occur) if o == "must"]
+        S = [t for t, o in zip(terms, occur) if o == "should"]
+        X = [t for t, o in zip(terms, occur) if o == "must_not"]
+        if not M and not S:
+            return []
+        excl = set().union(*[self.docs(t) for t in X]) if X else set()
+        if M:
+            order = sorted(range(len(M)), key=lambda i: (self.cost(M[i]), i))
+            ts = [M[i] for i in order]
+            cand = set.intersection(*[self.docs(t) for t in ts])
+        else:
+            cand = set().union(*[self.docs(t) for t in S])
+        hits = []
+        for d in cand - excl:
+            opt, any_s = F(0.0), False
+            for t in S:
+                if d in self.docs(t):
+                    opt = opt + self.term_score(t, d)
+                    any_s = True
+            if M:
+                if len(ts) == 1:
+                    req = self.term_score(ts[0], d)
+                else:
+                    others = F(0.0)
+                    for t in ts[2:]:
+                        others = others + self.term_score(t, d)
+                    req = (self.term_score(ts[0], d) + self.term_score(ts[1], d)) + others
+                sc = F(0.0) + req
+                if any_s:
+                    sc = sc + opt
+            else:
+                sc = opt
+            hits.append((sc, d))
+        if self.deleted is not None:
+            hits = [h for h in hits if not self.deleted[h[1]]]
+        hits.sort(key=lambda h: (-float(h[0]), h[1]))
+        return [[int(d), int(np.float32(s).view(np.uint32))] for s, d in hits[:k]]
+
     def search_filtered(self, terms, k, mode, fterms):
         """Bool[Must(text), Must(facet union)], the facet union alone, or AllQuery
         (src/db/search.rs:129-150); a union sums its matching clauses from 0.0
@@ -340,7 +384,44 @@ def facets_set(fname, n_docs, vocab, seeds, facet_seed):
     })
 
 
+OCCURS = ("must", "should", "must_not")
+
+
+def occur_set(fname, n_docs, vocab, seeds):
+    """Must / Should / MustNot mixes (`+a b -c`, `a OR b`): 2-5 terms with
+    per-clause occurs drawn from the query hash, on a corpus with names and
+    deletions; plus hand-picked edges (a term both Must and MustNot, missing
+    terms in each role, only MustNot, duplicate Should terms)."""
+    off, tok = sr.corpus(n_docs, vocab, 1.0, seeds[0], seeds[1])
+    name_cfg = {"vocab": 1 << 9, "seed": 4244}
+    del_cfg = {"seed": 79}
+    ix = Index(n_docs, (off, tok), sr.names(n_docs, **name_cfg), sr.deleted_mask(n_docs, **del_cfg))
+    queries = []
+    qo, qt = sr.queries(192, 2, 5, 1 << 9, 1.0, 37)
+    for i in range(192):
+        terms = qt[qo[i]:qo[i + 1]].tolist()
+        h = int(sr.h2(41, i))
+        occ = [OCCURS[(h >> (2 * j)) % 3] for j in range(len(terms))]
+        if i % 4 == 0:  # at least one Must
+            occ[0] = "must"
+        k = [10, 100, 1, 37][(h >> 20) % 4]
+        queries.append({"terms": terms, "occur": occ, "k": k, "hits": ix.search_occ(terms, occ, k)})
+    edges = [([1, 2, 1], ["must", "should", "must_not"]), ([MISSING, 3], ["must", "should"]),
+             ([3, MISSING], ["must", "should"]), ([3, MISSING], ["should", "must_not"]),
+             ([4, 5], ["must_not", "must_not"]), ([6, 6, 7], ["should", "should", "must_not"]),
+             ([8, 9, 10], ["must", "must", "should"]), ([11], ["should"]), ([12, 13], ["must", "must_not"])]
+    for terms, occ in edges:
+        for k in (10, 1000):
+            queries.append({"terms": terms, "occur": occ, "k": k, "hits": ix.search_occ(terms, occ, k)})
+    write(fname, {
+        "corpus": {"kind": "synth", "n_docs": n_docs, "vocab": vocab, "s": 1.0, "seed_l": seeds[0],
+                   "seed_t": seeds[1], "name": name_cfg, "deleted": del_cfg},
+        "queries": queries,
+    })
+
+
 def main():
+    occur_set("occur_2k.json", 2_000, 1 << 11, (0x5EED4, 103))
     kat()
     edge()
     facets_set("facets_2k.json", 2_000, 1 << 12, (0x5EED3, 101), 555)

@@ -104,10 +104,22 @@ def test_parser_device_subset(db):
     assert db.parse_query("+foo +bar") == (AND, ["foo", "bar"])
     assert db.parse_query("foo bar") == (OR, ["foo", "bar"])
     assert db.parse_query("straße ÜBER") == (OR, ["straße", "über"])
+    # binary OR = the default Should conjunction; prefixes give per-clause occurs
+    assert db.parse_query("foo OR Bar OR baz") == (OR, ["foo", "bar", "baz"])
+    M, S, X = 0, 1, 2
+    assert db.parse_query("+a b") == (db.MODE_MIXED, ["a", "b"])
+    assert db.parse_query_occur("+a b") == [(M, "a"), (S, "b")]
+    assert db.parse_query_occur("a -b") == [(S, "a"), (X, "b")]
+    assert db.parse_query_occur("+Alpha beta -Gamma +delta") == [(M, "alpha"), (S, "beta"), (X, "gamma"), (M, "delta")]
+    assert db.parse_query_occur("a OR b") == [(S, "a"), (S, "b")]
+    assert db.parse_query_occur("a AND b") == [(M, "a"), (M, "b")]
+    assert db.parse_query_occur("rust") == [(S, "rust")]
+    assert db.parse_query("-a b") == (db.MODE_MIXED, ["a", "b"])
 
 
-@pytest.mark.parametrize("q", ["", "   ", "a -b", "name:x", '"a b"', "foo-bar", "a OR b", "a AND", "AND a",
-                               "a AND b OR c", "(a b)", "a^2", "a~1", "fo*", "a AND AND b", "+a b", "..."])
+@pytest.mark.parametrize("q", ["", "   ", "name:x", '"a b"', "foo-bar", "a AND", "AND a", "a OR", "-a", "-a -b",
+                               "a AND b OR c", "(a b)", "a^2", "a~1", "fo*", "a AND AND b", "+a AND b", "a OR -b",
+                               "--a b", "..."])
 def test_parser_rejects_outside_subset(db, q):
     from fugu_amd import native
     with pytest.raises(native.Unsupported):
@@ -189,7 +201,7 @@ def test_commit_needs_a_device_and_search_before_commit_is_empty(db):
         d.search_json("nope", "hello")
     assert "Namespace 'nope' not found" in str(e.value)
     with pytest.raises(db.native.Unsupported):
-        d.search(None, "a -b")
+        d.search(None, "-a -b")
     with pytest.raises(db.native.Unsupported):
         d.search(None, "hello", page=1000, per_page=100)  # offset + per_page > FG_MAX_K
 
@@ -218,7 +230,7 @@ def test_response_shapes_byte_exact(db):
         d.search_json("nope", "x", shape=db.SHAPE_POST_SEARCH)
     assert e.value.body == '{"error":"Namespace \'nope\' not found","status":"error"}'
     with pytest.raises(db.native.Unsupported) as e:
-        d.search_json("ns1", "a -b")
+        d.search_json("ns1", "(a b)")
     assert e.value.body.startswith('{"error":"Search failed: Search failed: query outside the device subset')
 
 
@@ -451,6 +463,46 @@ def test_db_end_to_end_vs_oracle(db):
     assert r["results"][0]["facets"] == ["/namespace/docs", "/metadata/name"]
 
 
+@pytest.mark.gpu
+def test_db_occur_queries_vs_oracle(db):
+    """`+a b`, `a -b`, `a OR b`, `+a +b -c d`: the parser's occurs through
+    Dataset::search on the device, against the oracle's BooleanQuery."""
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("oc")
+    recs = build_corpus(23, 2500)
+    for rid, t, meta in recs:
+        d.upsert(db.ObjectRecord(rid, t, metadata=meta), "oc")
+    d.commit("oc")
+    ix, dic = oracle_of(recs)
+    rng = random.Random(31)
+    checked = 0
+    for _ in range(80):
+        m = rng.randint(1, 4)
+        ws = [rng.choice(WORDS) for _ in range(m)]
+        shape = rng.randint(0, 2)
+        if shape == 0 and m > 1:
+            q, occ = " OR ".join(ws), [1] * m
+        else:
+            pre = [rng.choice(["+", "", "-"]) for _ in ws]
+            if all(p == "-" for p in pre):
+                pre[0] = ""
+            q = " ".join(p + w for p, w in zip(pre, ws))
+            occ = [0 if p == "+" else 2 if p == "-" else 1 for p in pre]
+        assert [o for o, _ in db.parse_query_occur(q)] == occ
+        page, per_page = rng.randint(0, 2), rng.choice([5, 10, 20])
+        got = d.search("oc", q, page, per_page)
+        terms = [dic.get(py_analyze(w)[0], native.FG_TERM_MISSING) for w in ws]
+        s, dd = ix.search(np.array(terms, np.uint32), (page + 1) * per_page, occur=occ)
+        want = hits_of(s, dd)[page * per_page:]
+        assert hits_of([g[0] for g in got], [g[1] for g in got]) == want, q
+        checked += len(want)
+    assert checked > 200
+
+
 def facet_corpus(seed, n):
     rng = random.Random(seed)
     recs = []
@@ -610,7 +662,7 @@ def test_db_incremental_commits_segments_vs_oracle(db):
             got = d.search("inc", q, page, per_page)
             terms = [dic.get(t, native.FG_TERM_MISSING) for t in (py_analyze(w)[0] for w in ws)]
             s, dd = ix.search_segments(np.array(terms, np.uint32), (page + 1) * per_page, bounds, mode=mode)
-            want = [(keep[doc], bits) for doc, bits in hits_of(s, dd)[page * per_page:]]
+            want = [[keep[doc], bits] for doc, bits in hits_of(s, dd)[page * per_page:]]
             assert hits_of([g[0] for g in got], [g[1] for g in got]) == want, (n, q, bounds)
             checked += len(want)
         assert d.doc_count("inc")[0] == n

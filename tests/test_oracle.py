@@ -119,3 +119,43 @@ def test_facets_golden():
     sc, dc, cnt, _, _ = ix.search_batch(q_off, q_terms, 10, threads=3, f_off=f_off, f_terms=f_terms)
     for i, q in enumerate(qs):
         assert hits_of(sc[i, :cnt[i]], dc[i, :cnt[i]]) == q["hits"]
+
+
+OCC = {"must": orc.MUST, "should": orc.SHOULD, "must_not": orc.MUST_NOT}
+
+
+def test_occur_golden():
+    """Must / Should / MustNot mixes (RequiredOptionalScorer, Exclude) vs the numpy
+    restatement; the generic path also reproduces the all-Must / all-Should
+    fixtures and the segmented search."""
+    fx = load_golden("occur_2k.json")
+    n, nt, off, tok, no, ntk, dl = golden_corpus(fx)
+    ix = orc.OracleIndex(nt, off, tok, no, ntk, dl, threads=4)
+    bad = []
+    for q in fx["queries"]:
+        s, d = ix.search(q["terms"], q["k"], occur=[OCC[o] for o in q["occur"]])
+        if hits_of(s, d) != q["hits"]:
+            bad.append((q["terms"], q["occur"]))
+    assert not bad, bad
+    assert sum(len(q["hits"]) for q in fx["queries"]) > 2000
+    # batch entry point with per-term occurs
+    qs = [q for q in fx["queries"] if q["k"] == 10]
+    q_off = np.cumsum([0] + [len(q["terms"]) for q in qs]).astype(np.uint32)
+    q_terms = np.array([t for q in qs for t in q["terms"]], np.uint32)
+    occ = np.array([OCC[o] for q in qs for o in q["occur"]], np.uint8)
+    sc, dc, cnt, _, _ = ix.search_batch(q_off, q_terms, 10, threads=3, occur=occ)
+    for i, q in enumerate(qs):
+        assert hits_of(sc[i, :cnt[i]], dc[i, :cnt[i]]) == q["hits"], q
+    # all-Must / all-Should through the generic path = the mode fixtures
+    fx2 = load_golden("synth_names_2k.json")
+    n2, nt2, off2, tok2, no2, ntk2, dl2 = golden_corpus(fx2)
+    ix2 = orc.OracleIndex(nt2, off2, tok2, no2, ntk2, dl2, threads=4)
+    for q in fx2["queries"]:
+        o = [orc.MUST if q["mode"] == "and" else orc.SHOULD] * len(q["terms"])
+        s, d = ix2.search(q["terms"], q["k"], occur=o)
+        assert hits_of(s, d) == q["hits"], q
+        # segmented: the same as or_search_seg for AND / OR
+        sb = [0, 700, 701, 1500, n2]
+        s1, d1 = ix2.search(q["terms"], q["k"], occur=o, seg_bounds=sb)
+        s2, d2 = ix2.search_segments(q["terms"], q["k"], sb, mode=_mode(q["mode"]))
+        assert hits_of(s1, d1) == hits_of(s2, d2), q

@@ -48,7 +48,7 @@ def main():
         "wg_us": {p: round(float(np.percentile(dt, p)), 1) for p in (50, 90, 99, 100)},
         "wg_us_sum_ms": round(float(dt.sum()) * 1e-3, 1),
         "phase_ms_sum_over_wgs": {nm: round(float(wg[:, 8 + i].sum()) * 1e-5, 1) for i, nm in enumerate(
-            ["ranges", "split", "zero+stage", "scatter", "filter", "rescore", "scan_rest", "publish"])},
+            ["ranges+hist_read", "split", "exhaustive_tiles", "segment_list", "filter_bound1_bound2", "rescore", "truncate_publish", "hist_add_flush"])},
         "cand_per_query": [int(x) for x in np.percentile(plan.candidate_counts(), [50, 90, 100])],
     }
     print(json.dumps(out), flush=True)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Hardware-counter passes of the bench's k_conj (run on the MI355X box through
+# Hardware-counter passes of the bench's k_conj (or k_disj: pass --disj --k 1000) (run on the MI355X box through
 # gpurun).  One rocprofv3 --pmc run per pass (slot limits: 8 SQ, 4 TCP, 2 TA,
 # 2 TD, 4 TCC), each under its own hard time limit, then tools/pmc_summary.py.
 set -euo pipefail
@@ -20,5 +20,6 @@ pass sq2 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_
 pass tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum
 pass tlb TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_REQUEST_sum GRBM_GUI_ACTIVE GRBM_COUNT
 pass tcc TCC_HIT_sum TCC_MISS_sum TCC_TAG_STALL_sum TCC_REQ_sum
+pass dram TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B
 python3 "$R/tools/pmc_summary.py" "$OUT" > "$OUT/summary.json"
 echo "pmc done: $OUT"
