@@ -155,6 +155,57 @@ def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
                     "hits, pipelined over the workers' streams (planning overlaps other batches' kernels)"}
 
 
+def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
+    """The default API shape end to end through the host mirror: a 10M-doc
+    namespace ingested by n_seg POST /batch/upsert calls (one commit, one
+    segment each: src/db/document.rs:65), then batch-of-one GET /search?q=a b
+    (bare terms = Should, limit 20: src/server/handlers/search.rs:36, 370-374;
+    src/db/search.rs:112) through fg_db_search: parse, dictionary, ONE
+    fg_search_sharded over the 8 segments (shared thresholds, device merge),
+    hits out; and the same query through the full handler (JSON with the 20
+    docs fetched).  Parity sample: the oracle's top-20 (an OR does not depend
+    on the segmentation)."""
+    from fugu_amd import db as fdb
+    t0 = time.time()
+    d = fdb.Database(ctx)
+    d.create_namespace("api")
+    tb, to = synth.render_text(corp, threads)
+    ib, io = synth.render_ids(corp.n_docs)
+    bounds = [corp.n_docs * i // n_seg for i in range(n_seg + 1)]
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        d.upsert_batch("api", id_buf=ib[int(io[a]):int(io[b])], id_off=io[a:b + 1] - io[a],
+                       text_buf=tb[int(to[a]):int(to[b])], text_off=to[a:b + 1] - to[a])
+    del tb, ib
+    ingest_s = time.time() - t0
+    q_off, terms = synth.queries(nq, 2, 5, seed_q=333)
+    qs = [" ".join(f"t{t}" for t in terms[q_off[i]:q_off[i + 1]]) for i in range(nq)]
+    for q in qs[:8]:
+        d.search("api", q, 0, 20)
+    lat, lat_json, mism = [], [], 0
+    for i, q in enumerate(qs):
+        t1 = time.perf_counter()
+        got = d.search("api", q, 0, 20)
+        lat.append(time.perf_counter() - t1)
+        t1 = time.perf_counter()
+        d.search_json("api", q, 0, 20)
+        lat_json.append(time.perf_counter() - t1)
+        if ref is not None:
+            rs, rd = ref.search(terms[q_off[i]:q_off[i + 1]], 20, mode=1)
+            if [g[1] for g in got] != rd.tolist() or not np.allclose([g[0] for g in got], rs, rtol=1e-5, atol=0):
+                mism += 1
+    pct = lambda v, p: round(float(np.percentile(v, p) * 1e3), 4)  # noqa: E731
+    out = {"p50_ms": pct(lat, 50), "p90_ms": pct(lat, 90), "p99_ms": pct(lat, 99),
+           "json_p50_ms": pct(lat_json, 50), "json_p99_ms": pct(lat_json, 99), "queries": nq, "segments": n_seg,
+           "k": 20, "mode": "OR (bare terms)", "ingest_s": round(ingest_s, 1), "n_docs": corp.n_docs,
+           "note": "batch of one through fg_db_search (parse + dictionary + fg_search_sharded over the namespace's "
+                   "8 commit segments + device merge + hits out); json_*: the GET /search handler shape with the "
+                   "20 docs fetched from the host doc store"}
+    if ref is not None:
+        out["parity"] = {"queries_checked": nq, "mismatches": mism}
+    d.close()
+    return out
+
+
 def fanout(plans, gs, gd, gn, streams, torch, dev):
     """One fan-out step's shard executes: every shard's plan on its own stream
     (the shards are independent, so one shard's tail overlaps the next one's
@@ -277,16 +328,8 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     for off, tok in parts:
         x = native.docs_stats(off, tok, synth.VOCAB, threads=threads)
         g = x if g is None else g + x
-    old = os.environ.get("FUGU_RANK_GIB")
-    os.environ["FUGU_RANK_GIB"] = "12"
-    try:
-        ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=False, global_stats=g)
-               for off, tok in parts]
-    finally:
-        if old is None:
-            os.environ.pop("FUGU_RANK_GIB")
-        else:
-            os.environ["FUGU_RANK_GIB"] = old
+    ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=False, global_stats=g)
+           for off, tok in parts]
     del parts
     build_s = time.time() - t0
     log(f"[bench] C5: 100M docs as 8 shards built in {build_s:.1f}s")
@@ -350,6 +393,135 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     return ent
 
 
+def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist):
+    """BASELINE configs[3] (c4) / configs[4] (c5) across the job's GPUs (strong
+    scaling: the corpus is fixed, its 8 units are split over the ranks):
+      c4: the 10M-doc corpus as 8 namespaces x 1.25M (own statistics each), a
+          fan-out 3-term AND top-100 batch;
+      c5: 100M docs, Zipf s = 1.1, as 8 doc shards scored with the namespace's
+          global statistics (one all-reduce of the shard statistics at build),
+          a 2-5-term OR top-1000 batch.
+    Rank r holds units [8r/N, 8(r+1)/N) on its GPU, their plans linked (one
+    shared threshold per query); a step = every unit's kernels, the rank's
+    device merge, ONE all-gather of the rank lists (RCCL over xGMI) and the
+    final device merge by (score desc, unit asc, doc asc).  Every rank prints
+    nothing; rank 0 prints the JSON line, with a hash of the merged hits (equal
+    for every N)."""
+    import hashlib
+
+    from fugu_amd import native, synth
+    from fugu_amd.shard import allreduce_stats, gather_packed, merge_on_device, shard_ranges
+    c4 = cfg == "c4"
+    N, S, K = (10_000_000, 1.0, 100) if c4 else (100_000_000, 1.1, 1000)
+    mode = native.MODE_AND if c4 else native.MODE_OR
+    nq = args.batch
+    units = 8
+    if units % world:
+        raise SystemExit(f"--config {cfg}: {units} units do not split over {world} ranks")
+    ranges = shard_ranges(N, units)
+    per = units // world
+    mine = list(range(rank * per, (rank + 1) * per))
+    t0 = time.time()
+    parts = []
+    for u in mine:
+        b, e = ranges[u]
+        c = synth.corpus(e - b, synth.VOCAB, S, doc_begin=b, threads=threads)
+        parts.append((c.off, c.tok))
+    ctx = native.Context((local,))
+    g = None
+    if not c4:  # global statistics: the rank's shards summed, then one all-reduce over the ranks
+        for off, tok in parts:
+            x = native.docs_stats(off, tok, synth.VOCAB, threads=threads)
+            g = x if g is None else g + x
+        if world > 1:
+            g = allreduce_stats(g, device=dev if backend == "nccl" else None)
+    ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=False, global_stats=g)
+           for off, tok in parts]
+    del parts
+    build_s = time.time() - t0
+    log(f"[bench] {cfg}: rank {rank} built units {mine} in {build_s:.1f}s")
+    q_off, terms = synth.queries(nq, 3, 3) if c4 else synth.queries(nq, 2, 5)
+    plans = [ix.plan(q_off, terms, K, mode) for ix in ixs]
+    if len(plans) > 1:
+        native.link_plans(plans)
+    gs = torch.empty((len(plans), nq * K), dtype=torch.float32, device=dev)
+    gd = torch.empty((len(plans), nq * K), dtype=torch.int32, device=dev)
+    gn = torch.empty((len(plans), nq), dtype=torch.int32, device=dev)
+    # unit u's doc d as a global id: c5 the corpus doc id, c4 (namespace << 24) | doc
+    off_u = torch.tensor([ranges[u][0] if not c4 else (u << 24) for u in mine], dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    out = {}
+
+    def step():
+        for r, p in enumerate(plans):  # plans[0] first: it zeroes the shared thresholds
+            p.execute(st.cuda_stream, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+        ms, md, msh, mn = merge_on_device(gs, gd, gn, nq, K, st.cuda_stream)
+        gdoc = (md.to(torch.int64) + off_u[msh.to(torch.int64)]).to(torch.int32)
+        if world > 1:
+            s2, d2, c2 = gather_packed(ms, gdoc, mn)
+            out["m"] = merge_on_device(s2, d2, c2, nq, K, st.cuda_stream)
+        else:
+            out["m"] = (ms, gdoc, None, mn)
+
+    for p in plans:
+        p.profile(True)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    for p in plans:
+        p.kernel_ms()  # drop the warmup's events
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    kms = [p.kernel_ms() for p in plans]
+    kern = sum(m[0][0] for m in kms) / max(kms[0][1], 1)
+    fin = sum(m[0][1] for m in kms) / max(kms[0][1], 1)
+    if world > 1:
+        t = torch.tensor([el, kern], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kern = float(t[0].item()), float(t[1].item())
+    ms, md, _, mn = out["m"]
+    mn = mn.cpu().numpy()
+    ms = ms.cpu().numpy().reshape(nq, K)
+    md = md.cpu().numpy().view(np.uint32).reshape(nq, K)
+    h = hashlib.sha1()
+    for i in range(nq):
+        h.update(md[i, :mn[i]].tobytes())
+        h.update(ms[i, :mn[i]].tobytes())
+    if rank == 0:
+        kname = "k_conj" if c4 else "k_disj"
+        line = {
+            "metric": METRIC, "value": round(nq * args.steps / el, 1), "unit": "queries/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32+f32",
+            "data": "synthetic",
+            "config": {"workload": ("C4: 10M docs as 8 namespaces x 1.25M, fan-out 3-term AND top-100"
+                                    if c4 else "C5: 100M docs Zipf s=1.1 as 8 doc shards (global BM25 statistics), "
+                                               "2-5-term OR top-1000"),
+                       "n_docs": N, "batch": nq, "k": K, "units": units, "units_per_gpu": per,
+                       "parallelism": f"{'namespace' if c4 else 'doc'}-shard x{world}" + (
+                           (" + RCCL all-gather top-k" if backend == "nccl" else f" + {backend} all-gather (rehearsal)")
+                           if world > 1 else "")},
+            "kernels_ms_per_step_max_rank": {kname: round(kern, 4), "k_final": round(fin, 4)},
+            "result_sha1": h.hexdigest()[:16],
+            "hits": int(mn.sum()),
+            "snapshot_build_s_rank0": round(build_s, 1),
+            "cpu_baseline": None,
+            "note": "strong scaling of one fixed corpus; the headline mode (no --config) carries the CPU baseline "
+                    "and the roofline",
+        }
+        print(json.dumps(line), flush=True)
+    del plans[1:]
+    del plans
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -373,6 +545,8 @@ def main():
                          "1 -> 697K, 2 -> 816K, 4 -> 934K, 8 -> 868K q/s)")
     ap.add_argument("--disj", action="store_true",
                     help="headline batch = 2-5-term OR (k_disj; profiling runs, pass --k 1000 --no-cpu)")
+    ap.add_argument("--config", choices=["headline", "c4", "c5"], default="headline",
+                    help="c4 / c5: BASELINE configs[3] / [4] split over the job's GPUs (strong scaling)")
     args = ap.parse_args()
 
     import torch
@@ -396,6 +570,11 @@ def main():
 
     cores = host_cores()
     threads = args.threads or cores["nproc"]
+    if args.config != "headline":
+        run_config(args, args.config, rank, world, local, dev, backend, threads, torch, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     t0 = time.time()
     # namespace r: its own corpus (seeds offset by rank); rank 0 is the standard corpus
     corp = synth.corpus(args.docs, synth.VOCAB, 1.0, synth.SEED_L + rank, synth.SEED_T + rank, threads=threads)
@@ -471,7 +650,13 @@ def main():
     # layout (fg_bytes_model_gpu: k_conj's exhaustive cascade) over
     # its HIP-event time on the launch stream.  The SURVEY 8(d) tantivy byte
     # model (1 KiB block decode per probed block) is reported beside it, labelled.
-    bmg = ix.bytes_model_gpu(q_off, terms, K, qmode)
+    if args.disj:
+        # k_disj: MaxScore bytes at each query's final k-th score (fg_bytes_model_or)
+        s_h = out_s.cpu().numpy().reshape(nq, K)
+        n_h = out_n.cpu().numpy()
+        bmg = ix.bytes_model_or(q_off, terms, K, np.where(n_h >= K, s_h[:, K - 1], 0.0).astype(np.float32))
+    else:
+        bmg = ix.bytes_model_gpu(q_off, terms, K, qmode)
     alg_bytes = float(bmg[:, 3].sum())
     # (FG_MODE_OR: the exhaustive union is both models)
     cpu_model_bytes = alg_bytes if args.disj else float(ix.bytes_model(q_off, terms, K)[:, 2].sum())
@@ -545,7 +730,8 @@ def main():
     extra = None
     if rank == 0 and world == 1 and not args.no_extra:
         extra = {}
-        specs = [("C3_mixed_and", 1, 5, 100, native.MODE_AND), ("OR_top1000_10M", 2, 5, 1000, native.MODE_OR)]
+        specs = [("C3_mixed_and", 1, 5, 100, native.MODE_AND), ("OR_top1000_10M", 2, 5, 1000, native.MODE_OR),
+                 ("OR_top20_default_api", 2, 5, 20, native.MODE_OR)]
         for name, a_min, a_max, kk, mode in specs:
             qo_all, qt_all = synth.queries(4096, a_min, a_max)
             qo = qo_all[: nq + 1].copy()
@@ -567,6 +753,9 @@ def main():
             kms, kn = pl2.kernel_ms()
             dfs = np.array([ix.df(int(t)) for t in qt], np.float64)
             merge_bytes = 8.0 * dfs.sum()  # every posting of every clause once (exhaustive merge/union)
+            s2 = os2.cpu().numpy().reshape(nq, kk)
+            d2 = od2.cpu().numpy().view(np.uint32).reshape(nq, kk)
+            n2 = on2.cpu().numpy()
             ent = {"value": round(nq * args.extra_steps / el, 1), "unit": "queries/s",
                    "ms_per_step": round(el * 1e3 / args.extra_steps, 4), "batch": nq, "k": kk,
                    "terms": f"{a_min}-{a_max}", "mode": "AND" if mode == native.MODE_AND else "OR",
@@ -574,10 +763,23 @@ def main():
                    "kernel_ms": round(kms[0] / max(kn, 1), 4), "k_final_ms": round(kms[1] / max(kn, 1), 4),
                    "merge_bytes_per_launch": merge_bytes,
                    "merge_equiv_gbs": round(merge_bytes / (kms[0] / max(kn, 1) * 1e-3) / 1e9, 1)}
+            if mode == native.MODE_OR and kk == 1000:
+                # device-layout MaxScore bytes at each query's final k-th score (fg_bytes_model_or):
+                # the least an exact k_disj reads, over the kernel's time
+                thr = np.where(n2 >= kk, s2[:, kk - 1], 0.0).astype(np.float32)
+                bo = ix.bytes_model_or(qo, qt, kk, thr)
+                kms_ = kms[0] / max(kn, 1)
+                ent["roofline"] = {"bound": "hbm", "kernel": "k_disj", "alg_bytes_per_launch": float(bo[:, 3].sum()),
+                                   "alg_bytes_split": {"stream": float(bo[:, 0].sum()), "probe": float(bo[:, 1].sum()),
+                                                       "output": float(bo[:, 2].sum())},
+                                   "achieved": round(float(bo[:, 3].sum()) / (kms_ * 1e-3) / 1e9, 1),
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(float(bo[:, 3].sum()) / (kms_ * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "alg_model": "fg_bytes_model_or: MaxScore over 4096-doc tiles at the final k-th "
+                                                "score (12 B per tile-clause bound, 8 B per essential posting, rank "
+                                                "word / bucket max per posting past the tile bound, 4 B score per "
+                                                "present clause past the presence bound, 8 B per kept key)"}
             if ref is not None:
-                s2 = os2.cpu().numpy().reshape(nq, kk)
-                d2 = od2.cpu().numpy().view(np.uint32).reshape(nq, kk)
-                n2 = on2.cpu().numpy()
                 done, wall, mism = 0, 0.0, 0
                 budget = args.cpu_seconds / 2
                 while done < nq and wall < budget:
@@ -607,6 +809,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_extra:
         extra["commit_10M"] = commit_latency(ctx, ix, corp, native, synth, threads)
         log(f"[bench] commit on the 10M namespace: {extra['commit_10M']['commit_ms']} ms")
+        extra["db_api_default_search_10M_8seg"] = bench_db_api(ctx, corp, native, synth, ref, threads)
+        log(f"[bench] GET /search (OR, limit 20) through fg_db_search on 8 segments: "
+            f"p50 {extra['db_api_default_search_10M_8seg']['p50_ms']} ms")
     del plan
     ix.close()
     if rank == 0 and world == 1 and not args.no_extra:
@@ -650,11 +855,13 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": kname, "kernel_ms": round(conj_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
-                "alg_model": "fg_bytes_model_gpu: k_conj's exhaustive cascade at the HBM layout (8 B per lead "
-                             "posting; per probe 8 B rank word + 4 B score on a hit, or 8 B bucket bounds + 4 B per search step + "
-                             "4 B compare + 4 B score on a hit; 8 B per kept key)",
-                "alg_bytes_split": {"lead": float(bmg[:, 0].sum()), "probe": float(bmg[:, 1].sum()),
-                                    "output": float(bmg[:, 2].sum())},
+                "alg_model": ("fg_bytes_model_or: k_disj's MaxScore at the final k-th score (DESIGN.md §5)"
+                              if args.disj else
+                              "fg_bytes_model_gpu: k_conj's exhaustive cascade at the HBM layout (8 B per lead "
+                              "posting; per probe 8 B rank word + 4 B score on a hit, or 8 B bucket bounds + 4 B per "
+                              "search step + 4 B compare + 4 B score on a hit; 8 B per kept key)"),
+                "alg_bytes_split": {("stream" if args.disj else "lead"): float(bmg[:, 0].sum()),
+                                    "probe": float(bmg[:, 1].sum()), "output": float(bmg[:, 2].sum())},
                 "traffic_over_alg": round(traffic / alg_bytes, 3) if traffic else None,
                 "traffic_source": pmc.get("source") if traffic else None,
                 "hbm_gbs_measured": (round(traffic / (conj_ms * 1e-3) / 1e9, 1) if traffic else None),

@@ -45,6 +45,10 @@ constexpr uint32_t kDenseDiv = FG_DENSE_DIV;  // terms in >= 1/kDenseDiv of the 
 constexpr uint64_t kDenseBudget = (uint64_t)FG_DENSE_GIB << 30;  // ... densest first, within this many bytes
 constexpr uint32_t kRankDiv = FG_RANK_DIV;    // terms in >= 1/kRankDiv of the docs may get rank words
 constexpr uint64_t kRankBudget = (uint64_t)FG_RANK_GIB << 30;    // ... densest first, within this many bytes
+#ifndef FG_RANK_FACTOR
+#define FG_RANK_FACTOR 4.0  // tools/ab_rank_budget.py sweep (profiles/r03/ab_rank_sweep.log); env FUGU_RANK_FACTOR
+#endif
+constexpr double kRankFactor = FG_RANK_FACTOR;  // ... and within this many times the snapshot's posting bytes
 constexpr uint32_t kMaxDense = 32767;     // slots per kind (tmeta bits 16-30)
 constexpr uint32_t kRankChunkWords = 2048;  // k_rank: words (65536 docs) per workgroup
 #ifndef FG_DISJ_GPQ

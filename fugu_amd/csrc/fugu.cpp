@@ -45,6 +45,7 @@ int fail(int code, const char* fmt, ...) {
 
 // shared with host.cpp so fg_last_error() reports host-side failures too
 void fg_set_last_error(const std::string& msg) { g_err = msg; }
+int fg_host_threads();  // below (hw_threads(0)), shared with host.cpp
 
 namespace {
 
@@ -190,6 +191,10 @@ int hw_threads(int req) {
   }();
   return n;
 }
+
+}  // namespace
+int fg_host_threads() { return hw_threads(0); }
+namespace {
 
 // Host-side postings before upload (merged text U name per term).
 struct HostPostings {
@@ -765,12 +770,15 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   std::vector<uint32_t>().swap(hp.tf);
   std::vector<uint32_t>().swap(dir);
   g_bt.mark("upload");
-  // rank words for the densest terms (fg_internal.h DevIndex), chosen AFTER the
-  // uploads above so the budget sees the memory actually left: df >= N /
-  // kRankDiv, densest first (ties by term id), within FUGU_RANK_GIB and a
-  // quarter of the free memory; a failed allocation is retried with half the
-  // terms (down to none), so a build never fails for want of them.  They hang
-  // on doc ids only, so rescored snapshots share them.
+  // rank words for the densest terms (fg_internal.h DevIndex): df >= N /
+  // kRankDiv, densest first (ties by term id), within a budget of the
+  // snapshot's own: FUGU_RANK_FACTOR (default kRankFactor) times its postings'
+  // bytes (doc id + tf + score, 12 B each), at most FUGU_RANK_GIB -- so a
+  // namespace's share depends on its size, not on how many namespaces were
+  // built on the device before it.  A quarter of the free memory caps it only
+  // when HBM is short, and a failed allocation is retried with half the terms
+  // (down to none), so a build never fails for want of them.  They hang on doc
+  // ids only, so rescored snapshots share them.
   std::vector<uint32_t> by_df;
   for (uint32_t t = 0; t < V; ++t)
     if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * fg::kRankDiv >= N) by_df.push_back(t);
@@ -782,7 +790,10 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint64_t* d_rank = nullptr;
   {
     const char* v = getenv("FUGU_RANK_GIB");
-    const uint64_t want = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kRankBudget;
+    const uint64_t cap = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kRankBudget;
+    const char* f = getenv("FUGU_RANK_FACTOR");
+    const double factor = f && *f ? atof(f) : fg::kRankFactor;
+    const uint64_t want = std::min<uint64_t>(cap, (uint64_t)(factor * 12.0 * (double)hp.off[V]));
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t brk = std::min<uint64_t>(want, free_b / 4);

@@ -17,6 +17,7 @@
 #include <shared_mutex>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -24,6 +25,7 @@
 #include "../../include/fugu_host.h"
 
 void fg_set_last_error(const std::string& msg);  // fugu.cpp
+int fg_host_threads();                           // fugu.cpp: FUGU_THREADS / the process's CPU share
 
 namespace {
 
@@ -1239,6 +1241,92 @@ int fg_db_commit(fg_db* db, const char* nsname) {
     ns->st_df_facet.swap(df_f);
   }
   return FG_OK;
+}
+
+int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* ids, const uint64_t* id_off,
+                       const char* texts, const uint64_t* text_off) {
+  // batch_upsert_objects (src/server/handlers/ingest.rs:160-220) -> Dataset::
+  // batch_upsert -> NamedIndex::upsert (src/db/document.rs:23-73): every record
+  // validated first ("Validation failed for object at index i: ..."), then
+  // upserted in order under the writer lock (raw-id delete, add), then ONE
+  // commit (one segment).  Records are {id, text} (no metadata, namespace or facets).  The
+  // "default" analyzer runs on the host threads before the lock (each thread
+  // interns into its own dictionary; the dictionaries merge into the
+  // namespace's under the lock), so a bulk load does not serialise on it.
+  if (!db || (n && (!ids || !id_off || !texts || !text_off))) return hfail(FG_EINVAL, "bad arguments");
+  auto ns = find_ns(db, nsname);
+  if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
+  auto sv = [](const char* b, const uint64_t* off, uint32_t i) { return std::string_view(b + off[i], off[i + 1] - off[i]); };
+  for (uint32_t i = 0; i < n; ++i) {  // ObjectRecord::validate (src/object.rs:31-78)
+    const std::string_view id = sv(ids, id_off, i), tx = sv(texts, text_off, i);
+    const char* e = id.empty() ? "Object ID cannot be empty"
+                    : id.size() > 256 ? "Object ID too long (max 256 characters)"
+                    : tx.empty() ? "Object text cannot be empty"
+                    : tx.size() > 10000 ? "Text too long (max 10000 characters)" : nullptr;
+    if (e) return hfail(FG_EINVAL, "Validation failed for object at index " + std::to_string(i) + ": " + e);
+  }
+  const int T = std::max(1, std::min<int>(fg_host_threads(), (int)(n / 4096) + 1));
+  std::vector<std::unordered_map<std::string, uint32_t>> ldict(T);
+  std::vector<std::vector<const std::string*>> lterms(T);
+  std::vector<Doc> docs(n);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        const uint32_t b = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T);
+        std::vector<std::string> toks;
+        for (uint32_t i = b; i < e; ++i) {
+          Doc& d = docs[i];
+          d.id = std::string(sv(ids, id_off, i));
+          d.text = std::string(sv(texts, text_off, i));
+          analyze(d.text, toks);
+          d.text_tok.reserve(toks.size());
+          for (auto& w : toks) {
+            auto it = ldict[t].find(w);
+            if (it == ldict[t].end()) {
+              it = ldict[t].emplace(std::move(w), (uint32_t)lterms[t].size()).first;
+              lterms[t].push_back(&it->first);
+            }
+            d.text_tok.push_back(it->second);  // thread-local id until the merge
+          }
+          analyze(d.id, d.id_tokens);
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  {  // the writer lock: the dictionary merge and the ordered upserts
+    std::lock_guard<std::mutex> w(ns->writer);
+    std::vector<std::vector<uint32_t>> remap(T);
+    for (int t = 0; t < T; ++t) {
+      remap[t].resize(lterms[t].size());
+      for (size_t j = 0; j < lterms[t].size(); ++j) {
+        auto it = ns->dict.find(*lterms[t][j]);
+        if (it == ns->dict.end()) it = ns->dict.emplace(*lterms[t][j], (uint32_t)ns->dict.size()).first;
+        remap[t][j] = it->second;
+      }
+    }
+    {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+          const uint32_t b = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T);
+          for (uint32_t i = b; i < e; ++i)
+            for (auto& x : docs[i].text_tok) x = remap[t][x];
+        });
+      for (auto& x : th) x.join();
+    }
+    ns->docs.reserve(ns->docs.size() + n);
+    for (uint32_t i = 0; i < n; ++i) {
+      // delete_term(id_field, raw id) (src/db/document.rs:38-42), then add_document
+      auto it = ns->by_id_token.find(docs[i].id);
+      if (it != ns->by_id_token.end())
+        for (uint32_t d : it->second) ns->docs[d].deleted = true;
+      const uint32_t d = (uint32_t)ns->docs.size();
+      for (auto& t : docs[i].id_tokens) ns->by_id_token[t].push_back(d);
+      ns->docs.push_back(std::move(docs[i]));
+    }
+  }
+  return fg_db_commit(db, nsname);  // NamedIndex::upsert commits once per call (src/db/document.rs:65)
 }
 
 int fg_db_add_file(fg_db* db, const char* ns, const char* name, const char* body) {

@@ -17,6 +17,7 @@
 //            h3(seed_Q, q, i), i = 0,1,..., duplicates skipped, Zipf(s_q) on [1,max_rank]
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -128,6 +129,72 @@ int fgs_fill_tokens(uint64_t doc_begin, uint32_t n, const uint64_t* doc_off, uin
     }
   });
   return 0;
+}
+
+// Decimal digits of x at out (no terminator); returns the length.
+inline int put_u64(char* out, uint64_t x) {
+  char t[24];
+  int n = 0;
+  do { t[n++] = (char)('0' + x % 10); x /= 10; } while (x);
+  for (int i = 0; i < n; ++i) out[i] = t[n - 1 - i];
+  return n;
+}
+
+// Docs as text for the host mirror's ingest path: token id t is the word
+// "t<t>" (lowercase alphanumeric: the "default" analyzer keeps it as one token),
+// words joined by ' '.  out == NULL: only the byte total; else out receives the
+// texts back to back and out_off[n+1] their offsets.
+uint64_t fgs_render_text(const uint64_t* doc_off, const uint32_t* tok, uint32_t n, char* out, uint64_t* out_off,
+                         int threads) {
+  auto word_len = [](uint32_t t) {
+    int l = 2;
+    while (t >= 10) { t /= 10; ++l; }
+    return l;  // 't' + digits
+  };
+  std::vector<uint64_t> len(n + 1, 0);
+  parallel_for(n, threads, [&](uint32_t b, uint32_t e) {
+    for (uint32_t i = b; i < e; ++i) {
+      uint64_t l = 0;
+      for (uint64_t p = doc_off[i]; p < doc_off[i + 1]; ++p) l += word_len(tok[p]) + (p + 1 < doc_off[i + 1] ? 1 : 0);
+      len[i] = l;
+    }
+  });
+  uint64_t pos = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t l = len[i];
+    len[i] = pos;
+    pos += l;
+  }
+  len[n] = pos;
+  if (out_off) std::memcpy(out_off, len.data(), 8ull * (n + 1));
+  if (out)
+    parallel_for(n, threads, [&](uint32_t b, uint32_t e) {
+      for (uint32_t i = b; i < e; ++i) {
+        char* o = out + len[i];
+        for (uint64_t p = doc_off[i]; p < doc_off[i + 1]; ++p) {
+          *o++ = 't';
+          o += put_u64(o, tok[p]);
+          if (p + 1 < doc_off[i + 1]) *o++ = ' ';
+        }
+      }
+    });
+  return pos;
+}
+
+// Doc id strings "d<doc_begin + i>" for i < n, as fgs_render_text lays texts out.
+uint64_t fgs_render_ids(uint64_t doc_begin, uint32_t n, char* out, uint64_t* out_off) {
+  uint64_t pos = 0;
+  char buf[24];
+  for (uint32_t i = 0; i < n; ++i) {
+    if (out_off) out_off[i] = pos;
+    int len = 0;
+    buf[len++] = 'd';
+    len += put_u64(buf + len, doc_begin + i);
+    if (out) std::memcpy(out + pos, buf, (size_t)len);
+    pos += (uint64_t)len;
+  }
+  if (out_off) out_off[n] = pos;
+  return pos;
 }
 
 // Query stream: q_off[n_queries+1], q_terms[n_queries*m_max] (term ids).

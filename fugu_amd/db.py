@@ -26,7 +26,7 @@ HOST_EXPORTS = (
     "fg_db_create", "fg_db_destroy", "fg_db_namespace_create", "fg_db_namespace_delete",
     "fg_db_namespaces_json", "fg_db_upsert", "fg_db_commit", "fg_db_add_file", "fg_db_doc_count",
     "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query", "fg_parse_query_occur",
-    "fg_db_upsert_record", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
+    "fg_db_upsert_record", "fg_db_upsert_batch", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
     "fg_facet_clauses", "fg_db_search_json_post",
 )
 
@@ -64,6 +64,7 @@ _sig("fg_db_doc_count", _p, _s, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
 _sig("fg_db_search", _p, _s, _s, C.c_uint32, C.c_uint32, C.POINTER(Hit), C.c_uint32, C.POINTER(C.c_uint32))
 _sig("fg_db_search_json", _p, _s, _s, C.c_uint32, C.c_uint32, C.c_int, C.c_int, _s, _sz, C.POINTER(_sz))
 _sig("fg_db_upsert_record", _p, _s, C.POINTER(_Record))
+_sig("fg_db_upsert_batch", _p, _s, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
 _sig("fg_db_search_ex", _p, _s, _s, C.POINTER(_s), C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(Hit), C.c_uint32,
      C.POINTER(C.c_uint32))
 _sig("fg_db_search_json_ex", _p, _s, _s, C.POINTER(_s), C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, _s,
@@ -220,6 +221,30 @@ class Database:
         r = _Record(_b(obj.id), _b(obj.text), _b(meta), _b(rec_ns), _b(obj.organization),
                     _b(obj.conversation_id), _b(obj.data_type), farr, nf, 1 if obj.facets is not None else 0)
         _check(_lib.fg_db_upsert_record(self._h, _b(ns), C.byref(r)))
+
+    def upsert_batch(self, namespace: Optional[str], ids=None, texts=None, text_buf=None, text_off=None,
+                     id_buf=None, id_off=None):
+        """POST /batch/upsert: records {id, text}, validated first, upserted in
+        order, one commit.  ids / texts: lists of str, or each as one UTF-8
+        buffer (bytes / uint8 array) with offsets [n+1]."""
+        import numpy as np
+        if ids is not None:
+            ib = b"".join(x.encode() for x in ids)
+            io = np.cumsum([0] + [len(x.encode()) for x in ids]).astype(np.uint64)
+        else:
+            ib, io = bytes(np.ascontiguousarray(id_buf, np.uint8)), np.ascontiguousarray(id_off, np.uint64)
+        n = len(io) - 1
+        if texts is not None:
+            enc = [x.encode() for x in texts]
+            text_buf = np.frombuffer(b"".join(enc), np.uint8)
+            text_off = np.cumsum([0] + [len(x) for x in enc]).astype(np.uint64)
+        tb = np.ascontiguousarray(np.frombuffer(text_buf, np.uint8) if isinstance(text_buf, bytes) else text_buf,
+                                  np.uint8)
+        to = np.ascontiguousarray(text_off, np.uint64)
+        ibuf = np.frombuffer(ib, np.uint8) if ib else np.zeros(1, np.uint8)
+        _check(_lib.fg_db_upsert_batch(self._h, _b(namespace), n, ibuf.ctypes.data, io.ctypes.data,
+                                       tb.ctypes.data if tb.size else np.zeros(1, np.uint8).ctypes.data,
+                                       to.ctypes.data))
 
     def doc_facets(self, namespace: Optional[str], doc: int) -> list:
         out = _string_call(_lib.fg_db_doc_facets, self._h, _b(namespace), doc)

@@ -27,6 +27,10 @@ _lib.fgs_doc_lengths.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32,
 _lib.fgs_fill_tokens.restype = C.c_int
 _lib.fgs_fill_tokens.argtypes = [C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint32, C.c_double, C.c_uint64,
                                  C.c_void_p, C.c_int]
+_lib.fgs_render_text.restype = C.c_uint64
+_lib.fgs_render_text.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int]
+_lib.fgs_render_ids.restype = C.c_uint64
+_lib.fgs_render_ids.argtypes = [C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
 _lib.fgs_queries.restype = C.c_int
 _lib.fgs_queries.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, C.c_uint64, C.c_void_p,
                              C.c_void_p]
@@ -67,6 +71,26 @@ def queries(n_queries: int, m_min: int, m_max: int, max_rank: int = QUERY_MAX_RA
     if rc != 0:
         raise ValueError("bad query parameters")
     return q_off, q_terms[: q_off[-1]].copy()
+
+
+def render_text(c: "Corpus", threads: int = 0):
+    """The docs as text ("t<id>" words): (uint8 buffer, uint64 offsets [n+1]) for the
+    host mirror's ingest path (fg_db_upsert_batch)."""
+    th = threads if threads > 0 else min(os.cpu_count() or 1, 32)
+    off = np.zeros(c.n_docs + 1, np.uint64)
+    total = _lib.fgs_render_text(c.off.ctypes.data, c.tok.ctypes.data, c.n_docs, None, off.ctypes.data, th)
+    buf = np.empty(max(int(total), 1), np.uint8)
+    _lib.fgs_render_text(c.off.ctypes.data, c.tok.ctypes.data, c.n_docs, buf.ctypes.data, off.ctypes.data, th)
+    return buf[: int(total)], off
+
+
+def render_ids(n: int, doc_begin: int = 0):
+    """Doc ids "d<i>" for i in [doc_begin, doc_begin + n): (uint8 buffer, uint64 offsets)."""
+    total = _lib.fgs_render_ids(doc_begin, n, None, None)
+    buf = np.empty(max(int(total), 1), np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    _lib.fgs_render_ids(doc_begin, n, buf.ctypes.data, off.ctypes.data)
+    return buf[: int(total)], off
 
 
 def mix64(z: int) -> int:

@@ -81,6 +81,13 @@ typedef struct fg_object_record {
   int has_facets;               /* Some(facets) (even empty) vs None */
 } fg_object_record;
 int fg_db_upsert_record(fg_db* db, const char* ns, const fg_object_record* rec);
+/* POST /batch/upsert (src/server/handlers/ingest.rs:160-220, Dataset::
+ * batch_upsert src/db/document.rs:70-73): n records {id, text} (no metadata,
+ * namespace or facets) as two byte buffers with offsets [n+1]; every record is
+ * validated before any is upserted, then one commit (one segment), as
+ * NamedIndex::upsert commits once per call (src/db/document.rs:65). */
+int fg_db_upsert_batch(fg_db* db, const char* ns, uint32_t n, const char* ids, const uint64_t* id_off,
+                       const char* texts, const uint64_t* text_off);
 int fg_db_upsert(fg_db* db, const char* ns, const char* id, const char* text, const char* name,
                  const char* metadata_json);
 int fg_db_commit(fg_db* db, const char* ns);

@@ -705,3 +705,26 @@ def test_db_failed_commit_leaves_statistics_unchanged(db, monkeypatch):
         assert hits_of([g[0] for g in got], [g[1] for g in got]) == hits_of(s, dd), q
         checked += len(got)
     assert checked > 50
+
+
+def test_upsert_batch_validates_first_and_upserts_in_order(db):
+    """POST /batch/upsert: a bad record rejects the whole batch with its index;
+    otherwise every record is upserted in order (raw-id deletes included) and
+    one commit runs (no device here: FG_ENODEV after the upserts)."""
+    from fugu_amd import synth
+    d = db.Database()
+    with pytest.raises(db.native.FuguError) as e:
+        d.upsert_batch(None, ["a", "", "c"], ["x", "y", "z"])
+    assert "Validation failed for object at index 1: Object ID cannot be empty" in str(e.value)
+    assert d.doc_count() == (0, 0)
+    with pytest.raises(db.native.FuguError) as e:
+        d.upsert_batch(None, ["a", "b", "a"], ["x y", "z", "w"])
+    assert e.value.code == db.native.FG_ENODEV
+    assert d.doc_count() == (3, 2)  # the second "a" deleted the first
+    c = synth.corpus(50)
+    buf, off = synth.render_text(c)
+    first = bytes(buf[int(off[0]):int(off[1])]).decode()
+    assert first.split() == [f"t{t}" for t in c.tok[c.off[0]:c.off[1]]]
+    with pytest.raises(db.native.FuguError):
+        d.upsert_batch(None, [f"d{i}" for i in range(50)], text_buf=buf, text_off=off)
+    assert d.doc_count() == (53, 52)
