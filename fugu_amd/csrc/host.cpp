@@ -131,6 +131,68 @@ void analyze(std::string_view s, std::vector<std::string>& out) {
   }
 }
 
+// analyze() for bulk ingest: f(token) for each token as a string_view into a
+// scratch buffer (valid until the next call).  Pure-ASCII text takes a byte
+// loop (runs of [0-9A-Za-z], < 40 bytes, lowercased): the same tokens as
+// analyze(), whose Unicode path handles everything else.
+template <class F>
+void analyze_each(std::string_view s, std::string& scratch, std::vector<std::string>& toks, F&& f) {
+  bool ascii = true;
+  for (unsigned char c : s) ascii = ascii && c < 0x80;
+  if (!ascii) {
+    analyze(s, toks);
+    for (auto& t : toks) f(std::string_view(t));
+    return;
+  }
+  auto alnum = [](unsigned char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); };
+  size_t i = 0;
+  while (i < s.size()) {
+    while (i < s.size() && !alnum((unsigned char)s[i])) ++i;
+    const size_t b = i;
+    while (i < s.size() && alnum((unsigned char)s[i])) ++i;
+    if (i == b || i - b >= 40) continue;  // RemoveLongFilter
+    scratch.assign(s.data() + b, i - b);
+    for (char& c : scratch)
+      if (c >= 'A' && c <= 'Z') c = (char)(c + 32);
+    f(std::string_view(scratch));
+  }
+}
+
+// A thread's term dictionary during bulk ingest: open addressing over an
+// arena of the term bytes (no allocation per lookup).
+struct LocalDict {
+  std::string arena;
+  std::vector<std::pair<uint64_t, uint32_t>> ent;  // (arena offset << 8 | length, hash low bits)
+  std::vector<uint32_t> slot{std::vector<uint32_t>(1u << 16, 0)};  // entry + 1, 0 = empty
+  static uint64_t hash(std::string_view w) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ w.size();
+    for (unsigned char c : w) h = (h ^ c) * 0x100000001B3ull;
+    return h ^ (h >> 29);
+  }
+  std::string_view key(uint32_t e) const { return std::string_view(arena.data() + (ent[e].first >> 8), ent[e].first & 0xFF); }
+  uint32_t get(std::string_view w) {
+    if (2 * (ent.size() + 1) > slot.size()) grow();
+    const uint64_t h = hash(w);
+    for (size_t m = slot.size() - 1, i = h & m;; i = (i + 1) & m) {
+      if (!slot[i]) {
+        ent.emplace_back(((uint64_t)arena.size() << 8) | w.size(), (uint32_t)h);
+        arena.append(w.data(), w.size());
+        slot[i] = (uint32_t)ent.size();
+        return (uint32_t)ent.size() - 1;
+      }
+      const uint32_t e = slot[i] - 1;
+      if (ent[e].second == (uint32_t)h && key(e) == w) return e;
+    }
+  }
+  void grow() {
+    std::vector<uint32_t> ns(slot.size() * 2, 0);
+    for (uint32_t e = 0; e < ent.size(); ++e)
+      for (size_t m = ns.size() - 1, i = hash(key(e)) & m;; i = (i + 1) & m)
+        if (!ns[i]) { ns[i] = e + 1; break; }
+    slot.swap(ns);
+  }
+};
+
 // ---------------------------------------------------------------- query parser subset
 // QueryParser::for_index(index, [text, name]).parse_query (src/db/search.rs:108-127)
 // restricted to what the device runs (tantivy-query-grammar 0.24: the default
@@ -1266,8 +1328,7 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
     if (e) return hfail(FG_EINVAL, "Validation failed for object at index " + std::to_string(i) + ": " + e);
   }
   const int T = std::max(1, std::min<int>(fg_host_threads(), (int)(n / 4096) + 1));
-  std::vector<std::unordered_map<std::string, uint32_t>> ldict(T);
-  std::vector<std::vector<const std::string*>> lterms(T);
+  std::vector<LocalDict> ldict(T);
   std::vector<Doc> docs(n);
   {
     std::vector<std::thread> th;
@@ -1275,20 +1336,13 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
       th.emplace_back([&, t] {
         const uint32_t b = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T);
         std::vector<std::string> toks;
+        std::string scratch;
         for (uint32_t i = b; i < e; ++i) {
           Doc& d = docs[i];
           d.id = std::string(sv(ids, id_off, i));
           d.text = std::string(sv(texts, text_off, i));
-          analyze(d.text, toks);
-          d.text_tok.reserve(toks.size());
-          for (auto& w : toks) {
-            auto it = ldict[t].find(w);
-            if (it == ldict[t].end()) {
-              it = ldict[t].emplace(std::move(w), (uint32_t)lterms[t].size()).first;
-              lterms[t].push_back(&it->first);
-            }
-            d.text_tok.push_back(it->second);  // thread-local id until the merge
-          }
+          // thread-local term ids until the merge
+          analyze_each(d.text, scratch, toks, [&](std::string_view w) { d.text_tok.push_back(ldict[t].get(w)); });
           analyze(d.id, d.id_tokens);
         }
       });
@@ -1297,12 +1351,12 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
   {  // the writer lock: the dictionary merge and the ordered upserts
     std::lock_guard<std::mutex> w(ns->writer);
     std::vector<std::vector<uint32_t>> remap(T);
+    std::string key;
     for (int t = 0; t < T; ++t) {
-      remap[t].resize(lterms[t].size());
-      for (size_t j = 0; j < lterms[t].size(); ++j) {
-        auto it = ns->dict.find(*lterms[t][j]);
-        if (it == ns->dict.end()) it = ns->dict.emplace(*lterms[t][j], (uint32_t)ns->dict.size()).first;
-        remap[t][j] = it->second;
+      remap[t].resize(ldict[t].ent.size());
+      for (uint32_t j = 0; j < ldict[t].ent.size(); ++j) {
+        key.assign(ldict[t].key(j));
+        remap[t][j] = ns->dict.try_emplace(key, (uint32_t)ns->dict.size()).first->second;
       }
     }
     {
@@ -1316,6 +1370,7 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
       for (auto& x : th) x.join();
     }
     ns->docs.reserve(ns->docs.size() + n);
+    ns->by_id_token.reserve(ns->by_id_token.size() + n);
     for (uint32_t i = 0; i < n; ++i) {
       // delete_term(id_field, raw id) (src/db/document.rs:38-42), then add_document
       auto it = ns->by_id_token.find(docs[i].id);
