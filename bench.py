@@ -456,7 +456,9 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
         for r, p in enumerate(plans):  # plans[0] first: it zeroes the shared thresholds
             p.execute(st.cuda_stream, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
         ms, md, msh, mn = merge_on_device(gs, gd, gn, nq, K, st.cuda_stream)
-        gdoc = (md.to(torch.int64) + off_u[msh.to(torch.int64)]).to(torch.int32)
+        # slots past a query's count hold no hit (undefined shard / doc): clamp the
+        # gather index so it stays inside off_u; those slots are never read
+        gdoc = (md.to(torch.int64) + off_u[msh.to(torch.int64).clamp_(0, len(mine) - 1)]).to(torch.int32)
         if world > 1:
             s2, d2, c2 = gather_packed(ms, gdoc, mn)
             out["m"] = merge_on_device(s2, d2, c2, nq, K, st.cuda_stream)

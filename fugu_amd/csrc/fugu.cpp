@@ -449,7 +449,7 @@ struct UploadBatch {
   template <class T>
   void add(const T* src, size_t n, T** out) {
     es.push_back(E{src, n * sizeof(T), reinterpret_cast<void**>(out)});
-    total += (std::max<size_t>(n * sizeof(T), 16) + 255) & ~size_t(255);
+    total += (std::max<size_t>(n * sizeof(T), 16) + 16 + 255) & ~size_t(255);  // >= 16 B of slack after each array
   }
   int commit(DevAllocs& m, uint64_t* bytes) {
     void* p = nullptr;
@@ -460,7 +460,7 @@ struct UploadBatch {
       char* d = static_cast<char*>(p) + o;
       if (e.bytes) HIPCHK(hipMemcpy(d, e.src, e.bytes, hipMemcpyHostToDevice));
       *e.out = d;
-      o += (std::max<size_t>(e.bytes, 16) + 255) & ~size_t(255);
+      o += (std::max<size_t>(e.bytes, 16) + 16 + 255) & ~size_t(255);
     }
     *bytes += total;
     return FG_OK;
@@ -532,7 +532,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
     return FG_OK;
   };
   void* p;
-  if ((rc = dev_alloc(4ull * ix->n_postings, &p))) return rc;
+  if ((rc = dev_alloc(4ull * ix->n_postings + 16, &p))) return rc;  // 16 B of slack: k_conj's 16-B lead loads
   d_psc = static_cast<float*>(p);
   if ((rc = dev_alloc(4ull * ix->dir_entries, &p))) return rc;
   d_bmax = static_cast<float*>(p);
@@ -1746,8 +1746,7 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
                s_hb = al(4ull * nq);
   const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft +
                       s_fm + 4 * s_ch + 2 * s_hb;
-  // score histograms only for the queries of k_disj work items (k_conj keeps
-  // its per-item thresholds)
+  // one score histogram per query (DevPlan::hist: k_conj's and k_disj's running thresholds)
   const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]),
                s_hist = al(4ull * nq * fg::kQBins);
   const size_t s_ck = al(8ull * cand_off[nq]);
@@ -2115,7 +2114,9 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   // 1. plan every shard (one host thread per shard for a batch)
   auto plan = [&](uint32_t s) -> int {
     fg_plan* p = nullptr;
-    int rc = fg_plan_create(shards[s], q, k, &p);
+    // inline (one query): the upload is queued on this thread's stream, ahead of
+    // the execute on the same stream -- no host round trip per shard
+    int rc = plan_create(shards[s], q, k, &p, threaded);
     if (rc) return rc;
     plans[s].reset(p);
     return FG_OK;
@@ -2154,7 +2155,9 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     owner[s] = (int)s;
     for (uint32_t t = s + 1; t < n_shards; ++t)
       if (shards[t]->dev == shards[s]->dev) { grp.push_back(plans[t].get()); owner[t] = (int)s; }
-    if (grp.size() < 2) continue;
+    // a single query gains little from shared thresholds over a few segments and
+    // would pay the link's synchronous uploads on its latency path
+    if (grp.size() < 2 || !threaded) continue;
     if (int rc = fg_plan_link(grp.data(), (uint32_t)grp.size())) return rc;
     fg_plan* o = plans[s].get();
     HIPCHK(hipSetDevice(shards[s]->dev));
@@ -2192,6 +2195,21 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   for (hipEvent_t e : evs)
     if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
   HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
+  // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
+  const size_t span = 3 * o_k + 4ull * nq;
+  if (span <= (4ull << 20)) {
+    PinnedLease pin(shards[0]->pinned, span);
+    if (pin.p) {
+      HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
+      HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+      const char* h = static_cast<const char*>(pin.p);
+      std::memcpy(out_score, h, 4 * nk);
+      std::memcpy(out_doc, h + o_k, 4 * nk);
+      if (out_shard) std::memcpy(out_shard, h + 2 * o_k, 4 * nk);
+      std::memcpy(out_n, h + 3 * o_k, 4ull * nq);
+      return FG_OK;
+    }
+  }
   HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
   HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
   if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));

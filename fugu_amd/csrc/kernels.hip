@@ -145,6 +145,17 @@ __device__ uint64_t hist_threshold(const uint32_t* gh, uint32_t K, uint32_t lo, 
   return b < kQBins ? (uint64_t)(lo + (b << sh)) << 32 : 0ull;
 }
 
+// Add the LDS bins to the query's global histogram and clear them.
+__device__ inline void hist_add(uint32_t* lh, uint32_t* gh) {
+  for (uint32_t b = threadIdx.x; b < kQBins; b += kThreads) {
+    const uint32_t c = lh[b];
+    if (c) {
+      atomicAdd(&gh[b], c);
+      lh[b] = 0;
+    }
+  }
+}
+
 // Append `key` (when keep) to an LDS list through one LDS atomic per wave.
 __device__ inline void wave_append(bool keep, uint64_t key, uint64_t* list, uint32_t* count, uint32_t cap) {
   const uint32_t lane = lane_id();
@@ -468,6 +479,21 @@ __device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_
 // [0, n_single) (no probes; block-max chunk skipping), the general one
 // [n_single, total_chunks); separate launches keep the general kernel's
 // register allocation.
+// FG_LEADVEC (A/B): lead postings by 16-B loads
+#ifndef FG_LEADVEC
+#define FG_LEADVEC 0
+#endif
+struct alignas(4) U4a { uint32_t x, y, z, w; };  // a 16-B load at 4-B alignment
+// k_conj's running thresholds from the query's score histogram: every item
+// counts its final kept keys (its local top-k) into the query's bins when it
+// ends; k_final reads the bins' threshold once per query (FG_CONJ_HIST=3) --
+// the k-th best among all the query's items, where the threshold word carries
+// the best single item's k-th key.  A/B: 0 = off; 1 / 2 = items also read the
+// bins when they start / in their first chunk (tools/ab_variants.py,
+// ab_conj_hist.log).
+#ifndef FG_CONJ_HIST
+#define FG_CONJ_HIST 3
+#endif
 template <bool kSingle>
 __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPlan pl) {
   __shared__ ConjShared sh;
@@ -517,11 +543,22 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   // the plan's starting threshold (single-list queries: the term's K'-th best score)
   const uint64_t thr0 = pl.q_thr0[q];
   uint64_t pend = 0;
+#if FG_CONJ_HIST
+  uint32_t* const gh = pl.hist + (size_t)q * kQBins;
+  const uint32_t h_lo = pl.q_hlo[q], h_sh = pl.q_hsh[q];
+  // FG_CONJ_HIST=2: multi-list items read the bins in their first chunk, with
+  // its lead loads in flight; single-list items need it before the block-max skip
+  // FG_CONJ_HIST=3: count only (k_final reads the bins once per query)
+  const uint64_t thr_h = ((kSingle && FG_CONJ_HIST != 3) || FG_CONJ_HIST == 1)
+                             ? max(thr0, hist_threshold(gh, K, h_lo, h_sh, sh.scratch)) : thr0;
+#else
+  const uint64_t thr_h = thr0;
+#endif
   if (tid == 0) {
     sh.n_buf = 0;
     sh.n_dq = 0;
-    sh.thr = thr0;
-    pend = atomicMax(gthr, (unsigned long long)thr0);
+    sh.thr = thr_h;
+    pend = atomicMax(gthr, (unsigned long long)(thr_h & pl.pub_mask));
   }
 #ifdef FG_DIAG
   if (tid < 8) sh.dgc[tid] = 0;
@@ -531,7 +568,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   // maximum) cannot reach the threshold is not loaded.  thr_k is the threshold
   // as every thread last saw it (uniform), so the skip is uniform too.
   const float* __restrict__ cmax = ix.cmax + ix.coff[t0];
-  uint64_t thr_k = thr0;
+  uint64_t thr_k = thr_h;
   const bool defer = !kSingle && kDeferCap > 0 && m >= 3 && nm == m && !fmask;  // pure conjunctions
 
   for (uint32_t cc = 0; cc < nc; ++cc) {
@@ -545,6 +582,31 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
     uint32_t doc[kItems];
     float s0[kItems];
     uint32_t live = 0;
+#if FG_LEADVEC
+    // A/B: four consecutive postings per lane in one
+    // 16-B load (dword-aligned: gfx950 runs in unaligned access mode; the doc
+    // and score arrays carry 16 B of slack, so a group that starts inside the
+    // list may read up to 3 postings past it), item j of lane l =
+    // wv*512 + (j/4)*256 + 4l + j%4
+    static_assert(kItems == 8, "two 4-posting groups per lane");
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      const uint32_t i0 = wv * kWaveSpan + h * 256 + 4 * lane;
+      U4a d4{kInvalid, kInvalid, kInvalid, kInvalid}, p4{0u, 0u, 0u, 0u};
+      if (i0 < cnt) {
+        d4 = *reinterpret_cast<const U4a*>(ix.doc + base0 + i0);
+        p4 = *reinterpret_cast<const U4a*>(ix.psc + base0 + i0);
+      }
+      const uint32_t dv[4] = {d4.x, d4.y, d4.z, d4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+      for (uint32_t e = 0; e < 4; ++e) {
+        const bool in = i0 + e < cnt;
+        doc[4 * h + e] = in ? dv[e] : kInvalid;
+        s0[4 * h + e] = in ? __uint_as_float(pv[e]) : 0.0f;
+        live |= (in ? 1u : 0u) << (4 * h + e);
+      }
+    }
+#else
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
       const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
@@ -555,6 +617,13 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
       s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
       live |= (in ? 1u : 0u) << j;
     }
+#endif
+#if FG_CONJ_HIST == 2
+    if (!kSingle && cc == 0) {
+      const uint64_t H = hist_threshold(gh, K, h_lo, h_sh, sh.scratch);
+      if (tid == 0 && H > sh.thr) sh.thr = H;
+    }
+#endif
     if (tid == 0 && pend > sh.thr) sh.thr = pend;
     __syncthreads();
     const uint64_t thr = sh.thr;
@@ -784,6 +853,22 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   // write the kept keys that still clear the freshest threshold
   const uint32_t total = flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
   (void)total;
+#if FG_CONJ_HIST
+  // count the item's kept keys (distinct docs of its own lead chunks) into the
+  // query's bins, through LDS bins (sh.hist is free once the last select ran)
+  {
+    static_assert((1u << kConjHistBits) >= kQBins, "LDS bins");
+    const uint32_t n = min(sh.n_buf, kBuf);
+    for (uint32_t b = tid; b < kQBins; b += kThreads) sh.hist[b] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) {
+      const uint32_t b = qbin(sh.buf[i], h_lo, h_sh);
+      if (b < kQBins) atomicAdd(&sh.hist[b], 1u);
+    }
+    __syncthreads();
+    hist_add(sh.hist, gh);
+  }
+#endif
   FG_STAMP(w, 0, t_start);
   FG_STAMP(w, 1, t_probe);
   FG_STAMP(w, 2, t_keys);
@@ -893,20 +978,12 @@ struct QHist {
 #ifndef FG_DISJ_PREFETCH
 #define FG_DISJ_PREFETCH 0  // A/B: 1 = load the next pass's postings during this pass's gathers
 #endif
+#ifndef FG_DISJ_EBETA
+#define FG_DISJ_EBETA 0     // A/B: exhaustive tiles when all postings <= EBETA x the essential ones
+#endif
 #ifndef FG_DISJ_PRESENCE
 #define FG_DISJ_PRESENCE 0  // A/B (ab_disj_presence.log): 1 = presence bound before the score gathers, slower
 #endif
-
-// Add the LDS bins to the query's global histogram and clear them.
-__device__ inline void hist_add(uint32_t* lh, uint32_t* gh) {
-  for (uint32_t b = threadIdx.x; b < kQBins; b += kThreads) {
-    const uint32_t c = lh[b];
-    if (c) {
-      atomicAdd(&gh[b], c);
-      lh[b] = 0;
-    }
-  }
-}
 
 // Keep the threshold fresh: drop the keys appended since the last call whose
 // doc a MustNot clause holds (Exclude: the hit loops never probe them), count
@@ -1094,16 +1171,23 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       if (make_key(inflate_bound(s2 + fmax), d0) >= thr) break;
       s = s2;
     }
-    uint32_t ess = 0, any = 0, npost = 0;
-    for (uint32_t j = P; j < m; ++j) {
+    uint32_t ess = 0, any = 0, npost = 0, nall = 0;
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint32_t n = sh.r_hi[t * m + ord[j]] - sh.r_lo[t * m + ord[j]];
+      nall += n;
+      if (j < P) continue;
       ess |= 1u << ord[j];
-      any |= sh.r_hi[t * m + ord[j]] > sh.r_lo[t * m + ord[j]] ? 1u : 0u;
-      npost += sh.r_hi[t * m + ord[j]] - sh.r_lo[t * m + ord[j]];
+      any |= n ? 1u : 0u;
+      npost += n;
     }
     sh.t_ess[t] = ess;
     // every clause essential: the exhaustive LDS pass costs the whole tile
-    // (4096 docs), the posting-driven one its postings; take the cheaper
-    sh.t_mode[t] = (P == m || !any) ? 0u : (P == 0 && npost >= kExhaustiveMin ? 1u : 2u);
+    // (4096 docs), the posting-driven one its postings; take the cheaper.
+    // FG_DISJ_EBETA > 0 (A/B): also exhaustive when streaming every clause's
+    // postings costs at most EBETA x the essential ones (no per-posting gathers)
+    const bool exh = (P == 0 && npost >= kExhaustiveMin) ||
+                     (FG_DISJ_EBETA > 0 && nall >= kExhaustiveMin && nall <= FG_DISJ_EBETA * npost);
+    sh.t_mode[t] = (P == m || !any) ? 0u : (exh ? 1u : 2u);
   }
   __syncthreads();
   FG_PHASE(1);
@@ -1708,7 +1792,10 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
   (void)dq;
   FG_STAMP(dq, 0, FG_NOW());
   const uint32_t K = pl.k;
-  const uint64_t T0 = pl.thresh[q];
+  // the threshold word, or the query's histogram threshold when higher (>= K
+  // docs of the query -- or of its linked plans -- score at least that much)
+  const uint64_t T0 = max(pl.thresh[q], hist_threshold(pl.hist + (size_t)q * kQBins, K, pl.q_hlo[q], pl.q_hsh[q],
+                                                       sh.scratch));
   const uint32_t cnt = pl.cand_cnt[q];
   const uint64_t* src = pl.cand_keys + pl.cand_off[q];
   // every candidate of query q, f(key >= lb, key) with the whole workgroup
@@ -1846,6 +1933,13 @@ __global__ __launch_bounds__(kThreads) void k_merge_rank(uint32_t n_shards, uint
       if (out_shard) out_shard[(size_t)q * k + pos] = s;
     }
   }
+  // slots past the count: score 0, doc 0, shard 0 (defined, so a caller that
+  // gathers by shard over all k slots stays in bounds)
+  for (uint32_t e = min(total, k) + tid; e < k; e += kThreads) {
+    out_score[(size_t)q * k + e] = 0.0f;
+    out_doc[(size_t)q * k + e] = 0u;
+    if (out_shard) out_shard[(size_t)q * k + e] = 0u;
+  }
   if (tid == 0) out_n[q] = min(total, k);
 }
 
@@ -1881,6 +1975,11 @@ __global__ __launch_bounds__(kThreads) void k_merge(uint32_t n_shards, uint32_t 
     head[best]++;
   }
   out_n[q] = produced;
+  for (uint32_t e = produced; e < k; ++e) {  // slots past the count, as k_merge_rank
+    out_score[(size_t)q * k + e] = 0.0f;
+    out_doc[(size_t)q * k + e] = 0u;
+    if (out_shard) out_shard[(size_t)q * k + e] = 0u;
+  }
 }
 
 }  // namespace

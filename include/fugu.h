@@ -260,7 +260,8 @@ int fg_search_batch(fg_index* ix, const fg_query_batch* q, uint32_t k, float* ou
 /* Cross-shard merge: per-shard top-k lists gathered from
  * n_shards GPUs (RCCL all-gather) merged into the global top-k by (score
  * desc, shard asc, doc asc).  Device pointers, layout [n_shards][n_queries][k]
- * and [n_shards][n_queries]. */
+ * and [n_shards][n_queries].  Output slots past d_out_n[q] hold score 0, doc 0,
+ * shard 0. */
 int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* d_score, const uint32_t* d_doc,
                     const uint32_t* d_n, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_shard,
                     uint32_t* d_out_n, void* stream);

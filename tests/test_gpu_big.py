@@ -1,0 +1,125 @@
+"""One snapshot past 2^32 postings on the gfx950 path.
+
+Posting offsets are 64-bit end to end (fg_internal.h DevIndex::off, the
+kernels' list bases); this builds ONE index of 4.3M docs x 1024 distinct terms
+(4.40e9 postings, > 2^32) and queries terms whose lists start past posting
+2^32, so a 32-bit offset anywhere on the path would read another term's list.
+
+The corpus is built so the answer is known in closed form (no oracle index of
+4.4e9 postings): doc d holds the 1024 consecutive term ids starting at
+(d * 1031) mod 65536 (wrapping), once each, so every doc has length 1024,
+tf = 1 and one fieldnorm id; a term's df, each doc's membership and the BM25
+score of a term (tantivy's f32 order through the oracle's weight and tf-cache
+helpers) follow from numpy, and the top-k is the (score desc, doc asc) order
+of the matching docs.  Scores are bit-exact.
+
+Opt-in (FUGU_BIG=1): ~60 GB host memory, ~55 GB HBM, ~2 minutes on the box.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle.oracle as orc
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("FUGU_BIG") != "1",
+                                 reason="4.4e9-posting build (~2 min, ~60 GB host): set FUGU_BIG=1")]
+
+N, L, V, STRIDE = 4_300_000, 1024, 65536, 1031
+
+
+def corpus():
+    off = np.arange(N + 1, dtype=np.uint64) * L
+    tok = np.empty(N * L, np.uint32)
+    ar = np.arange(L, dtype=np.uint32)
+    for b in range(0, N, 1 << 16):
+        e = min(N, b + (1 << 16))
+        s = ((np.arange(b, e, dtype=np.uint64) * STRIDE) % V).astype(np.uint32)
+        tok[b * L:e * L] = ((s[:, None] + ar[None, :]) % V).ravel()
+    return off, tok
+
+
+def starts():
+    return ((np.arange(N, dtype=np.uint64) * STRIDE) % V).astype(np.int64)
+
+
+def member(st, t):
+    return ((t - st) % V) < L
+
+
+def term_score(st, t):
+    """Bm25Weight::score(fieldnorm_id(1024), 1) of term t (query/bm25.rs), f32."""
+    df = int(member(st, t).sum())
+    avgdl = np.float32(np.float32(N * L) / np.float32(N))  # total_num_tokens as f32 / N as f32
+    cache = orc.bm25_cache(float(avgdl))[orc.fieldnorm_to_id(L)]
+    w = np.float32(orc.term_weight(df, N))
+    return np.float32(w * (np.float32(1.0) / (np.float32(1.0) + np.float32(cache))))
+
+
+def expected(st, terms, occ, k):
+    """(score desc, doc asc) top-k of a 1-2 clause query over the closed-form corpus."""
+    must = [t for t, o in zip(terms, occ) if o == orc.MUST]
+    should = [t for t, o in zip(terms, occ) if o == orc.SHOULD]
+    mnot = [t for t, o in zip(terms, occ) if o == orc.MUST_NOT]
+    score = np.zeros(N, np.float32)
+    if must:
+        ok = np.ones(N, bool)
+        for t in must:
+            ok &= member(st, t)
+        # one or two Must children: s_a, or left + right (commutative in f32)
+        for t in must:
+            score = np.where(ok, score + term_score(st, t), score)
+    else:
+        ok = np.zeros(N, bool)
+        for t in should:  # 0.0 + s_a + s_b in clause order
+            m = member(st, t)
+            ok |= m
+            score = np.where(m, score + term_score(st, t), score)
+    for t in mnot:
+        ok &= ~member(st, t)
+    d = np.nonzero(ok)[0]
+    s = score[d]
+    o = np.lexsort((d, -s.astype(np.float64)))[:k]
+    return s[o], d[o].astype(np.uint32)
+
+
+def test_index_past_2_32_postings(monkeypatch):
+    from fugu_amd import native
+    monkeypatch.setenv("FUGU_RANK_GIB", "8")  # keep the rank words small: the point is the offsets
+    off, tok = corpus()
+    ctx = native.Context((0,))
+    ix = native.Index.from_docs(ctx, off, tok, V, threads=16, keep_host=False)
+    del tok
+    try:
+        stt = ix.stats()
+        assert stt.n_postings == N * L and stt.n_postings > 2**32
+        st = starts()
+        # term t's list starts near t * N * L / V: ids >= 63,900 start past posting 2^32
+        cases = [
+            ([65000, 65100], [orc.MUST, orc.MUST], 10),
+            ([65500, 300], [orc.MUST, orc.MUST], 25),      # a window that wraps the id space
+            ([65535], [orc.MUST], 5),
+            ([65000, 65300], [orc.SHOULD, orc.SHOULD], 20),
+            ([64000, 65535], [orc.SHOULD, orc.SHOULD], 100),
+            ([65000, 65010], [orc.MUST, orc.MUST_NOT], 30),
+            ([64500, 65400], [orc.MUST, orc.SHOULD], 40),
+        ]
+        for terms, occ, k in cases:
+            q_off = np.array([0, len(terms)], np.uint32)
+            s, d, n = ix.search_batch(q_off, np.array(terms, np.uint32), k, occur=np.array(occ, np.uint8))
+            if occ == [orc.MUST, orc.SHOULD]:
+                # (0.0 + s_a) + opt: the required doc set, scored with the optional term
+                ok = member(st, terms[0])
+                sa, sb = term_score(st, terms[0]), term_score(st, terms[1])
+                sc = np.where(member(st, terms[1]), np.float32(np.float32(0.0) + sa) + sb, sa).astype(np.float32)
+                dd = np.nonzero(ok)[0]
+                o = np.lexsort((dd, -sc[dd].astype(np.float64)))[:k]
+                es, ed = sc[dd][o], dd[o].astype(np.uint32)
+            else:
+                es, ed = expected(st, terms, occ, k)
+            assert int(n[0]) == len(ed), (terms, occ, int(n[0]), len(ed))
+            np.testing.assert_array_equal(d[0, :n[0]], ed, err_msg=str((terms, occ)))
+            np.testing.assert_array_equal(s[0, :n[0]], es, err_msg=str((terms, occ)))
+    finally:
+        ix.close()

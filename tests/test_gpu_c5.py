@@ -80,15 +80,26 @@ def test_c5_shards_use_global_statistics(native, c5):
     del synth
 
 
-def test_c5_or_top1000_100m_vs_oracle(native, c5):
+@pytest.fixture(scope="module")
+def c5_ref(c5):
+    """The 64-query OR top-1000 sample and ONE 100M-doc oracle index's answers."""
+    from fugu_amd import synth
+    from oracle import oracle as orc
+    c = c5[0]
+    q_off, terms = synth.queries(64, 2, 5)
+    ref = orc.OracleIndex(synth.VOCAB, c.off, c.tok, threads=16)
+    rs, rd, rn, _, _ = ref.search_batch(q_off, terms, K, mode=orc.OR, threads=16)
+    ref.close()
+    return q_off, terms, rs, rd, rn
+
+
+def test_c5_or_top1000_100m_vs_oracle(native, c5, c5_ref):
     import torch
 
-    from fugu_amd import synth
     from fugu_amd.shard import merge_on_device
-    from oracle import oracle as orc
     c, ranges, shards, g, _ = c5
-    nq = 64
-    q_off, terms = synth.queries(nq, 2, 5)
+    q_off, terms, rs, rd, rn = c5_ref
+    nq = len(q_off) - 1
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev).cuda_stream
     gs = torch.empty((SHARDS, nq * K), dtype=torch.float32, device=dev)
@@ -106,11 +117,41 @@ def test_c5_or_top1000_100m_vs_oracle(native, c5):
     gdoc = (md.cpu().numpy().view(np.uint32).reshape(nq, K).astype(np.uint64)
             + base[msh.cpu().numpy().reshape(nq, K)])
     mn = mn.cpu().numpy()
-    ref = orc.OracleIndex(synth.VOCAB, c.off, c.tok, threads=16)
-    rs, rd, rn, _, _ = ref.search_batch(q_off, terms, K, mode=orc.OR, threads=16)
     assert np.array_equal(mn, rn)
     for q in range(nq):
         m = int(rn[q])
         assert np.array_equal(gdoc[q, :m], rd[q, :m].astype(np.uint64)), q
         assert np.array_equal(ms[q, :m], rs[q, :m]), q
     assert (rn == K).mean() > 0.9
+
+
+def test_c5_as_one_index_past_2_32_postings(native, c5, c5_ref):
+    """The same 100M-doc namespace as ONE snapshot: 5.6e9 postings, past 2^32
+    (64-bit posting offsets end to end), against the same
+    100M oracle sample.  Runs last: it releases the 8 shards to make room."""
+    from fugu_amd import synth
+    c, ranges, shards, g, ctx = c5
+    q_off, terms, rs, rd, rn = c5_ref
+    for ix in shards:
+        ix.close()
+    shards.clear()
+    old = os.environ.get("FUGU_RANK_GIB")
+    os.environ["FUGU_RANK_GIB"] = "24"
+    try:
+        ix = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, keep_host=False)
+    finally:
+        if old is None:
+            os.environ.pop("FUGU_RANK_GIB")
+        else:
+            os.environ["FUGU_RANK_GIB"] = old
+    try:
+        st = ix.stats()
+        assert st.n_docs == N_DOCS and st.n_postings > 2**32, st.n_postings
+        s, d, n = ix.search_batch(q_off, terms, K, mode=native.MODE_OR)
+        assert np.array_equal(n, rn)
+        for q in range(len(rn)):
+            m = int(rn[q])
+            assert np.array_equal(d[q, :m], rd[q, :m]), q
+            assert np.array_equal(s[q, :m], rs[q, :m]), q
+    finally:
+        ix.close()
