@@ -73,10 +73,22 @@ constexpr uint32_t kConjHistBits = FG_HIST_BITS;   // ... k_conj's (its LDS sets
 #define FG_TILE_SHIFT 12
 #endif
 constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
+#ifndef FG_DISJ_SUB
+#define FG_DISJ_SUB 0  // A/B (ab_disj_sub_*.log): 1 = k_disj's bound 1 from 512-doc sub-tile maxima, slower
+#endif
+constexpr bool kDisjSubBounds = FG_DISJ_SUB;
+#ifndef FG_DISJ_EBETA
+#define FG_DISJ_EBETA 4  // k_disj: a tile is also exhaustive when all its postings <= EBETA x the essential
+                         // ones (ab_disj_ebeta_k1000.log: 0 / 2 / 4 / 8 -> 8.05 / 8.00 / 7.94 / 8.56 ms)
+#endif
+constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
+constexpr uint32_t kSubShift = 9;                    // ... of 512-doc sub-tiles (DevIndex::smax)
+constexpr uint32_t kSubPerTile = 1u << (FG_TILE_SHIFT - kSubShift);
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
 #endif
 constexpr uint32_t kDisjMaxGroup = FG_DISJ_MAXGROUP;  // ... at most this many tiles per work item
+constexpr uint32_t kDisjMaxPairs = 256;  // ... and at most this many (tile, Should clause) pairs (k_disj LDS)
 #ifndef FG_EXHMIN
 #define FG_EXHMIN 1024
 #endif
@@ -145,6 +157,8 @@ struct DevIndex {
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
   const uint32_t* toff;      // [V] first tmax entry of each term, or 0xFFFFFFFF (bucket >= tile: use bmax)
+  const float* smax;         // [tile entries * kSubPerTile] maxima of the same terms over 512-doc sub-tiles
+                             //     (k_disj's bound 1), entry toff[t] * kSubPerTile + (doc >> kSubShift)
   const float* cmax;         // [score chunks] largest posting score of each kChunk-posting chunk of a
                              //     list (block-max: k_conj skips a lead chunk that cannot reach the threshold)
   const uint32_t* coff;      // [V] index of each term's first chunk in cmax
@@ -261,6 +275,7 @@ struct ScoreJob {
   float* bmax;                // [D] out
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
+  uint32_t* smax;             // [tiles * kSubPerTile] out (f32 bits, zeroed first)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
   float* cmax;                // [score chunks] out: the largest score of each k_score chunk
   const uint32_t* ch_term;    // chunk tables

@@ -540,12 +540,18 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   d_tmaxs = static_cast<uint32_t*>(p);
   if ((rc = dev_alloc(4ull * ix->tile_entries, &p))) return rc;
   d_tmax = static_cast<uint32_t*>(p);
+  uint32_t* d_smax = nullptr;  // sub-tile maxima only for the FG_DISJ_SUB=1 A/B build
+  if (fg::kDisjSubBounds) {
+    if ((rc = dev_alloc(4ull * ix->tile_entries * fg::kSubPerTile, &p))) return rc;
+    d_smax = static_cast<uint32_t*>(p);
+  }
   if ((rc = dev_alloc(4ull * V * fg::kNumTopK, &p))) return rc;
   d_ktop = static_cast<float*>(p);
   if ((rc = dev_alloc(4ull * ix->n_sc, &p))) return rc;
   float* d_cmax = static_cast<float*>(p);
   HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, nullptr));
   HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), nullptr));
+  if (d_smax) HIPCHK(hipMemsetAsync(d_smax, 0, std::max<size_t>(4ull * ix->tile_entries * fg::kSubPerTile, 16), nullptr));
   HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, nullptr));
   fg::ScoreJob j{};
   j.doc = ix->d.doc;
@@ -565,6 +571,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.bmax = d_bmax;
   j.tmaxs = d_tmaxs;
   j.tmax = d_tmax;
+  j.smax = d_smax;
   j.ktop = d_ktop;
   j.cmax = d_cmax;
   j.ch_term = ix->d_sc_term;
@@ -635,6 +642,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
+  ix->d.smax = reinterpret_cast<const float*>(d_smax);
   ix->d.cmax = d_cmax;
   ix->d.alive = d_alive;
   ix->d.dense = d_dense;
@@ -1612,7 +1620,7 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
       set_bins(i, ub);
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
-      const uint32_t G = std::min<uint32_t>(fg::kDisjMaxGroup,
+      const uint32_t G = std::min<uint32_t>(std::min(fg::kDisjMaxGroup, fg::kDisjMaxPairs / ns),
                                             std::max<uint32_t>(1, (nt + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
       const uint32_t ng = (nt + G - 1) / G;
       ngroup[i] = ng;
@@ -2138,7 +2146,11 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       if (rcs[s]) return fail(rcs[s], "shard %u: %s", s, errs[s].c_str());
     return FG_OK;
   };
+  static const bool trace = getenv("FUGU_SHARD_TRACE") != nullptr;
+  auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t_0 = trace ? now() : 0.0;
   if (int rc = each(plan)) return rc;
+  const double t_plan = trace ? now() : 0.0;
   // 2. the shards of one device share per-query thresholds (fg_plan_link): the
   // merge keeps the k best across shards, so a shard need not keep a doc below
   // the k-th best score any shard has found.  The shared state is zeroed once,
@@ -2190,11 +2202,18 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     }
     return FG_OK;
   };
+  const double t_link = trace ? now() : 0.0;
   if (int rc = each(run)) return rc;
+  const double t_run = trace ? now() : 0.0;
   HIPCHK(hipSetDevice(dev0));
   for (hipEvent_t e : evs)
     if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
   HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
+  if (trace) {
+    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+    fprintf(stderr, "[fg_search_sharded] nq %u shards %u threaded %d: plan %.3f link %.3f launch %.3f kernels+merge %.3f ms\n",
+            nq, n_shards, (int)threaded, t_plan - t_0, t_link - t_plan, t_run - t_link, now() - t_run);
+  }
   // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
   const size_t span = 3 * o_k + 4ull * nq;
   if (span <= (4ull << 20)) {
@@ -2390,7 +2409,7 @@ int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, c
   const uint32_t* hd = ix->h_doc ? ix->h_doc->data() : nullptr;
   std::atomic<bool> bad{false};
   parallel_dynamic(nq, hw_threads(0), 1, [&](int, uint32_t qb, uint32_t qe) {
-    std::vector<float> tmx;
+    std::vector<float> tmx, smx;
     std::vector<uint32_t> tcnt;
     std::vector<uint64_t> pres;  // presence bitmaps, one per clause
     for (uint32_t i = qb; i < qe; ++i) {
@@ -2406,12 +2425,14 @@ int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, c
       }
       if (!m) continue;
       tmx.assign((size_t)nt * m, 0.0f);
+      smx.assign((size_t)nt * fg::kSubPerTile * m, 0.0f);
       tcnt.assign((size_t)nt * m, 0);
       pres.assign((size_t)m * ((N + 63) / 64), 0);
       for (uint32_t c = 0; c < m; ++c)
         for (uint64_t p = ix->off[t[c]]; p < ix->off[t[c] + 1]; ++p) {
           const uint32_t d = hd[p], ti = d >> TS;
           tmx[(size_t)ti * m + c] = std::max(tmx[(size_t)ti * m + c], psc[p]);
+          smx[(size_t)(d >> fg::kSubShift) * m + c] = std::max(smx[(size_t)(d >> fg::kSubShift) * m + c], psc[p]);
           tcnt[(size_t)ti * m + c]++;
           pres[(size_t)c * ((N + 63) / 64) + (d >> 6)] |= 1ull << (d & 63);
         }
@@ -2447,7 +2468,8 @@ int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, c
           for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
           continue;
         }
-        if (P == 0 && np >= fg::kExhaustiveMin) {  // every clause essential: exhaustive LDS tile
+        if ((P == 0 && np >= fg::kExhaustiveMin) ||
+            (fg::kDisjEBeta > 0 && np >= fg::kExhaustiveMin && np <= fg::kDisjEBeta * npe)) {  // exhaustive LDS tile
           stream += 8.0 * np;
           for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
           continue;
@@ -2461,7 +2483,22 @@ int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, c
           for (uint64_t p = p0; p < p1; ++p) {
             stream += 8.0;
             const uint32_t d = hd[p];
-            if (fg::make_key((psc[p] + (ubsum - ub[c])) * 1.00000762939453125f, d) < thk) continue;
+            // bound 1: the other clauses' 512-doc sub-tile maxima (k_disj keeps
+            // them as q / 255 of the tile bound, rounded up: modelled exactly)
+            float b1 = psc[p];
+            for (uint32_t c2 = 0; c2 < m; ++c2) {
+              if (c2 == c) continue;
+              const float tu = ub[c2], sx = smx[(size_t)(d >> fg::kSubShift) * m + c2];
+              float v = tu;
+              if (fg::kDisjSubBounds && tu > 0.0f && (ix->tmeta[t[c2]] & 0xFFu) <= fg::kDisjTileShift) {
+                uint32_t qq = std::min(255u, (uint32_t)std::ceil(sx * 255.0f / tu));
+                while (qq < 255u && tu * ((float)qq * (1.0f / 255.0f)) < sx) ++qq;
+                v = qq >= 255u ? tu : tu * ((float)qq * (1.0f / 255.0f));
+              }
+              b1 += v;
+            }
+            (void)ubsum;
+            if (fg::make_key(b1 * 1.00000762939453125f, d) < thk) continue;
             float pb = psc[p];
             bool all_dense = true;
             for (uint32_t c2 = 0; c2 < m; ++c2) {

@@ -914,20 +914,42 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
 // the exhaustive union.
 constexpr uint32_t kTileShift = kDisjTileShift;
 constexpr uint32_t kTile = 1u << kTileShift;   // docs per tile (LDS score array: 16 KB)
-constexpr uint32_t kRound = 1024;              // postings / docs per pass
+// k_disj shape knobs (A/B builds, ab_disj_occupancy.log): postings per pass,
+// the exhaustive LDS path, the select's digit width, waves per SIMD
+#ifndef FG_DISJ_ROUND
+#define FG_DISJ_ROUND 1024
+#endif
+#ifndef FG_DISJ_EXH
+#define FG_DISJ_EXH 1
+#endif
+#ifndef FG_DISJ_HBITS
+#define FG_DISJ_HBITS 11
+#endif
+constexpr uint32_t kRound = FG_DISJ_ROUND;     // postings / docs per pass
 constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
-constexpr uint32_t kPairs = 1024;              // (candidate, clause) rescoring pairs per pass
+constexpr uint32_t kPairs = kRound;            // (candidate, clause) rescoring pairs per pass
+constexpr uint32_t kDisjHistBits = FG_DISJ_HBITS;
 constexpr uint32_t kMaxTiles = kDisjMaxGroup;  // tiles per work item
-constexpr uint32_t kMaxSeg = kMaxTiles * kMaxTerms;
+constexpr uint32_t kMaxSeg = kDisjMaxPairs;    // (tile, clause) pairs per work item (the planner's cap)
 static_assert(kMaxSeg <= 2 * kThreads, "k_disj segment list: two (tile, clause) pairs per thread");
+static_assert(kMaxTiles <= 32 && kMaxTerms <= 16, "seg_info packs (tile << 4) | clause");
+
+// A sub-tile bound stored as q / 255 of its tile bound (q = 255: the tile
+// bound itself); the R phase picks the smallest q whose value is >= the
+// sub-tile maximum with this same f32 expression.
+__device__ inline float sub_bound(float tile_ub, uint32_t q) {
+  return q >= 255u ? tile_ub : tile_ub * ((float)q * (1.0f / 255.0f));
+}
 
 struct DisjShared {
   alignas(16) uint64_t buf[kBufD];
   union {
+#if FG_DISJ_EXH
     struct {
       float acc[kTile];              // E: exhaustive tile scores
       uint32_t hit[kTile / 32];      // E: docs matching any clause (a score may be 0)
     } e;
+#endif
     struct {
       uint64_t cand[kRound];         // P: (doc << 32) | (maybe-mask << 16) | (tile << 8) | clause
       float cand_s[kRound];          // P: the source clause's score of each candidate
@@ -935,11 +957,16 @@ struct DisjShared {
       uint32_t seg_start[kMaxSeg];   // P: prefix of the essential segments' lengths
     } p;
   } u;
-  uint32_t hist[kHistBins];
+  uint32_t hist[1u << kDisjHistBits];
   uint32_t scratch[8];
   // R: per (tile, clause) ranges and bounds, index t * m + i
   uint32_t r_lo[kMaxSeg], r_hi[kMaxSeg];
   float r_ub[kMaxSeg];
+#if FG_DISJ_SUB
+  // R: per (tile, clause) its 512-doc sub-tile maxima for bound 1, as q / 255
+  // of the tile bound (rounded up; 255 = the tile bound itself)
+  uint8_t r_sub[kMaxSeg * kSubPerTile];
+#endif
   uint32_t t_ess[kMaxTiles];         // essential-clause mask per tile
   uint32_t t_mode[kMaxTiles];        // 0 skip, 1 exhaustive, 2 posting-driven
   uint16_t seg_info[kMaxSeg];        // P: (tile << 4) | clause of each segment
@@ -977,9 +1004,6 @@ struct QHist {
 #endif
 #ifndef FG_DISJ_PREFETCH
 #define FG_DISJ_PREFETCH 0  // A/B: 1 = load the next pass's postings during this pass's gathers
-#endif
-#ifndef FG_DISJ_EBETA
-#define FG_DISJ_EBETA 0     // A/B: exhaustive tiles when all postings <= EBETA x the essential ones
 #endif
 #ifndef FG_DISJ_PRESENCE
 #define FG_DISJ_PRESENCE 0  // A/B (ab_disj_presence.log): 1 = presence bound before the score gathers, slower
@@ -1022,7 +1046,7 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
   }
   __syncthreads();
   uint64_t T = 0;
-  if (n > limit) T = truncate_keys<kBufD>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+  if (n > limit) T = truncate_keys<kBufD, kDisjHistBits>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
   uint64_t H = 0;
   if (publish && FG_HIST_EVERY_PUBLISH) {
     hist_add(sh.lh, hq.gh);
@@ -1142,6 +1166,35 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     sh.r_lo[p] = lo;
     sh.r_hi[p] = hi;
     sh.r_ub[p] = lo < hi ? ub : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
+#if FG_DISJ_SUB
+    // the sub-tile maxima (0 for a sub-tile without postings), quantized up
+    // against the tile bound; a term whose buckets are wider than a tile has one
+    // bound for the whole tile
+    {
+      uint32_t q8[kSubPerTile];
+      if (B <= kTileShift && sh.c_toff[i] != kInvalid && lo < hi && ub > 0.0f) {
+        const float4* sm = reinterpret_cast<const float4*>(ix.smax + ((size_t)sh.c_toff[i] + tile) * kSubPerTile);
+#pragma unroll
+        for (uint32_t v = 0; v < kSubPerTile / 4; ++v) {
+          const float4 x = sm[v];
+          const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (uint32_t u = 0; u < 4; ++u) {
+            uint32_t q = min(255u, (uint32_t)ceilf(xs[u] * 255.0f / ub));
+            while (q < 255u && sub_bound(ub, q) < xs[u]) ++q;
+            q8[4 * v + u] = q;
+          }
+        }
+      } else {
+#pragma unroll
+        for (uint32_t v = 0; v < kSubPerTile; ++v) q8[v] = 255u;
+      }
+      uint32_t* dst = reinterpret_cast<uint32_t*>(sh.r_sub + p * kSubPerTile);
+#pragma unroll
+      for (uint32_t v = 0; v < kSubPerTile / 4; ++v)
+        dst[v] = q8[4 * v] | (q8[4 * v + 1] << 8) | (q8[4 * v + 2] << 16) | (q8[4 * v + 3] << 24);
+    }
+#endif
   }
   {
     // the query's running threshold (every work item's counted hits so far)
@@ -1185,8 +1238,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     // (4096 docs), the posting-driven one its postings; take the cheaper.
     // FG_DISJ_EBETA > 0 (A/B): also exhaustive when streaming every clause's
     // postings costs at most EBETA x the essential ones (no per-posting gathers)
-    const bool exh = (P == 0 && npost >= kExhaustiveMin) ||
-                     (FG_DISJ_EBETA > 0 && nall >= kExhaustiveMin && nall <= FG_DISJ_EBETA * npost);
+    const bool exh = FG_DISJ_EXH && ((P == 0 && npost >= kExhaustiveMin) ||
+                                     (FG_DISJ_EBETA > 0 && nall >= kExhaustiveMin && nall <= FG_DISJ_EBETA * npost));
     sh.t_mode[t] = (P == m || !any) ? 0u : (exh ? 1u : 2u);
   }
   __syncthreads();
@@ -1201,6 +1254,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 #endif
 
   // ---- E: exhaustive tiles (every clause essential), clause-ordered LDS accumulation
+#if FG_DISJ_EXH
   for (uint32_t t = 0; t < ntile; ++t) {
     if (sh.t_mode[t] != 1u) continue;  // uniform
     const uint32_t d0 = (tile0 + t) << kTileShift;
@@ -1259,6 +1313,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
     }
     disj_truncate(ix, sh, K, K, gthr, true, hq, pend);
   }
+#endif
   FG_PHASE(2);
 
   // ---- P: posting-driven tiles: flat list of the essential clauses' segments,
@@ -1365,8 +1420,17 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       if (!pk[j]) continue;
       // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
       float ub = ps[j] + fmax;
+#if FG_DISJ_SUB
+      const uint32_t sb = (pd[j] >> kSubShift) & (kSubPerTile - 1);
+      for (uint32_t i = 0; i < m; ++i)
+        if (i != pcl[j]) {
+          const uint32_t pi = pt[j] * m + i;
+          ub += sub_bound(sh.r_ub[pi], sh.r_sub[pi * kSubPerTile + sb]);
+        }
+#else
       for (uint32_t i = 0; i < m; ++i)
         if (i != pcl[j]) ub += sh.r_ub[pt[j] * m + i];
+#endif
       pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
       if (pk[j] && fmask) pk[j] = filter_bits(fmask, fshift, pd[j]) != 0;
       ess[j] = sh.t_ess[pt[j]];
@@ -2125,12 +2189,29 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
   const uint32_t n = (uint32_t)(j.off[t + 1] - b);
   const uint32_t end = min(n, first + kScoreChunk);
   const float wt = j.w_text[t], wn = j.w_name[t];
+  const uint32_t to = j.toff[t];
   float mx = 0.0f;
-  for (uint32_t p = first + threadIdx.x; p < end; p += kThreads) {
-    const uint32_t d = j.doc[b + p];
-    const float v = posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache);
-    j.psc[b + p] = v;
+  for (uint32_t p0 = first; p0 < end; p0 += kThreads) {
+    const uint32_t p = p0 + threadIdx.x;
+    const bool in = p < end;
+    const uint32_t d = in ? j.doc[b + p] : 0xFFFFFFFFu;
+    const float v = in ? posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache) : 0.0f;
+    if (in) j.psc[b + p] = v;
     mx = fmaxf(mx, v);
+    if (j.smax && to != 0xFFFFFFFFu) {
+      // 512-doc sub-tile maxima: the wave's postings are consecutive (docs
+      // ascending), so a segmented max over equal sub-tiles leaves one atomic
+      // per sub-tile per wave
+      const uint32_t lane = threadIdx.x & 63u, sub = in ? d >> kSubShift : 0xFFFFFFFFu;
+      uint32_t vb = __float_as_uint(v);
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t vo = (uint32_t)__shfl_down((int)vb, o, 64), so = (uint32_t)__shfl_down((int)sub, o, 64);
+        if (lane + o < 64 && so == sub) vb = max(vb, vo);
+      }
+      const uint32_t prev = (uint32_t)__shfl_up((int)sub, 1, 64);
+      if (in && (lane == 0 || prev != sub)) atomicMax(&j.smax[(size_t)to * kSubPerTile + sub], vb);
+    }
   }
   // the chunk's block-max (scores >= 0)
   __shared__ float wmax[kThreads / 64];
