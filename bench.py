@@ -393,6 +393,23 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     return ent
 
 
+def pmc_traffic(path, kname, workload):
+    """(HBM bytes per launch of `kname`, source) from a committed rocprofv3 PMC summary when
+    its lib_id is this build's and its workload matches, else None."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from lib_id import lib_id
+    wl = pmc.get("workload", {})
+    if pmc.get("lib_id") != lib_id() or any(wl.get(k) != v for k, v in workload.items()):
+        log(f"[bench] {path} does not match this build/workload: no measured traffic for {kname}")
+        return None
+    v = pmc.get(f"{kname}_hbm_bytes_per_launch")
+    return (v, pmc.get("source")) if v else None
+
+
 def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist):
     """BASELINE configs[3] (c4) / configs[4] (c5) across the job's GPUs (strong
     scaling: the corpus is fixed, its 8 units are split over the ranks):
@@ -781,6 +798,14 @@ def main():
                                                 "score (12 B per tile-clause bound, 8 B per essential posting, rank "
                                                 "word / bucket max per posting past the tile bound, 4 B score per "
                                                 "present clause past the presence bound, 8 B per kept key)"}
+                # measured DRAM bytes per k_disj launch (rocprofv3 PMC of `bench.py --disj --k 1000`,
+                # profiles/latest_or.json) when it was taken on this build and workload
+                tr = pmc_traffic(os.path.join(ROOT, "profiles", "latest_or.json"), "k_disj",
+                                 {"n_docs": args.docs, "batch": nq, "k": kk, "terms": "2-5 OR"})
+                if tr:
+                    ent["roofline"].update({"traffic": tr[0], "traffic_source": tr[1],
+                                            "traffic_over_alg": round(tr[0] / float(bo[:, 3].sum()), 3),
+                                            "hbm_gbs_measured": round(tr[0] / (kms_ * 1e-3) / 1e9, 1)})
             if ref is not None:
                 done, wall, mism = 0, 0.0, 0
                 budget = args.cpu_seconds / 2

@@ -82,6 +82,27 @@ constexpr bool kDisjSubBounds = FG_DISJ_SUB;
                          // ones (ab_disj_ebeta_k1000.log: 0 / 2 / 4 / 8 -> 8.05 / 8.00 / 7.94 / 8.56 ms)
 #endif
 constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
+// k_disj shape (A/B builds, profiles/r03/ab/ab_disj_occ*.log): postings per
+// pass, the exhaustive LDS path, the select's digit width, waves per SIMD
+// (3 waves / 1024 / exhaustive tiles / 11 bits -> 5 / 512 / none / 10: OR top-1000
+// 7.97 -> 7.02 ms, top-20 5.28 -> 4.59 ms, identical outputs: more waves in
+// flight beat more postings per wave and the exhaustive path's LDS)
+#ifndef FG_DISJ_ROUND
+#define FG_DISJ_ROUND 512
+#endif
+#ifndef FG_DISJ_EXH
+#define FG_DISJ_EXH 0
+#endif
+#ifndef FG_DISJ_HBITS
+#define FG_DISJ_HBITS 10
+#endif
+#ifndef FG_DISJ_WAVES
+#define FG_DISJ_WAVES 5
+#endif
+#ifndef FG_DISJ_G
+#define FG_DISJ_G 1  // ab_disj_g_k*.log, ab_disj_gpq_k*.log: 4 / 2 / 1 -> OR top-1000 7.00 / 6.51 / 6.13 ms, top-20 4.60 / 4.27 / 3.94 ms
+#endif
+constexpr bool kDisjExhaustive = FG_DISJ_EXH;
 constexpr uint32_t kSubShift = 9;                    // ... of 512-doc sub-tiles (DevIndex::smax)
 constexpr uint32_t kSubPerTile = 1u << (FG_TILE_SHIFT - kSubShift);
 #ifndef FG_DISJ_MAXGROUP
@@ -93,8 +114,16 @@ constexpr uint32_t kDisjMaxPairs = 256;  // ... and at most this many (tile, Sho
 #define FG_EXHMIN 1024
 #endif
 constexpr uint32_t kExhaustiveMin = FG_EXHMIN;  // k_disj: all-essential tiles with fewer postings go posting-driven
-constexpr uint32_t kNumTopK = 4;          // per-term K-th best scores kept for these K
+#ifndef FG_KTOP20
+#define FG_KTOP20 1  // A/B: 0 = no K = 20 (the /search default limit) among the stored per-term K-th scores
+#endif
+#if FG_KTOP20
+constexpr uint32_t kNumTopK = 5;          // per-term K-th best scores kept for these K
+constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 20, 100, 1000};
+#else
+constexpr uint32_t kNumTopK = 4;
 constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 100, 1000};
+#endif
 
 constexpr uint32_t kMaxFacetClauses = 8;  // facet clauses per query (FG_MAX_FACET_CLAUSES)
 constexpr uint32_t kFmaskChunk = 8192;    // facet postings per k_fmask workgroup

@@ -14,6 +14,9 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -1432,7 +1435,8 @@ int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_nam
 }
 
 // ---------------------------------------------------------------- planning
-static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync);
+static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync,
+                       hipStream_t up = hipStreamPerThread);
 
 int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out) {
   return plan_create(ix, q, k, out, true);
@@ -1441,7 +1445,8 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
 // sync = false (fg_search_batch): the upload stays in flight on the calling
 // thread's per-thread stream, where the plan's execute is queued behind it;
 // the pinned staging is returned when the plan is destroyed
-static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync) {
+static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync,
+                       hipStream_t up) {
   if (!ix || !q || !out || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
   if (q->n_queries && q->q_off[q->n_queries] > q->q_off[0] && !q->terms) return fail(FG_EINVAL, "q_off without terms");
   if (q->f_off && q->n_queries && q->f_off[q->n_queries] > q->f_off[0] && !q->f_terms)
@@ -1812,12 +1817,13 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   p->d.f.ch_start = (const uint32_t*)put(ch_s.data(), 4ull * nch, s_ch);
   p->d.q_hlo = (const uint32_t*)put(q_hlo.data(), 4ull * nq, s_hb);
   p->d.q_hsh = (const uint32_t*)put(q_hsh.data(), 4ull * nq, s_hb);
-  // on the planning thread's own stream: a plan built while another thread's
-  // batch runs does not serialise against it through the legacy null stream
-  HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, hipStreamPerThread));
+  // on the planning thread's own stream (or the caller's `up`): a plan built
+  // while another thread's batch runs does not serialise against it through the
+  // legacy null stream
+  HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, up));
   p->zeroed = s_up > s_in;
   if (sync || !pin.p) {
-    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+    HIPCHK(hipStreamSynchronize(up));
   } else {
     p->pin = pin.p;  // the plan returns it (after a sync) when destroyed
     p->pin_n = pin.n;
@@ -2030,6 +2036,56 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
   return FG_OK;
 }
 
+// Persistent worker threads of fg_search_sharded's batch mode: a thread's
+// first HIP call sets up per-thread runtime state, so threads made per call
+// cost more than the planning they run.  Jobs never wait on other jobs, so a
+// fixed pool serves any number of concurrent callers.  Never destroyed (idle
+// workers end with the process).
+class ShardWorkers {
+ public:
+  static ShardWorkers& get() {
+    static ShardWorkers* w = new ShardWorkers(std::max(8, std::min(64, hw_threads(0))));
+    return *w;
+  }
+  // f(0..n-1) on the workers; returns when all have run
+  void run(uint32_t n, const std::function<void(uint32_t)>& f) {
+    struct Batch { std::mutex m; std::condition_variable c; uint32_t left; } b;
+    b.left = n;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      for (uint32_t i = 0; i < n; ++i)
+        q_.push_back([&b, &f, i] {
+          f(i);
+          std::lock_guard<std::mutex> lb(b.m);
+          if (--b.left == 0) b.c.notify_all();
+        });
+    }
+    cv_.notify_all();
+    std::unique_lock<std::mutex> lb(b.m);
+    b.c.wait(lb, [&] { return b.left == 0; });
+  }
+
+ private:
+  explicit ShardWorkers(int n) {
+    for (int i = 0; i < n; ++i)
+      std::thread([this] {
+        for (;;) {
+          std::function<void()> job;
+          {
+            std::unique_lock<std::mutex> l(mu_);
+            cv_.wait(l, [&] { return !q_.empty(); });
+            job = std::move(q_.front());
+            q_.pop_front();
+          }
+          job();
+        }
+      }).detach();
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+
 // Side streams of fg_search_sharded, per device, created once and shared by
 // every caller (a stream takes work from any thread; each call orders its own
 // work with events)
@@ -2124,20 +2180,19 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     fg_plan* p = nullptr;
     // inline (one query): the upload is queued on this thread's stream, ahead of
     // the execute on the same stream -- no host round trip per shard
-    int rc = plan_create(shards[s], q, k, &p, threaded);
+    // a batch: planned on its shard's thread, uploaded on the shard's side
+    // stream (a fresh thread's per-thread stream would be created per call)
+    int rc = threaded ? plan_create(shards[s], q, k, &p, true, sst[s]) : plan_create(shards[s], q, k, &p, false);
     if (rc) return rc;
     plans[s].reset(p);
     return FG_OK;
   };
   auto each = [&](auto&& f) {
     if (threaded) {
-      std::vector<std::thread> th;
-      for (uint32_t s = 0; s < n_shards; ++s)
-        th.emplace_back([&, s] {
-          rcs[s] = f(s);
-          if (rcs[s]) errs[s] = fg_last_error();
-        });
-      for (auto& x : th) x.join();
+      ShardWorkers::get().run(n_shards, [&](uint32_t s) {
+        rcs[s] = f(s);
+        if (rcs[s]) errs[s] = fg_last_error();
+      });
     } else {
       for (uint32_t s = 0; s < n_shards; ++s)
         if ((rcs[s] = f(s))) errs[s] = fg_last_error();
@@ -2468,8 +2523,9 @@ int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, c
           for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
           continue;
         }
-        if ((P == 0 && np >= fg::kExhaustiveMin) ||
-            (fg::kDisjEBeta > 0 && np >= fg::kExhaustiveMin && np <= fg::kDisjEBeta * npe)) {  // exhaustive LDS tile
+        if (fg::kDisjExhaustive && ((P == 0 && np >= fg::kExhaustiveMin) ||
+                                    (fg::kDisjEBeta > 0 && np >= fg::kExhaustiveMin && np <= fg::kDisjEBeta * npe))) {
+          // exhaustive LDS tile
           stream += 8.0 * np;
           for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
           continue;

@@ -914,17 +914,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
 // the exhaustive union.
 constexpr uint32_t kTileShift = kDisjTileShift;
 constexpr uint32_t kTile = 1u << kTileShift;   // docs per tile (LDS score array: 16 KB)
-// k_disj shape knobs (A/B builds, ab_disj_occupancy.log): postings per pass,
-// the exhaustive LDS path, the select's digit width, waves per SIMD
-#ifndef FG_DISJ_ROUND
-#define FG_DISJ_ROUND 1024
-#endif
-#ifndef FG_DISJ_EXH
-#define FG_DISJ_EXH 1
-#endif
-#ifndef FG_DISJ_HBITS
-#define FG_DISJ_HBITS 11
-#endif
+// k_disj shape knobs: fg_internal.h (FG_DISJ_ROUND / EXH / HBITS / WAVES)
 constexpr uint32_t kRound = FG_DISJ_ROUND;     // postings / docs per pass
 constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
 constexpr uint32_t kPairs = kRound;            // (candidate, clause) rescoring pairs per pass
@@ -1064,9 +1054,6 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
   __syncthreads();
 }
 
-#ifndef FG_DISJ_WAVES
-#define FG_DISJ_WAVES 3
-#endif
 
 __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, DevPlan pl) {
   __shared__ DisjShared sh;
@@ -1470,7 +1457,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
       maybe[j] = 0;
       exact[j] = true;
     }
-    constexpr uint32_t G = 4;
+    constexpr uint32_t G = FG_DISJ_G;  // clauses per bound-2 group (their loads in flight together)
     constexpr uint32_t kAbsent = 0xBF800000u;  // -1.0f: the clause is not on the doc
     for (uint32_t i0 = 0; i0 < m; i0 += G) {
       // y[g][j]: a rank clause's posting position (< 2^31) or kAbsent; an f32

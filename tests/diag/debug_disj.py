@@ -1,10 +1,11 @@
-"""Debug helper: k_disj vs the oracle on the 1M Zipf corpus (FUGU_LIB selects the build)."""
+"""Debug helper (test infrastructure: the oracle is the checker): k_disj vs the oracle on the 1M Zipf
+corpus (FUGU_LIB selects the build).  python tests/diag/debug_disj.py"""
 import os
 import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from fugu_amd import native, synth  # noqa: E402
 from oracle import oracle as orc  # noqa: E402
 

@@ -1,6 +1,6 @@
 """Snapshot build cost on the box: per-phase host/device time of
 fg_index_build_from_docs (FUGU_BUILD_TRACE) for a corpus, plus the corpus
-generation, shard statistics and oracle build times the C4/C5 tests pay.
+generation and shard statistics times the C4/C5 tests pay.
 
   FUGU_BUILD_TRACE=1 python tools/build_timing.py [--docs N] [--s S]
 """
@@ -17,7 +17,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=10_000_000)
     ap.add_argument("--s", type=float, default=1.0)
-    ap.add_argument("--oracle", action="store_true")
     args = ap.parse_args()
     from fugu_amd import native, synth
     ctx = native.Context((0,))
@@ -33,11 +32,6 @@ def main():
     print(f"index {time.time() - t:.2f}s: {s.n_postings} postings, {s.n_rank_terms} rank terms, "
           f"{s.device_bytes / 2**30:.1f} GiB", flush=True)
     del st
-    if args.oracle:
-        from oracle import oracle as orc
-        t = time.time()
-        orc.OracleIndex(synth.VOCAB, c.off, c.tok, threads=16)
-        print(f"oracle {time.time() - t:.2f}s", flush=True)
 
 
 if __name__ == "__main__":
