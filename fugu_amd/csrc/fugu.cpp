@@ -408,7 +408,7 @@ struct fg_plan {
     for (hipEvent_t e : pending) (void)hipEventDestroy(e);
     if (pin) {  // an upload nothing waited for yet (created without sync, never executed)
       (void)hipSetDevice(ix->dev);
-      (void)hipStreamSynchronize(hipStreamPerThread);
+      (void)hipStreamSynchronize(up_stream);
     }
     if (ws) {
       // the workspace may still be read by this plan's last launch (a per-thread
@@ -427,6 +427,7 @@ struct fg_plan {
   bool zeroed = false;        // the zero region arrived zeroed with the upload: the first execute skips its memset
   void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
   size_t pin_n = 0;
+  hipStream_t up_stream = hipStreamPerThread;  // the stream the plan was uploaded on
 };
 
 namespace {
@@ -1821,6 +1822,7 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   // while another thread's batch runs does not serialise against it through the
   // legacy null stream
   HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, up));
+  p->up_stream = up;
   p->zeroed = s_up > s_in;
   if (sync || !pin.p) {
     HIPCHK(hipStreamSynchronize(up));
@@ -2170,7 +2172,9 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       sh[0]->pool.put(p, n);
     }
   } back{shards, n_shards, base, got, sst, evs};
-  if (threaded)
+  // every shard of a multi-shard call runs on a side stream of its device, so a
+  // single query's shards overlap on the GPU too
+  if (n_shards > 1)
     for (uint32_t s = 0, nth = 0; s < n_shards; ++s, nth = 0) {
       for (uint32_t t = 0; t < s; ++t) nth += shards[t]->dev == shards[s]->dev ? 1u : 0u;
       if (!(sst[s] = side_stream(shards[s]->dev, nth % kSideStreams))) return fail(FG_EHIP, "side stream creation failed");
@@ -2182,7 +2186,8 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     // the execute on the same stream -- no host round trip per shard
     // a batch: planned on its shard's thread, uploaded on the shard's side
     // stream (a fresh thread's per-thread stream would be created per call)
-    int rc = threaded ? plan_create(shards[s], q, k, &p, true, sst[s]) : plan_create(shards[s], q, k, &p, false);
+    int rc = threaded ? plan_create(shards[s], q, k, &p, true, sst[s])
+                      : plan_create(shards[s], q, k, &p, false, sst[s] ? sst[s] : hipStreamPerThread);
     if (rc) return rc;
     plans[s].reset(p);
     return FG_OK;
@@ -2251,7 +2256,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc, d, 4 * nk, st));
       HIPCHK(hipMemcpyPeerAsync(gn + (size_t)s * nq, dev0, p->own_n, d, 4ull * nq, st));
     }
-    if (threaded || !local) {
+    if (sst[s] || !local) {
       HIPCHK(hipEventCreateWithFlags(&evs[s], hipEventDisableTiming));
       HIPCHK(hipEventRecord(evs[s], st));
     }
