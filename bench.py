@@ -266,12 +266,14 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
             p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
         merge_on_device(gs, gd, gn, nq, K, st)
 
-    def step():
+    def step_fan():
         fanout(plans, gs, gd, gn, streams, torch, dev)
         merge_on_device(gs, gd, gn, nq, K, st)
 
-    # per-namespace kernel times from back-to-back launches; the step itself
-    # runs the 8 namespaces on 8 streams
+    # per-namespace kernel times from back-to-back launches; then the 8
+    # namespaces on 8 streams; then the step: ONE multi-snapshot plan over the 8
+    # namespaces (one launch per kernel, shared score-only thresholds), the plan
+    # fg_search_sharded runs for a device's namespaces
     for p in plans:
         p.profile(True)
     el_seq = timed_steps(step_seq, steps, warmup, torch)
@@ -279,7 +281,16 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
     per_ns = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
     for p in plans:
         p.profile(False)
+    el_fan = timed_steps(step_fan, steps, warmup, torch)
+    mp = native.Plan(ixs, q_off, terms, K)
+
+    def step():
+        mp.execute(st, gs.data_ptr(), gd.data_ptr(), gn.data_ptr())
+        merge_on_device(gs, gd, gn, nq, K, st)
+
+    mp.profile(True)
     el = timed_steps(step, steps, warmup, torch)
+    mk, mkn = mp.kernel_ms()
     mms = merge_ms(gs, gd, gn, nq, K, torch)
     # the same fan-out through the ABI call a host makes: fg_search_sharded
     # (host batch in, merged host hits out: 8 plans, 8 executes, merge, D2H)
@@ -297,17 +308,20 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
         m = int(mn[i])
         same = same and np.array_equal(s2[i, :m], ms_[i, :m]) and np.array_equal(
             d2[i, :m], md[i, :m].view(np.uint32)) and np.array_equal(sh2[i, :m], msh[i, :m].astype(np.uint32))
-    del plans
+    del plans, mp
     for ix in ixs:
         ix.close()
     return {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
             "batch": nq, "k": K, "terms": 3, "mode": "AND", "namespaces": 8, "docs_per_namespace": ranges[0][1],
+            "step": "one multi-snapshot plan over the 8 namespaces (fg_plan_create_multi) + k_merge_rank",
+            "multi_plan_kernels_ms": [round(mk[0] / max(mkn, 1), 4), round(mk[1] / max(mkn, 1), 4)],
             "k_conj_ms_per_namespace": per_ns, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
-            "streams": 8, "ms_per_step_one_stream": round(el_seq * 1e3 / steps, 4),
+            "ms_per_step_8_plans_8_streams": round(el_fan * 1e3 / steps, 4),
+            "ms_per_step_8_plans_one_stream": round(el_seq * 1e3 / steps, 4),
             "fg_search_sharded": {"value": round(nq / sharded_ms * 1e3, 1), "ms_per_batch": round(sharded_ms, 4),
                                   "same_hits_as_step": same,
-                                  "note": "one synchronous ABI call per batch: host planning of 8 namespaces, "
-                                          "executes on side streams, device merge, D2H"},
+                                  "note": "one synchronous ABI call per batch: host planning of 8 namespaces "
+                                          "(in parallel), one multi-snapshot plan, device merge, D2H"},
             "workload": "C4: 10M docs as 8 namespaces x 1.25M (own statistics each), fan-out 3-term AND top-100 "
                         "on all 8 + device merge, all 8 namespaces on this one GPU",
             "projected_8gpu": "each GPU runs one namespace: step ~ max(k_conj_ms_per_namespace) + k_final + gather"}
@@ -335,32 +349,46 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     log(f"[bench] C5: 100M docs as 8 shards built in {build_s:.1f}s")
     q_off, terms = synth.queries(nq, 2, 5)
     plans = [ix.plan(q_off, terms, K, native.MODE_OR) for ix in ixs]
+    native.link_plans(plans)
     gs = torch.empty((8, nq * K), dtype=torch.float32, device=dev)
     gd = torch.empty((8, nq * K), dtype=torch.int32, device=dev)
     gn = torch.empty((8, nq), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     merged = {}
 
-    # back to back on one stream: a shard's k_disj fills the GPU by itself
-    # (8 streams measured 110.5 -> 112.6 ms per step)
-    def step():
+    # the round-2/3 step: 8 linked plans back to back on one stream (per-shard times)
+    def step_linked():
         for r, p in enumerate(plans):
             p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
-        merged["out"] = merge_on_device(gs, gd, gn, nq, K, st)
+        merge_on_device(gs, gd, gn, nq, K, st)
 
     for p in plans:
         p.profile(True)
-    el = timed_steps(step, steps, warmup, torch)
+    el_linked = timed_steps(step_linked, max(2, steps // 2), 1, torch)
     kms = [p.kernel_ms() for p in plans]
     per_shard = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
+    del plans
+    # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel)
+    mp = native.Plan(ixs, q_off, terms, K, native.MODE_OR)
+
+    def step():
+        mp.execute(st, gs.data_ptr(), gd.data_ptr(), gn.data_ptr())
+        merged["out"] = merge_on_device(gs, gd, gn, nq, K, st)
+
+    mp.profile(True)
+    el = timed_steps(step, steps, warmup, torch)
+    mk, mkn = mp.kernel_ms()
     mms = merge_ms(gs, gd, gn, nq, K, torch)
     ent = {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
            "batch": nq, "k": K, "terms": "2-5", "mode": "OR", "n_docs": N, "zipf_s": S, "shards": 8,
-           "k_disj_ms_per_shard": per_shard, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
+           "step": "one multi-snapshot plan over the 8 shards (fg_plan_create_multi) + k_merge_rank",
+           "multi_plan_kernels_ms": [round(mk[0] / max(mkn, 1), 4), round(mk[1] / max(mkn, 1), 4)],
+           "ms_per_step_8_linked_plans": round(el_linked * 1e3 / max(2, steps // 2), 4),
+           "k_disj_ms_per_shard_linked": per_shard, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
            "workload": "C5: 100M docs s=1.1 as 8 doc shards with global BM25 statistics, 2-5-term OR top-1000 on "
                        "all 8 + device merge, all 8 shards on this one GPU",
            "projected_8gpu": "each GPU runs one shard: step ~ max(k_disj_ms_per_shard) + k_final + gather"}
-    del plans
+    del mp
     for ix in ixs:
         ix.close()
     if do_cpu:
@@ -458,12 +486,17 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     build_s = time.time() - t0
     log(f"[bench] {cfg}: rank {rank} built units {mine} in {build_s:.1f}s")
     q_off, terms = synth.queries(nq, 3, 3) if c4 else synth.queries(nq, 2, 5)
-    plans = [ix.plan(q_off, terms, K, mode) for ix in ixs]
-    if len(plans) > 1:
-        native.link_plans(plans)
-    gs = torch.empty((len(plans), nq * K), dtype=torch.float32, device=dev)
-    gd = torch.empty((len(plans), nq * K), dtype=torch.int32, device=dev)
-    gn = torch.empty((len(plans), nq), dtype=torch.int32, device=dev)
+    # a rank's units: ONE multi-snapshot plan (one launch per kernel, shared
+    # score-only thresholds); FUGU_BENCH_LINKED=1: one linked plan per unit (A/B)
+    if len(ixs) > 1 and os.environ.get("FUGU_BENCH_LINKED") != "1":
+        plans = [native.Plan(ixs, q_off, terms, K, mode)]
+    else:
+        plans = [ix.plan(q_off, terms, K, mode) for ix in ixs]
+        if len(plans) > 1:
+            native.link_plans(plans)
+    gs = torch.empty((len(ixs), nq * K), dtype=torch.float32, device=dev)
+    gd = torch.empty((len(ixs), nq * K), dtype=torch.int32, device=dev)
+    gn = torch.empty((len(ixs), nq), dtype=torch.int32, device=dev)
     # unit u's doc d as a global id: c5 the corpus doc id, c4 (namespace << 24) | doc
     off_u = torch.tensor([ranges[u][0] if not c4 else (u << 24) for u in mine], dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream(dev)
@@ -529,6 +562,8 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
                            (" + RCCL all-gather top-k" if backend == "nccl" else f" + {backend} all-gather (rehearsal)")
                            if world > 1 else "")},
             "kernels_ms_per_step_max_rank": {kname: round(kern, 4), "k_final": round(fin, 4)},
+            "rank_plan": ("one multi-snapshot plan over the rank's units" if len(plans) == 1 and len(ixs) > 1
+                          else f"{len(plans)} linked plan(s)"),
             "result_sha1": h.hexdigest()[:16],
             "hits": int(mn.sum()),
             "snapshot_build_s_rank0": round(build_s, 1),

@@ -218,6 +218,7 @@ struct DevFilters {
   const uint32_t* ch_clause;    // [n_chunks] clause index in the filter
   const uint32_t* ch_term;      // [n_chunks] facet term
   const uint32_t* ch_start;     // [n_chunks] first posting of the chunk within the term's list
+  const uint32_t* f_seg;        // [n_filters] the snapshot of each filter (multi-snapshot plans), or nullptr
   uint32_t* fmask;              // workspace, zeroed per run
 };
 
@@ -257,8 +258,21 @@ struct DevPlan {
   uint32_t n_single;            // k_conj: the first n_single work items belong to single-list queries
   uint32_t n_scan;              // k_scan work items (queries with no text terms), after the total_chunks
                                 // k_conj / k_disj items in work_q / work_c / work_n
+  // Multi-snapshot plans (several segments / doc shards / namespaces of one
+  // device in ONE launch per kernel): query slot v = s * seg_nq + q is query q
+  // of the batch on snapshot segs[s]; every per-query array above is indexed by
+  // the slot, except thresh and hist, which are the batch query's own (shared
+  // score-only by the slots of q: pub_mask).  seg_nq = 0: one snapshot (the
+  // kernel's DevIndex argument).
+  const DevIndex* segs;         // [n_segs] or nullptr
+  uint32_t seg_nq;              // queries of the batch (slots per snapshot), 0 = one snapshot
   DevFilters f;
 };
+
+// The batch query of a query slot (thresh / hist index)
+__host__ __device__ inline uint32_t slot_query(const DevPlan& pl, uint32_t v) {
+  return pl.seg_nq ? v % pl.seg_nq : v;
+}
 
 constexpr uint32_t kDiagPerWg = 16;  // u64 stamps per workgroup in diagnostic builds
 

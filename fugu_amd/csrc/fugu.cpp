@@ -386,7 +386,9 @@ struct fg_index {
 
 struct fg_plan {
   fg_index* ix = nullptr;
-  uint32_t nq = 0, k = 0, total_chunks = 0, n_scan = 0;
+  // nq: query slots = n_segs x nq_batch (one snapshot: the batch's queries)
+  uint32_t nq = 0, k = 0, total_chunks = 0, n_scan = 0, nq_batch = 0, n_segs = 1;
+  std::vector<fg_index*> segs;  // a multi-snapshot plan's snapshots after ix (retained)
   int mode = FG_MODE_AND;
   fg::DevPlan d{};
   void* ws = nullptr;  // workspace from ix->pool
@@ -421,6 +423,7 @@ struct fg_plan {
       ix->pool.put(ws, ws_got);
     }
     if (ix) fg_index_release(ix);
+    for (fg_index* x : segs) fg_index_release(x);
   }
   bool last_stream_used = false;
   std::vector<uint32_t> h_lo, h_hi;  // per query: f32 bits spanned by its score histogram (fg_plan_link)
@@ -1438,9 +1441,15 @@ int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_nam
 // ---------------------------------------------------------------- planning
 static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync,
                        hipStream_t up = hipStreamPerThread);
+static int plan_create_multi(fg_index* const* ixs, uint32_t n_segs, const fg_query_batch* q, uint32_t k,
+                             fg_plan** out, bool sync, hipStream_t up);
 
 int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out) {
   return plan_create(ix, q, k, out, true);
+}
+
+int fg_plan_create_multi(fg_index* const* ixs, uint32_t n_segs, const fg_query_batch* q, uint32_t k, fg_plan** out) {
+  return plan_create_multi(ixs, n_segs, q, k, out, true, hipStreamPerThread);
 }
 
 // sync = false (fg_search_batch): the upload stays in flight on the calling
@@ -1448,7 +1457,33 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
 // the pinned staging is returned when the plan is destroyed
 static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out, bool sync,
                        hipStream_t up) {
-  if (!ix || !q || !out || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
+  return plan_create_multi(&ix, 1, q, k, out, sync, up);
+}
+
+namespace {
+
+struct WItem { double key; uint32_t q, c, n; };
+
+// One snapshot's side of a planned batch, built on the host alone (no HIP
+// call): per-query tables, facet filters (ids local to the snapshot) and the
+// unsorted work items.  plan_create_multi joins one per snapshot.
+struct HostPlan {
+  std::vector<uint32_t> q_m, q_terms, lead, nchunk, q_filter;
+  std::vector<uint64_t> thr0;
+  std::vector<float> q_ub;
+  uint32_t nf = 0;
+  std::vector<uint32_t> f_shift;
+  std::vector<uint64_t> f_woff;
+  std::vector<float> f_tab, f_max;
+  std::vector<uint32_t> ch_f, ch_c, ch_t, ch_s;
+  std::vector<WItem> citems, ditems, scan;
+  std::vector<uint32_t> ngroup, q_hlo, q_hhi, q_hsh;
+};
+
+// n_segs: the snapshots the plan spans; a query's work items are spread over
+// all of them, so each snapshot gets its share of the per-query item counts
+int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t n_segs, HostPlan& h) {
+  if (!ix || !q || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
   if (q->n_queries && q->q_off[q->n_queries] > q->q_off[0] && !q->terms) return fail(FG_EINVAL, "q_off without terms");
   if (q->f_off && q->n_queries && q->f_off[q->n_queries] > q->f_off[0] && !q->f_terms)
     return fail(FG_EINVAL, "f_off without f_terms");
@@ -1458,12 +1493,19 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   const uint32_t nq = q->n_queries;
   const uint64_t N = ix->n_docs;
   const bool disj = q->mode == FG_MODE_OR;
-  std::vector<uint32_t> q_m(nq), q_terms((size_t)nq * fg::kMaxTerms, 0), lead(nq), nchunk(nq);
-  std::vector<uint64_t> thr0(nq, 0);
-  std::vector<float> q_ub((size_t)nq * fg::kMaxTerms, 0.0f);
+  auto &q_m = h.q_m, &q_terms = h.q_terms, &lead = h.lead, &nchunk = h.nchunk;
+  auto& thr0 = h.thr0;
+  auto& q_ub = h.q_ub;
+  q_m.assign(nq, 0);
+  q_terms.assign((size_t)nq * fg::kMaxTerms, 0);
+  lead.assign(nq, 0);
+  nchunk.assign(nq, 0);
+  thr0.assign(nq, 0);
+  q_ub.assign((size_t)nq * fg::kMaxTerms, 0.0f);
 
   // ---- facet filters: one mask per distinct clause list (fg_internal.h DevFilters)
-  std::vector<uint32_t> q_filter(nq, 0xFFFFFFFFu);
+  auto& q_filter = h.q_filter;
+  q_filter.assign(nq, 0xFFFFFFFFu);
   std::vector<std::vector<uint32_t>> flist;
   std::vector<uint8_t> q_nomatch(nq, 0);  // the filter matches no doc: no work items
   if (q->f_off) {
@@ -1486,11 +1528,16 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
       q_filter[i] = it->second;
     }
   }
-  const uint32_t nf = (uint32_t)flist.size();
-  std::vector<uint32_t> f_shift(nf);
-  std::vector<uint64_t> f_woff(nf + 1, 0);
-  std::vector<float> f_tab((size_t)nf * 256, 0.0f), f_max(nf, 0.0f);
-  std::vector<uint32_t> ch_f, ch_c, ch_t, ch_s;
+  const uint32_t nf = h.nf = (uint32_t)flist.size();
+  auto& f_shift = h.f_shift;
+  auto& f_woff = h.f_woff;
+  auto& f_tab = h.f_tab;
+  auto& f_max = h.f_max;
+  auto &ch_f = h.ch_f, &ch_c = h.ch_c, &ch_t = h.ch_t, &ch_s = h.ch_s;
+  f_shift.assign(nf, 0);
+  f_woff.assign(nf + 1, 0);
+  f_tab.assign((size_t)nf * 256, 0.0f);
+  f_max.assign(nf, 0.0f);
   std::vector<uint32_t> f_lo(nf, 0xFFFFFFFFu), f_hi(nf, 0);  // doc span of the filter's postings
   for (uint32_t f = 0; f < nf; ++f) {
     const std::vector<uint32_t>& c = flist[f];
@@ -1522,8 +1569,6 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
       }
     }
   }
-  if (f_woff[nf] * 4 > (8ull << 30)) return fail(FG_EUNSUPPORTED, "facet masks of this batch exceed 8 GiB");
-  if (ch_f.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "facet postings of this batch too large");
 
   // work items: each query's chunks (Must-driven: k_conj) or doc tiles (Should
   // only: k_disj) in ~kGroupsPerQuery groups, ordered as a doc sweep across the
@@ -1532,9 +1577,14 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   // AllQuery) scan doc tiles (k_scan).  Per-term occurs (q->occur) make a
   // query Must-driven when it has a Must clause (RequiredOptionalScorer over
   // its Shoulds), a union of its Shoulds otherwise; MustNot clauses exclude.
-  struct W { double key; uint32_t q, c, n; };
-  std::vector<W> citems, ditems, scan;
-  std::vector<uint32_t> ngroup(nq, 0), q_hlo(nq, 0x3F800000u), q_hhi(nq, 0x3F800000u), q_hsh(nq, 31);
+  using W = WItem;
+  const uint32_t gpq = std::max<uint32_t>(1, fg::kGroupsPerQuery / n_segs);  // k_disj / k_scan groups per query
+  auto &citems = h.citems, &ditems = h.ditems, &scan = h.scan;
+  auto &ngroup = h.ngroup, &q_hlo = h.q_hlo, &q_hhi = h.q_hhi, &q_hsh = h.q_hsh;
+  ngroup.assign(nq, 0);
+  q_hlo.assign(nq, 0x3F800000u);
+  q_hhi.assign(nq, 0x3F800000u);
+  q_hsh.assign(nq, 31);
   auto present = [&](uint32_t t) { return t < ix->n_terms && ix->off[t + 1] > ix->off[t]; };
   // histogram bins of query i: bin 0 at the starting threshold (or ub / 256), the
   // top bin at the query's largest possible score ub; ~kQBins bins between
@@ -1564,7 +1614,7 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
       const uint32_t tlo = (uint32_t)(dlo >> fg::kDisjTileShift), thi = (uint32_t)(dhi >> fg::kDisjTileShift);
       const uint32_t nt = thi - tlo + 1;
       const uint32_t G = std::min<uint32_t>(fg::kScanMaxGroup,
-                                            std::max<uint32_t>(1, (nt + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
+                                            std::max<uint32_t>(1, (nt + gpq - 1) / gpq));
       const uint32_t ng = (nt + G - 1) / G;
       ngroup[i] = ng;
       // the groups of all queries in doc order: the first groups publish the
@@ -1627,7 +1677,7 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
       const uint32_t G = std::min<uint32_t>(std::min(fg::kDisjMaxGroup, fg::kDisjMaxPairs / ns),
-                                            std::max<uint32_t>(1, (nt + fg::kGroupsPerQuery - 1) / fg::kGroupsPerQuery));
+                                            std::max<uint32_t>(1, (nt + gpq - 1) / gpq));
       const uint32_t ng = (nt + G - 1) / G;
       ngroup[i] = ng;
       for (uint32_t g = 0; g < ng; ++g) {
@@ -1686,13 +1736,119 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
     // batch of one: the p50 latency) spreads a query over up to 64 items so its
     // chunks run side by side instead of up to kMaxGroup in a row, while its
     // k_final still reads at most 64 x k candidates
-    const uint32_t per_q = std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u)));
+    const uint32_t per_q = std::max<uint32_t>(
+        1, std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u))) / n_segs);
     const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + per_q - 1) / per_q));
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;
     for (uint32_t g = 0; g < ng; ++g)
       citems.push_back(W{(g + 0.5) / ng, i, g * G, std::min(G, nch - g * G)});
   }
+  return FG_OK;
+}
+
+}  // namespace
+
+// Plans of one batch on one or several snapshots of one device (a multi-
+// snapshot plan: DevPlan::segs, query slot v = s * nq + q): every snapshot is
+// planned on the host (in parallel for a large batch), then the slots are
+// joined into ONE set of work items, uploaded once and run by one launch per
+// kernel.  Several snapshots share each batch query's threshold and histogram
+// (score-only), and their bins span the union of the snapshots' score ranges.
+static void run_parallel(uint32_t n, const std::function<void(uint32_t)>& f);  // ShardWorkers, below
+
+static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_batch* q, uint32_t k,
+                             fg_plan** out, bool sync, hipStream_t up) {
+  if (!ixs || !q || !out || S == 0 || S > FG_MAX_SEGMENTS) return fail(FG_EINVAL, "bad arguments");
+  for (uint32_t s = 0; s < S; ++s) {
+    if (!ixs[s]) return fail(FG_EINVAL, "NULL snapshot");
+    if (ixs[s]->dev != ixs[0]->dev) return fail(FG_EINVAL, "the snapshots of one plan live on different devices");
+  }
+  fg_index* ix = ixs[0];
+  std::vector<HostPlan> hs(S);
+  if (S > 1 && q->n_queries >= 64) {
+    std::vector<int> rcs(S, FG_OK);
+    std::vector<std::string> errs(S);
+    run_parallel(S, [&](uint32_t s) {
+      if ((rcs[s] = plan_host(ixs[s], q, k, S, hs[s]))) errs[s] = fg_last_error();
+    });
+    for (uint32_t s = 0; s < S; ++s)
+      if (rcs[s]) return fail(rcs[s], "snapshot %u: %s", s, errs[s].c_str());
+  } else {
+    for (uint32_t s = 0; s < S; ++s)
+      if (int rc = plan_host(ixs[s], q, k, S, hs[s])) {
+        if (S == 1) return rc;
+        const std::string e = fg_last_error();
+        return fail(rc, "snapshot %u: %s", s, e.c_str());
+      }
+  }
+  const uint32_t nq1 = q->n_queries;  // batch queries
+  if ((uint64_t)S * nq1 > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%u x %u query slots)", S, nq1);
+  const uint32_t nq = S * nq1;  // query slots
+  // ---- join the snapshots' tables (one snapshot: its own, moved)
+  std::vector<uint32_t> q_m, q_terms, lead, q_filter, ngroup, q_hlo, q_hhi, q_hsh, f_shift, f_seg, ch_f, ch_c, ch_t, ch_s;
+  std::vector<uint64_t> thr0, f_woff;
+  std::vector<float> q_ub, f_tab, f_max;
+  std::vector<WItem> citems, ditems, scan;
+  uint32_t nf = 0;
+  if (S == 1) {
+    HostPlan& h = hs[0];
+    q_m.swap(h.q_m); q_terms.swap(h.q_terms); lead.swap(h.lead); q_filter.swap(h.q_filter); ngroup.swap(h.ngroup);
+    q_hlo.swap(h.q_hlo); q_hhi.swap(h.q_hhi); q_hsh.swap(h.q_hsh); thr0.swap(h.thr0); q_ub.swap(h.q_ub);
+    f_shift.swap(h.f_shift); f_woff.swap(h.f_woff); f_tab.swap(h.f_tab); f_max.swap(h.f_max);
+    ch_f.swap(h.ch_f); ch_c.swap(h.ch_c); ch_t.swap(h.ch_t); ch_s.swap(h.ch_s);
+    citems.swap(h.citems); ditems.swap(h.ditems); scan.swap(h.scan);
+    nf = h.nf;
+  } else {
+    auto cat = [](auto& dst, const auto& src) { dst.insert(dst.end(), src.begin(), src.end()); };
+    f_woff.push_back(0);
+    for (uint32_t s = 0; s < S; ++s) {
+      HostPlan& h = hs[s];
+      const uint32_t fb = nf, vb = s * nq1;
+      cat(q_m, h.q_m); cat(q_terms, h.q_terms); cat(lead, h.lead); cat(ngroup, h.ngroup); cat(thr0, h.thr0);
+      cat(q_ub, h.q_ub);
+      for (uint32_t f : h.q_filter) q_filter.push_back(f == 0xFFFFFFFFu ? f : fb + f);
+      cat(f_shift, h.f_shift); cat(f_tab, h.f_tab); cat(f_max, h.f_max);
+      const uint64_t wb = f_woff.back();
+      for (uint32_t f = 0; f < h.nf; ++f) {
+        f_woff.push_back(wb + h.f_woff[f + 1]);
+        f_seg.push_back(s);
+      }
+      for (uint32_t f : h.ch_f) ch_f.push_back(fb + f);
+      cat(ch_c, h.ch_c); cat(ch_t, h.ch_t); cat(ch_s, h.ch_s);
+      for (WItem x : h.citems) { x.q += vb; citems.push_back(x); }
+      for (WItem x : h.ditems) { x.q += vb; ditems.push_back(x); }
+      for (WItem x : h.scan) { x.q += vb; scan.push_back(x); }
+      nf += h.nf;
+    }
+    // one bin geometry per batch query over the snapshots where it has work
+    // items (fg_plan_link's rule): a bin counts the same scores in every slot
+    q_hlo.assign(nq, 0x3F800000u);
+    q_hhi.assign(nq, 0x3F800000u);
+    q_hsh.assign(nq, 31);
+    for (uint32_t i = 0; i < nq1; ++i) {
+      uint32_t l = 0, hh = 0;
+      bool any = false;
+      for (uint32_t s = 0; s < S; ++s) {
+        if (!hs[s].ngroup[i]) continue;
+        l = std::max(l, hs[s].q_hlo[i]);
+        hh = std::max(hh, hs[s].q_hhi[i]);
+        any = true;
+      }
+      if (!any) continue;
+      hh = std::max(hh, l);
+      for (uint32_t s = 0; s < S; ++s) {
+        q_hlo[s * nq1 + i] = l;
+        q_hhi[s * nq1 + i] = hh;
+        q_hsh[s * nq1 + i] = bin_shift(l, hh);
+      }
+    }
+  }
+  if (f_woff[nf] * 4 > (8ull << 30)) return fail(FG_EUNSUPPORTED, "facet masks of this batch exceed 8 GiB");
+  if (ch_f.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "facet postings of this batch too large");
+  if (citems.size() + ditems.size() + scan.size() > 0x7FFFFFFFull)
+    return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", citems.size() + ditems.size() + scan.size());
+  using W = WItem;
   // k_conj: single-list queries' items first (their own k_conj launch), each part
   // in sweep order; k_disj: sweep order.  A stable LSD radix sort on (not single,
   // key quantized to 31 bits): the order is a scheduling choice only (every
@@ -1744,6 +1900,8 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
 
   auto p = std::make_unique<fg_plan>();
   p->nq = nq;
+  p->nq_batch = nq1;
+  p->n_segs = S;
   p->k = k;
   p->mode = q->mode;
   p->total_chunks = (uint32_t)chunks;
@@ -1757,12 +1915,14 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
                s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq), s_ub = al(4ull * nq * fg::kMaxTerms),
                s_qf = al(4ull * nq), s_fs = al(4ull * nf),
                s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch),
-               s_hb = al(4ull * nq);
+               s_hb = al(4ull * nq), s_fg = S > 1 ? al(4ull * nf) : 0,
+               s_sg = S > 1 ? al(sizeof(fg::DevIndex) * S) : 0;
   const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft +
-                      s_fm + 4 * s_ch + 2 * s_hb;
+                      s_fm + 4 * s_ch + 2 * s_hb + s_fg + s_sg;
   // one score histogram per query (DevPlan::hist: k_conj's and k_disj's running thresholds)
-  const size_t s_thr = al(8ull * nq), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]),
-               s_hist = al(4ull * nq * fg::kQBins);
+  // (thresholds and histograms: one per batch query, shared by its slots)
+  const size_t s_thr = al(8ull * nq1), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]),
+               s_hist = al(4ull * nq1 * fg::kQBins);
   const size_t s_ck = al(8ull * cand_off[nq]);
   const size_t s_os = al(4ull * nq * k), s_od = al(4ull * nq * k), s_on = al(4ull * nq);
 #ifdef FG_DIAG
@@ -1777,6 +1937,10 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   p->ws = base;
   p->ix = ix;  // owns the workspace from here on (returned to ix->pool); retained below
   fg_index_retain(ix);
+  for (uint32_t s = 1; s < S; ++s) {
+    fg_index_retain(ixs[s]);
+    p->segs.push_back(ixs[s]);
+  }
   p->ws_bytes = total;
   // a small zero region (thresholds, candidate counts, facet masks) travels
   // zeroed with the upload, so the first execute needs no memset
@@ -1818,6 +1982,12 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   p->d.f.ch_start = (const uint32_t*)put(ch_s.data(), 4ull * nch, s_ch);
   p->d.q_hlo = (const uint32_t*)put(q_hlo.data(), 4ull * nq, s_hb);
   p->d.q_hsh = (const uint32_t*)put(q_hsh.data(), 4ull * nq, s_hb);
+  if (S > 1) {
+    std::vector<fg::DevIndex> segs(S);
+    for (uint32_t s = 0; s < S; ++s) segs[s] = ixs[s]->d;
+    p->d.f.f_seg = (const uint32_t*)put(f_seg.data(), 4ull * nf, s_fg);
+    p->d.segs = (const fg::DevIndex*)put(segs.data(), sizeof(fg::DevIndex) * S, s_sg);
+  }
   // on the planning thread's own stream (or the caller's `up`): a plan built
   // while another thread's batch runs does not serialise against it through the
   // legacy null stream
@@ -1858,7 +2028,11 @@ static int plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_pla
   p->d.n_scan = (uint32_t)n_scan;
   p->d.n_single = (uint32_t)n_single;
   p->d.k = k;
-  p->d.pub_mask = ~0ull;
+  p->d.seg_nq = S > 1 ? nq1 : 0;
+  // several snapshots: a batch query's slots share its threshold score-only, so a
+  // doc of another snapshot tied with the k-th score is never pruned (the merge
+  // breaks such ties by snapshot)
+  p->d.pub_mask = S > 1 ? 0xFFFFFFFF00000000ull : ~0ull;
   p->h_lo.swap(q_hlo);
   p->h_hi.swap(q_hhi);
   p->d.f.n_filters = nf;
@@ -1988,6 +2162,7 @@ int fg_plan_link(fg_plan* const* plans, uint32_t n) {
     if (!plans[i]) return fail(FG_EINVAL, "NULL plan");
     if (plans[i]->nq != o->nq || plans[i]->k != o->k) return fail(FG_EINVAL, "linked plans differ in batch or k");
     if (plans[i]->ix->dev != o->ix->dev) return fail(FG_EINVAL, "linked plans live on different devices");
+    if (plans[i]->n_segs > 1) return fail(FG_EUNSUPPORTED, "a multi-snapshot plan already shares its thresholds");
   }
   const uint32_t nq = o->nq;
   std::vector<uint32_t> lo(nq, 0), sh(nq, 0);
@@ -2088,6 +2263,8 @@ class ShardWorkers {
   std::deque<std::function<void()>> q_;
 };
 
+static void run_parallel(uint32_t n, const std::function<void(uint32_t)>& f) { ShardWorkers::get().run(n, f); }
+
 // Side streams of fg_search_sharded, per device, created once and shared by
 // every caller (a stream takes work from any thread; each call orders its own
 // work with events)
@@ -2117,8 +2294,8 @@ static hipStream_t side_stream(int dev, uint32_t i) {
 //     planned while earlier ones run and a device's shards overlap each other;
 //   otherwise (a single query: the host mirror's segment fan-out) everything
 //     runs inline on the calling thread's per-thread streams.
-int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
-                      float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
+static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q,
+                                    uint32_t k, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
   if (!shards || n_shards == 0 || n_shards > 64 || !q || k == 0 || !out_score || !out_doc || !out_n)
     return fail(FG_EINVAL, "bad arguments");
   for (uint32_t s = 0; s < n_shards; ++s) {
@@ -2273,6 +2450,158 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     HIPCHK(hipStreamSynchronize(hipStreamPerThread));
     fprintf(stderr, "[fg_search_sharded] nq %u shards %u threaded %d: plan %.3f link %.3f launch %.3f kernels+merge %.3f ms\n",
             nq, n_shards, (int)threaded, t_plan - t_0, t_link - t_plan, t_run - t_link, now() - t_run);
+  }
+  // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
+  const size_t span = 3 * o_k + 4ull * nq;
+  if (span <= (4ull << 20)) {
+    PinnedLease pin(shards[0]->pinned, span);
+    if (pin.p) {
+      HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
+      HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+      const char* h = static_cast<const char*>(pin.p);
+      std::memcpy(out_score, h, 4 * nk);
+      std::memcpy(out_doc, h + o_k, 4 * nk);
+      if (out_shard) std::memcpy(out_shard, h + 2 * o_k, 4 * nk);
+      std::memcpy(out_n, h + 3 * o_k, 4ull * nq);
+      return FG_OK;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
+  if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(out_n, mn, 4ull * nq, hipMemcpyDeviceToHost, hipStreamPerThread));
+  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+  return FG_OK;
+}
+
+// One batch over several shards / segments / namespaces of one logical index
+// (SURVEY.md §8b fg_search_sharded, §8e).  The shards of each device run as ONE
+// multi-snapshot plan (fg_plan_create_multi: one upload, one launch per kernel,
+// one shared score-only threshold per query); every shard's top-k lists land in
+// gathered buffers on the first shard's device -- directly, or over xGMI
+// (hipMemcpyPeerAsync) from another device -- and k_merge_rank merges them
+// there into (score desc, shard asc, doc asc): tantivy's merge_fruits over
+// DocAddress (segment_ord, doc).  Everything runs on the calling thread's
+// per-thread streams.  FUGU_SHARDED_PER_SHARD=1 selects the round-2 path (one
+// plan per shard, linked; A/B builds).
+int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
+                      float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
+  static const bool per_shard = getenv("FUGU_SHARDED_PER_SHARD") != nullptr;
+  if (per_shard) return search_sharded_per_shard(ctx, shards, n_shards, q, k, out_score, out_doc, out_shard, out_n);
+  if (!shards || n_shards == 0 || n_shards > FG_MAX_SEGMENTS || !q || k == 0 || !out_score || !out_doc || !out_n)
+    return fail(FG_EINVAL, "bad arguments");
+  for (uint32_t s = 0; s < n_shards; ++s) {
+    if (!shards[s]) return fail(FG_EINVAL, "NULL shard");
+    if (ctx && std::find(ctx->devs.begin(), ctx->devs.end(), shards[s]->dev) == ctx->devs.end())
+      return fail(FG_EINVAL, "a shard lives on a device outside the context");
+  }
+  const uint32_t nq = q->n_queries;
+  if (nq == 0) return FG_OK;
+  if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k > FG_MAX_K");
+  // ---- gathered lists + merged output on the first shard's device (its pool)
+  const int dev0 = shards[0]->dev;
+  const size_t nk = (size_t)nq * k;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t g_s = al(4 * nk * n_shards), g_n = al(4ull * nq * n_shards), o_k = al(4 * nk), o_n = al(4ull * nq);
+  const size_t total = 2 * g_s + g_n + 3 * o_k + o_n;
+  size_t got = 0;
+  HIPCHK(hipSetDevice(dev0));
+  char* base = static_cast<char*>(shards[0]->pool.get(total, &got));
+  if (!base) return fail(FG_EOOM, "hipMalloc of the shard merge buffers failed");
+  float* gs = reinterpret_cast<float*>(base);
+  uint32_t* gd = reinterpret_cast<uint32_t*>(base + g_s);
+  uint32_t* gn = reinterpret_cast<uint32_t*>(base + 2 * g_s);
+  float* ms = reinterpret_cast<float*>(base + 2 * g_s + g_n);
+  uint32_t* md = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + o_k);
+  uint32_t* msh = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 2 * o_k);
+  uint32_t* mn = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 3 * o_k);
+  // the shards of each device, in shard order
+  std::vector<int> gdev;
+  std::vector<std::vector<uint32_t>> groups;
+  for (uint32_t s = 0; s < n_shards; ++s) {
+    const auto it = std::find(gdev.begin(), gdev.end(), shards[s]->dev);
+    if (it == gdev.end()) {
+      gdev.push_back(shards[s]->dev);
+      groups.push_back({s});
+    } else {
+      groups[it - gdev.begin()].push_back(s);
+    }
+  }
+  const size_t ng = groups.size();
+  std::vector<std::unique_ptr<fg_plan>> plans(ng);
+  std::vector<hipEvent_t> evs(ng, nullptr);
+  // teardown (also on error returns): every device's stream drained, then the
+  // events, the plans and the buffers
+  struct Back {
+    const std::vector<int>& dv; int d0; fg_index* ix0; void* p; size_t n; std::vector<hipEvent_t>& ev;
+    ~Back() {
+      for (size_t g = 0; g < dv.size(); ++g) {
+        (void)hipSetDevice(dv[g]);
+        (void)hipStreamSynchronize(hipStreamPerThread);
+        if (ev[g]) (void)hipEventDestroy(ev[g]);
+      }
+      (void)hipSetDevice(d0);
+      (void)hipStreamSynchronize(hipStreamPerThread);
+      ix0->pool.put(p, n);
+    }
+  } back{gdev, dev0, shards[0], base, got, evs};
+  static const bool trace = getenv("FUGU_SHARD_TRACE") != nullptr;
+  auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t_0 = trace ? now() : 0.0;
+  double t_plan = 0.0;
+  for (size_t g = 0; g < ng; ++g) {
+    const std::vector<uint32_t>& gi = groups[g];
+    const uint32_t S = (uint32_t)gi.size();
+    std::vector<fg_index*> ixs(S);
+    for (uint32_t j = 0; j < S; ++j) ixs[j] = shards[gi[j]];
+    fg_plan* p = nullptr;
+    // the upload is queued on this thread's stream of the device, ahead of the
+    // execute on the same stream: no host round trip
+    const double t_p = trace ? now() : 0.0;
+    if (int rc = plan_create_multi(ixs.data(), S, q, k, &p, false, hipStreamPerThread)) {
+      if (n_shards == 1) return rc;
+      const std::string e = fg_last_error();
+      return fail(rc, "device %d: %s", gdev[g], e.c_str());
+    }
+    plans[g].reset(p);
+    if (trace) t_plan += now() - t_p;
+    // lists straight into the gathered buffers when the group's shards are
+    // consecutive and on dev0 ([S][nq][k] is the gathered layout)
+    const bool direct = gdev[g] == dev0 && gi.back() - gi.front() + 1 == S;
+    const size_t s0 = gi.front();
+    if (int rc = direct ? fg_plan_execute(p, hipStreamPerThread, gs + s0 * nk, gd + s0 * nk, gn + s0 * nq)
+                        : fg_plan_execute(p, hipStreamPerThread, nullptr, nullptr, nullptr))
+      return rc;
+    if (!direct) {
+      for (uint32_t j = 0; j < S; ++j) {
+        const size_t s = gi[j];
+        if (gdev[g] == dev0) {
+          HIPCHK(hipMemcpyAsync(gs + s * nk, p->own_score + j * nk, 4 * nk, hipMemcpyDeviceToDevice, hipStreamPerThread));
+          HIPCHK(hipMemcpyAsync(gd + s * nk, p->own_doc + j * nk, 4 * nk, hipMemcpyDeviceToDevice, hipStreamPerThread));
+          HIPCHK(hipMemcpyAsync(gn + s * nq, p->own_n + (size_t)j * nq, 4ull * nq, hipMemcpyDeviceToDevice,
+                                hipStreamPerThread));
+        } else {
+          HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score + j * nk, gdev[g], 4 * nk, hipStreamPerThread));
+          HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc + j * nk, gdev[g], 4 * nk, hipStreamPerThread));
+          HIPCHK(hipMemcpyPeerAsync(gn + s * nq, dev0, p->own_n + (size_t)j * nq, gdev[g], 4ull * nq,
+                                    hipStreamPerThread));
+        }
+      }
+    }
+    if (gdev[g] != dev0) {
+      HIPCHK(hipEventCreateWithFlags(&evs[g], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(evs[g], hipStreamPerThread));
+    }
+  }
+  const double t_run = trace ? now() : 0.0;
+  HIPCHK(hipSetDevice(dev0));
+  for (hipEvent_t e : evs)
+    if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
+  HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
+  if (trace) {
+    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+    fprintf(stderr, "[fg_search_sharded] nq %u shards %u devices %zu: plan %.3f launch %.3f kernels+merge %.3f ms\n",
+            nq, n_shards, ng, t_plan, t_run - t_0 - t_plan, now() - t_run);
   }
   // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
   const size_t span = 3 * o_k + 4ull * nq;

@@ -48,6 +48,18 @@ constexpr uint32_t kInvalid = 0xFFFFFFFFu;
 #endif
 
 __device__ inline uint32_t lane_id() { return threadIdx.x & 63; }
+
+// A multi-snapshot plan's DevIndex of slot v (DevPlan::segs), read through the
+// constant address space: the plan's tables never change during a launch, so
+// the compiler may keep the fields in SGPRs or reload them like kernel arguments
+typedef const __attribute__((address_space(4))) DevIndex ConstDevIndex;
+__device__ inline DevIndex seg_index(const DevPlan& pl, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ((ConstDevIndex*)pl.segs)[s];
+#else
+  return pl.segs[s];  // the host pass only parses device code
+#endif
+}
 __device__ inline uint32_t wave_id() { return threadIdx.x >> 6; }
 
 // Upper bounds are compared after inflating by 2^-17 relative: a bound sums at
@@ -494,8 +506,9 @@ struct alignas(4) U4a { uint32_t x, y, z, w; };  // a 16-B load at 4-B alignment
 #ifndef FG_CONJ_HIST
 #define FG_CONJ_HIST 3
 #endif
-template <bool kSingle>
-__global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPlan pl) {
+// kMulti: a multi-snapshot plan (DevPlan::segs): the item's snapshot from its query slot
+template <bool kSingle, bool kMulti>
+__global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPlan pl) {
   __shared__ ConjShared sh;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
 
@@ -509,6 +522,8 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   uint64_t t_start = FG_NOW(), t_probe = 0, t_keys = 0, t_sel = 0, n_app = 0;
   (void)t_start; (void)t_probe; (void)t_keys; (void)t_sel; (void)n_app;
   const uint32_t q = pl.work_q[w];
+  const DevIndex ix = kMulti ? seg_index(pl, q / pl.seg_nq) : ix0;
+  const uint32_t ql = kMulti ? q % pl.seg_nq : q;  // the batch query (threshold, histogram)
   const uint32_t c0 = pl.work_c[w], nc = pl.work_n[w];
   // terms: [Must (cost order)][MustNot][Should]; a query with Should clauses is
   // Must-driven (RequiredOptionalScorer): the Shoulds only add score
@@ -521,7 +536,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   const uint32_t t0 = terms[0];
   const uint64_t lead_base = ix.off[t0];
   const uint32_t lead_df = pl.q_lead_df[q];
-  unsigned long long* gthr = reinterpret_cast<unsigned long long*>(&pl.thresh[q]);
+  unsigned long long* gthr = reinterpret_cast<unsigned long long*>(&pl.thresh[ql]);
   // facet filter (uniform per work item): Bool[Must(text), Must(facet union)]
   const uint32_t fslot = pl.f.q_filter[q];
   const uint32_t* fmask = nullptr;
@@ -544,7 +559,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix, DevPla
   const uint64_t thr0 = pl.q_thr0[q];
   uint64_t pend = 0;
 #if FG_CONJ_HIST
-  uint32_t* const gh = pl.hist + (size_t)q * kQBins;
+  uint32_t* const gh = pl.hist + (size_t)ql * kQBins;
   const uint32_t h_lo = pl.q_hlo[q], h_sh = pl.q_hsh[q];
   // FG_CONJ_HIST=2: multi-list items read the bins in their first chunk, with
   // its lead loads in flight; single-list items need it before the block-max skip
@@ -1055,7 +1070,8 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
 }
 
 
-__global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, DevPlan pl) {
+template <bool kMulti>
+__global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, DevPlan pl) {
   __shared__ DisjShared sh;
   const uint32_t tid = threadIdx.x;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
@@ -1063,14 +1079,16 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
   const uint32_t w = pl.n_conj + (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 
   const uint32_t q = pl.work_q[w];
+  const DevIndex ix = kMulti ? seg_index(pl, q / pl.seg_nq) : ix0;
+  const uint32_t ql = kMulti ? q % pl.seg_nq : q;  // the batch query (threshold, histogram)
   const uint32_t tile0 = pl.work_c[w], ntile = pl.work_n[w];
   // terms: [Should clauses (clause order)][MustNot]; m = the Should clauses
   const uint32_t qmv = pl.q_m[q];
   const uint32_t mq = qm_terms(qmv), m = mq - qm_not(qmv);
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
-  uint64_t* gthr = &pl.thresh[q];
-  const QHist hq{pl.hist + (size_t)q * kQBins, pl.q_hlo[q], pl.q_hsh[q], pl.pub_mask, m, mq};
+  uint64_t* gthr = &pl.thresh[ql];
+  const QHist hq{pl.hist + (size_t)ql * kQBins, pl.q_hlo[q], pl.q_hsh[q], pl.pub_mask, m, mq};
   uint64_t pend = 0;  // thread 0: the last threshold exchange's reply, not yet folded in
 
   // facet filter: the union is intersected with the facet union, score = union + facet;
@@ -1717,9 +1735,11 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix, D
 // postings of one (filter, clause) facet list sets clause bit i of every doc
 // in it.  Postings ascend, so the lanes of a wave mostly hit the same or
 // neighbouring mask words: the atomics coalesce in L2.
-__global__ __launch_bounds__(kThreads) void k_fmask(DevIndex ix, DevPlan pl) {
+template <bool kMulti>
+__global__ __launch_bounds__(kThreads) void k_fmask(DevIndex ix0, DevPlan pl) {
   const uint32_t c = blockIdx.x;
   const uint32_t f = pl.f.ch_filter[c], i = pl.f.ch_clause[c], t = pl.f.ch_term[c], st = pl.f.ch_start[c];
+  const DevIndex ix = kMulti ? seg_index(pl, pl.f.f_seg[f]) : ix0;
   const uint64_t b0 = ix.foff[t];
   const uint32_t n = (uint32_t)(ix.foff[t + 1] - b0);
   const uint32_t end = min(n, st + kFmaskChunk);
@@ -1765,14 +1785,17 @@ __device__ inline void scan_truncate(ScanShared& sh, uint32_t K, uint32_t limit,
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kThreads) void k_scan(DevIndex ix, DevPlan pl) {
+template <bool kMulti>
+__global__ __launch_bounds__(kThreads) void k_scan(DevIndex ix0, DevPlan pl) {
   __shared__ ScanShared sh;
   const uint32_t tid = threadIdx.x;
   const uint32_t w = pl.total_chunks + blockIdx.x;  // scan items follow the k_conj / k_disj items
   const uint32_t q = pl.work_q[w];
+  const DevIndex ix = kMulti ? seg_index(pl, q / pl.seg_nq) : ix0;
+  const uint32_t ql = kMulti ? q % pl.seg_nq : q;
   const uint32_t tile0 = pl.work_c[w], ntile = pl.work_n[w];
   const uint32_t K = pl.k;
-  uint64_t* gthr = &pl.thresh[q];
+  uint64_t* gthr = &pl.thresh[ql];
   const uint32_t fslot = pl.f.q_filter[q];
   const uint32_t* fmask = nullptr;
   uint32_t fshift = 0;
@@ -1845,8 +1868,9 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
   const uint32_t K = pl.k;
   // the threshold word, or the query's histogram threshold when higher (>= K
   // docs of the query -- or of its linked plans -- score at least that much)
-  const uint64_t T0 = max(pl.thresh[q], hist_threshold(pl.hist + (size_t)q * kQBins, K, pl.q_hlo[q], pl.q_hsh[q],
-                                                       sh.scratch));
+  const uint32_t ql = slot_query(pl, q);  // a multi-snapshot plan: the slot's batch query
+  const uint64_t T0 = max(pl.thresh[ql], hist_threshold(pl.hist + (size_t)ql * kQBins, K, pl.q_hlo[q], pl.q_hsh[q],
+                                                        sh.scratch));
   const uint32_t cnt = pl.cand_cnt[q];
   const uint64_t* src = pl.cand_keys + pl.cand_off[q];
   // every candidate of query q, f(key >= lb, key) with the whole workgroup
@@ -2036,30 +2060,38 @@ __global__ __launch_bounds__(kThreads) void k_merge(uint32_t n_shards, uint32_t 
 }  // namespace
 
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
+  const bool multi = pl.segs != nullptr;
   if (pl.n_single) {
-    k_conj<true><<<pl.n_single, kThreads, 0, s>>>(ix, pl);
+    if (multi) k_conj<true, true><<<pl.n_single, kThreads, 0, s>>>(ix, pl);
+    else k_conj<true, false><<<pl.n_single, kThreads, 0, s>>>(ix, pl);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (pl.n_conj > pl.n_single) k_conj<false><<<pl.n_conj - pl.n_single, kThreads, 0, s>>>(ix, pl);
+  if (pl.n_conj > pl.n_single) {
+    if (multi) k_conj<false, true><<<pl.n_conj - pl.n_single, kThreads, 0, s>>>(ix, pl);
+    else k_conj<false, false><<<pl.n_conj - pl.n_single, kThreads, 0, s>>>(ix, pl);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   if (pl.total_chunks <= pl.n_conj) return hipSuccess;
-  k_disj<<<pl.total_chunks - pl.n_conj, kThreads, 0, s>>>(ix, pl);
+  if (pl.segs) k_disj<true><<<pl.total_chunks - pl.n_conj, kThreads, 0, s>>>(ix, pl);
+  else k_disj<false><<<pl.total_chunks - pl.n_conj, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 
 hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   if (pl.f.n_chunks == 0) return hipSuccess;
-  k_fmask<<<pl.f.n_chunks, kThreads, 0, s>>>(ix, pl);
+  if (pl.segs) k_fmask<true><<<pl.f.n_chunks, kThreads, 0, s>>>(ix, pl);
+  else k_fmask<false><<<pl.f.n_chunks, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 
 hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   if (pl.n_scan == 0) return hipSuccess;
-  k_scan<<<pl.n_scan, kThreads, 0, s>>>(ix, pl);
+  if (pl.segs) k_scan<true><<<pl.n_scan, kThreads, 0, s>>>(ix, pl);
+  else k_scan<false><<<pl.n_scan, kThreads, 0, s>>>(ix, pl);
   return hipGetLastError();
 }
 

@@ -52,7 +52,7 @@ EXPORTS = (
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
-    "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or",
+    "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -136,6 +136,7 @@ _sig("fg_index_stats_get", C.c_int, _p, C.POINTER(IndexStats))
 _sig("fg_index_df", C.c_uint64, _p, C.c_int, C.c_uint32)
 _sig("fg_index_bm25", C.c_int, _p, C.c_uint32, _f32p, _f32p, _f32p)
 _sig("fg_plan_create", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
+_sig("fg_plan_create_multi", C.c_int, C.POINTER(_p), C.c_uint32, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
 _sig("fg_plan_execute", C.c_int, _p, _p, _p, _p, _p)
 _sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
@@ -467,15 +468,25 @@ class Index:
 
 
 class Plan:
-    """A batch planned on the host and resident in HBM (fg_plan_create)."""
+    """A batch planned on the host and resident in HBM (fg_plan_create).  Given a
+    list of indexes of one device: a multi-snapshot plan (fg_plan_create_multi),
+    one launch per kernel over all of them; its results are per query slot
+    s * nq + q ([n_segs * nq, k]), the input layout of merge_shards."""
 
-    def __init__(self, index: Index, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None,
+    def __init__(self, index, q_off, terms, k: int, mode: int = MODE_AND, f_off=None, f_terms=None,
                  occur=None):
         qb, self._keep = _batch(q_off, terms, mode, f_off, f_terms, occur)
-        self.n_queries = qb.n_queries
         self.k = k
         h = _p()
-        _check(_lib.fg_plan_create(index.handle, C.byref(qb), k, C.byref(h)))
+        if isinstance(index, (list, tuple)):
+            self.n_segs = len(index)
+            hs = (_p * len(index))(*[ix.handle for ix in index])
+            _check(_lib.fg_plan_create_multi(hs, len(index), C.byref(qb), k, C.byref(h)))
+        else:
+            self.n_segs = 1
+            _check(_lib.fg_plan_create(index.handle, C.byref(qb), k, C.byref(h)))
+        self.n_batch = qb.n_queries
+        self.n_queries = qb.n_queries * self.n_segs  # query slots
         self._h = h
         self.index = index
 

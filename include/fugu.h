@@ -38,6 +38,7 @@ extern "C" {
 #define FG_MAX_TERMS 16        /* terms per query on the device path */
 #define FG_MAX_FACET_CLAUSES 8 /* facet filter clauses per query on the device path */
 #define FG_MAX_K 1024          /* largest k on the device path */
+#define FG_MAX_SEGMENTS 64     /* snapshots of one multi-snapshot plan / shards of one fg_search_sharded call */
 #define FG_TERM_MISSING 0xFFFFFFFFu /* a query term absent from the term dictionary */
 
 #define FG_MODE_AND 0 /* `t1 AND t2 ...` / `+t1 +t2`: Must clauses (src/db/search.rs:112 parser) */
@@ -216,6 +217,14 @@ typedef struct fg_query_batch {
  * Returns FG_EUNSUPPORTED for queries outside the device subset
  * (> FG_MAX_TERMS terms, > FG_MAX_FACET_CLAUSES clauses, k > FG_MAX_K). */
 int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** out);
+/* Plan a batch over n_segs snapshots of ONE device (a namespace's segments,
+ * doc shards scored with global statistics, or namespaces of a fan-out query)
+ * run by one launch per kernel: query slot s * n_queries + q is query q on
+ * ixs[s].  The slots of a query share its threshold score-only (as linked
+ * plans do).  Results (fg_plan_execute / fg_plan_results, fg_plan_info's
+ * n_queries) are per slot, layout [n_segs][n_queries][k] and [n_segs][n_queries]:
+ * the input of fg_merge_shards.  n_segs = 1 is fg_plan_create. */
+int fg_plan_create_multi(fg_index* const* ixs, uint32_t n_segs, const fg_query_batch* q, uint32_t k, fg_plan** out);
 /* Run a planned batch on `stream` (hipStream_t, NULL = default stream).
  * Outputs are device pointers [n_queries*k], [n_queries*k], [n_queries]; NULL
  * outputs use the plan's own buffers.  Asynchronous. */
@@ -273,8 +282,9 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
  * namespace built with global statistics, or several namespaces of a fan-out
  * query.  The shards share one term / facet dictionary; a term id >= a shard's
  * n_terms matches nothing there.  Each shard runs on its own device (one
- * process driving the node's GPUs; shards on the same device run back to back),
- * its per-shard top-k is copied over xGMI to shards[0]'s device and merged there
+ * process driving the node's GPUs; the shards of one device run as ONE
+ * multi-snapshot plan: fg_plan_create_multi), its per-shard top-k is copied
+ * over xGMI to shards[0]'s device and merged there
  * into (score desc, shard asc, doc asc) -- merge_fruits over (segment_ord, doc).
  * Host outputs [n_queries*k] (out_shard may be NULL) and out_n [n_queries].
  * ctx, when given, must hold every shard's device.  Thread-safe like

@@ -51,6 +51,32 @@ def main():
             ["ranges+hist_read", "split", "exhaustive_tiles", "segment_list", "filter_bound1_bound2", "rescore", "truncate_publish", "hist_add_flush"])},
         "cand_per_query": [int(x) for x in np.percentile(plan.candidate_counts(), [50, 90, 100])],
     }
+    # timeline: the kernel span and its tail (s_memrealtime: 100 MHz)
+    t0 = wg[:, 0].astype(np.int64)
+    t1 = wg[:, 1].astype(np.int64)
+    base = t0.min()
+    st, en = (t0 - base) * 10e-3, (t1 - base) * 10e-3  # us
+    span = float(en.max())
+    grid = np.linspace(0, span, 201)
+    busy = np.array([int(((st <= x) & (en > x)).sum()) for x in grid])
+    peak = max(int(busy.max()), 1)
+    out["timeline"] = {
+        "span_us": round(span, 1), "peak_busy_wgs": peak,
+        "us_below_half_busy": round(float((busy < peak / 2).mean() * span), 1),
+        "busy_at_pct": {str(p): int(busy[p * 2]) for p in (10, 50, 80, 90, 95, 99)},
+        "last_start_us": round(float(st.max()), 1),
+    }
+    post = wg[:, 5].astype(np.int64)
+    b1 = (wg[:, 6] >> np.uint64(32)).astype(np.int64)
+    qid = (wg[:, 7] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    top = np.argsort(-dt)[:12]
+    out["longest_items"] = [{"q": int(qid[i]), "us": round(float(dt[i]), 1), "start_us": round(float(st[i]), 1),
+                             "postings": int(post[i]), "past_bound1": int(b1[i]),
+                             "q_terms_df": [int(x) for x in dfs[q_off[qid[i]]:q_off[qid[i] + 1]]]} for i in top]
+    if post.sum() > 0:
+        out["us_per_posting_p50"] = round(float(np.median(dt[post > 0] / post[post > 0])), 5)
+        out["corr_us_postings"] = round(float(np.corrcoef(dt, post)[0, 1]), 3)
+        out["corr_us_past_bound1"] = round(float(np.corrcoef(dt, b1)[0, 1]), 3)
     print(json.dumps(out), flush=True)
 
 

@@ -7,6 +7,7 @@
 #   (separate --pmc passes: a pass holds <= 4 TCC counters; no trace domains with --pmc)
 # then tools/pmc_traffic.py -> per-launch HBM bytes.  Every step has its own limit.
 #   bash tools/profile_bench.sh TAG [bench args...]   (default: the headline workload)
+#   CALIB_FROM=<an earlier OUT dir> reuses its calib_fetch / calib_dram passes
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 TAG=${1:-r02}
@@ -20,9 +21,15 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 echo "[prof] trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err"
-echo "[prof] calib"
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- "$R/tools/calib_fetch" > "$OUT/calib_fetch.log" 2>&1
-timeout -s KILL 120 rocprofv3 --pmc $DRAM --output-format csv -d "$OUT/calib_dram" -o run -- "$R/tools/calib_fetch" > "$OUT/calib_dram.log" 2>&1
+if [ -n "${CALIB_FROM:-}" ]; then
+  # the calibration of an earlier pass of the same call (same box, same counters)
+  echo "[prof] calib from $CALIB_FROM"
+  cp -r "$CALIB_FROM/calib_fetch" "$CALIB_FROM/calib_dram" "$OUT/"
+else
+  echo "[prof] calib"
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- "$R/tools/calib_fetch" > "$OUT/calib_fetch.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $DRAM --output-format csv -d "$OUT/calib_dram" -o run -- "$R/tools/calib_fetch" > "$OUT/calib_dram.log" 2>&1
+fi
 echo "[prof] fetch"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.err"
 echo "[prof] write"
