@@ -93,8 +93,12 @@ constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
 #ifndef FG_DISJ_EXH
 #define FG_DISJ_EXH 0
 #endif
+#ifndef FG_DISJ_QUEUE
+#define FG_DISJ_QUEUE 1  // k_disj: bound 2 deferred through an LDS queue of the postings past bound 1
+                         // (ab_disj_queue_k*.log: OR top-20 3.92 -> 3.23 ms, top-1000 6.13 -> 5.94 ms)
+#endif
 #ifndef FG_DISJ_HBITS
-#define FG_DISJ_HBITS 10
+#define FG_DISJ_HBITS (FG_DISJ_QUEUE ? 9 : 10)  // the queue's LDS comes out of the select's digit width
 #endif
 #ifndef FG_DISJ_WAVES
 #define FG_DISJ_WAVES 5
@@ -110,6 +114,10 @@ constexpr uint32_t kSubPerTile = 1u << (FG_TILE_SHIFT - kSubShift);
 #endif
 constexpr uint32_t kDisjMaxGroup = FG_DISJ_MAXGROUP;  // ... at most this many tiles per work item
 constexpr uint32_t kDisjMaxPairs = 256;  // ... and at most this many (tile, Should clause) pairs (k_disj LDS)
+#ifndef FG_DISJ_ITEM_POSTINGS
+#define FG_DISJ_ITEM_POSTINGS 1000000000u  // A/B: cap on a k_disj item's postings (all its clauses, mean density)
+#endif
+constexpr uint32_t kDisjItemPostings = FG_DISJ_ITEM_POSTINGS;
 #ifndef FG_EXHMIN
 #define FG_EXHMIN 1024
 #endif

@@ -1676,7 +1676,14 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       set_bins(i, ub);
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
-      const uint32_t G = std::min<uint32_t>(std::min(fg::kDisjMaxGroup, fg::kDisjMaxPairs / ns),
+      // tiles per item: ~gpq items per query, and at most ~kDisjItemPostings
+      // postings per item at the clauses' mean density (a query of dense terms
+      // gets more, shorter items: its late items no longer make the kernel's tail)
+      double per_tile = 0.0;
+      for (uint32_t c = 0; c < ns; ++c) per_tile += (double)(ix->off[qt[c] + 1] - ix->off[qt[c]]);
+      per_tile *= (double)(1u << fg::kDisjTileShift) / (double)std::max<uint64_t>(N, 1);
+      const uint32_t g_cost = (uint32_t)std::max(1.0, std::min(1e9, (double)fg::kDisjItemPostings / std::max(per_tile, 1.0)));
+      const uint32_t G = std::min<uint32_t>(std::min(std::min(fg::kDisjMaxGroup, fg::kDisjMaxPairs / ns), g_cost),
                                             std::max<uint32_t>(1, (nt + gpq - 1) / gpq));
       const uint32_t ng = (nt + G - 1) / G;
       ngroup[i] = ng;
@@ -1736,8 +1743,9 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     // batch of one: the p50 latency) spreads a query over up to 64 items so its
     // chunks run side by side instead of up to kMaxGroup in a row, while its
     // k_final still reads at most 64 x k candidates
-    const uint32_t per_q = std::max<uint32_t>(
-        1, std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u))) / n_segs);
+    // (not divided over a multi-snapshot plan's snapshots: fewer, longer k_conj
+    // items per snapshot measured slower, multi_ab AND 1.45 -> 1.52 ms)
+    const uint32_t per_q = std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u)));
     const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + per_q - 1) / per_q));
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;

@@ -933,11 +933,12 @@ constexpr uint32_t kTile = 1u << kTileShift;   // docs per tile (LDS score array
 constexpr uint32_t kRound = FG_DISJ_ROUND;     // postings / docs per pass
 constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
 constexpr uint32_t kPairs = kRound;            // (candidate, clause) rescoring pairs per pass
+constexpr uint32_t kQCap = 2 * kRound;         // FG_DISJ_QUEUE: < one pass queued + one pass appended
 constexpr uint32_t kDisjHistBits = FG_DISJ_HBITS;
 constexpr uint32_t kMaxTiles = kDisjMaxGroup;  // tiles per work item
 constexpr uint32_t kMaxSeg = kDisjMaxPairs;    // (tile, clause) pairs per work item (the planner's cap)
 static_assert(kMaxSeg <= 2 * kThreads, "k_disj segment list: two (tile, clause) pairs per thread");
-static_assert(kMaxTiles <= 32 && kMaxTerms <= 16, "seg_info packs (tile << 4) | clause");
+static_assert(kMaxTiles <= 255 && kMaxTerms <= 16, "seg_info packs (tile << 4) | clause; cand (tile << 8) | clause");
 
 // A sub-tile bound stored as q / 255 of its tile bound (q = 255: the tile
 // bound itself); the R phase picks the smallest q whose value is >= the
@@ -956,8 +957,16 @@ struct DisjShared {
     } e;
 #endif
     struct {
+#if FG_DISJ_QUEUE
+      // P: postings past bound 1 waiting for bound 2, (score bits << 32) | (clause
+      // << kRelBits) | (doc - the item's first doc); a flushed chunk's slots then
+      // hold its rescoring candidates, (maybe-mask << kRelBits + 4) | (clause <<
+      // kRelBits) | doc offset (kRelBits: 17 for 32-tile items)
+      uint64_t q[kQCap];
+#else
       uint64_t cand[kRound];         // P: (doc << 32) | (maybe-mask << 16) | (tile << 8) | clause
       float cand_s[kRound];          // P: the source clause's score of each candidate
+#endif
       float cs[kPairs];              // P: per-(candidate, clause) term scores
       uint32_t seg_start[kMaxSeg];   // P: prefix of the essential segments' lengths
     } p;
@@ -980,6 +989,7 @@ struct DisjShared {
   uint64_t c_base[kMaxTerms];
   uint32_t max_s, n_seg, n_post;
   uint32_t n_buf, n_cand;
+  uint32_t n_q;                      // P: queued postings (FG_DISJ_QUEUE)
   uint32_t n_cnt;                    // buf[0, n_cnt) are counted in the query's histogram
   uint64_t thr;
   uint32_t lh[kQBins];               // hits per score bin not yet added to the global histogram
@@ -1388,6 +1398,285 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     }
   }
 #endif
+#if FG_DISJ_QUEUE
+  // Deferred bound 2.  A pass loads kRound postings and applies bound 1 (LDS
+  // only); the survivors wait in an LDS queue, and bound 2 + the rescoring run
+  // once the queue holds a full pass (or the item ends): their dependent gather
+  // chains then run with every lane busy, once per kRound survivors, instead of
+  // once per pass for the fraction of its postings that pass bound 1.
+  // the doc within the item in kRelBits, the clause in the next 4 bits, a
+  // candidate's maybe-mask above them
+  constexpr uint32_t kRelBits = 32 - __builtin_clz(kDisjMaxGroup * kTile - 1);
+  constexpr uint32_t kRelMask = (1u << kRelBits) - 1u;
+  static_assert(kRelBits + 4 <= 32 && kMaxTerms <= 16, "a queue entry: doc offset + clause in 32 bits");
+  const uint32_t dbase = tile0 << kTileShift;
+  if (tid == 0) sh.n_q = 0;
+  __syncthreads();
+  for (uint32_t e0 = 0; e0 < n_post; e0 += kRound) {
+    uint32_t pd[J], pcl[J];
+    float ps[J];
+    bool pk[J];
+#pragma unroll
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t e = e0 + j * kThreads + tid;
+      pk[j] = e < n_post;
+      pd[j] = dbase;
+      pcl[j] = 0;
+      ps[j] = 0.0f;
+      if (pk[j]) {
+        uint32_t t;
+        const uint64_t at = locate(e, t, pcl[j]);
+        pd[j] = ix.doc[at];
+        ps[j] = ix.psc[at];
+      }
+    }
+    // with this pass's posting loads in flight: the last exchange's reply
+    if (tid == 0 && pend > sh.thr) sh.thr = pend;
+    __syncthreads();
+    {
+      const uint64_t thr = sh.thr;
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        if (pk[j]) {
+          // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
+          const uint32_t t = (pd[j] - dbase) >> kTileShift;
+          float ub = ps[j] + fmax;
+          for (uint32_t i = 0; i < m; ++i)
+            if (i != pcl[j]) ub += sh.r_ub[t * m + i];
+          pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
+          if (pk[j] && fmask) pk[j] = filter_bits(fmask, fshift, pd[j]) != 0;
+#ifdef FG_DIAG
+          dg_b1 += pk[j] ? 1u : 0u;
+#endif
+        }
+        wave_append(pk[j], ((uint64_t)__float_as_uint(ps[j]) << 32) | (pcl[j] << kRelBits) | (pd[j] - dbase), sh.u.p.q,
+                    &sh.n_q, kQCap);
+      }
+    }
+    __syncthreads();
+    FG_PHASE(4);
+    const uint32_t nqd = sh.n_q;  // uniform
+    const bool last = e0 + kRound >= n_post;
+    if (nqd < kRound && !(last && nqd)) continue;
+    // flush: bound 2 and the rescoring over the queue, kRound entries at a time
+    uint32_t done = 0;
+    while (nqd - done >= kRound || (last && done < nqd)) {
+      const uint32_t cnt = min(kRound, nqd - done);
+      uint64_t ent[J];
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        const uint32_t i = j * kThreads + tid;
+        pk[j] = i < cnt;
+        ent[j] = pk[j] ? sh.u.p.q[done + i] : 0ull;
+      }
+      if (tid == 0) {
+        sh.n_cand = 0;
+        if (pend > sh.thr) sh.thr = pend;
+      }
+      __syncthreads();  // the chunk is in registers before its slots take the candidates
+      const uint64_t thr = sh.thr;
+      uint32_t pt[J], ess[J];
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        const uint32_t rel = (uint32_t)ent[j] & kRelMask;
+        pd[j] = dbase + rel;
+        pcl[j] = ((uint32_t)ent[j] >> kRelBits) & 15u;
+        ps[j] = __uint_as_float((uint32_t)(ent[j] >> 32));
+        pt[j] = rel >> kTileShift;
+        ess[j] = 0;
+        if (!pk[j]) continue;
+        // bound 1 again: the threshold may have risen since the posting was queued
+        float ub = ps[j] + fmax;
+        for (uint32_t i = 0; i < m; ++i)
+          if (i != pcl[j]) ub += sh.r_ub[pt[j] * m + i];
+        pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
+        ess[j] = sh.t_ess[pt[j]];
+      }
+      // bound 2: every other clause at d, one clause at a time in clause order:
+      // its rank word (presence bits + rank) and then the posting score, its
+      // f32 table score, or its bucket maximum (-0.0: empty bucket).  When every
+      // other clause is dense (or has no posting in the tile) the clause-order
+      // sum IS the doc's exact SumCombiner score: a hit right here.
+      float sum[J];
+      uint32_t maybe[J];  // clauses whose structure at d says they may match (the rest cannot)
+      bool exact[J];
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        sum[j] = 0.0f;
+        maybe[j] = 0;
+        exact[j] = true;
+      }
+      constexpr uint32_t kAbsent = 0xBF800000u;  // -1.0f: the clause is not on the doc
+      for (uint32_t i = 0; i < m; ++i) {
+        const uint32_t meta = sh.c_meta[i];
+        const uint32_t slot = meta_slot(meta);
+        const bool rank = slot && meta_rank(meta);
+        uint32_t y[J];
+        uint32_t need = 0;
+        {
+          uint64_t x[J];
+#pragma unroll
+          for (uint32_t j = 0; j < J; ++j) {
+            x[j] = kAbsent;
+            if (pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
+              need |= 1u << j;
+              if (rank) x[j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
+              else if (slot) x[j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
+              else x[j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
+            }
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < J; ++j) {
+            const uint32_t bits = (uint32_t)x[j], bt = pd[j] & 31u;
+            if (!rank || !((need >> j) & 1u)) y[j] = (uint32_t)x[j];
+            else y[j] = ((bits >> bt) & 1u) ? (uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))
+                                            : kAbsent;
+          }
+        }
+        if (rank) {
+          const float* __restrict__ sp = ix.psc + sh.c_base[i];
+#pragma unroll
+          for (uint32_t j = 0; j < J; ++j)
+            if (((need >> j) & 1u) && y[j] < 0x80000000u) y[j] = __float_as_uint(sp[y[j]]);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < J; ++j) {
+          if (!pk[j]) continue;
+          float b = ps[j];
+          if (i != pcl[j]) {
+            if (!((need >> j) & 1u)) continue;
+            b = __uint_as_float(y[j]);
+            exact[j] = exact[j] && slot != 0;
+            if (signbit(b)) continue;  // clause i cannot match d
+            maybe[j] |= 1u << i;
+          }
+          sum[j] += b;
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        bool keep = false, direct = false;
+        uint64_t dkey = 0;
+        if (pk[j]) {
+          if (exact[j]) {
+            // unique keys: the doc is kept only from the first essential clause it matches
+            const uint32_t first = (uint32_t)__builtin_ctz((maybe[j] | (1u << pcl[j])) & ess[j]);
+            const float s2 = fmask ? sum[j] + ftab[filter_bits(fmask, fshift, pd[j])] : sum[j];
+            dkey = make_key(s2, pd[j]);
+            direct = first == pcl[j] && dkey >= thr && doc_alive(ix, pd[j]);
+          } else {
+            keep = make_key(inflate_bound(sum[j] + fmax), pd[j]) >= thr && doc_alive(ix, pd[j]);
+          }
+        }
+        wave_append(direct, dkey, sh.buf, &sh.n_buf, kBufD);
+        wave_append(keep, ((uint64_t)maybe[j] << (kRelBits + 4)) | (pcl[j] << kRelBits) | (pd[j] - dbase),
+                    sh.u.p.q + done, &sh.n_cand, cnt);
+      }
+      __syncthreads();
+      FG_PHASE(5);
+      const uint32_t nc = sh.n_cand;
+#ifdef FG_DIAG
+      dg_cand += nc;
+#endif
+      // exact rescoring: every (candidate, clause) pair the doc may match -- its
+      // own clause included -- probed in parallel, summed in clause order
+      const uint64_t* cq = sh.u.p.q + done;
+      const uint32_t Q = kPairs / m;
+      for (uint32_t c0 = 0; c0 < nc; c0 += Q) {
+        const uint32_t nq_ = min(Q, nc - c0), np = nq_ * m;
+        constexpr uint32_t R = kPairs / kThreads;
+        uint32_t rd[R], pc[R], pos[R], hi[R];
+        float pv[R];  // the clause's score at the candidate, -1 = absent
+#pragma unroll
+        for (uint32_t j = 0; j < R; ++j) {
+          const uint32_t p = j * kThreads + tid;
+          pc[j] = kInvalid;
+          rd[j] = 0;
+          pv[j] = -1.0f;
+          pos[j] = 0;
+          hi[j] = 0;
+          if (p < np) {
+            const uint64_t cv = cq[c0 + p / m];
+            const uint32_t i = p % m, src = ((uint32_t)cv >> kRelBits) & 15u;
+            rd[j] = dbase + ((uint32_t)cv & kRelMask);
+            pc[j] = (i == src || ((uint32_t)(cv >> (kRelBits + 4)) >> i) & 1u) ? i : (0x80000000u | i);
+          }
+          if (!(pc[j] & 0x80000000u)) {
+            const uint32_t meta = sh.c_meta[pc[j]];
+            if (meta_slot(meta)) {
+              pv[j] = dense_score(ix, meta, sh.c_base[pc[j]], rd[j]);
+              pc[j] |= 0x80000000u;  // resolved
+            } else {
+              const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[pc[j]];
+              const uint32_t b = rd[j] >> (meta & 0xFFu);
+              pos[j] = dir[b];
+              hi[j] = dir[b + 1];
+            }
+          }
+        }
+        for (uint32_t st = sh.max_s; st > 0; --st) {
+#pragma unroll
+          for (uint32_t j = 0; j < R; ++j) {
+            if (pc[j] & 0x80000000u) continue;  // invalid or resolved
+            if (st > ((sh.c_meta[pc[j]] >> 8) & 0xFFu)) continue;
+            const uint32_t half = 1u << (st - 1);
+            const uint32_t idx = pos[j] + half - 1;
+            if (idx < hi[j] && ix.doc[sh.c_base[pc[j]] + idx] < rd[j]) pos[j] += half;
+          }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < R; ++j) {
+          if (pc[j] & 0x80000000u) continue;
+          const uint64_t base = sh.c_base[pc[j]];
+          if (pos[j] < hi[j] && ix.doc[base + pos[j]] == rd[j]) pv[j] = ix.psc[base + pos[j]];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < R; ++j) {
+          const uint32_t p = j * kThreads + tid;
+          if (p < np) sh.u.p.cs[p] = pv[j];
+        }
+        __syncthreads();
+        for (uint32_t cc0 = 0; cc0 < nq_; cc0 += kThreads) {
+          const uint32_t cc = cc0 + tid;
+          uint64_t key = 0;
+          bool keep = cc < nq_;
+          if (keep) {
+            const uint64_t cv = cq[c0 + cc];
+            const uint32_t rel = (uint32_t)cv & kRelMask, src = ((uint32_t)cv >> kRelBits) & 15u;
+            const uint32_t d = dbase + rel;
+            float sc = 0.0f;  // SumCombiner from 0.0 in clause order over the matching clauses
+            uint32_t matched = 0;
+            for (uint32_t i = 0; i < m; ++i) {
+              const float v = sh.u.p.cs[cc * m + i];
+              if (v >= 0.0f) {
+                sc += v;
+                matched |= 1u << i;
+              }
+            }
+            // unique keys: keep the doc only from the first essential clause it matches
+            const uint32_t first = (uint32_t)__builtin_ctz(matched & sh.t_ess[rel >> kTileShift]);
+            if (fmask) sc = sc + ftab[filter_bits(fmask, fshift, d)];
+            key = make_key(sc, d);
+            keep = first == src && key >= thr;
+          }
+          wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
+        }
+        __syncthreads();
+      }
+      FG_PHASE(6);
+#ifdef FG_DIAG
+      if (sh.n_buf > K) dg_trunc++;
+#endif
+      disj_truncate(ix, sh, K, K, gthr, true, hq, pend);
+      done += cnt;
+    }
+    // the rest of the queue (< kRound entries, behind the flushed chunks) moves to the front
+    const uint32_t rem = nqd - done;
+    for (uint32_t i = tid; i < rem; i += kThreads) sh.u.p.q[i] = sh.u.p.q[done + i];
+    if (tid == 0) sh.n_q = rem;
+    __syncthreads();
+  }
+#else
   for (uint32_t e0 = 0; e0 < n_post; e0 += kRound) {
     uint32_t pd[J], pt[J], pcl[J], ess[J];
     float ps[J];
@@ -1701,6 +1990,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     disj_truncate(ix, sh, K, K, gthr, true, hq, pend);
     FG_PHASE(6);
   }
+#endif  // FG_DISJ_QUEUE
   // the item's counted hits join the query's histogram (every key was counted
   // by the last disj_truncate)
   hist_add(sh.lh, hq.gh);
