@@ -817,7 +817,7 @@ def main():
                    "kernel_ms": round(kms[0] / max(kn, 1), 4), "k_final_ms": round(kms[1] / max(kn, 1), 4),
                    "merge_bytes_per_launch": merge_bytes,
                    "merge_equiv_gbs": round(merge_bytes / (kms[0] / max(kn, 1) * 1e-3) / 1e9, 1)}
-            if mode == native.MODE_OR and kk == 1000:
+            if mode == native.MODE_OR:
                 # device-layout MaxScore bytes at each query's final k-th score (fg_bytes_model_or):
                 # the least an exact k_disj reads, over the kernel's time
                 thr = np.where(n2 >= kk, s2[:, kk - 1], 0.0).astype(np.float32)

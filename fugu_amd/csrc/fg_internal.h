@@ -274,6 +274,9 @@ struct DevPlan {
   // kernel's DevIndex argument).
   const DevIndex* segs;         // [n_segs] or nullptr
   uint32_t seg_nq;              // queries of the batch (slots per snapshot), 0 = one snapshot
+  uint32_t n_segs;
+  const uint32_t* seg_base;     // [n_segs] first doc of each snapshot in the concatenation (k_final's merged
+                                // select), or nullptr when the snapshots hold >= 2^32 docs together
   DevFilters f;
 };
 
@@ -339,7 +342,9 @@ hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
-hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s);
+// out_shard != nullptr: the merged select of a multi-snapshot plan (one list per batch query)
+hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s,
+                        uint32_t* out_shard = nullptr);
 hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s);
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
                        uint32_t n_words, uint64_t* out, hipStream_t s);

@@ -1924,9 +1924,19 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
                s_qf = al(4ull * nq), s_fs = al(4ull * nf),
                s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch),
                s_hb = al(4ull * nq), s_fg = S > 1 ? al(4ull * nf) : 0,
-               s_sg = S > 1 ? al(sizeof(fg::DevIndex) * S) : 0;
+               s_sg = S > 1 ? al(sizeof(fg::DevIndex) * S) : 0, s_sb = S > 1 ? al(4ull * S) : 0;
+  // the snapshots' first docs in their concatenation (k_final's merged select)
+  std::vector<uint32_t> seg_base;
+  if (S > 1) {
+    uint64_t b = 0;
+    for (uint32_t x = 0; x < S; ++x) {
+      seg_base.push_back((uint32_t)std::min<uint64_t>(b, 0xFFFFFFFFull));
+      b += ixs[x]->n_docs;
+    }
+    if (b > 0xFFFFFFFFull) seg_base.clear();  // no merged select past 2^32 docs
+  }
   const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft +
-                      s_fm + 4 * s_ch + 2 * s_hb + s_fg + s_sg;
+                      s_fm + 4 * s_ch + 2 * s_hb + s_fg + s_sg + s_sb;
   // one score histogram per query (DevPlan::hist: k_conj's and k_disj's running thresholds)
   // (thresholds and histograms: one per batch query, shared by its slots)
   const size_t s_thr = al(8ull * nq1), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]),
@@ -1995,6 +2005,8 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     for (uint32_t s = 0; s < S; ++s) segs[s] = ixs[s]->d;
     p->d.f.f_seg = (const uint32_t*)put(f_seg.data(), 4ull * nf, s_fg);
     p->d.segs = (const fg::DevIndex*)put(segs.data(), sizeof(fg::DevIndex) * S, s_sg);
+    const uint32_t* sb = (const uint32_t*)put(seg_base.data(), 4ull * seg_base.size(), s_sb);
+    p->d.seg_base = seg_base.empty() ? nullptr : sb;
   }
   // on the planning thread's own stream (or the caller's `up`): a plan built
   // while another thread's batch runs does not serialise against it through the
@@ -2037,6 +2049,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->d.n_single = (uint32_t)n_single;
   p->d.k = k;
   p->d.seg_nq = S > 1 ? nq1 : 0;
+  p->d.n_segs = S;
   // several snapshots: a batch query's slots share its threshold score-only, so a
   // doc of another snapshot tied with the k-th score is never pruned (the merge
   // breaks such ties by snapshot)
@@ -2049,13 +2062,10 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   return FG_OK;
 }
 
-int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_n) {
-  if (!p) return fail(FG_EINVAL, "NULL plan");
-  hipStream_t s = static_cast<hipStream_t>(stream);
+// the kernels of a planned batch on stream s; out_shard != nullptr: a
+// multi-snapshot plan's merged select (one list per batch query)
+static int execute_impl(fg_plan* p, hipStream_t s, float* os, uint32_t* od, uint32_t* on, uint32_t* oshard) {
   HIPCHK(hipSetDevice(p->ix->dev));
-  float* os = d_out_score ? d_out_score : p->own_score;
-  uint32_t* od = d_out_doc ? d_out_doc : p->own_doc;
-  uint32_t* on = d_out_n ? d_out_n : p->own_n;
   if (p->zeroed) p->zeroed = false;  // the first execute after the upload
   else HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
   hipEvent_t ev[3] = {};
@@ -2068,7 +2078,7 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
   if (p->d.total_chunks > p->d.n_conj) HIPCHK(fg::launch_disj(p->ix->d, p->d, s));
   if (p->d.n_scan) HIPCHK(fg::launch_scan(p->ix->d, p->d, s));
   if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
-  HIPCHK(fg::launch_final(p->d, os, od, on, s));
+  HIPCHK(fg::launch_final(p->d, os, od, on, s, oshard));
   if (p->profile) {
     HIPCHK(hipEventRecord(ev[2], s));
     p->pending.insert(p->pending.end(), ev, ev + 3);
@@ -2076,6 +2086,23 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
   p->last_stream = s;
   p->last_stream_used = true;
   return FG_OK;
+}
+
+int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_n) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  return execute_impl(p, static_cast<hipStream_t>(stream), d_out_score ? d_out_score : p->own_score,
+                      d_out_doc ? d_out_doc : p->own_doc, d_out_n ? d_out_n : p->own_n, nullptr);
+}
+
+// A multi-snapshot plan straight to the merged top-k of every batch query: the
+// kernels of fg_plan_execute, then ONE k_final over all slots of each query
+// (keys shifted by the snapshots' bases) in place of per-slot lists + merge
+int fg_plan_execute_merged(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_shard,
+                           uint32_t* d_out_n) {
+  if (!p || !d_out_score || !d_out_doc || !d_out_shard || !d_out_n) return fail(FG_EINVAL, "bad arguments");
+  if (p->n_segs < 2 || !p->d.seg_base)
+    return fail(FG_EUNSUPPORTED, "not a multi-snapshot plan over < 2^32 docs (use fg_plan_execute + fg_merge_shards)");
+  return execute_impl(p, static_cast<hipStream_t>(stream), d_out_score, d_out_doc, d_out_n, d_out_shard);
 }
 
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n) {
@@ -2536,6 +2563,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     }
   }
   const size_t ng = groups.size();
+  bool merged = false;  // the plan's merged select already wrote ms / md / msh / mn
   std::vector<std::unique_ptr<fg_plan>> plans(ng);
   std::vector<hipEvent_t> evs(ng, nullptr);
   // teardown (also on error returns): every device's stream drained, then the
@@ -2573,6 +2601,14 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     }
     plans[g].reset(p);
     if (trace) t_plan += now() - t_p;
+    // every shard on dev0 in one plan: its merged select writes the merged
+    // lists directly (no per-shard lists, no k_merge_rank)
+    static const bool no_merged = getenv("FUGU_SHARDED_NO_MERGED_FINAL") != nullptr;
+    if (ng == 1 && gdev[0] == dev0 && S > 1 && p->d.seg_base && !no_merged) {
+      if (int rc = execute_impl(p, hipStreamPerThread, ms, md, mn, msh)) return rc;
+      merged = true;
+      break;
+    }
     // lists straight into the gathered buffers when the group's shards are
     // consecutive and on dev0 ([S][nq][k] is the gathered layout)
     const bool direct = gdev[g] == dev0 && gi.back() - gi.front() + 1 == S;
@@ -2605,11 +2641,11 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   HIPCHK(hipSetDevice(dev0));
   for (hipEvent_t e : evs)
     if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
-  HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
+  if (!merged) HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
   if (trace) {
     HIPCHK(hipStreamSynchronize(hipStreamPerThread));
-    fprintf(stderr, "[fg_search_sharded] nq %u shards %u devices %zu: plan %.3f launch %.3f kernels+merge %.3f ms\n",
-            nq, n_shards, ng, t_plan, t_run - t_0 - t_plan, now() - t_run);
+    fprintf(stderr, "[fg_search_sharded] nq %u shards %u devices %zu merged %d: plan %.3f launch %.3f kernels+merge %.3f ms\n",
+            nq, n_shards, ng, (int)merged, t_plan, t_run - t_0 - t_plan, now() - t_run);
   }
   // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
   const size_t span = 3 * o_k + 4ull * nq;

@@ -2147,8 +2147,16 @@ struct FinalShared {
 };
 constexpr size_t kFinalLds = sizeof(FinalShared);
 
+// kMerged (a multi-snapshot plan with DevPlan::seg_base): one workgroup per
+// batch query selects over the candidates of ALL its slots at once, each key's
+// doc shifted by its snapshot's base (key - base: ~(base + doc)), so the order
+// (score desc, snapshot base + doc asc) IS the merge by (score desc, shard asc,
+// doc asc): the merged top-k without per-slot lists and k_merge_rank.  Slots
+// past a query's count are written as score 0, doc 0, shard 0.
+template <bool kMerged>
 __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restrict__ out_score,
-                                                     uint32_t* __restrict__ out_doc, uint32_t* __restrict__ out_n) {
+                                                     uint32_t* __restrict__ out_doc, uint32_t* __restrict__ out_n,
+                                                     uint32_t* __restrict__ out_shard) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   FinalShared& sh = *reinterpret_cast<FinalShared*>(lds_raw);
   const uint32_t q = blockIdx.x, tid = threadIdx.x;
@@ -2158,27 +2166,35 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
   const uint32_t K = pl.k;
   // the threshold word, or the query's histogram threshold when higher (>= K
   // docs of the query -- or of its linked plans -- score at least that much)
-  const uint32_t ql = slot_query(pl, q);  // a multi-snapshot plan: the slot's batch query
+  const uint32_t ql = kMerged ? q : slot_query(pl, q);  // a multi-snapshot plan: the slot's batch query
   const uint64_t T0 = max(pl.thresh[ql], hist_threshold(pl.hist + (size_t)ql * kQBins, K, pl.q_hlo[q], pl.q_hsh[q],
                                                         sh.scratch));
-  const uint32_t cnt = pl.cand_cnt[q];
-  const uint64_t* src = pl.cand_keys + pl.cand_off[q];
-  // every candidate of query q, f(key >= lb, key) with the whole workgroup
-  // converged; eight loads per thread in flight per round (the list is read
-  // once per pass and the passes are latency-bound)
+  const uint32_t n_lists = kMerged ? pl.n_segs : 1;
+  uint32_t cnt = 0;  // candidates of all lists
+  for (uint32_t s = 0; s < n_lists; ++s) cnt += pl.cand_cnt[kMerged ? s * pl.seg_nq + q : q];
+  // every candidate of query q (of every slot of q), f(key >= lb, key) with the
+  // whole workgroup converged; eight loads per thread in flight per round (the
+  // lists are read once per pass and the passes are latency-bound).  Merged:
+  // keys as (score, ~(snapshot base + doc)); thresholds are score-only there
   auto each_key = [&](uint64_t lb, auto&& f) {
     constexpr uint32_t U = 8;
-    for (uint32_t i0 = 0; i0 < cnt; i0 += U * kThreads) {
-      uint64_t key[U];
+    for (uint32_t s = 0; s < n_lists; ++s) {
+      const uint32_t v = kMerged ? s * pl.seg_nq + q : q;
+      const uint32_t c = kMerged ? pl.cand_cnt[v] : cnt;
+      const uint64_t* src = pl.cand_keys + pl.cand_off[v];
+      const uint64_t sub = kMerged ? pl.seg_base[s] : 0u;
+      for (uint32_t i0 = 0; i0 < c; i0 += U * kThreads) {
+        uint64_t key[U];
 #pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t i = i0 + u * kThreads + tid;
-        key[u] = i < cnt ? src[i] : 0;
-      }
+        for (uint32_t u = 0; u < U; ++u) {
+          const uint32_t i = i0 + u * kThreads + tid;
+          key[u] = i < c ? src[i] - sub : 0;
+        }
 #pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t i = i0 + u * kThreads + tid;
-        f(i < cnt && key[u] >= lb, key[u]);
+        for (uint32_t u = 0; u < U; ++u) {
+          const uint32_t i = i0 + u * kThreads + tid;
+          f(i < c && key[u] >= lb, key[u]);
+        }
       }
     }
   };
@@ -2220,10 +2236,32 @@ __global__ __launch_bounds__(kThreads) void k_final(DevPlan pl, float* __restric
   for (uint32_t i = nout + tid; i < P; i += kThreads) sorted[i] = 0;
   __syncthreads();
   bitonic_sort_desc(sorted, P);
-  for (uint32_t i = tid; i < nout; i += kThreads) {
-    const uint64_t k = sorted[i];
-    out_score[(size_t)q * K + i] = key_score(k);
-    out_doc[(size_t)q * K + i] = key_doc(k);
+  if (kMerged) {
+    for (uint32_t i = tid; i < K; i += kThreads) {
+      float sc = 0.0f;
+      uint32_t d = 0, sd = 0;
+      if (i < nout) {
+        const uint64_t k = sorted[i];
+        const uint32_t g = key_doc(k);  // snapshot base + doc
+        uint32_t lo = 0, hi = pl.n_segs;  // the last snapshot whose base <= g
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pl.seg_base[mid] <= g) lo = mid; else hi = mid;
+        }
+        sc = key_score(k);
+        d = g - pl.seg_base[lo];
+        sd = lo;
+      }
+      out_score[(size_t)q * K + i] = sc;
+      out_doc[(size_t)q * K + i] = d;
+      if (out_shard) out_shard[(size_t)q * K + i] = sd;
+    }
+  } else {
+    for (uint32_t i = tid; i < nout; i += kThreads) {
+      const uint64_t k = sorted[i];
+      out_score[(size_t)q * K + i] = key_score(k);
+      out_doc[(size_t)q * K + i] = key_doc(k);
+    }
   }
   if (tid == 0) out_n[q] = nout;
   FG_STAMP(dq, 3, FG_NOW());
@@ -2385,20 +2423,25 @@ hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s) {
-  if (pl.n_queries == 0) return hipSuccess;
-  // opt in to > 64 KB of dynamic LDS once per device
-  static unsigned long long attr_set = 0;
+hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s,
+                        uint32_t* out_shard) {
+  const bool merged = out_shard != nullptr;
+  if (merged && (!pl.seg_base || !pl.seg_nq)) return hipErrorInvalidValue;
+  const uint32_t grid = merged ? pl.seg_nq : pl.n_queries;
+  if (grid == 0) return hipSuccess;
+  // opt in to > 64 KB of dynamic LDS once per device and instantiation
+  static unsigned long long attr_set[2] = {0, 0};
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (dev < 64 && !((__atomic_load_n(&attr_set, __ATOMIC_ACQUIRE) >> dev) & 1ull)) {
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_final), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kFinalLds);
+  if (dev < 64 && !((__atomic_load_n(&attr_set[merged], __ATOMIC_ACQUIRE) >> dev) & 1ull)) {
+    const void* fn = merged ? reinterpret_cast<const void*>(&k_final<true>) : reinterpret_cast<const void*>(&k_final<false>);
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFinalLds);
     if (e != hipSuccess) return e;
-    __atomic_fetch_or(&attr_set, 1ull << dev, __ATOMIC_RELEASE);
+    __atomic_fetch_or(&attr_set[merged], 1ull << dev, __ATOMIC_RELEASE);
   }
-  k_final<<<pl.n_queries, kThreads, kFinalLds, s>>>(pl, out_score, out_doc, out_n);
+  if (merged) k_final<true><<<grid, kThreads, kFinalLds, s>>>(pl, out_score, out_doc, out_n, out_shard);
+  else k_final<false><<<grid, kThreads, kFinalLds, s>>>(pl, out_score, out_doc, out_n, nullptr);
   return hipGetLastError();
 }
 

@@ -52,7 +52,7 @@ EXPORTS = (
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
-    "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi",
+    "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -137,6 +137,7 @@ _sig("fg_index_df", C.c_uint64, _p, C.c_int, C.c_uint32)
 _sig("fg_index_bm25", C.c_int, _p, C.c_uint32, _f32p, _f32p, _f32p)
 _sig("fg_plan_create", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
 _sig("fg_plan_create_multi", C.c_int, C.POINTER(_p), C.c_uint32, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
+_sig("fg_plan_execute_merged", C.c_int, _p, _p, _p, _p, _p, _p)
 _sig("fg_plan_execute", C.c_int, _p, _p, _p, _p, _p)
 _sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
@@ -499,6 +500,11 @@ class Plan:
                 out_n: int | None = None):
         """Asynchronous launch; `stream` and outputs are raw device addresses (ints)."""
         _check(_lib.fg_plan_execute(self._h, stream, out_score, out_doc, out_n))
+
+    def execute_merged(self, stream: int | None, out_score: int, out_doc: int, out_shard: int, out_n: int):
+        """A multi-snapshot plan straight to the merged top-k per batch query
+        (device outputs [n_batch*k] x 3, [n_batch]; raw device addresses)."""
+        _check(_lib.fg_plan_execute_merged(self._h, stream, out_score, out_doc, out_shard, out_n))
 
     def results(self):
         nq, k = self.n_queries, self.k

@@ -225,6 +225,13 @@ int fg_plan_create(fg_index* ix, const fg_query_batch* q, uint32_t k, fg_plan** 
  * n_queries) are per slot, layout [n_segs][n_queries][k] and [n_segs][n_queries]:
  * the input of fg_merge_shards.  n_segs = 1 is fg_plan_create. */
 int fg_plan_create_multi(fg_index* const* ixs, uint32_t n_segs, const fg_query_batch* q, uint32_t k, fg_plan** out);
+/* Run a multi-snapshot plan straight to the merged top-k of every batch query
+ * (what fg_merge_shards makes of its per-slot lists): one final select over all
+ * slots of a query.  Device outputs [n_queries*k] x 3 and [n_queries] (batch
+ * queries); slots past d_out_n[q] hold score 0, doc 0, shard 0.  FG_EUNSUPPORTED
+ * for a single-snapshot plan or snapshots holding >= 2^32 docs together. */
+int fg_plan_execute_merged(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_out_doc, uint32_t* d_out_shard,
+                           uint32_t* d_out_n);
 /* Run a planned batch on `stream` (hipStream_t, NULL = default stream).
  * Outputs are device pointers [n_queries*k], [n_queries*k], [n_queries]; NULL
  * outputs use the plan's own buffers.  Asynchronous. */

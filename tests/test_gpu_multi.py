@@ -11,7 +11,9 @@ numpy is the reference, plus the oracle's segmented search (`or_search_seg`
 model) on a sample.  Covered: AND / OR / mixed occurs (k_conj, single-list
 k_conj, k_disj and k_scan items of several snapshots in one launch), facet
 filters (k_fmask over several snapshots' facet postings), terms a snapshot
-lacks, one query (the GET /search latency path) and 1024-query batches.
+lacks, one query (the GET /search latency path) and 1024-query batches; the
+merged select (fg_plan_execute_merged: one final select over all slots of a
+query) against the per-slot lists through fg_merge_shards.
 Bar: doc ids exact, scores within 1e-5 relative (bit-identical in practice).
 """
 import numpy as np
@@ -176,3 +178,44 @@ def test_multi_plan_errors(native, ctx, segs):
         native.link_plans([p, native.Plan(ixs[2], q_off, terms, 10)])
     with pytest.raises(native.Unsupported):
         native.Plan(ixs[:2], q_off, terms, 2000)
+
+
+@pytest.mark.parametrize("mode,k,m0,m1,nq", [(0, 100, 3, 3, 256), (1, 20, 2, 4, 256), (1, 1000, 2, 5, 64),
+                                             (0, 10, 1, 5, 256), (1, 20, 2, 3, 1)])
+def test_merged_select_equals_slot_lists_merged(native, segs, mode, k, m0, m1, nq):
+    """fg_plan_execute_merged (one final select over all slots of a query, keys
+    shifted by the snapshots' bases) == the per-slot lists through
+    fg_merge_shards, entry for entry; slots past the count are zero."""
+    import torch
+    from fugu_amd import synth
+    from fugu_amd.shard import merge_on_device
+    _, ixs, _, _ = segs
+    S = len(ixs)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev).cuda_stream
+    q_off, terms = synth.queries(nq, m0, m1, seed_q=77 + k)
+    p = native.Plan(ixs, q_off, terms, k, mode)
+    gs = torch.zeros((S, nq * k), dtype=torch.float32, device=dev)
+    gd = torch.zeros((S, nq * k), dtype=torch.int32, device=dev)
+    gn = torch.zeros((S, nq), dtype=torch.int32, device=dev)
+    p.execute(st, gs.data_ptr(), gd.data_ptr(), gn.data_ptr())
+    ms, md, msh, mn = merge_on_device(gs, gd, gn, nq, k, st)
+    os_ = torch.full((nq * k,), 7.0, dtype=torch.float32, device=dev)
+    od, osh = (torch.full((nq * k,), 7, dtype=torch.int32, device=dev) for _ in range(2))
+    on = torch.zeros(nq, dtype=torch.int32, device=dev)
+    p.execute_merged(st, os_.data_ptr(), od.data_ptr(), osh.data_ptr(), on.data_ptr())
+    torch.cuda.synchronize()
+    mn, on_h = mn.cpu().numpy(), on.cpu().numpy()
+    assert np.array_equal(mn, on_h)
+    a = [x.cpu().numpy().reshape(nq, k) for x in (ms, md, msh)]
+    b = [x.cpu().numpy().reshape(nq, k) for x in (os_, od, osh)]
+    for q in range(nq):
+        n = int(on_h[q])
+        for x, y in zip(a, b):
+            assert np.array_equal(x[q, :n], y[q, :n]), q
+            assert not y[q, n:].any(), q  # slots past the count: 0
+    assert (on_h > 0).mean() > 0.5
+    p.close()
+    with pytest.raises(native.Unsupported):  # one snapshot: nothing to merge
+        native.Plan(ixs[0], q_off, terms, k, mode).execute_merged(st, os_.data_ptr(), od.data_ptr(), osh.data_ptr(),
+                                                                  on.data_ptr())

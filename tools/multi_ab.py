@@ -3,7 +3,9 @@ on one stream, or unlinked on 8 streams) against ONE multi-snapshot plan
 (fg_plan_create_multi: one launch per kernel over all snapshots), same batch,
 identical merged hits required.  Also the single-query latency of
 fg_search_sharded (the GET /search path over a namespace's segments) in a child
-process per mode (FUGU_SHARDED_PER_SHARD=1: the round-2 path).
+process per mode: one plan with its merged select (default), one plan with
+per-slot lists + k_merge_rank (FUGU_SHARDED_NO_MERGED_FINAL=1), one linked plan
+per shard (FUGU_SHARDED_PER_SHARD=1: the round-2 path).
 
   python tools/multi_ab.py [--docs 10000000] [--units 8] [--kind seg|ns] [--steps 10]
   python tools/multi_ab.py --latency-only ...   (child: prints one JSON line)
@@ -165,7 +167,8 @@ def main():
     del ixs, whole
     # single-query latency of fg_search_sharded, one child per mode
     lat = {}
-    for label, env in (("multi", {}), ("per_shard", {"FUGU_SHARDED_PER_SHARD": "1"})):
+    for label, env in (("multi_merged_select", {}), ("multi_slot_lists_merge", {"FUGU_SHARDED_NO_MERGED_FINAL": "1"}),
+                       ("per_shard", {"FUGU_SHARDED_PER_SHARD": "1"})):
         cmd = [sys.executable, os.path.abspath(__file__), "--latency-only", "--docs", str(args.docs), "--units",
                str(args.units), "--kind", args.kind]
         r = subprocess.run(cmd, env={**os.environ, **env}, capture_output=True, text=True, timeout=600)
