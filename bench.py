@@ -283,10 +283,11 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
         p.profile(False)
     el_fan = timed_steps(step_fan, steps, warmup, torch)
     mp = native.Plan(ixs, q_off, terms, K)
+    os_, od_, osh_ = (torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32))
+    on_ = torch.empty(nq, dtype=torch.int32, device=dev)
 
-    def step():
-        mp.execute(st, gs.data_ptr(), gd.data_ptr(), gn.data_ptr())
-        merge_on_device(gs, gd, gn, nq, K, st)
+    def step():  # the merged select: the merged lists straight from k_final
+        mp.execute_merged(st, os_.data_ptr(), od_.data_ptr(), osh_.data_ptr(), on_.data_ptr())
 
     mp.profile(True)
     el = timed_steps(step, steps, warmup, torch)
@@ -313,7 +314,8 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
         ix.close()
     return {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
             "batch": nq, "k": K, "terms": 3, "mode": "AND", "namespaces": 8, "docs_per_namespace": ranges[0][1],
-            "step": "one multi-snapshot plan over the 8 namespaces (fg_plan_create_multi) + k_merge_rank",
+            "step": "one multi-snapshot plan over the 8 namespaces (fg_plan_create_multi) and its merged select "
+                    "(fg_plan_execute_merged)",
             "multi_plan_kernels_ms": [round(mk[0] / max(mkn, 1), 4), round(mk[1] / max(mkn, 1), 4)],
             "k_conj_ms_per_namespace": per_ns, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
             "ms_per_step_8_plans_8_streams": round(el_fan * 1e3 / steps, 4),
@@ -370,10 +372,12 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     del plans
     # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel)
     mp = native.Plan(ixs, q_off, terms, K, native.MODE_OR)
+    outs = tuple(torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)) + (
+        torch.empty(nq, dtype=torch.int32, device=dev),)
 
-    def step():
-        mp.execute(st, gs.data_ptr(), gd.data_ptr(), gn.data_ptr())
-        merged["out"] = merge_on_device(gs, gd, gn, nq, K, st)
+    def step():  # the merged select: the merged lists straight from k_final
+        mp.execute_merged(st, *[x.data_ptr() for x in outs])
+        merged["out"] = outs
 
     mp.profile(True)
     el = timed_steps(step, steps, warmup, torch)
@@ -381,7 +385,8 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     mms = merge_ms(gs, gd, gn, nq, K, torch)
     ent = {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
            "batch": nq, "k": K, "terms": "2-5", "mode": "OR", "n_docs": N, "zipf_s": S, "shards": 8,
-           "step": "one multi-snapshot plan over the 8 shards (fg_plan_create_multi) + k_merge_rank",
+           "step": "one multi-snapshot plan over the 8 shards (fg_plan_create_multi) and its merged select "
+                   "(fg_plan_execute_merged)",
            "multi_plan_kernels_ms": [round(mk[0] / max(mkn, 1), 4), round(mk[1] / max(mkn, 1), 4)],
            "ms_per_step_8_linked_plans": round(el_linked * 1e3 / max(2, steps // 2), 4),
            "k_disj_ms_per_shard_linked": per_shard, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
@@ -502,10 +507,18 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     st = torch.cuda.current_stream(dev)
     out = {}
 
+    merged_sel = len(plans) == 1 and len(ixs) > 1
+    mouts = [torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)] + [
+        torch.empty(nq, dtype=torch.int32, device=dev)]
+
     def step():
-        for r, p in enumerate(plans):  # plans[0] first: it zeroes the shared thresholds
-            p.execute(st.cuda_stream, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
-        ms, md, msh, mn = merge_on_device(gs, gd, gn, nq, K, st.cuda_stream)
+        if merged_sel:  # the rank's units merged by the plan's own final select
+            plans[0].execute_merged(st.cuda_stream, *[x.data_ptr() for x in mouts])
+            ms, md, msh, mn = mouts
+        else:
+            for r, p in enumerate(plans):  # plans[0] first: it zeroes the shared thresholds
+                p.execute(st.cuda_stream, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+            ms, md, msh, mn = merge_on_device(gs, gd, gn, nq, K, st.cuda_stream)
         # slots past a query's count hold no hit (undefined shard / doc): clamp the
         # gather index so it stays inside off_u; those slots are never read
         gdoc = (md.to(torch.int64) + off_u[msh.to(torch.int64).clamp_(0, len(mine) - 1)]).to(torch.int32)
@@ -562,8 +575,8 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
                            (" + RCCL all-gather top-k" if backend == "nccl" else f" + {backend} all-gather (rehearsal)")
                            if world > 1 else "")},
             "kernels_ms_per_step_max_rank": {kname: round(kern, 4), "k_final": round(fin, 4)},
-            "rank_plan": ("one multi-snapshot plan over the rank's units" if len(plans) == 1 and len(ixs) > 1
-                          else f"{len(plans)} linked plan(s)"),
+            "rank_plan": ("one multi-snapshot plan over the rank's units, merged by its final select"
+                          if merged_sel else f"{len(plans)} linked plan(s) + k_merge_rank"),
             "result_sha1": h.hexdigest()[:16],
             "hits": int(mn.sum()),
             "snapshot_build_s_rank0": round(build_s, 1),

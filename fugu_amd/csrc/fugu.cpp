@@ -2601,10 +2601,16 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     }
     plans[g].reset(p);
     if (trace) t_plan += now() - t_p;
-    // every shard on dev0 in one plan: its merged select writes the merged
-    // lists directly (no per-shard lists, no k_merge_rank)
-    static const bool no_merged = getenv("FUGU_SHARDED_NO_MERGED_FINAL") != nullptr;
-    if (ng == 1 && gdev[0] == dev0 && S > 1 && p->d.seg_base && !no_merged) {
+    // every shard on dev0 in one plan, a batch: its merged select writes the
+    // merged lists directly (no per-shard lists, no k_merge_rank); a small batch
+    // keeps one final select per shard (more workgroups in parallel: a single
+    // query over 8 segments 0.070 vs 0.077 ms p50).  FUGU_SHARDED_MERGED_MIN:
+    // the smallest batch that takes the merged select (A/B)
+    static const uint32_t merged_min = [] {
+      const char* e = getenv("FUGU_SHARDED_MERGED_MIN");
+      return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 256u;
+    }();
+    if (ng == 1 && gdev[0] == dev0 && S > 1 && p->d.seg_base && nq >= merged_min) {
       if (int rc = execute_impl(p, hipStreamPerThread, ms, md, mn, msh)) return rc;
       merged = true;
       break;

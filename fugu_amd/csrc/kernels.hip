@@ -1507,50 +1507,72 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         exact[j] = true;
       }
       constexpr uint32_t kAbsent = 0xBF800000u;  // -1.0f: the clause is not on the doc
-      for (uint32_t i = 0; i < m; ++i) {
-        const uint32_t meta = sh.c_meta[i];
-        const uint32_t slot = meta_slot(meta);
-        const bool rank = slot && meta_rank(meta);
-        uint32_t y[J];
-        uint32_t need = 0;
+      // G clauses per step (FG_DISJ_G): their rank-word / table / bucket loads of
+      // all J postings in flight together, then their posting-score loads
+      constexpr uint32_t G = FG_DISJ_G;
+      for (uint32_t i0 = 0; i0 < m; i0 += G) {
+        uint32_t y[G][J];
+        uint32_t need = 0;  // bit g * J + j
         {
-          uint64_t x[J];
+          uint64_t x[G][J];
 #pragma unroll
-          for (uint32_t j = 0; j < J; ++j) {
-            x[j] = kAbsent;
-            if (pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
-              need |= 1u << j;
-              if (rank) x[j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
-              else if (slot) x[j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
-              else x[j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
+          for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t i = i0 + g;
+            const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
+            const uint32_t slot = meta_slot(meta);
+            const bool rank = slot && meta_rank(meta);
+#pragma unroll
+            for (uint32_t j = 0; j < J; ++j) {
+              x[g][j] = kAbsent;
+              if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
+                need |= 1u << (g * J + j);
+                if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
+                else if (slot) x[g][j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
+                else x[g][j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
+              }
             }
           }
 #pragma unroll
-          for (uint32_t j = 0; j < J; ++j) {
-            const uint32_t bits = (uint32_t)x[j], bt = pd[j] & 31u;
-            if (!rank || !((need >> j) & 1u)) y[j] = (uint32_t)x[j];
-            else y[j] = ((bits >> bt) & 1u) ? (uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))
-                                            : kAbsent;
+          for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t meta = i0 + g < m ? sh.c_meta[i0 + g] : 0u;
+            const bool rank = meta_slot(meta) && meta_rank(meta);
+#pragma unroll
+            for (uint32_t j = 0; j < J; ++j) {
+              const uint32_t bits = (uint32_t)x[g][j], bt = pd[j] & 31u;
+              if (!rank || !((need >> (g * J + j)) & 1u)) y[g][j] = (uint32_t)x[g][j];
+              else y[g][j] = ((bits >> bt) & 1u) ? (uint32_t)(x[g][j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))
+                                                 : kAbsent;
+            }
           }
         }
-        if (rank) {
-          const float* __restrict__ sp = ix.psc + sh.c_base[i];
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+          const uint32_t meta = i0 + g < m ? sh.c_meta[i0 + g] : 0u;
+          if (!(meta_slot(meta) && meta_rank(meta))) continue;
+          const float* __restrict__ sp = ix.psc + sh.c_base[i0 + g];
 #pragma unroll
           for (uint32_t j = 0; j < J; ++j)
-            if (((need >> j) & 1u) && y[j] < 0x80000000u) y[j] = __float_as_uint(sp[y[j]]);
+            if (((need >> (g * J + j)) & 1u) && y[g][j] < 0x80000000u) y[g][j] = __float_as_uint(sp[y[g][j]]);
         }
+        // the clause-order sum (the own clause: the streamed posting's score)
 #pragma unroll
-        for (uint32_t j = 0; j < J; ++j) {
-          if (!pk[j]) continue;
-          float b = ps[j];
-          if (i != pcl[j]) {
-            if (!((need >> j) & 1u)) continue;
-            b = __uint_as_float(y[j]);
-            exact[j] = exact[j] && slot != 0;
-            if (signbit(b)) continue;  // clause i cannot match d
-            maybe[j] |= 1u << i;
+        for (uint32_t g = 0; g < G; ++g) {
+          const uint32_t i = i0 + g;
+          if (i >= m) break;
+          const uint32_t slot = meta_slot(sh.c_meta[i]);
+#pragma unroll
+          for (uint32_t j = 0; j < J; ++j) {
+            if (!pk[j]) continue;
+            float b = ps[j];
+            if (i != pcl[j]) {
+              if (!((need >> (g * J + j)) & 1u)) continue;
+              b = __uint_as_float(y[g][j]);
+              exact[j] = exact[j] && slot != 0;
+              if (signbit(b)) continue;  // clause i cannot match d
+              maybe[j] |= 1u << i;
+            }
+            sum[j] += b;
           }
-          sum[j] += b;
         }
       }
 #pragma unroll

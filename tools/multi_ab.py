@@ -3,9 +3,9 @@ on one stream, or unlinked on 8 streams) against ONE multi-snapshot plan
 (fg_plan_create_multi: one launch per kernel over all snapshots), same batch,
 identical merged hits required.  Also the single-query latency of
 fg_search_sharded (the GET /search path over a namespace's segments) in a child
-process per mode: one plan with its merged select (default), one plan with
-per-slot lists + k_merge_rank (FUGU_SHARDED_NO_MERGED_FINAL=1), one linked plan
-per shard (FUGU_SHARDED_PER_SHARD=1: the round-2 path).
+process per mode: one plan with per-slot lists + k_merge_rank (the default for
+a small batch), one plan with its merged select (FUGU_SHARDED_MERGED_MIN=1), one
+linked plan per shard (FUGU_SHARDED_PER_SHARD=1: the round-2 path).
 
   python tools/multi_ab.py [--docs 10000000] [--units 8] [--kind seg|ns] [--steps 10]
   python tools/multi_ab.py --latency-only ...   (child: prints one JSON line)
@@ -140,6 +140,26 @@ def main():
         ent["multi_kernel_ms"] = [round(kms[0] / max(kn, 1), 4), round(kms[1] / max(kn, 1), 4)]
         ent["multi_sha"] = digest(*out["m"], nq, K)
         ent["same_hits"] = ent["multi_sha"] == ent["linked_sha"]
+        # (b2) the same plan through its merged select (no per-slot lists, no k_merge_rank)
+        mo = [torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)] + [
+            torch.empty(nq, dtype=torch.int32, device=dev)]
+
+        def step_merged():
+            mp.execute_merged(st, *[x.data_ptr() for x in mo])
+            out["m"] = tuple(mo)
+
+        for _ in range(2):
+            step_merged()
+        mp.kernel_ms()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_merged()
+        torch.cuda.synchronize()
+        ent["merged_select_ms"] = round((time.perf_counter() - t0) * 1e3 / args.steps, 4)
+        kms, kn = mp.kernel_ms()
+        ent["merged_select_kernel_ms"] = [round(kms[0] / max(kn, 1), 4), round(kms[1] / max(kn, 1), 4)]
+        ent["merged_select_same_hits"] = digest(*out["m"], nq, K) == ent["linked_sha"]
         del mp
         # (c) the corpus as one snapshot, same batch (what the segmentation costs)
         if whole is not None:
@@ -167,7 +187,7 @@ def main():
     del ixs, whole
     # single-query latency of fg_search_sharded, one child per mode
     lat = {}
-    for label, env in (("multi_merged_select", {}), ("multi_slot_lists_merge", {"FUGU_SHARDED_NO_MERGED_FINAL": "1"}),
+    for label, env in (("multi_slot_lists_merge", {}), ("multi_merged_select", {"FUGU_SHARDED_MERGED_MIN": "1"}),
                        ("per_shard", {"FUGU_SHARDED_PER_SHARD": "1"})):
         cmd = [sys.executable, os.path.abspath(__file__), "--latency-only", "--docs", str(args.docs), "--units",
                str(args.units), "--kind", args.kind]
