@@ -97,6 +97,9 @@ constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
 #define FG_DISJ_QUEUE 1  // k_disj: bound 2 deferred through an LDS queue of the postings past bound 1
                          // (ab_disj_queue_k*.log: OR top-20 3.92 -> 3.23 ms, top-1000 6.13 -> 5.94 ms)
 #endif
+#ifndef FG_DISJ_QPF
+#define FG_DISJ_QPF 0  // A/B: 1 = the queued k_disj loads the next pass's postings before this pass's bound 1
+#endif
 #ifndef FG_DISJ_HBITS
 #define FG_DISJ_HBITS (FG_DISJ_QUEUE ? 9 : 10)  // the queue's LDS comes out of the select's digit width
 #endif

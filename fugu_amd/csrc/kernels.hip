@@ -1412,10 +1412,42 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   const uint32_t dbase = tile0 << kTileShift;
   if (tid == 0) sh.n_q = 0;
   __syncthreads();
+#if FG_DISJ_QPF
+  // the next pass's postings are loaded before this pass's bound 1, so they are
+  // in flight through its queue append and any flush (bound 2) that follows
+  uint32_t npd[J], npcl[J];
+  float nps[J];
+  auto load_pass = [&](uint32_t e1) {
+#pragma unroll
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t e = e1 + j * kThreads + tid;
+      npd[j] = dbase;
+      npcl[j] = 0;
+      nps[j] = 0.0f;
+      if (e < n_post) {
+        uint32_t t;
+        const uint64_t at = locate(e, t, npcl[j]);
+        npd[j] = ix.doc[at];
+        nps[j] = ix.psc[at];
+      }
+    }
+  };
+  load_pass(0);
+#endif
   for (uint32_t e0 = 0; e0 < n_post; e0 += kRound) {
     uint32_t pd[J], pcl[J];
     float ps[J];
     bool pk[J];
+#if FG_DISJ_QPF
+#pragma unroll
+    for (uint32_t j = 0; j < J; ++j) {
+      pk[j] = e0 + j * kThreads + tid < n_post;
+      pd[j] = npd[j];
+      pcl[j] = npcl[j];
+      ps[j] = nps[j];
+    }
+    if (e0 + kRound < n_post) load_pass(e0 + kRound);
+#else
 #pragma unroll
     for (uint32_t j = 0; j < J; ++j) {
       const uint32_t e = e0 + j * kThreads + tid;
@@ -1430,6 +1462,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         ps[j] = ix.psc[at];
       }
     }
+#endif
     // with this pass's posting loads in flight: the last exchange's reply
     if (tid == 0 && pend > sh.thr) sh.thr = pend;
     __syncthreads();
