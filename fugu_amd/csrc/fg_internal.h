@@ -98,7 +98,8 @@ constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
                          // (ab_disj_queue_k*.log: OR top-20 3.92 -> 3.23 ms, top-1000 6.13 -> 5.94 ms)
 #endif
 #ifndef FG_DISJ_QPF
-#define FG_DISJ_QPF 0  // A/B: 1 = the queued k_disj loads the next pass's postings before this pass's bound 1
+#define FG_DISJ_QPF 1  // the queued k_disj loads the next pass's postings before this pass's bound 1
+                       // (ab_disj_qpf_k*.log: OR top-20 3.21 -> 3.15 ms, top-1000 5.94 -> 5.85 ms)
 #endif
 #ifndef FG_DISJ_HBITS
 #define FG_DISJ_HBITS (FG_DISJ_QUEUE ? 9 : 10)  // the queue's LDS comes out of the select's digit width
@@ -121,6 +122,10 @@ constexpr uint32_t kDisjMaxPairs = 256;  // ... and at most this many (tile, Sho
 #define FG_DISJ_ITEM_POSTINGS 1000000000u  // A/B: cap on a k_disj item's postings (all its clauses, mean density)
 #endif
 constexpr uint32_t kDisjItemPostings = FG_DISJ_ITEM_POSTINGS;
+#ifndef FG_DISJ_HEAVY
+#define FG_DISJ_HEAVY 0  // A/B: items of queries with more postings per item than this run first (0: sweep order)
+#endif
+constexpr uint32_t kDisjHeavy = FG_DISJ_HEAVY;
 #ifndef FG_EXHMIN
 #define FG_EXHMIN 1024
 #endif

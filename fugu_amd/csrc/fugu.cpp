@@ -1687,10 +1687,13 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
                                             std::max<uint32_t>(1, (nt + gpq - 1) / gpq));
       const uint32_t ng = (nt + G - 1) / G;
       ngroup[i] = ng;
+      // FG_DISJ_HEAVY > 0 (A/B): the items of queries whose items hold more than
+      // that many postings (mean density) run first, in their own sweep order
+      const bool heavy = fg::kDisjHeavy > 0 && per_tile * G > (double)fg::kDisjHeavy;
       for (uint32_t g = 0; g < ng; ++g) {
         const uint32_t t0 = tlo + g * G, n = std::min(G, nt - g * G);
         const double mid = ((double)t0 + 0.5 * n) * (double)(1u << fg::kDisjTileShift) / (double)ix->n_docs;
-        ditems.push_back(W{mid, i, t0, n});
+        ditems.push_back(W{fg::kDisjHeavy > 0 ? (heavy ? 0.05 * mid : 0.05 + 0.95 * mid) : mid, i, t0, n});
       }
       if (ditems.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", ditems.size());
       continue;
