@@ -55,6 +55,10 @@ constexpr uint32_t kRankChunkWords = 2048;  // k_rank: words (65536 docs) per wo
 #define FG_DISJ_GPQ 64
 #endif
 constexpr uint32_t kGroupsPerQuery = FG_DISJ_GPQ;  // k_disj / k_scan: a query's doc tiles in ~this many work items
+#ifndef FG_DISJ_SPREAD
+#define FG_DISJ_SPREAD 16
+#endif
+constexpr uint32_t kDisjSmallSpread = FG_DISJ_SPREAD;  // ... times up to this for a small batch (batch of one: x16)
 #ifndef FG_GPQ
 #define FG_GPQ 16  // tools/ab_variants.py (ab_group*.log): 64 -> 16 with FG_MAXGROUP 16 -> 8: k_conj 1.08 -> 1.00 ms
 #endif

@@ -1578,7 +1578,12 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   // query Must-driven when it has a Must clause (RequiredOptionalScorer over
   // its Shoulds), a union of its Shoulds otherwise; MustNot clauses exclude.
   using W = WItem;
-  const uint32_t gpq = std::max<uint32_t>(1, fg::kGroupsPerQuery / n_segs);  // k_disj / k_scan groups per query
+  // k_disj / k_scan groups per query, spread over the plan's snapshots; a small
+  // batch (the batch-of-one latency: the GPU holds nothing else) splits each
+  // query over up to 16x more, shorter items that run side by side
+  const uint32_t gpq_batch =
+      fg::kGroupsPerQuery * std::min<uint32_t>(fg::kDisjSmallSpread, std::max<uint32_t>(1, 256 / std::max(nq, 1u)));
+  const uint32_t gpq = std::max<uint32_t>(1, gpq_batch / n_segs);
   auto &citems = h.citems, &ditems = h.ditems, &scan = h.scan;
   auto &ngroup = h.ngroup, &q_hlo = h.q_hlo, &q_hhi = h.q_hhi, &q_hsh = h.q_hsh;
   ngroup.assign(nq, 0);
