@@ -101,9 +101,6 @@ constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
 #define FG_DISJ_QUEUE 1  // k_disj: bound 2 deferred through an LDS queue of the postings past bound 1
                          // (ab_disj_queue_k*.log: OR top-20 3.92 -> 3.23 ms, top-1000 6.13 -> 5.94 ms)
 #endif
-#ifndef FG_DISJ_HPRE
-#define FG_DISJ_HPRE 0  // A/B: 1 = k_disj loads the query's histogram bins before its range gathers
-#endif
 #ifndef FG_DISJ_QPF
 #define FG_DISJ_QPF 1  // the queued k_disj loads the next pass's postings before this pass's bound 1
                        // (ab_disj_qpf_k*.log: OR top-20 3.21 -> 3.15 ms, top-1000 5.94 -> 5.85 ms)

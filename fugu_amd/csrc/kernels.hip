@@ -141,19 +141,12 @@ __device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* scratch /*
 // the highest bin b with >= K counted docs in bins >= b (score-only key), or 0.
 // Relaxed agent-scope loads (sc1): the bins only grow, so a stale bin can only
 // lower the threshold.  Workgroup-uniform result; scratch[0..6] used.
-// In two halves: hist_load issues this thread's two bin loads, so a caller can
-// keep them in flight while it does other work; hist_threshold_of folds them.
-struct HistBins { uint32_t v0, v1; };
-__device__ inline HistBins hist_load(const uint32_t* gh) {
+__device__ uint64_t hist_threshold(const uint32_t* gh, uint32_t K, uint32_t lo, uint32_t sh, uint32_t* scratch) {
   static_assert(kQBins == 2 * kThreads, "two bins per thread");
-  const uint32_t b0 = kQBins - 1 - 2 * threadIdx.x, b1 = b0 - 1;  // descending
-  return HistBins{__hip_atomic_load(gh + b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                  __hip_atomic_load(gh + b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
-}
-__device__ uint64_t hist_threshold_of(HistBins hb, uint32_t K, uint32_t lo, uint32_t sh, uint32_t* scratch) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t b0 = kQBins - 1 - 2 * tid, b1 = b0 - 1;
-  const uint32_t v0 = hb.v0, v1 = hb.v1;
+  const uint32_t b0 = kQBins - 1 - 2 * tid, b1 = b0 - 1;  // descending
+  const uint32_t v0 = __hip_atomic_load(gh + b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t v1 = __hip_atomic_load(gh + b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid == 0) scratch[5] = kQBins;
   const uint32_t before = block_exclusive_scan(v0 + v1, scratch);
   if (before < K && before + v0 >= K) scratch[5] = b0;
@@ -162,9 +155,6 @@ __device__ uint64_t hist_threshold_of(HistBins hb, uint32_t K, uint32_t lo, uint
   const uint32_t b = scratch[5];
   __syncthreads();
   return b < kQBins ? (uint64_t)(lo + (b << sh)) << 32 : 0ull;
-}
-__device__ uint64_t hist_threshold(const uint32_t* gh, uint32_t K, uint32_t lo, uint32_t sh, uint32_t* scratch) {
-  return hist_threshold_of(hist_load(gh), K, lo, sh, scratch);
 }
 
 // Add the LDS bins to the query's global histogram and clear them.
@@ -1155,10 +1145,6 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     sh.max_s = ms;
   }
 
-  // the query's bins load while the R phase gathers its ranges (FG_DISJ_HPRE)
-#if FG_DISJ_HPRE
-  const HistBins hb = FG_DISJ_HIST ? hist_load(hq.gh) : HistBins{0, 0};
-#endif
   // ---- R: ranges and bounds of every (tile, clause) pair, one thread per pair
   const uint32_t npair = ntile * m;
   for (uint32_t p = tid; p < npair; p += kThreads) {
@@ -1227,11 +1213,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   }
   {
     // the query's running threshold (every work item's counted hits so far)
-#if FG_DISJ_HPRE
-    const uint64_t H = FG_DISJ_HIST ? hist_threshold_of(hb, K, hq.lo, hq.sh, sh.scratch) : 0ull;
-#else
     const uint64_t H = FG_DISJ_HIST ? hist_threshold(hq.gh, K, hq.lo, hq.sh, sh.scratch) : 0ull;
-#endif
     if (tid == 0 && H > sh.thr) sh.thr = H;
   }
   __syncthreads();
