@@ -219,3 +219,26 @@ def test_merged_select_equals_slot_lists_merged(native, segs, mode, k, m0, m1, n
     with pytest.raises(native.Unsupported):  # one snapshot: nothing to merge
         native.Plan(ixs[0], q_off, terms, k, mode).execute_merged(st, os_.data_ptr(), od.data_ptr(), osh.data_ptr(),
                                                                   on.data_ptr())
+
+
+def test_many_small_segments(native, ctx):
+    """17 small segments (a namespace between host merges, FG_MAX_SEGMENTS = 64):
+    one multi-snapshot plan through fg_search_sharded, batch (merged select) and
+    single queries (per-slot lists + k_merge_rank), against the per-segment merge."""
+    from fugu_amd import synth
+    c = synth.corpus(170_000)
+    V = synth.VOCAB
+    cuts = [i * 10_000 for i in range(18)]
+    parts = [(c.off[b:e + 1] - c.off[b], c.tok[c.off[b]:c.off[e]]) for b, e in zip(cuts[:-1], cuts[1:])]
+    g = None
+    for off, tok in parts:
+        x = native.docs_stats(off, tok, V)
+        g = x if g is None else g + x
+    ixs = [native.Index.from_docs(ctx, off, tok, V, global_stats=g, keep_host=False) for off, tok in parts]
+    for mode, k, nq in ((0, 100, 512), (1, 20, 512), (1, 10, 1), (0, 1000, 256)):
+        q_off, terms = synth.queries(nq, 1 if mode == 0 else 2, 4, seed_q=5 + k + nq)
+        _, want = per_segment_merged(ixs, q_off, terms, k, mode)
+        got = native.search_sharded(ixs, q_off, terms, k, mode=mode, ctx=ctx)
+        assert_merged(got, want, (mode, k, nq))
+    for ix in ixs:
+        ix.close()
