@@ -612,6 +612,8 @@ def main():
                          "1 -> 697K, 2 -> 816K, 4 -> 934K, 8 -> 868K q/s)")
     ap.add_argument("--disj", action="store_true",
                     help="headline batch = 2-5-term OR (k_disj; profiling runs, pass --k 1000 --no-cpu)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: gather + merge each step after its batch instead of behind the next batch")
     ap.add_argument("--config", choices=["headline", "c4", "c5"], default="headline",
                     help="c4 / c5: BASELINE configs[3] / [4] split over the job's GPUs (strong scaling)")
     args = ap.parse_args()
@@ -671,12 +673,42 @@ def main():
     out_n = torch.empty(nq, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    merged = {}  # N > 1: the last step's merged lists (result_sha1)
+
     def step():
         plan.execute(stream.cuda_stream, out_s.data_ptr(), out_d.data_ptr(), out_n.data_ptr())
         if world > 1:
             from fugu_amd.shard import gather_packed, merge_on_device
             s, d, c = gather_packed(out_s, out_d, out_n)
-            merge_on_device(s, d, c, nq, K, stream.cuda_stream)
+            merged["m"] = merge_on_device(s, d, c, nq, K, stream.cuda_stream)
+
+    if world > 1 and not args.no_overlap:
+        # N > 1: a step's all-gather + merge run on a side stream while the next
+        # step's batch runs (two output buffers in turn; a buffer is reused only
+        # after its gather has read it), so the collective hides behind the kernels
+        from fugu_amd.shard import gather_packed, merge_on_device
+        side = torch.cuda.Stream(dev)
+        bufs = [(torch.empty(nq * K, dtype=torch.float32, device=dev), torch.empty(nq * K, dtype=torch.int32, device=dev),
+                 torch.empty(nq, dtype=torch.int32, device=dev)) for _ in range(2)]
+        gathered = [None, None]
+        turn = [0]
+
+        def step():  # noqa: F811
+            b = turn[0] % 2
+            turn[0] += 1
+            s_, d_, n_ = bufs[b]
+            if gathered[b] is not None:
+                stream.wait_event(gathered[b])
+            plan.execute(stream.cuda_stream, s_.data_ptr(), d_.data_ptr(), n_.data_ptr())
+            ran = torch.cuda.Event()
+            ran.record(stream)
+            side.wait_event(ran)
+            with torch.cuda.stream(side):
+                s, d, c = gather_packed(s_, d_, n_)
+                merged["m"] = merge_on_device(s, d, c, nq, K, side.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                gathered[b] = ev
 
     for _ in range(args.warmup):
         step()
@@ -700,6 +732,15 @@ def main():
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
     total_queries = nq * world * args.steps
+    result_sha1 = None
+    if world > 1 and "m" in merged:  # the merged lists of the last step (equal with and without --no-overlap)
+        import hashlib
+        ms_, md_, msh_, mn_ = (x.cpu().numpy() for x in merged["m"])
+        h = hashlib.sha1()
+        for i in range(nq):
+            m = int(mn_[i])
+            h.update(ms_[i * K:i * K + m].tobytes() + md_[i * K:i * K + m].tobytes() + msh_[i * K:i * K + m].tobytes())
+        result_sha1 = h.hexdigest()[:16]
     qps = total_queries / elapsed
 
     # ---- p50 latency at batch = 1 (host query in, host hits out: plan + PCIe + kernels)
@@ -921,10 +962,11 @@ def main():
                 "terms": wl_terms, "namespaces": world,
                 "parallelism": f"namespace-shard x{world}" + (
                     (" + RCCL all-gather top-k" if backend == "nccl" else f" + {backend} all-gather top-k (rehearsal)")
-                    if world > 1 else ""),
+                    + ("" if args.no_overlap else ", overlapped with the next batch") if world > 1 else ""),
             },
             "p50_ms": round(p50_ms, 4) if p50_ms is not None else None,
             "latency_ms": tail_ms,  # batch-of-one p90 / p99 beside p50 (same sample)
+            **({"result_sha1": result_sha1} if result_sha1 else {}),
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
