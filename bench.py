@@ -612,8 +612,9 @@ def main():
                          "1 -> 697K, 2 -> 816K, 4 -> 934K, 8 -> 868K q/s)")
     ap.add_argument("--disj", action="store_true",
                     help="headline batch = 2-5-term OR (k_disj; profiling runs, pass --k 1000 --no-cpu)")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="N > 1: gather + merge each step after its batch instead of behind the next batch")
+    ap.add_argument("--overlap", action="store_true",
+                    help="N > 1: each step's gather + merge on a side stream behind the next batch (opt-in: a gloo "
+                         "rehearsal on one GPU measured it slower, RCCL unmeasured)")
     ap.add_argument("--config", choices=["headline", "c4", "c5"], default="headline",
                     help="c4 / c5: BASELINE configs[3] / [4] split over the job's GPUs (strong scaling)")
     args = ap.parse_args()
@@ -682,7 +683,7 @@ def main():
             s, d, c = gather_packed(out_s, out_d, out_n)
             merged["m"] = merge_on_device(s, d, c, nq, K, stream.cuda_stream)
 
-    if world > 1 and not args.no_overlap:
+    if world > 1 and args.overlap:
         # N > 1: a step's all-gather + merge run on a side stream while the next
         # step's batch runs (two output buffers in turn; a buffer is reused only
         # after its gather has read it), so the collective hides behind the kernels
@@ -733,7 +734,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total_queries = nq * world * args.steps
     result_sha1 = None
-    if world > 1 and "m" in merged:  # the merged lists of the last step (equal with and without --no-overlap)
+    if world > 1 and "m" in merged:  # the merged lists of the last step (equal with and without --overlap)
         import hashlib
         ms_, md_, msh_, mn_ = (x.cpu().numpy() for x in merged["m"])
         h = hashlib.sha1()
@@ -962,7 +963,7 @@ def main():
                 "terms": wl_terms, "namespaces": world,
                 "parallelism": f"namespace-shard x{world}" + (
                     (" + RCCL all-gather top-k" if backend == "nccl" else f" + {backend} all-gather top-k (rehearsal)")
-                    + ("" if args.no_overlap else ", overlapped with the next batch") if world > 1 else ""),
+                    + (", overlapped with the next batch" if args.overlap else "") if world > 1 else ""),
             },
             "p50_ms": round(p50_ms, 4) if p50_ms is not None else None,
             "latency_ms": tail_ms,  # batch-of-one p90 / p99 beside p50 (same sample)
