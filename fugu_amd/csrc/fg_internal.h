@@ -346,8 +346,17 @@ struct ScoreJob {
   float* cmax;                // [score chunks] out: the largest score of each k_score chunk
   const uint32_t* ch_term;    // chunk tables
   const uint32_t* ch_first;
-  const uint32_t* kt_terms;   // k_ktop: terms with postings
+  const uint32_t* kt_terms;   // k_ktop: terms with 1..kKtopChunk postings
+  // terms with more postings: k_ktop_part per chunk, then k_ktop_big per term
+  const uint32_t* kb_terms;   // [n_big] the long terms
+  const uint32_t* kb_chunk0;  // [n_big + 1] first chunk of each
+  const uint32_t* kc_big;     // [n_chunks] long-term index of each chunk
+  const uint32_t* kc_start;   // [n_chunks] first posting of each chunk within its term's list
+  uint64_t* kc_keys;          // [n_chunks * kTopKs[last]] each chunk's best keys
+  uint32_t* kc_cnt;           // [n_chunks]
+  uint32_t* kb_stat;          // [n_big * 3] alive postings, min / max alive score bits (0, ~0, 0 first)
 };
+constexpr uint32_t kKtopChunk = 32768;  // postings per k_ktop_part workgroup (and k_ktop's largest term)
 
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
@@ -362,7 +371,7 @@ hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uin
                        uint32_t n_words, uint64_t* out, hipStream_t s);
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);
-hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, hipStream_t s);
+hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

@@ -587,8 +587,61 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.ch_term = ix->d_bk_term;
   j.ch_first = ix->d_bk_first;
   HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, nullptr));
-  j.kt_terms = ix->d_kt_terms;
-  HIPCHK(fg::launch_ktop(j, ix->n_kt, nullptr));
+  // k_ktop: terms of <= kKtopChunk postings one workgroup each; longer terms in
+  // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
+  // chunks' best keys (k_ktop_big).  The chunk tables and key scratch are
+  // temporary (freed below, after the sync).
+  std::vector<uint32_t> kt_small, kb_terms, kb_chunk0, kc_big, kc_start;
+  for (uint32_t t = 0; t < V; ++t) {
+    const uint64_t df = ix->off[t + 1] - ix->off[t];
+    if (df == 0) continue;
+    if (df <= fg::kKtopChunk) {
+      kt_small.push_back(t);
+      continue;
+    }
+    kb_chunk0.push_back((uint32_t)kc_big.size());
+    for (uint64_t st = 0; st < df; st += fg::kKtopChunk) {
+      kc_big.push_back((uint32_t)kb_terms.size());
+      kc_start.push_back((uint32_t)st);
+    }
+    kb_terms.push_back(t);
+  }
+  kb_chunk0.push_back((uint32_t)kc_big.size());
+  const size_t n_small = kt_small.size(), n_big = kb_terms.size(), n_chunks = kc_big.size();
+  std::vector<void*> ktmp;
+  struct KtmpBack {
+    std::vector<void*>& v;
+    ~KtmpBack() {
+      (void)hipStreamSynchronize(nullptr);
+      for (void* x : v) (void)hipFree(x);
+    }
+  } ktmp_back{ktmp};
+  auto tmp_upload = [&](const void* src, size_t n_bytes, void** out) -> int {
+    void* q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(n_bytes, 16)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", n_bytes);
+    ktmp.push_back(q);
+    if (src && n_bytes) HIPCHK(hipMemcpy(q, src, n_bytes, hipMemcpyHostToDevice));
+    *out = q;
+    return FG_OK;
+  };
+  void *d_ks, *d_kbt, *d_kb0, *d_kcb, *d_kcs, *d_kck, *d_kcc, *d_kbs;
+  std::vector<uint32_t> kb_stat(3 * n_big, 0);
+  for (size_t x = 0; x < n_big; ++x) kb_stat[3 * x + 1] = 0xFFFFFFFFu;
+  if ((rc = tmp_upload(kt_small.data(), 4 * n_small, &d_ks)) || (rc = tmp_upload(kb_terms.data(), 4 * n_big, &d_kbt)) ||
+      (rc = tmp_upload(kb_chunk0.data(), 4 * (n_big + 1), &d_kb0)) ||
+      (rc = tmp_upload(kc_big.data(), 4 * n_chunks, &d_kcb)) || (rc = tmp_upload(kc_start.data(), 4 * n_chunks, &d_kcs)) ||
+      (rc = tmp_upload(nullptr, 8ull * n_chunks * fg::kTopKs[fg::kNumTopK - 1], &d_kck)) ||
+      (rc = tmp_upload(nullptr, 4 * n_chunks, &d_kcc)) || (rc = tmp_upload(kb_stat.data(), 4 * kb_stat.size(), &d_kbs)))
+    return rc;
+  j.kt_terms = static_cast<const uint32_t*>(d_ks);
+  j.kb_terms = static_cast<const uint32_t*>(d_kbt);
+  j.kb_chunk0 = static_cast<const uint32_t*>(d_kb0);
+  j.kc_big = static_cast<const uint32_t*>(d_kcb);
+  j.kc_start = static_cast<const uint32_t*>(d_kcs);
+  j.kc_keys = static_cast<uint64_t*>(d_kck);
+  j.kc_cnt = static_cast<uint32_t*>(d_kcc);
+  j.kb_stat = static_cast<uint32_t*>(d_kbs);
+  HIPCHK(fg::launch_ktop(j, (uint32_t)n_small, (uint32_t)n_chunks, (uint32_t)n_big, nullptr));
   HIPCHK(hipStreamSynchronize(nullptr));
   ix->tmaxs.resize(V);
   ix->ktop.resize((size_t)V * fg::kNumTopK);
@@ -1423,6 +1476,14 @@ uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term) {
   if (field == FG_FIELD_TEXT) return ix->df_text[term];
   if (field == FG_FIELD_NAME) return ix->df_name[term];
   return ix->off[term + 1] - ix->off[term];
+}
+
+int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out) {
+  if (!ix || !out) return fail(FG_EINVAL, "bad arguments");
+  static_assert(fg::kNumTopK == 5, "fugu.h documents five K");
+  for (uint32_t k = 0; k < fg::kNumTopK; ++k)
+    out[k] = term < ix->n_terms ? ix->ktop[(size_t)term * fg::kNumTopK + k] : 0.0f;
+  return FG_OK;
 }
 
 int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512) {

@@ -2664,44 +2664,89 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
 // Per term the K-th best score over its ALIVE postings for K in kTopKs (0 when
 // fewer): a doc among a term's top K scores at least that much in any
 // disjunction containing the term, so the query's K-th best is >= it (k_disj's
-// starting threshold).  One workgroup per term with postings; exact select
-// over unique (score, doc) keys.
-__global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
-  constexpr uint32_t KM = kTopKs[kNumTopK - 1];  // the largest K: its keys are kept in LDS
-  __shared__ uint32_t hist[kHistBins];
-  __shared__ uint32_t scratch[8];
-  __shared__ uint32_t red[2];  // alive postings, smallest alive score (bits)
-  __shared__ uint64_t top[KM];
-  __shared__ uint32_t n_top;
-  const uint32_t t = j.kt_terms[blockIdx.x];
-  const uint64_t b = j.off[t];
-  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
-  auto alive = [&](uint32_t d) { return !j.alive || ((j.alive[d >> 5] >> (d & 31u)) & 1u); };
-  // every posting as (valid && alive, key), U loads per thread in flight, the
-  // workgroup converged (callers may use wave-wide operations)
-  auto each_posting = [&](auto&& f) {
-    constexpr uint32_t U = 4;
-    for (uint32_t p0 = 0; p0 < n; p0 += U * kThreads) {
-      uint32_t d[U];
-      float s[U];
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t p = p0 + u * kThreads + threadIdx.x;
-        d[u] = p < n ? j.doc[b + p] : 0xFFFFFFFFu;
-        s[u] = p < n ? j.psc[b + p] : 0.0f;
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u) f(d[u] != 0xFFFFFFFFu && alive(d[u]), s[u], d[u]);
+// starting threshold).  Exact selects over unique (score, doc) keys.  A term of
+// <= kKtopChunk postings: one workgroup (k_ktop).  A longer one is cut into
+// kKtopChunk-posting chunks, one workgroup each (k_ktop_part: the chunk's
+// alive count / extremes and its KM best keys), then one workgroup per such
+// term selects over its chunks' keys (k_ktop_big): a 9M-posting term no longer
+// streams its list through one workgroup several times.
+constexpr uint32_t kKtopKM = kTopKs[kNumTopK - 1];  // the largest K: its keys are kept
+
+struct KtopShared {
+  uint32_t hist[kHistBins];
+  uint32_t scratch[8];
+  uint32_t red[3];  // alive postings, smallest alive score (bits), largest (bits)
+  uint64_t top[kKtopKM];
+  uint32_t n_top;
+};
+
+// term t's K-th best scores for K >= 10 from its na alive keys (each_key(f):
+// f(ok, key) for every key, the workgroup converged); the KM best into LDS with
+// one select over all keys, the smaller K then select inside LDS
+template <class EachKey>
+__device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, uint32_t mn_bits, KtopShared& sh,
+                            EachKey each_key) {
+  constexpr uint32_t KM = kKtopKM;
+  if (na < kTopKs[1]) return;  // uniform: only K = 1
+  uint64_t T = 0;
+  if (na > KM) {
+    T = select_kth(KM, sh.hist, sh.scratch, [&](auto&& f) {
+      each_key([&](bool ok, uint64_t key) { if (ok) f(key); });
+    });
+  }
+  each_key([&](bool ok, uint64_t key) { wave_append(ok && key >= T, key, sh.top, &sh.n_top, KM); });
+  __syncthreads();
+  const uint32_t nt = min(na, KM);  // keys in top[] (unique: exactly KM are >= T)
+  for (uint32_t kk = 1; kk < kNumTopK; ++kk) {
+    const uint32_t K = kTopKs[kk];
+    if (nt < K) break;  // uniform
+    float v;
+    if (na == K) {
+      v = __uint_as_float(mn_bits);  // every alive key is in: the minimum
+    } else if (K == KM) {
+      v = key_score(T);
+    } else {
+      v = key_score(select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
+        for (uint32_t i = threadIdx.x; i < nt; i += kThreads) f(sh.top[i]);
+      }));
     }
-  };
+    if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = v;
+  }
+}
+
+// postings [b + p0, b + p1) as f(valid && alive, score, doc), U loads per thread
+// in flight, the workgroup converged (callers may use wave-wide operations)
+template <class F>
+__device__ inline void ktop_each_posting(const ScoreJob& j, uint64_t b, uint32_t p0, uint32_t p1, F&& f) {
+  constexpr uint32_t U = 4;
+  for (uint32_t q0 = p0; q0 < p1; q0 += U * kThreads) {
+    uint32_t d[U];
+    float s[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t p = q0 + u * kThreads + threadIdx.x;
+      d[u] = p < p1 ? j.doc[b + p] : 0xFFFFFFFFu;
+      s[u] = p < p1 ? j.psc[b + p] : 0.0f;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const bool ok = d[u] != 0xFFFFFFFFu && (!j.alive || ((j.alive[d[u] >> 5] >> (d[u] & 31u)) & 1u));
+      f(ok, s[u], d[u]);
+    }
+  }
+}
+
+// alive count, smallest and largest alive score bits of postings [p0, p1) into sh.red
+__device__ inline void ktop_reduce(const ScoreJob& j, uint64_t b, uint32_t p0, uint32_t p1, KtopShared& sh) {
   if (threadIdx.x == 0) {
-    red[0] = 0;
-    red[1] = 0xFFFFFFFFu;
-    n_top = 0;
+    sh.red[0] = 0;
+    sh.red[1] = 0xFFFFFFFFu;
+    sh.red[2] = 0;
+    sh.n_top = 0;
   }
   __syncthreads();
   uint32_t c = 0, mx = 0, mn = 0xFFFFFFFFu;
-  each_posting([&](bool ok, float sv, uint32_t) {
+  ktop_each_posting(j, b, p0, p1, [&](bool ok, float sv, uint32_t) {
     if (!ok) return;
     const uint32_t bits = __float_as_uint(sv);
     ++c;
@@ -2714,42 +2759,83 @@ __global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
     mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
   }
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&red[0], c);
-    atomicMin(&red[1], mn);
-    if (c) atomicMax(reinterpret_cast<uint32_t*>(&j.ktop[(size_t)t * kNumTopK]), mx);  // K = 1: the maximum
+    atomicAdd(&sh.red[0], c);
+    atomicMin(&sh.red[1], mn);
+    atomicMax(&sh.red[2], mx);
   }
   __syncthreads();
-  const uint32_t na = red[0];
-  if (na < kTopKs[1]) return;  // uniform: only K = 1
-  // the KM best alive keys (all of them when there are no more) into LDS: one
-  // select over the whole list, the smaller K then select inside LDS
+}
+
+// one workgroup per term of <= kKtopChunk postings
+__global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
+  __shared__ KtopShared sh;
+  const uint32_t t = j.kt_terms[blockIdx.x];
+  const uint64_t b = j.off[t];
+  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
+  ktop_reduce(j, b, 0, n, sh);
+  const uint32_t na = sh.red[0];
+  if (threadIdx.x == 0 && na) j.ktop[(size_t)t * kNumTopK] = __uint_as_float(sh.red[2]);  // K = 1: the maximum
+  ktop_finish(j, t, na, sh.red[1], sh, [&](auto&& f) {
+    ktop_each_posting(j, b, 0, n, [&](bool ok, float sv, uint32_t d) { f(ok, make_key(sv, d)); });
+  });
+}
+
+// one workgroup per kKtopChunk-posting chunk of a long term: the chunk's alive
+// count and extremes (atomics into the term's slots) and its KM best keys
+__global__ __launch_bounds__(kThreads) void k_ktop_part(ScoreJob j) {
+  __shared__ KtopShared sh;
+  constexpr uint32_t KM = kKtopKM;
+  const uint32_t c = blockIdx.x, bt = j.kc_big[c];
+  const uint32_t t = j.kb_terms[bt];
+  const uint64_t b = j.off[t];
+  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
+  const uint32_t p0 = j.kc_start[c], p1 = min(n, p0 + kKtopChunk);
+  ktop_reduce(j, b, p0, p1, sh);
+  const uint32_t na = sh.red[0];
+  if (threadIdx.x == 0 && na) {
+    atomicAdd(&j.kb_stat[3 * bt], na);
+    atomicMin(&j.kb_stat[3 * bt + 1], sh.red[1]);
+    atomicMax(&j.kb_stat[3 * bt + 2], sh.red[2]);
+  }
   uint64_t T = 0;
   if (na > KM) {
-    T = select_kth(KM, hist, scratch, [&](auto&& f) {
-      each_posting([&](bool ok, float sv, uint32_t d) { if (ok) f(make_key(sv, d)); });
+    T = select_kth(KM, sh.hist, sh.scratch, [&](auto&& f) {
+      ktop_each_posting(j, b, p0, p1, [&](bool ok, float sv, uint32_t d) { if (ok) f(make_key(sv, d)); });
     });
   }
-  each_posting([&](bool ok, float sv, uint32_t d) {
+  ktop_each_posting(j, b, p0, p1, [&](bool ok, float sv, uint32_t d) {
     const uint64_t key = make_key(sv, d);
-    wave_append(ok && key >= T, key, top, &n_top, KM);
+    wave_append(ok && key >= T, key, sh.top, &sh.n_top, KM);
   });
   __syncthreads();
-  const uint32_t nt = min(na, KM);  // keys in top[] (unique: exactly KM are >= T)
-  for (uint32_t kk = 1; kk < kNumTopK; ++kk) {
-    const uint32_t K = kTopKs[kk];
-    if (nt < K) break;  // uniform
-    float v;
-    if (na == K) {
-      v = __uint_as_float(red[1]);  // every alive key is in: the minimum
-    } else if (K == KM) {
-      v = key_score(T);
-    } else {
-      v = key_score(select_kth(K, hist, scratch, [&](auto&& f) {
-        for (uint32_t i = threadIdx.x; i < nt; i += kThreads) f(top[i]);
-      }));
-    }
-    if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = v;
+  const uint32_t nt = min(na, KM);
+  uint64_t* out = j.kc_keys + (size_t)c * KM;
+  for (uint32_t i = threadIdx.x; i < nt; i += kThreads) out[i] = sh.top[i];
+  if (threadIdx.x == 0) j.kc_cnt[c] = nt;
+}
+
+// one workgroup per long term: its K-th best scores over its chunks' best keys
+__global__ __launch_bounds__(kThreads) void k_ktop_big(ScoreJob j) {
+  __shared__ KtopShared sh;
+  constexpr uint32_t KM = kKtopKM;
+  const uint32_t bt = blockIdx.x, t = j.kb_terms[bt];
+  const uint32_t na = j.kb_stat[3 * bt], mn = j.kb_stat[3 * bt + 1], mx = j.kb_stat[3 * bt + 2];
+  if (threadIdx.x == 0) {
+    sh.n_top = 0;
+    if (na) j.ktop[(size_t)t * kNumTopK] = __uint_as_float(mx);  // K = 1: the maximum
   }
+  __syncthreads();
+  const uint32_t c0 = j.kb_chunk0[bt], c1 = j.kb_chunk0[bt + 1];
+  ktop_finish(j, t, na, mn, sh, [&](auto&& f) {
+    for (uint32_t c = c0; c < c1; ++c) {
+      const uint32_t cn = j.kc_cnt[c];
+      const uint64_t* keys = j.kc_keys + (size_t)c * KM;
+      for (uint32_t i0 = 0; i0 < cn; i0 += kThreads) {
+        const uint32_t i = i0 + threadIdx.x;
+        f(i < cn, i < cn ? keys[i] : 0ull);
+      }
+    }
+  });
 }
 
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s) {
@@ -2764,9 +2850,18 @@ hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, 
   return hipGetLastError();
 }
 
-hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, hipStream_t s) {
-  if (!n_terms) return hipSuccess;
-  k_ktop<<<n_terms, kThreads, 0, s>>>(j);
+hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s) {
+  if (n_terms) {
+    k_ktop<<<n_terms, kThreads, 0, s>>>(j);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (n_chunks) {
+    k_ktop_part<<<n_chunks, kThreads, 0, s>>>(j);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (n_big) k_ktop_big<<<n_big, kThreads, 0, s>>>(j);
   return hipGetLastError();
 }
 

@@ -52,7 +52,7 @@ EXPORTS = (
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
-    "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged",
+    "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged", "fg_index_term_kth",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -138,6 +138,7 @@ _sig("fg_index_bm25", C.c_int, _p, C.c_uint32, _f32p, _f32p, _f32p)
 _sig("fg_plan_create", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
 _sig("fg_plan_create_multi", C.c_int, C.POINTER(_p), C.c_uint32, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
 _sig("fg_plan_execute_merged", C.c_int, _p, _p, _p, _p, _p, _p)
+_sig("fg_index_term_kth", C.c_int, _p, C.c_uint32, _f32p)
 _sig("fg_plan_execute", C.c_int, _p, _p, _p, _p, _p)
 _sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
@@ -406,6 +407,12 @@ class Index:
 
     def df(self, term: int, field: int = -1) -> int:
         return int(_lib.fg_index_df(self._h, field, term))
+
+    def term_kth(self, term: int):
+        """The per-term K-th best alive scores for K = 1, 10, 20, 100, 1000 (0: fewer postings)."""
+        out = np.zeros(5, np.float32)
+        _check(_lib.fg_index_term_kth(self._h, term, _ptr(out, _f32p)))
+        return out
 
     def bm25(self, term: int):
         wt, wn = C.c_float(), C.c_float()

@@ -187,6 +187,10 @@ int fg_index_stats_get(const fg_index* ix, fg_index_stats* out);
 uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term);
 /* Bm25Weight pieces the device uses, for host-side checks. */
 int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512);
+/* The snapshot's per-term K-th best alive posting scores for K = 1, 10, 20, 100,
+ * 1000 (0 when the term has fewer alive postings): the starting thresholds of
+ * its disjunctions.  out[5]. */
+int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out);
 
 /* ---- query batches -------------------------------------------------------- */
 typedef struct fg_query_batch {
