@@ -356,7 +356,10 @@ struct ScoreJob {
   uint32_t* kc_cnt;           // [n_chunks]
   uint32_t* kb_stat;          // [n_big * 3] alive postings, min / max alive score bits (0, ~0, 0 first)
 };
-constexpr uint32_t kKtopChunk = 32768;  // postings per k_ktop_part workgroup (and k_ktop's largest term)
+#ifndef FG_KTOP_CHUNK
+#define FG_KTOP_CHUNK 32768
+#endif
+constexpr uint32_t kKtopChunk = FG_KTOP_CHUNK;  // postings per k_ktop_part workgroup (and k_ktop's largest term)
 
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);

@@ -2678,7 +2678,26 @@ struct KtopShared {
   uint32_t red[3];  // alive postings, smallest alive score (bits), largest (bits)
   uint64_t top[kKtopKM];
   uint32_t n_top;
+  unsigned long long kmin;
 };
+
+// The smallest of top[0, nt) that is >= T: with exactly K keys >= T (select_kth's
+// contract, T possibly below the K-th key with its low bits cleared) it IS the
+// K-th key, so its score is the exact K-th score
+__device__ inline uint64_t ktop_min_at_least(KtopShared& sh, uint32_t nt, uint64_t T) {
+  if (threadIdx.x == 0) sh.kmin = ~0ull;
+  __syncthreads();
+  unsigned long long m = ~0ull;
+  for (uint32_t i = threadIdx.x; i < nt; i += kThreads)
+    if (sh.top[i] >= T && sh.top[i] < m) m = sh.top[i];
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = (unsigned long long)__shfl_xor((long long)m, o, 64);
+    m = y < m ? y : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMin(&sh.kmin, m);
+  __syncthreads();
+  return sh.kmin;
+}
 
 // term t's K-th best scores for K >= 10 from its na alive keys (each_key(f):
 // f(ok, key) for every key, the workgroup converged); the KM best into LDS with
@@ -2703,12 +2722,12 @@ __device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, uint32_t
     float v;
     if (na == K) {
       v = __uint_as_float(mn_bits);  // every alive key is in: the minimum
-    } else if (K == KM) {
-      v = key_score(T);
     } else {
-      v = key_score(select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
+      // T_K: exactly K keys of top[] are >= it (top[] holds the KM best)
+      const uint64_t TK = K == KM ? T : select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
         for (uint32_t i = threadIdx.x; i < nt; i += kThreads) f(sh.top[i]);
-      }));
+      });
+      v = key_score(ktop_min_at_least(sh, nt, TK));
     }
     if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = v;
   }
