@@ -2671,12 +2671,17 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
 // term selects over its chunks' keys (k_ktop_big): a 9M-posting term no longer
 // streams its list through one workgroup several times.
 constexpr uint32_t kKtopKM = kTopKs[kNumTopK - 1];  // the largest K: its keys are kept
+constexpr uint32_t kKtopSort = 1024;                 // ... and sorted (a power of two >= KM)
+static_assert(kKtopSort >= kKtopKM && (kKtopSort & (kKtopSort - 1)) == 0, "k_ktop sorts its KM keys in place");
+#ifndef FG_KTOP_SORT
+#define FG_KTOP_SORT 1  // A/B: 0 = one LDS select per K instead of one sort of the kept keys
+#endif
 
 struct KtopShared {
   uint32_t hist[kHistBins];
   uint32_t scratch[8];
   uint32_t red[3];  // alive postings, smallest alive score (bits), largest (bits)
-  uint64_t top[kKtopKM];
+  uint64_t top[kKtopSort];  // the KM best keys, then zero padding for the sort
   uint32_t n_top;
   unsigned long long kmin;
 };
@@ -2716,6 +2721,18 @@ __device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, uint32_t
   each_key([&](bool ok, uint64_t key) { wave_append(ok && key >= T, key, sh.top, &sh.n_top, KM); });
   __syncthreads();
   const uint32_t nt = min(na, KM);  // keys in top[] (unique: exactly KM are >= T)
+#if FG_KTOP_SORT
+  // one bitonic sort of the kept keys: the K-th key of every K is then top[K - 1]
+  uint32_t P = 16;
+  while (P < nt) P <<= 1;
+  for (uint32_t i = nt + threadIdx.x; i < P; i += kThreads) sh.top[i] = 0;
+  __syncthreads();
+  bitonic_sort_desc(sh.top, P);
+  if (threadIdx.x == 0)
+    for (uint32_t kk = 1; kk < kNumTopK; ++kk)
+      if (nt >= kTopKs[kk]) j.ktop[(size_t)t * kNumTopK + kk] = key_score(sh.top[kTopKs[kk] - 1]);
+  return;
+#endif
   for (uint32_t kk = 1; kk < kNumTopK; ++kk) {
     const uint32_t K = kTopKs[kk];
     if (nt < K) break;  // uniform
