@@ -505,10 +505,12 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   }
   ix->w_text.resize(V);
   ix->w_name.resize(V);
-  for (uint32_t t = 0; t < V; ++t) {
-    ix->w_text[t] = bm25_weight(df_t[t], Ns);
-    ix->w_name[t] = bm25_weight(df_n ? df_n[t] : 0u, Ns);
-  }
+  parallel_ranges(V, hw_threads(0), [&](int, uint32_t b, uint32_t e) {
+    for (uint32_t t = b; t < e; ++t) {
+      ix->w_text[t] = bm25_weight(df_t[t], Ns);
+      ix->w_name[t] = bm25_weight(df_n ? df_n[t] : 0u, Ns);
+    }
+  });
   // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
   // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
   const uint32_t VF = ix->n_fterms;
@@ -1183,7 +1185,9 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
   g_bt.start();
   const uint32_t N = in->n_docs, V = in->n_terms;
   const bool has_name_in = in->name_off && in->name_tok;
-  const int T = hw_threads(in->threads);
+  // every thread of pass 1 zeroes and merges three vocabulary-sized count
+  // arrays: a small build (a commit's new docs) uses few threads
+  const int T = std::max(1, std::min(hw_threads(in->threads), (int)(N / 4096)));
   HostPostings hp;
   hp.n_docs = N;
   hp.n_terms = V;
