@@ -31,6 +31,82 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def workload_key(kname, n_docs, batch, k, terms, extra=""):
+    """The key a committed rocprofv3 profile of a bench workload is filed under
+    (profiles/latest.json "workloads"), e.g. "k_conj|n10000000|b1024|k100|t3"."""
+    return f"{kname}|n{n_docs}|b{batch}|k{k}|t{terms}" + (f"|{extra}" if extra else "")
+
+
+def measured_traffic(key):
+    """(HBM bytes per launch of the workload's dominant kernel, source) from the
+    committed profile registry when its lib_id is this build's, else (None, reason)."""
+    reg = os.environ.get("FUGU_PMC_BYTES") or os.path.join(ROOT, "profiles", "latest.json")
+    if not os.path.exists(reg):
+        return None, "no profiles/latest.json"
+    with open(reg) as f:
+        pmc = json.load(f)
+    e = pmc.get("workloads", {}).get(key)
+    if e is None:
+        return None, f"no profile of {key}"
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from lib_id import lib_id
+    if e.get("lib_id") != lib_id():
+        return None, f"profile of {key} is of lib {e.get('lib_id')}, this build is {lib_id()}"
+    return e.get("hbm_bytes_per_launch"), e.get("source")
+
+
+def roofline(kname, kernel_ms, model, key, alg_model, pruned=None):
+    """The roofline object of one bench line: algorithmic bytes (fg_model_batch)
+    over the kernel's HIP-event time vs the HBM peak, the 128-B line floor of the
+    same loads, and the measured DRAM bytes of the same workload and build
+    (rocprofv3 PMC, committed under profiles/) when there is a profile."""
+    t = kernel_ms * 1e-3
+    if model is None:  # --no-model (profiling passes): the kernel and its workload only
+        return {"bound": "hbm", "kernel": kname, "kernel_ms": round(kernel_ms, 4), "workload_key": key}
+    alg = model["alg_bytes"]
+    r = {"bound": "hbm", "kernel": kname, "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": alg,
+         "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "alg_model": alg_model,
+         "alg_bytes_split": {"stream": model["stream_bytes"], "probe": model["probe_bytes"],
+                             "output": model["output_bytes"]},
+         "line_floor_bytes": model["line_bytes"], "query_line_bytes": model["query_line_bytes"],
+         "line_floor_gbs": round(model["line_bytes"] / t / 1e9, 1), "workload_key": key}
+    if pruned is not None:
+        r["at_final_threshold"] = {"alg_bytes": pruned["alg_bytes"], "line_floor_bytes": pruned["line_bytes"],
+                                   "query_line_bytes": pruned["query_line_bytes"]}
+    traffic, src = measured_traffic(key)
+    r["traffic"] = traffic
+    if traffic:
+        r.update({"traffic_source": src, "traffic_over_alg": round(traffic / alg, 3),
+                  "traffic_over_line_floor": round(traffic / model["line_bytes"], 3),
+                  "hbm_gbs_measured": round(traffic / t / 1e9, 1),
+                  "hbm_frac_measured": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4)})
+    else:
+        log(f"[bench] {key}: roofline.traffic = null ({src})")
+    return r
+
+
+NO_MODEL = False  # --no-model: profiling passes skip the host replays
+
+
+def model_sum(ixs, q_off, terms, k, thr, mode):
+    """fg_model_batch over the snapshots of one multi-snapshot plan (their arrays
+    are disjoint, so bytes and lines add up)."""
+    if NO_MODEL:
+        return None
+    tot = None
+    for ix in ixs:
+        m, _ = ix.model(q_off, terms, k, thr=thr, mode=mode)
+        tot = m if tot is None else {n: tot[n] + m[n] for n in tot}
+    return tot
+
+
+def final_thresholds(s, n, k):
+    """Each query's final k-th best score (0 when it has fewer than k hits)."""
+    s = np.asarray(s).reshape(len(n), k)
+    return np.where(np.asarray(n) >= k, s[:, k - 1], 0.0).astype(np.float32)
+
+
 def host_cores():
     """The host CPU share this process may use (T = nproc on the box).
     nproc honours OMP_NUM_THREADS (16 on the GPU box = its CPU share per GPU);
@@ -50,6 +126,18 @@ def host_cores():
         pass
     return {"nproc": nproc, "affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
             "cgroup_cpus": quota}
+
+
+def host_threads(cores):
+    """Host threads of this rank: FUGU_THREADS, else nproc -- except under a
+    launcher that sets OMP_NUM_THREADS=1 for every rank (torchrun), where the
+    CPU share (cgroup quota or affinity) is split over the node's ranks."""
+    if os.environ.get("FUGU_THREADS"):
+        return int(os.environ["FUGU_THREADS"])
+    if os.environ.get("OMP_NUM_THREADS") == "1" and "LOCAL_WORLD_SIZE" in os.environ:
+        share = cores["cgroup_cpus"] or cores["affinity"]
+        return max(1, int(share) // max(1, int(os.environ["LOCAL_WORLD_SIZE"])))
+    return cores["nproc"]
 
 
 def native_oracle():
@@ -78,36 +166,6 @@ def timed_steps(step, steps, warmup, torch):
         step()
     torch.cuda.synchronize()
     return time.perf_counter() - t0
-
-
-def commit_latency(ctx, ix, corp, native, synth, threads, n_new=1000):
-    """fg_db_commit's device work on a 10M-doc namespace: the
-    new docs become a segment built with the namespace statistics and the
-    10M-doc segment is rescored with them (fg_index_rescore: posting scores,
-    bounds, alive bitset recomputed on the device; postings, directory and rank
-    words shared).  The namespace's running statistics are kept per commit
-    (O(new docs)), so only the new docs' statistics are computed here."""
-    base_stats = native.docs_stats(corp.off, corp.tok, synth.VOCAB, threads=threads)  # maintained incrementally
-    new = synth.corpus(n_new, doc_begin=corp.n_docs)
-    out = {}
-    for rep in range(3):
-        t0 = time.perf_counter()
-        g = base_stats + native.docs_stats(new.off, new.tok, synth.VOCAB, threads=threads)
-        t1 = time.perf_counter()
-        re = ix.rescore(g)
-        t2 = time.perf_counter()
-        seg = native.Index.from_docs(ctx, new.off, new.tok, synth.VOCAB, threads=threads, keep_host=False,
-                                     global_stats=g)
-        t3 = time.perf_counter()
-        out = {"commit_ms": round((t3 - t0) * 1e3, 1), "stats_ms": round((t1 - t0) * 1e3, 1),
-               "rescore_10M_ms": round((t2 - t1) * 1e3, 1), "new_segment_ms": round((t3 - t2) * 1e3, 1),
-               "new_docs": n_new, "base_docs": corp.n_docs}
-        re.close()
-        seg.close()
-    out["note"] = ("device work of one commit of 1000 docs on a 10M-doc namespace: a new segment + the 10M "
-                   "segment rescored with the new statistics (third of 3 runs); a full rebuild is the "
-                   "'index built in' time")
-    return out
 
 
 def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
@@ -202,8 +260,40 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
                    "20 docs fetched from the host doc store"}
     if ref is not None:
         out["parity"] = {"queries_checked": nq, "mismatches": mism}
+    # ---- commits on the 10M namespace: 16 consecutive POST
+    # /batch/upsert calls of 1000 new docs, each one fg_db_commit (a new segment,
+    # every older segment rescored with the new statistics: src/db/document.rs:65);
+    # past 8 segments the background merger folds the small ones together
+    # (IndexWriter merge threads, src/db/core.rs:247-249), off the commit path
+    n_new, n_commits = 1000, 16
+    new = synth.corpus(n_new * n_commits, doc_begin=corp.n_docs, threads=threads)
+    tb2, to2 = synth.render_text(new, threads)
+    ib2, io2 = synth.render_ids(n_new * n_commits, doc_begin=corp.n_docs)
+    lat_c = []
+    t_all = time.perf_counter()
+    for c in range(n_commits):
+        a, b = c * n_new, (c + 1) * n_new
+        t1 = time.perf_counter()
+        d.upsert_batch("api", id_buf=ib2[int(io2[a]):int(io2[b])], id_off=io2[a:b + 1] - io2[a],
+                       text_buf=tb2[int(to2[a]):int(to2[b])], text_off=to2[a:b + 1] - to2[a])
+        lat_c.append(time.perf_counter() - t1)
+    t_commits = time.perf_counter() - t_all
+    d.merge_wait("api")
+    t_done = time.perf_counter() - t_all
+    mi = d.merge_info("api")
+    ms = [x * 1e3 for x in lat_c]
+    commits = {"commits": n_commits, "docs_per_commit": n_new, "base_docs": corp.n_docs,
+               "commit_ms": [round(x, 1) for x in ms],
+               "p50_ms": round(float(np.percentile(ms, 50)), 1), "p99_ms": round(float(np.percentile(ms, 99)), 1),
+               "max_ms": round(max(ms), 1), "wall_16_commits_ms": round(t_commits * 1e3, 1),
+               "wall_incl_background_merges_ms": round(t_done * 1e3, 1),
+               "merges": mi["merges"], "merge_ms_max": round(mi["merge_ms_max"], 1),
+               "merge_ms_total": round(mi["merge_ms_total"], 1), "segments_after": mi["segments"],
+               "note": "each commit = POST /batch/upsert of 1000 docs through fg_db_upsert_batch (analyzer, dictionary, "
+                       "raw-id deletes, a new segment built with the namespace statistics, every older segment "
+                       "rescored on the device); merges run on the background merger and are waited for at the end"}
     d.close()
-    return out
+    return out, commits
 
 
 def fanout(plans, gs, gd, gn, streams, torch, dev):
@@ -250,7 +340,7 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
     for b, e in ranges:
         off = corp.off[b:e + 1] - corp.off[b]
         ix = native.Index.from_docs(ctx, off, corp.tok[corp.off[b]:corp.off[e]], synth.VOCAB, threads=threads,
-                                    keep_host=False)
+                                    keep_host=True)
         ixs.append(ix)
         plans.append(ix.plan(q_off, terms, K))
     build_s = time.time() - t0
@@ -292,6 +382,15 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
     mp.profile(True)
     el = timed_steps(step, steps, warmup, torch)
     mk, mkn = mp.kernel_ms()
+    # roofline of the multi-snapshot k_conj: every namespace's exhaustive cascade
+    # (and pruned at the merged k-th score, the shared score-only threshold)
+    t0 = time.time()
+    thr = final_thresholds(os_.cpu().numpy(), on_.cpu().numpy(), K)
+    roof = roofline("k_conj", mk[0] / max(mkn, 1), model_sum(ixs, q_off, terms, K, None, native.MODE_AND),
+                    workload_key("k_conj", corp.n_docs, nq, K, 3, "c4 8ns"),
+                    "fg_model_batch over the 8 namespaces: k_conj's exhaustive cascade (as the headline)",
+                    model_sum(ixs, q_off, terms, K, thr, native.MODE_AND))
+    log(f"[bench] C4 models in {time.time() - t0:.1f}s")
     mms = merge_ms(gs, gd, gn, nq, K, torch)
     # the same fan-out through the ABI call a host makes: fg_search_sharded
     # (host batch in, merged host hits out: 8 plans, 8 executes, merge, D2H)
@@ -317,6 +416,7 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
             "step": "one multi-snapshot plan over the 8 namespaces (fg_plan_create_multi) and its merged select "
                     "(fg_plan_execute_merged)",
             "multi_plan_kernels_ms": [round(mk[0] / max(mkn, 1), 4), round(mk[1] / max(mkn, 1), 4)],
+            "roofline": roof,
             "k_conj_ms_per_namespace": per_ns, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
             "ms_per_step_8_plans_8_streams": round(el_fan * 1e3 / steps, 4),
             "ms_per_step_8_plans_one_stream": round(el_seq * 1e3 / steps, 4),
@@ -344,7 +444,7 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     for off, tok in parts:
         x = native.docs_stats(off, tok, synth.VOCAB, threads=threads)
         g = x if g is None else g + x
-    ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=False, global_stats=g)
+    ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=True, global_stats=g)
            for off, tok in parts]
     del parts
     build_s = time.time() - t0
@@ -382,12 +482,21 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     mp.profile(True)
     el = timed_steps(step, steps, warmup, torch)
     mk, mkn = mp.kernel_ms()
+    # roofline of the multi-snapshot k_disj: every shard replayed at the merged
+    # k-th score (the shards' shared score-only threshold)
+    t0 = time.time()
+    thr = final_thresholds(outs[0].cpu().numpy(), outs[3].cpu().numpy(), K)
+    roof = roofline("k_disj", mk[0] / max(mkn, 1), model_sum(ixs, q_off, terms, K, thr, native.MODE_OR),
+                    workload_key("k_disj", N, nq, K, "2-5 OR", "c5 s=1.1 8 shards"),
+                    "fg_model_batch over the 8 shards: k_disj at each query's final (merged) k-th score")
+    log(f"[bench] C5 models in {time.time() - t0:.1f}s")
     mms = merge_ms(gs, gd, gn, nq, K, torch)
     ent = {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 4),
            "batch": nq, "k": K, "terms": "2-5", "mode": "OR", "n_docs": N, "zipf_s": S, "shards": 8,
            "step": "one multi-snapshot plan over the 8 shards (fg_plan_create_multi) and its merged select "
                    "(fg_plan_execute_merged)",
            "multi_plan_kernels_ms": [round(mk[0] / max(mkn, 1), 4), round(mk[1] / max(mkn, 1), 4)],
+           "roofline": roof,
            "ms_per_step_8_linked_plans": round(el_linked * 1e3 / max(2, steps // 2), 4),
            "k_disj_ms_per_shard_linked": per_shard, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
            "workload": "C5: 100M docs s=1.1 as 8 doc shards with global BM25 statistics, 2-5-term OR top-1000 on "
@@ -424,23 +533,6 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
         ent["parity"] = {"queries_checked": done, "mismatches": mism}
         del ref
     return ent
-
-
-def pmc_traffic(path, kname, workload):
-    """(HBM bytes per launch of `kname`, source) from a committed rocprofv3 PMC summary when
-    its lib_id is this build's and its workload matches, else None."""
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        pmc = json.load(f)
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from lib_id import lib_id
-    wl = pmc.get("workload", {})
-    if pmc.get("lib_id") != lib_id() or any(wl.get(k) != v for k, v in workload.items()):
-        log(f"[bench] {path} does not match this build/workload: no measured traffic for {kname}")
-        return None
-    v = pmc.get(f"{kname}_hbm_bytes_per_launch")
-    return (v, pmc.get("source")) if v else None
 
 
 def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist):
@@ -485,7 +577,7 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
             g = x if g is None else g + x
         if world > 1:
             g = allreduce_stats(g, device=dev if backend == "nccl" else None)
-    ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=False, global_stats=g)
+    ixs = [native.Index.from_docs(ctx, off, tok, synth.VOCAB, threads=threads, keep_host=True, global_stats=g)
            for off, tok in parts]
     del parts
     build_s = time.time() - t0
@@ -560,8 +652,28 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     for i in range(nq):
         h.update(md[i, :mn[i]].tobytes())
         h.update(ms[i, :mn[i]].tobytes())
+    # this rank's roofline: its units replayed (fg_model_batch) at the merged
+    # k-th score of the whole job (c4: also k_conj's exhaustive cascade)
+    kname = "k_conj" if c4 else "k_disj"
+    my_ms = sum(m[0][0] for m in kms) / max(kms[0][1], 1)
+    thr = final_thresholds(ms, mn, K)
+    key = workload_key(kname, N, nq, K, 3 if c4 else "2-5 OR", f"c4 {per}ns" if c4 else f"c5 s=1.1 {per} shards")
+    if c4:
+        roof = roofline(kname, my_ms, model_sum(ixs, q_off, terms, K, None, mode), key,
+                        f"fg_model_batch over the rank's {per} namespaces: k_conj's exhaustive cascade",
+                        model_sum(ixs, q_off, terms, K, thr, mode))
+    else:
+        roof = roofline(kname, my_ms, model_sum(ixs, q_off, terms, K, thr, mode), key,
+                        f"fg_model_batch over the rank's {per} shards: k_disj at each query's final (merged) k-th score")
+    per_rank = None
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, {"rank": rank, "kernel_ms": roof["kernel_ms"], "frac": roof.get("frac"),
+                                      "alg_bytes_per_launch": roof.get("alg_bytes_per_launch"), "units": mine})
+        per_rank = {"ranks": allr, "kernel_ms_min": min(x["kernel_ms"] for x in allr),
+                    "kernel_ms_max": max(x["kernel_ms"] for x in allr),
+                    "frac_min": min(x["frac"] or 0 for x in allr), "frac_max": max(x["frac"] or 0 for x in allr)}
     if rank == 0:
-        kname = "k_conj" if c4 else "k_disj"
         line = {
             "metric": METRIC, "value": round(nq * args.steps / el, 1), "unit": "queries/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
@@ -575,18 +687,37 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
                            (" + RCCL all-gather top-k" if backend == "nccl" else f" + {backend} all-gather (rehearsal)")
                            if world > 1 else "")},
             "kernels_ms_per_step_max_rank": {kname: round(kern, 4), "k_final": round(fin, 4)},
+            "roofline": roof,
+            **({"per_rank": per_rank} if per_rank else {}),
             "rank_plan": ("one multi-snapshot plan over the rank's units, merged by its final select"
                           if merged_sel else f"{len(plans)} linked plan(s) + k_merge_rank"),
             "result_sha1": h.hexdigest()[:16],
             "hits": int(mn.sum()),
             "snapshot_build_s_rank0": round(build_s, 1),
             "cpu_baseline": None,
-            "note": "strong scaling of one fixed corpus; the headline mode (no --config) carries the CPU baseline "
-                    "and the roofline",
+            "note": "strong scaling of one fixed corpus; roofline = rank 0's units (per_rank: every rank's); the "
+                    "headline mode (no --config) carries the CPU baseline",
         }
         print(json.dumps(line), flush=True)
     del plans[1:]
     del plans
+
+
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) without a launcher: run the N ranks (one process per GPU,
+    torch.distributed.run on 127.0.0.1) as CHILD processes of this one, which
+    has not touched the GPU, and return their exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -615,9 +746,23 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="N > 1: each step's gather + merge on a side stream behind the next batch (opt-in: a gloo "
                          "rehearsal on one GPU measured it slower, RCCL unmeasured)")
+    ap.add_argument("--no-model", action="store_true",
+                    help="skip the host traffic models (profiling passes: only kernel times and counters matter)")
     ap.add_argument("--config", choices=["headline", "c4", "c5"], default="headline",
                     help="c4 / c5: BASELINE configs[3] / [4] split over the job's GPUs (strong scaling)")
     args = ap.parse_args()
+    global NO_MODEL
+    NO_MODEL = args.no_model
+
+    # one process per GPU: a launcher (torchrun) sets WORLD_SIZE; without one,
+    # --gpus N > 1 starts the N ranks itself (before anything touches the GPU)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return spawn_ranks(args.gpus)
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} ranks but --gpus {args.gpus}: pass --gpus equal to the rank count",
+              file=sys.stderr)
+        return 2
 
     import torch
     import torch.distributed as dist
@@ -639,7 +784,7 @@ def main():
     from fugu_amd import native, synth
 
     cores = host_cores()
-    threads = args.threads or cores["nproc"]
+    threads = args.threads or host_threads(cores)
     if args.config != "headline":
         run_config(args, args.config, rank, world, local, dev, backend, threads, torch, dist)
         if world > 1:
@@ -755,40 +900,51 @@ def main():
     p50_ms = float(np.median(lat) * 1e3) if lat else None
     tail_ms = {f"p{q}": round(float(np.percentile(lat, q) * 1e3), 4) for q in (90, 99)} if lat else None
 
-    # ---- roofline of the dominant kernel (k_conj): algorithmic bytes at the HBM
-    # layout (fg_bytes_model_gpu: k_conj's exhaustive cascade) over
-    # its HIP-event time on the launch stream.  The SURVEY 8(d) tantivy byte
-    # model (1 KiB block decode per probed block) is reported beside it, labelled.
-    if args.disj:
-        # k_disj: MaxScore bytes at each query's final k-th score (fg_bytes_model_or)
-        s_h = out_s.cpu().numpy().reshape(nq, K)
-        n_h = out_n.cpu().numpy()
-        bmg = ix.bytes_model_or(q_off, terms, K, np.where(n_h >= K, s_h[:, K - 1], 0.0).astype(np.float32))
-    else:
-        bmg = ix.bytes_model_gpu(q_off, terms, K, qmode)
-    alg_bytes = float(bmg[:, 3].sum())
-    # (FG_MODE_OR: the exhaustive union is both models)
-    cpu_model_bytes = alg_bytes if args.disj else float(ix.bytes_model(q_off, terms, K)[:, 2].sum())
+    # ---- roofline of the dominant kernel: algorithmic bytes of the batch at the
+    # HBM layout (fg_model_batch: the kernel's loads replayed on the host; k_conj:
+    # its exhaustive cascade, beside it the same replay pruned at each query's
+    # final k-th score; k_disj: MaxScore at the final k-th score) over the
+    # kernel's HIP-event time on its launch stream, with the 128-B line floor of
+    # those loads and the measured DRAM bytes of the same workload and build
+    t0 = time.time()
+    thr_h = final_thresholds(out_s.cpu().numpy(), out_n.cpu().numpy(), K)
     conj_ms = ms_k[0] / max(n_prof, 1)
-    achieved = alg_bytes / (conj_ms * 1e-3) / 1e9
-    # HBM bytes per k_conj launch from rocprofv3 PMC (FETCH_SIZE with the
-    # gather-calibrated gfx950 correction + WRITE_SIZE), collected by
-    # tools/profile_bench.sh on this exact workload and build, committed under
-    # profiles/ (profiles/latest.json)
-    traffic, pmc = None, {}
-    pmc_file = os.environ.get("FUGU_PMC_BYTES") or os.path.join(ROOT, "profiles", "latest.json")
-    if os.path.exists(pmc_file):
-        with open(pmc_file) as f:
-            pmc = json.load(f)
-        wl = pmc.get("workload", {})
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from lib_id import lib_id
-        same_build = pmc.get("lib_id") == lib_id()
-        if same_build and (not wl or (wl.get("n_docs") == args.docs and wl.get("batch") == nq and wl.get("k") == K
-                                      and wl.get("terms") == wl_terms)):
-            traffic = pmc.get(f"{kname}_hbm_bytes_per_launch")
-        else:
-            log(f"[bench] {pmc_file} does not match this build/workload: roofline.traffic = null")
+    if NO_MODEL:
+        mod = pruned = None
+        alg_model = None
+    elif args.disj:
+        mod, _ = ix.model(q_off, terms, K, thr=thr_h, mode=qmode)
+        pruned = None
+        alg_model = ("fg_model_batch: k_disj at each query's final k-th score (per (tile, clause) directory bounds "
+                     "+ tile maximum, 8 B per essential posting, per posting past bound 1 every other clause's rank "
+                     "word (8 B) + posting score (4 B) or bucket maximum (4 B), directory probes of rescored "
+                     "candidates, 8 B per kept key)")
+    else:
+        mod, _ = ix.model(q_off, terms, K)
+        pruned, _ = ix.model(q_off, terms, K, thr=thr_h)
+        alg_model = ("fg_model_batch: k_conj's exhaustive cascade at the HBM layout (8 B per lead posting; per probe "
+                     "8 B rank word + 4 B score on a hit, or 8 B bucket bounds + 4 B per search step + 4 B compare + "
+                     "4 B score on a hit; 8 B per kept key)")
+    roof = roofline(kname, conj_ms, mod, workload_key(kname, args.docs, nq, K, wl_terms), alg_model, pruned)
+    if not args.disj and not NO_MODEL:
+        # SURVEY.md 8(d)'s tantivy model (1 KiB block decode per probed block): a
+        # byte count of the CPU walk, not bytes this layout reads
+        roof["tantivy_walk_bytes_per_launch"] = float(ix.bytes_model(q_off, terms, K)[:, 2].sum())
+    if mod:
+        log(f"[bench] models in {time.time() - t0:.1f}s: alg {mod['alg_bytes'] / 1e9:.3f} GB, line floor "
+            f"{mod['line_bytes'] / 1e9:.3f} GB, frac {roof['frac']}")
+
+    # N > 1: every rank's kernel time and roofline fraction (its own namespace)
+    per_rank = None
+    if world > 1:
+        mine = {"rank": rank, "kernel_ms": roof["kernel_ms"], "frac": roof.get("frac"),
+                "alg_bytes_per_launch": roof.get("alg_bytes_per_launch"), "line_floor_bytes": roof.get("line_floor_bytes"),
+                "device": torch.cuda.get_device_name(dev), "local_rank": local}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        per_rank = {"ranks": allr,
+                    "kernel_ms_min": min(r["kernel_ms"] for r in allr), "kernel_ms_max": max(r["kernel_ms"] for r in allr),
+                    "frac_min": min(r["frac"] or 0 for r in allr), "frac_max": max(r["frac"] or 0 for r in allr)}
 
     # ---- CPU baseline: the oracle (tantivy's algorithm restated in C, compiled
     # -march=native on this host) on T = nproc host threads, each running whole
@@ -860,42 +1016,29 @@ def main():
             el = time.perf_counter() - t1
             pl2.profile(False)
             kms, kn = pl2.kernel_ms()
-            dfs = np.array([ix.df(int(t)) for t in qt], np.float64)
-            merge_bytes = 8.0 * dfs.sum()  # every posting of every clause once (exhaustive merge/union)
             s2 = os2.cpu().numpy().reshape(nq, kk)
             d2 = od2.cpu().numpy().view(np.uint32).reshape(nq, kk)
             n2 = on2.cpu().numpy()
+            kname2 = "k_conj" if mode == native.MODE_AND else "k_disj"
+            kms_ = kms[0] / max(kn, 1)
             ent = {"value": round(nq * args.extra_steps / el, 1), "unit": "queries/s",
                    "ms_per_step": round(el * 1e3 / args.extra_steps, 4), "batch": nq, "k": kk,
                    "terms": f"{a_min}-{a_max}", "mode": "AND" if mode == native.MODE_AND else "OR",
-                   "kernel": "k_conj" if mode == native.MODE_AND else "k_disj",
-                   "kernel_ms": round(kms[0] / max(kn, 1), 4), "k_final_ms": round(kms[1] / max(kn, 1), 4),
-                   "merge_bytes_per_launch": merge_bytes,
-                   "merge_equiv_gbs": round(merge_bytes / (kms[0] / max(kn, 1) * 1e-3) / 1e9, 1)}
-            if mode == native.MODE_OR:
-                # device-layout MaxScore bytes at each query's final k-th score (fg_bytes_model_or):
-                # the least an exact k_disj reads, over the kernel's time
-                thr = np.where(n2 >= kk, s2[:, kk - 1], 0.0).astype(np.float32)
-                bo = ix.bytes_model_or(qo, qt, kk, thr)
-                kms_ = kms[0] / max(kn, 1)
-                ent["roofline"] = {"bound": "hbm", "kernel": "k_disj", "alg_bytes_per_launch": float(bo[:, 3].sum()),
-                                   "alg_bytes_split": {"stream": float(bo[:, 0].sum()), "probe": float(bo[:, 1].sum()),
-                                                       "output": float(bo[:, 2].sum())},
-                                   "achieved": round(float(bo[:, 3].sum()) / (kms_ * 1e-3) / 1e9, 1),
-                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": round(float(bo[:, 3].sum()) / (kms_ * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                   "alg_model": "fg_bytes_model_or: MaxScore over 4096-doc tiles at the final k-th "
-                                                "score (12 B per tile-clause bound, 8 B per essential posting, rank "
-                                                "word / bucket max per posting past the tile bound, 4 B score per "
-                                                "present clause past the presence bound, 8 B per kept key)"}
-                # measured DRAM bytes per k_disj launch (rocprofv3 PMC of `bench.py --disj --k 1000`,
-                # profiles/latest_or.json) when it was taken on this build and workload
-                tr = pmc_traffic(os.path.join(ROOT, "profiles", "latest_or.json"), "k_disj",
-                                 {"n_docs": args.docs, "batch": nq, "k": kk, "terms": "2-5 OR"})
-                if tr:
-                    ent["roofline"].update({"traffic": tr[0], "traffic_source": tr[1],
-                                            "traffic_over_alg": round(tr[0] / float(bo[:, 3].sum()), 3),
-                                            "hbm_gbs_measured": round(tr[0] / (kms_ * 1e-3) / 1e9, 1)})
+                   "kernel": kname2, "kernel_ms": round(kms_, 4), "k_final_ms": round(kms[1] / max(kn, 1), 4)}
+            thr2 = final_thresholds(s2, n2, kk)
+            t0 = time.time()
+            if mode == native.MODE_AND:
+                mod2, _ = ix.model(qo, qt, kk)
+                pr2, _ = ix.model(qo, qt, kk, thr=thr2)
+                am = "fg_model_batch: k_conj's exhaustive cascade at the HBM layout (as the headline)"
+                wterms = f"{a_min}-{a_max}" if a_min != a_max else a_min
+            else:
+                mod2, _ = ix.model(qo, qt, kk, thr=thr2, mode=mode)
+                pr2 = None
+                am = "fg_model_batch: k_disj at each query's final k-th score (as the --disj headline)"
+                wterms = f"{a_min}-{a_max} OR"
+            ent["roofline"] = roofline(kname2, kms_, mod2, workload_key(kname2, args.docs, nq, kk, wterms), am, pr2)
+            log(f"[bench] {name}: models in {time.time() - t0:.1f}s")
             if ref is not None:
                 done, wall, mism = 0, 0.0, 0
                 budget = args.cpu_seconds / 2
@@ -924,11 +1067,12 @@ def main():
         extra["e2e_pipelined"] = e2e_pipeline(ix, native, synth, torch, dev, nq, K, 24, args.e2e_workers)
         log(f"[bench] e2e pipelined: {extra['e2e_pipelined']['value']} q/s")
     if rank == 0 and world == 1 and not args.no_extra:
-        extra["commit_10M"] = commit_latency(ctx, ix, corp, native, synth, threads)
-        log(f"[bench] commit on the 10M namespace: {extra['commit_10M']['commit_ms']} ms")
-        extra["db_api_default_search_10M_8seg"] = bench_db_api(ctx, corp, native, synth, ref, threads)
+        extra["db_api_default_search_10M_8seg"], extra["commit_10M"] = bench_db_api(ctx, corp, native, synth, ref,
+                                                                                     threads)
         log(f"[bench] GET /search (OR, limit 20) through fg_db_search on 8 segments: "
             f"p50 {extra['db_api_default_search_10M_8seg']['p50_ms']} ms")
+        log(f"[bench] 16 commits of 1000 docs on the 10M namespace: p50 {extra['commit_10M']['p50_ms']} ms, p99 "
+            f"{extra['commit_10M']['p99_ms']} ms, merges {extra['commit_10M']['merges']}")
     del plan
     ix.close()
     if rank == 0 and world == 1 and not args.no_extra:
@@ -968,27 +1112,8 @@ def main():
             "p50_ms": round(p50_ms, 4) if p50_ms is not None else None,
             "latency_ms": tail_ms,  # batch-of-one p90 / p99 beside p50 (same sample)
             **({"result_sha1": result_sha1} if result_sha1 else {}),
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": kname, "kernel_ms": round(conj_ms, 4),
-                "alg_bytes_per_launch": alg_bytes,
-                "alg_model": ("fg_bytes_model_or: k_disj's MaxScore at the final k-th score (DESIGN.md §5)"
-                              if args.disj else
-                              "fg_bytes_model_gpu: k_conj's exhaustive cascade at the HBM layout (8 B per lead "
-                              "posting; per probe 8 B rank word + 4 B score on a hit, or 8 B bucket bounds + 4 B per "
-                              "search step + 4 B compare + 4 B score on a hit; 8 B per kept key)"),
-                "alg_bytes_split": {("stream" if args.disj else "lead"): float(bmg[:, 0].sum()),
-                                    "probe": float(bmg[:, 1].sum()), "output": float(bmg[:, 2].sum())},
-                "traffic_over_alg": round(traffic / alg_bytes, 3) if traffic else None,
-                "traffic_source": pmc.get("source") if traffic else None,
-                "hbm_gbs_measured": (round(traffic / (conj_ms * 1e-3) / 1e9, 1) if traffic else None),
-                "hbm_frac_measured": (round(traffic / (conj_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None),
-                "cpu_model_bytes_per_launch": cpu_model_bytes,
-                "cpu_model": "SURVEY.md 8(d) B(q): tantivy's CPU walk (1 KiB block decode per probed 128-posting "
-                             "block); not bytes this layout reads",
-                "cpu_model_gbs": round(cpu_model_bytes / (conj_ms * 1e-3) / 1e9, 1),
-            },
+            "roofline": roof,
+            **({"per_rank": per_rank} if per_rank else {}),
             "kernels_ms_per_step": {kname: round(ms_k[0] / max(n_prof, 1), 4),
                                     "k_final": round(ms_k[1] / max(n_prof, 1), 4)},
             "cpu_baseline": cpu,
@@ -1002,4 +1127,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,0 +1,288 @@
+// Host-side internals of libfugu shared by fugu.cpp (snapshot build, plans,
+// execution, the C ABI) and model.cpp (the byte / line models of the roofline):
+// the opaque handles of include/fugu.h and their memory pools.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fugu.h"
+#include "fg_internal.h"
+
+namespace fgh {
+
+// set the thread-local message of fg_last_error() and return `code`
+int fail(int code, const char* fmt, ...);
+// host threads for builds, planning and models (FUGU_THREADS, the CPU share)
+int hw_threads(int req);
+
+template <class F>
+void parallel_ranges(uint32_t n, int threads, F&& f) {
+  if (threads <= 1 || n < 1024) { f(0, 0u, n); return; }
+  std::vector<std::thread> ts;
+  uint32_t step = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    uint32_t b = std::min<uint64_t>((uint64_t)t * step, n), e = std::min<uint64_t>((uint64_t)(t + 1) * step, n);
+    ts.emplace_back([&f, t, b, e] { f(t, b, e); });
+  }
+  for (auto& t : ts) t.join();
+}
+
+// Dynamic schedule over [0, n) in chunks of `grain` (per-term loops: Zipf term
+// ids put most postings in the first terms, so a static split leaves one
+// thread with nearly all the work).  f(thread, begin, end).
+template <class F>
+void parallel_dynamic(uint32_t n, int threads, uint32_t grain, F&& f) {
+  if (threads <= 1 || n <= grain) { f(0, 0u, n); return; }
+  std::atomic<uint64_t> next{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      for (;;) {
+        const uint64_t b = next.fetch_add(grain);
+        if (b >= n) break;
+        f(t, (uint32_t)b, (uint32_t)std::min<uint64_t>(n, b + grain));
+      }
+    });
+  for (auto& t : ts) t.join();
+}
+
+
+struct DevAllocs {
+  std::vector<void*> ptrs;
+  int dev = 0;
+  ~DevAllocs() {
+    if (ptrs.empty()) return;
+    (void)hipSetDevice(dev);
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+};
+
+
+}  // namespace fgh
+
+#define HIPCHK(x)                                                                  \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) return fgh::fail(FG_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+using fgh::DevAllocs;
+
+struct fg_ctx {
+  std::vector<int> devs;
+  std::vector<std::pair<int, int>> peers;  // (a, b): a reaches b's memory directly
+};
+
+// Plan workspaces of one index, recycled across batches (a server plans a new
+// batch every few ms; a hipMalloc/hipFree pair per batch would serialise the
+// device).  Buffers are reused when they fit a request within 2x; at most
+// kPoolKeep bytes stay cached.
+namespace fgh {
+struct WsPool {
+  static constexpr size_t kPoolKeep = 1ull << 30;
+  std::mutex mu;
+  std::multimap<size_t, void*> free_bufs;
+  size_t cached = 0;
+  int dev = 0;
+  void* get(size_t bytes, size_t* got) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      auto it = free_bufs.lower_bound(bytes);
+      if (it != free_bufs.end() && it->first <= 2 * bytes) {
+        void* p = it->second;
+        *got = it->first;
+        cached -= it->first;
+        free_bufs.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      // the cached workspaces may be what the device lacks: free them, retry once
+      (void)hipGetLastError();
+      {
+        std::lock_guard<std::mutex> l(mu);
+        for (auto& kv : free_bufs) (void)hipFree(kv.second);
+        free_bufs.clear();
+        cached = 0;
+      }
+      if (hipMalloc(&p, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    }
+    *got = bytes;
+    return p;
+  }
+  void put(void* p, size_t bytes) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (cached + bytes <= kPoolKeep) {
+        free_bufs.emplace(bytes, p);
+        cached += bytes;
+        return;
+      }
+    }
+    (void)hipSetDevice(dev);
+    (void)hipFree(p);
+  }
+  ~WsPool() {
+    if (free_bufs.empty()) return;
+    (void)hipSetDevice(dev);
+    for (auto& kv : free_bufs) (void)hipFree(kv.second);
+  }
+};
+
+// Pinned host buffers of one index: plan uploads and result copies go through
+// them (a pageable copy is staged by the runtime and synchronises on the way),
+// which takes ~tens of us off a batch-of-one search.
+struct PinnedPool {
+  static constexpr size_t kKeep = 16ull << 20;
+  std::mutex mu;
+  std::multimap<size_t, void*> free_bufs;
+  size_t cached = 0;
+  void* get(size_t bytes, size_t* got) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      auto it = free_bufs.lower_bound(bytes);
+      if (it != free_bufs.end() && it->first <= 4 * bytes + 65536) {
+        void* p = it->second;
+        *got = it->first;
+        cached -= it->first;
+        free_bufs.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    const size_t n = std::max<size_t>(bytes, 4096);
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    *got = n;
+    return p;
+  }
+  void put(void* p, size_t bytes) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (cached + bytes <= kKeep) {
+        free_bufs.emplace(bytes, p);
+        cached += bytes;
+        return;
+      }
+    }
+    (void)hipHostFree(p);
+  }
+  ~PinnedPool() {
+    for (auto& kv : free_bufs) (void)hipHostFree(kv.second);
+  }
+};
+// a pinned buffer of the pool for one scope
+struct PinnedLease {
+  PinnedPool& pool;
+  void* p = nullptr;
+  size_t n = 0;
+  PinnedLease(PinnedPool& pl, size_t bytes) : pool(pl) { p = pool.get(bytes, &n); }
+  ~PinnedLease() { if (p) pool.put(p, n); }
+};
+}  // namespace fgh
+using fgh::PinnedLease;
+using fgh::PinnedPool;
+using fgh::WsPool;
+
+struct fg_index {
+  std::atomic<int> refs{1};
+  int dev = 0;
+  uint32_t n_docs = 0, n_terms = 0;
+  bool has_name = false;
+  uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0, tile_entries = 0;
+  uint32_t n_dense = 0, n_rank = 0;
+  // ---- statistics and scoring (this snapshot's own)
+  uint64_t tot[2] = {0, 0};
+  uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
+  float avgdl[2] = {0, 0};
+  float cache[512];
+  std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
+  std::vector<float> tmaxs; // [V] largest posting score per term
+  std::vector<float> w_text, w_name;
+  // ---- structure (independent of the statistics; shared with rescored snapshots)
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> df_text, df_name;  // this snapshot's own postings (tantivy's per-segment cost order)
+  std::vector<uint32_t> first_doc, last_doc;
+  std::shared_ptr<const std::vector<uint32_t>> h_doc;  // optional host copy for fg_bytes_model(_gpu)
+  std::vector<uint32_t> tmeta;  // host copy of DevIndex::tmeta (probe kind of each term)
+  uint64_t tot_local[2] = {0, 0};
+  // facet field (FG_FIELD_FACET)
+  uint32_t n_fterms = 0;
+  uint64_t tot_f = 0, tot_f_local = 0;
+  float avgdl_f = 0.0f, cache_f1 = 0.0f;
+  std::vector<uint64_t> foff;
+  std::vector<uint32_t> df_facet, df_facet_local, ffirst, flast;
+  std::vector<float> fscore;    // a facet clause's score in a doc holding the term (tf 1, fieldnorm id 1)
+  // device: structure arrays (smem, shared) and the scoring tables (mem)
+  std::shared_ptr<DevAllocs> smem;
+  uint64_t struct_bytes = 0;
+  const uint32_t* d_tfp = nullptr;
+  const uint8_t* d_fn_text = nullptr;
+  const uint8_t* d_fn_name = nullptr;
+  const uint32_t *d_sc_term = nullptr, *d_sc_first = nullptr, *d_bk_term = nullptr, *d_bk_first = nullptr,
+                 *d_kt_terms = nullptr;
+  uint32_t n_sc = 0, n_bk = 0, n_kt = 0;
+  fg::DevIndex d{};
+  DevAllocs mem;
+  WsPool pool;  // plan workspaces (destroyed before mem: declared after it)
+  PinnedPool pinned;  // host staging of plan uploads and result copies
+};
+
+struct fg_plan {
+  fg_index* ix = nullptr;
+  // nq: query slots = n_segs x nq_batch (one snapshot: the batch's queries)
+  uint32_t nq = 0, k = 0, total_chunks = 0, n_scan = 0, nq_batch = 0, n_segs = 1;
+  std::vector<fg_index*> segs;  // a multi-snapshot plan's snapshots after ix (retained)
+  int mode = FG_MODE_AND;
+  fg::DevPlan d{};
+  void* ws = nullptr;  // workspace from ix->pool
+  size_t ws_got = 0;
+  float* own_score = nullptr;
+  uint32_t* own_doc = nullptr;
+  uint32_t* own_n = nullptr;
+  void* zero_region = nullptr;
+  size_t zero_bytes = 0;
+  size_t diag_words = 0;
+  uint64_t ws_bytes = 0;
+  DevAllocs mem;
+  hipStream_t last_stream = nullptr;
+  bool profile = false;
+  std::vector<hipEvent_t> pending;  // 3 per profiled execute
+  double ms[2] = {0, 0};
+  uint32_t n_prof = 0;
+  ~fg_plan() {
+    for (hipEvent_t e : pending) (void)hipEventDestroy(e);
+    if (pin) {  // an upload nothing waited for yet (created without sync, never executed)
+      (void)hipSetDevice(ix->dev);
+      (void)hipStreamSynchronize(up_stream);
+    }
+    if (ws) {
+      // the workspace may still be read by this plan's last launch (a per-thread
+      // stream handle resolves on the current device: select the plan's first)
+      if (last_stream_used) {
+        (void)hipSetDevice(ix->dev);
+        (void)hipStreamSynchronize(last_stream);
+      }
+      if (pin) ix->pinned.put(pin, pin_n);
+      ix->pool.put(ws, ws_got);
+    }
+    if (ix) fg_index_release(ix);
+    for (fg_index* x : segs) fg_index_release(x);
+  }
+  bool last_stream_used = false;
+  std::vector<uint32_t> h_lo, h_hi;  // per query: f32 bits spanned by its score histogram (fg_plan_link)
+  bool zeroed = false;        // the zero region arrived zeroed with the upload: the first execute skips its memset
+  void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
+  size_t pin_n = 0;
+  hipStream_t up_stream = hipStreamPerThread;  // the stream the plan was uploaded on
+};
+

@@ -16,9 +16,6 @@ constexpr uint32_t kThreads = 256;        // 4 waves of 64 per workgroup
 #ifndef FG_ITEMS
 #define FG_ITEMS 8
 #endif
-#ifndef FG_KARY
-#define FG_KARY 0
-#endif
 constexpr uint32_t kItems = FG_ITEMS;     // lead candidates per lane
 constexpr uint32_t kChunk = kThreads * kItems;   // 2048 lead candidates per work item
 constexpr uint32_t kWaveSpan = kChunk / 4;       // 512 consecutive candidates per wave
@@ -77,36 +74,18 @@ constexpr uint32_t kConjHistBits = FG_HIST_BITS;   // ... k_conj's (its LDS sets
 #define FG_TILE_SHIFT 12
 #endif
 constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
-#ifndef FG_DISJ_SUB
-#define FG_DISJ_SUB 0  // A/B (ab_disj_sub_*.log): 1 = k_disj's bound 1 from 512-doc sub-tile maxima, slower
-#endif
-constexpr bool kDisjSubBounds = FG_DISJ_SUB;
-#ifndef FG_DISJ_EBETA
-#define FG_DISJ_EBETA 4  // k_disj: a tile is also exhaustive when all its postings <= EBETA x the essential
-                         // ones (ab_disj_ebeta_k1000.log: 0 / 2 / 4 / 8 -> 8.05 / 8.00 / 7.94 / 8.56 ms)
-#endif
-constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
 // k_disj shape (A/B builds, profiles/r03/ab/ab_disj_occ*.log): postings per
-// pass, the exhaustive LDS path, the select's digit width, waves per SIMD
-// (3 waves / 1024 / exhaustive tiles / 11 bits -> 5 / 512 / none / 10: OR top-1000
-// 7.97 -> 7.02 ms, top-20 5.28 -> 4.59 ms, identical outputs: more waves in
-// flight beat more postings per wave and the exhaustive path's LDS)
+// pass, the select's digit width, waves per SIMD (3 waves / 1024 / exhaustive
+// LDS tiles / 11 bits -> 5 / 512 / none / 10: OR top-1000 7.97 -> 7.02 ms, top-20
+// 5.28 -> 4.59 ms, identical outputs: more waves in flight beat more postings per
+// wave and the exhaustive path's LDS; then the bound-2 LDS queue (9-bit digits):
+// ab_disj_queue_k*.log, OR top-20 3.92 -> 3.23 ms, top-1000 6.13 -> 5.94 ms, and the
+// next-pass prefetch: ab_disj_qpf_k*.log, 3.21 -> 3.15 / 5.94 -> 5.85 ms)
 #ifndef FG_DISJ_ROUND
 #define FG_DISJ_ROUND 512
 #endif
-#ifndef FG_DISJ_EXH
-#define FG_DISJ_EXH 0
-#endif
-#ifndef FG_DISJ_QUEUE
-#define FG_DISJ_QUEUE 1  // k_disj: bound 2 deferred through an LDS queue of the postings past bound 1
-                         // (ab_disj_queue_k*.log: OR top-20 3.92 -> 3.23 ms, top-1000 6.13 -> 5.94 ms)
-#endif
-#ifndef FG_DISJ_QPF
-#define FG_DISJ_QPF 1  // the queued k_disj loads the next pass's postings before this pass's bound 1
-                       // (ab_disj_qpf_k*.log: OR top-20 3.21 -> 3.15 ms, top-1000 5.94 -> 5.85 ms)
-#endif
 #ifndef FG_DISJ_HBITS
-#define FG_DISJ_HBITS (FG_DISJ_QUEUE ? 9 : 10)  // the queue's LDS comes out of the select's digit width
+#define FG_DISJ_HBITS 9  // the queue's LDS comes out of the select's digit width
 #endif
 #ifndef FG_DISJ_WAVES
 #define FG_DISJ_WAVES 5
@@ -114,36 +93,15 @@ constexpr uint32_t kDisjEBeta = FG_DISJ_EBETA;
 #ifndef FG_DISJ_G
 #define FG_DISJ_G 1  // ab_disj_g_k*.log, ab_disj_gpq_k*.log: 4 / 2 / 1 -> OR top-1000 7.00 / 6.51 / 6.13 ms, top-20 4.60 / 4.27 / 3.94 ms
 #endif
-constexpr bool kDisjExhaustive = FG_DISJ_EXH;
-constexpr uint32_t kSubShift = 9;                    // ... of 512-doc sub-tiles (DevIndex::smax)
-constexpr uint32_t kSubPerTile = 1u << (FG_TILE_SHIFT - kSubShift);
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
 #endif
 constexpr uint32_t kDisjMaxGroup = FG_DISJ_MAXGROUP;  // ... at most this many tiles per work item
 constexpr uint32_t kDisjMaxPairs = 256;  // ... and at most this many (tile, Should clause) pairs (k_disj LDS)
-#ifndef FG_DISJ_ITEM_POSTINGS
-#define FG_DISJ_ITEM_POSTINGS 1000000000u  // A/B: cap on a k_disj item's postings (all its clauses, mean density)
-#endif
-constexpr uint32_t kDisjItemPostings = FG_DISJ_ITEM_POSTINGS;
-#ifndef FG_DISJ_HEAVY
-#define FG_DISJ_HEAVY 0  // A/B: items of queries with more postings per item than this run first (0: sweep order)
-#endif
-constexpr uint32_t kDisjHeavy = FG_DISJ_HEAVY;
-#ifndef FG_EXHMIN
-#define FG_EXHMIN 1024
-#endif
-constexpr uint32_t kExhaustiveMin = FG_EXHMIN;  // k_disj: all-essential tiles with fewer postings go posting-driven
-#ifndef FG_KTOP20
-#define FG_KTOP20 1  // A/B: 0 = no K = 20 (the /search default limit) among the stored per-term K-th scores
-#endif
-#if FG_KTOP20
-constexpr uint32_t kNumTopK = 5;          // per-term K-th best scores kept for these K
+// per-term K-th best scores kept for these K (20: the /search default limit,
+// ab_ktop20_k20.log: OR top-20 k_disj 4.27 -> 4.22 ms starting from it)
+constexpr uint32_t kNumTopK = 5;
 constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 20, 100, 1000};
-#else
-constexpr uint32_t kNumTopK = 4;
-constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 100, 1000};
-#endif
 
 constexpr uint32_t kMaxFacetClauses = 8;  // facet clauses per query (FG_MAX_FACET_CLAUSES)
 constexpr uint32_t kFmaskChunk = 8192;    // facet postings per k_fmask workgroup
@@ -206,8 +164,6 @@ struct DevIndex {
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
   const uint32_t* toff;      // [V] first tmax entry of each term, or 0xFFFFFFFF (bucket >= tile: use bmax)
-  const float* smax;         // [tile entries * kSubPerTile] maxima of the same terms over 512-doc sub-tiles
-                             //     (k_disj's bound 1), entry toff[t] * kSubPerTile + (doc >> kSubShift)
   const float* cmax;         // [score chunks] largest posting score of each kChunk-posting chunk of a
                              //     list (block-max: k_conj skips a lead chunk that cannot reach the threshold)
   const uint32_t* coff;      // [V] index of each term's first chunk in cmax
@@ -341,7 +297,6 @@ struct ScoreJob {
   float* bmax;                // [D] out
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
-  uint32_t* smax;             // [tiles * kSubPerTile] out (f32 bits, zeroed first)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
   float* cmax;                // [score chunks] out: the largest score of each k_score chunk
   const uint32_t* ch_term;    // chunk tables

@@ -28,13 +28,14 @@
 #include <vector>
 
 #include "../../include/fugu.h"
+#include "fg_host.h"
 #include "fg_internal.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char* fmt, ...) {
+int fgh::fail(int code, const char* fmt, ...) {
   char buf[1024];
   va_list ap;
   va_start(ap, fmt);
@@ -44,19 +45,16 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-}  // namespace
-
 // shared with host.cpp so fg_last_error() reports host-side failures too
 void fg_set_last_error(const std::string& msg) { g_err = msg; }
 int fg_host_threads();  // below (hw_threads(0)), shared with host.cpp
 
 namespace {
 
-#define HIPCHK(x)                                                                  \
-  do {                                                                               \
-    hipError_t e_ = (x);                                                             \
-    if (e_ != hipSuccess) return fail(FG_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
-  } while (0)
+using fgh::fail;
+using fgh::hw_threads;
+using fgh::parallel_dynamic;
+using fgh::parallel_ranges;
 
 // ---------------------------------------------------------------- tantivy constants
 constexpr float kK1 = 1.2f;
@@ -132,43 +130,13 @@ struct BuildTrace {
 };
 thread_local BuildTrace g_bt;
 
-template <class F>
-void parallel_ranges(uint32_t n, int threads, F&& f) {
-  if (threads <= 1 || n < 1024) { f(0, 0u, n); return; }
-  std::vector<std::thread> ts;
-  uint32_t step = (n + threads - 1) / threads;
-  for (int t = 0; t < threads; ++t) {
-    uint32_t b = std::min<uint64_t>((uint64_t)t * step, n), e = std::min<uint64_t>((uint64_t)(t + 1) * step, n);
-    ts.emplace_back([&f, t, b, e] { f(t, b, e); });
-  }
-  for (auto& t : ts) t.join();
-}
-
-// Dynamic schedule over [0, n) in chunks of `grain` (per-term loops: Zipf term
-// ids put most postings in the first terms, so a static split leaves one
-// thread with nearly all the work).  f(thread, begin, end).
-template <class F>
-void parallel_dynamic(uint32_t n, int threads, uint32_t grain, F&& f) {
-  if (threads <= 1 || n <= grain) { f(0, 0u, n); return; }
-  std::atomic<uint64_t> next{0};
-  std::vector<std::thread> ts;
-  for (int t = 0; t < threads; ++t)
-    ts.emplace_back([&, t] {
-      for (;;) {
-        const uint64_t b = next.fetch_add(grain);
-        if (b >= n) break;
-        f(t, (uint32_t)b, (uint32_t)std::min<uint64_t>(n, b + grain));
-      }
-    });
-  for (auto& t : ts) t.join();
-}
-
+}  // namespace
 // Host threads for snapshot builds and planning: FUGU_THREADS when set; else
 // OMP_NUM_THREADS when it states a share above one (16 per GPU on the box; a
 // launcher's default of 1 -- torchrun sets it for every rank -- is not a CPU
 // share and is ignored); else the CPUs this process may run on (affinity,
 // capped by the cgroup quota), at most 64.
-int hw_threads(int req) {
+int fgh::hw_threads(int req) {
   if (req > 0) return std::min(req, 256);
   static const int n = [] {
     int t = 0;
@@ -194,8 +162,6 @@ int hw_threads(int req) {
   }();
   return n;
 }
-
-}  // namespace
 int fg_host_threads() { return hw_threads(0); }
 namespace {
 
@@ -217,221 +183,7 @@ struct HostPostings {
   uint64_t tot_f = 0;             // total_num_tokens(facet), duplicates included
 };
 
-struct DevAllocs {
-  std::vector<void*> ptrs;
-  int dev = 0;
-  ~DevAllocs() {
-    if (ptrs.empty()) return;
-    (void)hipSetDevice(dev);
-    for (void* p : ptrs) (void)hipFree(p);
-  }
-};
-
 }  // namespace
-
-struct fg_ctx {
-  std::vector<int> devs;
-  std::vector<std::pair<int, int>> peers;  // (a, b): a reaches b's memory directly
-};
-
-// Plan workspaces of one index, recycled across batches (a server plans a new
-// batch every few ms; a hipMalloc/hipFree pair per batch would serialise the
-// device).  Buffers are reused when they fit a request within 2x; at most
-// kPoolKeep bytes stay cached.
-struct WsPool {
-  static constexpr size_t kPoolKeep = 1ull << 30;
-  std::mutex mu;
-  std::multimap<size_t, void*> free_bufs;
-  size_t cached = 0;
-  int dev = 0;
-  void* get(size_t bytes, size_t* got) {
-    {
-      std::lock_guard<std::mutex> l(mu);
-      auto it = free_bufs.lower_bound(bytes);
-      if (it != free_bufs.end() && it->first <= 2 * bytes) {
-        void* p = it->second;
-        *got = it->first;
-        cached -= it->first;
-        free_bufs.erase(it);
-        return p;
-      }
-    }
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
-      // the cached workspaces may be what the device lacks: free them, retry once
-      (void)hipGetLastError();
-      {
-        std::lock_guard<std::mutex> l(mu);
-        for (auto& kv : free_bufs) (void)hipFree(kv.second);
-        free_bufs.clear();
-        cached = 0;
-      }
-      if (hipMalloc(&p, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-    }
-    *got = bytes;
-    return p;
-  }
-  void put(void* p, size_t bytes) {
-    {
-      std::lock_guard<std::mutex> l(mu);
-      if (cached + bytes <= kPoolKeep) {
-        free_bufs.emplace(bytes, p);
-        cached += bytes;
-        return;
-      }
-    }
-    (void)hipSetDevice(dev);
-    (void)hipFree(p);
-  }
-  ~WsPool() {
-    if (free_bufs.empty()) return;
-    (void)hipSetDevice(dev);
-    for (auto& kv : free_bufs) (void)hipFree(kv.second);
-  }
-};
-
-// Pinned host buffers of one index: plan uploads and result copies go through
-// them (a pageable copy is staged by the runtime and synchronises on the way),
-// which takes ~tens of us off a batch-of-one search.
-struct PinnedPool {
-  static constexpr size_t kKeep = 16ull << 20;
-  std::mutex mu;
-  std::multimap<size_t, void*> free_bufs;
-  size_t cached = 0;
-  void* get(size_t bytes, size_t* got) {
-    {
-      std::lock_guard<std::mutex> l(mu);
-      auto it = free_bufs.lower_bound(bytes);
-      if (it != free_bufs.end() && it->first <= 4 * bytes + 65536) {
-        void* p = it->second;
-        *got = it->first;
-        cached -= it->first;
-        free_bufs.erase(it);
-        return p;
-      }
-    }
-    void* p = nullptr;
-    const size_t n = std::max<size_t>(bytes, 4096);
-    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
-    *got = n;
-    return p;
-  }
-  void put(void* p, size_t bytes) {
-    {
-      std::lock_guard<std::mutex> l(mu);
-      if (cached + bytes <= kKeep) {
-        free_bufs.emplace(bytes, p);
-        cached += bytes;
-        return;
-      }
-    }
-    (void)hipHostFree(p);
-  }
-  ~PinnedPool() {
-    for (auto& kv : free_bufs) (void)hipHostFree(kv.second);
-  }
-};
-// a pinned buffer of the pool for one scope
-struct PinnedLease {
-  PinnedPool& pool;
-  void* p = nullptr;
-  size_t n = 0;
-  PinnedLease(PinnedPool& pl, size_t bytes) : pool(pl) { p = pool.get(bytes, &n); }
-  ~PinnedLease() { if (p) pool.put(p, n); }
-};
-
-struct fg_index {
-  std::atomic<int> refs{1};
-  int dev = 0;
-  uint32_t n_docs = 0, n_terms = 0;
-  bool has_name = false;
-  uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0, tile_entries = 0;
-  uint32_t n_dense = 0, n_rank = 0;
-  // ---- statistics and scoring (this snapshot's own)
-  uint64_t tot[2] = {0, 0};
-  uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
-  float avgdl[2] = {0, 0};
-  float cache[512];
-  std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
-  std::vector<float> tmaxs; // [V] largest posting score per term
-  std::vector<float> w_text, w_name;
-  // ---- structure (independent of the statistics; shared with rescored snapshots)
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> df_text, df_name;  // this snapshot's own postings (tantivy's per-segment cost order)
-  std::vector<uint32_t> first_doc, last_doc;
-  std::shared_ptr<const std::vector<uint32_t>> h_doc;  // optional host copy for fg_bytes_model(_gpu)
-  std::vector<uint32_t> tmeta;  // host copy of DevIndex::tmeta (probe kind of each term)
-  uint64_t tot_local[2] = {0, 0};
-  // facet field (FG_FIELD_FACET)
-  uint32_t n_fterms = 0;
-  uint64_t tot_f = 0, tot_f_local = 0;
-  float avgdl_f = 0.0f, cache_f1 = 0.0f;
-  std::vector<uint64_t> foff;
-  std::vector<uint32_t> df_facet, df_facet_local, ffirst, flast;
-  std::vector<float> fscore;    // a facet clause's score in a doc holding the term (tf 1, fieldnorm id 1)
-  // device: structure arrays (smem, shared) and the scoring tables (mem)
-  std::shared_ptr<DevAllocs> smem;
-  uint64_t struct_bytes = 0;
-  const uint32_t* d_tfp = nullptr;
-  const uint8_t* d_fn_text = nullptr;
-  const uint8_t* d_fn_name = nullptr;
-  const uint32_t *d_sc_term = nullptr, *d_sc_first = nullptr, *d_bk_term = nullptr, *d_bk_first = nullptr,
-                 *d_kt_terms = nullptr;
-  uint32_t n_sc = 0, n_bk = 0, n_kt = 0;
-  fg::DevIndex d{};
-  DevAllocs mem;
-  WsPool pool;  // plan workspaces (destroyed before mem: declared after it)
-  PinnedPool pinned;  // host staging of plan uploads and result copies
-};
-
-struct fg_plan {
-  fg_index* ix = nullptr;
-  // nq: query slots = n_segs x nq_batch (one snapshot: the batch's queries)
-  uint32_t nq = 0, k = 0, total_chunks = 0, n_scan = 0, nq_batch = 0, n_segs = 1;
-  std::vector<fg_index*> segs;  // a multi-snapshot plan's snapshots after ix (retained)
-  int mode = FG_MODE_AND;
-  fg::DevPlan d{};
-  void* ws = nullptr;  // workspace from ix->pool
-  size_t ws_got = 0;
-  float* own_score = nullptr;
-  uint32_t* own_doc = nullptr;
-  uint32_t* own_n = nullptr;
-  void* zero_region = nullptr;
-  size_t zero_bytes = 0;
-  size_t diag_words = 0;
-  uint64_t ws_bytes = 0;
-  DevAllocs mem;
-  hipStream_t last_stream = nullptr;
-  bool profile = false;
-  std::vector<hipEvent_t> pending;  // 3 per profiled execute
-  double ms[2] = {0, 0};
-  uint32_t n_prof = 0;
-  ~fg_plan() {
-    for (hipEvent_t e : pending) (void)hipEventDestroy(e);
-    if (pin) {  // an upload nothing waited for yet (created without sync, never executed)
-      (void)hipSetDevice(ix->dev);
-      (void)hipStreamSynchronize(up_stream);
-    }
-    if (ws) {
-      // the workspace may still be read by this plan's last launch (a per-thread
-      // stream handle resolves on the current device: select the plan's first)
-      if (last_stream_used) {
-        (void)hipSetDevice(ix->dev);
-        (void)hipStreamSynchronize(last_stream);
-      }
-      if (pin) ix->pinned.put(pin, pin_n);
-      ix->pool.put(ws, ws_got);
-    }
-    if (ix) fg_index_release(ix);
-    for (fg_index* x : segs) fg_index_release(x);
-  }
-  bool last_stream_used = false;
-  std::vector<uint32_t> h_lo, h_hi;  // per query: f32 bits spanned by its score histogram (fg_plan_link)
-  bool zeroed = false;        // the zero region arrived zeroed with the upload: the first execute skips its memset
-  void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
-  size_t pin_n = 0;
-  hipStream_t up_stream = hipStreamPerThread;  // the stream the plan was uploaded on
-};
 
 namespace {
 
@@ -549,18 +301,12 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   d_tmaxs = static_cast<uint32_t*>(p);
   if ((rc = dev_alloc(4ull * ix->tile_entries, &p))) return rc;
   d_tmax = static_cast<uint32_t*>(p);
-  uint32_t* d_smax = nullptr;  // sub-tile maxima only for the FG_DISJ_SUB=1 A/B build
-  if (fg::kDisjSubBounds) {
-    if ((rc = dev_alloc(4ull * ix->tile_entries * fg::kSubPerTile, &p))) return rc;
-    d_smax = static_cast<uint32_t*>(p);
-  }
   if ((rc = dev_alloc(4ull * V * fg::kNumTopK, &p))) return rc;
   d_ktop = static_cast<float*>(p);
   if ((rc = dev_alloc(4ull * ix->n_sc, &p))) return rc;
   float* d_cmax = static_cast<float*>(p);
   HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, nullptr));
   HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), nullptr));
-  if (d_smax) HIPCHK(hipMemsetAsync(d_smax, 0, std::max<size_t>(4ull * ix->tile_entries * fg::kSubPerTile, 16), nullptr));
   HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, nullptr));
   fg::ScoreJob j{};
   j.doc = ix->d.doc;
@@ -580,7 +326,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.bmax = d_bmax;
   j.tmaxs = d_tmaxs;
   j.tmax = d_tmax;
-  j.smax = d_smax;
   j.ktop = d_ktop;
   j.cmax = d_cmax;
   j.ch_term = ix->d_sc_term;
@@ -704,7 +449,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
-  ix->d.smax = reinterpret_cast<const float*>(d_smax);
   ix->d.cmax = d_cmax;
   ix->d.alive = d_alive;
   ix->d.dense = d_dense;
@@ -1054,7 +798,8 @@ int build_facets(const fg_docs_input* in, HostPostings& hp, int T) {
 extern "C" {
 
 const char* fg_last_error(void) { return g_err.c_str(); }
-const char* fg_version(void) { return "libfugu 0.1 (gfx950)"; }
+const char* fg_version(void) { return "libfugu 0.4 (gfx950)"; }
+int fg_abi_version(void) { return FG_ABI_VERSION; }
 
 int fg_device_count(int* out) {
   if (!out) return fail(FG_EINVAL, "out is NULL");
@@ -1746,24 +1491,17 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       set_bins(i, ub);
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
-      // tiles per item: ~gpq items per query, and at most ~kDisjItemPostings
-      // postings per item at the clauses' mean density (a query of dense terms
-      // gets more, shorter items: its late items no longer make the kernel's tail)
-      double per_tile = 0.0;
-      for (uint32_t c = 0; c < ns; ++c) per_tile += (double)(ix->off[qt[c] + 1] - ix->off[qt[c]]);
-      per_tile *= (double)(1u << fg::kDisjTileShift) / (double)std::max<uint64_t>(N, 1);
-      const uint32_t g_cost = (uint32_t)std::max(1.0, std::min(1e9, (double)fg::kDisjItemPostings / std::max(per_tile, 1.0)));
-      const uint32_t G = std::min<uint32_t>(std::min(std::min(fg::kDisjMaxGroup, fg::kDisjMaxPairs / ns), g_cost),
+      // tiles per item: ~gpq items per query (capping an item's postings, or the
+      // items of heavy queries first, measured slower: ab_disj_itemcap_k*.log,
+      // ab_disj_heavy_k*.log)
+      const uint32_t G = std::min<uint32_t>(std::min(fg::kDisjMaxGroup, fg::kDisjMaxPairs / ns),
                                             std::max<uint32_t>(1, (nt + gpq - 1) / gpq));
       const uint32_t ng = (nt + G - 1) / G;
       ngroup[i] = ng;
-      // FG_DISJ_HEAVY > 0 (A/B): the items of queries whose items hold more than
-      // that many postings (mean density) run first, in their own sweep order
-      const bool heavy = fg::kDisjHeavy > 0 && per_tile * G > (double)fg::kDisjHeavy;
       for (uint32_t g = 0; g < ng; ++g) {
         const uint32_t t0 = tlo + g * G, n = std::min(G, nt - g * G);
         const double mid = ((double)t0 + 0.5 * n) * (double)(1u << fg::kDisjTileShift) / (double)ix->n_docs;
-        ditems.push_back(W{fg::kDisjHeavy > 0 ? (heavy ? 0.05 * mid : 0.05 + 0.95 * mid) : mid, i, t0, n});
+        ditems.push_back(W{mid, i, t0, n});
       }
       if (ditems.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", ditems.size());
       continue;
@@ -2746,304 +2484,6 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
   HIPCHK(hipMemcpyAsync(out_n, mn, 4ull * nq, hipMemcpyDeviceToHost, hipStreamPerThread));
   HIPCHK(hipStreamSynchronize(hipStreamPerThread));
-  return FG_OK;
-}
-
-// ---------------------------------------------------------------- bytes model
-int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out) {
-  if (!ix || !q || !out) return fail(FG_EINVAL, "bad arguments");
-  if (!ix->h_doc && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
-  const double F = ix->has_name ? 2.0 : 1.0;
-  std::vector<uint32_t> S;
-  for (uint32_t i = 0; i < q->n_queries; ++i) {
-    const uint32_t b = q->q_off[i], m = q->q_off[i + 1] - b;
-    double* o = out + 4ull * i;
-    struct L { uint64_t n, off; uint32_t pos; };
-    std::vector<L> ls;
-    bool missing = false;
-    for (uint32_t j = 0; j < m; ++j) {
-      uint32_t t = q->terms[b + j];
-      if (t >= ix->n_terms || ix->off[t + 1] == ix->off[t]) { missing = true; break; }
-      ls.push_back(L{ix->off[t + 1] - ix->off[t], ix->off[t], j});
-    }
-    if (m == 0 || missing) { o[0] = o[1] = o[2] = o[3] = 0; continue; }
-    if (m == 1) {
-      double df = (double)ls[0].n;
-      o[0] = o[1] = 8.0 * df;
-      o[2] = 8.0 * df + 8.0 * std::min<double>(df, k);
-      o[3] = df;
-      continue;
-    }
-    std::stable_sort(ls.begin(), ls.end(), [](const L& x, const L& y) { return x.n < y.n; });
-    double bmerge = 0;
-    for (auto& l : ls) bmerge += 8.0 * (double)l.n;
-    double bskip = 8.0 * (double)ls[0].n;
-    S.assign(ix->h_doc->begin() + ls[0].off, ix->h_doc->begin() + ls[0].off + ls[0].n);
-    for (size_t t = 1; t < ls.size(); ++t) {
-      const uint32_t* d = ix->h_doc->data() + ls[t].off;
-      const uint64_t n = ls[t].n;
-      uint64_t blocks = 0, lb = 0;
-      int64_t last_block = -1;
-      size_t keep = 0;
-      for (size_t x = 0; x < S.size(); ++x) {
-        lb = std::lower_bound(d + lb, d + n, S[x]) - d;
-        if (lb < n) {
-          int64_t blk = (int64_t)(lb / fg::kBlock);
-          if (blk != last_block) { ++blocks; last_block = blk; }
-          if (d[lb] == S[x]) S[keep++] = S[x];
-        }
-      }
-      S.resize(keep);
-      bskip += 1024.0 * (double)blocks + 4.0 * (double)((n + fg::kBlock - 1) / fg::kBlock);
-    }
-    const double ns = (double)S.size();
-    o[0] = bmerge;
-    o[1] = bskip;
-    o[2] = std::min(bmerge, bskip) + F * ns + 8.0 * std::min<double>(ns, k);
-    o[3] = ns;
-  }
-  return FG_OK;
-}
-
-// ---------------------------------------------------------------- bytes model at the device layout
-// The bytes k_conj's exhaustive cascade reads at this snapshot's HBM layout
-// (DESIGN.md §5): the roofline numerator.  The probes replay the kernel's
-// access sequence (kernels.hip k_conj) on the host copy of the postings.
-int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out) {
-  if (!ix || !q || !out || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
-  if (!ix->h_doc && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
-  const uint32_t nq = q->n_queries;
-  std::atomic<bool> bad{false};
-  parallel_ranges(nq, nq >= 64 ? hw_threads(0) : 1, [&](int, uint32_t qb, uint32_t qe) {
-    std::vector<uint32_t> cand, next;
-    for (uint32_t i = qb; i < qe; ++i) {
-      double* o = out + 4ull * i;
-      o[0] = o[1] = o[2] = o[3] = 0.0;
-      const uint32_t b = q->q_off[i], m = q->q_off[i + 1] - b;
-      if (q->q_off[i + 1] < b || m > fg::kMaxTerms) { bad = true; return; }
-      if (m == 0) continue;
-      if (q->mode == FG_MODE_OR) {
-        // k_disj's exhaustive union: every posting (doc + score) of every clause once
-        for (uint32_t j = 0; j < m; ++j) {
-          const uint32_t t = q->terms[b + j];
-          if (t < ix->n_terms) o[0] += 8.0 * (double)(ix->off[t + 1] - ix->off[t]);
-        }
-        o[2] = 8.0 * k;
-        o[3] = o[0] + o[2];
-        continue;
-      }
-      // intersection order: cost = df_text + df_name, stable (fg_plan_create)
-      struct T { uint64_t cost; uint32_t term; };
-      T ts[fg::kMaxTerms];
-      bool missing = false;
-      for (uint32_t j = 0; j < m; ++j) {
-        const uint32_t t = q->terms[b + j];
-        const uint64_t cost = t < ix->n_terms ? (uint64_t)ix->df_text[t] + ix->df_name[t] : 0;
-        missing |= cost == 0;
-        ts[j] = T{cost, t};
-      }
-      if (missing) continue;
-      std::stable_sort(ts, ts + m, [](const T& x, const T& y) { return x.cost < y.cost; });
-      const uint32_t t0 = ts[0].term;
-      const uint64_t df0 = ix->off[t0 + 1] - ix->off[t0];
-      o[0] = 8.0 * (double)df0;  // lead doc id + posting score
-      cand.assign(ix->h_doc->begin() + ix->off[t0], ix->h_doc->begin() + ix->off[t0 + 1]);
-      double probe = 0.0;
-      for (uint32_t j = 1; j < m && !cand.empty(); ++j) {
-        const uint32_t t = ts[j].term, meta = ix->tmeta[t];
-        const uint32_t* d = ix->h_doc->data() + ix->off[t];
-        const uint64_t n = ix->off[t + 1] - ix->off[t];
-        next.clear();
-        if (fg::meta_slot(meta)) {
-          // f32 score table: one 4-B element per candidate; rank words: one 8-B
-          // word per candidate + the 4-B posting score on a hit
-          for (uint32_t x : cand)
-            if (std::binary_search(d, d + n, x)) next.push_back(x);
-          probe += fg::meta_rank(meta) ? 8.0 * (double)cand.size() + 4.0 * (double)next.size()
-                                       : 4.0 * (double)cand.size();
-        } else {
-          // bucket directory: the bucket's two bounds, the search steps inside it,
-          // the final compare and, on a hit, the posting score
-          const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu;
-          for (uint32_t x : cand) {
-            const uint64_t lo = (uint64_t)(x >> B) << B;
-            uint64_t pos = std::lower_bound(d, d + n, (uint32_t)std::min<uint64_t>(lo, 0xFFFFFFFFull)) - d;
-            const uint64_t hi = std::lower_bound(d + pos, d + n, (uint32_t)std::min<uint64_t>(lo + (1ull << B),
-                                                                                             0xFFFFFFFFull)) - d;
-            double words = 2.0;
-            for (uint32_t st = S; st > 0; --st) {
-              const uint64_t half = 1ull << (st - 1), idx = pos + half - 1;
-              if (idx < hi) {
-                words += 1.0;
-                if (d[idx] < x) pos += half;
-              }
-            }
-            if (pos < hi) {
-              words += 1.0;
-              if (d[pos] == x) { words += 1.0; next.push_back(x); }
-            }
-            probe += 4.0 * words;
-          }
-        }
-        cand.swap(next);
-      }
-      o[1] = probe;
-      o[2] = 8.0 * (double)std::min<size_t>(cand.size(), k);  // the work item's kept keys
-      o[3] = o[0] + o[1] + o[2];
-    }
-  });
-  if (bad) return fail(FG_EINVAL, "bad query batch");
-  return FG_OK;
-}
-
-// ---------------------------------------------------------------- OR bytes model at the device layout
-// k_disj's MaxScore with the pruning threshold fixed at thr[i] (the query's
-// final k-th best score: no exact MaxScore run can prune harder), replayed on
-// the host over this snapshot's layout:
-//   stream: per (tile, clause) 8 B of directory bounds + 4 B tile maximum; per
-//           essential posting of a posting-driven tile 8 B (doc + score); per
-//           posting of an exhaustive tile 8 B;
-//   probe : per posting past bound 1 (the other clauses' tile maxima), for every
-//           other clause with postings in the tile its rank word (8 B) or its
-//           bucket maximum (4 B); per posting past the presence bound 4 B per
-//           present rank clause's posting score; per candidate a non-dense
-//           clause's directory probe (8 B bounds + 4 B per search step + 4 B)
-//           and score (4 B on a hit);
-//   output: 8 B per kept key (<= k).
-int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, const float* thr, double* out) {
-  if (!ix || !q || !out || !thr || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
-  if (!ix->h_doc && ix->n_postings) return fail(FG_EINVAL, "index built without keep_host_postings");
-  std::vector<float> psc(ix->n_postings);
-  HIPCHK(hipSetDevice(ix->dev));
-  if (ix->n_postings) HIPCHK(hipMemcpy(psc.data(), ix->d.psc, 4ull * ix->n_postings, hipMemcpyDeviceToHost));
-  const uint32_t nq = q->n_queries, N = ix->n_docs;
-  const uint32_t TS = fg::kDisjTileShift, nt = (N + (1u << TS) - 1) >> TS;
-  const uint32_t* hd = ix->h_doc ? ix->h_doc->data() : nullptr;
-  std::atomic<bool> bad{false};
-  parallel_dynamic(nq, hw_threads(0), 1, [&](int, uint32_t qb, uint32_t qe) {
-    std::vector<float> tmx, smx;
-    std::vector<uint32_t> tcnt;
-    std::vector<uint64_t> pres;  // presence bitmaps, one per clause
-    for (uint32_t i = qb; i < qe; ++i) {
-      double* o = out + 4ull * i;
-      o[0] = o[1] = o[2] = o[3] = 0.0;
-      const uint32_t b = q->q_off[i], e = q->q_off[i + 1];
-      if (e < b || e - b > fg::kMaxTerms) { bad = true; return; }
-      uint32_t t[fg::kMaxTerms], m = 0;
-      for (uint32_t j = b; j < e; ++j) {
-        const uint8_t oc = q->occur ? q->occur[j] : FG_OCCUR_SHOULD;
-        const uint32_t tt = q->terms[j];
-        if (oc == FG_OCCUR_SHOULD && tt < ix->n_terms && ix->off[tt + 1] > ix->off[tt]) t[m++] = tt;
-      }
-      if (!m) continue;
-      tmx.assign((size_t)nt * m, 0.0f);
-      smx.assign((size_t)nt * fg::kSubPerTile * m, 0.0f);
-      tcnt.assign((size_t)nt * m, 0);
-      pres.assign((size_t)m * ((N + 63) / 64), 0);
-      for (uint32_t c = 0; c < m; ++c)
-        for (uint64_t p = ix->off[t[c]]; p < ix->off[t[c] + 1]; ++p) {
-          const uint32_t d = hd[p], ti = d >> TS;
-          tmx[(size_t)ti * m + c] = std::max(tmx[(size_t)ti * m + c], psc[p]);
-          smx[(size_t)(d >> fg::kSubShift) * m + c] = std::max(smx[(size_t)(d >> fg::kSubShift) * m + c], psc[p]);
-          tcnt[(size_t)ti * m + c]++;
-          pres[(size_t)c * ((N + 63) / 64) + (d >> 6)] |= 1ull << (d & 63);
-        }
-      const float th = thr[i];
-      const uint64_t thk = fg::make_key(th, 0xFFFFFFFFu);
-      double stream = 0, probe = 0;
-      std::vector<uint64_t> cur(m);
-      for (uint32_t c = 0; c < m; ++c) cur[c] = ix->off[t[c]];
-      for (uint32_t ti = 0; ti < nt; ++ti) {
-        float ub[fg::kMaxTerms];
-        uint32_t ord[fg::kMaxTerms], np = 0;
-        for (uint32_t c = 0; c < m; ++c) {
-          ub[c] = tcnt[(size_t)ti * m + c] ? tmx[(size_t)ti * m + c] : 0.0f;
-          np += tcnt[(size_t)ti * m + c];
-          uint32_t j = c;
-          while (j > 0 && ub[ord[j - 1]] > ub[c]) { ord[j] = ord[j - 1]; --j; }
-          ord[j] = c;
-        }
-        stream += 12.0 * m;  // R: directory bounds + tile maximum per clause
-        float sacc = 0.0f;
-        uint32_t P = 0;
-        for (; P < m; ++P) {
-          const float s2 = sacc + ub[ord[P]];
-          if (fg::make_key(s2 * 1.00000762939453125f, 0u) >= thk) break;
-          sacc = s2;
-        }
-        uint32_t ess = 0, npe = 0;
-        for (uint32_t j = P; j < m; ++j) {
-          ess |= 1u << ord[j];
-          npe += tcnt[(size_t)ti * m + ord[j]];
-        }
-        if (P == m || npe == 0) {
-          for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
-          continue;
-        }
-        if (fg::kDisjExhaustive && ((P == 0 && np >= fg::kExhaustiveMin) ||
-                                    (fg::kDisjEBeta > 0 && np >= fg::kExhaustiveMin && np <= fg::kDisjEBeta * npe))) {
-          // exhaustive LDS tile
-          stream += 8.0 * np;
-          for (uint32_t c = 0; c < m; ++c) cur[c] += tcnt[(size_t)ti * m + c];
-          continue;
-        }
-        float ubsum = 0.0f;
-        for (uint32_t c = 0; c < m; ++c) ubsum += ub[c];
-        for (uint32_t c = 0; c < m; ++c) {
-          const uint64_t p0 = cur[c], p1 = p0 + tcnt[(size_t)ti * m + c];
-          cur[c] = p1;
-          if (!((ess >> c) & 1u)) continue;
-          for (uint64_t p = p0; p < p1; ++p) {
-            stream += 8.0;
-            const uint32_t d = hd[p];
-            // bound 1: the other clauses' 512-doc sub-tile maxima (k_disj keeps
-            // them as q / 255 of the tile bound, rounded up: modelled exactly)
-            float b1 = psc[p];
-            for (uint32_t c2 = 0; c2 < m; ++c2) {
-              if (c2 == c) continue;
-              const float tu = ub[c2], sx = smx[(size_t)(d >> fg::kSubShift) * m + c2];
-              float v = tu;
-              if (fg::kDisjSubBounds && tu > 0.0f && (ix->tmeta[t[c2]] & 0xFFu) <= fg::kDisjTileShift) {
-                uint32_t qq = std::min(255u, (uint32_t)std::ceil(sx * 255.0f / tu));
-                while (qq < 255u && tu * ((float)qq * (1.0f / 255.0f)) < sx) ++qq;
-                v = qq >= 255u ? tu : tu * ((float)qq * (1.0f / 255.0f));
-              }
-              b1 += v;
-            }
-            (void)ubsum;
-            if (fg::make_key(b1 * 1.00000762939453125f, d) < thk) continue;
-            float pb = psc[p];
-            bool all_dense = true;
-            for (uint32_t c2 = 0; c2 < m; ++c2) {
-              if (c2 == c || !tcnt[(size_t)ti * m + c2]) continue;
-              const uint32_t meta = ix->tmeta[t[c2]];
-              const bool rank = fg::meta_slot(meta) && fg::meta_rank(meta);
-              const bool here = (pres[(size_t)c2 * ((N + 63) / 64) + (d >> 6)] >> (d & 63)) & 1ull;
-              probe += rank ? 8.0 : 4.0;
-              all_dense = all_dense && fg::meta_slot(meta);
-              if (here) pb += ub[c2];
-            }
-            if (fg::make_key(pb * 1.00000762939453125f, d) < thk) continue;
-            for (uint32_t c2 = 0; c2 < m; ++c2) {
-              if (c2 == c || !tcnt[(size_t)ti * m + c2]) continue;
-              const uint32_t meta = ix->tmeta[t[c2]];
-              const bool here = (pres[(size_t)c2 * ((N + 63) / 64) + (d >> 6)] >> (d & 63)) & 1ull;
-              if (fg::meta_slot(meta) && fg::meta_rank(meta)) probe += here ? 4.0 : 0.0;
-              else if (!all_dense && !fg::meta_slot(meta)) {
-                const uint32_t S = (meta >> 8) & 0xFFu;
-                probe += 8.0 + 4.0 * S + 4.0 + (here ? 4.0 : 0.0);
-              }
-            }
-          }
-        }
-      }
-      o[0] = stream;
-      o[1] = probe;
-      o[2] = 8.0 * k;
-      o[3] = stream + probe + o[2];
-    }
-  });
-  if (bad) return fail(FG_EINVAL, "bad query batch");
   return FG_OK;
 }
 

@@ -4,13 +4,17 @@
 // reference's Rust toolchain is absent.  Reference citations
 // are on each function.
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cctype>
 #include <cinttypes>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -650,13 +654,25 @@ struct Doc {
   std::vector<uint32_t> facet_tok;   // FacetTokenizer tokens of all of them (facet dictionary ids)
 };
 
+// One segment's share of the namespace statistics: tantivy's Searcher sums
+// max_doc, total_num_tokens and doc_freq over the segments (deleted docs
+// included until a merge drops them).  doc_freq as (term, count) pairs.
+struct SegStats {
+  uint64_t n = 0, tot[2] = {0, 0}, tot_f = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> df_t, df_n, df_f;
+};
+
 // A committed view of a namespace: tantivy's segments, one per commit
-// (src/db/document.rs:65) until kMaxSegments, then merged into one (the merge
-// policy's job).  Every segment scores with the namespace-wide statistics.
+// (src/db/document.rs:65), in global doc order; the background merger
+// (tantivy's merge threads, IndexWriter at src/db/core.rs:247-249) replaces
+// contiguous runs of small segments by one.  Every segment scores with the
+// namespace-wide statistics.
 struct Segment {
   fg_index* ix = nullptr;
   uint32_t base = 0, n = 0;  // global doc ids [base, base + n) ...
   std::shared_ptr<const std::vector<uint32_t>> gid;  // ... or, for a merged segment, gid[local doc]
+  uint64_t id = 0;                                   // stable across rescores (the merger finds its sources)
+  std::shared_ptr<const SegStats> st;
   uint32_t global(uint32_t d) const { return gid ? (*gid)[d] : base + d; }
 };
 struct Snapshot {
@@ -666,12 +682,14 @@ struct Snapshot {
       if (s.ix) fg_index_release(s.ix);
   }
 };
-constexpr size_t kMaxSegments = 8;
+constexpr size_t kMaxSegments = 8;    // more segments than this: the merger takes a run of small ones
+constexpr size_t kHardSegments = 48;  // ... and a commit that would pass this waits for a merge first
 
 struct Namespace {
   std::string name;
   std::mutex writer;                                   // IndexWriter lock (src/db/core.rs:211)
-  std::mutex committer;                                // serialises commits (snapshot order)
+  std::mutex committer;                                // serialises commits and merge swaps (snapshot order)
+  std::mutex merging;                                  // one merge of this namespace at a time
   std::vector<Doc> docs;                               // global doc id = insertion order
   std::unordered_map<std::string, uint32_t> dict;      // term dictionary (text and name tokens)
   std::unordered_map<std::string, uint32_t> fdict;     // facet dictionary (encoded facet terms)
@@ -679,12 +697,19 @@ struct Namespace {
   std::shared_ptr<Snapshot> snap;                      // committed device snapshot
   std::shared_mutex snap_mu;
   size_t committed_docs = 0;
-  // BM25 statistics of the committed segments, deleted docs included (tantivy's
-  // Searcher counts them until a merge drops them): N, token totals, doc
-  // frequencies.  Updated with each commit's new docs only; recomputed from the
-  // alive docs when segments merge.
-  uint64_t st_n = 0, st_tot[2] = {0, 0}, st_tot_f = 0;
+  uint64_t next_seg = 1;
+  // BM25 statistics of the committed segments (the sum of their SegStats),
+  // deleted docs included: N, token totals, doc frequencies.  Written under the
+  // writer lock together with the snapshot; st_ver counts the changes.
+  uint64_t st_n = 0, st_tot[2] = {0, 0}, st_tot_f = 0, st_ver = 0;
   std::vector<uint32_t> st_df_text, st_df_name, st_df_facet;
+  // merger bookkeeping
+  std::mutex mq;
+  std::condition_variable mq_cv;
+  bool queued = false, running = false;
+  uint64_t merges = 0, merged_docs = 0;
+  double merge_ms_total = 0, merge_ms_last = 0, merge_ms_max = 0;
+  std::string merge_error;
 };
 
 }  // namespace
@@ -695,6 +720,20 @@ struct fg_db {
   std::string default_ns;
   std::map<std::string, std::shared_ptr<Namespace>> ns;
   std::shared_mutex mu;
+  // the background merger: one thread per db working through queued namespaces
+  std::thread merger;
+  std::mutex mq;
+  std::condition_variable mq_cv;
+  std::deque<std::weak_ptr<Namespace>> queue;
+  bool stop = false;
+  ~fg_db() {
+    {
+      std::lock_guard<std::mutex> l(mq);
+      stop = true;
+    }
+    mq_cv.notify_all();
+    if (merger.joinable()) merger.join();
+  }
 };
 
 namespace {
@@ -1147,6 +1186,450 @@ int upsert_record(fg_db* db, const char* nsname, const fg_object_record* r, cons
   return FG_OK;
 }
 
+// ---------------------------------------------------------------- commits and merges
+// FIELD_NORMS_TABLE (fieldnorm/code.rs): 0..40 exactly, then groups of 8 with a
+// doubling step; a length is stored as the largest entry <= it.
+uint64_t quantized_len(uint64_t n) {
+  static const std::vector<uint64_t> t = [] {
+    std::vector<uint64_t> v;
+    for (uint64_t i = 0; i <= 40; ++i) v.push_back(i);
+    uint64_t x = 40, step = 2;
+    while (v.size() < 256) {
+      for (int j = 0; j < 8 && v.size() < 256; ++j) v.push_back(x += step);
+      step <<= 1;
+    }
+    return v;
+  }();
+  return *(std::upper_bound(t.begin(), t.end(), n) - 1);
+}
+
+// the distinct terms of a doc counted once into df
+void count_distinct(const std::vector<uint32_t>& toks, std::vector<uint32_t>& scratch, std::vector<uint32_t>& df) {
+  scratch = toks;
+  std::sort(scratch.begin(), scratch.end());
+  scratch.erase(std::unique(scratch.begin(), scratch.end()), scratch.end());
+  for (uint32_t t : scratch) df[t]++;
+}
+
+std::vector<std::pair<uint32_t, uint32_t>> sparse_of(const std::vector<uint32_t>& df) {
+  std::vector<std::pair<uint32_t, uint32_t>> v;
+  for (uint32_t t = 0; t < df.size(); ++t)
+    if (df[t]) v.emplace_back(t, df[t]);
+  return v;
+}
+
+void df_add(std::vector<uint32_t>& df, const std::vector<std::pair<uint32_t, uint32_t>>& sp, bool sub) {
+  for (auto& e : sp) {
+    if (e.first >= df.size()) df.resize(e.first + 1, 0);
+    df[e.first] = sub ? df[e.first] - e.second : df[e.first] + e.second;
+  }
+}
+
+// Dense namespace statistics in local copies (fg_global_stats points into them).
+struct Stats {
+  uint64_t n = 0, tot[2] = {0, 0}, tot_f = 0;
+  std::vector<uint32_t> df_t, df_n, df_f;
+  void load(const Namespace& ns, uint32_t n_terms, uint32_t n_fterms) {
+    n = ns.st_n;
+    tot[0] = ns.st_tot[0];
+    tot[1] = ns.st_tot[1];
+    tot_f = ns.st_tot_f;
+    df_t = ns.st_df_text;
+    df_n = ns.st_df_name;
+    df_f = ns.st_df_facet;
+    df_t.resize(n_terms, 0);
+    df_n.resize(n_terms, 0);
+    df_f.resize(n_fterms, 0);
+  }
+  void add(const SegStats& s, bool sub) {
+    n = sub ? n - s.n : n + s.n;
+    tot[0] = sub ? tot[0] - s.tot[0] : tot[0] + s.tot[0];
+    tot[1] = sub ? tot[1] - s.tot[1] : tot[1] + s.tot[1];
+    tot_f = sub ? tot_f - s.tot_f : tot_f + s.tot_f;
+    df_add(df_t, s.df_t, sub);
+    df_add(df_n, s.df_n, sub);
+    df_add(df_f, s.df_f, sub);
+  }
+  fg_global_stats global() const {
+    fg_global_stats g{};
+    g.n_docs = n;
+    g.tot_tokens[0] = tot[0];
+    g.tot_tokens[1] = tot[1];
+    g.df_text = df_t.data();
+    g.df_name = df_n.data();
+    g.df_facet = df_f.empty() ? nullptr : df_f.data();
+    g.tot_facet_tokens = tot_f;
+    return g;
+  }
+  void store(Namespace& ns) {  // under the writer lock
+    ns.st_n = n;
+    ns.st_tot[0] = tot[0];
+    ns.st_tot[1] = tot[1];
+    ns.st_tot_f = tot_f;
+    ns.st_df_text = df_t;
+    ns.st_df_name = df_n;
+    ns.st_df_facet = df_f;
+    ns.st_ver++;
+  }
+};
+
+// The docs `ids` (global, in order) as fg_docs_input arrays
+struct DocsBuf {
+  std::vector<uint64_t> toff{0}, noff{0}, foff{0};
+  std::vector<uint32_t> ttok, ntok, ftok;
+  std::vector<uint8_t> del;
+  bool any_name = false, any_del = false;
+  void add(const Doc& d, bool deleted) {
+    ttok.insert(ttok.end(), d.text_tok.begin(), d.text_tok.end());
+    ntok.insert(ntok.end(), d.name_tok.begin(), d.name_tok.end());
+    ftok.insert(ftok.end(), d.facet_tok.begin(), d.facet_tok.end());
+    toff.push_back(ttok.size());
+    noff.push_back(ntok.size());
+    foff.push_back(ftok.size());
+    any_name |= !d.name_tok.empty();
+    del.push_back(deleted ? 1 : 0);
+    any_del |= deleted;
+  }
+  fg_docs_input input(uint32_t n_terms, uint32_t n_fterms, bool with_name) const {
+    fg_docs_input in{};
+    in.n_docs = (uint32_t)del.size();
+    in.n_terms = n_terms;
+    in.text_off = toff.data();
+    in.text_tok = ttok.data();
+    in.name_off = with_name ? noff.data() : nullptr;
+    in.name_tok = with_name ? ntok.data() : nullptr;
+    in.deleted = any_del ? del.data() : nullptr;
+    in.threads = 0;
+    in.keep_host_postings = 0;
+    in.n_facet_terms = n_fterms;
+    in.facet_off = n_fterms ? foff.data() : nullptr;
+    in.facet_tok = n_fterms ? ftok.data() : nullptr;
+    return in;
+  }
+};
+
+// every segment of `segs` rescored with g and the current deleted flags
+// (`del`, global); appended to out.  Returns an error code (out then owns the
+// ones made so far).
+int rescore_into(const std::vector<Segment>& segs, const fg_global_stats& g, const std::vector<uint8_t>& del,
+                 std::vector<Segment>& out) {
+  std::vector<uint8_t> sdel;
+  for (const Segment& s0 : segs) {
+    sdel.assign(s0.n, 0);
+    bool sany = false;
+    for (uint32_t d = 0; d < s0.n; ++d) sany |= (sdel[d] = del[s0.global(d)]) != 0;
+    fg_index* re = nullptr;
+    if (int rc = fg_index_rescore(s0.ix, &g, sany ? sdel.data() : nullptr, &re)) return hfail(rc, fg_last_error());
+    Segment x = s0;
+    x.ix = re;
+    out.push_back(std::move(x));
+  }
+  return FG_OK;
+}
+
+// A commit: the docs since the last one as a new segment (the first commit:
+// every doc, deleted ones included), the older segments rescored with the new
+// statistics.  The statistics and the snapshot change together, only when
+// every step succeeded.
+int commit_segment(fg_db* db, Namespace& ns) {
+  std::lock_guard<std::mutex> c(ns.committer);
+  std::shared_ptr<Snapshot> cur;
+  {
+    std::shared_lock<std::shared_mutex> l(ns.snap_mu);
+    cur = ns.snap;
+  }
+  // gather under the writer lock, build outside it so searches (doc fetch) and
+  // upserts are not blocked by the device work
+  std::unique_lock<std::mutex> w(ns.writer);
+  const uint32_t N = (uint32_t)ns.docs.size();
+  const uint32_t old = cur ? (uint32_t)ns.committed_docs : 0;
+  if (N == 0 || (N == old && cur)) return FG_OK;
+  const uint32_t n_terms = std::max<uint32_t>(1, (uint32_t)ns.dict.size());
+  const uint32_t n_fterms = (uint32_t)ns.fdict.size();
+  DocsBuf buf;
+  auto st = std::make_shared<SegStats>();
+  std::vector<uint32_t> dt(n_terms, 0), dn(n_terms, 0), dfc(n_fterms, 0), scratch;
+  for (uint32_t d = old; d < N; ++d) {
+    const Doc& doc = ns.docs[d];
+    buf.add(doc, doc.deleted);
+    st->n++;
+    st->tot[0] += doc.text_tok.size();
+    st->tot[1] += doc.name_tok.size();
+    st->tot_f += doc.facet_tok.size();
+    count_distinct(doc.text_tok, scratch, dt);
+    count_distinct(doc.name_tok, scratch, dn);
+    count_distinct(doc.facet_tok, scratch, dfc);
+  }
+  st->df_t = sparse_of(dt);
+  st->df_n = sparse_of(dn);
+  st->df_f = sparse_of(dfc);
+  bool any_name = buf.any_name;
+  for (uint32_t d = 0; d < old && !any_name; ++d) any_name |= !ns.docs[d].name_tok.empty();
+  std::vector<uint8_t> del(N, 0);
+  for (uint32_t d = 0; d < N; ++d) del[d] = ns.docs[d].deleted ? 1 : 0;
+  Stats S;
+  S.load(ns, n_terms, n_fterms);
+  S.add(*st, false);
+  w.unlock();
+  const fg_global_stats g = S.global();
+  const fg_docs_input in = buf.input(n_terms, n_fterms, any_name);
+  auto snap = std::make_shared<Snapshot>();
+  if (cur)
+    if (int rc = rescore_into(cur->segs, g, del, snap->segs)) return rc;  // snap releases the rescored ones
+  if (const char* f = getenv("FUGU_FAULT_INJECT"))  // tests only: a commit whose device build fails
+    if (std::strcmp(f, "commit_build") == 0) return hfail(FG_EHIP, "injected fault: segment build");
+  fg_index* ix = nullptr;
+  if (int rc = fg_index_build_from_docs_global(db->ctx, db->dev, &in, &g, &ix)) return hfail(rc, fg_last_error());
+  {
+    std::lock_guard<std::mutex> w2(ns.writer);  // the statistics are read under the writer lock
+    snap->segs.push_back(Segment{ix, old, N - old, nullptr, ns.next_seg++, st});
+    std::unique_lock<std::shared_mutex> l(ns.snap_mu);  // readers keep the old snapshot (refcount)
+    ns.snap = snap;
+    ns.committed_docs = N;
+    S.store(ns);
+  }
+  return FG_OK;
+}
+
+// The merge policy (tantivy's LogMergePolicy keeps segments of similar size
+// together; here runs stay contiguous so the merged segment keeps global doc
+// order, which merge_fruits' (segment, doc) tie order needs): with more than
+// kMaxSegments segments, the newest (two or more) segments that together hold
+// at most half the docs of the segment before them; else the newest run of
+// segments of one size level (factor 4); else, from 2 x kMaxSegments segments
+// on, the two newest.  Returns [j0, j1) or j0 == j1 (nothing to merge).
+std::pair<size_t, size_t> pick_merge(const std::vector<uint64_t>& n) {
+  const size_t c = n.size();
+  if (c <= kMaxSegments) return {c, c};
+  std::vector<uint64_t> suffix(c + 1, 0);
+  for (size_t j = c; j-- > 0;) suffix[j] = suffix[j + 1] + n[j];
+  for (size_t j = 1; j + 2 <= c; ++j)
+    if (2 * suffix[j] <= n[j - 1]) return {j, c};
+  auto level = [](uint64_t x) {
+    uint32_t l = 0;
+    while (x >= 4) { x >>= 2; ++l; }
+    return l;
+  };
+  size_t j = c - 1;
+  while (j > 0 && level(n[j - 1]) == level(n[c - 1])) --j;
+  if (c - j >= 2) return {j, c};
+  if (c >= 2 * kMaxSegments) return {c - 2, c};  // rare: one small segment after big ones, repeatedly
+  return {c, c};
+}
+
+// One merge of a run of segments into one, as a tantivy merge does it: the
+// deleted docs are dropped (N and doc_freq then count the alive docs), and the
+// merged total_num_tokens is, per source segment, its own total when it has no
+// deletes, else the sum over its alive docs of their quantized field lengths
+// (FIELD_NORMS_TABLE[fieldnorm_id]; a field without fieldnorms -- the facet
+// field -- counts 1 per alive doc) (merger.rs compute_total_num_tokens).
+// The merged segment is built outside the locks; the swap re-checks what
+// commits did meanwhile (new statistics, new deletions) and rescores.
+int merge_once(fg_db* db, Namespace& ns, bool* did) {
+  *did = false;
+  std::lock_guard<std::mutex> mg(ns.merging);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::shared_ptr<Snapshot> cur;
+  {
+    std::shared_lock<std::shared_mutex> l(ns.snap_mu);
+    cur = ns.snap;
+  }
+  if (!cur) return FG_OK;
+  std::vector<uint64_t> sizes;
+  for (auto& sg : cur->segs) sizes.push_back(sg.n);
+  const auto run = pick_merge(sizes);
+  if (run.first >= run.second) return FG_OK;
+  const std::vector<Segment> src(cur->segs.begin() + run.first, cur->segs.begin() + run.second);
+  // ---- gather the run's alive docs and the merged statistics
+  DocsBuf buf;
+  auto mst = std::make_shared<SegStats>();
+  std::vector<uint32_t> ids;
+  Stats S;
+  uint64_t ver0 = 0;
+  uint32_t n_terms = 0, n_fterms = 0;
+  bool any_name = false;
+  {
+    std::lock_guard<std::mutex> w(ns.writer);
+    n_terms = std::max<uint32_t>(1, (uint32_t)ns.dict.size());
+    n_fterms = (uint32_t)ns.fdict.size();
+    std::vector<uint32_t> dt(n_terms, 0), dn(n_terms, 0), dfc(n_fterms, 0), scratch;
+    for (const Segment& sg : src) {
+      bool has_del = false;
+      for (uint32_t d = 0; d < sg.n && !has_del; ++d) has_del = ns.docs[sg.global(d)].deleted;
+      if (!has_del) {
+        mst->tot[0] += sg.st->tot[0];
+        mst->tot[1] += sg.st->tot[1];
+        mst->tot_f += sg.st->tot_f;
+      }
+      for (uint32_t d = 0; d < sg.n; ++d) {
+        const uint32_t gd = sg.global(d);
+        const Doc& doc = ns.docs[gd];
+        if (doc.deleted) continue;
+        ids.push_back(gd);
+        buf.add(doc, false);
+        mst->n++;
+        if (has_del) {
+          mst->tot[0] += quantized_len(doc.text_tok.size());
+          mst->tot[1] += quantized_len(doc.name_tok.size());
+          mst->tot_f += 1;
+        }
+        count_distinct(doc.text_tok, scratch, dt);
+        count_distinct(doc.name_tok, scratch, dn);
+        count_distinct(doc.facet_tok, scratch, dfc);
+      }
+    }
+    mst->df_t = sparse_of(dt);
+    mst->df_n = sparse_of(dn);
+    mst->df_f = sparse_of(dfc);
+    for (auto& d : ns.docs)
+      if (!d.name_tok.empty()) { any_name = true; break; }
+    S.load(ns, n_terms, n_fterms);
+    for (const Segment& sg : src) S.add(*sg.st, true);
+    S.add(*mst, false);
+    ver0 = ns.st_ver;
+  }
+  fg_index* mix = nullptr;
+  if (!ids.empty()) {
+    const fg_global_stats g = S.global();
+    const fg_docs_input in = buf.input(n_terms, n_fterms, any_name);
+    if (int rc = fg_index_build_from_docs_global(db->ctx, db->dev, &in, &g, &mix)) return hfail(rc, fg_last_error());
+  }
+  if (const char* e = getenv("FUGU_MERGE_DELAY_MS"))  // tests only: searches run while the merge is in flight
+    std::this_thread::sleep_for(std::chrono::milliseconds(atoi(e)));
+  // ---- swap: no commit runs meanwhile
+  std::lock_guard<std::mutex> c(ns.committer);
+  std::shared_ptr<Snapshot> now;
+  {
+    std::shared_lock<std::shared_mutex> l(ns.snap_mu);
+    now = ns.snap;
+  }
+  size_t j0 = now->segs.size();
+  for (size_t j = 0; j < now->segs.size(); ++j)
+    if (now->segs[j].id == src[0].id) { j0 = j; break; }
+  bool same = j0 + src.size() <= now->segs.size();
+  for (size_t i = 0; same && i < src.size(); ++i) same = now->segs[j0 + i].id == src[i].id;
+  if (!same) {  // only the merger removes segments: cannot happen
+    if (mix) fg_index_release(mix);
+    return hfail(FG_EINVAL, "merge sources vanished from the snapshot");
+  }
+  uint64_t src_n = 0;
+  for (const Segment& sg : src) src_n += sg.n;
+  const bool stats_change = ids.size() != src_n;  // deleted docs dropped (their N, df and tokens go)
+  std::vector<uint8_t> del, mdel(ids.size(), 0);
+  bool new_del = false, moved = false;
+  {
+    std::lock_guard<std::mutex> w(ns.writer);
+    moved = ns.st_ver != ver0;  // commits since the gather: other statistics
+    if (moved) {
+      const uint32_t nt = std::max<uint32_t>(1, (uint32_t)ns.dict.size()), nf = (uint32_t)ns.fdict.size();
+      S = Stats();
+      S.load(ns, nt, nf);
+      for (const Segment& sg : src) S.add(*sg.st, true);
+      S.add(*mst, false);
+    }
+    for (size_t i = 0; i < ids.size(); ++i) new_del |= (mdel[i] = ns.docs[ids[i]].deleted ? 1 : 0) != 0;
+    del.resize(ns.docs.size());
+    for (size_t d = 0; d < ns.docs.size(); ++d) del[d] = ns.docs[d].deleted ? 1 : 0;
+  }
+  const fg_global_stats g = S.global();
+  if (mix && (moved || new_del || stats_change)) {
+    fg_index* re = nullptr;
+    const int rc = fg_index_rescore(mix, &g, new_del ? mdel.data() : nullptr, &re);
+    fg_index_release(mix);
+    if (rc) return hfail(rc, fg_last_error());
+    mix = re;
+  }
+  auto snap = std::make_shared<Snapshot>();
+  const std::vector<Segment> before(now->segs.begin(), now->segs.begin() + j0),
+      after(now->segs.begin() + j0 + src.size(), now->segs.end());
+  auto keep = [&](const std::vector<Segment>& v) -> int {
+    if (stats_change) return rescore_into(v, g, del, snap->segs);  // N / df changed: every segment rescores
+    for (const Segment& sg : v) {
+      fg_index_retain(sg.ix);
+      snap->segs.push_back(sg);
+    }
+    return FG_OK;
+  };
+  if (int rc = keep(before)) {
+    if (mix) fg_index_release(mix);
+    return rc;
+  }
+  if (mix) {
+    Segment m{mix, 0, (uint32_t)ids.size(), nullptr, 0, mst};
+    if (ids.back() - ids.front() + 1 == ids.size()) m.base = ids.front();  // contiguous: no id table
+    else m.gid = std::make_shared<const std::vector<uint32_t>>(ids);
+    snap->segs.push_back(std::move(m));
+  }
+  if (int rc = keep(after)) return rc;
+  {
+    std::lock_guard<std::mutex> w(ns.writer);
+    if (mix) snap->segs[before.size()].id = ns.next_seg++;
+    std::unique_lock<std::shared_mutex> l(ns.snap_mu);
+    ns.snap = snap;
+    if (stats_change || moved) S.store(ns);
+  }
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  {
+    std::lock_guard<std::mutex> l(ns.mq);
+    ns.merges++;
+    ns.merged_docs += ids.size();
+    ns.merge_ms_total += ms;
+    ns.merge_ms_last = ms;
+    ns.merge_ms_max = std::max(ns.merge_ms_max, ms);
+  }
+  *did = true;
+  return FG_OK;
+}
+
+void merger_main(fg_db* db) {
+  for (;;) {
+    std::shared_ptr<Namespace> ns;
+    {
+      std::unique_lock<std::mutex> l(db->mq);
+      db->mq_cv.wait(l, [&] { return db->stop || !db->queue.empty(); });
+      if (db->stop) return;
+      ns = db->queue.front().lock();
+      db->queue.pop_front();
+    }
+    if (!ns) continue;
+    {
+      std::lock_guard<std::mutex> l(ns->mq);
+      ns->queued = false;
+      ns->running = true;
+    }
+    std::string err;
+    for (;;) {
+      bool did = false;
+      if (merge_once(db, *ns, &did)) {
+        err = fg_last_error();
+        break;
+      }
+      std::lock_guard<std::mutex> l(db->mq);
+      if (!did || db->stop) break;
+    }
+    {
+      std::lock_guard<std::mutex> l(ns->mq);
+      ns->running = false;
+      if (!err.empty()) ns->merge_error = err;
+    }
+    ns->mq_cv.notify_all();
+  }
+}
+
+void enqueue_merge(fg_db* db, const std::shared_ptr<Namespace>& ns) {
+  {
+    std::lock_guard<std::mutex> l(ns->mq);
+    if (ns->queued) return;
+    ns->queued = true;
+  }
+  {
+    std::lock_guard<std::mutex> l(db->mq);
+    db->queue.push_back(ns);
+    if (!db->merger.joinable()) db->merger = std::thread(merger_main, db);
+  }
+  db->mq_cv.notify_one();
+}
+
 }  // namespace
 
 extern "C" {
@@ -1168,140 +1651,87 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   // IndexWriter::commit (src/db/document.rs:65): the docs upserted since the
   // last commit become a new segment; the namespace statistics change, so the
   // older segments are rescored on the device (fg_index_rescore: their postings
-  // stay where they are) and pick up the new deletions.  Past kMaxSegments the
-  // alive docs are rebuilt into one segment (the merge policy): like a tantivy
-  // merge, it drops the deleted docs, so N, df and token totals are recomputed
-  // from the alive docs, and the merged segment keeps their global order.
-  // Readers keep the snapshot they hold (refcounted).  The namespace's
-  // statistics and snapshot change together, only when every step succeeded.
+  // stay where they are) and pick up the new deletions.  Merges run on the
+  // background merger (merge_once); a commit waits for one only when the
+  // namespace holds kHardSegments segments.
   if (!db) return hfail(FG_EINVAL, "bad arguments");
   auto ns = find_ns(db, nsname);
   if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
   if (!db->ctx) return hfail(FG_ENODEV, "fg_db created without a device context");
-  std::lock_guard<std::mutex> c(ns->committer);
-  std::shared_ptr<Snapshot> cur;
+  size_t nseg = 0;
   {
     std::shared_lock<std::shared_mutex> l(ns->snap_mu);
-    cur = ns->snap;
+    nseg = ns->snap ? ns->snap->segs.size() : 0;
   }
-  // gather under the writer lock, build outside it so searches (doc fetch) and
-  // upserts are not blocked by the device work
-  std::unique_lock<std::mutex> w(ns->writer);
-  const uint32_t N = (uint32_t)ns->docs.size();
-  const uint32_t old = (uint32_t)ns->committed_docs;
-  if (N == 0 || (N == old && cur)) return FG_OK;
-  const bool merge = !cur || cur->segs.size() + 1 > kMaxSegments;
-  // docs of the segment to build (global ids): the new ones, or every alive one on a merge
-  // (the first commit keeps its deleted docs: no merge has dropped them yet)
-  std::vector<uint32_t> build_ids;
-  for (uint32_t d = merge ? 0 : old; d < N; ++d)
-    if (!cur || !merge || !ns->docs[d].deleted) build_ids.push_back(d);
-  const uint32_t nb = (uint32_t)build_ids.size();
-  const uint32_t n_terms = std::max<uint32_t>(1, (uint32_t)ns->dict.size());
-  const uint32_t n_fterms = (uint32_t)ns->fdict.size();
-  std::vector<uint64_t> toff(nb + 1, 0), noff(nb + 1, 0), foff(nb + 1, 0);
-  std::vector<uint32_t> ttok, ntok, ftok;
-  std::vector<uint8_t> del(N, 0), bdel(nb, 0);
-  bool any_name = false, any_del = false;
-  for (uint32_t d = 0; d < N; ++d) {
-    del[d] = ns->docs[d].deleted ? 1 : 0;
-    any_del |= ns->docs[d].deleted;
+  if (nseg + 1 > kHardSegments) {
+    bool did = false;
+    if (int rc = merge_once(db, *ns, &did)) return rc;
   }
-  // statistics after this commit, in local copies
-  uint64_t st_n = merge ? 0 : ns->st_n, st_tot[2] = {merge ? 0 : ns->st_tot[0], merge ? 0 : ns->st_tot[1]};
-  uint64_t st_tot_f = merge ? 0 : ns->st_tot_f;
-  std::vector<uint32_t> df_t, df_n, df_f;
-  if (!merge) { df_t = ns->st_df_text; df_n = ns->st_df_name; df_f = ns->st_df_facet; }
-  df_t.resize(n_terms, 0);
-  df_n.resize(n_terms, 0);
-  df_f.resize(n_fterms, 0);
-  std::vector<uint32_t> sc;
-  auto distinct = [&](const std::vector<uint32_t>& v, std::vector<uint32_t>& df) {
-    sc = v;
-    std::sort(sc.begin(), sc.end());
-    sc.erase(std::unique(sc.begin(), sc.end()), sc.end());
-    for (uint32_t t : sc) df[t]++;
-  };
-  bool built_del = false;
-  for (uint32_t i = 0; i < nb; ++i) {
-    const Doc& doc = ns->docs[build_ids[i]];
-    ttok.insert(ttok.end(), doc.text_tok.begin(), doc.text_tok.end());
-    ntok.insert(ntok.end(), doc.name_tok.begin(), doc.name_tok.end());
-    ftok.insert(ftok.end(), doc.facet_tok.begin(), doc.facet_tok.end());
-    toff[i + 1] = ttok.size();
-    noff[i + 1] = ntok.size();
-    foff[i + 1] = ftok.size();
-    any_name |= !doc.name_tok.empty();
-    bdel[i] = doc.deleted ? 1 : 0;
-    built_del |= doc.deleted;
-    // namespace statistics += this segment's docs (distinct terms per doc per field)
-    st_n++;
-    st_tot[0] += doc.text_tok.size();
-    st_tot[1] += doc.name_tok.size();
-    st_tot_f += doc.facet_tok.size();
-    distinct(doc.text_tok, df_t);
-    distinct(doc.name_tok, df_n);
-    distinct(doc.facet_tok, df_f);
-  }
-  if (!merge)
-    for (uint32_t d = 0; d < old && !any_name; ++d) any_name |= !ns->docs[d].name_tok.empty();
-  w.unlock();
-  fg_global_stats g{};
-  g.n_docs = st_n;
-  g.tot_tokens[0] = st_tot[0];
-  g.tot_tokens[1] = st_tot[1];
-  g.df_text = df_t.data();
-  g.df_name = df_n.data();
-  g.df_facet = n_fterms ? df_f.data() : nullptr;
-  g.tot_facet_tokens = st_tot_f;
-  fg_docs_input in{};
-  in.n_docs = nb;
-  in.n_terms = n_terms;
-  in.text_off = toff.data();
-  in.text_tok = ttok.data();
-  in.name_off = any_name ? noff.data() : nullptr;
-  in.name_tok = any_name ? ntok.data() : nullptr;
-  in.deleted = built_del ? bdel.data() : nullptr;
-  in.threads = 0;
-  in.keep_host_postings = 0;
-  in.n_facet_terms = n_fterms;
-  in.facet_off = n_fterms ? foff.data() : nullptr;
-  in.facet_tok = n_fterms ? ftok.data() : nullptr;
-  auto snap = std::make_shared<Snapshot>();
-  if (!merge) {
-    std::vector<uint8_t> sdel;
-    for (const Segment& s0 : cur->segs) {
-      // this segment's deleted flags in its own doc order
-      sdel.assign(s0.n, 0);
-      bool sany = false;
-      for (uint32_t d = 0; d < s0.n; ++d) sany |= (sdel[d] = del[s0.global(d)]) != 0;
-      fg_index* re = nullptr;
-      int rc = fg_index_rescore(s0.ix, &g, sany ? sdel.data() : nullptr, &re);
-      if (rc) return hfail(rc, fg_last_error());  // snap releases the rescored ones
-      snap->segs.push_back(Segment{re, s0.base, s0.n, s0.gid});
-    }
-  }
-  if (const char* f = getenv("FUGU_FAULT_INJECT"))  // tests only: a commit whose device build fails
-    if (std::strcmp(f, "commit_build") == 0) return hfail(FG_EHIP, "injected fault: segment build");
-  fg_index* ix = nullptr;
-  int rc = fg_index_build_from_docs_global(db->ctx, db->dev, &in, &g, &ix);
-  if (rc) return hfail(rc, fg_last_error());
-  Segment ns_seg{ix, merge ? 0u : old, nb, nullptr};
-  if (merge && nb != N) ns_seg.gid = std::make_shared<const std::vector<uint32_t>>(std::move(build_ids));
-  snap->segs.push_back(std::move(ns_seg));
+  if (int rc = commit_segment(db, *ns)) return rc;
   {
-    std::lock_guard<std::mutex> w2(ns->writer);  // the statistics are read under the writer lock
-    std::unique_lock<std::shared_mutex> l(ns->snap_mu);  // readers keep the old snapshot (refcount)
-    ns->snap = snap;
-    ns->committed_docs = N;
-    ns->st_n = st_n;
-    ns->st_tot[0] = st_tot[0];
-    ns->st_tot[1] = st_tot[1];
-    ns->st_tot_f = st_tot_f;
-    ns->st_df_text.swap(df_t);
-    ns->st_df_name.swap(df_n);
-    ns->st_df_facet.swap(df_f);
+    std::shared_lock<std::shared_mutex> l(ns->snap_mu);
+    nseg = ns->snap ? ns->snap->segs.size() : 0;
   }
+  if (nseg > kMaxSegments) enqueue_merge(db, ns);
+  return FG_OK;
+}
+
+int fg_db_merge_wait(fg_db* db, const char* nsname) {
+  if (!db) return hfail(FG_EINVAL, "bad arguments");
+  auto ns = find_ns(db, nsname);
+  if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
+  std::unique_lock<std::mutex> l(ns->mq);
+  ns->mq_cv.wait(l, [&] { return !ns->queued && !ns->running; });
+  if (!ns->merge_error.empty()) {
+    const std::string e = ns->merge_error;
+    ns->merge_error.clear();
+    return hfail(FG_EHIP, "background merge failed: " + e);
+  }
+  return FG_OK;
+}
+
+int fg_db_merge_info_get(fg_db* db, const char* nsname, fg_merge_info* out) {
+  if (!db || !out) return hfail(FG_EINVAL, "bad arguments");
+  auto ns = find_ns(db, nsname);
+  if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
+  std::memset(out, 0, sizeof *out);
+  {
+    std::lock_guard<std::mutex> l(ns->mq);
+    out->merges = ns->merges;
+    out->merged_docs = ns->merged_docs;
+    out->merge_ms_total = ns->merge_ms_total;
+    out->merge_ms_last = ns->merge_ms_last;
+    out->merge_ms_max = ns->merge_ms_max;
+    out->pending = (ns->queued || ns->running) ? 1 : 0;
+  }
+  std::shared_ptr<Snapshot> snap;
+  {
+    std::shared_lock<std::shared_mutex> l(ns->snap_mu);
+    snap = ns->snap;
+  }
+  out->segments = snap ? (uint32_t)snap->segs.size() : 0;
+  std::lock_guard<std::mutex> w(ns->writer);
+  out->n_docs_stats = ns->st_n;
+  out->tot_tokens[0] = ns->st_tot[0];
+  out->tot_tokens[1] = ns->st_tot[1];
+  out->tot_facet_tokens = ns->st_tot_f;
+  return FG_OK;
+}
+
+int fg_db_segment_docs(fg_db* db, const char* nsname, uint32_t seg, uint32_t* out, uint32_t cap, uint32_t* n) {
+  if (!db || !n) return hfail(FG_EINVAL, "bad arguments");
+  auto ns = find_ns(db, nsname);
+  if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
+  std::shared_ptr<Snapshot> snap;
+  {
+    std::shared_lock<std::shared_mutex> l(ns->snap_mu);
+    snap = ns->snap;
+  }
+  if (!snap || seg >= snap->segs.size()) return hfail(FG_EINVAL, "no such segment");
+  const Segment& s0 = snap->segs[seg];
+  *n = s0.n;
+  if (out)
+    for (uint32_t d = 0; d < s0.n && d < cap; ++d) out[d] = s0.global(d);
   return FG_OK;
 }
 

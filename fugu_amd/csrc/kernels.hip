@@ -280,9 +280,6 @@ __device__ void bitonic_sort_desc(uint64_t* s, uint32_t P) {
 #ifndef FG_TRUNC
 #define FG_TRUNC 1024
 #endif
-#ifndef FG_MAXPROBE
-#define FG_MAXPROBE kMaxTerms  // timing experiments only (tools/ab_variants.py): lists probed per query
-#endif
 #ifndef FG_WAVES
 #define FG_WAVES 4  // tools/ab_variants.py: 3 -> 4 waves/SIMD took k_conj 3.18 -> 2.58 ms
 #endif
@@ -456,7 +453,7 @@ __device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_
     acc[r] = 0.0f;
     live |= (doc[r] != kInvalid ? 1u : 0u) << r;
   }
-  for (uint32_t i = 2; i < min(m, (uint32_t)FG_MAXPROBE); ++i) {
+  for (uint32_t i = 2; i < m; ++i) {
     if (!__any(live != 0)) break;
     float sc[kDeferR];
     probe_list<kDeferR>(ix, terms[i], doc, live, sc);
@@ -491,21 +488,12 @@ __device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_
 // [0, n_single) (no probes; block-max chunk skipping), the general one
 // [n_single, total_chunks); separate launches keep the general kernel's
 // register allocation.
-// FG_LEADVEC (A/B): lead postings by 16-B loads
-#ifndef FG_LEADVEC
-#define FG_LEADVEC 0
-#endif
-struct alignas(4) U4a { uint32_t x, y, z, w; };  // a 16-B load at 4-B alignment
 // k_conj's running thresholds from the query's score histogram: every item
 // counts its final kept keys (its local top-k) into the query's bins when it
-// ends; k_final reads the bins' threshold once per query (FG_CONJ_HIST=3) --
-// the k-th best among all the query's items, where the threshold word carries
-// the best single item's k-th key.  A/B: 0 = off; 1 / 2 = items also read the
-// bins when they start / in their first chunk (tools/ab_variants.py,
-// ab_conj_hist.log).
-#ifndef FG_CONJ_HIST
-#define FG_CONJ_HIST 3
-#endif
+// ends, and k_final reads the bins' threshold once per query -- the k-th best
+// among all the query's items, where the threshold word carries the best
+// single item's k-th key (items reading the bins themselves cost more than
+// they pruned: profiles/r03/ab/ab_conj_hist.log).
 // kMulti: a multi-snapshot plan (DevPlan::segs): the item's snapshot from its query slot
 template <bool kSingle, bool kMulti>
 __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPlan pl) {
@@ -558,22 +546,13 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
   // the plan's starting threshold (single-list queries: the term's K'-th best score)
   const uint64_t thr0 = pl.q_thr0[q];
   uint64_t pend = 0;
-#if FG_CONJ_HIST
   uint32_t* const gh = pl.hist + (size_t)ql * kQBins;
   const uint32_t h_lo = pl.q_hlo[q], h_sh = pl.q_hsh[q];
-  // FG_CONJ_HIST=2: multi-list items read the bins in their first chunk, with
-  // its lead loads in flight; single-list items need it before the block-max skip
-  // FG_CONJ_HIST=3: count only (k_final reads the bins once per query)
-  const uint64_t thr_h = ((kSingle && FG_CONJ_HIST != 3) || FG_CONJ_HIST == 1)
-                             ? max(thr0, hist_threshold(gh, K, h_lo, h_sh, sh.scratch)) : thr0;
-#else
-  const uint64_t thr_h = thr0;
-#endif
   if (tid == 0) {
     sh.n_buf = 0;
     sh.n_dq = 0;
-    sh.thr = thr_h;
-    pend = atomicMax(gthr, (unsigned long long)(thr_h & pl.pub_mask));
+    sh.thr = thr0;
+    pend = atomicMax(gthr, (unsigned long long)(thr0 & pl.pub_mask));
   }
 #ifdef FG_DIAG
   if (tid < 8) sh.dgc[tid] = 0;
@@ -583,7 +562,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
   // maximum) cannot reach the threshold is not loaded.  thr_k is the threshold
   // as every thread last saw it (uniform), so the skip is uniform too.
   const float* __restrict__ cmax = ix.cmax + ix.coff[t0];
-  uint64_t thr_k = thr_h;
+  uint64_t thr_k = thr0;
   const bool defer = !kSingle && kDeferCap > 0 && m >= 3 && nm == m && !fmask;  // pure conjunctions
 
   for (uint32_t cc = 0; cc < nc; ++cc) {
@@ -597,31 +576,6 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     uint32_t doc[kItems];
     float s0[kItems];
     uint32_t live = 0;
-#if FG_LEADVEC
-    // A/B: four consecutive postings per lane in one
-    // 16-B load (dword-aligned: gfx950 runs in unaligned access mode; the doc
-    // and score arrays carry 16 B of slack, so a group that starts inside the
-    // list may read up to 3 postings past it), item j of lane l =
-    // wv*512 + (j/4)*256 + 4l + j%4
-    static_assert(kItems == 8, "two 4-posting groups per lane");
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-      const uint32_t i0 = wv * kWaveSpan + h * 256 + 4 * lane;
-      U4a d4{kInvalid, kInvalid, kInvalid, kInvalid}, p4{0u, 0u, 0u, 0u};
-      if (i0 < cnt) {
-        d4 = *reinterpret_cast<const U4a*>(ix.doc + base0 + i0);
-        p4 = *reinterpret_cast<const U4a*>(ix.psc + base0 + i0);
-      }
-      const uint32_t dv[4] = {d4.x, d4.y, d4.z, d4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
-#pragma unroll
-      for (uint32_t e = 0; e < 4; ++e) {
-        const bool in = i0 + e < cnt;
-        doc[4 * h + e] = in ? dv[e] : kInvalid;
-        s0[4 * h + e] = in ? __uint_as_float(pv[e]) : 0.0f;
-        live |= (in ? 1u : 0u) << (4 * h + e);
-      }
-    }
-#else
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) {
       const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
@@ -632,13 +586,6 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
       s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
       live |= (in ? 1u : 0u) << j;
     }
-#endif
-#if FG_CONJ_HIST == 2
-    if (!kSingle && cc == 0) {
-      const uint64_t H = hist_threshold(gh, K, h_lo, h_sh, sh.scratch);
-      if (tid == 0 && H > sh.thr) sh.thr = H;
-    }
-#endif
     if (tid == 0 && pend > sh.thr) sh.thr = pend;
     __syncthreads();
     const uint64_t thr = sh.thr;
@@ -695,7 +642,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     float acc_o[kItems];
 #pragma unroll
     for (uint32_t j = 0; j < kItems; ++j) acc_o[j] = 0.0f;
-    for (uint32_t i = 1; i < min(m, (uint32_t)FG_MAXPROBE); ++i) {
+    for (uint32_t i = 1; i < m; ++i) {
       if (!__any(live != 0)) break;  // wave-uniform early exit
       if (i == nmx && nm > 1) {
 #pragma unroll
@@ -868,7 +815,6 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
   // write the kept keys that still clear the freshest threshold
   const uint32_t total = flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
   (void)total;
-#if FG_CONJ_HIST
   // count the item's kept keys (distinct docs of its own lead chunks) into the
   // query's bins, through LDS bins (sh.hist is free once the last select ran)
   {
@@ -883,7 +829,6 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     __syncthreads();
     hist_add(sh.hist, gh);
   }
-#endif
   FG_STAMP(w, 0, t_start);
   FG_STAMP(w, 1, t_probe);
   FG_STAMP(w, 2, t_keys);
@@ -910,17 +855,18 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
 //      threshold: sorted by bound, the longest prefix of clauses whose summed
 //      bound cannot reach it is non-essential (a doc matching only those cannot
 //      enter the top-k); all clauses non-essential: the tile is skipped;
-//   E. tiles where every clause is essential (low threshold) are scored
-//      exhaustively: the clauses' postings are scatter-added into an LDS score
-//      array clause by clause (so each doc's sum is formed in clause order);
-//   P. the other tiles are posting-driven: the postings of their essential
-//      clauses are streamed as one flat list in passes of 1024.  A posting of
-//      clause c at doc d is a candidate when s_c(d) plus the other clauses'
-//      bounds (tile bound, then the bucket maximum at d) can reach the
-//      threshold; candidates are rescored exactly by probing every clause
-//      through the directory ((candidate, clause) pairs in parallel) and summed
-//      in clause order.  A doc found through several essential clauses is kept
-//      only from the first of them that it matches, so keys stay unique;
+//   P. the essential clauses' postings of the tiles left are streamed as one
+//      flat list, two per thread per pass of 512 (the next pass's loads in
+//      flight through this one).  Bound 1: a posting of clause c at doc d
+//      plus the other clauses' tile bounds must reach the threshold; the
+//      survivors wait in an LDS queue, and once it holds a full pass bound 2
+//      runs over it with every lane busy: every other clause at d in clause
+//      order (its rank word and posting score, or its bucket maximum).  When
+//      every other clause is dense the bound-2 sum IS the exact score (a hit
+//      right there); otherwise the candidate is rescored by probing every
+//      clause ((candidate, clause) pairs in parallel), summed in clause
+//      order.  A doc found through several essential clauses is kept only
+//      from the first of them that it matches, so keys stay unique;
 //   then hits go through the same local top-k buffer / threshold publication
 //   as k_conj, and k_final selects the query's top-k.
 // Bounds are compared after inflating by 2^-17 relative, which covers any f32
@@ -929,67 +875,42 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
 // the exhaustive union.
 constexpr uint32_t kTileShift = kDisjTileShift;
 constexpr uint32_t kTile = 1u << kTileShift;   // docs per tile (LDS score array: 16 KB)
-// k_disj shape knobs: fg_internal.h (FG_DISJ_ROUND / EXH / HBITS / WAVES)
+// k_disj shape knobs: fg_internal.h (FG_DISJ_ROUND / HBITS / WAVES / G)
 constexpr uint32_t kRound = FG_DISJ_ROUND;     // postings / docs per pass
 constexpr uint32_t kBufD = kTrunc + kRound;    // kept keys + one pass of hits
 constexpr uint32_t kPairs = kRound;            // (candidate, clause) rescoring pairs per pass
-constexpr uint32_t kQCap = 2 * kRound;         // FG_DISJ_QUEUE: < one pass queued + one pass appended
+constexpr uint32_t kQCap = 2 * kRound;         // the bound-2 queue: < one pass queued + one pass appended
 constexpr uint32_t kDisjHistBits = FG_DISJ_HBITS;
 constexpr uint32_t kMaxTiles = kDisjMaxGroup;  // tiles per work item
 constexpr uint32_t kMaxSeg = kDisjMaxPairs;    // (tile, clause) pairs per work item (the planner's cap)
 static_assert(kMaxSeg <= 2 * kThreads, "k_disj segment list: two (tile, clause) pairs per thread");
 static_assert(kMaxTiles <= 255 && kMaxTerms <= 16, "seg_info packs (tile << 4) | clause; cand (tile << 8) | clause");
 
-// A sub-tile bound stored as q / 255 of its tile bound (q = 255: the tile
-// bound itself); the R phase picks the smallest q whose value is >= the
-// sub-tile maximum with this same f32 expression.
-__device__ inline float sub_bound(float tile_ub, uint32_t q) {
-  return q >= 255u ? tile_ub : tile_ub * ((float)q * (1.0f / 255.0f));
-}
-
 struct DisjShared {
   alignas(16) uint64_t buf[kBufD];
-  union {
-#if FG_DISJ_EXH
-    struct {
-      float acc[kTile];              // E: exhaustive tile scores
-      uint32_t hit[kTile / 32];      // E: docs matching any clause (a score may be 0)
-    } e;
-#endif
-    struct {
-#if FG_DISJ_QUEUE
-      // P: postings past bound 1 waiting for bound 2, (score bits << 32) | (clause
-      // << kRelBits) | (doc - the item's first doc); a flushed chunk's slots then
-      // hold its rescoring candidates, (maybe-mask << kRelBits + 4) | (clause <<
-      // kRelBits) | doc offset (kRelBits: 17 for 32-tile items)
-      uint64_t q[kQCap];
-#else
-      uint64_t cand[kRound];         // P: (doc << 32) | (maybe-mask << 16) | (tile << 8) | clause
-      float cand_s[kRound];          // P: the source clause's score of each candidate
-#endif
-      float cs[kPairs];              // P: per-(candidate, clause) term scores
-      uint32_t seg_start[kMaxSeg];   // P: prefix of the essential segments' lengths
-    } p;
-  } u;
+  struct {
+    // P: postings past bound 1 waiting for bound 2, (score bits << 32) | (clause
+    // << kRelBits) | (doc - the item's first doc); a flushed chunk's slots then
+    // hold its rescoring candidates, (maybe-mask << kRelBits + 4) | (clause <<
+    // kRelBits) | doc offset (kRelBits: 17 for 32-tile items)
+    uint64_t q[kQCap];
+    float cs[kPairs];              // P: per-(candidate, clause) term scores
+    uint32_t seg_start[kMaxSeg];   // P: prefix of the essential segments' lengths
+  } p;
   uint32_t hist[1u << kDisjHistBits];
   uint32_t scratch[8];
   // R: per (tile, clause) ranges and bounds, index t * m + i
   uint32_t r_lo[kMaxSeg], r_hi[kMaxSeg];
   float r_ub[kMaxSeg];
-#if FG_DISJ_SUB
-  // R: per (tile, clause) its 512-doc sub-tile maxima for bound 1, as q / 255
-  // of the tile bound (rounded up; 255 = the tile bound itself)
-  uint8_t r_sub[kMaxSeg * kSubPerTile];
-#endif
   uint32_t t_ess[kMaxTiles];         // essential-clause mask per tile
-  uint32_t t_mode[kMaxTiles];        // 0 skip, 1 exhaustive, 2 posting-driven
+  uint32_t t_post[kMaxTiles];        // 1: the tile's essential postings are streamed, 0: skipped
   uint16_t seg_info[kMaxSeg];        // P: (tile << 4) | clause of each segment
   // per-clause constants of the work item's query
   uint32_t c_meta[kMaxTerms], c_dir[kMaxTerms], c_toff[kMaxTerms];
   uint64_t c_base[kMaxTerms];
   uint32_t max_s, n_seg, n_post;
   uint32_t n_buf, n_cand;
-  uint32_t n_q;                      // P: queued postings (FG_DISJ_QUEUE)
+  uint32_t n_q;                      // P: queued postings
   uint32_t n_cnt;                    // buf[0, n_cnt) are counted in the query's histogram
   uint64_t thr;
   uint32_t lh[kQBins];               // hits per score bin not yet added to the global histogram
@@ -1007,29 +928,13 @@ struct QHist {
   uint32_t m, mq;    // MustNot clauses: c_meta[m, mq)
 };
 
-// A query's work items run about one after another (the items are ordered as
-// a doc sweep across the batch, ~one per query in flight), so the global
-// histogram is read when an item starts and added to when it ends;
-// FG_HIST_EVERY_PUBLISH=1 also does both at every publication (A/B builds).
-#ifndef FG_HIST_EVERY_PUBLISH
-#define FG_HIST_EVERY_PUBLISH 0
-#endif
-#ifndef FG_DISJ_HIST
-#define FG_DISJ_HIST 1      // A/B: 0 = no running-threshold histogram reads
-#endif
-#ifndef FG_DISJ_PREFETCH
-#define FG_DISJ_PREFETCH 0  // A/B: 1 = load the next pass's postings during this pass's gathers
-#endif
-#ifndef FG_DISJ_PRESENCE
-#define FG_DISJ_PRESENCE 0  // A/B (ab_disj_presence.log): 1 = presence bound before the score gathers, slower
-#endif
-
 // Keep the threshold fresh: drop the keys appended since the last call whose
 // doc a MustNot clause holds (Exclude: the hit loops never probe them), count
 // the rest into the LDS bins, truncate the local buffer to K when it passes
-// `limit`; when publishing, add the LDS bins to the query's histogram, read
-// back its running threshold, and exchange the threshold with the query's
-// (possibly shared) threshold word.
+// `limit`, and (publish) exchange the threshold with the query's (possibly
+// shared) threshold word.  A query's work items run about one after another
+// (the doc sweep keeps ~one per query in flight), so the LDS bins join the
+// query's histogram once, when the item ends.
 __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr,
                                      bool publish, const QHist& hq, uint64_t& pend) {
   uint32_t n = sh.n_buf;
@@ -1062,14 +967,8 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
   __syncthreads();
   uint64_t T = 0;
   if (n > limit) T = truncate_keys<kBufD, kDisjHistBits>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
-  uint64_t H = 0;
-  if (publish && FG_HIST_EVERY_PUBLISH) {
-    hist_add(sh.lh, hq.gh);
-    H = hist_threshold(hq.gh, K, hq.lo, hq.sh, sh.scratch);
-  }
   if (threadIdx.x == 0) {
-    uint64_t mine = T > sh.thr ? T : sh.thr;
-    mine = H > mine ? H : mine;
+    const uint64_t mine = T > sh.thr ? T : sh.thr;
     // the exchange does not wait: the returned best is folded in when the
     // next pass starts (pend), after that pass's posting loads are in flight
     if (publish) pend = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)(mine & hq.pub));
@@ -1181,39 +1080,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     sh.r_lo[p] = lo;
     sh.r_hi[p] = hi;
     sh.r_ub[p] = lo < hi ? ub : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
-#if FG_DISJ_SUB
-    // the sub-tile maxima (0 for a sub-tile without postings), quantized up
-    // against the tile bound; a term whose buckets are wider than a tile has one
-    // bound for the whole tile
-    {
-      uint32_t q8[kSubPerTile];
-      if (B <= kTileShift && sh.c_toff[i] != kInvalid && lo < hi && ub > 0.0f) {
-        const float4* sm = reinterpret_cast<const float4*>(ix.smax + ((size_t)sh.c_toff[i] + tile) * kSubPerTile);
-#pragma unroll
-        for (uint32_t v = 0; v < kSubPerTile / 4; ++v) {
-          const float4 x = sm[v];
-          const float xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-          for (uint32_t u = 0; u < 4; ++u) {
-            uint32_t q = min(255u, (uint32_t)ceilf(xs[u] * 255.0f / ub));
-            while (q < 255u && sub_bound(ub, q) < xs[u]) ++q;
-            q8[4 * v + u] = q;
-          }
-        }
-      } else {
-#pragma unroll
-        for (uint32_t v = 0; v < kSubPerTile; ++v) q8[v] = 255u;
-      }
-      uint32_t* dst = reinterpret_cast<uint32_t*>(sh.r_sub + p * kSubPerTile);
-#pragma unroll
-      for (uint32_t v = 0; v < kSubPerTile / 4; ++v)
-        dst[v] = q8[4 * v] | (q8[4 * v + 1] << 8) | (q8[4 * v + 2] << 16) | (q8[4 * v + 3] << 24);
-    }
-#endif
   }
   {
     // the query's running threshold (every work item's counted hits so far)
-    const uint64_t H = FG_DISJ_HIST ? hist_threshold(hq.gh, K, hq.lo, hq.sh, sh.scratch) : 0ull;
+    const uint64_t H = hist_threshold(hq.gh, K, hq.lo, hq.sh, sh.scratch);
     if (tid == 0 && H > sh.thr) sh.thr = H;
   }
   __syncthreads();
@@ -1239,99 +1109,30 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       if (make_key(inflate_bound(s2 + fmax), d0) >= thr) break;
       s = s2;
     }
-    uint32_t ess = 0, any = 0, npost = 0, nall = 0;
+    uint32_t ess = 0, any = 0;
     for (uint32_t j = 0; j < m; ++j) {
       const uint32_t n = sh.r_hi[t * m + ord[j]] - sh.r_lo[t * m + ord[j]];
-      nall += n;
       if (j < P) continue;
       ess |= 1u << ord[j];
       any |= n ? 1u : 0u;
-      npost += n;
     }
     sh.t_ess[t] = ess;
-    // every clause essential: the exhaustive LDS pass costs the whole tile
-    // (4096 docs), the posting-driven one its postings; take the cheaper.
-    // FG_DISJ_EBETA > 0 (A/B): also exhaustive when streaming every clause's
-    // postings costs at most EBETA x the essential ones (no per-posting gathers)
-    const bool exh = FG_DISJ_EXH && ((P == 0 && npost >= kExhaustiveMin) ||
-                                     (FG_DISJ_EBETA > 0 && nall >= kExhaustiveMin && nall <= FG_DISJ_EBETA * npost));
-    sh.t_mode[t] = (P == m || !any) ? 0u : (exh ? 1u : 2u);
+    sh.t_post[t] = (P < m && any) ? 1u : 0u;
   }
   __syncthreads();
   FG_PHASE(1);
 #ifdef FG_DIAG
   if (tid == 0)
     for (uint32_t t = 0; t < ntile; ++t) {
-      dg_mode[sh.t_mode[t]]++;
+      dg_mode[sh.t_post[t] ? 2 : 0]++;
       for (uint32_t i = 0; i < m; ++i)
-        if (sh.t_mode[t] && ((sh.t_ess[t] >> i) & 1u)) dg_post += sh.r_hi[t * m + i] - sh.r_lo[t * m + i];
+        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) dg_post += sh.r_hi[t * m + i] - sh.r_lo[t * m + i];
     }
 #endif
 
-  // ---- E: exhaustive tiles (every clause essential), clause-ordered LDS accumulation
-#if FG_DISJ_EXH
-  for (uint32_t t = 0; t < ntile; ++t) {
-    if (sh.t_mode[t] != 1u) continue;  // uniform
-    const uint32_t d0 = (tile0 + t) << kTileShift;
-    const uint32_t span = min(d0 + kTile, ix.n_docs) - d0;
-    for (uint32_t x = tid; x < kTile; x += kThreads) sh.u.e.acc[x] = 0.0f;
-    for (uint32_t x = tid; x < kTile / 32; x += kThreads) sh.u.e.hit[x] = 0u;
-    __syncthreads();
-    for (uint32_t i = 0; i < m; ++i) {
-      const uint64_t bi = sh.c_base[i];
-      const uint32_t lo = sh.r_lo[t * m + i], hi = sh.r_hi[t * m + i];
-      for (uint32_t p0 = lo; p0 < hi; p0 += 4 * kThreads) {
-        uint32_t dd[4];
-        float ps[4];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-          const uint32_t p = p0 + j * kThreads + tid;
-          dd[j] = p < hi ? ix.doc[bi + p] : kInvalid;
-          ps[j] = p < hi ? ix.psc[bi + p] : 0.0f;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-          if (dd[j] != kInvalid) {
-            const uint32_t x = dd[j] - d0;
-            sh.u.e.acc[x] += ps[j];
-            if (i == 0 || !((sh.u.e.hit[x >> 5] >> (x & 31)) & 1u)) atomicOr(&sh.u.e.hit[x >> 5], 1u << (x & 31));
-          }
-      }
-      __syncthreads();
-    }
-    if (tid == 0 && pend > sh.thr) sh.thr = pend;
-    __syncthreads();
-    for (uint32_t r0 = 0; r0 < span; r0 += kRound) {
-      const uint64_t thr = sh.thr;
-#pragma unroll
-      for (uint32_t j = 0; j < kRound / kThreads; ++j) {
-        const uint32_t x = r0 + j * kThreads + tid;
-        float sc = x < span ? sh.u.e.acc[x] : 0.0f;
-        uint64_t key = 0;
-        bool keep = x < span && ((sh.u.e.hit[x >> 5] >> (x & 31)) & 1u) && doc_alive(ix, d0 + x);
-        if (keep && fmask) {
-          const uint32_t fb = filter_bits(fmask, fshift, d0 + x);
-          keep = fb != 0;
-          sc = sc + ftab[fb];
-        }
-        if (keep) {
-          key = make_key(sc, d0 + x);
-          keep = key >= thr;
-        }
-        wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
-      }
-      __syncthreads();
-#ifdef FG_DIAG
-      if (sh.n_buf > kTrunc) dg_trunc++;
-#endif
-      disj_truncate(ix, sh, K, kTrunc, gthr, false, hq, pend);
-    }
-    disj_truncate(ix, sh, K, K, gthr, true, hq, pend);
-  }
-#endif
   FG_PHASE(2);
 
-  // ---- P: posting-driven tiles: flat list of the essential clauses' segments,
+  // ---- P: flat list of the essential clauses' segments of the streamed tiles,
   // (tile, clause) pairs in order, compacted by two workgroup prefix sums
   {
     uint32_t len[2], cnt = 0, tot = 0;
@@ -1341,7 +1142,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       len[r] = 0;
       if (p < npair) {
         const uint32_t t = p / m, i = p - t * m;
-        if (sh.t_mode[t] == 2u && ((sh.t_ess[t] >> i) & 1u)) len[r] = sh.r_hi[p] - sh.r_lo[p];
+        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) len[r] = sh.r_hi[p] - sh.r_lo[p];
       }
       cnt += len[r] ? 1u : 0u;
       tot += len[r];
@@ -1352,7 +1153,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     for (uint32_t r = 0; r < 2; ++r) {
       if (!len[r]) continue;
       const uint32_t p = 2 * tid + r, t = p / m, i = p - t * m;
-      sh.u.p.seg_start[sb] = pb;
+      sh.p.seg_start[sb] = pb;
       sh.seg_info[sb] = (uint16_t)((t << 4) | i);
       ++sb;
       pb += len[r];
@@ -1374,31 +1175,13 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     uint32_t lo = 0, hi = n_seg;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (sh.u.p.seg_start[mid] <= e) lo = mid; else hi = mid;
+      if (sh.p.seg_start[mid] <= e) lo = mid; else hi = mid;
     }
     const uint32_t info = sh.seg_info[lo];
     t = info >> 4;
     c = info & 15u;
-    return sh.c_base[c] + sh.r_lo[t * m + c] + (e - sh.u.p.seg_start[lo]);
+    return sh.c_base[c] + sh.r_lo[t * m + c] + (e - sh.p.seg_start[lo]);
   };
-#if FG_DISJ_PREFETCH
-  // the next pass's postings are loaded while this pass gathers (bound 2)
-  uint32_t npd[J];
-  float nps[J];
-#pragma unroll
-  for (uint32_t j = 0; j < J; ++j) {
-    const uint32_t e = j * kThreads + tid;
-    uint32_t t, c;
-    npd[j] = 0;
-    nps[j] = 0.0f;
-    if (e < n_post) {
-      const uint64_t at = locate(e, t, c);
-      npd[j] = ix.doc[at];
-      nps[j] = ix.psc[at];
-    }
-  }
-#endif
-#if FG_DISJ_QUEUE
   // Deferred bound 2.  A pass loads kRound postings and applies bound 1 (LDS
   // only); the survivors wait in an LDS queue, and bound 2 + the rescoring run
   // once the queue holds a full pass (or the item ends): their dependent gather
@@ -1412,7 +1195,6 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   const uint32_t dbase = tile0 << kTileShift;
   if (tid == 0) sh.n_q = 0;
   __syncthreads();
-#if FG_DISJ_QPF
   // the next pass's postings are loaded before this pass's bound 1, so they are
   // in flight through its queue append and any flush (bound 2) that follows
   uint32_t npd[J], npcl[J];
@@ -1433,12 +1215,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     }
   };
   load_pass(0);
-#endif
   for (uint32_t e0 = 0; e0 < n_post; e0 += kRound) {
     uint32_t pd[J], pcl[J];
     float ps[J];
     bool pk[J];
-#if FG_DISJ_QPF
 #pragma unroll
     for (uint32_t j = 0; j < J; ++j) {
       pk[j] = e0 + j * kThreads + tid < n_post;
@@ -1447,22 +1227,6 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       ps[j] = nps[j];
     }
     if (e0 + kRound < n_post) load_pass(e0 + kRound);
-#else
-#pragma unroll
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t e = e0 + j * kThreads + tid;
-      pk[j] = e < n_post;
-      pd[j] = dbase;
-      pcl[j] = 0;
-      ps[j] = 0.0f;
-      if (pk[j]) {
-        uint32_t t;
-        const uint64_t at = locate(e, t, pcl[j]);
-        pd[j] = ix.doc[at];
-        ps[j] = ix.psc[at];
-      }
-    }
-#endif
     // with this pass's posting loads in flight: the last exchange's reply
     if (tid == 0 && pend > sh.thr) sh.thr = pend;
     __syncthreads();
@@ -1482,7 +1246,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
           dg_b1 += pk[j] ? 1u : 0u;
 #endif
         }
-        wave_append(pk[j], ((uint64_t)__float_as_uint(ps[j]) << 32) | (pcl[j] << kRelBits) | (pd[j] - dbase), sh.u.p.q,
+        wave_append(pk[j], ((uint64_t)__float_as_uint(ps[j]) << 32) | (pcl[j] << kRelBits) | (pd[j] - dbase), sh.p.q,
                     &sh.n_q, kQCap);
       }
     }
@@ -1500,7 +1264,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       for (uint32_t j = 0; j < J; ++j) {
         const uint32_t i = j * kThreads + tid;
         pk[j] = i < cnt;
-        ent[j] = pk[j] ? sh.u.p.q[done + i] : 0ull;
+        ent[j] = pk[j] ? sh.p.q[done + i] : 0ull;
       }
       if (tid == 0) {
         sh.n_cand = 0;
@@ -1625,7 +1389,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         }
         wave_append(direct, dkey, sh.buf, &sh.n_buf, kBufD);
         wave_append(keep, ((uint64_t)maybe[j] << (kRelBits + 4)) | (pcl[j] << kRelBits) | (pd[j] - dbase),
-                    sh.u.p.q + done, &sh.n_cand, cnt);
+                    sh.p.q + done, &sh.n_cand, cnt);
       }
       __syncthreads();
       FG_PHASE(5);
@@ -1635,7 +1399,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
 #endif
       // exact rescoring: every (candidate, clause) pair the doc may match -- its
       // own clause included -- probed in parallel, summed in clause order
-      const uint64_t* cq = sh.u.p.q + done;
+      const uint64_t* cq = sh.p.q + done;
       const uint32_t Q = kPairs / m;
       for (uint32_t c0 = 0; c0 < nc; c0 += Q) {
         const uint32_t nq_ = min(Q, nc - c0), np = nq_ * m;
@@ -1688,7 +1452,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
 #pragma unroll
         for (uint32_t j = 0; j < R; ++j) {
           const uint32_t p = j * kThreads + tid;
-          if (p < np) sh.u.p.cs[p] = pv[j];
+          if (p < np) sh.p.cs[p] = pv[j];
         }
         __syncthreads();
         for (uint32_t cc0 = 0; cc0 < nq_; cc0 += kThreads) {
@@ -1702,7 +1466,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
             float sc = 0.0f;  // SumCombiner from 0.0 in clause order over the matching clauses
             uint32_t matched = 0;
             for (uint32_t i = 0; i < m; ++i) {
-              const float v = sh.u.p.cs[cc * m + i];
+              const float v = sh.p.cs[cc * m + i];
               if (v >= 0.0f) {
                 sc += v;
                 matched |= 1u << i;
@@ -1727,325 +1491,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     }
     // the rest of the queue (< kRound entries, behind the flushed chunks) moves to the front
     const uint32_t rem = nqd - done;
-    for (uint32_t i = tid; i < rem; i += kThreads) sh.u.p.q[i] = sh.u.p.q[done + i];
+    for (uint32_t i = tid; i < rem; i += kThreads) sh.p.q[i] = sh.p.q[done + i];
     if (tid == 0) sh.n_q = rem;
     __syncthreads();
   }
-#else
-  for (uint32_t e0 = 0; e0 < n_post; e0 += kRound) {
-    uint32_t pd[J], pt[J], pcl[J], ess[J];
-    float ps[J];
-    bool pk[J];
-#pragma unroll
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t e = e0 + j * kThreads + tid;
-      pk[j] = e < n_post;
-      pd[j] = 0;
-      pt[j] = 0;
-      pcl[j] = 0;
-      ps[j] = 0.0f;
-      if (pk[j]) {
-        const uint64_t at = locate(e, pt[j], pcl[j]);
-#if FG_DISJ_PREFETCH
-        (void)at;
-        pd[j] = npd[j];
-        ps[j] = nps[j];
-#else
-        pd[j] = ix.doc[at];
-        ps[j] = ix.psc[at];
-#endif
-      }
-    }
-    // with this pass's posting loads in flight: the last exchange's reply
-    if (tid == 0) {
-      sh.n_cand = 0;
-      if (pend > sh.thr) sh.thr = pend;
-    }
-    __syncthreads();
-    const uint64_t thr = sh.thr;
-#pragma unroll
-    for (uint32_t j = 0; j < J; ++j) {
-      ess[j] = 0;
-      if (!pk[j]) continue;
-      // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
-      float ub = ps[j] + fmax;
-#if FG_DISJ_SUB
-      const uint32_t sb = (pd[j] >> kSubShift) & (kSubPerTile - 1);
-      for (uint32_t i = 0; i < m; ++i)
-        if (i != pcl[j]) {
-          const uint32_t pi = pt[j] * m + i;
-          ub += sub_bound(sh.r_ub[pi], sh.r_sub[pi * kSubPerTile + sb]);
-        }
-#else
-      for (uint32_t i = 0; i < m; ++i)
-        if (i != pcl[j]) ub += sh.r_ub[pt[j] * m + i];
-#endif
-      pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
-      if (pk[j] && fmask) pk[j] = filter_bits(fmask, fshift, pd[j]) != 0;
-      ess[j] = sh.t_ess[pt[j]];
-#ifdef FG_DIAG
-      dg_b1 += pk[j] ? 1u : 0u;
-#endif
-    }
-#if FG_DISJ_PREFETCH
-#pragma unroll
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t e = e0 + kRound + j * kThreads + tid;
-      if (e < n_post) {
-        uint32_t t, c;
-        const uint64_t at = locate(e, t, c);
-        npd[j] = ix.doc[at];
-        nps[j] = ix.psc[at];
-      }
-    }
-#endif
-    // bound 2: every other clause at d, in two steps per group of G clauses.
-    //  (a) presence: its rank word (presence bits + rank), its f32 table score or
-    //      its bucket maximum (-0.0: empty bucket), the loads of all J postings
-    //      in flight together; a clause the doc lacks adds 0 to the bound, one
-    //      it holds its tile bound (rank words) / exact table score / bucket
-    //      maximum, the clauses of later groups their tile bounds; a posting
-    //      whose bound cannot reach the threshold stops before any score gather;
-    //  (b) the survivors' posting scores of the clauses present by rank word.
-    // When every other clause is dense (or has no posting in the tile) the
-    // clause-order sum IS the doc's exact SumCombiner score (0.0 + s_i over the
-    // matching clauses): the doc is a hit right here and skips the rescoring.
-    float sum[J];
-    uint32_t maybe[J];  // clauses whose structure at d says they may match (the rest cannot)
-    bool exact[J];
-#pragma unroll
-    for (uint32_t j = 0; j < J; ++j) {
-      sum[j] = 0.0f;
-      maybe[j] = 0;
-      exact[j] = true;
-    }
-    constexpr uint32_t G = FG_DISJ_G;  // clauses per bound-2 group (their loads in flight together)
-    constexpr uint32_t kAbsent = 0xBF800000u;  // -1.0f: the clause is not on the doc
-    for (uint32_t i0 = 0; i0 < m; i0 += G) {
-      // y[g][j]: a rank clause's posting position (< 2^31) or kAbsent; an f32
-      // table clause's score (-1.0: absent); a directory clause's bucket
-      // maximum (-0.0: empty bucket) -- one word per (clause, posting) once the
-      // loads (all G x J in flight together) have landed
-      uint32_t y[G][J];
-      uint32_t need = 0;  // bit g * J + j
-      {
-        uint64_t x[G][J];
-#pragma unroll
-        for (uint32_t g = 0; g < G; ++g) {
-          const uint32_t i = i0 + g;
-          const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
-          const uint32_t slot = meta_slot(meta);
-          const bool rank = slot && meta_rank(meta);
-#pragma unroll
-          for (uint32_t j = 0; j < J; ++j) {
-            x[g][j] = kAbsent;
-            if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
-              need |= 1u << (g * J + j);
-              if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
-              else if (slot) x[g][j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
-              else x[g][j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
-            }
-          }
-        }
-#pragma unroll
-        for (uint32_t g = 0; g < G; ++g) {
-          const uint32_t i = i0 + g;
-          const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
-          const bool rank = meta_slot(meta) && meta_rank(meta);
-#pragma unroll
-          for (uint32_t j = 0; j < J; ++j) {
-            const uint32_t bits = (uint32_t)x[g][j], bt = pd[j] & 31u;
-            if (!rank || !((need >> (g * J + j)) & 1u)) y[g][j] = (uint32_t)x[g][j];
-            else y[g][j] = ((bits >> bt) & 1u) ? (uint32_t)(x[g][j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))
-                                               : kAbsent;
-          }
-        }
-      }
-      // (a) the presence bound: the earlier groups' clause-order sum (exact
-      // scores or bucket maxima), the own posting's score if not in it yet, this
-      // group's presence contributions, the later groups' tile bounds
-#pragma unroll
-      for (uint32_t j = 0; j < J; ++j) {
-        if (!FG_DISJ_PRESENCE || !pk[j]) continue;
-        float b = sum[j] + fmax;
-        if (pcl[j] >= i0) b += ps[j];
-#pragma unroll
-        for (uint32_t g = 0; g < G; ++g) {
-          if (!((need >> (g * J + j)) & 1u)) continue;
-          const uint32_t i = i0 + g, meta = sh.c_meta[i];
-          if (meta_slot(meta) && meta_rank(meta)) {
-            if (y[g][j] < 0x80000000u) b += sh.r_ub[pt[j] * m + i];
-          } else if (!signbit(__uint_as_float(y[g][j]))) {
-            b += __uint_as_float(y[g][j]);
-          }
-        }
-        for (uint32_t i = i0 + G; i < m; ++i)
-          if (i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) b += sh.r_ub[pt[j] * m + i];
-        pk[j] = make_key(inflate_bound(b), pd[j]) >= thr;
-      }
-      // (b) the posting scores of the present rank clauses, survivors only
-#pragma unroll
-      for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t i = i0 + g;
-        const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
-        if (!(meta_slot(meta) && meta_rank(meta))) continue;
-        const float* __restrict__ sp = ix.psc + sh.c_base[i];
-#pragma unroll
-        for (uint32_t j = 0; j < J; ++j)
-          if (pk[j] && ((need >> (g * J + j)) & 1u) && y[g][j] < 0x80000000u) y[g][j] = __float_as_uint(sp[y[g][j]]);
-      }
-      // the clause-order sum (the own clause: the streamed posting's score)
-#pragma unroll
-      for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t i = i0 + g;
-        if (i >= m) break;
-        const uint32_t slot = meta_slot(sh.c_meta[i]);
-#pragma unroll
-        for (uint32_t j = 0; j < J; ++j) {
-          if (!pk[j]) continue;
-          float b = ps[j];
-          if (i != pcl[j]) {
-            if (!((need >> (g * J + j)) & 1u)) continue;
-            b = __uint_as_float(y[g][j]);
-            exact[j] = exact[j] && slot != 0;
-            if (signbit(b)) continue;  // clause i cannot match d
-            maybe[j] |= 1u << i;
-          }
-          sum[j] += b;
-        }
-      }
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < J; ++j) {
-      bool keep = false, direct = false;
-      uint64_t dkey = 0;
-      if (pk[j]) {
-        if (exact[j]) {
-          // unique keys: the doc is kept only from the first essential clause it matches
-          const uint32_t first = (uint32_t)__builtin_ctz((maybe[j] | (1u << pcl[j])) & ess[j]);
-          const float s2 = fmask ? sum[j] + ftab[filter_bits(fmask, fshift, pd[j])] : sum[j];
-          dkey = make_key(s2, pd[j]);
-          direct = first == pcl[j] && dkey >= thr && doc_alive(ix, pd[j]);
-        } else {
-          keep = make_key(inflate_bound(sum[j] + fmax), pd[j]) >= thr && doc_alive(ix, pd[j]);
-        }
-      }
-      wave_append(direct, dkey, sh.buf, &sh.n_buf, kBufD);
-      const unsigned long long bal = __ballot(keep);
-      if (bal) {
-        const uint32_t nw = (uint32_t)__popcll(bal);
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(&sh.n_cand, nw);
-        base = (uint32_t)__shfl((int)base, 0, 64);
-        const uint32_t at = base + (uint32_t)__popcll(bal & ((1ull << lane_id()) - 1ull));
-        if (keep) {
-          sh.u.p.cand[at] = ((uint64_t)pd[j] << 32) | (maybe[j] << 16) | (pt[j] << 8) | pcl[j];
-          sh.u.p.cand_s[at] = ps[j];
-        }
-      }
-    }
-    __syncthreads();
-    FG_PHASE(4);
-    const uint32_t nc = sh.n_cand;
-#ifdef FG_DIAG
-    dg_cand += nc;
-#endif
-    // exact rescoring: every (candidate, clause) pair probed in parallel, four
-    // pairs per thread in lockstep so their directory loads overlap
-    const uint32_t Q = kPairs / m;
-    for (uint32_t c0 = 0; c0 < nc; c0 += Q) {
-      const uint32_t nq_ = min(Q, nc - c0), np = nq_ * m;
-      constexpr uint32_t R = kPairs / kThreads;
-      uint32_t pd[R], pc[R], pos[R], hi[R];
-      float pv[R];  // the clause's score at the candidate, -1 = absent
-#pragma unroll
-      for (uint32_t j = 0; j < R; ++j) {
-        const uint32_t p = j * kThreads + tid;
-        pc[j] = kInvalid;
-        pd[j] = 0;
-        pv[j] = -1.0f;
-        pos[j] = 0;
-        hi[j] = 0;
-        if (p < np) {
-          const uint64_t cv = sh.u.p.cand[c0 + p / m];
-          const uint32_t i = p % m;
-          pd[j] = (uint32_t)(cv >> 32);
-          // the source clause is known; a clause with an empty bucket at d cannot match
-          pc[j] = (i == ((uint32_t)cv & 0xFFu) || !(((uint32_t)cv >> 16 >> i) & 1u)) ? (0x80000000u | i) : i;
-        }
-        if (!(pc[j] & 0x80000000u)) {
-          const uint32_t meta = sh.c_meta[pc[j]];
-          if (meta_slot(meta)) {
-            pv[j] = dense_score(ix, meta, sh.c_base[pc[j]], pd[j]);
-            pc[j] |= 0x80000000u;  // resolved
-          } else {
-            const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[pc[j]];
-            const uint32_t b = pd[j] >> (meta & 0xFFu);
-            pos[j] = dir[b];
-            hi[j] = dir[b + 1];
-          }
-        }
-      }
-      for (uint32_t st = sh.max_s; st > 0; --st) {
-#pragma unroll
-        for (uint32_t j = 0; j < R; ++j) {
-          if (pc[j] & 0x80000000u) continue;  // invalid or dense
-          if (st > ((sh.c_meta[pc[j]] >> 8) & 0xFFu)) continue;
-          const uint32_t half = 1u << (st - 1);
-          const uint32_t idx = pos[j] + half - 1;
-          if (idx < hi[j] && ix.doc[sh.c_base[pc[j]] + idx] < pd[j]) pos[j] += half;
-        }
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < R; ++j) {
-        if (pc[j] & 0x80000000u) continue;
-        const uint64_t base = sh.c_base[pc[j]];
-        if (pos[j] < hi[j] && ix.doc[base + pos[j]] == pd[j]) pv[j] = ix.psc[base + pos[j]];
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < R; ++j) {
-        const uint32_t p = j * kThreads + tid;
-        if (p >= np) continue;
-        const uint32_t c = pc[j] & 0x7FFFFFFFu;
-        const uint64_t cv = sh.u.p.cand[c0 + p / m];
-        sh.u.p.cs[p] = c == ((uint32_t)cv & 0xFFu) ? sh.u.p.cand_s[c0 + p / m] : pv[j];
-      }
-      __syncthreads();
-      for (uint32_t cc0 = 0; cc0 < nq_; cc0 += kThreads) {
-        const uint32_t cc = cc0 + tid;
-        uint64_t key = 0;
-        bool keep = cc < nq_;
-        if (keep) {
-          const uint64_t cv = sh.u.p.cand[c0 + cc];
-          const uint32_t t = ((uint32_t)cv >> 8) & 0xFFu, src = (uint32_t)cv & 0xFFu;
-          (void)t;
-          float sc = 0.0f;  // SumCombiner from 0.0 in clause order over the matching clauses
-          uint32_t matched = 0;
-          for (uint32_t i = 0; i < m; ++i) {
-            const float v = sh.u.p.cs[cc * m + i];
-            if (v >= 0.0f) {
-              sc += v;
-              matched |= 1u << i;
-            }
-          }
-          // unique keys: keep the doc only from the first essential clause it matches
-          const uint32_t first = (uint32_t)__builtin_ctz(matched & sh.t_ess[t]);
-          if (fmask) sc = sc + ftab[filter_bits(fmask, fshift, (uint32_t)(cv >> 32))];
-          key = make_key(sc, (uint32_t)(cv >> 32));
-          keep = first == src && key >= thr;
-        }
-        wave_append(keep, key, sh.buf, &sh.n_buf, kBufD);
-      }
-      __syncthreads();
-    }
-    FG_PHASE(5);
-#ifdef FG_DIAG
-    if (sh.n_buf > K) dg_trunc++;
-#endif
-    disj_truncate(ix, sh, K, K, gthr, true, hq, pend);
-    FG_PHASE(6);
-  }
-#endif  // FG_DISJ_QUEUE
   // the item's counted hits join the query's histogram (every key was counted
   // by the last disj_truncate)
   hist_add(sh.lh, hq.gh);
@@ -2596,7 +2045,6 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
   const uint32_t n = (uint32_t)(j.off[t + 1] - b);
   const uint32_t end = min(n, first + kScoreChunk);
   const float wt = j.w_text[t], wn = j.w_name[t];
-  const uint32_t to = j.toff[t];
   float mx = 0.0f;
   for (uint32_t p0 = first; p0 < end; p0 += kThreads) {
     const uint32_t p = p0 + threadIdx.x;
@@ -2605,20 +2053,6 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
     const float v = in ? posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache) : 0.0f;
     if (in) j.psc[b + p] = v;
     mx = fmaxf(mx, v);
-    if (j.smax && to != 0xFFFFFFFFu) {
-      // 512-doc sub-tile maxima: the wave's postings are consecutive (docs
-      // ascending), so a segmented max over equal sub-tiles leaves one atomic
-      // per sub-tile per wave
-      const uint32_t lane = threadIdx.x & 63u, sub = in ? d >> kSubShift : 0xFFFFFFFFu;
-      uint32_t vb = __float_as_uint(v);
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t vo = (uint32_t)__shfl_down((int)vb, o, 64), so = (uint32_t)__shfl_down((int)sub, o, 64);
-        if (lane + o < 64 && so == sub) vb = max(vb, vo);
-      }
-      const uint32_t prev = (uint32_t)__shfl_up((int)sub, 1, 64);
-      if (in && (lane == 0 || prev != sub)) atomicMax(&j.smax[(size_t)to * kSubPerTile + sub], vb);
-    }
   }
   // the chunk's block-max (scores >= 0)
   __shared__ float wmax[kThreads / 64];
@@ -2673,9 +2107,6 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
 constexpr uint32_t kKtopKM = kTopKs[kNumTopK - 1];  // the largest K: its keys are kept
 constexpr uint32_t kKtopSort = 1024;                 // ... and sorted (a power of two >= KM)
 static_assert(kKtopSort >= kKtopKM && (kKtopSort & (kKtopSort - 1)) == 0, "k_ktop sorts its KM keys in place");
-#ifndef FG_KTOP_SORT
-#define FG_KTOP_SORT 1  // A/B: 0 = one LDS select per K instead of one sort of the kept keys
-#endif
 
 struct KtopShared {
   uint32_t hist[kHistBins];
@@ -2683,33 +2114,13 @@ struct KtopShared {
   uint32_t red[3];  // alive postings, smallest alive score (bits), largest (bits)
   uint64_t top[kKtopSort];  // the KM best keys, then zero padding for the sort
   uint32_t n_top;
-  unsigned long long kmin;
 };
 
-// The smallest of top[0, nt) that is >= T: with exactly K keys >= T (select_kth's
-// contract, T possibly below the K-th key with its low bits cleared) it IS the
-// K-th key, so its score is the exact K-th score
-__device__ inline uint64_t ktop_min_at_least(KtopShared& sh, uint32_t nt, uint64_t T) {
-  if (threadIdx.x == 0) sh.kmin = ~0ull;
-  __syncthreads();
-  unsigned long long m = ~0ull;
-  for (uint32_t i = threadIdx.x; i < nt; i += kThreads)
-    if (sh.top[i] >= T && sh.top[i] < m) m = sh.top[i];
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long y = (unsigned long long)__shfl_xor((long long)m, o, 64);
-    m = y < m ? y : m;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMin(&sh.kmin, m);
-  __syncthreads();
-  return sh.kmin;
-}
-
 // term t's K-th best scores for K >= 10 from its na alive keys (each_key(f):
-// f(ok, key) for every key, the workgroup converged); the KM best into LDS with
-// one select over all keys, the smaller K then select inside LDS
+// f(ok, key) for every key, the workgroup converged): the KM best into LDS with
+// one select over all keys, then one bitonic sort of them gives every K
 template <class EachKey>
-__device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, uint32_t mn_bits, KtopShared& sh,
-                            EachKey each_key) {
+__device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, KtopShared& sh, EachKey each_key) {
   constexpr uint32_t KM = kKtopKM;
   if (na < kTopKs[1]) return;  // uniform: only K = 1
   uint64_t T = 0;
@@ -2721,7 +2132,6 @@ __device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, uint32_t
   each_key([&](bool ok, uint64_t key) { wave_append(ok && key >= T, key, sh.top, &sh.n_top, KM); });
   __syncthreads();
   const uint32_t nt = min(na, KM);  // keys in top[] (unique: exactly KM are >= T)
-#if FG_KTOP_SORT
   // one bitonic sort of the kept keys: the K-th key of every K is then top[K - 1]
   uint32_t P = 16;
   while (P < nt) P <<= 1;
@@ -2731,23 +2141,6 @@ __device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, uint32_t
   if (threadIdx.x == 0)
     for (uint32_t kk = 1; kk < kNumTopK; ++kk)
       if (nt >= kTopKs[kk]) j.ktop[(size_t)t * kNumTopK + kk] = key_score(sh.top[kTopKs[kk] - 1]);
-  return;
-#endif
-  for (uint32_t kk = 1; kk < kNumTopK; ++kk) {
-    const uint32_t K = kTopKs[kk];
-    if (nt < K) break;  // uniform
-    float v;
-    if (na == K) {
-      v = __uint_as_float(mn_bits);  // every alive key is in: the minimum
-    } else {
-      // T_K: exactly K keys of top[] are >= it (top[] holds the KM best)
-      const uint64_t TK = K == KM ? T : select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
-        for (uint32_t i = threadIdx.x; i < nt; i += kThreads) f(sh.top[i]);
-      });
-      v = key_score(ktop_min_at_least(sh, nt, TK));
-    }
-    if (threadIdx.x == 0) j.ktop[(size_t)t * kNumTopK + kk] = v;
-  }
 }
 
 // postings [b + p0, b + p1) as f(valid && alive, score, doc), U loads per thread
@@ -2811,7 +2204,7 @@ __global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
   ktop_reduce(j, b, 0, n, sh);
   const uint32_t na = sh.red[0];
   if (threadIdx.x == 0 && na) j.ktop[(size_t)t * kNumTopK] = __uint_as_float(sh.red[2]);  // K = 1: the maximum
-  ktop_finish(j, t, na, sh.red[1], sh, [&](auto&& f) {
+  ktop_finish(j, t, na, sh, [&](auto&& f) {
     ktop_each_posting(j, b, 0, n, [&](bool ok, float sv, uint32_t d) { f(ok, make_key(sv, d)); });
   });
 }
@@ -2855,14 +2248,14 @@ __global__ __launch_bounds__(kThreads) void k_ktop_big(ScoreJob j) {
   __shared__ KtopShared sh;
   constexpr uint32_t KM = kKtopKM;
   const uint32_t bt = blockIdx.x, t = j.kb_terms[bt];
-  const uint32_t na = j.kb_stat[3 * bt], mn = j.kb_stat[3 * bt + 1], mx = j.kb_stat[3 * bt + 2];
+  const uint32_t na = j.kb_stat[3 * bt], mx = j.kb_stat[3 * bt + 2];
   if (threadIdx.x == 0) {
     sh.n_top = 0;
     if (na) j.ktop[(size_t)t * kNumTopK] = __uint_as_float(mx);  // K = 1: the maximum
   }
   __syncthreads();
   const uint32_t c0 = j.kb_chunk0[bt], c1 = j.kb_chunk0[bt + 1];
-  ktop_finish(j, t, na, mn, sh, [&](auto&& f) {
+  ktop_finish(j, t, na, sh, [&](auto&& f) {
     for (uint32_t c = c0; c < c1; ++c) {
       const uint32_t cn = j.kc_cnt[c];
       const uint64_t* keys = j.kc_keys + (size_t)c * KM;

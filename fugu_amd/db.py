@@ -27,7 +27,7 @@ HOST_EXPORTS = (
     "fg_db_namespaces_json", "fg_db_upsert", "fg_db_commit", "fg_db_add_file", "fg_db_doc_count",
     "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query", "fg_parse_query_occur",
     "fg_db_upsert_record", "fg_db_upsert_batch", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
-    "fg_facet_clauses", "fg_db_search_json_post",
+    "fg_facet_clauses", "fg_db_search_json_post", "fg_db_merge_wait", "fg_db_merge_info_get", "fg_db_segment_docs",
 )
 
 _lib = native.lib()
@@ -46,6 +46,13 @@ class _Record(C.Structure):
                 ("has_facets", C.c_int)]
 
 
+class MergeInfo(C.Structure):
+    _fields_ = [("merges", C.c_uint64), ("merged_docs", C.c_uint64), ("merge_ms_total", C.c_double),
+                ("merge_ms_last", C.c_double), ("merge_ms_max", C.c_double), ("segments", C.c_uint32),
+                ("pending", C.c_int), ("n_docs_stats", C.c_uint64), ("tot_tokens", C.c_uint64 * 2),
+                ("tot_facet_tokens", C.c_uint64)]
+
+
 def _sig(name, *args):
     f = getattr(_lib, name)
     f.restype = C.c_int
@@ -59,6 +66,9 @@ _sig("fg_db_namespace_delete", _p, _s)
 _sig("fg_db_namespaces_json", _p, _s, _sz, C.POINTER(_sz))
 _sig("fg_db_upsert", _p, _s, _s, _s, _s, _s)
 _sig("fg_db_commit", _p, _s)
+_sig("fg_db_merge_wait", _p, _s)
+_sig("fg_db_merge_info_get", _p, _s, C.POINTER(MergeInfo))
+_sig("fg_db_segment_docs", _p, _s, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32))
 _sig("fg_db_add_file", _p, _s, _s, _s)
 _sig("fg_db_doc_count", _p, _s, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
 _sig("fg_db_search", _p, _s, _s, C.c_uint32, C.c_uint32, C.POINTER(Hit), C.c_uint32, C.POINTER(C.c_uint32))
@@ -252,6 +262,28 @@ class Database:
 
     def commit(self, namespace: Optional[str] = None):
         _check(_lib.fg_db_commit(self._h, _b(namespace)))
+
+    def merge_wait(self, namespace: Optional[str] = None):
+        """Block until the namespace's background merges are done (fg_db_merge_wait)."""
+        _check(_lib.fg_db_merge_wait(self._h, _b(namespace)))
+
+    def merge_info(self, namespace: Optional[str] = None) -> dict:
+        m = MergeInfo()
+        _check(_lib.fg_db_merge_info_get(self._h, _b(namespace), C.byref(m)))
+        d = {n: getattr(m, n) for n, _ in MergeInfo._fields_}
+        d["tot_tokens"] = list(m.tot_tokens)
+        return d
+
+    def segments(self, namespace: Optional[str] = None) -> list:
+        """Global doc ids of every segment of the current snapshot, in order."""
+        out, seg = [], 0
+        n = C.c_uint32(0)
+        for seg in range(self.merge_info(namespace)["segments"]):
+            _check(_lib.fg_db_segment_docs(self._h, _b(namespace), seg, None, 0, C.byref(n)))
+            buf = (C.c_uint32 * max(n.value, 1))()
+            _check(_lib.fg_db_segment_docs(self._h, _b(namespace), seg, buf, n.value, C.byref(n)))
+            out.append(list(buf[:n.value]))
+        return out
 
     def add_file(self, namespace: str, name: str, body: str):
         _check(_lib.fg_db_add_file(self._h, _b(namespace), _b(name), _b(body)))

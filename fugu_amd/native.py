@@ -53,7 +53,9 @@ EXPORTS = (
     "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
     "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged", "fg_index_term_kth",
+    "fg_model_batch", "fg_abi_version",
 )
+ABI_VERSION = 4  # include/fugu.h FG_ABI_VERSION this binding's structs follow
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -100,6 +102,11 @@ class IndexStats(C.Structure):
                 ("device_bytes", C.c_uint64), ("tot_tokens", C.c_uint64 * 2), ("avgdl", C.c_float * 2),
                 ("has_name", C.c_int), ("device", C.c_int), ("n_facet_terms", C.c_uint32),
                 ("tot_facet_tokens", C.c_uint64), ("n_dense_f32", C.c_uint32), ("n_rank_terms", C.c_uint32)]
+
+
+class ModelOut(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("stream_bytes", "probe_bytes", "output_bytes", "alg_bytes", "line_bytes",
+                                          "query_line_bytes", "loads", "candidates")]
 
 
 class PlanInfo(C.Structure):
@@ -152,6 +159,10 @@ _sig("fg_search_sharded", C.c_int, _p, C.POINTER(_p), C.c_uint32, C.POINTER(Quer
 _sig("fg_merge_shards", C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("fg_bytes_model", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f64p)
 _sig("fg_bytes_model_gpu", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f64p)
+_sig("fg_model_batch", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, _f32p, _f64p, C.POINTER(ModelOut))
+_sig("fg_abi_version", C.c_int)
+if _lib.fg_abi_version() != ABI_VERSION:
+    raise ImportError(f"{LIB_PATH} has ABI {_lib.fg_abi_version()}, this binding follows {ABI_VERSION}: rebuild")
 
 
 class FuguError(RuntimeError):
@@ -452,6 +463,19 @@ class Index:
         out = np.zeros(4 * qb.n_queries, np.float64)
         _check(_lib.fg_bytes_model_or(self._h, C.byref(qb), k, _ptr(t, _f32p), _ptr(out, _f64p)))
         return out.reshape(qb.n_queries, 4)
+
+    def model(self, q_off, terms, k: int, thr=None, mode: int = MODE_AND):
+        """fg_model_batch: the loads k_conj / k_disj issue for the batch replayed on the
+        host (thr: each query's final k-th best score, or None = k_conj's exhaustive
+        cascade).  Returns (dict of the launch's bytes: algorithmic, 128-B line floor,
+        per-query line sum, ...; per-query {stream, probe, output, total} array)."""
+        qb, keep = _batch(q_off, terms, mode)
+        t = None if thr is None else np.ascontiguousarray(thr, np.float32)
+        per = np.zeros(4 * qb.n_queries, np.float64)
+        o = ModelOut()
+        _check(_lib.fg_model_batch(self._h, C.byref(qb), k, None if t is None else _ptr(t, _f32p), _ptr(per, _f64p),
+                                   C.byref(o)))
+        return {n: getattr(o, n) for n, _ in ModelOut._fields_}, per.reshape(qb.n_queries, 4)
 
     def bytes_model_gpu(self, q_off, terms, k: int, mode: int = MODE_AND):
         """fg_bytes_model_gpu: per query {lead, probe, output, total} bytes at the HBM layout."""

@@ -28,6 +28,11 @@
 extern "C" {
 #endif
 
+/* ABI revision: bumped whenever a struct of this header changes layout
+ * (4: fg_query_batch.occur; fg_model_out).  A binding checks fg_abi_version()
+ * against the value it was written for before passing any struct. */
+#define FG_ABI_VERSION 4
+
 #define FG_OK 0
 #define FG_EINVAL (-1)        /* bad argument (e.g. k == 0: tantivy asserts limit >= 1) */
 #define FG_ENODEV (-2)        /* no usable gfx950 device */
@@ -70,6 +75,7 @@ int fg_ctx_destroy(fg_ctx* ctx);
 int fg_ctx_peer_access(const fg_ctx* ctx, int a, int b, int* enabled);
 const char* fg_last_error(void);
 const char* fg_version(void);
+int fg_abi_version(void); /* FG_ABI_VERSION of the library */
 
 /* ---- index snapshot ------------------------------------------------------ */
 /* Documents as analyzed token streams: for each doc the term ids produced by
@@ -303,29 +309,40 @@ int fg_merge_shards(uint32_t n_shards, uint32_t n_queries, uint32_t k, const flo
 int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
                       float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n);
 
-/* SURVEY.md §8(d) algorithmic bytes per query: out[4*i..] = {B_merge, B_skip,
- * B, |I|}.  Host analysis over the host posting copy (keep_host_postings). */
+/* ---- traffic models (roofline numerators; host analysis, model.cpp) --------- */
+/* The loads k_conj / k_disj issue for a batch, replayed on the host over this
+ * snapshot's layout (needs keep_host_postings, reads the score,
+ * bound and directory tables back from the device).  thr_score[i] = query i's
+ * final k-th best score: the replay prunes as an exact MaxScore kernel at that
+ * threshold must at least (k_conj's bounds after each list and a single
+ * list's block-max chunk skip; k_disj's tile split and both bounds); NULL =
+ * k_conj's exhaustive cascade (k_disj at threshold 0).  Pure Must and pure
+ * Should queries only (FG_EINVAL otherwise).  per_query[4*i..] (may be NULL) =
+ * {stream, probe, output, total} bytes of query i. */
+typedef struct fg_model_out {
+  double stream_bytes;     /* lead / essential postings (doc + score); k_disj's per-(tile, clause) ranges + bounds */
+  double probe_bytes;      /* other lists: rank words, posting scores, directory steps, bucket maxima */
+  double output_bytes;     /* 8 B per kept key, <= k per query */
+  double alg_bytes;        /* their sum: the algorithmic bytes of the launch */
+  double line_bytes;       /* 128 B x the distinct 128-B lines those loads touch in the launch: the line floor */
+  double query_line_bytes; /* 128 B x sum over queries of the distinct lines each touches (no cross-query reuse) */
+  double loads;            /* modelled loads (lanes) */
+  double candidates;       /* docs the replay keeps (at the threshold) */
+} fg_model_out;
+int fg_model_batch(const fg_index* ix, const fg_query_batch* q, uint32_t k, const float* thr_score, double* per_query,
+                   fg_model_out* out);
+
+/* SURVEY.md §8(d) algorithmic bytes of tantivy's CPU walk per query: out[4*i..]
+ * = {B_merge, B_skip, B, |I|} (1 KiB block decode per probed 128-posting block;
+ * not bytes the device layout reads). */
 int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);
-/* Algorithmic bytes at THIS snapshot's HBM layout (the roofline numerator,
- * DESIGN.md §5): out[4*i..] = {lead, probe, output, total} bytes of query i.
- * FG_MODE_AND replays k_conj's exhaustive cascade (no MaxScore pruning): 8 B
- * per lead posting (doc id + posting score); then, in intersection order, one
- * probe per candidate still alive -- 8 B rank word + 4 B score on a hit, or
- * 4 B on an f32 score table, or on the bucket directory 8 B of bucket bounds +
- * 4 B per search step + 4 B final compare + 4 B score on a hit; then 8 B per
- * kept key (<= k).  FG_MODE_OR: 8 B
- * per posting of every clause (exhaustive union) + 8 B * k.  Needs
- * keep_host_postings. */
+/* fg_model_batch's per-query bytes with no threshold (FG_MODE_AND: k_conj's
+ * exhaustive cascade -- 8 B per lead posting, then per candidate still alive
+ * 8 B rank word + 4 B score on a hit, or 8 B bucket bounds + 4 B per search
+ * step + 4 B final compare + 4 B score on a hit; 8 B per kept key) or, for
+ * FG_MODE_OR, k_disj at threshold 0. */
 int fg_bytes_model_gpu(const fg_index* ix, const fg_query_batch* q, uint32_t k, double* out);
-/* Algorithmic bytes of k_disj (Should clauses) at THIS layout
- * with the MaxScore threshold fixed at thr_score[i], the query's final k-th
- * best score (the least any exact MaxScore pass reads): out[4*i..] = {stream,
- * probe, output, total} bytes.  Per (tile, clause) 12 B of bounds; per
- * essential posting 8 B (every posting of an all-essential tile: 8 B); per
- * posting past the tile bound, each other clause's rank word (8 B) or bucket
- * maximum (4 B); per posting past the presence bound each present rank
- * clause's score (4 B) and each other clause's directory probe; 8 B * k.
- * Reads the posting scores back from the device; needs keep_host_postings. */
+/* fg_model_batch's per-query bytes at thresholds thr_score (k_disj / k_conj). */
 int fg_bytes_model_or(const fg_index* ix, const fg_query_batch* q, uint32_t k, const float* thr_score, double* out);
 
 #ifdef __cplusplus

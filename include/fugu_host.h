@@ -90,7 +90,29 @@ int fg_db_upsert_batch(fg_db* db, const char* ns, uint32_t n, const char* ids, c
                        const char* texts, const uint64_t* text_off);
 int fg_db_upsert(fg_db* db, const char* ns, const char* id, const char* text, const char* name,
                  const char* metadata_json);
+/* IndexWriter::commit (src/db/document.rs:65): the docs since the last commit
+ * become a segment, the older segments are rescored with the new statistics.
+ * With more than 8 segments the namespace is queued for the background merger
+ * (tantivy's merge threads): a run of small segments becomes one, off the
+ * commit path; readers keep the snapshot they hold. */
 int fg_db_commit(fg_db* db, const char* ns);
+/* Block until no merge of the namespace is queued or running (tests, shutdown);
+ * FG_EHIP with the message when a background merge failed. */
+int fg_db_merge_wait(fg_db* db, const char* ns);
+typedef struct fg_merge_info {
+  uint64_t merges;           /* merges done */
+  uint64_t merged_docs;      /* alive docs written by them */
+  double merge_ms_total, merge_ms_last, merge_ms_max;
+  uint32_t segments;         /* segments of the current snapshot */
+  int pending;               /* a merge is queued or running */
+  uint64_t n_docs_stats;     /* the namespace's BM25 statistics: N (deleted-not-merged included) */
+  uint64_t tot_tokens[2];    /* total_num_tokens(text), (name) */
+  uint64_t tot_facet_tokens; /* total_num_tokens(facet) */
+} fg_merge_info;
+int fg_db_merge_info_get(fg_db* db, const char* ns, fg_merge_info* out);
+/* Global doc ids of segment `seg` of the current snapshot, in its doc order:
+ * *n = its size, out[0..min(n, cap)) (out may be NULL). */
+int fg_db_segment_docs(fg_db* db, const char* ns, uint32_t seg, uint32_t* out, uint32_t cap, uint32_t* n);
 int fg_db_add_file(fg_db* db, const char* ns, const char* name, const char* body);
 /* docs stored in the namespace (deleted included = tantivy max_doc) and alive ones */
 int fg_db_doc_count(fg_db* db, const char* ns, uint64_t* total, uint64_t* alive);

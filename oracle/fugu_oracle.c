@@ -291,6 +291,18 @@ int or_index_set_facets(or_index* ix, uint32_t n_fterms, const uint64_t* facet_o
   return 0;
 }
 
+/* total_num_tokens of `field` set from outside (a merged segment's total
+ * follows tantivy's merger: per source segment with deletes the alive docs'
+ * quantized lengths, merger.rs compute_total_num_tokens), then avgdl and the
+ * tf cache recomputed from it as or_index_build does. */
+int or_index_set_total_tokens(or_index* ix, int field, uint64_t tot) {
+  if (!ix || field < 0 || field >= OR_FIELDS) return -1;
+  ix->tot[field] = tot;
+  ix->avgdl[field] = (float)tot / (float)ix->n_docs;
+  or_bm25_cache(ix->avgdl[field], ix->cache[field]);
+  return 0;
+}
+
 uint32_t or_df(const or_index* ix, int field, uint32_t term) {
   uint32_t nt = field == OR_FACET ? ix->n_fterms : ix->n_terms;
   return term < nt && ix->fld[field] ? ix->fld[field][term].n : 0;

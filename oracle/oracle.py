@@ -61,6 +61,8 @@ _lib.or_search_q.restype = C.c_int
 _lib.or_search_q.argtypes = [_p, _p, _p, C.c_uint32, _p, C.c_uint32, C.c_int, _p, C.c_uint32, C.c_uint32, _p, _p]
 _lib.or_search_batch_q.restype = C.c_double
 _lib.or_search_batch_q.argtypes = [_p, _p, _p, _p, _p, _p, C.c_uint32, C.c_int, C.c_uint32, _p, _p, _p, _p, C.c_int]
+_lib.or_index_set_total_tokens.restype = C.c_int
+_lib.or_index_set_total_tokens.argtypes = [_p, C.c_int, C.c_uint64]
 _lib.or_bytes_model.restype = C.c_int
 _lib.or_bytes_model.argtypes = [_p, _p, C.c_uint32, C.c_uint32, _p]
 
@@ -203,6 +205,11 @@ class OracleIndex:
                                        None if f_off is None else f_terms.ctypes.data, nq, mode, k, score.ctypes.data,
                                        doc.ctypes.data, n.ctypes.data, None if lat is None else lat.ctypes.data, threads)
         return score.reshape(nq, k), doc.reshape(nq, k), n, wall, lat
+
+    def set_total_tokens(self, field: int, tot: int):
+        """total_num_tokens of a field from outside (a merged segment's, tantivy's rule); avgdl follows."""
+        if _lib.or_index_set_total_tokens(self._h, field, tot) != 0:
+            raise ValueError("bad field")
 
     def bytes_model(self, terms, k: int):
         t = np.ascontiguousarray(terms, np.uint32)

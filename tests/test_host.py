@@ -621,39 +621,99 @@ def test_json_shapes_with_hits_and_canonical_metadata(db):
     assert g["query"] == "alpha gamma" and (g["page"], g["per_page"]) == (0, 20) and g["results"][0]["id"] == "d2"
 
 
+def pick_merge(n):
+    """host.cpp pick_merge, restated: with more than 8 segments, the newest
+    segments holding together at most half the docs of the one before them;
+    else the newest run of one size level (factor 4); else, from 16 segments
+    on, the two newest."""
+    c = len(n)
+    if c <= 8:
+        return None
+    suffix = [0] * (c + 1)
+    for j in range(c - 1, -1, -1):
+        suffix[j] = suffix[j + 1] + n[j]
+    for j in range(1, c - 1):
+        if 2 * suffix[j] <= n[j - 1]:
+            return j, c
+
+    def level(x):
+        lv = 0
+        while x >= 4:
+            x >>= 2
+            lv += 1
+        return lv
+    j = c - 1
+    while j > 0 and level(n[j - 1]) == level(n[c - 1]):
+        j -= 1
+    if c - j >= 2:
+        return j, c
+    return (c - 2, c) if c >= 16 else None
+
+
+def quantized(n):
+    """FIELD_NORMS_TABLE[fieldnorm_id(n)]."""
+    from oracle import oracle as orc
+    return int(orc.fieldnorm_table()[orc.fieldnorm_to_id(n)])
+
+
 @pytest.mark.gpu
 def test_db_incremental_commits_segments_vs_oracle(db):
-    """A commit per 200 upserts: each commit adds a segment and rescores the
-    older ones with the new statistics (fg_index_rescore); the ninth merges all
-    into one segment that, like a tantivy merge, drops the deleted docs (N, df
-    and token totals then count the alive docs only).  After every commit the
-    paged AND / OR results equal the oracle run over the same segments
-    (per-segment intersection order, namespace-wide statistics), bit for bit."""
+    """A commit per 100 upserts: each commit adds a segment and rescores the
+    older ones with the new statistics (fg_index_rescore); past 8 segments the
+    background merger replaces a run of small segments by one that, like a
+    tantivy merge, drops the deleted docs (N and df count the alive docs) and
+    takes its total_num_tokens per source segment: the source's own total
+    without deletes, else its alive docs' quantized lengths (merger.rs
+    compute_total_num_tokens).  The model below restates the policy and the
+    statistics; after every commit (and its merges) the host's segments and
+    statistics equal it, and the paged AND / OR results equal the oracle run
+    over the same segments with those totals, bit for bit."""
     from fugu_amd import native
+    from oracle import oracle as orc
     if native.device_count() == 0:
         pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
     ctx = native.Context((0,))
     d = db.Database(ctx)
     d.create_namespace("inc")
     recs = build_corpus(11, 2400)
-    segs = []  # the model's segments: global doc ids each (mirror of the host's merge policy)
+    length = [len(py_analyze(t)) for _, t, _ in recs]
+    nlen = [len(py_analyze(m["name"])) if m and isinstance(m.get("name"), str) else 0 for _, _, m in recs]
+    segs = []  # the model: {"ids": global ids (deleted included), "tot": [text, name]}
     rng = random.Random(5)
-    checked = merged_dropped = 0
-    for c in range(0, len(recs), 200):
-        for rid, t, meta in recs[c:c + 200]:
+    checked = merges = dropped = 0
+    for c in range(0, len(recs), 100):
+        for rid, t, meta in recs[c:c + 100]:
             d.upsert(db.ObjectRecord(rid, t, metadata=meta), "inc")
         d.commit("inc")
-        n = c + 200
-        if len(segs) + 1 > 8:
-            dele = deleted_of(recs[:n])
-            segs = [[g for g in range(n) if not dele[g]]]
-            merged_dropped = n - len(segs[0])
-        else:
-            segs.append(list(range(c, n)))
-        keep = [g for sg in segs for g in sg]
-        bounds = list(np.cumsum([0] + [len(sg) for sg in segs]))
+        d.merge_wait("inc")
+        n = c + 100
+        dele = deleted_of(recs[:n])
+        segs.append({"ids": list(range(c, n)), "tot": [sum(length[c:n]), sum(nlen[c:n])]})
+        while (run := pick_merge([len(sg["ids"]) for sg in segs])) is not None:
+            j0, j1 = run
+            ids, tot = [], [0, 0]
+            for sg in segs[j0:j1]:
+                alive = [g for g in sg["ids"] if not dele[g]]
+                ids += alive
+                if len(alive) == len(sg["ids"]):
+                    tot = [tot[0] + sg["tot"][0], tot[1] + sg["tot"][1]]
+                else:
+                    tot = [tot[0] + sum(quantized(length[g]) for g in alive),
+                           tot[1] + sum(quantized(nlen[g]) for g in alive)]
+                    dropped += len(sg["ids"]) - len(alive)
+            segs[j0:j1] = [{"ids": ids, "tot": tot}]
+            merges += 1
+        assert d.segments("inc") == [sg["ids"] for sg in segs], n
+        info = d.merge_info("inc")
+        keep = [g for sg in segs for g in sg["ids"]]
+        tot = [sum(sg["tot"][f] for sg in segs) for f in (0, 1)]
+        assert info["n_docs_stats"] == len(keep) and info["tot_tokens"] == tot, (n, info, tot)
+        assert info["merges"] == merges
+        bounds = list(np.cumsum([0] + [len(sg["ids"]) for sg in segs]))
         ix, dic = oracle_of(recs[:n], keep)
-        for _ in range(12):
+        for f in (0, 1):
+            ix.set_total_tokens(f, tot[f])
+        for _ in range(8):
             m = rng.randint(1, 4)
             ws = [rng.choice(WORDS) for _ in range(m)]
             q = ws[0] if m == 1 else (" AND ".join(ws) if rng.random() < 0.6 else " ".join(ws))
@@ -666,7 +726,68 @@ def test_db_incremental_commits_segments_vs_oracle(db):
             assert hits_of([g[0] for g in got], [g[1] for g in got]) == want, (n, q, bounds)
             checked += len(want)
         assert d.doc_count("inc")[0] == n
-    assert checked > 300 and merged_dropped > 0
+    assert checked > 300 and merges >= 3 and dropped > 0
+    assert orc.fieldnorm_to_id(41) == 40
+
+
+@pytest.mark.gpu
+def test_db_search_during_background_merge(db, monkeypatch):
+    """Searches while a merge is in flight (FUGU_MERGE_DELAY_MS holds the merge
+    between its build and its swap) see the snapshot before the merge, bit-exact
+    vs the oracle over those segments; after fg_db_merge_wait, the merged one."""
+    import threading
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    monkeypatch.setenv("FUGU_MERGE_DELAY_MS", "1500")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("bg")
+    recs = build_corpus(23, 900)
+    for c in range(0, 900, 100):
+        for rid, t, meta in recs[c:c + 100]:
+            d.upsert(db.ObjectRecord(rid, t, metadata=meta), "bg")
+        d.commit("bg")  # the ninth commit queues a merge of all nine segments
+    assert d.merge_info("bg")["pending"] == 1
+    before = d.segments("bg")
+    assert len(before) == 9
+    rng = random.Random(3)
+    qs = []
+    for _ in range(24):
+        ws = [rng.choice(WORDS) for _ in range(rng.randint(1, 3))]
+        qs.append((ws, " AND ".join(ws) if rng.random() < 0.5 else " ".join(ws)))
+
+    def check(segments):
+        keep = [g for sg in segments for g in sg]
+        bounds = list(np.cumsum([0] + [len(sg) for sg in segments]))
+        ix, dic = oracle_of(recs, keep)
+        if len(segments) == 1:  # merged: per source segment its own total, or its alive docs' quantized lengths
+            dele = deleted_of(recs)
+            length = [len(py_analyze(t)) for _, t, _ in recs]
+            nlen = [len(py_analyze(m["name"])) if m and isinstance(m.get("name"), str) else 0 for _, _, m in recs]
+            for f, ln in ((0, length), (1, nlen)):
+                tot = 0
+                for sg in before:
+                    alive = [g for g in sg if not dele[g]]
+                    tot += sum(ln[g] for g in sg) if len(alive) == len(sg) else sum(quantized(ln[g]) for g in alive)
+                ix.set_total_tokens(f, tot)
+        n = 0
+        for ws, q in qs:
+            mode = 1 if (len(ws) > 1 and " AND " not in q) else 0
+            got = d.search("bg", q, 0, 20)
+            terms = [dic.get(py_analyze(w)[0], native.FG_TERM_MISSING) for w in ws]
+            s, dd = ix.search_segments(np.array(terms, np.uint32), 20, bounds, mode=mode)
+            assert hits_of([g[0] for g in got], [g[1] for g in got]) == [[keep[x], b] for x, b in hits_of(s, dd)], q
+            n += 1
+        return n
+    assert d.merge_info("bg")["pending"] == 1  # still in flight: the old segments answer
+    assert check(before) == len(qs)
+    t = threading.Thread(target=d.merge_wait, args=("bg",))
+    t.start()
+    t.join(60)
+    after = d.segments("bg")
+    assert len(after) == 1 and d.merge_info("bg")["merges"] == 1
+    assert check(after) == len(qs)
 
 
 @pytest.mark.gpu
