@@ -93,6 +93,9 @@ constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #ifndef FG_DISJ_G
 #define FG_DISJ_G 1  // ab_disj_g_k*.log, ab_disj_gpq_k*.log: 4 / 2 / 1 -> OR top-1000 7.00 / 6.51 / 6.13 ms, top-20 4.60 / 4.27 / 3.94 ms
 #endif
+#ifndef FG_LEADPACK
+#define FG_LEADPACK 0  // A/B: packed (doc, score) u64 postings for the streamed lists
+#endif
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
 #endif
@@ -167,6 +170,8 @@ struct DevIndex {
   const float* cmax;         // [score chunks] largest posting score of each kChunk-posting chunk of a
                              //     list (block-max: k_conj skips a lead chunk that cannot reach the threshold)
   const uint32_t* coff;      // [V] index of each term's first chunk in cmax
+  const uint64_t* dps;       // [P] doc | score bits << 32 (FG_LEADPACK builds: the streamed lead /
+                             //     essential postings in one 8-B load), else nullptr
   const uint32_t* fdoc;      // [PF] facet postings (doc ids, ascending), CSR by facet term
   const uint64_t* foff;      // [VF+1]
   uint32_t n_docs;
@@ -294,6 +299,7 @@ struct ScoreJob {
   const float* w_name;        // [V]
   const float* cache;         // [512] K1 * ((1 - B) + B * TABLE[id] / avgdl), text then name
   float* psc;                 // [P] out
+  uint64_t* dps;              // [P] out (doc | score bits << 32) or nullptr
   float* bmax;                // [D] out
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)

@@ -295,6 +295,11 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   void* p;
   if ((rc = dev_alloc(4ull * ix->n_postings + 16, &p))) return rc;  // 16 B of slack: k_conj's 16-B lead loads
   d_psc = static_cast<float*>(p);
+  uint64_t* d_dps = nullptr;
+  if (FG_LEADPACK) {
+    if ((rc = dev_alloc(8ull * ix->n_postings + 16, &p))) return rc;
+    d_dps = static_cast<uint64_t*>(p);
+  }
   if ((rc = dev_alloc(4ull * ix->dir_entries, &p))) return rc;
   d_bmax = static_cast<float*>(p);
   if ((rc = dev_alloc(4ull * V, &p))) return rc;
@@ -323,6 +328,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.w_name = d_wn;
   j.cache = d_cache;
   j.psc = d_psc;
+  j.dps = d_dps;
   j.bmax = d_bmax;
   j.tmaxs = d_tmaxs;
   j.tmax = d_tmax;
@@ -337,7 +343,8 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   // k_ktop: terms of <= kKtopChunk postings one workgroup each; longer terms in
   // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
   // chunks' best keys (k_ktop_big).  The chunk tables and key scratch are
-  // temporary (freed below, after the sync).
+  // temporary: stream-ordered allocations on the build stream, so freeing them
+  // does not synchronize the device (searches on other streams keep running).
   std::vector<uint32_t> kt_small, kb_terms, kb_chunk0, kc_big, kc_start;
   for (uint32_t t = 0; t < V; ++t) {
     const uint64_t df = ix->off[t + 1] - ix->off[t];
@@ -359,15 +366,15 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   struct KtmpBack {
     std::vector<void*>& v;
     ~KtmpBack() {
-      (void)hipStreamSynchronize(nullptr);
-      for (void* x : v) (void)hipFree(x);
+      for (void* x : v) (void)hipFreeAsync(x, nullptr);
     }
   } ktmp_back{ktmp};
   auto tmp_upload = [&](const void* src, size_t n_bytes, void** out) -> int {
     void* q = nullptr;
-    if (hipMalloc(&q, std::max<size_t>(n_bytes, 16)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", n_bytes);
+    if (hipMallocAsync(&q, std::max<size_t>(n_bytes, 16), nullptr) != hipSuccess)
+      return fail(FG_EOOM, "hipMallocAsync(%zu) failed", n_bytes);
     ktmp.push_back(q);
-    if (src && n_bytes) HIPCHK(hipMemcpy(q, src, n_bytes, hipMemcpyHostToDevice));
+    if (src && n_bytes) HIPCHK(hipMemcpyAsync(q, src, n_bytes, hipMemcpyHostToDevice, nullptr));
     *out = q;
     return FG_OK;
   };
@@ -446,6 +453,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   }
   ix->n_dense = (uint32_t)f32_terms.size();
   ix->d.psc = d_psc;
+  ix->d.dps = d_dps;
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
@@ -825,21 +833,27 @@ int fg_ctx_create(int ndev, const int* devs, fg_ctx** out) {
     if (rc) return rc;
   }
   // fg_search_sharded moves each shard's top-k to the first shard's device
-  // with hipMemcpyPeerAsync: direct xGMI transfers need peer access enabled
-  // between every pair of the context's devices (already-enabled is fine)
+  // with hipMemcpyPeerAsync: direct xGMI transfers need peer access, so it is
+  // enabled on every pair that supports it (already-enabled is fine).  A pair
+  // without it still works (the runtime stages the copy through the host);
+  // fg_ctx_peer_access reports which pairs are direct.  The caller's current
+  // device is restored.
+  int prev = 0;
+  HIPCHK(hipGetDevice(&prev));
   for (int a : c->devs)
     for (int b : c->devs) {
       if (a == b) continue;
       int can = 0;
-      HIPCHK(hipDeviceCanAccessPeer(&can, a, b));
-      if (!can) return fail(FG_ENODEV, "device %d cannot access device %d over xGMI", a, b);
-      HIPCHK(hipSetDevice(a));
+      if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) {
+        (void)hipGetLastError();
+        continue;
+      }
+      if (hipSetDevice(a) != hipSuccess) break;
       const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-        return fail(FG_EHIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", a, b, hipGetErrorString(e));
       (void)hipGetLastError();
-      c->peers.emplace_back(a, b);
+      if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) c->peers.emplace_back(a, b);
     }
+  (void)hipSetDevice(prev);
   *out = c.release();
   return FG_OK;
 }

@@ -582,8 +582,14 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
       const bool in = idx < cnt;
       // predicated loads: tools/ab_variants.py measured clamped unconditional
       // loads (every lane issuing) slower here, 1.57 -> 2.05 ms
+#if FG_LEADPACK
+      const uint64_t x = in ? ix.dps[base0 + idx] : (uint64_t)kInvalid;
+      doc[j] = (uint32_t)x;
+      s0[j] = __uint_as_float((uint32_t)(x >> 32));
+#else
       doc[j] = in ? ix.doc[base0 + idx] : kInvalid;
       s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
+#endif
       live |= (in ? 1u : 0u) << j;
     }
     if (tid == 0 && pend > sh.thr) sh.thr = pend;
@@ -1209,8 +1215,14 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       if (e < n_post) {
         uint32_t t;
         const uint64_t at = locate(e, t, npcl[j]);
+#if FG_LEADPACK
+        const uint64_t x = ix.dps[at];
+        npd[j] = (uint32_t)x;
+        nps[j] = __uint_as_float((uint32_t)(x >> 32));
+#else
         npd[j] = ix.doc[at];
         nps[j] = ix.psc[at];
+#endif
       }
     }
   };
@@ -2052,6 +2064,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
     const uint32_t d = in ? j.doc[b + p] : 0xFFFFFFFFu;
     const float v = in ? posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache) : 0.0f;
     if (in) j.psc[b + p] = v;
+    if (in && j.dps) j.dps[b + p] = (uint64_t)d | ((uint64_t)__float_as_uint(v) << 32);
     mx = fmaxf(mx, v);
   }
   // the chunk's block-max (scores >= 0)
