@@ -96,6 +96,12 @@ constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #ifndef FG_LEADPACK
 #define FG_LEADPACK 0  // A/B: packed (doc, score) u64 postings for the streamed lists
 #endif
+#ifndef FG_TDIR
+#define FG_TDIR 1  // A/B: k_disj tile ranges from the tile directory (0: the bucket directory)
+#endif
+#ifndef FG_PBITS
+#define FG_PBITS 0  // A/B: k_conj probes a rank term's presence bitmap first (1024 docs per line)
+#endif
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
 #endif
@@ -162,11 +168,14 @@ struct DevIndex {
   const uint32_t* tmeta;     // [V] meta_slot / meta_rank above
   const float* dense;        // [n_dense * N] doc-indexed term score (-1 = absent), f32-kind slots
   const uint64_t* rank;      // [n_rank * rank_words] rank words, rank-kind slots
+  const uint32_t* pbits;     // [n_rank * rank_words] their presence bits alone (FG_PBITS builds), or nullptr
   const float* tmaxs;        // [V] largest posting score of each term (MaxScore bound)
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
-  const uint32_t* toff;      // [V] first tmax entry of each term, or 0xFFFFFFFF (bucket >= tile: use bmax)
+  const uint32_t* toff;      // [V] first tmax / tdir entry of each term (n_tiles + 1 per term), or
+                             //     0xFFFFFFFF (bucket >= tile: use bmax)
+  const uint32_t* tdir;      // tile directory: tdir[toff[t] + i] = first posting of t at doc >= i << kDisjTileShift
   const float* cmax;         // [score chunks] largest posting score of each kChunk-posting chunk of a
                              //     list (block-max: k_conj skips a lead chunk that cannot reach the threshold)
   const uint32_t* coff;      // [V] index of each term's first chunk in cmax
@@ -332,7 +341,7 @@ hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, 
                         uint32_t* out_shard = nullptr);
 hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s);
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
-                       uint32_t n_words, uint64_t* out, hipStream_t s);
+                       uint32_t n_words, uint64_t* out, uint32_t* pbits, hipStream_t s);
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);

@@ -536,16 +536,31 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   });
   g_bt.mark("directory");
   // per-term tile maxima (4096-doc tiles of k_disj) for terms whose buckets are
-  // no wider than a tile: one load gives a clause's bound over a tile
+  // no wider than a tile: one load gives a clause's bound over a tile; and the
+  // tile directory beside them: tdir[toff + i] = the first posting of tile i
+  // (n_tiles + 1 entries per term, the last = df), so a tile's posting range
+  // is two adjacent loads -- 32 tiles per line, where the bucket directory puts
+  // a dense term's consecutive tile boundaries 4096 >> B_t entries apart
   std::vector<uint32_t> toff(V, 0xFFFFFFFFu);
   const uint64_t n_tiles = ((uint64_t)N + (1u << fg::kDisjTileShift) - 1) >> fg::kDisjTileShift;
   uint64_t ntm = 0;
   for (uint32_t t = 0; t < V; ++t)
     if ((tmeta[t] & 0xFFu) <= fg::kDisjTileShift && hp.off[t + 1] > hp.off[t]) {
-      if (ntm + n_tiles > 0xFFFFFFFFull) break;
+      if (ntm + n_tiles + 1 > 0xFFFFFFFFull) break;
       toff[t] = (uint32_t)ntm;
-      ntm += n_tiles;
+      ntm += n_tiles + 1;
     }
+  std::vector<uint32_t> tdir(ntm);
+  parallel_dynamic(V, hw_threads(0), 64, [&](int, uint32_t tb, uint32_t te) {
+    for (uint32_t t = tb; t < te; ++t) {
+      if (toff[t] == 0xFFFFFFFFu) continue;
+      const uint32_t B = tmeta[t] & 0xFFu;
+      const uint64_t nbk = ((N - 1) >> B) + 1;
+      const uint32_t* dt = dir.data() + dir_off[t];
+      for (uint64_t i = 0; i <= n_tiles; ++i)
+        tdir[toff[t] + i] = dt[std::min<uint64_t>(i << (fg::kDisjTileShift - B), nbk)];
+    }
+  });
   ix->dir_entries = nd;
   ix->tile_entries = ntm;
   // chunk tables of the scoring kernels: (term, first posting) per <= kScoreChunk
@@ -565,7 +580,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   DevAllocs& sm = *ix->smem;
   uint64_t& bytes = ix->struct_bytes;
   int rc;
-  uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_fdoc;
+  uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc;
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
   uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt, *d_coff;
@@ -579,6 +594,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ub.add(dir.data(), dir.size(), &d_dir);
     ub.add(dir_off.data(), dir_off.size(), &d_dir_off);
     ub.add(toff.data(), toff.size(), &d_toff);
+    ub.add(tdir.data(), tdir.size(), &d_tdir);
     ub.add(hp.fdoc.data(), hp.fdoc.size(), &d_fdoc);
     ub.add(hp.foff.data(), hp.foff.size(), &d_foff);
     ub.add(sc_t.data(), sc_t.size(), &d_sct);
@@ -591,6 +607,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   }
   std::vector<uint32_t>().swap(hp.tf);
   std::vector<uint32_t>().swap(dir);
+  std::vector<uint32_t>().swap(tdir);
   g_bt.mark("upload");
   // rank words for the densest terms (fg_internal.h DevIndex): df >= N /
   // kRankDiv, densest first (ties by term id), within a budget of the
@@ -610,6 +627,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   const uint32_t rank_words = (uint32_t)((N + 31) / 32);
   std::vector<uint32_t> rank_terms;
   uint64_t* d_rank = nullptr;
+  uint32_t* d_pbits = nullptr;
   {
     const char* v = getenv("FUGU_RANK_GIB");
     const uint64_t cap = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kRankBudget;
@@ -652,7 +670,15 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     uint64_t tb = 0;
     if ((rc = dev_upload(tmp, sb.data(), sb.size(), &d_sb, &tb))) return rc;
     if ((rc = dev_upload(tmp, sn.data(), sn.size(), &d_sn, &tb))) return rc;
-    HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, nullptr));
+    if (FG_PBITS) {
+      void* q = nullptr;
+      if (hipMalloc(&q, rank_words * 4ull * rank_terms.size()) != hipSuccess)
+        return fail(FG_EOOM, "hipMalloc(presence bits) failed");
+      sm.ptrs.push_back(q);
+      bytes += rank_words * 4ull * rank_terms.size();
+      d_pbits = static_cast<uint32_t*>(q);
+    }
+    HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, d_pbits, nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
   }
   ix->n_rank = (uint32_t)rank_terms.size();
@@ -676,7 +702,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d.dir_off = d_dir_off;
   ix->d.tmeta = d_tmeta;
   ix->d.rank = d_rank;
+  ix->d.pbits = d_pbits;
   ix->d.toff = d_toff;
+  ix->d.tdir = d_tdir;
   ix->d.coff = d_coff;
   ix->d.fdoc = d_fdoc;
   ix->d.foff = d_foff;

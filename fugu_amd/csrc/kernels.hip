@@ -666,6 +666,22 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
         // loads in flight together), then the posting score of the hits
         const uint64_t* __restrict__ rw = ix.rank + (size_t)(dslot - 1) * ix.rank_words;
         const float* __restrict__ ps = ix.psc + ix.off[ti];
+#if FG_PBITS
+        // presence bits first (a line covers 1024 docs), the rank word of the hits
+        const uint32_t* __restrict__ pb = ix.pbits + (size_t)(dslot - 1) * ix.rank_words;
+        uint32_t hit = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+          hit |= (((live >> j) & 1u) ? ((pb[doc[j] >> 5] >> (doc[j] & 31u)) & 1u) : 0u) << j;
+        uint64_t x[kItems];
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) x[j] = (hit & (1u << j)) ? rw[doc[j] >> 5] : 0ull;
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j) {
+          const uint32_t bits = (uint32_t)x[j], b = doc[j] & 31u;
+          sc[j] = (hit & (1u << j)) ? ps[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))] : -1.0f;
+        }
+#else
         uint64_t x[kItems];
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> 5] : 0ull;
@@ -674,6 +690,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
           const uint32_t bits = (uint32_t)x[j], b = doc[j] & 31u;
           sc[j] = ((bits >> b) & 1u) ? ps[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))] : -1.0f;
         }
+#endif
       } else if (dslot) {
         // f32 score table: doc-indexed, one 4-B load per item (-1 = absent)
         const float* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
@@ -1060,10 +1077,16 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[i];
     uint32_t lo, hi;
     float ub;
-    if (B <= kTileShift) {
+    if (FG_TDIR && B <= kTileShift && sh.c_toff[i] != kInvalid) {
+      // the tile directory: adjacent entries (32 tiles of a clause per line)
+      const uint32_t to = sh.c_toff[i] + tile;
+      lo = ix.tdir[to];
+      hi = ix.tdir[to + 1];
+      ub = ix.tmax[to];
+    } else if (B <= kTileShift) {
       lo = dir[d0 >> B];
       hi = dir[((d1 - 1) >> B) + 1];
-      ub = sh.c_toff[i] != kInvalid ? ix.tmax[sh.c_toff[i] + tile] : 0.0f;
+      ub = sh.c_toff[i] != kInvalid ? ix.tmax[sh.c_toff[i] + tile] : ix.tmaxs[terms[i]];
     } else {
       // one bucket holds the tile: branchless searches for d0 and d1 inside it
       const uint32_t b = d0 >> B;
@@ -1977,7 +2000,8 @@ __global__ __launch_bounds__(kThreads) void k_dense(const uint32_t* __restrict__
 __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ doc_all,
                                                    const uint64_t* __restrict__ slot_base,
                                                    const uint32_t* __restrict__ slot_n, uint32_t chunks_per_slot,
-                                                   uint32_t n_words, uint64_t* __restrict__ out_all) {
+                                                   uint32_t n_words, uint64_t* __restrict__ out_all,
+                                                   uint32_t* __restrict__ pbits_all) {
   __shared__ uint32_t bits[kRankChunkWords];
   __shared__ uint32_t scratch[8];
   __shared__ uint32_t range[2];
@@ -2015,16 +2039,17 @@ __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ 
   for (uint32_t i = 0; i < R; ++i) {
     const uint32_t w = w0 + tid * R + i;
     if (w < n_words) out[w] = (uint64_t)bits[tid * R + i] | ((uint64_t)r << 32);
+    if (pbits_all && w < n_words) pbits_all[(size_t)slot * n_words + w] = bits[tid * R + i];
     r += c[i];
   }
 }
 
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
-                       uint32_t n_words, uint64_t* out, hipStream_t s) {
+                       uint32_t n_words, uint64_t* out, uint32_t* pbits, hipStream_t s) {
   if (n_words == 0 || n_slots == 0) return hipSuccess;
   const uint32_t cps = (n_words + kRankChunkWords - 1) / kRankChunkWords;
   if ((uint64_t)cps * n_slots > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  k_rank<<<cps * n_slots, kThreads, 0, s>>>(doc, slot_base, slot_n, cps, n_words, out);
+  k_rank<<<cps * n_slots, kThreads, 0, s>>>(doc, slot_base, slot_n, cps, n_words, out, pbits);
   return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ using fgh::parallel_dynamic;
 
 namespace {
 
-enum Arr : uint32_t { A_DOC, A_PSC, A_RANK, A_DENSE, A_DIR, A_BMAX, A_TMAX, A_CMAX, A_N };
+enum Arr : uint32_t { A_DOC, A_PSC, A_RANK, A_DENSE, A_DIR, A_BMAX, A_TMAX, A_TDIR, A_CMAX, A_N };
 constexpr uint64_t kLine = 128;
 constexpr float kInflate = 1.00000762939453125f;  // kernels.hip inflate_bound: 1 + 2^-17
 
@@ -65,7 +65,7 @@ struct Snap {
     bytes[A_RANK] = 8ull * x->n_rank * x->d.rank_words;
     bytes[A_DENSE] = 4ull * x->n_dense * x->n_docs;
     bytes[A_DIR] = bytes[A_BMAX] = 4 * x->dir_entries;
-    bytes[A_TMAX] = 4 * x->tile_entries;
+    bytes[A_TMAX] = bytes[A_TDIR] = 4 * x->tile_entries;
     bytes[A_CMAX] = 4ull * x->n_sc;
     return FG_OK;
   }
@@ -276,16 +276,20 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
       const uint32_t* l = S.list(t[c]);
       const uint64_t base = ix->off[t[c]], dob = S.dir_off[t[c]];
       float u;
-      if (B[c] <= TS) {
+      if (B[c] <= TS && S.toff[t[c]] != 0xFFFFFFFFu) {
+        const uint64_t to = (uint64_t)S.toff[t[c]] + ti;
+        A.gather(c, A_TDIR, to * 4, 4, A.stream);
+        A.gather(c, A_TDIR, (to + 1) * 4, 4, A.stream);
+        lo[c] = S.pos_ge(t[c], d0);
+        hi[c] = S.pos_ge(t[c], d1);
+        A.gather(c, A_TMAX, to * 4, 4, A.stream);
+        u = S.tmax[to];
+      } else if (B[c] <= TS) {
         A.gather(c, A_DIR, (dob + (d0 >> B[c])) * 4, 4, A.stream);
         A.gather(c, A_DIR, (dob + ((d1 - 1) >> B[c]) + 1) * 4, 4, A.stream);
         lo[c] = S.pos_ge(t[c], d0);
         hi[c] = S.pos_ge(t[c], d1);
-        u = 0.0f;
-        if (S.toff[t[c]] != 0xFFFFFFFFu) {
-          A.gather(c, A_TMAX, ((uint64_t)S.toff[t[c]] + ti) * 4, 4, A.stream);
-          u = S.tmax[S.toff[t[c]] + ti];
-        }
+        u = S.ix->tmaxs[t[c]];
       } else {
         const uint64_t b = d0 >> B[c];
         A.gather(c, A_DIR, (dob + b) * 4, 4, A.stream);

@@ -1,9 +1,9 @@
 set -o pipefail
-# A/B of the packed (doc, score) lead layout (FG_LEADPACK) against the product
-# shape, AND headline batch and OR top-1000 batch, interleaved rounds
+# A/B builds, interleaved rounds on one box (tools/ab_variants.py):
+#   e0 = k_disj tile ranges from the bucket directory (round-3 shape), e1 = the tile directory
+#   l1 = packed (doc, score) postings for the streamed lead / essential lists
+#   p1 = k_conj probes a rank term's presence bitmap before its rank word
 O=gpurun_out/r04b; mkdir -p $O
-V=fugu_amd/variants
-A=$V/libfugu_i8w4t1024b4d256m0g8f4096q896x448h10n16o64_32z12y11u5r512h9g1s16k32768l0.so
-B=$V/libfugu_i8w4t1024b4d256m0g8f4096q896x448h10n16o64_32z12y11u5r512h9g1s16k32768l1.so
-timeout -k 10 500 python -u tools/ab_variants.py --rounds 2 $A $B > $O/ab_leadpack_and.log 2>&1 && tail -1 $O/ab_leadpack_and.log &&
-timeout -k 10 500 python -u tools/ab_variants.py --rounds 2 --disj --k 1000 $A $B > $O/ab_leadpack_k1000.log 2>&1 && tail -1 $O/ab_leadpack_k1000.log
+V=fugu_amd/variants/libfugu_i8w4t1024b4d256m0g8f4096q896x448h10n16o64_32z12y11u5r512h9g1s16k32768
+timeout -k 10 560 python -u tools/ab_variants.py --rounds 2 ${V}l0e1p0.so ${V}l0e1p1.so ${V}l1e1p0.so ${V}l1e1p1.so > $O/ab_and.log 2>&1 && tail -1 $O/ab_and.log &&
+timeout -k 10 480 python -u tools/ab_variants.py --rounds 2 --disj --k 1000 ${V}l0e0p0.so ${V}l0e1p0.so ${V}l1e1p0.so > $O/ab_k1000.log 2>&1 && tail -1 $O/ab_k1000.log
