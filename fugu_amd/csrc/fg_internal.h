@@ -100,7 +100,7 @@ constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #define FG_TDIR 1  // A/B: k_disj tile ranges from the tile directory (0: the bucket directory)
 #endif
 #ifndef FG_PBITS
-#define FG_PBITS 0  // A/B: k_conj probes a rank term's presence bitmap first (1024 docs per line)
+#define FG_PBITS 0  // A/B: a rank term's presence bitmap probed first (1024 docs per line): bit 0 k_conj, bit 1 k_disj bound 2
 #endif
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
@@ -133,6 +133,42 @@ __host__ __device__ inline uint32_t qm_terms(uint32_t qm) { return qm & 0xFFu; }
 __host__ __device__ inline uint32_t qm_must(uint32_t qm) { return (qm >> 8) & 0xFFu; }
 __host__ __device__ inline uint32_t qm_not(uint32_t qm) { return (qm >> 16) & 0xFFu; }
 __host__ __device__ inline uint32_t qm_pack(uint32_t m, uint32_t nm, uint32_t nx) { return m | (nm << 8) | (nx << 16); }
+
+// Rank words (DevIndex::rank): docs per word and the rank field.  FG_RW40 (A/B):
+// 40 presence bits + a 24-bit rank (1.25x the docs per 128-B line; terms of
+// < 2^24 postings only), else 32 presence bits + a 32-bit rank.
+#ifndef FG_RW40
+#define FG_RW40 0
+#endif
+constexpr uint32_t kRankDocs = FG_RW40 ? 40u : 32u;
+static_assert(FG_RW40 == 0 || FG_PBITS == 0, "presence bitmaps are the 32-doc words' low halves");
+constexpr uint64_t kRankMaxDf = FG_RW40 ? (1ull << 24) : (1ull << 32);
+__host__ __device__ inline uint32_t rank_word(uint32_t d) { return d / kRankDocs; }
+__host__ __device__ inline uint32_t rank_bit(uint32_t d) { return d % kRankDocs; }
+// the term's posting position of doc d from its rank word, or 0xFFFFFFFF (absent)
+__host__ __device__ inline uint32_t rank_pos(uint64_t x, uint32_t d) {
+#if FG_RW40 && defined(__HIP_DEVICE_COMPILE__)
+  // recompute the bit from d after the load instead of keeping d % 40 live across it
+  asm volatile("" : "+v"(d));
+#endif
+  const uint32_t b = rank_bit(d);
+  if (!((x >> b) & 1ull)) return 0xFFFFFFFFu;
+#if FG_RW40
+  const uint64_t below = x & ((1ull << b) - 1ull);
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)(x >> 40) + (uint32_t)__popcll(below);
+#else
+  return (uint32_t)(x >> 40) + (uint32_t)__builtin_popcountll(below);
+#endif
+#else
+  const uint32_t below = (uint32_t)x & ((1u << b) - 1u);
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)(x >> 32) + (uint32_t)__popc(below);
+#else
+  return (uint32_t)(x >> 32) + (uint32_t)__builtin_popcount(below);
+#endif
+#endif
+}
 
 // tmeta of a term: bits 0-7 = B_t (bucket shift), 8-15 = S_t (search steps),
 // 16-30 = dense slot + 1 (0: none), bit 31 = the slot's kind (1: rank words, 0: f32 table)

@@ -620,11 +620,13 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   // ids only, so rescored snapshots share them.
   std::vector<uint32_t> by_df;
   for (uint32_t t = 0; t < V; ++t)
-    if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * fg::kRankDiv >= N) by_df.push_back(t);
+    if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * fg::kRankDiv >= N &&
+        hp.off[t + 1] - hp.off[t] < fg::kRankMaxDf)
+      by_df.push_back(t);
   std::stable_sort(by_df.begin(), by_df.end(), [&](uint32_t a, uint32_t b) {
     return hp.off[a + 1] - hp.off[a] > hp.off[b + 1] - hp.off[b];
   });
-  const uint32_t rank_words = (uint32_t)((N + 31) / 32);
+  const uint32_t rank_words = (uint32_t)((N + fg::kRankDocs - 1) / fg::kRankDocs);
   std::vector<uint32_t> rank_terms;
   uint64_t* d_rank = nullptr;
   uint32_t* d_pbits = nullptr;
@@ -670,7 +672,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     uint64_t tb = 0;
     if ((rc = dev_upload(tmp, sb.data(), sb.size(), &d_sb, &tb))) return rc;
     if ((rc = dev_upload(tmp, sn.data(), sn.size(), &d_sn, &tb))) return rc;
-    if (FG_PBITS) {
+    if (FG_PBITS != 0) {
       void* q = nullptr;
       if (hipMalloc(&q, rank_words * 4ull * rank_terms.size()) != hipSuccess)
         return fail(FG_EOOM, "hipMalloc(presence bits) failed");

@@ -75,10 +75,8 @@ __device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f
 __device__ inline float dense_score(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t d) {
   const uint32_t slot = meta_slot(meta);
   if (meta_rank(meta)) {
-    const uint64_t x = ix.rank[(size_t)(slot - 1) * ix.rank_words + (d >> 5)];
-    const uint32_t bits = (uint32_t)x, b = d & 31u;
-    if (!((bits >> b) & 1u)) return -1.0f;
-    return ix.psc[base + (uint32_t)(x >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))];
+    const uint32_t p = rank_pos(ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(d)], d);
+    return p == kInvalid ? -1.0f : ix.psc[base + p];
   }
   return ix.dense[(size_t)(slot - 1) * ix.n_docs + d];
 }
@@ -92,7 +90,7 @@ __device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t t
 // Does term (meta, postings at base, directory at dir_off) hold doc d?  (MustNot probes)
 __device__ inline bool term_has_doc(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t dir_off, uint32_t d) {
   const uint32_t slot = meta_slot(meta);
-  if (slot && meta_rank(meta)) return (ix.rank[(size_t)(slot - 1) * ix.rank_words + (d >> 5)] >> (d & 31u)) & 1ull;
+  if (slot && meta_rank(meta)) return (ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(d)] >> rank_bit(d)) & 1ull;
   if (slot) return ix.dense[(size_t)(slot - 1) * ix.n_docs + d] >= 0.0f;
   const uint32_t* __restrict__ dir = ix.dir + dir_off;
   const uint32_t b = d >> (meta & 0xFFu);
@@ -391,11 +389,11 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
     const float* __restrict__ ps = ix.psc + ix.off[ti];
     uint64_t x[N];
 #pragma unroll
-    for (uint32_t j = 0; j < N; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> 5] : 0ull;
+    for (uint32_t j = 0; j < N; ++j) x[j] = (live & (1u << j)) ? rw[rank_word(doc[j])] : 0ull;
 #pragma unroll
     for (uint32_t j = 0; j < N; ++j) {
-      const uint32_t bits = (uint32_t)x[j], b = doc[j] & 31u;
-      sc[j] = ((bits >> b) & 1u) ? ps[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))] : -1.0f;
+      const uint32_t p = rank_pos(x[j], doc[j]);
+      sc[j] = p != kInvalid ? ps[p] : -1.0f;
     }
   } else if (dslot) {
     // f32 score table: doc-indexed, one 4-B load per item (-1 = absent)
@@ -666,7 +664,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
         // loads in flight together), then the posting score of the hits
         const uint64_t* __restrict__ rw = ix.rank + (size_t)(dslot - 1) * ix.rank_words;
         const float* __restrict__ ps = ix.psc + ix.off[ti];
-#if FG_PBITS
+#if FG_PBITS & 1
         // presence bits first (a line covers 1024 docs), the rank word of the hits
         const uint32_t* __restrict__ pb = ix.pbits + (size_t)(dslot - 1) * ix.rank_words;
         uint32_t hit = 0;
@@ -684,11 +682,11 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
 #else
         uint64_t x[kItems];
 #pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> 5] : 0ull;
+        for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[rank_word(doc[j])] : 0ull;
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
-          const uint32_t bits = (uint32_t)x[j], b = doc[j] & 31u;
-          sc[j] = ((bits >> b) & 1u) ? ps[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))] : -1.0f;
+          const uint32_t p = rank_pos(x[j], doc[j]);
+          sc[j] = p != kInvalid ? ps[p] : -1.0f;
         }
 #endif
       } else if (dslot) {
@@ -1353,12 +1351,26 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
             const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
             const uint32_t slot = meta_slot(meta);
             const bool rank = slot && meta_rank(meta);
+#if FG_PBITS & 2
+            // a rank clause's presence bit first (a line covers 1024 docs): the
+            // rank word only where the clause holds the doc
+            uint32_t pres = 0;
+            if (rank) {
+#pragma unroll
+              for (uint32_t j = 0; j < J; ++j)
+                if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i]))
+                  pres |= ((ix.pbits[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)] >> (pd[j] & 31u)) & 1u) << j;
+            }
+#endif
 #pragma unroll
             for (uint32_t j = 0; j < J; ++j) {
               x[g][j] = kAbsent;
               if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
+#if FG_PBITS & 2
+                if (rank && !((pres >> j) & 1u)) continue;  // absent: contributes nothing, stays exact
+#endif
                 need |= 1u << (g * J + j);
-                if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)];
+                if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(pd[j])];
                 else if (slot) x[g][j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
                 else x[g][j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
               }
@@ -1370,10 +1382,12 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
             const bool rank = meta_slot(meta) && meta_rank(meta);
 #pragma unroll
             for (uint32_t j = 0; j < J; ++j) {
-              const uint32_t bits = (uint32_t)x[g][j], bt = pd[j] & 31u;
-              if (!rank || !((need >> (g * J + j)) & 1u)) y[g][j] = (uint32_t)x[g][j];
-              else y[g][j] = ((bits >> bt) & 1u) ? (uint32_t)(x[g][j] >> 32) + (uint32_t)__popc(bits & ((1u << bt) - 1u))
-                                                 : kAbsent;
+              if (!rank || !((need >> (g * J + j)) & 1u)) {
+                y[g][j] = (uint32_t)x[g][j];
+              } else {
+                const uint32_t p = rank_pos(x[g][j], pd[j]);
+                y[g][j] = p != kInvalid ? p : kAbsent;
+              }
             }
           }
         }
@@ -2003,6 +2017,7 @@ __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ 
                                                    uint32_t n_words, uint64_t* __restrict__ out_all,
                                                    uint32_t* __restrict__ pbits_all) {
   __shared__ uint32_t bits[kRankChunkWords];
+  __shared__ uint32_t bits_hi[FG_RW40 ? kRankChunkWords : 1];  // presence bits 32.. of a 40-doc word
   __shared__ uint32_t scratch[8];
   __shared__ uint32_t range[2];
   const uint32_t tid = threadIdx.x;
@@ -2012,7 +2027,7 @@ __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ 
   uint64_t* __restrict__ out = out_all + (size_t)slot * n_words;
   const uint32_t w0 = chunk * kRankChunkWords;
   if (tid < 2) {
-    const uint64_t target = ((uint64_t)w0 + (tid ? kRankChunkWords : 0u)) << 5;
+    const uint64_t target = ((uint64_t)w0 + (tid ? kRankChunkWords : 0u)) * kRankDocs;
     uint32_t lo = 0, hi = n;  // first posting with doc >= target
     while (lo < hi) {
       const uint32_t mid = lo + ((hi - lo) >> 1);
@@ -2020,25 +2035,30 @@ __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ 
     }
     range[tid] = lo;
   }
-  for (uint32_t i = tid; i < kRankChunkWords; i += kThreads) bits[i] = 0u;
+  for (uint32_t i = tid; i < kRankChunkWords; i += kThreads) {
+    bits[i] = 0u;
+    if (FG_RW40) bits_hi[i] = 0u;
+  }
   __syncthreads();
   for (uint32_t p = range[0] + tid; p < range[1]; p += kThreads) {
-    const uint32_t d = doc[p];
-    atomicOr(&bits[(d >> 5) - w0], 1u << (d & 31u));
+    const uint32_t d = doc[p], b = rank_bit(d);
+    if (FG_RW40 && b >= 32) atomicOr(&bits_hi[rank_word(d) - w0], 1u << (b - 32));
+    else atomicOr(&bits[rank_word(d) - w0], 1u << b);
   }
   __syncthreads();
   constexpr uint32_t R = kRankChunkWords / kThreads;
   uint32_t c[R], sum = 0;
 #pragma unroll
   for (uint32_t i = 0; i < R; ++i) {
-    c[i] = (uint32_t)__popc(bits[tid * R + i]);
+    c[i] = (uint32_t)__popc(bits[tid * R + i]) + (FG_RW40 ? (uint32_t)__popc(bits_hi[FG_RW40 ? tid * R + i : 0]) : 0u);
     sum += c[i];
   }
   uint32_t r = range[0] + block_exclusive_scan(sum, scratch);
 #pragma unroll
   for (uint32_t i = 0; i < R; ++i) {
     const uint32_t w = w0 + tid * R + i;
-    if (w < n_words) out[w] = (uint64_t)bits[tid * R + i] | ((uint64_t)r << 32);
+    const uint64_t pres = (uint64_t)bits[tid * R + i] | (FG_RW40 ? (uint64_t)bits_hi[FG_RW40 ? tid * R + i : 0] << 32 : 0ull);
+    if (w < n_words) out[w] = pres | ((uint64_t)r << kRankDocs);
     if (pbits_all && w < n_words) pbits_all[(size_t)slot * n_words + w] = bits[tid * R + i];
     r += c[i];
   }

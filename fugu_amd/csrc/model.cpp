@@ -153,7 +153,7 @@ float probe_term(const Snap& S, Acc& A, uint32_t s, uint32_t t, uint32_t d, doub
   const uint32_t* l = S.list(t);
   const uint64_t n = S.len(t), base = S.ix->off[t];
   if (slot && fg::meta_rank(meta)) {
-    A.gather(s, A_RANK, ((uint64_t)(slot - 1) * S.ix->d.rank_words + (d >> 5)) * 8, 8, cat);
+    A.gather(s, A_RANK, ((uint64_t)(slot - 1) * S.ix->d.rank_words + fg::rank_word(d)) * 8, 8, cat);
     const uint64_t p = std::lower_bound(l, l + n, d) - l;
     if (p < n && l[p] == d) {
       A.gather(s, A_PSC, (base + p) * 4, 4, cat);
@@ -361,7 +361,7 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
           while (cur[i] < hi[i] && li[cur[i]] < d) ++cur[i];
           const bool here = cur[i] < hi[i] && li[cur[i]] == d;
           if (slot && fg::meta_rank(meta[i])) {
-            A.gather(i, A_RANK, ((uint64_t)(slot - 1) * ix->d.rank_words + (d >> 5)) * 8, 8, A.probe);
+            A.gather(i, A_RANK, ((uint64_t)(slot - 1) * ix->d.rank_words + fg::rank_word(d)) * 8, 8, A.probe);
             if (here) {
               A.gather(i, A_PSC, (bi + cur[i]) * 4, 4, A.probe);
               v[i] = S.psc[bi + cur[i]];
