@@ -93,14 +93,8 @@ constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #ifndef FG_DISJ_G
 #define FG_DISJ_G 1  // ab_disj_g_k*.log, ab_disj_gpq_k*.log: 4 / 2 / 1 -> OR top-1000 7.00 / 6.51 / 6.13 ms, top-20 4.60 / 4.27 / 3.94 ms
 #endif
-#ifndef FG_LEADPACK
-#define FG_LEADPACK 0  // A/B: packed (doc, score) u64 postings for the streamed lists
-#endif
 #ifndef FG_TDIR
 #define FG_TDIR 1  // A/B: k_disj tile ranges from the tile directory (0: the bucket directory)
-#endif
-#ifndef FG_PBITS
-#define FG_PBITS 0  // A/B: a rank term's presence bitmap probed first (1024 docs per line): bit 0 k_conj, bit 1 k_disj bound 2
 #endif
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
@@ -134,39 +128,26 @@ __host__ __device__ inline uint32_t qm_must(uint32_t qm) { return (qm >> 8) & 0x
 __host__ __device__ inline uint32_t qm_not(uint32_t qm) { return (qm >> 16) & 0xFFu; }
 __host__ __device__ inline uint32_t qm_pack(uint32_t m, uint32_t nm, uint32_t nx) { return m | (nm << 8) | (nx << 16); }
 
-// Rank words (DevIndex::rank): docs per word and the rank field.  FG_RW40 (A/B):
-// 40 presence bits + a 24-bit rank (1.25x the docs per 128-B line; terms of
-// < 2^24 postings only), else 32 presence bits + a 32-bit rank.
-#ifndef FG_RW40
-#define FG_RW40 0
-#endif
-constexpr uint32_t kRankDocs = FG_RW40 ? 40u : 32u;
-static_assert(FG_RW40 == 0 || FG_PBITS == 0, "presence bitmaps are the 32-doc words' low halves");
-constexpr uint64_t kRankMaxDf = FG_RW40 ? (1ull << 24) : (1ull << 32);
-__host__ __device__ inline uint32_t rank_word(uint32_t d) { return d / kRankDocs; }
-__host__ __device__ inline uint32_t rank_bit(uint32_t d) { return d % kRankDocs; }
+// Rank words (DevIndex::rank): one u64 per 32 docs, the low half the docs'
+// presence bits, the high half the number of the term's postings before the
+// word's first doc.  (40 presence bits + a 24-bit rank per word -- 1.25x the docs
+// per 128-B line -- measured slower: profiles/r04/ab/ab_and.log.)
+__host__ __device__ inline uint32_t rank_word(uint32_t d) { return d >> 5; }
 // the term's posting position of doc d from its rank word, or 0xFFFFFFFF (absent)
 __host__ __device__ inline uint32_t rank_pos(uint64_t x, uint32_t d) {
-#if FG_RW40 && defined(__HIP_DEVICE_COMPILE__)
-  // recompute the bit from d after the load instead of keeping d % 40 live across it
+#if defined(__HIP_DEVICE_COMPILE__)
+  // recompute the bit from d after the word's load instead of keeping it live
+  // across the load (without this k_conj spills 14 VGPRs: 1.06 -> 1.41 ms,
+  // profiles/r04/ab/spilled_ab_and.log)
   asm volatile("" : "+v"(d));
 #endif
-  const uint32_t b = rank_bit(d);
+  const uint32_t b = d & 31u;
   if (!((x >> b) & 1ull)) return 0xFFFFFFFFu;
-#if FG_RW40
-  const uint64_t below = x & ((1ull << b) - 1ull);
-#if defined(__HIP_DEVICE_COMPILE__)
-  return (uint32_t)(x >> 40) + (uint32_t)__popcll(below);
-#else
-  return (uint32_t)(x >> 40) + (uint32_t)__builtin_popcountll(below);
-#endif
-#else
   const uint32_t below = (uint32_t)x & ((1u << b) - 1u);
 #if defined(__HIP_DEVICE_COMPILE__)
   return (uint32_t)(x >> 32) + (uint32_t)__popc(below);
 #else
   return (uint32_t)(x >> 32) + (uint32_t)__builtin_popcount(below);
-#endif
 #endif
 }
 
@@ -204,7 +185,6 @@ struct DevIndex {
   const uint32_t* tmeta;     // [V] meta_slot / meta_rank above
   const float* dense;        // [n_dense * N] doc-indexed term score (-1 = absent), f32-kind slots
   const uint64_t* rank;      // [n_rank * rank_words] rank words, rank-kind slots
-  const uint32_t* pbits;     // [n_rank * rank_words] their presence bits alone (FG_PBITS builds), or nullptr
   const float* tmaxs;        // [V] largest posting score of each term (MaxScore bound)
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
@@ -215,8 +195,6 @@ struct DevIndex {
   const float* cmax;         // [score chunks] largest posting score of each kChunk-posting chunk of a
                              //     list (block-max: k_conj skips a lead chunk that cannot reach the threshold)
   const uint32_t* coff;      // [V] index of each term's first chunk in cmax
-  const uint64_t* dps;       // [P] doc | score bits << 32 (FG_LEADPACK builds: the streamed lead /
-                             //     essential postings in one 8-B load), else nullptr
   const uint32_t* fdoc;      // [PF] facet postings (doc ids, ascending), CSR by facet term
   const uint64_t* foff;      // [VF+1]
   uint32_t n_docs;
@@ -344,7 +322,6 @@ struct ScoreJob {
   const float* w_name;        // [V]
   const float* cache;         // [512] K1 * ((1 - B) + B * TABLE[id] / avgdl), text then name
   float* psc;                 // [P] out
-  uint64_t* dps;              // [P] out (doc | score bits << 32) or nullptr
   float* bmax;                // [D] out
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
@@ -377,7 +354,7 @@ hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, 
                         uint32_t* out_shard = nullptr);
 hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s);
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
-                       uint32_t n_words, uint64_t* out, uint32_t* pbits, hipStream_t s);
+                       uint32_t n_words, uint64_t* out, hipStream_t s);
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);

@@ -295,11 +295,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   void* p;
   if ((rc = dev_alloc(4ull * ix->n_postings + 16, &p))) return rc;  // 16 B of slack: k_conj's 16-B lead loads
   d_psc = static_cast<float*>(p);
-  uint64_t* d_dps = nullptr;
-  if (FG_LEADPACK) {
-    if ((rc = dev_alloc(8ull * ix->n_postings + 16, &p))) return rc;
-    d_dps = static_cast<uint64_t*>(p);
-  }
   if ((rc = dev_alloc(4ull * ix->dir_entries, &p))) return rc;
   d_bmax = static_cast<float*>(p);
   if ((rc = dev_alloc(4ull * V, &p))) return rc;
@@ -328,7 +323,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.w_name = d_wn;
   j.cache = d_cache;
   j.psc = d_psc;
-  j.dps = d_dps;
   j.bmax = d_bmax;
   j.tmaxs = d_tmaxs;
   j.tmax = d_tmax;
@@ -453,7 +447,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   }
   ix->n_dense = (uint32_t)f32_terms.size();
   ix->d.psc = d_psc;
-  ix->d.dps = d_dps;
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
@@ -620,16 +613,13 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   // ids only, so rescored snapshots share them.
   std::vector<uint32_t> by_df;
   for (uint32_t t = 0; t < V; ++t)
-    if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * fg::kRankDiv >= N &&
-        hp.off[t + 1] - hp.off[t] < fg::kRankMaxDf)
-      by_df.push_back(t);
+    if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * fg::kRankDiv >= N) by_df.push_back(t);
   std::stable_sort(by_df.begin(), by_df.end(), [&](uint32_t a, uint32_t b) {
     return hp.off[a + 1] - hp.off[a] > hp.off[b + 1] - hp.off[b];
   });
-  const uint32_t rank_words = (uint32_t)((N + fg::kRankDocs - 1) / fg::kRankDocs);
+  const uint32_t rank_words = (uint32_t)((N + 31) / 32);
   std::vector<uint32_t> rank_terms;
   uint64_t* d_rank = nullptr;
-  uint32_t* d_pbits = nullptr;
   {
     const char* v = getenv("FUGU_RANK_GIB");
     const uint64_t cap = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kRankBudget;
@@ -672,15 +662,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     uint64_t tb = 0;
     if ((rc = dev_upload(tmp, sb.data(), sb.size(), &d_sb, &tb))) return rc;
     if ((rc = dev_upload(tmp, sn.data(), sn.size(), &d_sn, &tb))) return rc;
-    if (FG_PBITS != 0) {
-      void* q = nullptr;
-      if (hipMalloc(&q, rank_words * 4ull * rank_terms.size()) != hipSuccess)
-        return fail(FG_EOOM, "hipMalloc(presence bits) failed");
-      sm.ptrs.push_back(q);
-      bytes += rank_words * 4ull * rank_terms.size();
-      d_pbits = static_cast<uint32_t*>(q);
-    }
-    HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, d_pbits, nullptr));
+    HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
   }
   ix->n_rank = (uint32_t)rank_terms.size();
@@ -704,7 +686,6 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d.dir_off = d_dir_off;
   ix->d.tmeta = d_tmeta;
   ix->d.rank = d_rank;
-  ix->d.pbits = d_pbits;
   ix->d.toff = d_toff;
   ix->d.tdir = d_tdir;
   ix->d.coff = d_coff;

@@ -90,7 +90,7 @@ __device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t t
 // Does term (meta, postings at base, directory at dir_off) hold doc d?  (MustNot probes)
 __device__ inline bool term_has_doc(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t dir_off, uint32_t d) {
   const uint32_t slot = meta_slot(meta);
-  if (slot && meta_rank(meta)) return (ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(d)] >> rank_bit(d)) & 1ull;
+  if (slot && meta_rank(meta)) return (ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(d)] >> (d & 31u)) & 1ull;
   if (slot) return ix.dense[(size_t)(slot - 1) * ix.n_docs + d] >= 0.0f;
   const uint32_t* __restrict__ dir = ix.dir + dir_off;
   const uint32_t b = d >> (meta & 0xFFu);
@@ -580,14 +580,8 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
       const bool in = idx < cnt;
       // predicated loads: tools/ab_variants.py measured clamped unconditional
       // loads (every lane issuing) slower here, 1.57 -> 2.05 ms
-#if FG_LEADPACK
-      const uint64_t x = in ? ix.dps[base0 + idx] : (uint64_t)kInvalid;
-      doc[j] = (uint32_t)x;
-      s0[j] = __uint_as_float((uint32_t)(x >> 32));
-#else
       doc[j] = in ? ix.doc[base0 + idx] : kInvalid;
       s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
-#endif
       live |= (in ? 1u : 0u) << j;
     }
     if (tid == 0 && pend > sh.thr) sh.thr = pend;
@@ -664,22 +658,6 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
         // loads in flight together), then the posting score of the hits
         const uint64_t* __restrict__ rw = ix.rank + (size_t)(dslot - 1) * ix.rank_words;
         const float* __restrict__ ps = ix.psc + ix.off[ti];
-#if FG_PBITS & 1
-        // presence bits first (a line covers 1024 docs), the rank word of the hits
-        const uint32_t* __restrict__ pb = ix.pbits + (size_t)(dslot - 1) * ix.rank_words;
-        uint32_t hit = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j)
-          hit |= (((live >> j) & 1u) ? ((pb[doc[j] >> 5] >> (doc[j] & 31u)) & 1u) : 0u) << j;
-        uint64_t x[kItems];
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) x[j] = (hit & (1u << j)) ? rw[doc[j] >> 5] : 0ull;
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) {
-          const uint32_t bits = (uint32_t)x[j], b = doc[j] & 31u;
-          sc[j] = (hit & (1u << j)) ? ps[(uint32_t)(x[j] >> 32) + (uint32_t)__popc(bits & ((1u << b) - 1u))] : -1.0f;
-        }
-#else
         uint64_t x[kItems];
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[rank_word(doc[j])] : 0ull;
@@ -688,7 +666,6 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
           const uint32_t p = rank_pos(x[j], doc[j]);
           sc[j] = p != kInvalid ? ps[p] : -1.0f;
         }
-#endif
       } else if (dslot) {
         // f32 score table: doc-indexed, one 4-B load per item (-1 = absent)
         const float* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
@@ -1236,14 +1213,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       if (e < n_post) {
         uint32_t t;
         const uint64_t at = locate(e, t, npcl[j]);
-#if FG_LEADPACK
-        const uint64_t x = ix.dps[at];
-        npd[j] = (uint32_t)x;
-        nps[j] = __uint_as_float((uint32_t)(x >> 32));
-#else
         npd[j] = ix.doc[at];
         nps[j] = ix.psc[at];
-#endif
       }
     }
   };
@@ -1351,24 +1322,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
             const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
             const uint32_t slot = meta_slot(meta);
             const bool rank = slot && meta_rank(meta);
-#if FG_PBITS & 2
-            // a rank clause's presence bit first (a line covers 1024 docs): the
-            // rank word only where the clause holds the doc
-            uint32_t pres = 0;
-            if (rank) {
-#pragma unroll
-              for (uint32_t j = 0; j < J; ++j)
-                if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i]))
-                  pres |= ((ix.pbits[(size_t)(slot - 1) * ix.rank_words + (pd[j] >> 5)] >> (pd[j] & 31u)) & 1u) << j;
-            }
-#endif
 #pragma unroll
             for (uint32_t j = 0; j < J; ++j) {
               x[g][j] = kAbsent;
               if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
-#if FG_PBITS & 2
-                if (rank && !((pres >> j) & 1u)) continue;  // absent: contributes nothing, stays exact
-#endif
                 need |= 1u << (g * J + j);
                 if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(pd[j])];
                 else if (slot) x[g][j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
@@ -2014,10 +1971,8 @@ __global__ __launch_bounds__(kThreads) void k_dense(const uint32_t* __restrict__
 __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ doc_all,
                                                    const uint64_t* __restrict__ slot_base,
                                                    const uint32_t* __restrict__ slot_n, uint32_t chunks_per_slot,
-                                                   uint32_t n_words, uint64_t* __restrict__ out_all,
-                                                   uint32_t* __restrict__ pbits_all) {
+                                                   uint32_t n_words, uint64_t* __restrict__ out_all) {
   __shared__ uint32_t bits[kRankChunkWords];
-  __shared__ uint32_t bits_hi[FG_RW40 ? kRankChunkWords : 1];  // presence bits 32.. of a 40-doc word
   __shared__ uint32_t scratch[8];
   __shared__ uint32_t range[2];
   const uint32_t tid = threadIdx.x;
@@ -2027,7 +1982,7 @@ __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ 
   uint64_t* __restrict__ out = out_all + (size_t)slot * n_words;
   const uint32_t w0 = chunk * kRankChunkWords;
   if (tid < 2) {
-    const uint64_t target = ((uint64_t)w0 + (tid ? kRankChunkWords : 0u)) * kRankDocs;
+    const uint64_t target = ((uint64_t)w0 + (tid ? kRankChunkWords : 0u)) << 5;
     uint32_t lo = 0, hi = n;  // first posting with doc >= target
     while (lo < hi) {
       const uint32_t mid = lo + ((hi - lo) >> 1);
@@ -2035,41 +1990,35 @@ __global__ __launch_bounds__(kThreads) void k_rank(const uint32_t* __restrict__ 
     }
     range[tid] = lo;
   }
-  for (uint32_t i = tid; i < kRankChunkWords; i += kThreads) {
-    bits[i] = 0u;
-    if (FG_RW40) bits_hi[i] = 0u;
-  }
+  for (uint32_t i = tid; i < kRankChunkWords; i += kThreads) bits[i] = 0u;
   __syncthreads();
   for (uint32_t p = range[0] + tid; p < range[1]; p += kThreads) {
-    const uint32_t d = doc[p], b = rank_bit(d);
-    if (FG_RW40 && b >= 32) atomicOr(&bits_hi[rank_word(d) - w0], 1u << (b - 32));
-    else atomicOr(&bits[rank_word(d) - w0], 1u << b);
+    const uint32_t d = doc[p];
+    atomicOr(&bits[rank_word(d) - w0], 1u << (d & 31u));
   }
   __syncthreads();
   constexpr uint32_t R = kRankChunkWords / kThreads;
   uint32_t c[R], sum = 0;
 #pragma unroll
   for (uint32_t i = 0; i < R; ++i) {
-    c[i] = (uint32_t)__popc(bits[tid * R + i]) + (FG_RW40 ? (uint32_t)__popc(bits_hi[FG_RW40 ? tid * R + i : 0]) : 0u);
+    c[i] = (uint32_t)__popc(bits[tid * R + i]);
     sum += c[i];
   }
   uint32_t r = range[0] + block_exclusive_scan(sum, scratch);
 #pragma unroll
   for (uint32_t i = 0; i < R; ++i) {
     const uint32_t w = w0 + tid * R + i;
-    const uint64_t pres = (uint64_t)bits[tid * R + i] | (FG_RW40 ? (uint64_t)bits_hi[FG_RW40 ? tid * R + i : 0] << 32 : 0ull);
-    if (w < n_words) out[w] = pres | ((uint64_t)r << kRankDocs);
-    if (pbits_all && w < n_words) pbits_all[(size_t)slot * n_words + w] = bits[tid * R + i];
+    if (w < n_words) out[w] = (uint64_t)bits[tid * R + i] | ((uint64_t)r << 32);
     r += c[i];
   }
 }
 
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
-                       uint32_t n_words, uint64_t* out, uint32_t* pbits, hipStream_t s) {
+                       uint32_t n_words, uint64_t* out, hipStream_t s) {
   if (n_words == 0 || n_slots == 0) return hipSuccess;
   const uint32_t cps = (n_words + kRankChunkWords - 1) / kRankChunkWords;
   if ((uint64_t)cps * n_slots > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  k_rank<<<cps * n_slots, kThreads, 0, s>>>(doc, slot_base, slot_n, cps, n_words, out, pbits);
+  k_rank<<<cps * n_slots, kThreads, 0, s>>>(doc, slot_base, slot_n, cps, n_words, out);
   return hipGetLastError();
 }
 
@@ -2109,7 +2058,6 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
     const uint32_t d = in ? j.doc[b + p] : 0xFFFFFFFFu;
     const float v = in ? posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache) : 0.0f;
     if (in) j.psc[b + p] = v;
-    if (in && j.dps) j.dps[b + p] = (uint64_t)d | ((uint64_t)__float_as_uint(v) << 32);
     mx = fmaxf(mx, v);
   }
   // the chunk's block-max (scores >= 0)

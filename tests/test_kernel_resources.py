@@ -1,0 +1,61 @@
+"""Register budget of the hot kernels, read from the gfx950 code object inside
+the built libfugu.so (no GPU needed).
+
+k_conj and k_disj are latency-bound; their occupancy (4 and 5 waves/SIMD) is
+their main lever, and a spill puts scratch traffic on every probe.  A source
+change that silently made k_conj spill took the headline kernel from 1.06 to
+1.41 ms (profiles/r04/ab/spilled_ab_and.log), so the budget is checked here:
+  * single-snapshot k_conj / k_disj instantiations: no scratch, no VGPR spill;
+  * k_conj <= 128 VGPRs (4 waves/SIMD), k_disj <= 96 VGPRs (5 waves/SIMD);
+  * the multi-snapshot k_conj (segmented namespaces, C4) at most the 20 B of
+    scratch it has carried since round 3.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "fugu_amd", "libfugu.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def kernel_meta(tmp_path):
+    fat = tmp_path / "fatbin.bin"
+    co = tmp_path / "gfx950.co"
+    subprocess.run([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", LIB, str(fat)], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], check=True, capture_output=True,
+                           text=True).stdout
+    meta, cur = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s+\.name:\s+(\S+)", line)
+        if m:
+            cur = m.group(1)
+            meta[cur] = {}
+            continue
+        m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count|vgpr_count):\s+(\d+)", line)
+        if m and cur:
+            meta[cur][m.group(1)] = int(m.group(2))
+    return meta
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(f"{LLVM}/llvm-readelf")),
+                    reason="needs the built libfugu.so and the ROCm LLVM tools")
+def test_hot_kernels_fit_their_register_budget(tmp_path):
+    meta = kernel_meta(tmp_path)
+    conj = {k: v for k, v in meta.items() if "k_conjI" in k}
+    disj = {k: v for k, v in meta.items() if "k_disjI" in k}
+    assert len(conj) == 4 and len(disj) == 2, sorted(meta)
+    for name, v in conj.items():
+        multi_general = "k_conjILb0ELb1E" in name
+        assert v["vgpr_count"] <= 128, (name, v)
+        if multi_general:
+            assert v["private_segment_fixed_size"] <= 20, (name, v)
+        else:
+            assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (name, v)
+    for name, v in disj.items():
+        assert v["vgpr_count"] <= 96, (name, v)
+        assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (name, v)
