@@ -187,13 +187,23 @@ struct HostPostings {
 
 namespace {
 
+// Snapshot builds and rescores run on the calling thread's own stream (never
+// the legacy null stream, which serialises with every other stream): a
+// commit's rescores of the older segments, its new segment's build and the
+// background merger's build run side by side.  Uploads are synchronous with
+// the host (the sources may be freed right after).
+const hipStream_t kBuildStream = hipStreamPerThread;
+
 template <class T>
 int dev_upload(DevAllocs& m, const T* src, size_t n, T** out, uint64_t* bytes) {
   size_t b = std::max<size_t>(n * sizeof(T), 16);
   void* p = nullptr;
   if (hipMalloc(&p, b) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", b);
   m.ptrs.push_back(p);
-  if (n) HIPCHK(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(p, src, n * sizeof(T), hipMemcpyHostToDevice, kBuildStream));
+    HIPCHK(hipStreamSynchronize(kBuildStream));
+  }
   *out = static_cast<T*>(p);
   *bytes += b;
   return FG_OK;
@@ -217,10 +227,11 @@ struct UploadBatch {
     size_t o = 0;
     for (const E& e : es) {
       char* d = static_cast<char*>(p) + o;
-      if (e.bytes) HIPCHK(hipMemcpy(d, e.src, e.bytes, hipMemcpyHostToDevice));
+      if (e.bytes) HIPCHK(hipMemcpyAsync(d, e.src, e.bytes, hipMemcpyHostToDevice, kBuildStream));
       *e.out = d;
       o += (std::max<size_t>(e.bytes, 16) + 16 + 255) & ~size_t(255);
     }
+    HIPCHK(hipStreamSynchronize(kBuildStream));
     *bytes += total;
     return FG_OK;
   }
@@ -244,8 +255,48 @@ int check_device(int dev) {
 // K-th best alive scores (k_ktop), optional f32 score tables, the alive
 // bitset.  `df_t`/`df_n`/`df_f`: the statistics' doc frequencies (global for a
 // doc-sharded namespace).  Structure arrays must be in ix->d already.
+// Pinned host memory of the calling thread for the read-back of a snapshot's
+// per-term bounds (pageable read-backs of several snapshots scored side by side
+// serialise on the staging copies).
+uint8_t* pinned_scratch(size_t bytes) {
+  struct Buf {
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    ~Buf() {
+      if (p) (void)hipHostFree(p);
+    }
+  };
+  thread_local Buf b;
+  if (b.n < bytes) {
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&b.p), bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    b.n = bytes;
+  }
+  return b.p;
+}
+
+// BM25 weights of terms [0, V) for statistics (Ns, df_t, df_n) (tantivy's f32 order)
+void bm25_weights(uint64_t Ns, const uint32_t* df_t, const uint32_t* df_n, uint32_t V, std::vector<float>& wt,
+                  std::vector<float>& wn) {
+  wt.resize(V);
+  wn.resize(V);
+  parallel_ranges(V, hw_threads(0), [&](int, uint32_t b, uint32_t e) {
+    for (uint32_t t = b; t < e; ++t) {
+      wt[t] = bm25_weight(df_t[t], Ns);
+      wn[t] = bm25_weight(df_n ? df_n[t] : 0u, Ns);
+    }
+  });
+}
+
+// wts: the weights of (Ns, df_t, df_n) for at least ix's terms, or nullptr (computed here)
 int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_t* df_t, const uint32_t* df_n,
-                const std::vector<uint32_t>& alive, uint64_t tot_f, const uint32_t* df_f) {
+                const std::vector<uint32_t>& alive, uint64_t tot_f, const uint32_t* df_f,
+                const std::pair<std::vector<float>, std::vector<float>>* wts = nullptr) {
   const uint32_t V = ix->n_terms;
   const uint64_t N = ix->n_docs;
   ix->n_stats = Ns;
@@ -255,14 +306,12 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
     ix->avgdl[f] = (float)ix->tot[f] / (float)Ns;  // total_num_tokens as f32 / N as f32
     bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
   }
-  ix->w_text.resize(V);
-  ix->w_name.resize(V);
-  parallel_ranges(V, hw_threads(0), [&](int, uint32_t b, uint32_t e) {
-    for (uint32_t t = b; t < e; ++t) {
-      ix->w_text[t] = bm25_weight(df_t[t], Ns);
-      ix->w_name[t] = bm25_weight(df_n ? df_n[t] : 0u, Ns);
-    }
-  });
+  if (wts) {
+    ix->w_text.assign(wts->first.begin(), wts->first.begin() + V);
+    ix->w_name.assign(wts->second.begin(), wts->second.begin() + V);
+  } else {
+    bm25_weights(Ns, df_t, df_n, V, ix->w_text, ix->w_name);
+  }
   // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
   // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
   const uint32_t VF = ix->n_fterms;
@@ -305,9 +354,9 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   d_ktop = static_cast<float*>(p);
   if ((rc = dev_alloc(4ull * ix->n_sc, &p))) return rc;
   float* d_cmax = static_cast<float*>(p);
-  HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, nullptr));
-  HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), nullptr));
-  HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, nullptr));
+  HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, kBuildStream));
+  HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), kBuildStream));
+  HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, kBuildStream));
   fg::ScoreJob j{};
   j.doc = ix->d.doc;
   j.tfp = ix->d_tfp;
@@ -330,10 +379,10 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.cmax = d_cmax;
   j.ch_term = ix->d_sc_term;
   j.ch_first = ix->d_sc_first;
-  HIPCHK(fg::launch_score(j, ix->n_sc, nullptr));
+  HIPCHK(fg::launch_score(j, ix->n_sc, kBuildStream));
   j.ch_term = ix->d_bk_term;
   j.ch_first = ix->d_bk_first;
-  HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, nullptr));
+  HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
   // k_ktop: terms of <= kKtopChunk postings one workgroup each; longer terms in
   // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
   // chunks' best keys (k_ktop_big).  The chunk tables and key scratch are
@@ -360,15 +409,15 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   struct KtmpBack {
     std::vector<void*>& v;
     ~KtmpBack() {
-      for (void* x : v) (void)hipFreeAsync(x, nullptr);
+      for (void* x : v) (void)hipFreeAsync(x, kBuildStream);
     }
   } ktmp_back{ktmp};
   auto tmp_upload = [&](const void* src, size_t n_bytes, void** out) -> int {
     void* q = nullptr;
-    if (hipMallocAsync(&q, std::max<size_t>(n_bytes, 16), nullptr) != hipSuccess)
+    if (hipMallocAsync(&q, std::max<size_t>(n_bytes, 16), kBuildStream) != hipSuccess)
       return fail(FG_EOOM, "hipMallocAsync(%zu) failed", n_bytes);
     ktmp.push_back(q);
-    if (src && n_bytes) HIPCHK(hipMemcpyAsync(q, src, n_bytes, hipMemcpyHostToDevice, nullptr));
+    if (src && n_bytes) HIPCHK(hipMemcpyAsync(q, src, n_bytes, hipMemcpyHostToDevice, kBuildStream));
     *out = q;
     return FG_OK;
   };
@@ -389,12 +438,20 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.kc_keys = static_cast<uint64_t*>(d_kck);
   j.kc_cnt = static_cast<uint32_t*>(d_kcc);
   j.kb_stat = static_cast<uint32_t*>(d_kbs);
-  HIPCHK(fg::launch_ktop(j, (uint32_t)n_small, (uint32_t)n_chunks, (uint32_t)n_big, nullptr));
-  HIPCHK(hipStreamSynchronize(nullptr));
+  HIPCHK(fg::launch_ktop(j, (uint32_t)n_small, (uint32_t)n_chunks, (uint32_t)n_big, kBuildStream));
   ix->tmaxs.resize(V);
   ix->ktop.resize((size_t)V * fg::kNumTopK);
-  HIPCHK(hipMemcpy(ix->tmaxs.data(), d_tmaxs, 4ull * V, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(ix->ktop.data(), d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost));
+  if (uint8_t* pin = pinned_scratch(4ull * V * (1 + fg::kNumTopK))) {
+    HIPCHK(hipMemcpyAsync(pin, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
+    HIPCHK(hipMemcpyAsync(pin + 4ull * V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
+    HIPCHK(hipStreamSynchronize(kBuildStream));
+    std::memcpy(ix->tmaxs.data(), pin, 4ull * V);
+    std::memcpy(ix->ktop.data(), pin + 4ull * V, 4ull * V * fg::kNumTopK);
+  } else {
+    HIPCHK(hipMemcpyAsync(ix->tmaxs.data(), d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
+    HIPCHK(hipMemcpyAsync(ix->ktop.data(), d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
+    HIPCHK(hipStreamSynchronize(kBuildStream));
+  }
   g_bt.mark("device scoring");
   // f32 score tables (FUGU_DENSE_GIB, default none: rank words serve the dense
   // terms) for the densest terms without rank words, filled from the new scores
@@ -432,14 +489,14 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   }
   std::vector<uint32_t> tmeta = ix->tmeta;
   if (!f32_terms.empty()) {
-    HIPCHK(hipMemsetD32(d_dense, (int)0xBF800000u, N * f32_terms.size()));  // -1.0f: absent
+    HIPCHK(hipMemsetD32Async(d_dense, (int)0xBF800000u, N * f32_terms.size(), kBuildStream));  // -1.0f: absent
     for (uint32_t s2 = 0; s2 < f32_terms.size(); ++s2) {
       const uint32_t t = f32_terms[s2];
       HIPCHK(fg::launch_dense(ix->d.doc, d_psc, ix->off[t], (uint32_t)(ix->off[t + 1] - ix->off[t]),
-                              d_dense + (size_t)s2 * N, nullptr));
+                              d_dense + (size_t)s2 * N, kBuildStream));
       tmeta[t] |= (s2 + 1) << 16;  // f32 kind (bit 31 clear)
     }
-    HIPCHK(hipStreamSynchronize(nullptr));
+    HIPCHK(hipStreamSynchronize(kBuildStream));
     uint32_t* d_tm;
     if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tm, &bytes))) return rc;
     ix->d.tmeta = d_tm;
@@ -655,15 +712,18 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       sn[s2] = (uint32_t)(hp.off[t + 1] - hp.off[t]);
       tmeta[t] |= ((s2 + 1) << 16) | 0x80000000u;
     }
-    DevAllocs tmp;
-    tmp.dev = dev;
-    uint64_t* d_sb;
-    uint32_t* d_sn;
-    uint64_t tb = 0;
-    if ((rc = dev_upload(tmp, sb.data(), sb.size(), &d_sb, &tb))) return rc;
-    if ((rc = dev_upload(tmp, sn.data(), sn.size(), &d_sn, &tb))) return rc;
-    HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, nullptr));
-    HIPCHK(hipStreamSynchronize(nullptr));
+    // the slot tables are stream-ordered temporaries: freeing them does not
+    // synchronise the device (hipFree would wait for every stream's work)
+    void* d_tab = nullptr;
+    const size_t nb = sb.size() * 8, nn = sn.size() * 4;
+    if (hipMallocAsync(&d_tab, nb + nn + 16, kBuildStream) != hipSuccess) return fail(FG_EOOM, "hipMallocAsync failed");
+    uint64_t* d_sb = static_cast<uint64_t*>(d_tab);
+    uint32_t* d_sn = reinterpret_cast<uint32_t*>(static_cast<char*>(d_tab) + nb);
+    HIPCHK(hipMemcpyAsync(d_sb, sb.data(), nb, hipMemcpyHostToDevice, kBuildStream));
+    HIPCHK(hipMemcpyAsync(d_sn, sn.data(), nn, hipMemcpyHostToDevice, kBuildStream));
+    HIPCHK(fg::launch_rank(d_doc, d_sb, d_sn, (uint32_t)rank_terms.size(), rank_words, d_rank, kBuildStream));
+    HIPCHK(hipFreeAsync(d_tab, kBuildStream));
+    HIPCHK(hipStreamSynchronize(kBuildStream));
   }
   ix->n_rank = (uint32_t)rank_terms.size();
   if ((rc = dev_upload(sm, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
@@ -1135,7 +1195,11 @@ int fg_index_build_global(fg_ctx* ctx, int dev, const fg_index_input* in, const 
   return finish_index(dev, hp, true, out, g);
 }
 
-int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out) {
+}  // extern "C"
+
+// one snapshot rescored (fg_index_rescore); wts: shared precomputed weights or nullptr
+static int rescore_one(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out,
+                       const std::pair<std::vector<float>, std::vector<float>>* wts) {
   if (!base || !g || !out || !g->df_text) return fail(FG_EINVAL, "bad arguments");
   const uint32_t N = base->n_docs, V = base->n_terms, VF = base->n_fterms;
   if (g->n_docs < N || g->n_docs >= 0x7FFFFFFFull) return fail(FG_EINVAL, "bad global statistics");
@@ -1207,9 +1271,51 @@ int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8
       if (!deleted[d]) alive[d >> 5] |= 1u << (d & 31);
   }
   if ((rc = score_index(ix.get(), g->n_docs, g->tot_tokens, g->df_text, g->df_name, alive, g->tot_facet_tokens,
-                        VF ? g->df_facet : nullptr)))
+                        VF ? g->df_facet : nullptr, wts)))
     return rc;
   *out = ix.release();
+  return FG_OK;
+}
+
+extern "C" {
+
+int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out) {
+  return rescore_one(base, g, deleted, out, nullptr);
+}
+
+int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_global_stats* g,
+                          const uint8_t* const* deleted, fg_index** outs) {
+  if ((n && (!bases || !outs)) || !g || !g->df_text) return fail(FG_EINVAL, "bad arguments");
+  uint32_t V = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!bases[i]) return fail(FG_EINVAL, "NULL snapshot %u", i);
+    V = std::max(V, bases[i]->n_terms);
+    outs[i] = nullptr;
+  }
+  if (n == 0) return FG_OK;
+  // the weights once for every snapshot (they depend on the statistics only)
+  std::pair<std::vector<float>, std::vector<float>> wts;
+  bm25_weights(g->n_docs, g->df_text, g->df_name, V, wts.first, wts.second);
+  std::vector<int> rc(n, FG_OK);
+  std::vector<std::string> err(n);
+  std::atomic<uint32_t> next{0};
+  auto worker = [&] {
+    for (uint32_t i; (i = next.fetch_add(1)) < n;)
+      if ((rc[i] = rescore_one(bases[i], g, deleted ? deleted[i] : nullptr, &outs[i], &wts))) err[i] = fg_last_error();
+  };
+  std::vector<std::thread> th;
+  for (uint32_t t = 1; t < std::min<uint32_t>(n, 8); ++t) th.emplace_back(worker);
+  worker();
+  for (auto& x : th) x.join();
+  for (uint32_t i = 0; i < n; ++i)
+    if (rc[i]) {
+      for (uint32_t j2 = 0; j2 < n; ++j2)
+        if (outs[j2]) {
+          fg_index_release(outs[j2]);
+          outs[j2] = nullptr;
+        }
+      return fail(rc[i], "snapshot %u: %s", i, err[i].c_str());
+    }
   return FG_OK;
 }
 

@@ -690,7 +690,11 @@ struct Namespace {
   std::mutex writer;                                   // IndexWriter lock (src/db/core.rs:211)
   std::mutex committer;                                // serialises commits and merge swaps (snapshot order)
   std::mutex merging;                                  // one merge of this namespace at a time
-  std::vector<Doc> docs;                               // global doc id = insertion order
+  // global doc id = insertion order; a deque: appending never moves the ~250 B
+  // Doc records (a vector's reallocation moved all 10M of them inside a commit)
+  std::deque<Doc> docs;
+  std::vector<uint8_t> del;                            // del[d] == docs[d].deleted (commits copy this, not the docs)
+  bool any_name = false;                               // some doc has a name field
   std::unordered_map<std::string, uint32_t> dict;      // term dictionary (text and name tokens)
   std::unordered_map<std::string, uint32_t> fdict;     // facet dictionary (encoded facet terms)
   std::unordered_map<std::string, std::vector<uint32_t>> by_id_token;
@@ -1175,18 +1179,38 @@ int upsert_record(fg_db* db, const char* nsname, const fg_object_record* r, cons
   // uppercase or punctuation never match and are not replaced
   auto it = ns->by_id_token.find(sid);
   if (it != ns->by_id_token.end())
-    for (uint32_t d : it->second) ns->docs[d].deleted = true;
+    for (uint32_t d : it->second) {
+      ns->docs[d].deleted = true;
+      ns->del[d] = 1;
+    }
   doc.text_tok = intern(*ns, doc.text);
   if (doc.has_name) doc.name_tok = intern(*ns, doc.name);
   doc.facet_tok = intern_facet(*ns, doc.facets);
   analyze(doc.id, doc.id_tokens);
   const uint32_t d = (uint32_t)ns->docs.size();
   for (auto& t : doc.id_tokens) ns->by_id_token[t].push_back(d);
+  ns->any_name |= !doc.name_tok.empty();
+  ns->del.push_back(0);
   ns->docs.push_back(std::move(doc));
   return FG_OK;
 }
 
 // ---------------------------------------------------------------- commits and merges
+// FUGU_COMMIT_TRACE=1: per-phase wall time of upserts, commits and merges on stderr
+struct PhaseTrace {
+  const char* what;
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseTrace(const char* w)
+      : what(w), on(getenv("FUGU_COMMIT_TRACE") != nullptr), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* phase) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[fg %s] %-28s %9.2f ms\n", what, phase, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+
 // FIELD_NORMS_TABLE (fieldnorm/code.rs): 0..40 exactly, then groups of 8 with a
 // doubling step; a length is stored as the largest entry <= it.
 uint64_t quantized_len(uint64_t n) {
@@ -1308,20 +1332,42 @@ struct DocsBuf {
   }
 };
 
+// Runs f(0..n-1) on up to `width` threads (this one included).
+template <class F>
+void run_threads(size_t n, size_t width, F&& f) {
+  std::atomic<size_t> next{0};
+  auto worker = [&] {
+    for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < std::min(n, width); ++t) th.emplace_back(worker);
+  worker();
+  for (auto& x : th) x.join();
+}
+
 // every segment of `segs` rescored with g and the current deleted flags
-// (`del`, global); appended to out.  Returns an error code (out then owns the
-// ones made so far).
+// (`del`, global); appended to out in order.  One fg_index_rescore_many: the
+// weights once, the segments side by side on their own threads and streams.
+// Returns an error code (out then owns nothing new).
 int rescore_into(const std::vector<Segment>& segs, const fg_global_stats& g, const std::vector<uint8_t>& del,
                  std::vector<Segment>& out) {
-  std::vector<uint8_t> sdel;
-  for (const Segment& s0 : segs) {
-    sdel.assign(s0.n, 0);
+  const size_t n = segs.size();
+  std::vector<std::vector<uint8_t>> sdel(n);
+  std::vector<const uint8_t*> dp(n, nullptr);
+  std::vector<const fg_index*> bases(n);
+  run_threads(n, 8, [&](size_t i) {
+    const Segment& s0 = segs[i];
+    bases[i] = s0.ix;
+    sdel[i].assign(s0.n, 0);
     bool sany = false;
-    for (uint32_t d = 0; d < s0.n; ++d) sany |= (sdel[d] = del[s0.global(d)]) != 0;
-    fg_index* re = nullptr;
-    if (int rc = fg_index_rescore(s0.ix, &g, sany ? sdel.data() : nullptr, &re)) return hfail(rc, fg_last_error());
-    Segment x = s0;
-    x.ix = re;
+    for (uint32_t d = 0; d < s0.n; ++d) sany |= (sdel[i][d] = del[s0.global(d)]) != 0;
+    dp[i] = sany ? sdel[i].data() : nullptr;
+  });
+  std::vector<fg_index*> re(n, nullptr);
+  if (int rc = fg_index_rescore_many(bases.data(), (uint32_t)n, &g, dp.data(), re.data())) return hfail(rc, fg_last_error());
+  for (size_t i = 0; i < n; ++i) {
+    Segment x = segs[i];
+    x.ix = re[i];
     out.push_back(std::move(x));
   }
   return FG_OK;
@@ -1332,6 +1378,7 @@ int rescore_into(const std::vector<Segment>& segs, const fg_global_stats& g, con
 // statistics.  The statistics and the snapshot change together, only when
 // every step succeeded.
 int commit_segment(fg_db* db, Namespace& ns) {
+  PhaseTrace tr("commit");
   std::lock_guard<std::mutex> c(ns.committer);
   std::shared_ptr<Snapshot> cur;
   {
@@ -1363,23 +1410,37 @@ int commit_segment(fg_db* db, Namespace& ns) {
   st->df_t = sparse_of(dt);
   st->df_n = sparse_of(dn);
   st->df_f = sparse_of(dfc);
-  bool any_name = buf.any_name;
-  for (uint32_t d = 0; d < old && !any_name; ++d) any_name |= !ns.docs[d].name_tok.empty();
-  std::vector<uint8_t> del(N, 0);
-  for (uint32_t d = 0; d < N; ++d) del[d] = ns.docs[d].deleted ? 1 : 0;
+  const bool any_name = ns.any_name;
+  const std::vector<uint8_t> del(ns.del.begin(), ns.del.begin() + N);
   Stats S;
   S.load(ns, n_terms, n_fterms);
   S.add(*st, false);
   w.unlock();
+  tr.mark("gather (writer lock)");
   const fg_global_stats g = S.global();
   const fg_docs_input in = buf.input(n_terms, n_fterms, any_name);
   auto snap = std::make_shared<Snapshot>();
-  if (cur)
-    if (int rc = rescore_into(cur->segs, g, del, snap->segs)) return rc;  // snap releases the rescored ones
-  if (const char* f = getenv("FUGU_FAULT_INJECT"))  // tests only: a commit whose device build fails
-    if (std::strcmp(f, "commit_build") == 0) return hfail(FG_EHIP, "injected fault: segment build");
+  // the new segment builds while the older ones rescore (their own threads and streams)
   fg_index* ix = nullptr;
-  if (int rc = fg_index_build_from_docs_global(db->ctx, db->dev, &in, &g, &ix)) return hfail(rc, fg_last_error());
+  int brc = FG_OK;
+  std::string berr;
+  std::thread builder([&] {
+    if (const char* f = getenv("FUGU_FAULT_INJECT"))  // tests only: a commit whose device build fails
+      if (std::strcmp(f, "commit_build") == 0) {
+        brc = FG_EHIP;
+        berr = "injected fault: segment build";
+        return;
+      }
+    if ((brc = fg_index_build_from_docs_global(db->ctx, db->dev, &in, &g, &ix))) berr = fg_last_error();
+  });
+  const int rrc = cur ? rescore_into(cur->segs, g, del, snap->segs) : FG_OK;  // snap releases the rescored ones
+  const std::string rerr = rrc ? fg_last_error() : std::string();
+  builder.join();
+  tr.mark("rescore older + build new");
+  if (rrc || brc) {
+    if (ix) fg_index_release(ix);
+    return rrc ? hfail(rrc, rerr) : hfail(brc, berr);
+  }
   {
     std::lock_guard<std::mutex> w2(ns.writer);  // the statistics are read under the writer lock
     snap->segs.push_back(Segment{ix, old, N - old, nullptr, ns.next_seg++, st});
@@ -1388,6 +1449,7 @@ int commit_segment(fg_db* db, Namespace& ns) {
     ns.committed_docs = N;
     S.store(ns);
   }
+  tr.mark("swap");
   return FG_OK;
 }
 
@@ -1427,6 +1489,7 @@ std::pair<size_t, size_t> pick_merge(const std::vector<uint64_t>& n) {
 // commits did meanwhile (new statistics, new deletions) and rescores.
 int merge_once(fg_db* db, Namespace& ns, bool* did) {
   *did = false;
+  PhaseTrace tr("merge");
   std::lock_guard<std::mutex> mg(ns.merging);
   const auto t0 = std::chrono::steady_clock::now();
   std::shared_ptr<Snapshot> cur;
@@ -1455,7 +1518,7 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     std::vector<uint32_t> dt(n_terms, 0), dn(n_terms, 0), dfc(n_fterms, 0), scratch;
     for (const Segment& sg : src) {
       bool has_del = false;
-      for (uint32_t d = 0; d < sg.n && !has_del; ++d) has_del = ns.docs[sg.global(d)].deleted;
+      for (uint32_t d = 0; d < sg.n && !has_del; ++d) has_del = ns.del[sg.global(d)] != 0;
       if (!has_del) {
         mst->tot[0] += sg.st->tot[0];
         mst->tot[1] += sg.st->tot[1];
@@ -1481,13 +1544,13 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     mst->df_t = sparse_of(dt);
     mst->df_n = sparse_of(dn);
     mst->df_f = sparse_of(dfc);
-    for (auto& d : ns.docs)
-      if (!d.name_tok.empty()) { any_name = true; break; }
+    any_name = ns.any_name;
     S.load(ns, n_terms, n_fterms);
     for (const Segment& sg : src) S.add(*sg.st, true);
     S.add(*mst, false);
     ver0 = ns.st_ver;
   }
+  tr.mark("gather (writer lock)");
   fg_index* mix = nullptr;
   if (!ids.empty()) {
     const fg_global_stats g = S.global();
@@ -1496,8 +1559,10 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
   }
   if (const char* e = getenv("FUGU_MERGE_DELAY_MS"))  // tests only: searches run while the merge is in flight
     std::this_thread::sleep_for(std::chrono::milliseconds(atoi(e)));
+  tr.mark("build merged segment");
   // ---- swap: no commit runs meanwhile
   std::lock_guard<std::mutex> c(ns.committer);
+  tr.mark("wait for the committer");
   std::shared_ptr<Snapshot> now;
   {
     std::shared_lock<std::shared_mutex> l(ns.snap_mu);
@@ -1527,9 +1592,8 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
       for (const Segment& sg : src) S.add(*sg.st, true);
       S.add(*mst, false);
     }
-    for (size_t i = 0; i < ids.size(); ++i) new_del |= (mdel[i] = ns.docs[ids[i]].deleted ? 1 : 0) != 0;
-    del.resize(ns.docs.size());
-    for (size_t d = 0; d < ns.docs.size(); ++d) del[d] = ns.docs[d].deleted ? 1 : 0;
+    for (size_t i = 0; i < ids.size(); ++i) new_del |= (mdel[i] = ns.del[ids[i]]) != 0;
+    del = ns.del;
   }
   const fg_global_stats g = S.global();
   if (mix && (moved || new_del || stats_change)) {
@@ -1568,6 +1632,7 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     ns.snap = snap;
     if (stats_change || moved) S.store(ns);
   }
+  tr.mark("rescore + swap");
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   {
     std::lock_guard<std::mutex> l(ns.mq);
@@ -1757,6 +1822,7 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
                     : tx.size() > 10000 ? "Text too long (max 10000 characters)" : nullptr;
     if (e) return hfail(FG_EINVAL, "Validation failed for object at index " + std::to_string(i) + ": " + e);
   }
+  PhaseTrace tr("upsert");
   const int T = std::max(1, std::min<int>(fg_host_threads(), (int)(n / 4096) + 1));
   std::vector<LocalDict> ldict(T);
   std::vector<Doc> docs(n);
@@ -1778,6 +1844,7 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
       });
     for (auto& x : th) x.join();
   }
+  tr.mark("analyze");
   {  // the writer lock: the dictionary merge and the ordered upserts
     std::lock_guard<std::mutex> w(ns->writer);
     std::vector<std::vector<uint32_t>> remap(T);
@@ -1799,18 +1866,24 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
         });
       for (auto& x : th) x.join();
     }
-    ns->docs.reserve(ns->docs.size() + n);
-    ns->by_id_token.reserve(ns->by_id_token.size() + n);
+    // a bulk load sizes the id map once; a small batch lets it grow geometrically
+    // (reserving size + n on every call rehashed all 10M entries per commit)
+    if (n > ns->by_id_token.size()) ns->by_id_token.reserve(ns->by_id_token.size() + n);
     for (uint32_t i = 0; i < n; ++i) {
       // delete_term(id_field, raw id) (src/db/document.rs:38-42), then add_document
       auto it = ns->by_id_token.find(docs[i].id);
       if (it != ns->by_id_token.end())
-        for (uint32_t d : it->second) ns->docs[d].deleted = true;
+        for (uint32_t d : it->second) {
+      ns->docs[d].deleted = true;
+      ns->del[d] = 1;
+    }
       const uint32_t d = (uint32_t)ns->docs.size();
       for (auto& t : docs[i].id_tokens) ns->by_id_token[t].push_back(d);
+      ns->del.push_back(0);
       ns->docs.push_back(std::move(docs[i]));
     }
   }
+  tr.mark("dictionary + upserts");
   return fg_db_commit(db, nsname);  // NamedIndex::upsert commits once per call (src/db/document.rs:65)
 }
 
@@ -1839,7 +1912,7 @@ int fg_db_doc_count(fg_db* db, const char* nsname, uint64_t* total, uint64_t* al
   std::lock_guard<std::mutex> w(ns->writer);
   *total = ns->docs.size();
   *alive = 0;
-  for (auto& d : ns->docs) *alive += d.deleted ? 0 : 1;
+  for (uint8_t x : ns->del) *alive += x ? 0 : 1;
   return FG_OK;
 }
 

@@ -51,7 +51,8 @@ EXPORTS = (
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
-    "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore", "fg_index_build_global",
+    "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore",
+    "fg_index_rescore_many", "fg_index_build_global",
     "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged", "fg_index_term_kth",
     "fg_model_batch", "fg_abi_version",
 )
@@ -137,6 +138,8 @@ _sig("fg_docs_facet_stats", C.c_int, C.POINTER(DocsInput), _u32p, _u64p)
 _sig("fg_index_build_from_docs_global", C.c_int, _p, C.c_int, C.POINTER(DocsInput), C.POINTER(GlobalStats),
      C.POINTER(_p))
 _sig("fg_index_rescore", C.c_int, _p, C.POINTER(GlobalStats), _u8p, C.POINTER(_p))
+_sig("fg_index_rescore_many", C.c_int, C.POINTER(_p), C.c_uint32, C.POINTER(GlobalStats), C.POINTER(_u8p),
+     C.POINTER(_p))
 _sig("fg_index_retain", C.c_int, _p)
 _sig("fg_index_release", C.c_int, _p)
 _sig("fg_index_stats_get", C.c_int, _p, C.POINTER(IndexStats))
@@ -208,6 +211,25 @@ class Context:
         _check(_lib.fg_ctx_create(len(devices), devs, C.byref(h)))
         self._h = h
         self.devices = tuple(devices)
+
+    @staticmethod
+    def rescore_many(indexes, global_stats: "ShardStats", deleted=None) -> list:
+        """fg_index_rescore_many: several snapshots scored with one set of
+        statistics side by side (the weights once); deleted: None or a list of
+        per-snapshot flag arrays (entries may be None)."""
+        g = global_stats
+        dft, dfn = _u32(g.df_text), _u32(g.df_name)
+        dff = None if g.df_facet is None else _u32(g.df_facet)
+        gs = GlobalStats(int(g.n_docs), (C.c_uint64 * 2)(*[int(x) for x in g.tot_tokens]), _ptr(dft, _u32p),
+                         _ptr(dfn, _u32p), _ptr(dff, _u32p), int(g.tot_facet_tokens))
+        n = len(indexes)
+        bases = (_p * n)(*[ix._h for ix in indexes])
+        dls = [None if deleted is None or deleted[i] is None else np.ascontiguousarray(deleted[i], np.uint8)
+               for i in range(n)]
+        dp = (_u8p * n)(*[_ptr(d, _u8p) for d in dls])
+        outs = (_p * n)()
+        _check(_lib.fg_index_rescore_many(bases, n, C.byref(gs), dp, outs))
+        return [Index(outs[i]) for i in range(n)]
 
     @property
     def handle(self):

@@ -169,6 +169,13 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
  * the alive bitset are recomputed on the device.  `deleted` [n_docs of base]
  * or NULL (none).  g must cover base's own doc frequencies. */
 int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out);
+/* n snapshots rescored with ONE set of statistics (a commit's older segments):
+ * the BM25 weights computed once, every snapshot's device work on its own
+ * host thread and stream, side by side.  deleted[i] as fg_index_rescore's
+ * (deleted itself may be NULL: none anywhere).  On error no snapshot is made
+ * (outs[] all NULL). */
+int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_global_stats* g,
+                          const uint8_t* const* deleted, fg_index** outs);
 
 int fg_index_retain(fg_index* ix);
 int fg_index_release(fg_index* ix);

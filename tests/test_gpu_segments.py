@@ -107,3 +107,22 @@ def test_rescore_twice_and_segment_merge_equals_single_index(native, ctx, parts)
             gdoc = md[i, :m] + np.array([0, cut], np.uint32)[msh[i, :m]]
             assert np.array_equal(gdoc, d1[i, :m]), (mode, i)
             assert np.array_equal(ms[i, :m], s1[i, :m]), (mode, i)
+
+
+def test_rescore_many_equals_one_by_one(native, ctx, parts):
+    """fg_index_rescore_many (a commit's older segments rescored side by side,
+    the weights once) gives every snapshot exactly what fg_index_rescore gives it,
+    with and without deletes."""
+    from fugu_amd import synth
+    c, cut, (ao, at), (bo, bt) = parts
+    V = synth.VOCAB
+    g = native.docs_stats(ao, at, V, threads=16) + native.docs_stats(bo, bt, V, threads=16)
+    seg_a = native.Index.from_docs(ctx, ao, at, V, threads=16)
+    seg_b = native.Index.from_docs(ctx, bo, bt, V, threads=16)
+    da = (np.arange(cut) % 5 == 1).astype(np.uint8)
+    many = native.Index.rescore_many([seg_a, seg_b], g, deleted=[da, None])
+    one = [seg_a.rescore(g, deleted=da), seg_b.rescore(g)]
+    for (m0, m1, k, mode) in [(3, 3, 100, native.MODE_AND), (2, 5, 1000, native.MODE_OR)]:
+        q_off, terms = synth.queries(256, m0, m1, seed_q=123)
+        for x, y in zip(many, one):
+            same(x.search_batch(q_off, terms, k, mode=mode), y.search_batch(q_off, terms, k, mode=mode), (m0, k, mode))
