@@ -66,6 +66,71 @@ struct DevAllocs {
   }
 };
 
+// The scoring tables of the snapshots of ONE structure (a segment and its
+// rescores) come in one block of one size; a released snapshot's block is kept
+// for the structure's next rescore instead of freed (a commit rescores every
+// older segment: fresh hipMallocs of those blocks from several threads
+// serialised in the runtime, 10s of ms per commit).  The release waits for the
+// device to drain, as hipFree would, so no kernel still reads a block handed out
+// again.
+struct ScorePool {
+  static constexpr size_t kKeep = 2;  // blocks cached per structure
+  std::mutex mu;
+  std::vector<std::pair<size_t, void*>> free_blocks;
+  int dev = 0;
+  void* get(size_t bytes) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      for (size_t i = 0; i < free_blocks.size(); ++i)
+        if (free_blocks[i].first == bytes) {
+          void* p = free_blocks[i].second;
+          free_blocks.erase(free_blocks.begin() + i);
+          return p;
+        }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      release_all();
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+    }
+    return p;
+  }
+  void put(void* p, size_t bytes) {
+    (void)hipSetDevice(dev);
+    (void)hipDeviceSynchronize();
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (free_blocks.size() < kKeep) {
+        free_blocks.emplace_back(bytes, p);
+        return;
+      }
+    }
+    (void)hipFree(p);
+  }
+  void release_all() {
+    std::lock_guard<std::mutex> l(mu);
+    for (auto& b : free_blocks) (void)hipFree(b.second);
+    free_blocks.clear();
+  }
+  ~ScorePool() {
+    if (free_blocks.empty()) return;
+    (void)hipSetDevice(dev);
+    for (auto& b : free_blocks) (void)hipFree(b.second);
+  }
+};
+struct ScoreBlock {
+  void* p = nullptr;
+  size_t bytes = 0;
+  std::shared_ptr<ScorePool> pool;
+  ~ScoreBlock() {
+    if (p && pool) pool->put(p, bytes);
+  }
+};
+
 
 }  // namespace fgh
 
@@ -222,17 +287,22 @@ struct fg_index {
   std::vector<uint64_t> foff;
   std::vector<uint32_t> df_facet, df_facet_local, ffirst, flast;
   std::vector<float> fscore;    // a facet clause's score in a doc holding the term (tf 1, fieldnorm id 1)
-  // device: structure arrays (smem, shared) and the scoring tables (mem)
+  // device: structure arrays (smem, shared), the scoring tables (sblock, from the
+  // structure's spool) and other snapshot-own arrays (mem)
   std::shared_ptr<DevAllocs> smem;
+  std::shared_ptr<fgh::ScorePool> spool;
   uint64_t struct_bytes = 0;
   const uint32_t* d_tfp = nullptr;
   const uint8_t* d_fn_text = nullptr;
   const uint8_t* d_fn_name = nullptr;
   const uint32_t *d_sc_term = nullptr, *d_sc_first = nullptr, *d_bk_term = nullptr, *d_bk_first = nullptr,
                  *d_kt_terms = nullptr;
-  uint32_t n_sc = 0, n_bk = 0, n_kt = 0;
+  // k_ktop's tables (structure): long terms, their first chunk, each chunk's term and first posting
+  const uint32_t *d_kb_terms = nullptr, *d_kb_chunk0 = nullptr, *d_kc_big = nullptr, *d_kc_start = nullptr;
+  uint32_t n_sc = 0, n_bk = 0, n_kt = 0, n_kbig = 0, n_kchunks = 0;
   fg::DevIndex d{};
   DevAllocs mem;
+  fgh::ScoreBlock sblock;
   WsPool pool;  // plan workspaces (destroyed before mem: declared after it)
   PinnedPool pinned;  // host staging of plan uploads and result copies
 };

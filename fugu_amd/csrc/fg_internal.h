@@ -337,7 +337,8 @@ struct ScoreJob {
   const uint32_t* kc_start;   // [n_chunks] first posting of each chunk within its term's list
   uint64_t* kc_keys;          // [n_chunks * kTopKs[last]] each chunk's best keys
   uint32_t* kc_cnt;           // [n_chunks]
-  uint32_t* kb_stat;          // [n_big * 3] alive postings, min / max alive score bits (0, ~0, 0 first)
+  uint32_t* kb_stat;          // [3][n_big] alive postings, min / max alive score bits (0, ~0, 0 first)
+  uint32_t n_big;
 };
 #ifndef FG_KTOP_CHUNK
 #define FG_KTOP_CHUNK 32768

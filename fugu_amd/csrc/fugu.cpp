@@ -329,31 +329,47 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   HIPCHK(hipSetDevice(ix->dev));
   uint64_t bytes = 0;
   int rc;
-  float *d_wt, *d_wn, *d_cache, *d_psc, *d_bmax, *d_ktop;
+  // every scoring table in ONE block of the structure's pool (a rescore of the
+  // same structure gets a released snapshot's block back: ScorePool)
+  struct Part { size_t bytes; void** out; };
+  float *d_wt, *d_wn, *d_cache, *d_psc, *d_bmax, *d_ktop, *d_cmax;
   uint32_t *d_alive = nullptr, *d_tmaxs, *d_tmax;
-  if ((rc = dev_upload(ix->mem, ix->w_text.data(), V, &d_wt, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, ix->w_name.data(), V, &d_wn, &bytes))) return rc;
-  if ((rc = dev_upload(ix->mem, ix->cache, 512, &d_cache, &bytes))) return rc;
-  if (!alive.empty() && (rc = dev_upload(ix->mem, alive.data(), alive.size(), &d_alive, &bytes))) return rc;
-  auto dev_alloc = [&](size_t n_bytes, void** p) -> int {
-    if (hipMalloc(p, std::max<size_t>(n_bytes, 16)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", n_bytes);
-    ix->mem.ptrs.push_back(*p);
-    bytes += std::max<size_t>(n_bytes, 16);
-    return FG_OK;
+  const Part parts[] = {
+      {4ull * V, reinterpret_cast<void**>(&d_wt)},
+      {4ull * V, reinterpret_cast<void**>(&d_wn)},
+      {4ull * 512, reinterpret_cast<void**>(&d_cache)},
+      {alive.empty() ? 0 : 4ull * alive.size(), reinterpret_cast<void**>(&d_alive)},
+      {4ull * ix->n_postings + 16, reinterpret_cast<void**>(&d_psc)},  // 16 B of slack after the scores
+      {4ull * ix->dir_entries, reinterpret_cast<void**>(&d_bmax)},
+      {4ull * V, reinterpret_cast<void**>(&d_tmaxs)},
+      {4ull * ix->tile_entries, reinterpret_cast<void**>(&d_tmax)},
+      {4ull * V * fg::kNumTopK, reinterpret_cast<void**>(&d_ktop)},
+      {4ull * ix->n_sc, reinterpret_cast<void**>(&d_cmax)},
   };
-  void* p;
-  if ((rc = dev_alloc(4ull * ix->n_postings + 16, &p))) return rc;  // 16 B of slack: k_conj's 16-B lead loads
-  d_psc = static_cast<float*>(p);
-  if ((rc = dev_alloc(4ull * ix->dir_entries, &p))) return rc;
-  d_bmax = static_cast<float*>(p);
-  if ((rc = dev_alloc(4ull * V, &p))) return rc;
-  d_tmaxs = static_cast<uint32_t*>(p);
-  if ((rc = dev_alloc(4ull * ix->tile_entries, &p))) return rc;
-  d_tmax = static_cast<uint32_t*>(p);
-  if ((rc = dev_alloc(4ull * V * fg::kNumTopK, &p))) return rc;
-  d_ktop = static_cast<float*>(p);
-  if ((rc = dev_alloc(4ull * ix->n_sc, &p))) return rc;
-  float* d_cmax = static_cast<float*>(p);
+  size_t total = 0;
+  for (const Part& pt : parts) total += (std::max<size_t>(pt.bytes, 16) + 255) & ~size_t(255);
+  if (!ix->spool) {
+    ix->spool = std::make_shared<fgh::ScorePool>();
+    ix->spool->dev = ix->dev;
+  }
+  char* blk = static_cast<char*>(ix->spool->get(total));
+  if (!blk) return fail(FG_EOOM, "scoring tables: hipMalloc(%zu) failed", total);
+  ix->sblock.p = blk;
+  ix->sblock.bytes = total;
+  ix->sblock.pool = ix->spool;
+  bytes += total;
+  {
+    size_t o = 0;
+    for (const Part& pt : parts) {
+      *pt.out = pt.bytes ? blk + o : nullptr;
+      o += (std::max<size_t>(pt.bytes, 16) + 255) & ~size_t(255);
+    }
+  }
+  HIPCHK(hipMemcpyAsync(d_wt, ix->w_text.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
+  HIPCHK(hipMemcpyAsync(d_wn, ix->w_name.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
+  HIPCHK(hipMemcpyAsync(d_cache, ix->cache, 4ull * 512, hipMemcpyHostToDevice, kBuildStream));
+  if (d_alive) HIPCHK(hipMemcpyAsync(d_alive, alive.data(), 4ull * alive.size(), hipMemcpyHostToDevice, kBuildStream));
+  g_bt.mark("scoring uploads + allocs");
   HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, kBuildStream));
   HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), kBuildStream));
   HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, kBuildStream));
@@ -385,60 +401,37 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
   // k_ktop: terms of <= kKtopChunk postings one workgroup each; longer terms in
   // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
-  // chunks' best keys (k_ktop_big).  The chunk tables and key scratch are
-  // temporary: stream-ordered allocations on the build stream, so freeing them
-  // does not synchronize the device (searches on other streams keep running).
-  std::vector<uint32_t> kt_small, kb_terms, kb_chunk0, kc_big, kc_start;
-  for (uint32_t t = 0; t < V; ++t) {
-    const uint64_t df = ix->off[t + 1] - ix->off[t];
-    if (df == 0) continue;
-    if (df <= fg::kKtopChunk) {
-      kt_small.push_back(t);
-      continue;
-    }
-    kb_chunk0.push_back((uint32_t)kc_big.size());
-    for (uint64_t st = 0; st < df; st += fg::kKtopChunk) {
-      kc_big.push_back((uint32_t)kb_terms.size());
-      kc_start.push_back((uint32_t)st);
-    }
-    kb_terms.push_back(t);
-  }
-  kb_chunk0.push_back((uint32_t)kc_big.size());
-  const size_t n_small = kt_small.size(), n_big = kb_terms.size(), n_chunks = kc_big.size();
-  std::vector<void*> ktmp;
+  // chunks' best keys (k_ktop_big).  The chunk tables are the structure's; the
+  // key scratch is one stream-ordered temporary (freeing it does not
+  // synchronize the device: searches on other streams keep running).
+  const size_t n_small = ix->n_kt, n_big = ix->n_kbig, n_chunks = ix->n_kchunks;
+  const size_t kck_b = (8ull * n_chunks * fg::kTopKs[fg::kNumTopK - 1] + 255) & ~size_t(255);
+  const size_t kcc_b = (4ull * n_chunks + 255) & ~size_t(255), kbs_b = 4ull * 3 * n_big;
+  void* ktmp = nullptr;
+  if (hipMallocAsync(&ktmp, kck_b + kcc_b + kbs_b + 16, kBuildStream) != hipSuccess)
+    return fail(FG_EOOM, "hipMallocAsync(%zu) failed", kck_b + kcc_b + kbs_b);
   struct KtmpBack {
-    std::vector<void*>& v;
-    ~KtmpBack() {
-      for (void* x : v) (void)hipFreeAsync(x, kBuildStream);
-    }
+    void* p;
+    ~KtmpBack() { (void)hipFreeAsync(p, kBuildStream); }
   } ktmp_back{ktmp};
-  auto tmp_upload = [&](const void* src, size_t n_bytes, void** out) -> int {
-    void* q = nullptr;
-    if (hipMallocAsync(&q, std::max<size_t>(n_bytes, 16), kBuildStream) != hipSuccess)
-      return fail(FG_EOOM, "hipMallocAsync(%zu) failed", n_bytes);
-    ktmp.push_back(q);
-    if (src && n_bytes) HIPCHK(hipMemcpyAsync(q, src, n_bytes, hipMemcpyHostToDevice, kBuildStream));
-    *out = q;
-    return FG_OK;
-  };
-  void *d_ks, *d_kbt, *d_kb0, *d_kcb, *d_kcs, *d_kck, *d_kcc, *d_kbs;
-  std::vector<uint32_t> kb_stat(3 * n_big, 0);
-  for (size_t x = 0; x < n_big; ++x) kb_stat[3 * x + 1] = 0xFFFFFFFFu;
-  if ((rc = tmp_upload(kt_small.data(), 4 * n_small, &d_ks)) || (rc = tmp_upload(kb_terms.data(), 4 * n_big, &d_kbt)) ||
-      (rc = tmp_upload(kb_chunk0.data(), 4 * (n_big + 1), &d_kb0)) ||
-      (rc = tmp_upload(kc_big.data(), 4 * n_chunks, &d_kcb)) || (rc = tmp_upload(kc_start.data(), 4 * n_chunks, &d_kcs)) ||
-      (rc = tmp_upload(nullptr, 8ull * n_chunks * fg::kTopKs[fg::kNumTopK - 1], &d_kck)) ||
-      (rc = tmp_upload(nullptr, 4 * n_chunks, &d_kcc)) || (rc = tmp_upload(kb_stat.data(), 4 * kb_stat.size(), &d_kbs)))
-    return rc;
-  j.kt_terms = static_cast<const uint32_t*>(d_ks);
-  j.kb_terms = static_cast<const uint32_t*>(d_kbt);
-  j.kb_chunk0 = static_cast<const uint32_t*>(d_kb0);
-  j.kc_big = static_cast<const uint32_t*>(d_kcb);
-  j.kc_start = static_cast<const uint32_t*>(d_kcs);
-  j.kc_keys = static_cast<uint64_t*>(d_kck);
-  j.kc_cnt = static_cast<uint32_t*>(d_kcc);
-  j.kb_stat = static_cast<uint32_t*>(d_kbs);
+  char* kb = static_cast<char*>(ktmp);
+  uint32_t* d_kbs = reinterpret_cast<uint32_t*>(kb + kck_b + kcc_b);
+  // per long term: alive postings 0, min alive score bits ~0, max 0 ([3][n_big])
+  if (n_big) {
+    HIPCHK(hipMemsetAsync(d_kbs, 0, 4ull * 3 * n_big, kBuildStream));
+    HIPCHK(hipMemsetD32Async(d_kbs + n_big, (int)0xFFFFFFFFu, n_big, kBuildStream));
+  }
+  j.kt_terms = ix->d_kt_terms;
+  j.kb_terms = ix->d_kb_terms;
+  j.kb_chunk0 = ix->d_kb_chunk0;
+  j.kc_big = ix->d_kc_big;
+  j.kc_start = ix->d_kc_start;
+  j.kc_keys = reinterpret_cast<uint64_t*>(kb);
+  j.kc_cnt = reinterpret_cast<uint32_t*>(kb + kck_b);
+  j.kb_stat = d_kbs;
+  j.n_big = (uint32_t)n_big;
   HIPCHK(fg::launch_ktop(j, (uint32_t)n_small, (uint32_t)n_chunks, (uint32_t)n_big, kBuildStream));
+  g_bt.mark("scoring launches");
   ix->tmaxs.resize(V);
   ix->ktop.resize((size_t)V * fg::kNumTopK);
   if (uint8_t* pin = pinned_scratch(4ull * V * (1 + fg::kNumTopK))) {
@@ -615,7 +608,11 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->tile_entries = ntm;
   // chunk tables of the scoring kernels: (term, first posting) per <= kScoreChunk
   // postings, (term, first bucket) per <= kBucketChunk buckets, terms with postings
-  std::vector<uint32_t> sc_t, sc_f, bk_t, bk_f, kt, coff(V);
+  // and of k_ktop (they depend on the postings only, so every rescore reuses
+  // them): terms of <= kKtopChunk postings one workgroup each (kt); longer terms
+  // (kb_terms) in kKtopChunk-posting chunks (kc_big / kc_start, the chunks of
+  // long term x from kb_chunk0[x])
+  std::vector<uint32_t> sc_t, sc_f, bk_t, bk_f, kt, coff(V), kb_terms, kb_chunk0, kc_big, kc_start;
   for (uint32_t t = 0; t < V; ++t) {
     const uint64_t n = hp.off[t + 1] - hp.off[t];
     coff[t] = (uint32_t)sc_t.size();  // the term's first score chunk (DevIndex::cmax)
@@ -623,8 +620,18 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     for (uint64_t f = 0; f < n; f += fg::kScoreChunk) { sc_t.push_back(t); sc_f.push_back((uint32_t)f); }
     const uint64_t nbk = ((N - 1) >> (tmeta[t] & 0xFFu)) + 1;
     for (uint64_t f = 0; f < nbk; f += fg::kBucketChunk) { bk_t.push_back(t); bk_f.push_back((uint32_t)f); }
-    kt.push_back(t);
+    if (n <= fg::kKtopChunk) {
+      kt.push_back(t);
+      continue;
+    }
+    kb_chunk0.push_back((uint32_t)kc_big.size());
+    for (uint64_t st = 0; st < n; st += fg::kKtopChunk) {
+      kc_big.push_back((uint32_t)kb_terms.size());
+      kc_start.push_back((uint32_t)st);
+    }
+    kb_terms.push_back(t);
   }
+  kb_chunk0.push_back((uint32_t)kc_big.size());
   if (sc_t.size() > 0x7FFFFFFFull || bk_t.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "index too large");
   HIPCHK(hipSetDevice(dev));
   DevAllocs& sm = *ix->smem;
@@ -633,7 +640,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc;
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
-  uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt, *d_coff;
+  uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs;
   {
     UploadBatch ub;
     ub.add(hp.doc.data(), hp.doc.size(), &d_doc);
@@ -652,6 +659,10 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ub.add(bk_t.data(), bk_t.size(), &d_bkt);
     ub.add(bk_f.data(), bk_f.size(), &d_bkf);
     ub.add(kt.data(), kt.size(), &d_kt);
+    ub.add(kb_terms.data(), kb_terms.size(), &d_kbt);
+    ub.add(kb_chunk0.data(), kb_chunk0.size(), &d_kb0);
+    ub.add(kc_big.data(), kc_big.size(), &d_kcb);
+    ub.add(kc_start.data(), kc_start.size(), &d_kcs);
     ub.add(coff.data(), coff.size(), &d_coff);
     if ((rc = ub.commit(sm, &bytes))) return rc;
   }
@@ -737,6 +748,12 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d_bk_term = d_bkt;
   ix->d_bk_first = d_bkf;
   ix->d_kt_terms = d_kt;
+  ix->d_kb_terms = d_kbt;
+  ix->d_kb_chunk0 = d_kb0;
+  ix->d_kc_big = d_kcb;
+  ix->d_kc_start = d_kcs;
+  ix->n_kbig = (uint32_t)kb_terms.size();
+  ix->n_kchunks = (uint32_t)kc_big.size();
   ix->n_sc = (uint32_t)sc_t.size();
   ix->n_bk = (uint32_t)bk_t.size();
   ix->n_kt = (uint32_t)kt.size();
@@ -1217,6 +1234,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->pool.dev = base->dev;
   // the structure: shared device arrays, copied host bookkeeping
   ix->smem = base->smem;
+  ix->spool = base->spool;  // the structure's scoring blocks (a released rescore's block comes back)
   ix->struct_bytes = base->struct_bytes;
   ix->n_docs = N;
   ix->n_terms = V;
@@ -1252,6 +1270,12 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->d_bk_term = base->d_bk_term;
   ix->d_bk_first = base->d_bk_first;
   ix->d_kt_terms = base->d_kt_terms;
+  ix->d_kb_terms = base->d_kb_terms;
+  ix->d_kb_chunk0 = base->d_kb_chunk0;
+  ix->d_kc_big = base->d_kc_big;
+  ix->d_kc_start = base->d_kc_start;
+  ix->n_kbig = base->n_kbig;
+  ix->n_kchunks = base->n_kchunks;
   ix->n_sc = base->n_sc;
   ix->n_bk = base->n_bk;
   ix->n_kt = base->n_kt;

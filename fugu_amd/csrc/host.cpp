@@ -1441,14 +1441,18 @@ int commit_segment(fg_db* db, Namespace& ns) {
     if (ix) fg_index_release(ix);
     return rrc ? hfail(rrc, rerr) : hfail(brc, berr);
   }
+  std::shared_ptr<Snapshot> prev;  // released after the locks (its blocks wait for the device to drain)
   {
     std::lock_guard<std::mutex> w2(ns.writer);  // the statistics are read under the writer lock
     snap->segs.push_back(Segment{ix, old, N - old, nullptr, ns.next_seg++, st});
     std::unique_lock<std::shared_mutex> l(ns.snap_mu);  // readers keep the old snapshot (refcount)
+    prev = std::move(ns.snap);
     ns.snap = snap;
     ns.committed_docs = N;
     S.store(ns);
   }
+  cur.reset();
+  prev.reset();
   tr.mark("swap");
   return FG_OK;
 }
@@ -1625,13 +1629,18 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     snap->segs.push_back(std::move(m));
   }
   if (int rc = keep(after)) return rc;
+  std::shared_ptr<Snapshot> prev;  // released after the locks
   {
     std::lock_guard<std::mutex> w(ns.writer);
     if (mix) snap->segs[before.size()].id = ns.next_seg++;
     std::unique_lock<std::shared_mutex> l(ns.snap_mu);
+    prev = std::move(ns.snap);
     ns.snap = snap;
     if (stats_change || moved) S.store(ns);
   }
+  now.reset();
+  cur.reset();
+  prev.reset();
   tr.mark("rescore + swap");
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   {

@@ -2052,12 +2052,29 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
   const uint32_t end = min(n, first + kScoreChunk);
   const float wt = j.w_text[t], wn = j.w_name[t];
   float mx = 0.0f;
-  for (uint32_t p0 = first; p0 < end; p0 += kThreads) {
-    const uint32_t p = p0 + threadIdx.x;
-    const bool in = p < end;
-    const uint32_t d = in ? j.doc[b + p] : 0xFFFFFFFFu;
-    const float v = in ? posting_score(j.tfp[b + p], j.fn_text[d], j.fn_name ? j.fn_name[d] : 0u, wt, wn, cache) : 0.0f;
-    if (in) j.psc[b + p] = v;
+  // the chunk's postings in one step per thread: every doc / tf load, then every
+  // fieldnorm gather, in flight together (kScoreChunk / kThreads per thread)
+  constexpr uint32_t R = kScoreChunk / kThreads;
+  uint32_t d[R], tf[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t p = first + r * kThreads + threadIdx.x;
+    d[r] = p < end ? j.doc[b + p] : 0xFFFFFFFFu;
+    tf[r] = p < end ? j.tfp[b + p] : 0u;
+  }
+  uint32_t fnt[R], fnn[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const bool in = d[r] != 0xFFFFFFFFu;
+    fnt[r] = in ? j.fn_text[d[r]] : 0u;
+    fnn[r] = in && j.fn_name ? j.fn_name[d[r]] : 0u;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t p = first + r * kThreads + threadIdx.x;
+    if (p >= end) continue;
+    const float v = posting_score(tf[r], fnt[r], fnn[r], wt, wn, cache);
+    j.psc[b + p] = v;
     mx = fmaxf(mx, v);
   }
   // the chunk's block-max (scores >= 0)
@@ -2084,17 +2101,34 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
   const float* ps = j.psc + j.off[t];
   const uint32_t to = j.toff[t];
   uint32_t tm = 0;
-  for (uint32_t bk = first + threadIdx.x; bk < end; bk += kThreads) {
-    const uint32_t lo = dir[bk], hi = dir[bk + 1];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t bk0 = first; bk0 < end; bk0 += kThreads) {  // uniform trip count: every lane shuffles
+    const uint32_t bk = bk0 + threadIdx.x;
+    const bool in = bk < end;
+    const uint32_t lo = in ? dir[bk] : 0u, hi = in ? dir[bk + 1] : 0u;
     float mx = -0.0f;
+    uint32_t bits = 0;
     if (hi > lo) {
       mx = 0.0f;
       for (uint32_t p = lo; p < hi; ++p) mx = fmaxf(mx, ps[p]);
-      const uint32_t bits = __float_as_uint(mx);
+      bits = __float_as_uint(mx);
       tm = max(tm, bits);
-      if (to != 0xFFFFFFFFu) atomicMax(&j.tmax[to + (uint32_t)(((uint64_t)bk << B) >> kDisjTileShift)], bits);
     }
-    j.bmax[j.dir_off[t] + bk] = mx;
+    if (in) j.bmax[j.dir_off[t] + bk] = mx;
+    if (to != 0xFFFFFFFFu) {
+      // tile maxima: a segmented max over the wave's buckets (their tiles ascend
+      // with the lane), then one atomic per tile the wave touches -- not one per
+      // bucket, which put up to 64 atomics on one address for a dense term
+      const uint32_t tile = (uint32_t)(((uint64_t)(in ? bk : bk0) << B) >> kDisjTileShift);
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t b2 = (uint32_t)__shfl_down((int)bits, o, 64);
+        const uint32_t t2 = (uint32_t)__shfl_down((int)tile, o, 64);
+        if (lane + o < 64 && t2 == tile) bits = max(bits, b2);
+      }
+      const uint32_t prev = (uint32_t)__shfl_up((int)tile, 1, 64);
+      if (in && bits && (lane == 0 || prev != tile)) atomicMax(&j.tmax[to + tile], bits);
+    }
   }
   // one atomic per wave for the term maximum
   for (int o = 32; o > 0; o >>= 1) tm = max(tm, (uint32_t)__shfl_xor((int)tm, o, 64));
@@ -2228,9 +2262,9 @@ __global__ __launch_bounds__(kThreads) void k_ktop_part(ScoreJob j) {
   ktop_reduce(j, b, p0, p1, sh);
   const uint32_t na = sh.red[0];
   if (threadIdx.x == 0 && na) {
-    atomicAdd(&j.kb_stat[3 * bt], na);
-    atomicMin(&j.kb_stat[3 * bt + 1], sh.red[1]);
-    atomicMax(&j.kb_stat[3 * bt + 2], sh.red[2]);
+    atomicAdd(&j.kb_stat[bt], na);
+    atomicMin(&j.kb_stat[j.n_big + bt], sh.red[1]);
+    atomicMax(&j.kb_stat[2 * j.n_big + bt], sh.red[2]);
   }
   uint64_t T = 0;
   if (na > KM) {
@@ -2254,7 +2288,7 @@ __global__ __launch_bounds__(kThreads) void k_ktop_big(ScoreJob j) {
   __shared__ KtopShared sh;
   constexpr uint32_t KM = kKtopKM;
   const uint32_t bt = blockIdx.x, t = j.kb_terms[bt];
-  const uint32_t na = j.kb_stat[3 * bt], mx = j.kb_stat[3 * bt + 2];
+  const uint32_t na = j.kb_stat[bt], mx = j.kb_stat[2 * j.n_big + bt];
   if (threadIdx.x == 0) {
     sh.n_top = 0;
     if (na) j.ktop[(size_t)t * kNumTopK] = __uint_as_float(mx);  // K = 1: the maximum

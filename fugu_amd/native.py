@@ -212,25 +212,6 @@ class Context:
         self._h = h
         self.devices = tuple(devices)
 
-    @staticmethod
-    def rescore_many(indexes, global_stats: "ShardStats", deleted=None) -> list:
-        """fg_index_rescore_many: several snapshots scored with one set of
-        statistics side by side (the weights once); deleted: None or a list of
-        per-snapshot flag arrays (entries may be None)."""
-        g = global_stats
-        dft, dfn = _u32(g.df_text), _u32(g.df_name)
-        dff = None if g.df_facet is None else _u32(g.df_facet)
-        gs = GlobalStats(int(g.n_docs), (C.c_uint64 * 2)(*[int(x) for x in g.tot_tokens]), _ptr(dft, _u32p),
-                         _ptr(dfn, _u32p), _ptr(dff, _u32p), int(g.tot_facet_tokens))
-        n = len(indexes)
-        bases = (_p * n)(*[ix._h for ix in indexes])
-        dls = [None if deleted is None or deleted[i] is None else np.ascontiguousarray(deleted[i], np.uint8)
-               for i in range(n)]
-        dp = (_u8p * n)(*[_ptr(d, _u8p) for d in dls])
-        outs = (_p * n)()
-        _check(_lib.fg_index_rescore_many(bases, n, C.byref(gs), dp, outs))
-        return [Index(outs[i]) for i in range(n)]
-
     @property
     def handle(self):
         return self._h
@@ -415,6 +396,25 @@ class Index:
             _check(_lib.fg_index_build_global(ctx.handle, dev, C.byref(inp), C.byref(gs), C.byref(h)))
             del keep
         return cls(h)
+
+    @staticmethod
+    def rescore_many(indexes, global_stats: "ShardStats", deleted=None) -> list:
+        """fg_index_rescore_many: several snapshots scored with one set of
+        statistics side by side (the weights once); deleted: None or a list of
+        per-snapshot flag arrays (entries may be None)."""
+        g = global_stats
+        dft, dfn = _u32(g.df_text), _u32(g.df_name)
+        dff = None if g.df_facet is None else _u32(g.df_facet)
+        gs = GlobalStats(int(g.n_docs), (C.c_uint64 * 2)(*[int(x) for x in g.tot_tokens]), _ptr(dft, _u32p),
+                         _ptr(dfn, _u32p), _ptr(dff, _u32p), int(g.tot_facet_tokens))
+        n = len(indexes)
+        bases = (_p * n)(*[ix._h for ix in indexes])
+        dls = [None if deleted is None or deleted[i] is None else np.ascontiguousarray(deleted[i], np.uint8)
+               for i in range(n)]
+        dp = (_u8p * n)(*[_ptr(d, _u8p) for d in dls])
+        outs = (_p * n)()
+        _check(_lib.fg_index_rescore_many(bases, n, C.byref(gs), dp, outs))
+        return [Index(outs[i]) for i in range(n)]
 
     def rescore(self, global_stats: "ShardStats", deleted=None) -> "Index":
         """fg_index_rescore: this snapshot's structure scored with other statistics."""
