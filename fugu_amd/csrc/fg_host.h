@@ -295,8 +295,11 @@ struct fg_index {
   const uint32_t* d_tfp = nullptr;
   const uint8_t* d_fn_text = nullptr;
   const uint8_t* d_fn_name = nullptr;
-  const uint32_t *d_sc_term = nullptr, *d_sc_first = nullptr, *d_bk_term = nullptr, *d_bk_first = nullptr,
-                 *d_kt_terms = nullptr;
+  // packed chunk tables of k_score / k_bucket (fg_internal.h ScoreJob::sc_* / bk_*)
+  const uint32_t *d_sc_tf = nullptr, *d_sc_tl = nullptr, *d_bk_tf = nullptr, *d_bk_tl = nullptr, *d_bk_e0 = nullptr,
+                 *d_bk_e1 = nullptr, *d_kt_terms = nullptr, *d_kt_tiny = nullptr;
+  const uint64_t *d_sc_e0 = nullptr, *d_sc_e1 = nullptr;
+  uint32_t n_scb = 0, n_ktiny = 0;  // k_score chunks; k_ktop_tiny terms
   // k_ktop's tables (structure): long terms, their first chunk, each chunk's term and first posting
   const uint32_t *d_kb_terms = nullptr, *d_kb_chunk0 = nullptr, *d_kc_big = nullptr, *d_kc_start = nullptr;
   uint32_t n_sc = 0, n_bk = 0, n_kt = 0, n_kbig = 0, n_kchunks = 0;

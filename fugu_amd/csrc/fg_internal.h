@@ -326,10 +326,23 @@ struct ScoreJob {
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
-  float* cmax;                // [score chunks] out: the largest score of each k_score chunk
-  const uint32_t* ch_term;    // chunk tables
-  const uint32_t* ch_first;
-  const uint32_t* kt_terms;   // k_ktop: terms with 1..kKtopChunk postings
+  float* cmax;                // [cmax entries] out: the largest score of each kChunk postings of a term
+  const uint32_t* coff;       // [V] first cmax entry of each term
+  // packed chunk tables (a chunk: terms [tf, tl], postings / directory entries
+  // [e0, e1) of them; one long term's slice, or several whole short terms)
+  const uint32_t* sc_tf;      // k_score chunks
+  const uint32_t* sc_tl;
+  const uint64_t* sc_e0;
+  const uint64_t* sc_e1;
+  const uint32_t* bk_tf;      // k_bucket chunks (global directory entries)
+  const uint32_t* bk_tl;
+  const uint32_t* bk_e0;
+  const uint32_t* bk_e1;
+  uint32_t n_terms;
+  uint64_t n_dir;             // directory entries (dir_off of term n_terms)
+  const uint32_t* kt_tiny;    // k_ktop_tiny: terms with 1..kKtopTiny postings (one wave each)
+  uint32_t n_tiny;
+  const uint32_t* kt_terms;   // k_ktop: terms with kKtopTiny+1..kKtopChunk postings
   // terms with more postings: k_ktop_part per chunk, then k_ktop_big per term
   const uint32_t* kb_terms;   // [n_big] the long terms
   const uint32_t* kb_chunk0;  // [n_big + 1] first chunk of each
@@ -344,6 +357,8 @@ struct ScoreJob {
 #define FG_KTOP_CHUNK 32768
 #endif
 constexpr uint32_t kKtopChunk = FG_KTOP_CHUNK;  // postings per k_ktop_part workgroup (and k_ktop's largest term)
+constexpr uint32_t kKtopTiny = 64;              // k_ktop_tiny: terms of at most this many postings, one wave each
+constexpr uint32_t kPackTerms = 256;            // k_score / k_bucket: term ids per packed chunk
 
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
@@ -357,7 +372,7 @@ hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, ui
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
                        uint32_t n_words, uint64_t* out, hipStream_t s);
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
-hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);
+hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);  // packed chunks
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,

@@ -393,11 +393,20 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.tmax = d_tmax;
   j.ktop = d_ktop;
   j.cmax = d_cmax;
-  j.ch_term = ix->d_sc_term;
-  j.ch_first = ix->d_sc_first;
-  HIPCHK(fg::launch_score(j, ix->n_sc, kBuildStream));
-  j.ch_term = ix->d_bk_term;
-  j.ch_first = ix->d_bk_first;
+  j.sc_tf = ix->d_sc_tf;
+  j.sc_tl = ix->d_sc_tl;
+  j.sc_e0 = ix->d_sc_e0;
+  j.sc_e1 = ix->d_sc_e1;
+  j.bk_tf = ix->d_bk_tf;
+  j.bk_tl = ix->d_bk_tl;
+  j.bk_e0 = ix->d_bk_e0;
+  j.bk_e1 = ix->d_bk_e1;
+  j.n_terms = V;
+  j.n_dir = ix->dir_entries;
+  j.kt_tiny = ix->d_kt_tiny;
+  j.n_tiny = ix->n_ktiny;
+  j.coff = ix->d.coff;
+  HIPCHK(fg::launch_score(j, ix->n_scb, kBuildStream));
   HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
   // k_ktop: terms of <= kKtopChunk postings one workgroup each; longer terms in
   // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
@@ -612,14 +621,91 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   // them): terms of <= kKtopChunk postings one workgroup each (kt); longer terms
   // (kb_terms) in kKtopChunk-posting chunks (kc_big / kc_start, the chunks of
   // long term x from kb_chunk0[x])
-  std::vector<uint32_t> sc_t, sc_f, bk_t, bk_f, kt, coff(V), kb_terms, kb_chunk0, kc_big, kc_start;
+  // k_score / k_bucket chunks are PACKED: a long term's slice of kScoreChunk
+  // postings (kBucketChunk directory entries), or several whole short terms
+  // (<= kPackTerms term ids, <= a slice's postings / entries together) -- the
+  // long tail of a vocabulary in a workgroup per term was most of a small
+  // segment's scoring time
+  std::vector<uint32_t> kt, kt_tiny, coff(V), kb_terms, kb_chunk0, kc_big, kc_start;
+  std::vector<uint32_t> sc_tf, sc_tl, bk_tf, bk_tl, bk_e0, bk_e1;
+  std::vector<uint64_t> sc_e0, sc_e1;
+  uint32_t n_cmax = 0;
+  {
+    // postings: pack [pt0, t) open while short terms fit
+    uint32_t pt0 = 0;
+    uint64_t pe0 = 0;
+    bool open = false;
+    auto flush_sc = [&](uint32_t t_end) {  // terms [pt0, t_end)
+      if (!open) return;
+      sc_tf.push_back(pt0);
+      sc_tl.push_back(t_end - 1);
+      sc_e0.push_back(pe0);
+      sc_e1.push_back(hp.off[t_end]);
+      open = false;
+    };
+    for (uint32_t t = 0; t < V; ++t) {
+      const uint64_t n = hp.off[t + 1] - hp.off[t];
+      coff[t] = n_cmax;  // the term's first block-max entry (DevIndex::cmax: kChunk postings each)
+      n_cmax += (uint32_t)((n + fg::kChunk - 1) / fg::kChunk);
+      if (n >= fg::kScoreChunk) {
+        flush_sc(t);
+        for (uint64_t f = 0; f < n; f += fg::kScoreChunk) {
+          sc_tf.push_back(t);
+          sc_tl.push_back(t);
+          sc_e0.push_back(hp.off[t] + f);
+          sc_e1.push_back(hp.off[t] + std::min<uint64_t>(n, f + fg::kScoreChunk));
+        }
+        continue;
+      }
+      if (open && (hp.off[t + 1] - pe0 > fg::kScoreChunk || t - pt0 >= fg::kPackTerms)) flush_sc(t);
+      if (!open) {
+        pt0 = t;
+        pe0 = hp.off[t];
+        open = true;
+      }
+    }
+    flush_sc(V);
+  }
+  {
+    // directory entries (each term: its nbk buckets + the end entry)
+    uint32_t pt0 = 0, pe0 = 0;
+    bool open = false;
+    auto flush_bk = [&](uint32_t t_end) {
+      if (!open) return;
+      bk_tf.push_back(pt0);
+      bk_tl.push_back(t_end - 1);
+      bk_e0.push_back(pe0);
+      bk_e1.push_back(t_end < V ? dir_off[t_end] : (uint32_t)nd);
+      open = false;
+    };
+    for (uint32_t t = 0; t < V; ++t) {
+      const uint32_t ne = (t + 1 < V ? dir_off[t + 1] : (uint32_t)nd) - dir_off[t];  // nbk + 1
+      if (ne > fg::kBucketChunk) {
+        flush_bk(t);
+        for (uint32_t f = 0; f < ne; f += fg::kBucketChunk) {
+          bk_tf.push_back(t);
+          bk_tl.push_back(t);
+          bk_e0.push_back(dir_off[t] + f);
+          bk_e1.push_back(dir_off[t] + std::min<uint32_t>(ne, f + fg::kBucketChunk));
+        }
+        continue;
+      }
+      if (open && (dir_off[t] + ne - pe0 > fg::kBucketChunk || t - pt0 >= fg::kPackTerms)) flush_bk(t);
+      if (!open) {
+        pt0 = t;
+        pe0 = dir_off[t];
+        open = true;
+      }
+    }
+    flush_bk(V);
+  }
   for (uint32_t t = 0; t < V; ++t) {
     const uint64_t n = hp.off[t + 1] - hp.off[t];
-    coff[t] = (uint32_t)sc_t.size();  // the term's first score chunk (DevIndex::cmax)
     if (!n) continue;
-    for (uint64_t f = 0; f < n; f += fg::kScoreChunk) { sc_t.push_back(t); sc_f.push_back((uint32_t)f); }
-    const uint64_t nbk = ((N - 1) >> (tmeta[t] & 0xFFu)) + 1;
-    for (uint64_t f = 0; f < nbk; f += fg::kBucketChunk) { bk_t.push_back(t); bk_f.push_back((uint32_t)f); }
+    if (n <= fg::kKtopTiny) {
+      kt_tiny.push_back(t);
+      continue;
+    }
     if (n <= fg::kKtopChunk) {
       kt.push_back(t);
       continue;
@@ -632,7 +718,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     kb_terms.push_back(t);
   }
   kb_chunk0.push_back((uint32_t)kc_big.size());
-  if (sc_t.size() > 0x7FFFFFFFull || bk_t.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "index too large");
+  if (sc_tf.size() > 0x7FFFFFFFull || bk_tf.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "index too large");
   HIPCHK(hipSetDevice(dev));
   DevAllocs& sm = *ix->smem;
   uint64_t& bytes = ix->struct_bytes;
@@ -640,7 +726,8 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc;
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
-  uint32_t *d_sct, *d_scf, *d_bkt, *d_bkf, *d_kt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs;
+  uint32_t *d_sctf, *d_sctl, *d_bktf, *d_bktl, *d_bke0, *d_bke1, *d_kt, *d_ktt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs;
+  uint64_t *d_sce0, *d_sce1;
   {
     UploadBatch ub;
     ub.add(hp.doc.data(), hp.doc.size(), &d_doc);
@@ -654,11 +741,16 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ub.add(tdir.data(), tdir.size(), &d_tdir);
     ub.add(hp.fdoc.data(), hp.fdoc.size(), &d_fdoc);
     ub.add(hp.foff.data(), hp.foff.size(), &d_foff);
-    ub.add(sc_t.data(), sc_t.size(), &d_sct);
-    ub.add(sc_f.data(), sc_f.size(), &d_scf);
-    ub.add(bk_t.data(), bk_t.size(), &d_bkt);
-    ub.add(bk_f.data(), bk_f.size(), &d_bkf);
+    ub.add(sc_tf.data(), sc_tf.size(), &d_sctf);
+    ub.add(sc_tl.data(), sc_tl.size(), &d_sctl);
+    ub.add(sc_e0.data(), sc_e0.size(), &d_sce0);
+    ub.add(sc_e1.data(), sc_e1.size(), &d_sce1);
+    ub.add(bk_tf.data(), bk_tf.size(), &d_bktf);
+    ub.add(bk_tl.data(), bk_tl.size(), &d_bktl);
+    ub.add(bk_e0.data(), bk_e0.size(), &d_bke0);
+    ub.add(bk_e1.data(), bk_e1.size(), &d_bke1);
     ub.add(kt.data(), kt.size(), &d_kt);
+    ub.add(kt_tiny.data(), kt_tiny.size(), &d_ktt);
     ub.add(kb_terms.data(), kb_terms.size(), &d_kbt);
     ub.add(kb_chunk0.data(), kb_chunk0.size(), &d_kb0);
     ub.add(kc_big.data(), kc_big.size(), &d_kcb);
@@ -743,10 +835,16 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d_tfp = d_tfp;
   ix->d_fn_text = d_fnt;
   ix->d_fn_name = d_fnn;
-  ix->d_sc_term = d_sct;
-  ix->d_sc_first = d_scf;
-  ix->d_bk_term = d_bkt;
-  ix->d_bk_first = d_bkf;
+  ix->d_sc_tf = d_sctf;
+  ix->d_sc_tl = d_sctl;
+  ix->d_sc_e0 = d_sce0;
+  ix->d_sc_e1 = d_sce1;
+  ix->d_bk_tf = d_bktf;
+  ix->d_bk_tl = d_bktl;
+  ix->d_bk_e0 = d_bke0;
+  ix->d_bk_e1 = d_bke1;
+  ix->d_kt_tiny = d_ktt;
+  ix->n_ktiny = (uint32_t)kt_tiny.size();
   ix->d_kt_terms = d_kt;
   ix->d_kb_terms = d_kbt;
   ix->d_kb_chunk0 = d_kb0;
@@ -754,8 +852,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d_kc_start = d_kcs;
   ix->n_kbig = (uint32_t)kb_terms.size();
   ix->n_kchunks = (uint32_t)kc_big.size();
-  ix->n_sc = (uint32_t)sc_t.size();
-  ix->n_bk = (uint32_t)bk_t.size();
+  ix->n_sc = n_cmax;
+  ix->n_scb = (uint32_t)sc_tf.size();
+  ix->n_bk = (uint32_t)bk_tf.size();
   ix->n_kt = (uint32_t)kt.size();
   ix->d.doc = d_doc;
   ix->d.off = d_off;
@@ -1265,10 +1364,16 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->d_tfp = base->d_tfp;
   ix->d_fn_text = base->d_fn_text;
   ix->d_fn_name = base->d_fn_name;
-  ix->d_sc_term = base->d_sc_term;
-  ix->d_sc_first = base->d_sc_first;
-  ix->d_bk_term = base->d_bk_term;
-  ix->d_bk_first = base->d_bk_first;
+  ix->d_sc_tf = base->d_sc_tf;
+  ix->d_sc_tl = base->d_sc_tl;
+  ix->d_sc_e0 = base->d_sc_e0;
+  ix->d_sc_e1 = base->d_sc_e1;
+  ix->d_bk_tf = base->d_bk_tf;
+  ix->d_bk_tl = base->d_bk_tl;
+  ix->d_bk_e0 = base->d_bk_e0;
+  ix->d_bk_e1 = base->d_bk_e1;
+  ix->d_kt_tiny = base->d_kt_tiny;
+  ix->n_ktiny = base->n_ktiny;
   ix->d_kt_terms = base->d_kt_terms;
   ix->d_kb_terms = base->d_kb_terms;
   ix->d_kb_chunk0 = base->d_kb_chunk0;
@@ -1277,6 +1382,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->n_kbig = base->n_kbig;
   ix->n_kchunks = base->n_kchunks;
   ix->n_sc = base->n_sc;
+  ix->n_scb = base->n_scb;
   ix->n_bk = base->n_bk;
   ix->n_kt = base->n_kt;
   ix->d = base->d;
@@ -1832,6 +1938,9 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   auto radix = [&](std::vector<W>& items, bool conj) {
     const size_t n = items.size();
     std::vector<uint64_t> a(n), bb(n);  // (sort key << 32) | item index
+    // (items of queries probing the same list next to each other within each
+    // 1/2048 of the sweep, so one XCD's L2 serves that list to all of them:
+    // measured slower, profiles/r04/ab/ab_sweep_*.log)
     for (size_t x = 0; x < n; ++x) {
       const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
       const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | (uint32_t)(kk * 2147483647.0);

@@ -2042,25 +2042,39 @@ __device__ inline float posting_score(uint32_t tfp, uint32_t fn_t, uint32_t fn_n
   return s;
 }
 
+// Packed chunks (ScoreJob::sc_*): a long term's 2048-posting slice, or the
+// postings of several whole short terms (a vocabulary's long tail would
+// otherwise cost one workgroup per term).  A posting's term: the last of the
+// chunk's term offsets (staged in LDS) at or below it.
+template <class Off>
+__device__ inline uint32_t slot_of(const Off* s_off, uint32_t nterm, uint64_t p) {
+  uint32_t lo = 0, hi = nterm;  // s_off[lo] <= p < s_off[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((uint64_t)s_off[mid] <= p) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
   __shared__ float cache[512];
+  __shared__ uint64_t s_off[kPackTerms + 1];
+  __shared__ uint32_t s_max[kPackTerms];
+  const uint32_t c = blockIdx.x, tf = j.sc_tf[c], nterm = j.sc_tl[c] - tf + 1;
+  const uint64_t e0 = j.sc_e0[c], e1 = j.sc_e1[c];
   for (uint32_t i = threadIdx.x; i < 512; i += kThreads) cache[i] = j.cache[i];
+  for (uint32_t i = threadIdx.x; i <= nterm; i += kThreads) s_off[i] = j.off[tf + i];
+  for (uint32_t i = threadIdx.x; i < nterm; i += kThreads) s_max[i] = 0u;
   __syncthreads();
-  const uint32_t t = j.ch_term[blockIdx.x], first = j.ch_first[blockIdx.x];
-  const uint64_t b = j.off[t];
-  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
-  const uint32_t end = min(n, first + kScoreChunk);
-  const float wt = j.w_text[t], wn = j.w_name[t];
-  float mx = 0.0f;
   // the chunk's postings in one step per thread: every doc / tf load, then every
   // fieldnorm gather, in flight together (kScoreChunk / kThreads per thread)
   constexpr uint32_t R = kScoreChunk / kThreads;
-  uint32_t d[R], tf[R];
+  uint32_t d[R], tfp[R];
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t p = first + r * kThreads + threadIdx.x;
-    d[r] = p < end ? j.doc[b + p] : 0xFFFFFFFFu;
-    tf[r] = p < end ? j.tfp[b + p] : 0u;
+    const uint64_t p = e0 + r * kThreads + threadIdx.x;
+    d[r] = p < e1 ? j.doc[p] : 0xFFFFFFFFu;
+    tfp[r] = p < e1 ? j.tfp[p] : 0u;
   }
   uint32_t fnt[R], fnn[R];
 #pragma unroll
@@ -2069,23 +2083,30 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
     fnt[r] = in ? j.fn_text[d[r]] : 0u;
     fnn[r] = in && j.fn_name ? j.fn_name[d[r]] : 0u;
   }
+  float mx = 0.0f;  // one term (uniform): reduced per wave, one LDS atomic
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t p = first + r * kThreads + threadIdx.x;
-    if (p >= end) continue;
-    const float v = posting_score(tf[r], fnt[r], fnn[r], wt, wn, cache);
-    j.psc[b + p] = v;
-    mx = fmaxf(mx, v);
+    const uint64_t p = e0 + r * kThreads + threadIdx.x;
+    if (p >= e1) continue;
+    const uint32_t sl = nterm == 1 ? 0u : slot_of(s_off, nterm, p);
+    const uint32_t t = tf + sl;
+    const float v = posting_score(tfp[r], fnt[r], fnn[r], j.w_text[t], j.w_name[t], cache);
+    j.psc[p] = v;
+    if (nterm == 1) mx = fmaxf(mx, v);
+    else atomicMax(&s_max[sl], __float_as_uint(v));
   }
-  // the chunk's block-max (scores >= 0)
-  __shared__ float wmax[kThreads / 64];
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  if (nterm == 1) {
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(&s_max[0], __float_as_uint(mx));
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float m = wmax[0];
-    for (uint32_t w = 1; w < kThreads / 64; ++w) m = fmaxf(m, wmax[w]);
-    j.cmax[blockIdx.x] = m;
+  // block-max of each term chunk (DevIndex::cmax: kChunk postings from the term's start)
+  for (uint32_t i = threadIdx.x; i < nterm; i += kThreads) {
+    const uint64_t b = s_off[i];
+    if (s_off[i + 1] == b) continue;  // an empty term id
+    const uint32_t t = tf + i;
+    const uint64_t first = e0 > b ? e0 : b;
+    j.cmax[j.coff[t] + (uint32_t)((first - b) / kChunk)] = __uint_as_float(s_max[i]);
   }
 }
 
@@ -2093,46 +2114,52 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
 // the 4096-doc tile maxima (terms whose buckets are no wider than a tile).
 // Scores are >= 0, so their f32 bits order like the values (atomicMax on u32).
 __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs) {
-  const uint32_t t = j.ch_term[blockIdx.x], first = j.ch_first[blockIdx.x];
-  const uint32_t meta = j.tmeta[t], B = meta & 0xFFu;
-  const uint32_t nbk = (uint32_t)(((uint64_t)(n_docs - 1) >> B) + 1);
-  const uint32_t end = min(nbk, first + kBucketChunk);
-  const uint32_t* dir = j.dir + j.dir_off[t];
-  const float* ps = j.psc + j.off[t];
-  const uint32_t to = j.toff[t];
-  uint32_t tm = 0;
+  __shared__ uint32_t s_doff[kPackTerms + 1];
+  __shared__ uint32_t s_max[kPackTerms];
+  const uint32_t c = blockIdx.x, tf = j.bk_tf[c], nterm = j.bk_tl[c] - tf + 1;
+  const uint32_t e0 = j.bk_e0[c], e1 = j.bk_e1[c];
+  for (uint32_t i = threadIdx.x; i <= nterm; i += kThreads)
+    s_doff[i] = tf + i < j.n_terms ? j.dir_off[tf + i] : (uint32_t)j.n_dir;
+  for (uint32_t i = threadIdx.x; i < nterm; i += kThreads) s_max[i] = 0u;
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t bk0 = first; bk0 < end; bk0 += kThreads) {  // uniform trip count: every lane shuffles
-    const uint32_t bk = bk0 + threadIdx.x;
-    const bool in = bk < end;
-    const uint32_t lo = in ? dir[bk] : 0u, hi = in ? dir[bk + 1] : 0u;
+  for (uint32_t i0 = e0; i0 < e1; i0 += kThreads) {  // uniform trip count: every lane shuffles
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t sl = nterm == 1 ? 0u : slot_of(s_doff, nterm, min(i, e1 - 1));
+    const uint32_t t = tf + sl;
+    const uint32_t meta = j.tmeta[t], B = meta & 0xFFu;
+    const uint32_t nbk = (uint32_t)(((uint64_t)(n_docs - 1) >> B) + 1);
+    const uint32_t bk = min(i, e1 - 1) - s_doff[sl];
+    const bool in = i < e1 && bk < nbk;  // the term's last entry is its end, not a bucket
+    const uint32_t lo = in ? j.dir[i] : 0u, hi = in ? j.dir[i + 1] : 0u;
+    const float* ps = j.psc + j.off[t];
     float mx = -0.0f;
     uint32_t bits = 0;
     if (hi > lo) {
       mx = 0.0f;
       for (uint32_t p = lo; p < hi; ++p) mx = fmaxf(mx, ps[p]);
       bits = __float_as_uint(mx);
-      tm = max(tm, bits);
+      atomicMax(&s_max[sl], bits);
     }
-    if (in) j.bmax[j.dir_off[t] + bk] = mx;
-    if (to != 0xFFFFFFFFu) {
-      // tile maxima: a segmented max over the wave's buckets (their tiles ascend
-      // with the lane), then one atomic per tile the wave touches -- not one per
-      // bucket, which put up to 64 atomics on one address for a dense term
-      const uint32_t tile = (uint32_t)(((uint64_t)(in ? bk : bk0) << B) >> kDisjTileShift);
+    if (in) j.bmax[i] = mx;
+    // tile maxima: a segmented max over the wave's buckets (their (term, tile)
+    // keys ascend with the lane), then one atomic per key the wave touches --
+    // not one per bucket, which put up to 64 atomics on one address
+    const uint32_t to = j.toff[t];
+    const uint32_t key = (in && to != 0xFFFFFFFFu) ? to + (uint32_t)(((uint64_t)bk << B) >> kDisjTileShift) : 0xFFFFFFFFu;
 #pragma unroll
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t b2 = (uint32_t)__shfl_down((int)bits, o, 64);
-        const uint32_t t2 = (uint32_t)__shfl_down((int)tile, o, 64);
-        if (lane + o < 64 && t2 == tile) bits = max(bits, b2);
-      }
-      const uint32_t prev = (uint32_t)__shfl_up((int)tile, 1, 64);
-      if (in && bits && (lane == 0 || prev != tile)) atomicMax(&j.tmax[to + tile], bits);
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t b2 = (uint32_t)__shfl_down((int)bits, o, 64);
+      const uint32_t k2 = (uint32_t)__shfl_down((int)key, o, 64);
+      if (lane + o < 64 && k2 == key) bits = max(bits, b2);
     }
+    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1, 64);
+    if (key != 0xFFFFFFFFu && bits && (lane == 0 || prev != key)) atomicMax(&j.tmax[key], bits);
   }
-  // one atomic per wave for the term maximum
-  for (int o = 32; o > 0; o >>= 1) tm = max(tm, (uint32_t)__shfl_xor((int)tm, o, 64));
-  if ((threadIdx.x & 63) == 0 && tm) atomicMax(&j.tmaxs[t], tm);
+  __syncthreads();
+  // the term maxima (a long term spans chunks: atomics)
+  for (uint32_t i = threadIdx.x; i < nterm; i += kThreads)
+    if (s_max[i]) atomicMax(&j.tmaxs[tf + i], s_max[i]);
 }
 
 // Per term the K-th best score over its ALIVE postings for K in kTopKs (0 when
@@ -2235,6 +2262,35 @@ __device__ inline void ktop_reduce(const ScoreJob& j, uint64_t b, uint32_t p0, u
   __syncthreads();
 }
 
+// terms of <= kKtopTiny postings: one wave per term (four per workgroup), the
+// alive keys sorted descending by a wave bitonic network (lane i: the i-th best)
+__global__ __launch_bounds__(kThreads) void k_ktop_tiny(ScoreJob j) {
+  const uint32_t lane = threadIdx.x & 63, x = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (x >= j.n_tiny) return;  // wave-uniform
+  const uint32_t t = j.kt_tiny[x];
+  const uint64_t b = j.off[t];
+  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
+  uint64_t key = 0;
+  if (lane < n) {
+    const uint32_t d = j.doc[b + lane];
+    if (!j.alive || ((j.alive[d >> 5] >> (d & 31u)) & 1u)) key = make_key(j.psc[b + lane], d);
+  }
+  const uint32_t na = (uint32_t)__popcll(__ballot(key != 0));
+  if (na == 0) return;
+  for (uint32_t k = 2; k <= 64; k <<= 1)
+    for (uint32_t h = k >> 1; h > 0; h >>= 1) {
+      const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)key, (int)h, 64);
+      const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), (int)h, 64);
+      const uint64_t other = ((uint64_t)hi32 << 32) | lo32;
+      const bool desc = (lane & k) == 0, lower = (lane & h) == 0;
+      key = (lower == desc) ? (key > other ? key : other) : (key < other ? key : other);
+    }
+  // lane i holds the i-th best key (zeros -- dead or absent postings -- last)
+  if (lane == 0) j.ktop[(size_t)t * kNumTopK] = key_score(key);
+  for (uint32_t kk = 1; kk < kNumTopK; ++kk)
+    if (kTopKs[kk] <= na && lane == kTopKs[kk] - 1) j.ktop[(size_t)t * kNumTopK + kk] = key_score(key);
+}
+
 // one workgroup per term of <= kKtopChunk postings
 __global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
   __shared__ KtopShared sh;
@@ -2320,6 +2376,11 @@ hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, 
 }
 
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s) {
+  if (j.n_tiny) {
+    k_ktop_tiny<<<(j.n_tiny + kThreads / 64 - 1) / (kThreads / 64), kThreads, 0, s>>>(j);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   if (n_terms) {
     k_ktop<<<n_terms, kThreads, 0, s>>>(j);
     const hipError_t e = hipGetLastError();

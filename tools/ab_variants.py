@@ -46,7 +46,7 @@ def child(args):
         h.update(d[i, :n[i]].tobytes())
         h.update(s[i, :n[i]].tobytes())
     t = np.array(times)
-    print(json.dumps({"lib": os.environ.get("FUGU_LIB"), "k_conj_ms_med": float(np.median(t[:, 0])),
+    print(json.dumps({"lib": os.environ.get("FUGU_LIB"), "env": os.environ.get("FUGU_SWEEP_TERM"), "k_conj_ms_med": float(np.median(t[:, 0])),
                       "k_conj_ms_min": float(t[:, 0].min()), "k_final_ms_med": float(np.median(t[:, 1])),
                       "hash": h.hexdigest()[:16]}))
 
@@ -69,7 +69,12 @@ def main():
     res = {}
     for r in range(args.rounds):
         for lib in args.libs:
-            env = dict(os.environ, FUGU_LIB=os.path.abspath(lib))
+            # "lib.so@NAME=VALUE,...": the variant is the library under that environment
+            path, _, envs = lib.partition("@")
+            env = dict(os.environ, FUGU_LIB=os.path.abspath(path))
+            for kv in filter(None, envs.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
             cmd = [sys.executable, __file__, "--child", "--docs", str(args.docs), "--batch", str(args.batch),
                    "--terms", str(args.terms), "--k", str(args.k), "--steps", str(args.steps)]
             if args.mixed:
