@@ -682,8 +682,7 @@ struct Snapshot {
       if (s.ix) fg_index_release(s.ix);
   }
 };
-constexpr size_t kMaxSegments = 8;    // more segments than this: the merger takes a run of small ones
-constexpr size_t kHardSegments = 48;  // ... and a commit that would pass this waits for a merge first
+constexpr size_t kHardSegments = 48;  // a commit that would pass this many segments waits for a merge first
 
 struct Namespace {
   std::string name;
@@ -730,6 +729,34 @@ struct fg_db {
   std::condition_variable mq_cv;
   std::deque<std::weak_ptr<Namespace>> queue;
   bool stop = false;
+  // replaced snapshots are released on the reaper thread: releasing a
+  // snapshot's scoring blocks waits for the device to drain (fgh::ScorePool),
+  // which must not hold up the commit or merge that replaced it
+  std::thread reaper;
+  std::mutex rq;
+  std::condition_variable rq_cv;
+  std::deque<std::shared_ptr<Snapshot>> dead;
+  bool rstop = false;
+  void retire(std::shared_ptr<Snapshot> s) {
+    if (!s) return;
+    std::lock_guard<std::mutex> l(rq);
+    dead.push_back(std::move(s));
+    if (!reaper.joinable())
+      reaper = std::thread([this] {
+        for (;;) {
+          std::shared_ptr<Snapshot> x;
+          {
+            std::unique_lock<std::mutex> l2(rq);
+            rq_cv.wait(l2, [&] { return rstop || !dead.empty(); });
+            if (dead.empty()) return;  // stopping, drained
+            x = std::move(dead.front());
+            dead.pop_front();
+          }
+          x.reset();  // the last reference, unless a search still holds it
+        }
+      });
+    rq_cv.notify_one();
+  }
   ~fg_db() {
     {
       std::lock_guard<std::mutex> l(mq);
@@ -737,6 +764,12 @@ struct fg_db {
     }
     mq_cv.notify_all();
     if (merger.joinable()) merger.join();
+    {
+      std::lock_guard<std::mutex> l(rq);
+      rstop = true;
+    }
+    rq_cv.notify_all();
+    if (reaper.joinable()) reaper.join();
   }
 };
 
@@ -1452,34 +1485,38 @@ int commit_segment(fg_db* db, Namespace& ns) {
     S.store(ns);
   }
   cur.reset();
-  prev.reset();
+  db->retire(std::move(prev));
   tr.mark("swap");
   return FG_OK;
 }
 
-// The merge policy (tantivy's LogMergePolicy keeps segments of similar size
-// together; here runs stay contiguous so the merged segment keeps global doc
-// order, which merge_fruits' (segment, doc) tie order needs): with more than
-// kMaxSegments segments, the newest (two or more) segments that together hold
-// at most half the docs of the segment before them; else the newest run of
-// segments of one size level (factor 4); else, from 2 x kMaxSegments segments
-// on, the two newest.  Returns [j0, j1) or j0 == j1 (nothing to merge).
+// The merge policy, tantivy's LogMergePolicy (indexer/log_merge_policy.rs:
+// levels of log4 size, kMergeFactor segments of one level merge together,
+// segments of kMergeMaxDocs docs or more are left alone) with runs kept
+// contiguous, so the merged segment keeps global doc order (merge_fruits' (segment,
+// doc) tie order needs it): the newest run of kMergeFactor segments of one level,
+// all under kMergeMaxDocs; else, from kHardSegments on, the two newest.  A
+// commit per upsert thus merges once every kMergeFactor commits, not after each.
+// Returns [j0, j1) or j0 == j1 (nothing to merge).
+constexpr size_t kMergeFactor = 8;            // LogMergePolicy::min_num_segments
+constexpr uint64_t kMergeMaxDocs = 1u << 20;  // ... max_docs_before_merge (a bulk load's segments stay)
+uint32_t merge_level(uint64_t x) {
+  uint32_t l = 0;
+  while (x >= 4) {
+    x >>= 2;
+    ++l;
+  }
+  return l;
+}
 std::pair<size_t, size_t> pick_merge(const std::vector<uint64_t>& n) {
   const size_t c = n.size();
-  if (c <= kMaxSegments) return {c, c};
-  std::vector<uint64_t> suffix(c + 1, 0);
-  for (size_t j = c; j-- > 0;) suffix[j] = suffix[j + 1] + n[j];
-  for (size_t j = 1; j + 2 <= c; ++j)
-    if (2 * suffix[j] <= n[j - 1]) return {j, c};
-  auto level = [](uint64_t x) {
-    uint32_t l = 0;
-    while (x >= 4) { x >>= 2; ++l; }
-    return l;
-  };
-  size_t j = c - 1;
-  while (j > 0 && level(n[j - 1]) == level(n[c - 1])) --j;
-  if (c - j >= 2) return {j, c};
-  if (c >= 2 * kMaxSegments) return {c - 2, c};  // rare: one small segment after big ones, repeatedly
+  if (c >= 2 && n[c - 1] < kMergeMaxDocs) {
+    size_t j = c - 1;
+    while (j > 0 && n[j - 1] < kMergeMaxDocs && merge_level(n[j - 1]) == merge_level(n[c - 1]) && c - j < kMergeFactor)
+      --j;
+    if (c - j >= kMergeFactor) return {j, c};
+  }
+  if (c >= kHardSegments) return {c - 2, c};
   return {c, c};
 }
 
@@ -1564,6 +1601,41 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
   if (const char* e = getenv("FUGU_MERGE_DELAY_MS"))  // tests only: searches run while the merge is in flight
     std::this_thread::sleep_for(std::chrono::milliseconds(atoi(e)));
   tr.mark("build merged segment");
+  // ---- the merged segment brought to the statistics and deletions of this
+  // moment OUTSIDE the committer lock (commits go on meanwhile); under the lock
+  // it is rescored again only if another commit slipped in
+  uint64_t src_n = 0;
+  for (const Segment& sg : src) src_n += sg.n;
+  const bool stats_change = ids.size() != src_n;  // deleted docs dropped (their N, df and tokens go)
+  uint64_t ver_used = ver0;
+  std::vector<uint8_t> mdel_used(ids.size(), 0);
+  auto refresh = [&](uint64_t& ver, std::vector<uint8_t>& md) {  // under the writer lock
+    ver = ns.st_ver;
+    if (ver != ver0) {
+      const uint32_t nt = std::max<uint32_t>(1, (uint32_t)ns.dict.size()), nf = (uint32_t)ns.fdict.size();
+      S = Stats();
+      S.load(ns, nt, nf);
+      for (const Segment& sg : src) S.add(*sg.st, true);
+      S.add(*mst, false);
+    }
+    for (size_t i = 0; i < ids.size(); ++i) md[i] = ns.del[ids[i]];
+  };
+  if (mix) {
+    {
+      std::lock_guard<std::mutex> w(ns.writer);
+      refresh(ver_used, mdel_used);
+    }
+    const bool any_del = std::find(mdel_used.begin(), mdel_used.end(), 1) != mdel_used.end();
+    if (ver_used != ver0 || any_del || stats_change) {
+      const fg_global_stats g0 = S.global();
+      fg_index* re = nullptr;
+      const int rc = fg_index_rescore(mix, &g0, any_del ? mdel_used.data() : nullptr, &re);
+      fg_index_release(mix);
+      if (rc) return hfail(rc, fg_last_error());
+      mix = re;
+    }
+  }
+  tr.mark("rescore merged segment");
   // ---- swap: no commit runs meanwhile
   std::lock_guard<std::mutex> c(ns.committer);
   tr.mark("wait for the committer");
@@ -1581,28 +1653,21 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     if (mix) fg_index_release(mix);
     return hfail(FG_EINVAL, "merge sources vanished from the snapshot");
   }
-  uint64_t src_n = 0;
-  for (const Segment& sg : src) src_n += sg.n;
-  const bool stats_change = ids.size() != src_n;  // deleted docs dropped (their N, df and tokens go)
   std::vector<uint8_t> del, mdel(ids.size(), 0);
-  bool new_del = false, moved = false;
+  bool moved = false, new_del = false;
   {
     std::lock_guard<std::mutex> w(ns.writer);
-    moved = ns.st_ver != ver0;  // commits since the gather: other statistics
-    if (moved) {
-      const uint32_t nt = std::max<uint32_t>(1, (uint32_t)ns.dict.size()), nf = (uint32_t)ns.fdict.size();
-      S = Stats();
-      S.load(ns, nt, nf);
-      for (const Segment& sg : src) S.add(*sg.st, true);
-      S.add(*mst, false);
-    }
-    for (size_t i = 0; i < ids.size(); ++i) new_del |= (mdel[i] = ns.del[ids[i]]) != 0;
+    uint64_t ver = 0;
+    refresh(ver, mdel);
+    moved = ver != ver_used;  // a commit since the pre-swap rescore: other statistics
+    new_del = mdel != mdel_used;
     del = ns.del;
   }
   const fg_global_stats g = S.global();
-  if (mix && (moved || new_del || stats_change)) {
+  if (mix && (moved || new_del)) {
     fg_index* re = nullptr;
-    const int rc = fg_index_rescore(mix, &g, new_del ? mdel.data() : nullptr, &re);
+    const bool any_del = std::find(mdel.begin(), mdel.end(), 1) != mdel.end();  // every deletion, not just the new ones
+    const int rc = fg_index_rescore(mix, &g, any_del ? mdel.data() : nullptr, &re);
     fg_index_release(mix);
     if (rc) return hfail(rc, fg_last_error());
     mix = re;
@@ -1640,7 +1705,7 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
   }
   now.reset();
   cur.reset();
-  prev.reset();
+  db->retire(std::move(prev));
   tr.mark("rescore + swap");
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   {
@@ -1742,11 +1807,14 @@ int fg_db_commit(fg_db* db, const char* nsname) {
     if (int rc = merge_once(db, *ns, &did)) return rc;
   }
   if (int rc = commit_segment(db, *ns)) return rc;
+  std::vector<uint64_t> sizes;
   {
     std::shared_lock<std::shared_mutex> l(ns->snap_mu);
-    nseg = ns->snap ? ns->snap->segs.size() : 0;
+    if (ns->snap)
+      for (auto& sg : ns->snap->segs) sizes.push_back(sg.n);
   }
-  if (nseg > kMaxSegments) enqueue_merge(db, ns);
+  const auto run = pick_merge(sizes);
+  if (run.first < run.second) enqueue_merge(db, ns);
   return FG_OK;
 }
 

@@ -622,19 +622,10 @@ def test_json_shapes_with_hits_and_canonical_metadata(db):
 
 
 def pick_merge(n):
-    """host.cpp pick_merge, restated: with more than 8 segments, the newest
-    segments holding together at most half the docs of the one before them;
-    else the newest run of one size level (factor 4); else, from 16 segments
-    on, the two newest."""
+    """host.cpp pick_merge, restated (tantivy's LogMergePolicy with contiguous
+    runs): the newest run of 8 segments of one log4 size level, each under 2^20
+    docs; else, from 48 segments on, the two newest."""
     c = len(n)
-    if c <= 8:
-        return None
-    suffix = [0] * (c + 1)
-    for j in range(c - 1, -1, -1):
-        suffix[j] = suffix[j + 1] + n[j]
-    for j in range(1, c - 1):
-        if 2 * suffix[j] <= n[j - 1]:
-            return j, c
 
     def level(x):
         lv = 0
@@ -642,12 +633,13 @@ def pick_merge(n):
             x >>= 2
             lv += 1
         return lv
-    j = c - 1
-    while j > 0 and level(n[j - 1]) == level(n[c - 1]):
-        j -= 1
-    if c - j >= 2:
-        return j, c
-    return (c - 2, c) if c >= 16 else None
+    if c >= 2 and n[c - 1] < (1 << 20):
+        j = c - 1
+        while j > 0 and n[j - 1] < (1 << 20) and level(n[j - 1]) == level(n[c - 1]) and c - j < 8:
+            j -= 1
+        if c - j >= 8:
+            return j, c
+    return (c - 2, c) if c >= 48 else None
 
 
 def quantized(n):
@@ -743,14 +735,14 @@ def test_db_search_during_background_merge(db, monkeypatch):
     ctx = native.Context((0,))
     d = db.Database(ctx)
     d.create_namespace("bg")
-    recs = build_corpus(23, 900)
-    for c in range(0, 900, 100):
+    recs = build_corpus(23, 800)
+    for c in range(0, 800, 100):
         for rid, t, meta in recs[c:c + 100]:
             d.upsert(db.ObjectRecord(rid, t, metadata=meta), "bg")
-        d.commit("bg")  # the ninth commit queues a merge of all nine segments
+        d.commit("bg")  # the eighth commit queues a merge of the eight segments (one size level)
     assert d.merge_info("bg")["pending"] == 1
     before = d.segments("bg")
-    assert len(before) == 9
+    assert len(before) == 8
     rng = random.Random(3)
     qs = []
     for _ in range(24):
