@@ -118,27 +118,34 @@ struct Union {
   std::vector<std::atomic<uint64_t>> bm[A_N];
   void init(const Snap& s) {
     for (uint32_t a = 0; a < A_N; ++a) {
+      qlines[a].store(0, std::memory_order_relaxed);
       const uint64_t words = (s.bytes[a] / kLine + 2 + 63) / 64;
       std::vector<std::atomic<uint64_t>> v(words);
       for (auto& w : v) w.store(0, std::memory_order_relaxed);
       bm[a].swap(v);
     }
   }
+  std::atomic<uint64_t> qlines[A_N];  // per-query distinct lines summed, by array
   // sorts / dedups the query's lines; returns how many are distinct
   uint64_t add(std::vector<uint64_t>& lines) {
     std::sort(lines.begin(), lines.end());
     lines.erase(std::unique(lines.begin(), lines.end()), lines.end());
     for (uint64_t x : lines) {
+      qlines[x >> 56].fetch_add(1, std::memory_order_relaxed);
       const uint32_t a = (uint32_t)(x >> 56);
       const uint64_t l = x & ((1ull << 56) - 1);
       if ((l >> 6) < bm[a].size()) bm[a][l >> 6].fetch_or(1ull << (l & 63), std::memory_order_relaxed);
     }
     return lines.size();
   }
+  uint64_t count(uint32_t a) const {
+    uint64_t n = 0;
+    for (const auto& w : bm[a]) n += (uint64_t)__builtin_popcountll(w.load(std::memory_order_relaxed));
+    return n;
+  }
   uint64_t count() const {
     uint64_t n = 0;
-    for (uint32_t a = 0; a < A_N; ++a)
-      for (const auto& w : bm[a]) n += (uint64_t)__builtin_popcountll(w.load(std::memory_order_relaxed));
+    for (uint32_t a = 0; a < A_N; ++a) n += count(a);
     return n;
   }
 };
@@ -483,6 +490,12 @@ int fg_model_batch(const fg_index* ix, const fg_query_batch* q, uint32_t k, cons
   }
   out->alg_bytes = out->stream_bytes + out->probe_bytes + out->output_bytes;
   out->line_bytes = (double)kLine * (double)U.count();
+  if (getenv("FUGU_MODEL_TRACE")) {  // the line floor and the per-query line sum, by array
+    static const char* names[A_N] = {"doc", "psc", "rank", "dense", "dir", "bmax", "tmax", "tdir", "cmax"};
+    for (uint32_t a = 0; a < A_N; ++a)
+      fprintf(stderr, "[fg model] %-6s floor %8.3f GB  per-query sum %8.3f GB\n", names[a],
+              (double)kLine * (double)U.count(a) * 1e-9, (double)kLine * (double)U.qlines[a].load() * 1e-9);
+  }
   return FG_OK;
 }
 
