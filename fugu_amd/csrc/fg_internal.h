@@ -96,6 +96,9 @@ constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #ifndef FG_TDIR
 #define FG_TDIR 1  // A/B: k_disj tile ranges from the tile directory (0: the bucket directory)
 #endif
+#ifndef FG_MULTI_DEFER
+#define FG_MULTI_DEFER 1  // A/B: the multi-snapshot k_conj with (1) or without (0) deferred probes
+#endif
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
 #endif

@@ -1933,6 +1933,7 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
         remap[t][j] = ns->dict.try_emplace(key, (uint32_t)ns->dict.size()).first->second;
       }
     }
+    tr.mark("dictionary merge");
     {
       std::vector<std::thread> th;
       for (int t = 0; t < T; ++t)
@@ -1943,6 +1944,7 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
         });
       for (auto& x : th) x.join();
     }
+    tr.mark("remap");
     // a bulk load sizes the id map once; a small batch lets it grow geometrically
     // (reserving size + n on every call rehashed all 10M entries per commit)
     if (n > ns->by_id_token.size()) ns->by_id_token.reserve(ns->by_id_token.size() + n);
