@@ -197,6 +197,59 @@ struct LocalDict {
   }
 };
 
+// A namespace's term dictionary (term -> id, ids in insertion order): open
+// addressing over an arena, each slot holding the hash's high half beside the
+// id, so a lookup touches one slot line and, on a hash match, the term's bytes
+// (a node-based map chased two or three pointers per lookup; a 1000-doc upsert
+// looks up ~20K distinct words in a dictionary of 10^6 terms).
+struct TermDict {
+  static constexpr uint32_t kMissing = 0xFFFFFFFFu;
+  std::string arena;
+  std::vector<uint64_t> ent;                                  // by id: arena offset << 8 | length
+  std::vector<uint64_t> slot = std::vector<uint64_t>(1u << 16, 0);  // (hash >> 32) << 32 | (id + 1); 0 = empty
+  uint32_t size() const { return (uint32_t)ent.size(); }
+  static uint64_t hash(std::string_view w) { return LocalDict::hash(w); }
+  std::string_view key(uint32_t id) const {
+    return std::string_view(arena.data() + (ent[id] >> 8), ent[id] & 0xFF);
+  }
+  void prefetch(uint64_t h) const { __builtin_prefetch(&slot[h & (slot.size() - 1)]); }
+  uint32_t find(std::string_view w, uint64_t h) const {
+    for (size_t m = slot.size() - 1, i = h & m;; i = (i + 1) & m) {
+      const uint64_t x = slot[i];
+      if (!x) return kMissing;
+      if ((x >> 32) == (h >> 32) && key((uint32_t)x - 1) == w) return (uint32_t)x - 1;
+    }
+  }
+  uint32_t find(std::string_view w) const { return find(w, hash(w)); }
+  uint32_t get(std::string_view w, uint64_t h) {  // find, else insert with the next id
+    const uint32_t f = find(w, h);
+    if (f != kMissing) return f;
+    if (2 * (ent.size() + 1) > slot.size()) grow();
+    const uint32_t id = (uint32_t)ent.size();
+    ent.push_back(((uint64_t)arena.size() << 8) | w.size());
+    arena.append(w.data(), w.size());
+    for (size_t m = slot.size() - 1, i = h & m;; i = (i + 1) & m)
+      if (!slot[i]) {
+        slot[i] = ((h >> 32) << 32) | (id + 1ull);
+        break;
+      }
+    return id;
+  }
+  uint32_t get(std::string_view w) { return get(w, hash(w)); }
+  void grow() {
+    std::vector<uint64_t> ns(slot.size() * 2, 0);
+    for (uint32_t id = 0; id < ent.size(); ++id) {
+      const uint64_t h = hash(key(id));
+      for (size_t m = ns.size() - 1, i = h & m;; i = (i + 1) & m)
+        if (!ns[i]) {
+          ns[i] = ((h >> 32) << 32) | (id + 1ull);
+          break;
+        }
+    }
+    slot.swap(ns);
+  }
+};
+
 // ---------------------------------------------------------------- query parser subset
 // QueryParser::for_index(index, [text, name]).parse_query (src/db/search.rs:108-127)
 // restricted to what the device runs (tantivy-query-grammar 0.24: the default
@@ -694,7 +747,7 @@ struct Namespace {
   std::deque<Doc> docs;
   std::vector<uint8_t> del;                            // del[d] == docs[d].deleted (commits copy this, not the docs)
   bool any_name = false;                               // some doc has a name field
-  std::unordered_map<std::string, uint32_t> dict;      // term dictionary (text and name tokens)
+  TermDict dict;                                       // term dictionary (text and name tokens)
   std::unordered_map<std::string, uint32_t> fdict;     // facet dictionary (encoded facet terms)
   std::unordered_map<std::string, std::vector<uint32_t>> by_id_token;
   std::shared_ptr<Snapshot> snap;                      // committed device snapshot
@@ -794,11 +847,7 @@ std::vector<uint32_t> intern(Namespace& ns, std::string_view text) {
   analyze(text, toks);
   std::vector<uint32_t> ids;
   ids.reserve(toks.size());
-  for (auto& t : toks) {
-    auto it = ns.dict.find(t);
-    if (it == ns.dict.end()) it = ns.dict.emplace(t, (uint32_t)ns.dict.size()).first;
-    ids.push_back(it->second);
-  }
+  for (auto& t : toks) ids.push_back(ns.dict.get(t));
   return ids;
 }
 
@@ -878,8 +927,8 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
     // term ids are stable once interned; ids interned after the snapshot are >= its n_terms
     std::lock_guard<std::mutex> w(ns.writer);
     for (auto& t : terms) {
-      auto it = ns.dict.find(t);
-      ids.push_back(it == ns.dict.end() ? FG_TERM_MISSING : it->second);
+      const uint32_t id = ns.dict.find(t);
+      ids.push_back(id == TermDict::kMissing ? FG_TERM_MISSING : id);
     }
     for (auto& c : clauses) {
       auto it = ns.fdict.find(c);
@@ -1925,12 +1974,16 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
   {  // the writer lock: the dictionary merge and the ordered upserts
     std::lock_guard<std::mutex> w(ns->writer);
     std::vector<std::vector<uint32_t>> remap(T);
-    std::string key;
     for (int t = 0; t < T; ++t) {
-      remap[t].resize(ldict[t].ent.size());
-      for (uint32_t j = 0; j < ldict[t].ent.size(); ++j) {
-        key.assign(ldict[t].key(j));
-        remap[t][j] = ns->dict.try_emplace(key, (uint32_t)ns->dict.size()).first->second;
+      const uint32_t ne = (uint32_t)ldict[t].ent.size();
+      std::vector<uint64_t> hs(ne);
+      for (uint32_t j = 0; j < ne; ++j) hs[j] = TermDict::hash(ldict[t].key(j));
+      remap[t].resize(ne);
+      constexpr uint32_t kAhead = 16;  // the slot lines of later lookups in flight
+      for (uint32_t j = 0; j < std::min(ne, kAhead); ++j) ns->dict.prefetch(hs[j]);
+      for (uint32_t j = 0; j < ne; ++j) {
+        if (j + kAhead < ne) ns->dict.prefetch(hs[j + kAhead]);
+        remap[t][j] = ns->dict.get(ldict[t].key(j), hs[j]);
       }
     }
     tr.mark("dictionary merge");
