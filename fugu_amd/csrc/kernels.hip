@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[i];
     uint32_t lo, hi;
     float ub;
-    if (FG_TDIR && B <= kTileShift && sh.c_toff[i] != kInvalid) {
+    if (B <= kTileShift && sh.c_toff[i] != kInvalid) {
       // the tile directory: adjacent entries (32 tiles of a clause per line)
       const uint32_t to = sh.c_toff[i] + tile;
       lo = ix.tdir[to];
@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     } else if (B <= kTileShift) {
       lo = dir[d0 >> B];
       hi = dir[((d1 - 1) >> B) + 1];
-      ub = sh.c_toff[i] != kInvalid ? ix.tmax[sh.c_toff[i] + tile] : ix.tmaxs[terms[i]];
+      ub = ix.tmaxs[terms[i]];
     } else {
       // one bucket holds the tile: branchless searches for d0 and d1 inside it
       const uint32_t b = d0 >> B;
