@@ -77,7 +77,39 @@ struct ScorePool {
   static constexpr size_t kKeep = 2;  // blocks cached per structure
   std::mutex mu;
   std::vector<std::pair<size_t, void*>> free_blocks;
+  // pinned host blocks of the per-term maxima read back after every scoring
+  // (tmaxs, ktop: 24 B per vocabulary term): the device writes them in place and
+  // a rescore reuses a released snapshot's block (a fresh pageable array per
+  // rescore cost page faults on every page and a staging copy)
+  std::vector<std::pair<size_t, void*>> free_host;
   int dev = 0;
+  void* get_host(size_t bytes) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      for (size_t i = 0; i < free_host.size(); ++i)
+        if (free_host[i].first == bytes) {
+          void* p = free_host[i].second;
+          free_host.erase(free_host.begin() + i);
+          return p;
+        }
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 16), hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    return p;
+  }
+  void put_host(void* p, size_t bytes) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (free_host.size() < kKeep) {
+        free_host.emplace_back(bytes, p);
+        return;
+      }
+    }
+    (void)hipHostFree(p);
+  }
   void* get(size_t bytes) {
     {
       std::lock_guard<std::mutex> l(mu);
@@ -117,18 +149,63 @@ struct ScorePool {
     free_blocks.clear();
   }
   ~ScorePool() {
+    for (auto& b : free_host) (void)hipHostFree(b.second);
     if (free_blocks.empty()) return;
     (void)hipSetDevice(dev);
     for (auto& b : free_blocks) (void)hipFree(b.second);
   }
 };
 struct ScoreBlock {
-  void* p = nullptr;
+  void* p = nullptr;  // device scoring tables
   size_t bytes = 0;
+  void* hp = nullptr;  // pinned host block (tmaxs, ktop) or nullptr
+  size_t hbytes = 0;
   std::shared_ptr<ScorePool> pool;
   ~ScoreBlock() {
+    if (hp && pool) pool->put_host(hp, hbytes);
     if (p && pool) pool->put(p, bytes);
   }
+};
+
+// A host array of a snapshot's structure (or of one scoring's weights), shared
+// by the snapshot and its rescores: copying one copies the pointer.  Written
+// only while a single owner holds it (the build); mut() copies it first
+// otherwise.  A rescore used to copy ~28 MB of such arrays per segment.
+template <class T>
+class SharedVec {
+  std::shared_ptr<std::vector<T>> p_ = std::make_shared<std::vector<T>>();
+
+ public:
+  SharedVec() = default;
+  SharedVec(std::vector<T>&& v) : p_(std::make_shared<std::vector<T>>(std::move(v))) {}
+  SharedVec& operator=(std::vector<T>&& v) {
+    p_ = std::make_shared<std::vector<T>>(std::move(v));
+    return *this;
+  }
+  SharedVec& operator=(const std::vector<T>& v) {
+    p_ = std::make_shared<std::vector<T>>(v);
+    return *this;
+  }
+  const T& operator[](size_t i) const { return (*p_)[i]; }
+  size_t size() const { return p_->size(); }
+  bool empty() const { return p_->empty(); }
+  const T* data() const { return p_->data(); }
+  typename std::vector<T>::const_iterator begin() const { return p_->begin(); }
+  typename std::vector<T>::const_iterator end() const { return p_->end(); }
+  const std::vector<T>& vec() const { return *p_; }
+  std::vector<T>& mut() {
+    if (p_.use_count() > 1) p_ = std::make_shared<std::vector<T>>(*p_);
+    return *p_;
+  }
+};
+
+// BM25 weights of one set of statistics, shared by the snapshots scored with
+// them (fg_index_rescore_many); d_w: the same on the device (text [V], name [V])
+// or nullptr
+struct Weights {
+  SharedVec<float> wt, wn;
+  const float* d_w = nullptr;
+  int dev = -1;
 };
 
 
@@ -270,22 +347,24 @@ struct fg_index {
   uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
   float avgdl[2] = {0, 0};
   float cache[512];
-  std::vector<float> ktop;  // [V * kNumTopK] K-th best alive score per term (kTopKs)
-  std::vector<float> tmaxs; // [V] largest posting score per term
-  std::vector<float> w_text, w_name;
+  const float* ktop = nullptr;   // [V * kNumTopK] K-th best alive score per term (kTopKs)
+  const float* tmaxs = nullptr;  // [V] largest posting score per term
+  std::vector<float> hown;       // ktop / tmaxs when no pinned block was had (sblock.hp)
+  fgh::SharedVec<float> w_text, w_name;
   // ---- structure (independent of the statistics; shared with rescored snapshots)
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> df_text, df_name;  // this snapshot's own postings (tantivy's per-segment cost order)
-  std::vector<uint32_t> first_doc, last_doc;
+  fgh::SharedVec<uint64_t> off;
+  fgh::SharedVec<uint32_t> df_text, df_name;  // this snapshot's own postings (tantivy's per-segment cost order)
+  fgh::SharedVec<uint32_t> first_doc, last_doc;
   std::shared_ptr<const std::vector<uint32_t>> h_doc;  // optional host copy for fg_bytes_model(_gpu)
-  std::vector<uint32_t> tmeta;  // host copy of DevIndex::tmeta (probe kind of each term)
+  fgh::SharedVec<uint32_t> tmeta;  // host copy of DevIndex::tmeta (probe kind of each term)
   uint64_t tot_local[2] = {0, 0};
   // facet field (FG_FIELD_FACET)
   uint32_t n_fterms = 0;
   uint64_t tot_f = 0, tot_f_local = 0;
   float avgdl_f = 0.0f, cache_f1 = 0.0f;
-  std::vector<uint64_t> foff;
-  std::vector<uint32_t> df_facet, df_facet_local, ffirst, flast;
+  fgh::SharedVec<uint64_t> foff;
+  std::vector<uint32_t> df_facet;
+  fgh::SharedVec<uint32_t> df_facet_local, ffirst, flast;
   std::vector<float> fscore;    // a facet clause's score in a doc holding the term (tf 1, fieldnorm id 1)
   // device: structure arrays (smem, shared), the scoring tables (sblock, from the
   // structure's spool) and other snapshot-own arrays (mem)

@@ -93,9 +93,6 @@ constexpr uint32_t kDisjTileShift = FG_TILE_SHIFT;   // k_disj: 4096-doc tiles
 #ifndef FG_DISJ_G
 #define FG_DISJ_G 1  // ab_disj_g_k*.log, ab_disj_gpq_k*.log: 4 / 2 / 1 -> OR top-1000 7.00 / 6.51 / 6.13 ms, top-20 4.60 / 4.27 / 3.94 ms
 #endif
-#ifndef FG_MULTI_DEFER
-#define FG_MULTI_DEFER 1  // A/B: the multi-snapshot k_conj with (1) or without (0) deferred probes
-#endif
 #ifndef FG_DISJ_MAXGROUP
 #define FG_DISJ_MAXGROUP 32
 #endif

@@ -255,30 +255,6 @@ int check_device(int dev) {
 // K-th best alive scores (k_ktop), optional f32 score tables, the alive
 // bitset.  `df_t`/`df_n`/`df_f`: the statistics' doc frequencies (global for a
 // doc-sharded namespace).  Structure arrays must be in ix->d already.
-// Pinned host memory of the calling thread for the read-back of a snapshot's
-// per-term bounds (pageable read-backs of several snapshots scored side by side
-// serialise on the staging copies).
-uint8_t* pinned_scratch(size_t bytes) {
-  struct Buf {
-    uint8_t* p = nullptr;
-    size_t n = 0;
-    ~Buf() {
-      if (p) (void)hipHostFree(p);
-    }
-  };
-  thread_local Buf b;
-  if (b.n < bytes) {
-    if (b.p) (void)hipHostFree(b.p);
-    b.p = nullptr;
-    b.n = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&b.p), bytes, hipHostMallocDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    b.n = bytes;
-  }
-  return b.p;
-}
 
 // BM25 weights of terms [0, V) for statistics (Ns, df_t, df_n) (tantivy's f32 order)
 void bm25_weights(uint64_t Ns, const uint32_t* df_t, const uint32_t* df_n, uint32_t V, std::vector<float>& wt,
@@ -296,7 +272,7 @@ void bm25_weights(uint64_t Ns, const uint32_t* df_t, const uint32_t* df_n, uint3
 // wts: the weights of (Ns, df_t, df_n) for at least ix's terms, or nullptr (computed here)
 int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_t* df_t, const uint32_t* df_n,
                 const std::vector<uint32_t>& alive, uint64_t tot_f, const uint32_t* df_f,
-                const std::pair<std::vector<float>, std::vector<float>>* wts = nullptr) {
+                const fgh::Weights* wts = nullptr) {
   const uint32_t V = ix->n_terms;
   const uint64_t N = ix->n_docs;
   ix->n_stats = Ns;
@@ -306,12 +282,17 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
     ix->avgdl[f] = (float)ix->tot[f] / (float)Ns;  // total_num_tokens as f32 / N as f32
     bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
   }
-  if (wts) {
-    ix->w_text.assign(wts->first.begin(), wts->first.begin() + V);
-    ix->w_name.assign(wts->second.begin(), wts->second.begin() + V);
+  if (wts) {  // shared: at least V terms
+    ix->w_text = wts->wt;
+    ix->w_name = wts->wn;
   } else {
-    bm25_weights(Ns, df_t, df_n, V, ix->w_text, ix->w_name);
+    std::vector<float> wt, wn;
+    bm25_weights(Ns, df_t, df_n, V, wt, wn);
+    ix->w_text = std::move(wt);
+    ix->w_name = std::move(wn);
   }
+  // the weights already on this device (one upload for every snapshot of a rescore_many)
+  const bool dev_w = wts && wts->d_w && wts->dev == ix->dev;
   // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
   // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
   const uint32_t VF = ix->n_fterms;
@@ -365,8 +346,13 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       o += (std::max<size_t>(pt.bytes, 16) + 255) & ~size_t(255);
     }
   }
-  HIPCHK(hipMemcpyAsync(d_wt, ix->w_text.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
-  HIPCHK(hipMemcpyAsync(d_wn, ix->w_name.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
+  if (dev_w) {  // (the block keeps its two weight parts: one block size for every scoring of the structure)
+    d_wt = const_cast<float*>(wts->d_w);
+    d_wn = const_cast<float*>(wts->d_w) + wts->wt.size();
+  } else {
+    HIPCHK(hipMemcpyAsync(d_wt, ix->w_text.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
+    HIPCHK(hipMemcpyAsync(d_wn, ix->w_name.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
+  }
   HIPCHK(hipMemcpyAsync(d_cache, ix->cache, 4ull * 512, hipMemcpyHostToDevice, kBuildStream));
   if (d_alive) HIPCHK(hipMemcpyAsync(d_alive, alive.data(), 4ull * alive.size(), hipMemcpyHostToDevice, kBuildStream));
   g_bt.mark("scoring uploads + allocs");
@@ -441,18 +427,23 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.n_big = (uint32_t)n_big;
   HIPCHK(fg::launch_ktop(j, (uint32_t)n_small, (uint32_t)n_chunks, (uint32_t)n_big, kBuildStream));
   g_bt.mark("scoring launches");
-  ix->tmaxs.resize(V);
-  ix->ktop.resize((size_t)V * fg::kNumTopK);
-  if (uint8_t* pin = pinned_scratch(4ull * V * (1 + fg::kNumTopK))) {
-    HIPCHK(hipMemcpyAsync(pin, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
-    HIPCHK(hipMemcpyAsync(pin + 4ull * V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
+  // tmaxs [V] then ktop [V * kNumTopK], read straight into the structure's
+  // pooled pinned block (a released snapshot's, after the first rescores)
+  {
+    const size_t hb = 4ull * V * (1 + fg::kNumTopK);
+    float* h = static_cast<float*>(ix->spool->get_host(hb));
+    if (h) {
+      ix->sblock.hp = h;
+      ix->sblock.hbytes = hb;
+    } else {
+      ix->hown.resize((size_t)V * (1 + fg::kNumTopK));
+      h = ix->hown.data();
+    }
+    HIPCHK(hipMemcpyAsync(h, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
+    HIPCHK(hipMemcpyAsync(h + V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
     HIPCHK(hipStreamSynchronize(kBuildStream));
-    std::memcpy(ix->tmaxs.data(), pin, 4ull * V);
-    std::memcpy(ix->ktop.data(), pin + 4ull * V, 4ull * V * fg::kNumTopK);
-  } else {
-    HIPCHK(hipMemcpyAsync(ix->tmaxs.data(), d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
-    HIPCHK(hipMemcpyAsync(ix->ktop.data(), d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
-    HIPCHK(hipStreamSynchronize(kBuildStream));
+    ix->tmaxs = h;
+    ix->ktop = h + V;
   }
   g_bt.mark("device scoring");
   // f32 score tables (FUGU_DENSE_GIB, default none: rank words serve the dense
@@ -489,8 +480,9 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       }
     }
   }
-  std::vector<uint32_t> tmeta = ix->tmeta;
+  std::vector<uint32_t> tmeta;
   if (!f32_terms.empty()) {
+    tmeta = ix->tmeta.vec();
     HIPCHK(hipMemsetD32Async(d_dense, (int)0xBF800000u, N * f32_terms.size(), kBuildStream));  // -1.0f: absent
     for (uint32_t s2 = 0; s2 < f32_terms.size(); ++s2) {
       const uint32_t t = f32_terms[s2];
@@ -876,25 +868,31 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->off = std::move(hp.off);
   ix->df_text = std::move(hp.df_text);
   ix->df_name = std::move(hp.df_name);
-  ix->first_doc.assign(V, 0);
-  ix->last_doc.assign(V, 0);
-  for (uint32_t t = 0; t < V; ++t)
-    if (ix->off[t + 1] > ix->off[t]) {
-      ix->first_doc[t] = hp.doc[ix->off[t]];
-      ix->last_doc[t] = hp.doc[ix->off[t + 1] - 1];
-    }
+  {
+    std::vector<uint32_t> fd(V, 0), ld(V, 0);
+    for (uint32_t t = 0; t < V; ++t)
+      if (ix->off[t + 1] > ix->off[t]) {
+        fd[t] = hp.doc[ix->off[t]];
+        ld[t] = hp.doc[ix->off[t + 1] - 1];
+      }
+    ix->first_doc = std::move(fd);
+    ix->last_doc = std::move(ld);
+  }
   if (keep_host) ix->h_doc = std::make_shared<const std::vector<uint32_t>>(std::move(hp.doc));
   const uint32_t VF = hp.n_fterms;
   ix->n_fterms = VF;
   ix->df_facet_local = hp.df_facet;
   ix->tot_f_local = hp.tot_f;
-  ix->ffirst.assign(VF, 0);
-  ix->flast.assign(VF, 0);
-  for (uint32_t t = 0; t < VF; ++t)
-    if (hp.foff[t + 1] > hp.foff[t]) {
-      ix->ffirst[t] = hp.fdoc[hp.foff[t]];
-      ix->flast[t] = hp.fdoc[hp.foff[t + 1] - 1];
-    }
+  {
+    std::vector<uint32_t> ff(VF, 0), fl(VF, 0);
+    for (uint32_t t = 0; t < VF; ++t)
+      if (hp.foff[t + 1] > hp.foff[t]) {
+        ff[t] = hp.fdoc[hp.foff[t]];
+        fl[t] = hp.fdoc[hp.foff[t + 1] - 1];
+      }
+    ix->ffirst = std::move(ff);
+    ix->flast = std::move(fl);
+  }
   ix->foff = std::move(hp.foff);
   // statistics: the shard's own, or the namespace's global ones
   if (g && VF && !g->df_facet) return fail(FG_EINVAL, "global statistics lack df_facet for a faceted shard");
@@ -1315,7 +1313,7 @@ int fg_index_build_global(fg_ctx* ctx, int dev, const fg_index_input* in, const 
 
 // one snapshot rescored (fg_index_rescore); wts: shared precomputed weights or nullptr
 static int rescore_one(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out,
-                       const std::pair<std::vector<float>, std::vector<float>>* wts) {
+                       const fgh::Weights* wts) {
   if (!base || !g || !out || !g->df_text) return fail(FG_EINVAL, "bad arguments");
   const uint32_t N = base->n_docs, V = base->n_terms, VF = base->n_fterms;
   if (g->n_docs < N || g->n_docs >= 0x7FFFFFFFull) return fail(FG_EINVAL, "bad global statistics");
@@ -1331,7 +1329,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->dev = base->dev;
   ix->mem.dev = base->dev;
   ix->pool.dev = base->dev;
-  // the structure: shared device arrays, copied host bookkeeping
+  // the structure: shared device arrays and host bookkeeping (SharedVec)
   ix->smem = base->smem;
   ix->spool = base->spool;  // the structure's scoring blocks (a released rescore's block comes back)
   ix->struct_bytes = base->struct_bytes;
@@ -1353,8 +1351,11 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   // f32 score tables belong to the scoring: drop base's slots of that kind
   ix->tmeta = base->tmeta;
   bool f32_slots = false;
-  for (auto& m : ix->tmeta)
-    if (fg::meta_slot(m) && !fg::meta_rank(m)) { m &= 0xFFFFu; f32_slots = true; }
+  for (uint32_t m : base->tmeta)
+    if (fg::meta_slot(m) && !fg::meta_rank(m)) { f32_slots = true; break; }
+  if (f32_slots)
+    for (auto& m : ix->tmeta.mut())
+      if (fg::meta_slot(m) && !fg::meta_rank(m)) m &= 0xFFFFu;
   ix->n_fterms = VF;
   ix->tot_f_local = base->tot_f_local;
   ix->foff = base->foff;
@@ -1423,9 +1424,36 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
     outs[i] = nullptr;
   }
   if (n == 0) return FG_OK;
-  // the weights once for every snapshot (they depend on the statistics only)
-  std::pair<std::vector<float>, std::vector<float>> wts;
-  bm25_weights(g->n_docs, g->df_text, g->df_name, V, wts.first, wts.second);
+  // the weights once for every snapshot (they depend on the statistics only),
+  // and once on the device when the snapshots share one
+  fgh::Weights wts;
+  {
+    std::vector<float> wt, wn;
+    bm25_weights(g->n_docs, g->df_text, g->df_name, V, wt, wn);
+    wts.wt = std::move(wt);
+    wts.wn = std::move(wn);
+  }
+  bool one_dev = true;
+  for (uint32_t i = 1; i < n; ++i) one_dev &= bases[i]->dev == bases[0]->dev;
+  void* d_w = nullptr;
+  if (one_dev && n > 1) {
+    HIPCHK(hipSetDevice(bases[0]->dev));
+    if (hipMallocAsync(&d_w, 8ull * V, kBuildStream) == hipSuccess) {
+      const hipError_t e1 = hipMemcpyAsync(d_w, wts.wt.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream);
+      const hipError_t e2 = hipMemcpyAsync(static_cast<float*>(d_w) + V, wts.wn.data(), 4ull * V, hipMemcpyHostToDevice,
+                                           kBuildStream);
+      const hipError_t e3 = hipStreamSynchronize(kBuildStream);
+      if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+        (void)hipFreeAsync(d_w, kBuildStream);
+        return fail(FG_EHIP, "rescore weights upload: %s", hipGetErrorString(e1 ? e1 : e2 ? e2 : e3));
+      }
+      wts.d_w = static_cast<const float*>(d_w);
+      wts.dev = bases[0]->dev;
+    } else {
+      (void)hipGetLastError();
+      d_w = nullptr;  // each snapshot uploads its own
+    }
+  }
   std::vector<int> rc(n, FG_OK);
   std::vector<std::string> err(n);
   std::atomic<uint32_t> next{0};
@@ -1437,6 +1465,15 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
   for (uint32_t t = 1; t < std::min<uint32_t>(n, 8); ++t) th.emplace_back(worker);
   worker();
   for (auto& x : th) x.join();
+  bool any_fail = false;
+  for (uint32_t i = 0; i < n; ++i) any_fail |= rc[i] != FG_OK;
+  if (d_w) {
+    // a successful scoring waited for its kernels (its read-back); a failed one
+    // may have left some reading the weights
+    (void)hipSetDevice(wts.dev);
+    if (any_fail) (void)hipDeviceSynchronize();
+    (void)hipFreeAsync(d_w, kBuildStream);
+  }
   for (uint32_t i = 0; i < n; ++i)
     if (rc[i]) {
       for (uint32_t j2 = 0; j2 < n; ++j2)

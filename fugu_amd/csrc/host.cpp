@@ -1685,13 +1685,46 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     }
   }
   tr.mark("rescore merged segment");
-  // ---- swap: no commit runs meanwhile
-  std::lock_guard<std::mutex> c(ns.committer);
+  // ---- swap: no commit runs meanwhile.  A commit that landed since the last
+  // rescore changed the statistics (or deleted docs): the merged segment is
+  // rescored again OUTSIDE the committer lock and the swap retried, so a commit
+  // waits on a merge only for the swap itself; after kSwapTries the rescore
+  // runs under the lock (commits arriving faster than one rescore).
+  constexpr int kSwapTries = 3;
+  std::unique_lock<std::mutex> c(ns.committer);
   tr.mark("wait for the committer");
   std::shared_ptr<Snapshot> now;
-  {
-    std::shared_lock<std::shared_mutex> l(ns.snap_mu);
-    now = ns.snap;
+  std::vector<uint8_t> del, mdel(ids.size(), 0);
+  bool moved = false, new_del = false;
+  for (int attempt = 1;; ++attempt) {
+    {
+      std::shared_lock<std::shared_mutex> l(ns.snap_mu);
+      now = ns.snap;
+    }
+    {
+      std::lock_guard<std::mutex> w(ns.writer);
+      uint64_t ver = 0;
+      refresh(ver, mdel);
+      moved = ver != ver_used;  // a commit since the last rescore: other statistics
+      new_del = mdel != mdel_used;
+      del = ns.del;
+      if (mix && (moved || new_del) && attempt < kSwapTries) {
+        ver_used = ver;
+        mdel_used = mdel;
+      }
+    }
+    if (!mix || !(moved || new_del) || attempt >= kSwapTries) break;
+    c.unlock();
+    const fg_global_stats g1 = S.global();
+    const bool any_del = std::find(mdel_used.begin(), mdel_used.end(), 1) != mdel_used.end();
+    fg_index* re = nullptr;
+    const int rc = fg_index_rescore(mix, &g1, any_del ? mdel_used.data() : nullptr, &re);
+    fg_index_release(mix);
+    if (rc) return hfail(rc, fg_last_error());
+    mix = re;
+    tr.mark("rescore merged segment (a commit landed)");
+    c.lock();
+    tr.mark("wait for the committer");
   }
   size_t j0 = now->segs.size();
   for (size_t j = 0; j < now->segs.size(); ++j)
@@ -1701,16 +1734,6 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
   if (!same) {  // only the merger removes segments: cannot happen
     if (mix) fg_index_release(mix);
     return hfail(FG_EINVAL, "merge sources vanished from the snapshot");
-  }
-  std::vector<uint8_t> del, mdel(ids.size(), 0);
-  bool moved = false, new_del = false;
-  {
-    std::lock_guard<std::mutex> w(ns.writer);
-    uint64_t ver = 0;
-    refresh(ver, mdel);
-    moved = ver != ver_used;  // a commit since the pre-swap rescore: other statistics
-    new_del = mdel != mdel_used;
-    del = ns.del;
   }
   const fg_global_stats g = S.global();
   if (mix && (moved || new_del)) {

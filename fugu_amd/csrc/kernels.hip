@@ -561,9 +561,10 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
   // as every thread last saw it (uniform), so the skip is uniform too.
   const float* __restrict__ cmax = ix.cmax + ix.coff[t0];
   uint64_t thr_k = thr0;
-  // pure conjunctions (a multi-snapshot plan's instantiation without them when
-  // FG_MULTI_DEFER=0: it then fits 128 VGPRs without scratch)
-  const bool defer = !kSingle && (FG_MULTI_DEFER || !kMulti) && kDeferCap > 0 && m >= 3 && nm == m && !fmask;
+  // pure conjunctions (the multi-snapshot instantiation too: without deferred
+  // probes it fits 128 VGPRs with no scratch, but C4 ran 1.44 -> 1.57 ms,
+  // profiles/r04/ab/ab_multi_defer_c4.log)
+  const bool defer = !kSingle && kDeferCap > 0 && m >= 3 && nm == m && !fmask;
 
   for (uint32_t cc = 0; cc < nc; ++cc) {
     const uint32_t c = c0 + cc;
