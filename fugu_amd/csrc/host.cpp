@@ -23,6 +23,7 @@
 #include <string_view>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/fugu.h"
@@ -746,6 +747,10 @@ struct Namespace {
   // Doc records (a vector's reallocation moved all 10M of them inside a commit)
   std::deque<Doc> docs;
   std::vector<uint8_t> del;                            // del[d] == docs[d].deleted (commits copy this, not the docs)
+  // docs deleted by upserts since the last commit, in order: a delete takes
+  // effect at the commit (IndexWriter::delete_term), so a merge in between
+  // neither drops them nor flags them (committed_del)
+  std::vector<uint32_t> pend_del;
   bool any_name = false;                               // some doc has a name field
   TermDict dict;                                       // term dictionary (text and name tokens)
   std::unordered_map<std::string, uint32_t> fdict;     // facet dictionary (encoded facet terms)
@@ -1262,6 +1267,7 @@ int upsert_record(fg_db* db, const char* nsname, const fg_object_record* r, cons
   auto it = ns->by_id_token.find(sid);
   if (it != ns->by_id_token.end())
     for (uint32_t d : it->second) {
+      if (!ns->del[d]) ns->pend_del.push_back(d);
       ns->docs[d].deleted = true;
       ns->del[d] = 1;
     }
@@ -1494,6 +1500,7 @@ int commit_segment(fg_db* db, Namespace& ns) {
   st->df_f = sparse_of(dfc);
   const bool any_name = ns.any_name;
   const std::vector<uint8_t> del(ns.del.begin(), ns.del.begin() + N);
+  const size_t n_pend = ns.pend_del.size();  // committed by this commit
   Stats S;
   S.load(ns, n_terms, n_fterms);
   S.add(*st, false);
@@ -1531,6 +1538,7 @@ int commit_segment(fg_db* db, Namespace& ns) {
     prev = std::move(ns.snap);
     ns.snap = snap;
     ns.committed_docs = N;
+    ns.pend_del.erase(ns.pend_del.begin(), ns.pend_del.begin() + n_pend);
     S.store(ns);
   }
   cur.reset();
@@ -1606,9 +1614,11 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     n_terms = std::max<uint32_t>(1, (uint32_t)ns.dict.size());
     n_fterms = (uint32_t)ns.fdict.size();
     std::vector<uint32_t> dt(n_terms, 0), dn(n_terms, 0), dfc(n_fterms, 0), scratch;
+    const std::unordered_set<uint32_t> pend(ns.pend_del.begin(), ns.pend_del.end());
+    auto gone = [&](uint32_t g) { return ns.del[g] && !pend.count(g); };  // a committed deletion
     for (const Segment& sg : src) {
       bool has_del = false;
-      for (uint32_t d = 0; d < sg.n && !has_del; ++d) has_del = ns.del[sg.global(d)] != 0;
+      for (uint32_t d = 0; d < sg.n && !has_del; ++d) has_del = gone(sg.global(d));
       if (!has_del) {
         mst->tot[0] += sg.st->tot[0];
         mst->tot[1] += sg.st->tot[1];
@@ -1617,7 +1627,7 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
       for (uint32_t d = 0; d < sg.n; ++d) {
         const uint32_t gd = sg.global(d);
         const Doc& doc = ns.docs[gd];
-        if (doc.deleted) continue;
+        if (gone(gd)) continue;
         ids.push_back(gd);
         buf.add(doc, false);
         mst->n++;
@@ -1668,6 +1678,10 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
       S.add(*mst, false);
     }
     for (size_t i = 0; i < ids.size(); ++i) md[i] = ns.del[ids[i]];
+    for (uint32_t g : ns.pend_del) {  // not committed yet
+      const auto it = std::lower_bound(ids.begin(), ids.end(), g);
+      if (it != ids.end() && *it == g) md[it - ids.begin()] = 0;
+    }
   };
   if (mix) {
     {
@@ -1708,6 +1722,7 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
       moved = ver != ver_used;  // a commit since the last rescore: other statistics
       new_del = mdel != mdel_used;
       del = ns.del;
+      for (uint32_t g : ns.pend_del) del[g] = 0;  // committed deletions only
       if (mix && (moved || new_del) && attempt < kSwapTries) {
         ver_used = ver;
         mdel_used = mdel;
@@ -2029,9 +2044,10 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
       auto it = ns->by_id_token.find(docs[i].id);
       if (it != ns->by_id_token.end())
         for (uint32_t d : it->second) {
-      ns->docs[d].deleted = true;
-      ns->del[d] = 1;
-    }
+          if (!ns->del[d]) ns->pend_del.push_back(d);
+          ns->docs[d].deleted = true;
+          ns->del[d] = 1;
+        }
       const uint32_t d = (uint32_t)ns->docs.size();
       for (auto& t : docs[i].id_tokens) ns->by_id_token[t].push_back(d);
       ns->del.push_back(0);

@@ -126,3 +126,52 @@ def test_rescore_many_equals_one_by_one(native, ctx, parts):
         q_off, terms = synth.queries(256, m0, m1, seed_q=123)
         for x, y in zip(many, one):
             same(x.search_batch(q_off, terms, k, mode=mode), y.search_batch(q_off, terms, k, mode=mode), (m0, k, mode))
+
+
+def test_rescore_shares_structure_and_leaves_base_intact(native, ctx, parts):
+    """A rescore shares its base's host structure (copy-on-write: the f32
+    table slots it drops stay in the base) and reads its per-term maxima into
+    the structure's pooled pinned blocks: the base answers as before while and
+    after rescores come and go, and a rescore in a recycled block answers like
+    the first one."""
+    import os
+
+    from fugu_amd import synth
+    c, cut, (ao, at), (bo, bt) = parts
+    V = synth.VOCAB
+    g = native.docs_stats(ao, at, V, threads=16) + native.docs_stats(bo, bt, V, threads=16)
+    env = {"FUGU_RANK_GIB": "0.02", "FUGU_DENSE_GIB": "0.05"}  # f32 tables for dense terms past the rank budget
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        base = native.Index.from_docs(ctx, ao, at, V, threads=16)
+        fresh = native.Index.from_docs(ctx, ao, at, V, threads=16, global_stats=g)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert base.stats().n_dense_f32 > 0
+    cases = [(3, 3, 100, native.MODE_AND), (2, 5, 1000, native.MODE_OR)]
+    qs = [synth.queries(256, m0, m1, seed_q=31) for (m0, m1, _, _) in cases]
+    before = [base.search_batch(q_off, terms, k, mode=mode) for (q_off, terms), (_, _, k, mode) in zip(qs, cases)]
+    kth = np.stack([base.term_kth(t) for t in (0, 7, 300)])
+    first = None
+    for rnd in range(3):  # rounds 2 and 3 reuse the blocks released by the previous rescore
+        re = base.rescore(g)
+        assert re.stats().n_dense_f32 == 0  # a rescore drops the f32 tables (its own probe kinds)
+        got = [re.search_batch(q_off, terms, k, mode=mode) for (q_off, terms), (_, _, k, mode) in zip(qs, cases)]
+        for x, (q_off, terms), (_, _, k, mode) in zip(got, qs, cases):
+            same(x, fresh.search_batch(q_off, terms, k, mode=mode), ("rescore vs fresh", rnd, k, mode))
+        if first is None:
+            first = got
+        for x, y in zip(got, first):
+            same(x, y, ("rescore in a recycled block", rnd))
+        re.close()
+        for x, y, cs in zip(before, [base.search_batch(q_off, terms, k, mode=mode)
+                                     for (q_off, terms), (_, _, k, mode) in zip(qs, cases)], cases):
+            same(x, y, ("base after rescore", rnd, cs))
+        assert np.array_equal(np.stack([base.term_kth(t) for t in (0, 7, 300)]), kth)
+    base.close()
+    fresh.close()

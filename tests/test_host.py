@@ -783,6 +783,127 @@ def test_db_search_during_background_merge(db, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_db_commits_during_background_merge(db, monkeypatch):
+    """Commits that land while a merge is in flight (FUGU_MERGE_DELAY_MS holds it
+    between its build and its swap) change the statistics and delete docs of the
+    merge's sources: the merger rescores the merged segment with them outside the
+    committer lock (again if another commit slips in) and swaps it in.  The
+    namespace then answers like the oracle over [merged, the new segments], the
+    merged segment keeping the docs alive at its gather (later deletions are
+    flags, as in a tantivy segment)."""
+    import threading
+    import time
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    monkeypatch.setenv("FUGU_MERGE_DELAY_MS", "1500")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("bgc")
+    recs = build_corpus(29, 1000)
+    for c in range(0, 1000, 100):
+        for rid, t, meta in recs[c:c + 100]:
+            d.upsert(db.ObjectRecord(rid, t, metadata=meta), "bgc")
+        d.commit("bgc")  # commits 9 and 10 land while the merge of the first eight sleeps
+        if c == 700:
+            assert d.merge_info("bgc")["pending"] == 1
+            time.sleep(0.3)  # the merger has gathered its run (its build then sleeps 1.5 s)
+    assert d.merge_info("bgc")["merges"] == 0  # commits 9 and 10 came before the swap
+    t = threading.Thread(target=d.merge_wait, args=("bgc",))
+    t.start()
+    t.join(60)
+    length = [len(py_analyze(x)) for _, x, _ in recs]
+    nlen = [len(py_analyze(m["name"])) if m and isinstance(m.get("name"), str) else 0 for _, _, m in recs]
+    dele0 = deleted_of(recs[:800])  # the deletions the merge's gather saw
+    merged, tot = [], [0, 0]
+    for c in range(0, 800, 100):
+        alive = [g for g in range(c, c + 100) if not dele0[g]]
+        merged += alive
+        for f, ln in ((0, length), (1, nlen)):
+            tot[f] += sum(ln[c:c + 100]) if len(alive) == 100 else sum(quantized(ln[g]) for g in alive)
+    for f, ln in ((0, length), (1, nlen)):
+        tot[f] += sum(ln[800:1000])
+    assert len(merged) < 800 and any(deleted_of(recs)[g] for g in merged)  # later commits deleted merged docs
+    assert d.segments("bgc") == [merged, list(range(800, 900)), list(range(900, 1000))]
+    info = d.merge_info("bgc")
+    assert info["merges"] == 1 and info["n_docs_stats"] == len(merged) + 200 and info["tot_tokens"] == tot, info
+    keep = merged + list(range(800, 1000))
+    bounds = [0, len(merged), len(merged) + 100, len(merged) + 200]
+    ix, dic = oracle_of(recs, keep)
+    for f in (0, 1):
+        ix.set_total_tokens(f, tot[f])
+    rng = random.Random(8)
+    for _ in range(32):
+        ws = [rng.choice(WORDS) for _ in range(rng.randint(1, 3))]
+        q = " AND ".join(ws) if rng.random() < 0.5 else " ".join(ws)
+        mode = 1 if (len(ws) > 1 and " AND " not in q) else 0
+        got = d.search("bgc", q, 0, 20)
+        terms = [dic.get(py_analyze(w)[0], native.FG_TERM_MISSING) for w in ws]
+        s, dd = ix.search_segments(np.array(terms, np.uint32), 20, bounds, mode=mode)
+        assert hits_of([g[0] for g in got], [g[1] for g in got]) == [[keep[x], b] for x, b in hits_of(s, dd)], q
+
+
+@pytest.mark.gpu
+def test_db_uncommitted_delete_survives_a_merge(db, monkeypatch):
+    """An upsert's delete takes effect at the next commit (IndexWriter::delete_term
+    + commit, src/db/document.rs:38-65): a merge that swaps in between neither
+    drops nor flags the doc, so searches keep finding it until the commit."""
+    import threading
+    import time
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    monkeypatch.setenv("FUGU_MERGE_DELAY_MS", "800")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("ud")
+    recs = build_corpus(41, 800)
+    for c in range(0, 800, 100):
+        for rid, t, meta in recs[c:c + 100]:
+            d.upsert(db.ObjectRecord(rid, t, metadata=meta), "ud")
+        d.commit("ud")
+    assert d.merge_info("ud")["pending"] == 1
+    time.sleep(0.3)  # the merger has gathered its run
+    dele = deleted_of(recs)
+    # an alive doc whose id is its own token (lowercase alphanumeric): re-upserting that id deletes it
+    x = next(g for g in range(100, 800) if not dele[g] and recs[g][0].isalnum() and recs[g][0].islower()
+             and py_analyze(recs[g][0]) == [recs[g][0]])
+    word = py_analyze(recs[x][1])[0]
+    d.upsert(db.ObjectRecord(recs[x][0], "qqqzz"), "ud")  # deletes doc x -- not committed
+    t = threading.Thread(target=d.merge_wait, args=("ud",))
+    t.start()
+    t.join(60)
+    assert d.merge_info("ud")["merges"] == 1 and len(d.segments("ud")) == 1
+    assert x in d.segments("ud")[0]
+
+    def found(q):
+        hits = []
+        for page in range(0, 400):
+            got = d.search("ud", q, page, 20)
+            if not got:
+                return hits
+            hits += [int(g[1]) for g in got]
+        return hits
+    # the merged snapshot still holds doc x alive; the oracle over the committed docs agrees
+    keep = d.segments("ud")[0]
+    ix, dic = oracle_of(recs, keep)
+    length = [len(py_analyze(r[1])) for r in recs]
+    nlen = [len(py_analyze(m["name"])) if m and isinstance(m.get("name"), str) else 0 for _, _, m in recs]
+    for f, ln in ((0, length), (1, nlen)):
+        tot = 0
+        for c in range(0, 800, 100):
+            alive = [g for g in range(c, c + 100) if not dele[g]]
+            tot += sum(ln[c:c + 100]) if len(alive) == 100 else sum(quantized(ln[g]) for g in alive)
+        ix.set_total_tokens(f, tot)
+    got = d.search("ud", word, 0, 20)
+    s, dd = ix.search_segments(np.array([dic[word]], np.uint32), 20, [0, len(keep)], mode=0)
+    assert hits_of([g[0] for g in got], [g[1] for g in got]) == [[keep[i], b] for i, b in hits_of(s, dd)]
+    assert x in found(word)
+    d.commit("ud")  # now the delete takes effect
+    assert x not in found(word)
+
+
+@pytest.mark.gpu
 def test_db_failed_commit_leaves_statistics_unchanged(db, monkeypatch):
     """A commit whose device build fails (injected) changes nothing: the next
     commit counts the same docs once, so scores equal the oracle's."""
