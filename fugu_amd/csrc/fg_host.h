@@ -285,10 +285,11 @@ struct WsPool {
 // them (a pageable copy is staged by the runtime and synchronises on the way),
 // which takes ~tens of us off a batch-of-one search.
 struct PinnedPool {
-  static constexpr size_t kKeep = 16ull << 20;
+  const size_t kKeep;  // bytes kept cached
   std::mutex mu;
   std::multimap<size_t, void*> free_bufs;
   size_t cached = 0;
+  explicit PinnedPool(size_t keep = 16ull << 20) : kKeep(keep) {}
   void* get(size_t bytes, size_t* got) {
     {
       std::lock_guard<std::mutex> l(mu);
@@ -327,7 +328,9 @@ struct PinnedLease {
   PinnedPool& pool;
   void* p = nullptr;
   size_t n = 0;
-  PinnedLease(PinnedPool& pl, size_t bytes) : pool(pl) { p = pool.get(bytes, &n); }
+  PinnedLease(PinnedPool& pl, size_t bytes) : pool(pl) {
+    if (bytes) p = pool.get(bytes, &n);
+  }
   ~PinnedLease() { if (p) pool.put(p, n); }
 };
 }  // namespace fgh
@@ -379,6 +382,8 @@ struct fg_index {
                  *d_bk_e1 = nullptr, *d_kt_terms = nullptr, *d_kt_tiny = nullptr;
   const uint64_t *d_sc_e0 = nullptr, *d_sc_e1 = nullptr;
   uint32_t n_scb = 0, n_ktiny = 0;  // k_score chunks; k_ktop_tiny terms
+  const uint32_t* d_tterm = nullptr;  // tile-table terms in toff order (k_tsub)
+  uint32_t n_tterm = 0, n_tiles = 0;
   // k_ktop's tables (structure): long terms, their first chunk, each chunk's term and first posting
   const uint32_t *d_kb_terms = nullptr, *d_kb_chunk0 = nullptr, *d_kc_big = nullptr, *d_kc_start = nullptr;
   uint32_t n_sc = 0, n_bk = 0, n_kt = 0, n_kbig = 0, n_kchunks = 0;

@@ -148,6 +148,21 @@ __host__ __device__ inline uint32_t rank_pos(uint64_t x, uint32_t d) {
 #endif
 }
 
+// u8 bounds of a score range [0, M] (k_disj's sub-tile maxima): a score s as
+// the least q with q8_bound(q, M) >= s; q8_bound(255, M) = M covers every
+// rounding.  The kernels compute q8_bound with the same f32 operations
+// (-ffp-contract=off), so the bound holds bit for bit.
+__host__ __device__ inline float q8_step(float M) { return M * (1.0f / 255.0f); }
+__host__ __device__ inline float q8_bound(uint32_t q, float M) { return q >= 255u ? M : (float)q * q8_step(M); }
+__host__ __device__ inline uint32_t quant8(float s, float M) {
+  const float st = q8_step(M);
+  if (!(st > 0.0f) || !(s < M)) return 255u;
+  uint32_t q = (uint32_t)fminf(254.0f, ceilf(s / st));
+  while (q < 255u && q8_bound(q, M) < s) ++q;
+  return q;
+}
+constexpr uint32_t kSubShift = 9;  // 512-doc blocks: 8 per k_disj tile
+
 // tmeta of a term: bits 0-7 = B_t (bucket shift), 8-15 = S_t (search steps),
 // 16-30 = dense slot + 1 (0: none), bit 31 = the slot's kind (1: rank words, 0: f32 table)
 __host__ __device__ inline uint32_t meta_slot(uint32_t meta) { return (meta >> 16) & 0x7FFFu; }
@@ -189,6 +204,9 @@ struct DevIndex {
   const uint32_t* toff;      // [V] first tmax / tdir entry of each term (n_tiles + 1 per term), or
                              //     0xFFFFFFFF (bucket >= tile: use bmax)
   const uint32_t* tdir;      // tile directory: tdir[toff[t] + i] = first posting of t at doc >= i << kDisjTileShift
+  const uint64_t* tsub;      // parallel to tmax: byte b = the largest posting score among the tile's docs
+                             //     [b << kSubShift, (b + 1) << kSubShift) quantized up against the tile maximum
+                             //     (q8_bound); a bucket wider than a block counts in every block it covers
   const float* cmax;         // [score chunks] largest posting score of each kChunk-posting chunk of a
                              //     list (block-max: k_conj skips a lead chunk that cannot reach the threshold)
   const uint32_t* coff;      // [V] index of each term's first chunk in cmax
@@ -322,6 +340,10 @@ struct ScoreJob {
   float* bmax;                // [D] out
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
+  uint64_t* tsub;             // [tiles] out (k_tsub)
+  const uint32_t* tterm;      // [tile-table terms] the term of each n_tiles + 1 tile entries, in toff order
+  uint32_t n_tterm;           // tile-table terms
+  uint32_t n_tiles;           // tiles per term (4096-doc k_disj tiles)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
   float* cmax;                // [cmax entries] out: the largest score of each kChunk postings of a term
   const uint32_t* coff;       // [V] first cmax entry of each term
@@ -370,6 +392,7 @@ hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uin
                        uint32_t n_words, uint64_t* out, hipStream_t s);
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);  // packed chunks
+hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s);                        // after k_bucket
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,

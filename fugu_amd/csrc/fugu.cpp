@@ -192,7 +192,33 @@ namespace {
 // commit's rescores of the older segments, its new segment's build and the
 // background merger's build run side by side.  Uploads are synchronous with
 // the host (the sources may be freed right after).
-const hipStream_t kBuildStream = hipStreamPerThread;
+// (a thread may point it at another stream: fg_index_rescore_many's workers
+// use low-priority ones, so a commit's new segment and the searches running
+// beside its rescores are dispatched first)
+thread_local hipStream_t tl_build_stream = hipStreamPerThread;
+#define kBuildStream tl_build_stream
+
+// low-priority streams of a device for background rescoring, created once
+hipStream_t low_priority_stream(int dev, uint32_t i) {
+  static std::mutex mu;
+  static std::map<int, std::vector<hipStream_t>> streams;
+  constexpr uint32_t kN = 8;
+  std::lock_guard<std::mutex> l(mu);
+  auto& v = streams[dev];
+  if (v.empty()) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    for (uint32_t j = 0; j < kN; ++j) {
+      hipStream_t st = nullptr;
+      if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least) != hipSuccess) {
+        (void)hipGetLastError();
+        st = nullptr;
+      }
+      v.push_back(st);
+    }
+  }
+  return v[i % kN];
+}
 
 template <class T>
 int dev_upload(DevAllocs& m, const T* src, size_t n, T** out, uint64_t* bytes) {
@@ -224,16 +250,45 @@ struct UploadBatch {
     void* p = nullptr;
     if (hipMalloc(&p, std::max<size_t>(total, 256)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", total);
     m.ptrs.push_back(p);
+    // the arrays laid out in a pooled pinned staging buffer by all host threads,
+    // then ONE copy: a small segment's arrays are sized by the vocabulary (~40 MB
+    // for 2^20 terms), and pageable copies of them -- staged by the runtime,
+    // beside a commit's rescores -- took ~16 ms of a 1000-doc segment's build
+    // (a bulk build's arrays are larger than the pool keeps: pageable copies)
+    PinnedLease pin(stage_pool(), total <= kStageMax ? total : 0);
+    if (pin.p && total <= kStageMax) {
+      struct Piece { char* dst; const char* src; size_t n; };
+      std::vector<Piece> pieces;
+      size_t o = 0;
+      for (const E& e : es) {
+        for (size_t b = 0; b < e.bytes; b += kStagePiece)
+          pieces.push_back(Piece{static_cast<char*>(pin.p) + o + b, static_cast<const char*>(e.src) + b,
+                                 std::min(kStagePiece, e.bytes - b)});
+        o += (std::max<size_t>(e.bytes, 16) + 16 + 255) & ~size_t(255);
+      }
+      parallel_dynamic((uint32_t)pieces.size(), std::min<int>(hw_threads(0), (int)pieces.size()), 1,
+                       [&](int, uint32_t b, uint32_t e) {
+        for (uint32_t i = b; i < e; ++i) std::memcpy(pieces[i].dst, pieces[i].src, pieces[i].n);
+      });
+      HIPCHK(hipMemcpyAsync(p, pin.p, total, hipMemcpyHostToDevice, kBuildStream));
+    }
     size_t o = 0;
     for (const E& e : es) {
       char* d = static_cast<char*>(p) + o;
-      if (e.bytes) HIPCHK(hipMemcpyAsync(d, e.src, e.bytes, hipMemcpyHostToDevice, kBuildStream));
+      if (!(pin.p && total <= kStageMax) && e.bytes) HIPCHK(hipMemcpyAsync(d, e.src, e.bytes, hipMemcpyHostToDevice, kBuildStream));
       *e.out = d;
       o += (std::max<size_t>(e.bytes, 16) + 16 + 255) & ~size_t(255);
     }
     HIPCHK(hipStreamSynchronize(kBuildStream));
     *bytes += total;
     return FG_OK;
+  }
+  static constexpr size_t kStagePiece = 1u << 20;
+  static constexpr size_t kStageMax = 128ull << 20;
+  // process-wide: builds run on many threads (a commit's builder, the merger)
+  static PinnedPool& stage_pool() {
+    static PinnedPool pool(256ull << 20);
+    return pool;
   }
 };
 
@@ -314,6 +369,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   // same structure gets a released snapshot's block back: ScorePool)
   struct Part { size_t bytes; void** out; };
   float *d_wt, *d_wn, *d_cache, *d_psc, *d_bmax, *d_ktop, *d_cmax;
+  uint64_t* d_tsub = nullptr;
   uint32_t *d_alive = nullptr, *d_tmaxs, *d_tmax;
   const Part parts[] = {
       {4ull * V, reinterpret_cast<void**>(&d_wt)},
@@ -326,6 +382,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       {4ull * ix->tile_entries, reinterpret_cast<void**>(&d_tmax)},
       {4ull * V * fg::kNumTopK, reinterpret_cast<void**>(&d_ktop)},
       {4ull * ix->n_sc, reinterpret_cast<void**>(&d_cmax)},
+      {8ull * ix->tile_entries, reinterpret_cast<void**>(&d_tsub)},
   };
   size_t total = 0;
   for (const Part& pt : parts) total += (std::max<size_t>(pt.bytes, 16) + 255) & ~size_t(255);
@@ -394,6 +451,11 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.coff = ix->d.coff;
   HIPCHK(fg::launch_score(j, ix->n_scb, kBuildStream));
   HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
+  j.tsub = d_tsub;
+  j.tterm = ix->d_tterm;
+  j.n_tterm = ix->n_tterm;
+  j.n_tiles = ix->n_tiles;
+  HIPCHK(fg::launch_tsub(j, ix->n_docs, kBuildStream));
   // k_ktop: terms of <= kKtopChunk postings one workgroup each; longer terms in
   // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
   // chunks' best keys (k_ktop_big).  The chunk tables are the structure's; the
@@ -501,6 +563,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
+  ix->d.tsub = d_tsub;
   ix->d.cmax = d_cmax;
   ix->d.alive = d_alive;
   ix->d.dense = d_dense;
@@ -595,6 +658,10 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       ntm += n_tiles + 1;
     }
   std::vector<uint32_t> tdir(ntm);
+  std::vector<uint32_t> tterm;  // the tile-table terms in toff order (k_tsub)
+  tterm.reserve(ntm / (n_tiles + 1));
+  for (uint32_t t = 0; t < V; ++t)
+    if (toff[t] != 0xFFFFFFFFu) tterm.push_back(t);
   parallel_dynamic(V, hw_threads(0), 64, [&](int, uint32_t tb, uint32_t te) {
     for (uint32_t t = tb; t < te; ++t) {
       if (toff[t] == 0xFFFFFFFFu) continue;
@@ -715,7 +782,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   DevAllocs& sm = *ix->smem;
   uint64_t& bytes = ix->struct_bytes;
   int rc;
-  uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc;
+  uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc, *d_tterm;
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
   uint32_t *d_sctf, *d_sctl, *d_bktf, *d_bktl, *d_bke0, *d_bke1, *d_kt, *d_ktt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs;
@@ -731,6 +798,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ub.add(dir_off.data(), dir_off.size(), &d_dir_off);
     ub.add(toff.data(), toff.size(), &d_toff);
     ub.add(tdir.data(), tdir.size(), &d_tdir);
+    ub.add(tterm.data(), tterm.size(), &d_tterm);
     ub.add(hp.fdoc.data(), hp.fdoc.size(), &d_fdoc);
     ub.add(hp.foff.data(), hp.foff.size(), &d_foff);
     ub.add(sc_tf.data(), sc_tf.size(), &d_sctf);
@@ -837,6 +905,9 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d_bk_e1 = d_bke1;
   ix->d_kt_tiny = d_ktt;
   ix->n_ktiny = (uint32_t)kt_tiny.size();
+  ix->d_tterm = d_tterm;
+  ix->n_tterm = (uint32_t)tterm.size();
+  ix->n_tiles = (uint32_t)n_tiles;
   ix->d_kt_terms = d_kt;
   ix->d_kb_terms = d_kbt;
   ix->d_kb_chunk0 = d_kb0;
@@ -1375,6 +1446,9 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->d_bk_e1 = base->d_bk_e1;
   ix->d_kt_tiny = base->d_kt_tiny;
   ix->n_ktiny = base->n_ktiny;
+  ix->d_tterm = base->d_tterm;
+  ix->n_tterm = base->n_tterm;
+  ix->n_tiles = base->n_tiles;
   ix->d_kt_terms = base->d_kt_terms;
   ix->d_kb_terms = base->d_kb_terms;
   ix->d_kb_chunk0 = base->d_kb_chunk0;
@@ -1457,9 +1531,16 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
   std::vector<int> rc(n, FG_OK);
   std::vector<std::string> err(n);
   std::atomic<uint32_t> next{0};
+  std::atomic<uint32_t> slot{0};
   auto worker = [&] {
-    for (uint32_t i; (i = next.fetch_add(1)) < n;)
+    const hipStream_t saved = tl_build_stream;
+    for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+      const int dev = bases[i]->dev;
+      if (hipSetDevice(dev) == hipSuccess)
+        if (hipStream_t st = low_priority_stream(dev, slot.fetch_add(1))) tl_build_stream = st;
       if ((rc[i] = rescore_one(bases[i], g, deleted ? deleted[i] : nullptr, &outs[i], &wts))) err[i] = fg_last_error();
+      tl_build_stream = saved;
+    }
   };
   std::vector<std::thread> th;
   for (uint32_t t = 1; t < std::min<uint32_t>(n, 8); ++t) th.emplace_back(worker);

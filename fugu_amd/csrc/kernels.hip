@@ -895,15 +895,18 @@ struct DisjShared {
     // hold its rescoring candidates, (maybe-mask << kRelBits + 4) | (clause <<
     // kRelBits) | doc offset (kRelBits: 17 for 32-tile items)
     uint64_t q[kQCap];
-    float cs[kPairs];              // P: per-(candidate, clause) term scores
+    union {                        // never live together: rescoring, then the truncation after it
+      float cs[kPairs];            // P: per-(candidate, clause) term scores
+      uint32_t hist[1u << kDisjHistBits];  // truncate_keys' select bins
+    };
     uint32_t seg_start[kMaxSeg];   // P: prefix of the essential segments' lengths
   } p;
-  uint32_t hist[1u << kDisjHistBits];
   uint32_t scratch[8];
   // R: per (tile, clause) ranges and bounds, index t * m + i
   uint32_t r_lo[kMaxSeg], r_hi[kMaxSeg];
   float r_ub[kMaxSeg];
-  uint32_t t_ess[kMaxTiles];         // essential-clause mask per tile
+  uint16_t b_ess[kMaxTiles * 8];     // S: essential-clause mask per 512-doc block
+  uint32_t t_ess[kMaxTiles];         // essential-clause mask per tile (the union of its blocks')
   uint32_t t_post[kMaxTiles];        // 1: the tile's essential postings are streamed, 0: skipped
   uint16_t seg_info[kMaxSeg];        // P: (tile << 4) | clause of each segment
   // per-clause constants of the work item's query
@@ -919,6 +922,12 @@ struct DisjShared {
 
 __device__ inline bool doc_alive(const DevIndex& ix, uint32_t d) {
   return !ix.alive || ((ix.alive[d >> 5] >> (d & 31)) & 1u);
+}
+
+// a clause's bound over 512-doc block z of a tile: its sub-tile byte against the
+// tile bound M (-0.0, no posting in the tile: stays -0.0, adds nothing)
+__device__ inline float sub_bound(uint64_t sub, uint32_t z, float M) {
+  return q8_bound((uint32_t)(sub >> (8 * z)) & 0xFFu, M);
 }
 
 // The query's score histogram (DevPlan::hist) and its bin geometry.
@@ -967,7 +976,7 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
   }
   __syncthreads();
   uint64_t T = 0;
-  if (n > limit) T = truncate_keys<kBufD, kDisjHistBits>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
+  if (n > limit) T = truncate_keys<kBufD, kDisjHistBits>(sh.buf, &sh.n_buf, sh.p.hist, sh.scratch, n, K);
   if (threadIdx.x == 0) {
     const uint64_t mine = T > sh.thr ? T : sh.thr;
     // the exchange does not wait: the returned best is folded in when the
@@ -1127,6 +1136,42 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     sh.t_post[t] = (P < m && any) ? 1u : 0u;
   }
   __syncthreads();
+  static_assert(kMaxTiles * 8 <= kThreads, "one thread per (tile, block)");
+  // per 512-doc block (one thread per (tile, block)): the tile's non-essential
+  // clauses plus more of its essential ones, smallest tile bound first, while
+  // their block bounds (DevIndex::tsub) stay below the threshold together.  A
+  // doc of the block scoring >= the threshold matches a clause left essential
+  // there, whose tile segment is streamed; a posting of a clause not essential
+  // in its block is dropped once loaded.
+  if (tid < ntile * 8) {
+    const uint32_t t = tid >> 3, z = tid & 7u, tile = tile0 + t;
+    const uint32_t d0 = tile << kTileShift;
+    const uint64_t thr = sh.thr;
+    const float* ub = sh.r_ub + t * m;
+    const uint32_t ess = sh.t_ess[t];
+    auto bound = [&](uint32_t i) {
+      const uint32_t to = sh.c_toff[i];
+      return to != kInvalid ? sub_bound(ix.tsub[to + tile], z, ub[i]) : ub[i];
+    };
+    float sz = 0.0f;
+    for (uint32_t i = 0; i < m; ++i)
+      if (!((ess >> i) & 1u)) sz += bound(i);
+    uint32_t ez = ess, left = ess;
+    while (left) {
+      uint32_t c = __builtin_ctz(left);  // the remaining essential clause of the smallest tile bound
+      for (uint32_t r = left & (left - 1); r; r &= r - 1) {
+        const uint32_t i = __builtin_ctz(r);
+        if (ub[i] < ub[c]) c = i;
+      }
+      left &= ~(1u << c);
+      const float s2 = sz + bound(c);
+      if (make_key(inflate_bound(s2 + fmax), d0) >= thr) break;
+      sz = s2;
+      ez &= ~(1u << c);
+    }
+    sh.b_ess[tid] = (uint16_t)ez;
+  }
+  __syncthreads();
   FG_PHASE(1);
 #ifdef FG_DIAG
   if (tid == 0)
@@ -1248,6 +1293,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
           for (uint32_t i = 0; i < m; ++i)
             if (i != pcl[j]) ub += sh.r_ub[t * m + i];
           pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
+          pk[j] = pk[j] && ((sh.b_ess[(pd[j] - dbase) >> kSubShift] >> pcl[j]) & 1u);
           if (pk[j] && fmask) pk[j] = filter_bits(fmask, fshift, pd[j]) != 0;
 #ifdef FG_DIAG
           dg_b1 += pk[j] ? 1u : 0u;
@@ -1294,7 +1340,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         for (uint32_t i = 0; i < m; ++i)
           if (i != pcl[j]) ub += sh.r_ub[pt[j] * m + i];
         pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
-        ess[j] = sh.t_ess[pt[j]];
+        ess[j] = sh.b_ess[rel >> kSubShift];
       }
       // bound 2: every other clause at d, one clause at a time in clause order:
       // its rank word (presence bits + rank) and then the posting score, its
@@ -1482,7 +1528,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
               }
             }
             // unique keys: keep the doc only from the first essential clause it matches
-            const uint32_t first = (uint32_t)__builtin_ctz(matched & sh.t_ess[rel >> kTileShift]);
+            const uint32_t first = (uint32_t)__builtin_ctz(matched & sh.b_ess[rel >> kSubShift]);
             if (fmask) sc = sc + ftab[filter_bits(fmask, fshift, d)];
             key = make_key(sc, d);
             keep = first == src && key >= thr;
@@ -2165,6 +2211,44 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
     if (s_max[i]) atomicMax(&j.tmaxs[tf + i], s_max[i]);
 }
 
+// Sub-tile maxima (DevIndex::tsub): one thread per tile entry walks
+// the tile's buckets (bucket maxima from k_bucket, -0.0 = empty), takes the
+// largest per 512-doc block -- a bucket wider than a block counts in each block
+// it covers -- and quantizes them up against the tile maximum.  After k_bucket.
+static_assert(kDisjTileShift - kSubShift == 3, "8 sub-tile blocks per tile: one byte each of a u64");
+__global__ __launch_bounds__(kThreads) void k_tsub(ScoreJob j, uint32_t n_docs) {
+  const uint32_t nt1 = j.n_tiles + 1;
+  const uint64_t e = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= (uint64_t)j.n_tterm * nt1) return;
+  const uint32_t k = (uint32_t)(e / nt1), tile = (uint32_t)(e - (uint64_t)k * nt1);
+  if (tile >= j.n_tiles) {  // the entry past a term's last tile (tdir's end): never read as a tile
+    j.tsub[e] = ~0ull;
+    return;
+  }
+  const uint32_t t = j.tterm[k];
+  const uint32_t B = j.tmeta[t] & 0xFFu;  // <= kDisjTileShift for a tile-table term
+  const uint32_t nbk = (uint32_t)(((uint64_t)(n_docs - 1) >> B) + 1);
+  const uint32_t b0 = tile << (kDisjTileShift - B), b1 = min(nbk, (tile + 1) << (kDisjTileShift - B));
+  const float* bm = j.bmax + j.dir_off[t];
+  float mx[8];
+#pragma unroll
+  for (uint32_t z = 0; z < 8; ++z) mx[z] = 0.0f;
+  const uint32_t span = B > kSubShift ? 1u << (B - kSubShift) : 1u;  // blocks a bucket covers
+  for (uint32_t b = b0; b < b1; ++b) {
+    const float v = bm[b];
+    if (signbit(v)) continue;  // empty bucket
+    const uint32_t z0 = (((b - b0) << B) >> kSubShift);
+#pragma unroll
+    for (uint32_t z = 0; z < 8; ++z)
+      if (z >= z0 && z < z0 + span) mx[z] = fmaxf(mx[z], v);
+  }
+  const float M = __uint_as_float(j.tmax[e]);
+  uint64_t w = 0;
+#pragma unroll
+  for (uint32_t z = 0; z < 8; ++z) w |= (uint64_t)quant8(mx[z], M) << (8 * z);
+  j.tsub[e] = w;
+}
+
 // Per term the K-th best score over its ALIVE postings for K in kTopKs (0 when
 // fewer): a doc among a term's top K scores at least that much in any
 // disjunction containing the term, so the query's K-th best is >= it (k_disj's
@@ -2375,6 +2459,14 @@ hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s) {
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s) {
   if (!n_chunks) return hipSuccess;
   k_bucket<<<n_chunks, kThreads, 0, s>>>(j, n_docs);
+  return hipGetLastError();
+}
+
+hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s) {
+  const uint64_t n = (uint64_t)j.n_tterm * (j.n_tiles + 1);
+  if (!n || !j.tsub) return hipSuccess;
+  if ((n + kThreads - 1) / kThreads > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  k_tsub<<<(uint32_t)((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(j, n_docs);
   return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ using fgh::parallel_dynamic;
 
 namespace {
 
-enum Arr : uint32_t { A_DOC, A_PSC, A_RANK, A_DENSE, A_DIR, A_BMAX, A_TMAX, A_TDIR, A_CMAX, A_N };
+enum Arr : uint32_t { A_DOC, A_PSC, A_RANK, A_DENSE, A_DIR, A_BMAX, A_TMAX, A_TDIR, A_CMAX, A_TSUB, A_N };
 constexpr uint64_t kLine = 128;
 constexpr float kInflate = 1.00000762939453125f;  // kernels.hip inflate_bound: 1 + 2^-17
 
@@ -37,6 +37,7 @@ struct Snap {
   const fg_index* ix = nullptr;
   const uint32_t* doc = nullptr;
   std::vector<float> psc, tmax, bmax, cmax;
+  std::vector<uint64_t> tsub;
   std::vector<uint32_t> dir_off, toff, coff;
   uint64_t bytes[A_N] = {0};
   int load(const fg_index* x) {
@@ -49,6 +50,7 @@ struct Snap {
     toff.resize(V);
     coff.resize(V);
     tmax.resize(x->tile_entries);
+    tsub.assign(x->d.tsub ? x->tile_entries : 0, ~0ull);
     bmax.resize(x->dir_entries);
     cmax.resize(x->n_sc);
     auto rd = [](void* dst, const void* src, size_t n) -> hipError_t {
@@ -59,6 +61,7 @@ struct Snap {
     HIPCHK(rd(toff.data(), x->d.toff, 4 * V));
     HIPCHK(rd(coff.data(), x->d.coff, 4 * V));
     HIPCHK(rd(tmax.data(), x->d.tmax, 4 * tmax.size()));
+    HIPCHK(rd(tsub.data(), x->d.tsub, 8 * tsub.size()));
     HIPCHK(rd(bmax.data(), x->d.bmax, 4 * bmax.size()));
     HIPCHK(rd(cmax.data(), x->d.cmax, 4 * cmax.size()));
     bytes[A_DOC] = bytes[A_PSC] = 4 * P;
@@ -67,6 +70,7 @@ struct Snap {
     bytes[A_DIR] = bytes[A_BMAX] = 4 * x->dir_entries;
     bytes[A_TMAX] = bytes[A_TDIR] = 4 * x->tile_entries;
     bytes[A_CMAX] = 4ull * x->n_sc;
+    bytes[A_TSUB] = 8ull * tsub.size();
     return FG_OK;
   }
   uint64_t len(uint32_t t) const { return ix->off[t + 1] - ix->off[t]; }
@@ -254,7 +258,8 @@ uint64_t model_conj(const Snap& S, const uint32_t* terms, uint32_t m, bool has_t
 // One Should-only query (clauses in clause order, >= 2 present) as k_disj runs
 // it at the threshold: per (tile, clause) the posting range and bound (R), the
 // MaxScore split per tile (S), the essential clauses' postings (P) through
-// bound 1 (the other clauses' tile bounds) and bound 2 (every other clause at
+// bound 1 (the other clauses' tile bounds; a posting of a clause not essential
+// in its 512-doc block -- the block split over the sub-tile maxima -- dropped) and bound 2 (every other clause at
 // the doc: its rank word + posting score, or its bucket maximum); a doc whose
 // other clauses are all dense is exact there, any other is rescored by probing
 // every clause that may hold it.  Returns the keys formed at the threshold.
@@ -337,6 +342,41 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
       any |= hi[ord[j]] > lo[ord[j]] ? 1u : 0u;
     }
     if (P == m || !any) continue;
+    // the block split (k_disj's S phase, one thread per (tile, block)): the
+    // tile's non-essential clauses plus essential ones, smallest tile bound
+    // first, while their sub-tile bounds stay below the threshold together
+    uint32_t bess[8];
+    {
+      uint64_t sub[fg::kMaxTerms];
+      for (uint32_t c = 0; c < m; ++c) {
+        sub[c] = ~0ull;
+        if (B[c] <= TS && S.toff[t[c]] != 0xFFFFFFFFu && !S.tsub.empty()) {
+          const uint64_t to = (uint64_t)S.toff[t[c]] + ti;
+          A.gather(c, A_TSUB, to * 8, 8, A.stream);
+          sub[c] = S.tsub[to];
+        }
+      }
+      for (uint32_t z = 0; z < 8; ++z) {
+        auto bound = [&](uint32_t i) { return fg::q8_bound((uint32_t)(sub[i] >> (8 * z)) & 0xFFu, ub[i]); };
+        float sz = 0.0f;
+        for (uint32_t i = 0; i < m; ++i)
+          if (!((ess >> i) & 1u)) sz += bound(i);
+        uint32_t ez = ess, left = ess;
+        while (left) {
+          uint32_t cc = (uint32_t)__builtin_ctz(left);
+          for (uint32_t r = left & (left - 1); r; r &= r - 1) {
+            const uint32_t i = (uint32_t)__builtin_ctz(r);
+            if (ub[i] < ub[cc]) cc = i;
+          }
+          left &= ~(1u << cc);
+          const float s2 = sz + bound(cc);
+          if (key_of(s2 * kInflate, d0) >= thk) break;
+          sz = s2;
+          ez &= ~(1u << cc);
+        }
+        bess[z] = S.tsub.empty() ? ess : ez;
+      }
+    }
     // P: the essential clauses' postings
     for (uint32_t c = 0; c < m; ++c) {
       if (!((ess >> c) & 1u) || lo[c] >= hi[c]) continue;
@@ -353,6 +393,8 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
         for (uint32_t i = 0; i < m; ++i)
           if (i != c) b1 += ub[i];
         if (key_of(b1 * kInflate, d) < thk) continue;  // bound 1
+        const uint32_t bz = bess[((d - d0) >> fg::kSubShift) & 7u];
+        if (!((bz >> c) & 1u)) continue;  // not essential in its block
         // bound 2, clause order; the own clause adds the streamed score
         float sum = 0.0f;
         uint32_t maybe = 0, first = 0xFFFFFFFFu;
@@ -395,7 +437,7 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
           }
         }
         if (exact) {
-          first = (uint32_t)__builtin_ctz((maybe | (1u << c)) & ess);
+          first = (uint32_t)__builtin_ctz((maybe | (1u << c)) & bz);
           if (first == c && key_of(sum, d) >= thk) ++kept;
           continue;
         }
@@ -409,7 +451,7 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
           if (x >= 0.0f) { sc += x; matched |= 1u << i; }
         }
         (void)v;
-        first = (uint32_t)__builtin_ctz(matched & ess);
+        first = (uint32_t)__builtin_ctz(matched & bz);
         if (first == c && key_of(sc, d) >= thk) ++kept;
       }
     }
@@ -491,7 +533,7 @@ int fg_model_batch(const fg_index* ix, const fg_query_batch* q, uint32_t k, cons
   out->alg_bytes = out->stream_bytes + out->probe_bytes + out->output_bytes;
   out->line_bytes = (double)kLine * (double)U.count();
   if (getenv("FUGU_MODEL_TRACE")) {  // the line floor and the per-query line sum, by array
-    static const char* names[A_N] = {"doc", "psc", "rank", "dense", "dir", "bmax", "tmax", "tdir", "cmax"};
+    static const char* names[A_N] = {"doc", "psc", "rank", "dense", "dir", "bmax", "tmax", "tdir", "cmax", "tsub"};
     for (uint32_t a = 0; a < A_N; ++a)
       fprintf(stderr, "[fg model] %-6s floor %8.3f GB  per-query sum %8.3f GB\n", names[a],
               (double)kLine * (double)U.count(a) * 1e-9, (double)kLine * (double)U.qlines[a].load() * 1e-9);
