@@ -91,10 +91,13 @@ int fg_db_upsert_batch(fg_db* db, const char* ns, uint32_t n, const char* ids, c
 int fg_db_upsert(fg_db* db, const char* ns, const char* id, const char* text, const char* name,
                  const char* metadata_json);
 /* IndexWriter::commit (src/db/document.rs:65): the docs since the last commit
- * become a segment, the older segments are rescored with the new statistics.
- * With more than 8 segments the namespace is queued for the background merger
- * (tantivy's merge threads): a run of small segments becomes one, off the
- * commit path; readers keep the snapshot they hold. */
+ * become a segment, the older segments are rescored with the new statistics
+ * and pick up the deletes of the upserts since the last commit (a delete takes
+ * effect at the commit, as delete_term does; a merge in between neither drops
+ * nor flags the doc).  When 8 segments of one size level have accumulated
+ * (tantivy's LogMergePolicy) the namespace is queued for the background merger:
+ * the run becomes one segment, built and rescored off the commit path and
+ * swapped in between commits; readers keep the snapshot they hold. */
 int fg_db_commit(fg_db* db, const char* ns);
 /* Block until no merge of the namespace is queued or running (tests, shutdown);
  * FG_EHIP with the message when a background merge failed. */
