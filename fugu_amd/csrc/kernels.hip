@@ -1194,7 +1194,30 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       len[r] = 0;
       if (p < npair) {
         const uint32_t t = p / m, i = p - t * m;
-        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) len[r] = sh.r_hi[p] - sh.r_lo[p];
+        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) {
+          // the segment trimmed to the blocks where the clause is essential
+          // (first to last; the bucket directory's entries at those block
+          // boundaries, or the enclosing buckets' when a bucket spans blocks)
+          uint32_t bm = 0;
+          for (uint32_t z = 0; z < 8; ++z) bm |= ((uint32_t)(sh.b_ess[t * 8 + z] >> i) & 1u) << z;
+          const uint32_t B = sh.c_meta[i] & 0xFFu;
+          if (bm != 0xFFu && B <= kTileShift && sh.r_lo[p] < sh.r_hi[p]) {
+            uint32_t lo = sh.r_lo[p], hi = sh.r_lo[p];
+            if (bm) {
+              const uint32_t z0 = __builtin_ctz(bm), z1 = 31u - __builtin_clz(bm);
+              const uint32_t d0 = (tile0 + t) << kTileShift;
+              const uint32_t da = d0 + (z0 << kSubShift), db = min(d0 + ((z1 + 1) << kSubShift), ix.n_docs);
+              if (da < db) {
+                const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[i];
+                lo = max(lo, dir[da >> B]);
+                hi = max(lo, min(sh.r_hi[p], dir[((db - 1) >> B) + 1]));
+              }
+            }
+            sh.r_lo[p] = lo;
+            sh.r_hi[p] = hi;
+          }
+          len[r] = sh.r_hi[p] - sh.r_lo[p];
+        }
       }
       cnt += len[r] ? 1u : 0u;
       tot += len[r];

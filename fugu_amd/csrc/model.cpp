@@ -377,16 +377,36 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
         bess[z] = S.tsub.empty() ? ess : ez;
       }
     }
-    // P: the essential clauses' postings
+    // P: the essential clauses' postings, each segment trimmed to its first..last
+    // essential block (the bucket directory's entries there: two 4-B loads)
     for (uint32_t c = 0; c < m; ++c) {
       if (!((ess >> c) & 1u) || lo[c] >= hi[c]) continue;
+      uint32_t bm = 0, plo = lo[c], phi = hi[c];  // the streamed range (lo / hi stay the tile's: bound 2 walks them)
+      for (uint32_t z = 0; z < 8; ++z) bm |= ((bess[z] >> c) & 1u) << z;
+      if (bm != 0xFFu && B[c] <= TS) {
+        uint32_t l2 = lo[c], h2 = lo[c];
+        if (bm) {
+          const uint32_t z0 = (uint32_t)__builtin_ctz(bm), z1 = 31u - (uint32_t)__builtin_clz(bm);
+          const uint32_t da = d0 + (z0 << fg::kSubShift), db = std::min<uint32_t>(d0 + ((z1 + 1) << fg::kSubShift), N);
+          if (da < db) {
+            const uint64_t dob = S.dir_off[t[c]], ba = da >> B[c], bb = ((db - 1) >> B[c]) + 1;
+            A.gather(c, A_DIR, (dob + ba) * 4, 4, A.stream);
+            A.gather(c, A_DIR, (dob + bb) * 4, 4, A.stream);
+            l2 = std::max(l2, S.pos_ge(t[c], ba << B[c]));
+            h2 = std::max(l2, std::min(hi[c], S.pos_ge(t[c], bb << B[c])));
+          }
+        }
+        plo = l2;
+        phi = h2;
+        if (plo >= phi) continue;
+      }
       const uint64_t base = ix->off[t[c]];
       const uint32_t* l = S.list(t[c]);
-      A.range(c, A_DOC, base + lo[c], hi[c] - lo[c], 4, A.stream);
-      A.range(c, A_PSC, base + lo[c], hi[c] - lo[c], 4, A.stream);
+      A.range(c, A_DOC, base + plo, phi - plo, 4, A.stream);
+      A.range(c, A_PSC, base + plo, phi - plo, 4, A.stream);
       uint32_t cur[fg::kMaxTerms];
       for (uint32_t i = 0; i < m; ++i) cur[i] = lo[i];
-      for (uint32_t p = lo[c]; p < hi[c]; ++p) {
+      for (uint32_t p = plo; p < phi; ++p) {
         const uint32_t d = l[p];
         const float ps = S.psc[base + p];
         float b1 = ps;
