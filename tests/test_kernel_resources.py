@@ -8,7 +8,9 @@ change that silently made k_conj spill took the headline kernel from 1.06 to
   * single-snapshot k_conj / k_disj instantiations: no scratch, no VGPR spill;
   * k_conj <= 128 VGPRs (4 waves/SIMD), k_disj <= 96 VGPRs (5 waves/SIMD);
   * the multi-snapshot k_conj (segmented namespaces, C4) at most the 20 B of
-    scratch it has carried since round 3.
+    scratch it has carried since round 3 (DESIGN.md §3);
+  * LDS: k_conj <= 40 KB (4 workgroups of 4 waves per CU's 160 KB), k_disj
+    <= 32 KB (5 workgroups).
 """
 import os
 import re
@@ -29,12 +31,16 @@ def kernel_meta(tmp_path):
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
     notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], check=True, capture_output=True,
                            text=True).stdout
-    meta, cur = {}, None
+    meta, cur, lds = {}, None, None
     for line in notes.splitlines():
+        m = re.match(r"\s+\.group_segment_fixed_size:\s+(\d+)", line)  # sorts before .name in a kernel's map
+        if m:
+            lds = int(m.group(1))
+            continue
         m = re.match(r"\s+\.name:\s+(\S+)", line)
         if m:
             cur = m.group(1)
-            meta[cur] = {}
+            meta[cur] = {"lds": lds}
             continue
         m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count|vgpr_count):\s+(\d+)", line)
         if m and cur:
@@ -51,11 +57,11 @@ def test_hot_kernels_fit_their_register_budget(tmp_path):
     assert len(conj) == 4 and len(disj) == 2, sorted(meta)
     for name, v in conj.items():
         multi_general = "k_conjILb0ELb1E" in name
-        assert v["vgpr_count"] <= 128, (name, v)
+        assert v["vgpr_count"] <= 128 and v["lds"] <= 40 * 1024, (name, v)
         if multi_general:
             assert v["private_segment_fixed_size"] <= 20, (name, v)
         else:
             assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (name, v)
     for name, v in disj.items():
-        assert v["vgpr_count"] <= 96, (name, v)
+        assert v["vgpr_count"] <= 96 and v["lds"] <= 32 * 1024, (name, v)
         assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (name, v)
