@@ -10,7 +10,7 @@ change that silently made k_conj spill took the headline kernel from 1.06 to
   * the multi-snapshot k_conj (segmented namespaces, C4) at most the 20 B of
     scratch it has carried since round 3 (DESIGN.md §3);
   * LDS: k_conj <= 40 KB (4 workgroups of 4 waves per CU's 160 KB), k_disj
-    <= 32 KB (5 workgroups).
+    <= 31.9 KB (5 workgroups: 32400 B already fell to 4).
 """
 import os
 import re
@@ -63,5 +63,6 @@ def test_hot_kernels_fit_their_register_budget(tmp_path):
         else:
             assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (name, v)
     for name, v in disj.items():
-        assert v["vgpr_count"] <= 96 and v["lds"] <= 32 * 1024, (name, v)
+        # 32400 B measured 17% slower than 30352 B (4 workgroups per CU instead of 5, ab_rsub_lds_cliff.log)
+        assert v["vgpr_count"] <= 96 and v["lds"] <= 31 * 1024 + 896, (name, v)
         assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (name, v)
