@@ -903,9 +903,11 @@ struct DisjShared {
   } p;
   uint32_t scratch[8];
   // R: per (tile, clause) ranges and bounds, index t * m + i
-  uint32_t r_lo[kMaxSeg], r_hi[kMaxSeg];
+  uint32_t r_lo[kMaxSeg];            // R: first posting of the pair (within the term's list)
+  uint16_t r_n[kMaxSeg];             // R: its postings in the tile (<= 4096)
   float r_ub[kMaxSeg];
   uint16_t b_ess[kMaxTiles * 8];     // S: essential-clause mask per 512-doc block
+  uint64_t r_sub[kMaxSeg];           // R: the pair's sub-tile maxima (DevIndex::tsub; ~0: the tile bound)
   uint32_t t_ess[kMaxTiles];         // essential-clause mask per tile (the union of its blocks')
   uint32_t t_post[kMaxTiles];        // 1: the tile's essential postings are streamed, 0: skipped
   uint16_t seg_info[kMaxSeg];        // P: (tile << 4) | clause of each segment
@@ -1070,6 +1072,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       lo = ix.tdir[to];
       hi = ix.tdir[to + 1];
       ub = ix.tmax[to];
+      sh.r_sub[p] = ix.tsub[to];
     } else if (B <= kTileShift) {
       lo = dir[d0 >> B];
       hi = dir[((d1 - 1) >> B) + 1];
@@ -1094,8 +1097,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       ub = ix.bmax[sh.c_dir[i] + b];
     }
     sh.r_lo[p] = lo;
-    sh.r_hi[p] = hi;
+    sh.r_n[p] = (uint16_t)(hi > lo ? hi - lo : 0u);
     sh.r_ub[p] = lo < hi ? ub : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
+    if (!(B <= kTileShift && sh.c_toff[i] != kInvalid)) sh.r_sub[p] = ~0ull;
   }
   {
     // the query's running threshold (every work item's counted hits so far)
@@ -1127,7 +1131,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     }
     uint32_t ess = 0, any = 0;
     for (uint32_t j = 0; j < m; ++j) {
-      const uint32_t n = sh.r_hi[t * m + ord[j]] - sh.r_lo[t * m + ord[j]];
+      const uint32_t n = sh.r_n[t * m + ord[j]];
       if (j < P) continue;
       ess |= 1u << ord[j];
       any |= n ? 1u : 0u;
@@ -1149,10 +1153,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     const uint64_t thr = sh.thr;
     const float* ub = sh.r_ub + t * m;
     const uint32_t ess = sh.t_ess[t];
-    auto bound = [&](uint32_t i) {
-      const uint32_t to = sh.c_toff[i];
-      return to != kInvalid ? sub_bound(ix.tsub[to + tile], z, ub[i]) : ub[i];
-    };
+    auto bound = [&](uint32_t i) { return sub_bound(sh.r_sub[t * m + i], z, ub[i]); };
     float sz = 0.0f;
     for (uint32_t i = 0; i < m; ++i)
       if (!((ess >> i) & 1u)) sz += bound(i);
@@ -1178,7 +1179,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     for (uint32_t t = 0; t < ntile; ++t) {
       dg_mode[sh.t_post[t] ? 2 : 0]++;
       for (uint32_t i = 0; i < m; ++i)
-        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) dg_post += sh.r_hi[t * m + i] - sh.r_lo[t * m + i];
+        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) dg_post += sh.r_n[t * m + i];
     }
 #endif
 
@@ -1201,7 +1202,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
           uint32_t bm = 0;
           for (uint32_t z = 0; z < 8; ++z) bm |= ((uint32_t)(sh.b_ess[t * 8 + z] >> i) & 1u) << z;
           const uint32_t B = sh.c_meta[i] & 0xFFu;
-          if (bm != 0xFFu && B <= kTileShift && sh.r_lo[p] < sh.r_hi[p]) {
+          if (bm != 0xFFu && B <= kTileShift && sh.r_n[p]) {
+            const uint32_t hi0 = sh.r_lo[p] + sh.r_n[p];
             uint32_t lo = sh.r_lo[p], hi = sh.r_lo[p];
             if (bm) {
               const uint32_t z0 = __builtin_ctz(bm), z1 = 31u - __builtin_clz(bm);
@@ -1210,13 +1212,13 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
               if (da < db) {
                 const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[i];
                 lo = max(lo, dir[da >> B]);
-                hi = max(lo, min(sh.r_hi[p], dir[((db - 1) >> B) + 1]));
+                hi = max(lo, min(hi0, dir[((db - 1) >> B) + 1]));
               }
             }
             sh.r_lo[p] = lo;
-            sh.r_hi[p] = hi;
+            sh.r_n[p] = (uint16_t)(hi - lo);
           }
-          len[r] = sh.r_hi[p] - sh.r_lo[p];
+          len[r] = sh.r_n[p];
         }
       }
       cnt += len[r] ? 1u : 0u;
@@ -1313,8 +1315,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
           // bound 1: the other clauses' tile bounds (LDS) and the facet maximum
           const uint32_t t = (pd[j] - dbase) >> kTileShift;
           float ub = ps[j] + fmax;
+          const uint32_t zz = ((pd[j] - dbase) >> kSubShift) & 7u;
           for (uint32_t i = 0; i < m; ++i)
-            if (i != pcl[j]) ub += sh.r_ub[t * m + i];
+            if (i != pcl[j]) ub += sub_bound(sh.r_sub[t * m + i], zz, sh.r_ub[t * m + i]);
           pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
           pk[j] = pk[j] && ((sh.b_ess[(pd[j] - dbase) >> kSubShift] >> pcl[j]) & 1u);
           if (pk[j] && fmask) pk[j] = filter_bits(fmask, fshift, pd[j]) != 0;
@@ -1360,8 +1363,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         if (!pk[j]) continue;
         // bound 1 again: the threshold may have risen since the posting was queued
         float ub = ps[j] + fmax;
+        const uint32_t zz = (rel >> kSubShift) & 7u;
         for (uint32_t i = 0; i < m; ++i)
-          if (i != pcl[j]) ub += sh.r_ub[pt[j] * m + i];
+          if (i != pcl[j]) ub += sub_bound(sh.r_sub[pt[j] * m + i], zz, sh.r_ub[pt[j] * m + i]);
         pk[j] = make_key(inflate_bound(ub), pd[j]) >= thr;
         ess[j] = sh.b_ess[rel >> kSubShift];
       }

@@ -346,8 +346,9 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
     // tile's non-essential clauses plus essential ones, smallest tile bound
     // first, while their sub-tile bounds stay below the threshold together
     uint32_t bess[8];
+    uint64_t subq[fg::kMaxTerms];  // each clause's sub-tile maxima (~0: its tile bound)
     {
-      uint64_t sub[fg::kMaxTerms];
+      uint64_t* sub = subq;
       for (uint32_t c = 0; c < m; ++c) {
         sub[c] = ~0ull;
         if (B[c] <= TS && S.toff[t[c]] != 0xFFFFFFFFu && !S.tsub.empty()) {
@@ -409,10 +410,12 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
       for (uint32_t p = plo; p < phi; ++p) {
         const uint32_t d = l[p];
         const float ps = S.psc[base + p];
+        // bound 1: the other clauses' bounds over the doc's 512-doc block
+        const uint32_t zb = ((d - d0) >> fg::kSubShift) & 7u;
         float b1 = ps;
         for (uint32_t i = 0; i < m; ++i)
-          if (i != c) b1 += ub[i];
-        if (key_of(b1 * kInflate, d) < thk) continue;  // bound 1
+          if (i != c) b1 += fg::q8_bound((uint32_t)(subq[i] >> (8 * zb)) & 0xFFu, ub[i]);
+        if (key_of(b1 * kInflate, d) < thk) continue;
         const uint32_t bz = bess[((d - d0) >> fg::kSubShift) & 7u];
         if (!((bz >> c) & 1u)) continue;  // not essential in its block
         // bound 2, clause order; the own clause adds the streamed score
