@@ -157,6 +157,16 @@ def native_oracle():
     return "-O3 -ffp-contract=off -march=x86-64-v2 (portable build: native compile failed)"
 
 
+def throughput_fields(nq, world, steps, elapsed_s):
+    """The headline's throughput at N ranks: a step is ONE fan-out batch of nq
+    queries (each answered once, from the N namespaces' merged lists), so `value`
+    counts nq per step whatever N is; the (query, namespace) pairs the ranks
+    searched are reported beside it, never as `value`."""
+    return {"value": round(nq * steps / elapsed_s, 1),
+            "namespace_queries_per_s": round(nq * world * steps / elapsed_s, 1),
+            "queries_per_step": nq}
+
+
 def timed_steps(step, steps, warmup, torch):
     for _ in range(warmup):
         step()
@@ -429,6 +439,48 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
             "projected_8gpu": "each GPU runs one namespace: step ~ max(k_conj_ms_per_namespace) + k_final + gather"}
 
 
+def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps):
+    """Every shard's plan run ALONE (no shared threshold word): each shard's
+    kernel ms as one GPU of an 8-GPU doc-sharded run sees it (k_disj / k_conj,
+    k_final), and the hash of the hits merged from the shards' lists."""
+    from fugu_amd.shard import merge_on_device
+    import torch
+    nq = len(q_off) - 1
+    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
+    gs = torch.empty((len(ixs), nq * K), dtype=torch.float32, device=dev)
+    gd = torch.empty((len(ixs), nq * K), dtype=torch.int32, device=dev)
+    gn = torch.empty((len(ixs), nq), dtype=torch.int32, device=dev)
+    ms = []
+    for r, ix in enumerate(ixs):
+        p = ix.plan(q_off, terms, K, mode)
+        p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+        torch.cuda.synchronize()
+        p.profile(True)
+        for _ in range(reps):
+            p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+        torch.cuda.synchronize()
+        m, n = p.kernel_ms()
+        ms.append((round(m[0] / max(n, 1), 4), round(m[1] / max(n, 1), 4)))
+        p.close()
+    out = merge_on_device(gs, gd, gn, nq, K, st)
+    torch.cuda.synchronize()
+    return ms, hits_sha1(out[0], out[1], out[2], out[3], K)
+
+
+def hits_sha1(s, d, sh, n, K):
+    """sha1 (16 hex) of merged (score, doc, shard) lists, each query's first n entries."""
+    import hashlib
+    s, d, n = s.cpu().numpy(), d.cpu().numpy(), n.cpu().numpy()
+    sh = None if sh is None else sh.cpu().numpy()
+    h = hashlib.sha1()
+    for i in range(len(n)):
+        m = int(n[i])
+        h.update(s[i * K:i * K + m].tobytes() + d[i * K:i * K + m].tobytes())
+        if sh is not None:
+            h.update(sh[i * K:i * K + m].tobytes())
+    return h.hexdigest()[:16]
+
+
 def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_seconds, do_cpu):
     """C5 (BASELINE configs[4]) on one GPU: 100M docs, Zipf s=1.1, as 8
     contiguous doc shards scored with the GLOBAL statistics (tantivy's segment
@@ -470,10 +522,31 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     kms = [p.kernel_ms() for p in plans]
     per_shard = [round(m[0][0] / max(m[1], 1), 4) for m in kms]
     del plans
-    # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel)
-    mp = native.Plan(ixs, q_off, terms, K, native.MODE_OR)
+    # every shard ALONE (what each GPU of the 8-GPU split runs: no threshold word
+    # shared across devices), from its own K-th scores, then from the
+    # namespace-wide floor (ladders exchanged once at build: shard.seed_kth_floor)
+    alone_un, sha_un = alone_kernel_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2))
+    from fugu_amd.shard import seed_kth_floor
+    t0 = time.time()
+    seed_kth_floor(ixs)
+    seed_s = time.time() - t0
+    alone_se, sha_se = alone_kernel_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2))
+    log(f"[bench] C5 shards alone: unseeded max {max(x[0] for x in alone_un)} ms, seeded max "
+        f"{max(x[0] for x in alone_se)} ms (linked mean {np.mean(per_shard):.3f}); floor in {seed_s:.1f}s")
+    # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel),
+    # planned with the floor; beside it the same plan without the floor
     outs = tuple(torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)) + (
         torch.empty(nq, dtype=torch.int32, device=dev),)
+    for ix in ixs:
+        ix.set_kth_floor(None)
+    mp0 = native.Plan(ixs, q_off, terms, K, native.MODE_OR)
+    mp0.profile(True)
+    el0 = timed_steps(lambda: mp0.execute_merged(st, *[x.data_ptr() for x in outs]), max(2, steps // 2), 1, torch)
+    mk0, mkn0 = mp0.kernel_ms()
+    sha_multi_un = hits_sha1(outs[0], outs[1], outs[2], outs[3], K)
+    del mp0
+    seed_kth_floor(ixs)
+    mp = native.Plan(ixs, q_off, terms, K, native.MODE_OR)
 
     def step():  # the merged select: the merged lists straight from k_final
         mp.execute_merged(st, *[x.data_ptr() for x in outs])
@@ -482,6 +555,7 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     mp.profile(True)
     el = timed_steps(step, steps, warmup, torch)
     mk, mkn = mp.kernel_ms()
+    sha_multi = hits_sha1(outs[0], outs[1], outs[2], outs[3], K)
     # roofline of the multi-snapshot k_disj: every shard replayed at the merged
     # k-th score (the shards' shared score-only threshold)
     t0 = time.time()
@@ -498,10 +572,27 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
            "multi_plan_kernels_ms": [round(mk[0] / max(mkn, 1), 4), round(mk[1] / max(mkn, 1), 4)],
            "roofline": roof,
            "ms_per_step_8_linked_plans": round(el_linked * 1e3 / max(2, steps // 2), 4),
-           "k_disj_ms_per_shard_linked": per_shard, "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
+           "k_disj_ms_per_shard_linked": per_shard, "k_disj_ms_per_shard_linked_mean": round(float(np.mean(per_shard)), 4),
+           "k_disj_ms_per_shard_independent": {
+               "unseeded": [x[0] for x in alone_un], "seeded": [x[0] for x in alone_se],
+               "unseeded_max": max(x[0] for x in alone_un), "seeded_max": max(x[0] for x in alone_se),
+               "k_final_ms_seeded": [x[1] for x in alone_se],
+               "seeded_max_over_linked_mean": round(max(x[0] for x in alone_se) / float(np.mean(per_shard)), 3),
+               "result_sha1_unseeded": sha_un, "result_sha1_seeded": sha_se, "same_hits": sha_un == sha_se,
+               "floor_s": round(seed_s, 2),
+               "note": "each shard's plan alone (no shared threshold word: one GPU of the 8-GPU split); seeded = "
+                       "its starting thresholds floored by the namespace-wide per-term K-th score bounds "
+                       "(fg_index_term_ladder of every shard, one all-gather, fg_kth_floor_combine)"},
+           "multi_plan_unseeded": {"ms_per_step": round(el0 * 1e3 / max(2, steps // 2), 4),
+                                   "kernels_ms": [round(mk0[0] / max(mkn0, 1), 4), round(mk0[1] / max(mkn0, 1), 4)],
+                                   "result_sha1": sha_multi_un},
+           "result_sha1": sha_multi, "same_hits_seeded_unseeded": sha_multi == sha_multi_un,
+           "merge_ms": mms, "snapshot_build_s": round(build_s, 1),
            "workload": "C5: 100M docs s=1.1 as 8 doc shards with global BM25 statistics, 2-5-term OR top-1000 on "
-                       "all 8 + device merge, all 8 shards on this one GPU",
-           "projected_8gpu": "each GPU runs one shard: step ~ max(k_disj_ms_per_shard) + k_final + gather"}
+                       "all 8 + device merge, all 8 shards on this one GPU (the step: one multi-snapshot plan, "
+                       "seeded with the namespace-wide K-th floors)",
+           "projected_8gpu": "each GPU runs one shard alone: step ~ max(k_disj_ms_per_shard_independent.seeded) + "
+                             "k_final + all-gather + merge"}
     del mp
     for ix in ixs:
         ix.close()
@@ -582,6 +673,16 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     del parts
     build_s = time.time() - t0
     log(f"[bench] {cfg}: rank {rank} built units {mine} in {build_s:.1f}s")
+    floor_info = None
+    if not c4 and os.environ.get("FUGU_C5_SEED", "1") != "0":
+        # the doc shards' ladders all-gathered once (RCCL), combined into the
+        # namespace-wide floor of every term's K-th scores: each rank's shards start
+        # their thresholds from it (no threshold word is shared across GPUs)
+        from fugu_amd.shard import seed_kth_floor
+        t1 = time.time()
+        seed_kth_floor(ixs, device=dev if backend == "nccl" else None)
+        floor_info = {"seconds": round(time.time() - t1, 2),
+                      "all_gather_bytes_per_rank": 4 * len(ixs) * synth.VOCAB * len(native.LADDER_KS)}
     q_off, terms = synth.queries(nq, 3, 3) if c4 else synth.queries(nq, 2, 5)
     # a rank's units: ONE multi-snapshot plan (one launch per kernel, shared
     # score-only thresholds); FUGU_BENCH_LINKED=1: one linked plan per unit (A/B)
@@ -637,6 +738,7 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t1
+    el_rank = el
     kms = [p.kernel_ms() for p in plans]
     kern = sum(m[0][0] for m in kms) / max(kms[0][1], 1)
     fin = sum(m[0][1] for m in kms) / max(kms[0][1], 1)
@@ -668,11 +770,17 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     per_rank = None
     if world > 1:
         allr = [None] * world
+        alg = roof.get("alg_bytes_per_launch")
         dist.all_gather_object(allr, {"rank": rank, "kernel_ms": roof["kernel_ms"], "frac": roof.get("frac"),
-                                      "alg_bytes_per_launch": roof.get("alg_bytes_per_launch"), "units": mine})
+                                      "step_ms": round(el_rank * 1e3 / args.steps, 4),
+                                      "frac_step": round(alg / (el_rank / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
+                                      if alg else None,
+                                      "alg_bytes_per_launch": alg, "units": mine})
         per_rank = {"ranks": allr, "kernel_ms_min": min(x["kernel_ms"] for x in allr),
                     "kernel_ms_max": max(x["kernel_ms"] for x in allr),
-                    "frac_min": min(x["frac"] or 0 for x in allr), "frac_max": max(x["frac"] or 0 for x in allr)}
+                    "frac_min": min(x["frac"] or 0 for x in allr), "frac_max": max(x["frac"] or 0 for x in allr),
+                    "frac_step_min": min(x["frac_step"] or 0 for x in allr),
+                    "frac_step_max": max(x["frac_step"] or 0 for x in allr)}
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(nq * args.steps / el, 1), "unit": "queries/s", "n_gpus": world,
@@ -693,6 +801,7 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
                           if merged_sel else f"{len(plans)} linked plan(s) + k_merge_rank"),
             "result_sha1": h.hexdigest()[:16],
             "hits": int(mn.sum()),
+            **({"kth_floor": floor_info} if floor_info else {}),
             "snapshot_build_s_rank0": round(build_s, 1),
             "cpu_baseline": None,
             "note": "strong scaling of one fixed corpus; roofline = rank 0's units (per_rank: every rank's); the "
@@ -870,6 +979,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    el_rank = elapsed
     plan.profile(False)
     ms_k, n_prof = plan.kernel_ms()
     if world > 1:
@@ -877,7 +987,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    total_queries = nq * world * args.steps
+    tput = throughput_fields(nq, world, args.steps, elapsed)
     result_sha1 = None
     if world > 1 and "m" in merged:  # the merged lists of the last step (equal with and without --overlap)
         import hashlib
@@ -887,7 +997,7 @@ def main():
             m = int(mn_[i])
             h.update(ms_[i * K:i * K + m].tobytes() + md_[i * K:i * K + m].tobytes() + msh_[i * K:i * K + m].tobytes())
         result_sha1 = h.hexdigest()[:16]
-    qps = total_queries / elapsed
+    qps = tput["value"]
 
     # ---- p50 latency at batch = 1 (host query in, host hits out: plan + PCIe + kernels)
     lat = []
@@ -937,14 +1047,22 @@ def main():
     # N > 1: every rank's kernel time and roofline fraction (its own namespace)
     per_rank = None
     if world > 1:
+        alg = roof.get("alg_bytes_per_launch")
         mine = {"rank": rank, "kernel_ms": roof["kernel_ms"], "frac": roof.get("frac"),
-                "alg_bytes_per_launch": roof.get("alg_bytes_per_launch"), "line_floor_bytes": roof.get("line_floor_bytes"),
+                "step_ms": round(el_rank * 1e3 / args.steps, 4),
+                # the same bytes over the rank's whole step (kernels + all-gather + merge)
+                "frac_step": round(alg / (el_rank / args.steps) / 1e9 / HBM_PEAK_GBS, 4) if alg else None,
+                "alg_bytes_per_launch": alg, "line_floor_bytes": roof.get("line_floor_bytes"),
                 "device": torch.cuda.get_device_name(dev), "local_rank": local}
         allr = [None] * world
         dist.all_gather_object(allr, mine)
         per_rank = {"ranks": allr,
                     "kernel_ms_min": min(r["kernel_ms"] for r in allr), "kernel_ms_max": max(r["kernel_ms"] for r in allr),
-                    "frac_min": min(r["frac"] or 0 for r in allr), "frac_max": max(r["frac"] or 0 for r in allr)}
+                    "frac_min": min(r["frac"] or 0 for r in allr), "frac_max": max(r["frac"] or 0 for r in allr),
+                    "frac_step_min": min(r["frac_step"] or 0 for r in allr),
+                    "frac_step_max": max(r["frac_step"] or 0 for r in allr),
+                    "note": "frac: the rank's algorithmic bytes over its kernel time; frac_step: over its step time "
+                            "(north_star: the 1-GPU fraction held within 10% at 8 GPUs)"}
 
     # ---- CPU baseline: the oracle (tantivy's algorithm restated in C, compiled
     # -march=native on this host) on T = nproc host threads, each running whole
@@ -1090,6 +1208,9 @@ def main():
             "metric": METRIC,
             "value": round(qps, 1),
             "unit": "queries/s",
+            **({"namespace_queries_per_s": tput["namespace_queries_per_s"], "queries_per_step": nq,
+                "value_counts": "fan-out queries answered (one merged top-k list each over the N namespaces)"}
+               if world > 1 else {}),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,

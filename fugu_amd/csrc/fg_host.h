@@ -353,6 +353,9 @@ struct fg_index {
   const float* ktop = nullptr;   // [V * kNumTopK] K-th best alive score per term (kTopKs)
   const float* tmaxs = nullptr;  // [V] largest posting score per term
   std::vector<float> hown;       // ktop / tmaxs when no pinned block was had (sblock.hp)
+  // [V * kNumTopK] namespace-wide floor of ktop (fg_index_set_kth_floor) or null;
+  // read and replaced with std::atomic_load / atomic_store
+  std::shared_ptr<const std::vector<float>> kth_floor;
   fgh::SharedVec<float> w_text, w_name;
   // ---- structure (independent of the statistics; shared with rescored snapshots)
   fgh::SharedVec<uint64_t> off;

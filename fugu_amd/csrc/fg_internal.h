@@ -102,6 +102,14 @@ constexpr uint32_t kDisjMaxPairs = 256;  // ... and at most this many (tile, Sho
 // ab_ktop20_k20.log: OR top-20 k_disj 4.27 -> 4.22 ms starting from it)
 constexpr uint32_t kNumTopK = 5;
 constexpr uint32_t kTopKs[kNumTopK] = {1, 10, 20, 100, 1000};
+// fg_index_term_ladder: the same K-th scores at the ranks between them as well
+// (ascending), from which the shards of a doc-sharded namespace bound the
+// namespace-wide K-th score of a term (fg_kth_floor_combine: K = 1000 over 8
+// shards needs each shard's 125th).  Computed on demand, never stored.
+constexpr uint32_t kNumLadderExtra = 9;
+constexpr uint32_t kLadderExtra[kNumLadderExtra] = {2, 3, 5, 13, 25, 50, 125, 250, 500};
+constexpr uint32_t kNumLadder = kNumTopK + kNumLadderExtra;  // FG_LADDER_LEVELS
+constexpr uint32_t kLadderKs[kNumLadder] = {1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000};
 
 constexpr uint32_t kMaxFacetClauses = 8;  // facet clauses per query (FG_MAX_FACET_CLAUSES)
 constexpr uint32_t kFmaskChunk = 8192;    // facet postings per k_fmask workgroup
@@ -345,7 +353,8 @@ struct ScoreJob {
   uint32_t n_tterm;           // tile-table terms
   uint32_t n_tiles;           // tiles per term (4096-doc k_disj tiles)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
-  float* cmax;                // [cmax entries] out: the largest score of each kChunk postings of a term
+  float* ladder;              // [V * kNumLadderExtra] out (zeroed first) or nullptr: fg_index_term_ladder only
+  float* cmax;               // [cmax entries] out: the largest score of each kChunk postings of a term
   const uint32_t* coff;       // [V] first cmax entry of each term
   // packed chunk tables (a chunk: terms [tf, tl], postings / directory entries
   // [e0, e1) of them; one long term's slice, or several whole short terms)

@@ -324,6 +324,45 @@ void bm25_weights(uint64_t Ns, const uint32_t* df_t, const uint32_t* df_n, uint3
   });
 }
 
+// k_ktop over the snapshot's scores (j.psc, j.alive -> j.ktop, and j.ladder when
+// set): terms of <= kKtopChunk postings one workgroup each; longer terms in
+// kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
+// chunks' best keys (k_ktop_big).  The chunk tables are the structure's; the key
+// scratch is one stream-ordered temporary (freeing it does not synchronize the
+// device: searches on other streams keep running).
+static int ktop_pass(const fg_index* ix, fg::ScoreJob& j) {
+  const size_t n_small = ix->n_kt, n_big = ix->n_kbig, n_chunks = ix->n_kchunks;
+  const size_t kck_b = (8ull * n_chunks * fg::kTopKs[fg::kNumTopK - 1] + 255) & ~size_t(255);
+  const size_t kcc_b = (4ull * n_chunks + 255) & ~size_t(255), kbs_b = 4ull * 3 * n_big;
+  void* ktmp = nullptr;
+  if (hipMallocAsync(&ktmp, kck_b + kcc_b + kbs_b + 16, kBuildStream) != hipSuccess)
+    return fail(FG_EOOM, "hipMallocAsync(%zu) failed", kck_b + kcc_b + kbs_b);
+  struct KtmpBack {
+    void* p;
+    ~KtmpBack() { (void)hipFreeAsync(p, kBuildStream); }
+  } ktmp_back{ktmp};
+  char* kb = static_cast<char*>(ktmp);
+  uint32_t* d_kbs = reinterpret_cast<uint32_t*>(kb + kck_b + kcc_b);
+  // per long term: alive postings 0, min alive score bits ~0, max 0 ([3][n_big])
+  if (n_big) {
+    HIPCHK(hipMemsetAsync(d_kbs, 0, 4ull * 3 * n_big, kBuildStream));
+    HIPCHK(hipMemsetD32Async(d_kbs + n_big, (int)0xFFFFFFFFu, n_big, kBuildStream));
+  }
+  j.kt_tiny = ix->d_kt_tiny;
+  j.n_tiny = ix->n_ktiny;
+  j.kt_terms = ix->d_kt_terms;
+  j.kb_terms = ix->d_kb_terms;
+  j.kb_chunk0 = ix->d_kb_chunk0;
+  j.kc_big = ix->d_kc_big;
+  j.kc_start = ix->d_kc_start;
+  j.kc_keys = reinterpret_cast<uint64_t*>(kb);
+  j.kc_cnt = reinterpret_cast<uint32_t*>(kb + kck_b);
+  j.kb_stat = d_kbs;
+  j.n_big = (uint32_t)n_big;
+  HIPCHK(fg::launch_ktop(j, (uint32_t)n_small, (uint32_t)n_chunks, (uint32_t)n_big, kBuildStream));
+  return FG_OK;
+}
+
 // wts: the weights of (Ns, df_t, df_n) for at least ix's terms, or nullptr (computed here)
 int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_t* df_t, const uint32_t* df_n,
                 const std::vector<uint32_t>& alive, uint64_t tot_f, const uint32_t* df_f,
@@ -456,38 +495,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.n_tterm = ix->n_tterm;
   j.n_tiles = ix->n_tiles;
   HIPCHK(fg::launch_tsub(j, ix->n_docs, kBuildStream));
-  // k_ktop: terms of <= kKtopChunk postings one workgroup each; longer terms in
-  // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
-  // chunks' best keys (k_ktop_big).  The chunk tables are the structure's; the
-  // key scratch is one stream-ordered temporary (freeing it does not
-  // synchronize the device: searches on other streams keep running).
-  const size_t n_small = ix->n_kt, n_big = ix->n_kbig, n_chunks = ix->n_kchunks;
-  const size_t kck_b = (8ull * n_chunks * fg::kTopKs[fg::kNumTopK - 1] + 255) & ~size_t(255);
-  const size_t kcc_b = (4ull * n_chunks + 255) & ~size_t(255), kbs_b = 4ull * 3 * n_big;
-  void* ktmp = nullptr;
-  if (hipMallocAsync(&ktmp, kck_b + kcc_b + kbs_b + 16, kBuildStream) != hipSuccess)
-    return fail(FG_EOOM, "hipMallocAsync(%zu) failed", kck_b + kcc_b + kbs_b);
-  struct KtmpBack {
-    void* p;
-    ~KtmpBack() { (void)hipFreeAsync(p, kBuildStream); }
-  } ktmp_back{ktmp};
-  char* kb = static_cast<char*>(ktmp);
-  uint32_t* d_kbs = reinterpret_cast<uint32_t*>(kb + kck_b + kcc_b);
-  // per long term: alive postings 0, min alive score bits ~0, max 0 ([3][n_big])
-  if (n_big) {
-    HIPCHK(hipMemsetAsync(d_kbs, 0, 4ull * 3 * n_big, kBuildStream));
-    HIPCHK(hipMemsetD32Async(d_kbs + n_big, (int)0xFFFFFFFFu, n_big, kBuildStream));
-  }
-  j.kt_terms = ix->d_kt_terms;
-  j.kb_terms = ix->d_kb_terms;
-  j.kb_chunk0 = ix->d_kb_chunk0;
-  j.kc_big = ix->d_kc_big;
-  j.kc_start = ix->d_kc_start;
-  j.kc_keys = reinterpret_cast<uint64_t*>(kb);
-  j.kc_cnt = reinterpret_cast<uint32_t*>(kb + kck_b);
-  j.kb_stat = d_kbs;
-  j.n_big = (uint32_t)n_big;
-  HIPCHK(fg::launch_ktop(j, (uint32_t)n_small, (uint32_t)n_chunks, (uint32_t)n_big, kBuildStream));
+  if (int rc = ktop_pass(ix, j)) return rc;
   g_bt.mark("scoring launches");
   // tmaxs [V] then ktop [V * kNumTopK], read straight into the structure's
   // pooled pinned block (a released snapshot's, after the first rescores)
@@ -1614,6 +1622,102 @@ int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out) {
   return FG_OK;
 }
 
+int fg_index_term_ladder(const fg_index* ix, float* out) {
+  if (!ix || !out) return fail(FG_EINVAL, "bad arguments");
+  static_assert(fg::kNumLadder == FG_LADDER_LEVELS, "fugu.h FG_LADDER_LEVELS");
+  const uint32_t V = ix->n_terms;
+  if (V == 0) return FG_OK;
+  HIPCHK(hipSetDevice(ix->dev));
+  // one temporary: the main K-th scores [V * kNumTopK], then the extra levels
+  const size_t nm = (size_t)V * fg::kNumTopK, nx = (size_t)V * fg::kNumLadderExtra;
+  void* tmp = nullptr;
+  if (hipMallocAsync(&tmp, 4 * (nm + nx) + 16, kBuildStream) != hipSuccess)
+    return fail(FG_EOOM, "hipMallocAsync(%zu) failed", 4 * (nm + nx));
+  struct Back {
+    void* p;
+    ~Back() { (void)hipFreeAsync(p, kBuildStream); }
+  } back{tmp};
+  float* d = static_cast<float*>(tmp);
+  HIPCHK(hipMemsetAsync(d, 0, 4 * (nm + nx), kBuildStream));
+  fg::ScoreJob j{};
+  j.doc = ix->d.doc;
+  j.off = ix->d.off;
+  j.alive = ix->d.alive;
+  j.psc = const_cast<float*>(ix->d.psc);  // read only by k_ktop*
+  j.n_terms = V;
+  j.ktop = d;
+  j.ladder = d + nm;
+  if (int rc = ktop_pass(ix, j)) return rc;
+  std::vector<float> h(nm + nx);
+  HIPCHK(hipMemcpyAsync(h.data(), d, 4 * (nm + nx), hipMemcpyDeviceToHost, kBuildStream));
+  HIPCHK(hipStreamSynchronize(kBuildStream));
+  // interleave into ascending K per term
+  uint32_t src[fg::kNumLadder];  // level l: (main?, index)
+  for (uint32_t l = 0; l < fg::kNumLadder; ++l) {
+    src[l] = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < fg::kNumTopK; ++i)
+      if (fg::kTopKs[i] == fg::kLadderKs[l]) src[l] = i;
+    for (uint32_t i = 0; i < fg::kNumLadderExtra; ++i)
+      if (fg::kLadderExtra[i] == fg::kLadderKs[l]) src[l] = 0x10000u | i;
+    if (src[l] == 0xFFFFFFFFu) return fail(FG_EINVAL, "ladder level %u unmapped", l);
+  }
+  for (uint32_t t = 0; t < V; ++t)
+    for (uint32_t l = 0; l < fg::kNumLadder; ++l) {
+      const uint32_t s = src[l];
+      out[(size_t)t * fg::kNumLadder + l] = (s & 0x10000u) ? h[nm + (size_t)t * fg::kNumLadderExtra + (s & 0xFFFFu)]
+                                                            : h[(size_t)t * fg::kNumTopK + s];
+    }
+  return FG_OK;
+}
+
+int fg_kth_floor_combine(uint32_t n_shards, uint32_t n_terms, const float* const* ladders, float* out) {
+  if (!out || (n_shards && !ladders) || (n_terms && n_shards == 0)) return fail(FG_EINVAL, "bad arguments");
+  for (uint32_t s = 0; s < n_shards; ++s)
+    if (!ladders[s]) return fail(FG_EINVAL, "NULL ladder of shard %u", s);
+  constexpr uint32_t L = fg::kNumLadder;
+  fgh::parallel_dynamic(n_terms, fgh::hw_threads(0), 8192, [&](int, uint32_t b, uint32_t e) {
+    std::vector<std::pair<float, uint32_t>> c;  // (score, shard * L + level)
+    std::vector<uint32_t> cur(n_shards);        // the largest K of each shard at or above the sweep
+    for (uint32_t t = b; t < e; ++t) {
+      c.clear();
+      for (uint32_t s = 0; s < n_shards; ++s)
+        for (uint32_t l = 0; l < L; ++l) {
+          const float v = ladders[s][(size_t)t * L + l];
+          if (v > 0.0f) c.emplace_back(v, s * L + l);
+        }
+      std::sort(c.begin(), c.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+      std::fill(cur.begin(), cur.end(), 0u);
+      uint64_t total = 0;  // docs known to score >= the sweep's score
+      float res[fg::kNumTopK] = {0, 0, 0, 0, 0};
+      uint32_t next = 0;
+      for (size_t i = 0; i < c.size() && next < fg::kNumTopK;) {
+        const float x = c[i].first;
+        for (; i < c.size() && c[i].first == x; ++i) {  // every level scoring exactly x counts at x
+          const uint32_t s = c[i].second / L, K = fg::kLadderKs[c[i].second % L];
+          if (K > cur[s]) {
+            total += K - cur[s];
+            cur[s] = K;
+          }
+        }
+        for (; next < fg::kNumTopK && total >= fg::kTopKs[next]; ++next) res[next] = x;
+      }
+      for (uint32_t k = 0; k < fg::kNumTopK; ++k) out[(size_t)t * fg::kNumTopK + k] = res[k];
+    }
+  });
+  return FG_OK;
+}
+
+int fg_index_set_kth_floor(fg_index* ix, const float* floor, uint32_t n_terms) {
+  if (!ix) return fail(FG_EINVAL, "NULL index");
+  std::shared_ptr<const std::vector<float>> f;
+  if (floor) {
+    if (n_terms != ix->n_terms) return fail(FG_EINVAL, "floor of %u terms for a snapshot of %u", n_terms, ix->n_terms);
+    f = std::make_shared<const std::vector<float>>(floor, floor + (size_t)n_terms * fg::kNumTopK);
+  }
+  std::atomic_store(&ix->kth_floor, f);
+  return FG_OK;
+}
+
 int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512) {
   if (!ix) return fail(FG_EINVAL, "NULL index");
   if (term < ix->n_terms) {
@@ -1780,6 +1884,14 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   q_hhi.assign(nq, 0x3F800000u);
   q_hsh.assign(nq, 31);
   auto present = [&](uint32_t t) { return t < ix->n_terms && ix->off[t + 1] > ix->off[t]; };
+  // the term's K-th best alive score at level j: the snapshot's own, or the
+  // namespace-wide floor of a doc-sharded namespace's shard when higher
+  // (fg_index_set_kth_floor)
+  const std::shared_ptr<const std::vector<float>> floor = std::atomic_load(&ix->kth_floor);
+  auto kth = [&](uint32_t t, uint32_t j) {
+    const size_t x = (size_t)t * fg::kNumTopK + j;
+    return floor ? std::max(ix->ktop[x], (*floor)[x]) : ix->ktop[x];
+  };
   // histogram bins of query i: bin 0 at the starting threshold (or ub / 256), the
   // top bin at the query's largest possible score ub; ~kQBins bins between
   auto set_bins = [&](uint32_t i, float ub) {
@@ -1861,7 +1973,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       for (uint32_t j = 0; j < fg::kNumTopK && q_filter[i] == 0xFFFFFFFFu && nx == 0; ++j) {
         if (fg::kTopKs[j] < k) continue;
         float v = 0.0f;
-        for (uint32_t c = 0; c < ns; ++c) v = std::max(v, ix->ktop[(size_t)qt[c] * fg::kNumTopK + j]);
+        for (uint32_t c = 0; c < ns; ++c) v = std::max(v, kth(qt[c], j));
         if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
         break;
       }
@@ -1913,7 +2025,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     // pruning tantivy's TopDocs runs on a single TermScorer: block_wand_single_scorer)
     for (uint32_t j = 0; j < fg::kNumTopK && mt == 1 && q_filter[i] == 0xFFFFFFFFu; ++j) {
       if (fg::kTopKs[j] < k) continue;
-      const float v = ix->ktop[(size_t)qt[0] * fg::kNumTopK + j];
+      const float v = kth(qt[0], j);
       if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
       break;
     }

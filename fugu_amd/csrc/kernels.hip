@@ -2303,7 +2303,7 @@ struct KtopShared {
 template <class EachKey>
 __device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, KtopShared& sh, EachKey each_key) {
   constexpr uint32_t KM = kKtopKM;
-  if (na < kTopKs[1]) return;  // uniform: only K = 1
+  if (na < (j.ladder ? kLadderExtra[0] : kTopKs[1])) return;  // uniform: only K = 1
   uint64_t T = 0;
   if (na > KM) {
     T = select_kth(KM, sh.hist, sh.scratch, [&](auto&& f) {
@@ -2322,6 +2322,8 @@ __device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, KtopShar
   if (threadIdx.x == 0)
     for (uint32_t kk = 1; kk < kNumTopK; ++kk)
       if (nt >= kTopKs[kk]) j.ktop[(size_t)t * kNumTopK + kk] = key_score(sh.top[kTopKs[kk] - 1]);
+  if (j.ladder && threadIdx.x < kNumLadderExtra && nt >= kLadderExtra[threadIdx.x])
+    j.ladder[(size_t)t * kNumLadderExtra + threadIdx.x] = key_score(sh.top[kLadderExtra[threadIdx.x] - 1]);
 }
 
 // postings [b + p0, b + p1) as f(valid && alive, score, doc), U loads per thread
@@ -2403,6 +2405,10 @@ __global__ __launch_bounds__(kThreads) void k_ktop_tiny(ScoreJob j) {
   if (lane == 0) j.ktop[(size_t)t * kNumTopK] = key_score(key);
   for (uint32_t kk = 1; kk < kNumTopK; ++kk)
     if (kTopKs[kk] <= na && lane == kTopKs[kk] - 1) j.ktop[(size_t)t * kNumTopK + kk] = key_score(key);
+  if (j.ladder)
+    for (uint32_t kk = 0; kk < kNumLadderExtra; ++kk)
+      if (kLadderExtra[kk] <= na && lane == kLadderExtra[kk] - 1)
+        j.ladder[(size_t)t * kNumLadderExtra + kk] = key_score(key);
 }
 
 // one workgroup per term of <= kKtopChunk postings

@@ -54,8 +54,10 @@ EXPORTS = (
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore",
     "fg_index_rescore_many", "fg_index_build_global",
     "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged", "fg_index_term_kth",
-    "fg_model_batch", "fg_abi_version",
+    "fg_model_batch", "fg_abi_version", "fg_index_term_ladder", "fg_kth_floor_combine", "fg_index_set_kth_floor",
 )
+LADDER_KS = (1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000)  # FG_LADDER_LEVELS ranks
+KTH_KS = (1, 10, 20, 100, 1000)  # fg_index_term_kth / fg_index_set_kth_floor ranks
 ABI_VERSION = 4  # include/fugu.h FG_ABI_VERSION this binding's structs follow
 
 if not os.path.exists(LIB_PATH):
@@ -149,6 +151,9 @@ _sig("fg_plan_create", C.c_int, _p, C.POINTER(QueryBatch), C.c_uint32, C.POINTER
 _sig("fg_plan_create_multi", C.c_int, C.POINTER(_p), C.c_uint32, C.POINTER(QueryBatch), C.c_uint32, C.POINTER(_p))
 _sig("fg_plan_execute_merged", C.c_int, _p, _p, _p, _p, _p, _p)
 _sig("fg_index_term_kth", C.c_int, _p, C.c_uint32, _f32p)
+_sig("fg_index_term_ladder", C.c_int, _p, _f32p)
+_sig("fg_kth_floor_combine", C.c_int, C.c_uint32, C.c_uint32, C.POINTER(_f32p), _f32p)
+_sig("fg_index_set_kth_floor", C.c_int, _p, _f32p, C.c_uint32)
 _sig("fg_plan_execute", C.c_int, _p, _p, _p, _p, _p)
 _sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
@@ -447,6 +452,23 @@ class Index:
         _check(_lib.fg_index_term_kth(self._h, term, _ptr(out, _f32p)))
         return out
 
+    def term_ladder(self) -> np.ndarray:
+        """fg_index_term_ladder: [n_terms, len(LADDER_KS)] K-th best alive scores (one k_ktop pass)."""
+        V = self.stats().n_terms
+        out = np.zeros((V, len(LADDER_KS)), np.float32)
+        _check(_lib.fg_index_term_ladder(self._h, _ptr(out, _f32p)))
+        return out
+
+    def set_kth_floor(self, floor):
+        """fg_index_set_kth_floor: [n_terms, 5] namespace-wide floor of the starting thresholds (None clears)."""
+        if floor is None:
+            _check(_lib.fg_index_set_kth_floor(self._h, None, 0))
+            return
+        f = np.ascontiguousarray(floor, np.float32)
+        if f.ndim != 2 or f.shape[1] != len(KTH_KS):
+            raise ValueError(f"floor must be [n_terms, {len(KTH_KS)}]")
+        _check(_lib.fg_index_set_kth_floor(self._h, _ptr(f, _f32p), f.shape[0]))
+
     def bm25(self, term: int):
         wt, wn = C.c_float(), C.c_float()
         cache = np.zeros(512, np.float32)
@@ -601,6 +623,22 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+def kth_floor_combine(ladders) -> np.ndarray:
+    """fg_kth_floor_combine (host only): shard ladders [n_shards][n_terms, len(LADDER_KS)]
+    -> [n_terms, 5] lower bounds of the namespace-wide K-th scores (K = KTH_KS)."""
+    ls = [np.ascontiguousarray(x, np.float32) for x in ladders]
+    if not ls:
+        raise ValueError("no ladders")
+    V = ls[0].shape[0]
+    for x in ls:
+        if x.shape != (V, len(LADDER_KS)):
+            raise ValueError(f"ladder shape {x.shape}, expected ({V}, {len(LADDER_KS)})")
+    arr = (_f32p * len(ls))(*[_ptr(x, _f32p) for x in ls])
+    out = np.zeros((V, len(KTH_KS)), np.float32)
+    _check(_lib.fg_kth_floor_combine(len(ls), V, arr, _ptr(out, _f32p)))
+    return out
 
 
 def link_plans(plans):

@@ -87,6 +87,42 @@ def allreduce_stats(local, group=None, device=None):
                       out[4 + V:4 + 2 * V].astype(np.uint32), dff, int(out[3]))
 
 
+def exchange_ladders(local, group=None, device=None):
+    """All-gather the score ladders of every rank's shards ([n_local, V, L] f32,
+    fg_index_term_ladder each) -> [world * n_local, V, L] in rank order: ONE
+    all-gather at build (RCCL when `device` is the rank's cuda device).  Every
+    rank must hold the same number of shards of one vocabulary."""
+    import numpy as np
+    loc = np.ascontiguousarray(local, np.float32)
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return loc
+    world = dist.get_world_size(group)
+    t = torch.from_numpy(loc.reshape(-1))
+    if device is not None:
+        t = t.to(device)
+    out = torch.empty(world * t.numel(), dtype=torch.float32, device=t.device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return out.cpu().numpy().reshape((world * loc.shape[0],) + loc.shape[1:])
+
+
+def seed_kth_floor(indexes, group=None, device=None):
+    """Doc-sharded namespace (C5): give every shard the namespace-wide floor of its
+    per-term K-th scores, so each shard's disjunctions start from a threshold
+    valid for the whole namespace instead of its own docs' (fg_index_term_ladder
+    -> exchange_ladders -> fg_kth_floor_combine -> fg_index_set_kth_floor).  The
+    floor is score-only and the merged results are unchanged.  Returns the floor
+    [V, 5] (identical on every rank)."""
+    import numpy as np
+
+    from . import native
+    lad = np.stack([ix.term_ladder() for ix in indexes])
+    allv = exchange_ladders(lad, group, device)
+    floor = native.kth_floor_combine(list(allv))
+    for ix in indexes:
+        ix.set_kth_floor(floor)
+    return floor
+
+
 def shard_ranges(n_docs: int, world: int):
     """Contiguous doc-id ranges [b, e) of the shards (tantivy segments)."""
     step = (n_docs + world - 1) // world

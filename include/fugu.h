@@ -205,6 +205,36 @@ int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_nam
  * its disjunctions.  out[5]. */
 int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out);
 
+/* ---- doc-sharded namespaces: namespace-wide starting thresholds ----------------
+ * A shard of a doc-sharded namespace (tantivy's segments, config C5) only sees its
+ * own docs, so its per-term K-th scores bound the namespace's K-th score far
+ * below it (K = 1000 over 8 shards: the namespace's 1000th best is about each
+ * shard's 125th).  Every shard's score LADDER -- the K-th best alive score at the
+ * ranks FG_LADDER_KS -- is exchanged once at build (an all-gather), combined into
+ * per-term lower bounds of the namespace-wide K-th scores, and set on every shard
+ * as a floor of its starting thresholds.  Score-only: a doc scoring exactly the
+ * floor is still kept (the merge breaks ties by shard).  Results are unchanged;
+ * the shards' disjunctions and single-list queries start closer to their final
+ * thresholds, as a multi-snapshot plan's shards do through their shared threshold
+ * word on one device (reference: Searcher-global statistics, src/db/search.rs:162). */
+#define FG_LADDER_LEVELS 14 /* K = 1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000 */
+/* out[n_terms * FG_LADDER_LEVELS], term-major, ascending K; 0 where the term has
+ * fewer alive postings.  Runs one k_ktop pass of the snapshot on the device into
+ * temporaries (the calling thread's stream; ~10 ms for a 12.5M-doc shard). */
+int fg_index_term_ladder(const fg_index* ix, float* out);
+/* Host only: ladders[s] = shard s's fg_index_term_ladder output (n_terms terms
+ * each, one vocabulary); out[n_terms * 5] = for K = 1, 10, 20, 100, 1000 the
+ * largest score x with sum over shards of max{K_l : ladder_s(K_l) >= x} >= K,
+ * i.e. at least K docs of the namespace score >= x: a lower bound of the term's
+ * namespace-wide K-th best alive score. */
+int fg_kth_floor_combine(uint32_t n_shards, uint32_t n_terms, const float* const* ladders, float* out);
+/* Set (or replace; floor = NULL clears) the snapshot's floor of its per-term K-th
+ * scores for K = 1, 10, 20, 100, 1000: plans created afterwards start their
+ * thresholds from max(own K-th score, floor).  floor[n_terms * 5] is copied; a
+ * floor that is not a valid lower bound of the namespace-wide K-th scores can drop
+ * hits.  Safe against concurrent plan creation (plans see the old or new floor). */
+int fg_index_set_kth_floor(fg_index* ix, const float* floor, uint32_t n_terms);
+
 /* ---- query batches -------------------------------------------------------- */
 typedef struct fg_query_batch {
   uint32_t n_queries;

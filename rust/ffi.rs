@@ -202,6 +202,9 @@ extern "C" {
     pub fn fg_index_bm25(ix: *const fg_index, term: u32, w_text: *mut f32, w_name: *mut f32, cache512: *mut f32)
                          -> c_int;
     pub fn fg_index_term_kth(ix: *const fg_index, term: u32, out: *mut f32) -> c_int;  // K = 1, 10, 20, 100, 1000
+    pub fn fg_index_term_ladder(ix: *const fg_index, out: *mut f32) -> c_int;  // [n_terms * FG_LADDER_LEVELS]
+    pub fn fg_kth_floor_combine(n_shards: u32, n_terms: u32, ladders: *const *const f32, out: *mut f32) -> c_int;
+    pub fn fg_index_set_kth_floor(ix: *mut fg_index, floor: *const f32, n_terms: u32) -> c_int;
 
     // ---- query batches: the searcher.search(.., TopDocs::with_limit(k)) replacement
     pub fn fg_plan_create(ix: *mut fg_index, q: *const fg_query_batch, k: u32, out: *mut *mut fg_plan) -> c_int;

@@ -1,0 +1,126 @@
+"""Namespace-wide starting thresholds of doc shards on the device
+(fg_index_term_ladder, fg_kth_floor_combine, fg_index_set_kth_floor).
+
+- a shard's ladder (one k_ktop pass into temporaries) equals the K-th scores of
+  the term's own top-1000 list from a single-term search of that shard, and its
+  main columns equal fg_index_term_kth;
+- the combined floor never exceeds the namespace-wide K-th score of the term
+  (the oracle's single-term search over the whole corpus with its statistics);
+- shards searched with the floor return exactly the hits they return without it,
+  and the oracle's segmented search (OR top-k for k in 10..1000, single-term
+  queries, AND): the floor only moves where each shard starts pruning.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def native():
+    from fugu_amd import native as nat
+    if nat.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    return nat
+
+
+@pytest.fixture(scope="module")
+def shards(native):
+    from fugu_amd import synth
+    from fugu_amd.shard import shard_ranges
+    from oracle import oracle as orc
+    ctx = native.Context((0,))
+    c = synth.corpus(400_000)
+    V = synth.VOCAB
+    ranges = shard_ranges(c.n_docs, 4)
+    parts = [(c.off[b:e + 1] - c.off[b], c.tok[c.off[b]:c.off[e]]) for b, e in ranges]
+    g = None
+    for off, tok in parts:
+        x = native.docs_stats(off, tok, V, threads=16)
+        g = x if g is None else g + x
+    ixs = [native.Index.from_docs(ctx, off, tok, V, threads=16, keep_host=False, global_stats=g) for off, tok in parts]
+    ref = orc.OracleIndex(V, c.off, c.tok, threads=16)
+    return ctx, c, ranges, ixs, ref
+
+
+def test_ladder_equals_single_term_lists(native, shards):
+    ctx, c, ranges, ixs, ref = shards
+    terms = np.array([1, 2, 3, 7, 40, 300, 2000, 9000, 60000, 500000], np.uint32)
+    LK = np.array(native.LADDER_KS)
+    main = [list(LK).index(k) for k in native.KTH_KS]
+    for ix in ixs[:2]:
+        lad = ix.term_ladder()
+        q_off = np.arange(len(terms) + 1, dtype=np.uint32)
+        s, d, n = ix.search_batch(q_off, terms, 1000)
+        for i, t in enumerate(terms):
+            exp = np.array([s[i, k - 1] if k <= n[i] else 0.0 for k in LK], np.float32)
+            assert np.array_equal(lad[t], exp), (int(t), lad[t], exp)
+            assert np.array_equal(lad[t, main], ix.term_kth(int(t)))
+
+
+def test_floor_bounds_namespace_kth(native, shards):
+    from fugu_amd.shard import seed_kth_floor
+    ctx, c, ranges, ixs, ref = shards
+    floor = seed_kth_floor(ixs)
+    LKK = native.KTH_KS
+    own = np.stack([[ix.term_kth(int(t)) for t in range(1, 4000, 37)] for ix in ixs]).max(axis=0)
+    for row, t in enumerate(range(1, 4000, 37)):
+        rs, rd = ref.search(np.array([t], np.uint32), 1000, mode=1)
+        for j, K in enumerate(LKK):
+            exact = rs[K - 1] if K <= len(rs) else 0.0
+            assert floor[t, j] <= exact * (1 + 1e-7), (t, K, floor[t, j], exact)
+            assert floor[t, j] >= own[row, j]
+    # what pruning gains: at K = 1000 over 4 shards the floor sits above every shard's own 1000th
+    sample = floor[1:4000:37, 4]
+    has = own[:, 4] > 0
+    assert has.sum() > 20 and (sample[has] > own[has, 4]).mean() > 0.9
+    for ix in ixs:
+        ix.set_kth_floor(None)
+
+
+@pytest.mark.parametrize("m0,m1,k,mode", [(2, 5, 1000, 1), (2, 4, 100, 1), (2, 3, 20, 1), (2, 5, 10, 1),
+                                          (1, 1, 100, 0), (1, 1, 1000, 0), (3, 3, 100, 0)])
+def test_seeded_shards_same_hits(native, shards, m0, m1, k, mode):
+    from fugu_amd import synth
+    from fugu_amd.shard import seed_kth_floor
+    ctx, c, ranges, ixs, ref = shards
+    q_off, terms = synth.queries(96, m0, m1, seed_q=11)
+    for ix in ixs:
+        ix.set_kth_floor(None)
+    s0, d0, sh0, n0 = native.search_sharded(ixs, q_off, terms, k, mode=mode, ctx=ctx)
+    # every shard alone (no shared threshold) with and without the floor, merged on the host
+    per0 = [ix.search_batch(q_off, terms, k, mode=mode) for ix in ixs]
+    seed_kth_floor(ixs)
+    try:
+        s1, d1, sh1, n1 = native.search_sharded(ixs, q_off, terms, k, mode=mode, ctx=ctx)
+        per1 = [ix.search_batch(q_off, terms, k, mode=mode) for ix in ixs]
+    finally:
+        for ix in ixs:
+            ix.set_kth_floor(None)
+    assert np.array_equal(n0, n1)
+    for i in range(len(n0)):
+        m = int(n0[i])
+        assert np.array_equal(d0[i, :m], d1[i, :m]) and np.array_equal(sh0[i, :m], sh1[i, :m])
+        assert np.array_equal(s0[i, :m], s1[i, :m])
+    from shard_ref import merge_topk_numpy
+    merged = []
+    for per in (per0, per1):
+        sc = np.stack([p[0] for p in per])
+        dc = np.stack([p[1] for p in per])
+        nn = np.stack([p[2] for p in per]).astype(np.int64)
+        merged.append(merge_topk_numpy(sc, dc, nn, k))
+    ms0, md0, msh0, mn0 = merged[0]
+    ms1, md1, msh1, mn1 = merged[1]
+    assert np.array_equal(mn0, mn1) and np.array_equal(mn0, n0.astype(mn0.dtype))
+    base = np.array([b for b, _ in ranges], np.uint64)
+    bounds = np.array([b for b, _ in ranges] + [c.n_docs], np.uint32)
+    for i in range(len(n0)):
+        m = int(mn0[i])
+        assert np.array_equal(md0[i, :m], md1[i, :m]) and np.array_equal(msh0[i, :m], msh1[i, :m])
+        rs, rd = ref.search_segments(terms[q_off[i]:q_off[i + 1]], k, bounds, mode=mode)
+        assert m == len(rd)
+        gdoc = md1[i, :m].astype(np.uint64) + base[msh1[i, :m]]
+        assert np.array_equal(gdoc, rd.astype(np.uint64))
+        rel = np.abs(ms1[i, :m].astype(np.float64) - rs) / np.maximum(np.abs(rs), 1e-30)
+        assert (rel <= RTOL).all()
