@@ -186,17 +186,21 @@ def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
     import threading
     batches = [synth.queries(nq, 3, 3, seed_q=1000 + i) for i in range(steps + workers)]
     streams = [torch.cuda.Stream(dev) for _ in range(workers)]
-    plan_ms, errors = [], []
+    plan_ms, run_ms, close_ms, errors = [], [], [], []
 
     def work(w, idxs):
         try:
             for i in idxs:
                 t1 = time.perf_counter()
                 p = ix.plan(batches[i][0], batches[i][1], K)
-                plan_ms.append((time.perf_counter() - t1) * 1e3)
+                t2 = time.perf_counter()
                 p.execute(streams[w].cuda_stream)
                 p.results()
+                t3 = time.perf_counter()
                 p.close()
+                plan_ms.append((t2 - t1) * 1e3)
+                run_ms.append((t3 - t2) * 1e3)
+                close_ms.append((time.perf_counter() - t3) * 1e3)
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))
 
@@ -209,6 +213,8 @@ def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
 
     run(list(range(steps, steps + workers)))  # warm the workspace pool and the streams
     plan_ms.clear()
+    run_ms.clear()
+    close_ms.clear()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(list(range(steps)))
@@ -219,8 +225,14 @@ def e2e_pipeline(ix, native, synth, torch, dev, nq, K, steps, workers):
     return {"value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_batch": round(el * 1e3 / steps, 3),
             "batches": steps, "batch": nq, "k": K, "workers": workers,
             "plan_ms_per_batch_p50": round(float(np.median(plan_ms)), 3),
+            "breakdown_ms_p50": {"plan_host": round(float(np.median(plan_ms)), 3),
+                                 "execute_to_hits_on_host": round(float(np.median(run_ms)), 3),
+                                 "plan_destroy": round(float(np.median(close_ms)), 3)},
+            "breakdown_ms_p90": {"plan_host": round(float(np.percentile(plan_ms, 90)), 3),
+                                 "execute_to_hits_on_host": round(float(np.percentile(run_ms, 90)), 3)},
             "note": "each step = a different 3-term AND batch: host planning + H2D + k_conj + k_final + D2H of the "
-                    "hits, pipelined over the workers' streams (planning overlaps other batches' kernels)"}
+                    "hits, pipelined over the workers' streams (planning overlaps other batches' kernels); "
+                    "execute_to_hits_on_host includes waiting behind the other workers' kernels on the GPU"}
 
 
 def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
@@ -247,17 +259,37 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     ingest_s = time.time() - t0
     q_off, terms = synth.queries(nq, 2, 5, seed_q=333)
     qs = [" ".join(f"t{t}" for t in terms[q_off[i]:q_off[i + 1]]) for i in range(nq)]
+    # the JSON handler on queries of its own (not a warm repeat of a query just run)
+    qj_off, qj_terms = synth.queries(nq, 2, 5, seed_q=334)
+    qjs = [" ".join(f"t{t}" for t in qj_terms[qj_off[i]:qj_off[i + 1]]) for i in range(nq)]
     for q in qs[:8]:
         d.search("api", q, 0, 20)
     lat, lat_json, mism = [], [], 0
+    got_all = []
     for i, q in enumerate(qs):
         t1 = time.perf_counter()
-        got = d.search("api", q, 0, 20)
+        got_all.append(d.search("api", q, 0, 20))
         lat.append(time.perf_counter() - t1)
+    for q in qjs:
         t1 = time.perf_counter()
         d.search_json("api", q, 0, 20)
         lat_json.append(time.perf_counter() - t1)
-        if ref is not None:
+    # the same queries again with the phase trace on (fg_search_trace): where a
+    # GET /search batch of one spends its time
+    fdb.search_trace(1)
+    fdb.search_trace()
+    for q in qs:
+        d.search("api", q, 0, 20)
+    ph = fdb.search_trace(0)
+    phases = {k: round(v / max(ph["calls"], 1), 4) for k, v in ph.items() if k not in ("calls", "json_fetch")}
+    fdb.search_trace(1)
+    fdb.search_trace()
+    for q in qjs:
+        d.search_json("api", q, 0, 20)
+    phj = fdb.search_trace(0)
+    phases["json_fetch"] = round(phj["json_fetch"] / max(phj["calls"], 1), 4)
+    if ref is not None:
+        for i, got in enumerate(got_all):
             rs, rd = ref.search(terms[q_off[i]:q_off[i + 1]], 20, mode=1)
             if [g[1] for g in got] != rd.tolist() or not np.allclose([g[0] for g in got], rs, rtol=1e-5, atol=0):
                 mism += 1
@@ -265,9 +297,11 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     out = {"p50_ms": pct(lat, 50), "p90_ms": pct(lat, 90), "p99_ms": pct(lat, 99),
            "json_p50_ms": pct(lat_json, 50), "json_p99_ms": pct(lat_json, 99), "queries": nq, "segments": n_seg,
            "k": 20, "mode": "OR (bare terms)", "ingest_s": round(ingest_s, 1), "n_docs": corp.n_docs,
+           "phases_ms_mean": phases,
            "note": "batch of one through fg_db_search (parse + dictionary + fg_search_sharded over the namespace's "
                    "8 commit segments + device merge + hits out); json_*: the GET /search handler shape with the "
-                   "20 docs fetched from the host doc store"}
+                   "20 docs fetched from the host doc store, on queries of its own; phases_ms_mean: fg_search_trace "
+                   "means per call (a second pass over the same queries with the trace on)"}
     if ref is not None:
         out["parity"] = {"queries_checked": nq, "mismatches": mism}
     # ---- commits on the 10M namespace: 16 consecutive POST
@@ -280,6 +314,26 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     tb2, to2 = synth.render_text(new, threads)
     ib2, io2 = synth.render_ids(n_new * n_commits, doc_begin=corp.n_docs)
     lat_c = []
+    # GET /search from a reader thread the whole time the commits (and the
+    # merges they queue) run: ctypes drops the GIL inside both calls, so the
+    # reader searches while the writer gathers, builds and swaps
+    import threading
+    stop = threading.Event()
+    lat_r, err_r = [], []
+
+    def reader():
+        i = 0
+        try:
+            while not stop.is_set():
+                t1 = time.perf_counter()
+                d.search("api", qs[i % nq], 0, 20)
+                lat_r.append(time.perf_counter() - t1)
+                i += 1
+        except Exception as e:  # noqa: BLE001
+            err_r.append(repr(e))
+
+    th = threading.Thread(target=reader)
+    th.start()
     t_all = time.perf_counter()
     for c in range(n_commits):
         a, b = c * n_new, (c + 1) * n_new
@@ -288,8 +342,17 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
                        text_buf=tb2[int(to2[a]):int(to2[b])], text_off=to2[a:b + 1] - to2[a])
         lat_c.append(time.perf_counter() - t1)
     t_commits = time.perf_counter() - t_all
+    stop.set()
+    th.join()
+    if err_r:
+        raise RuntimeError(err_r[0])
     d.merge_wait("api")
     t_done = time.perf_counter() - t_all
+    out["during_commits"] = {"p50_ms": pct(lat_r, 50), "p90_ms": pct(lat_r, 90), "p99_ms": pct(lat_r, 99),
+                             "max_ms": round(max(lat_r) * 1e3, 3), "searches": len(lat_r),
+                             "p99_over_idle_p99": round(pct(lat_r, 99) / max(out["p99_ms"], 1e-9), 3),
+                             "note": "GET /search (fg_db_search, OR limit 20) back to back from a second thread while "
+                                     "the 16 commits of commit_10M run; the read path takes no writer lock"}
     mi = d.merge_info("api")
     ms = [x * 1e3 for x in lat_c]
     commits = {"commits": n_commits, "docs_per_commit": n_new, "base_docs": corp.n_docs,

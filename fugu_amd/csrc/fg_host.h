@@ -16,6 +16,7 @@
 
 #include "../../include/fugu.h"
 #include "fg_internal.h"
+#include "fg_trace.h"
 
 namespace fgh {
 

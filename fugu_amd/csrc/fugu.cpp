@@ -2824,6 +2824,24 @@ static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32
 // DocAddress (segment_ord, doc).  Everything runs on the calling thread's
 // per-thread streams.  FUGU_SHARDED_PER_SHARD=1 selects the round-2 path (one
 // plan per shard, linked; A/B builds).
+}  // extern "C"
+namespace fgh {
+SearchTrace& search_trace() {
+  static SearchTrace t;
+  return t;
+}
+}  // namespace fgh
+extern "C" {
+
+int fg_search_trace(int enable, double* out_ms, uint32_t n, uint64_t* calls) {
+  fgh::SearchTrace& t = fgh::search_trace();
+  if (out_ms)
+    for (uint32_t i = 0; i < n; ++i) out_ms[i] = i < fgh::kNumPhases ? (double)t.ns[i].exchange(0) * 1e-6 : 0.0;
+  if (calls) *calls = t.calls.exchange(0);
+  if (enable >= 0) t.on.store(enable ? 1 : 0);
+  return FG_OK;
+}
+
 int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
                       float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
   static const bool per_shard = getenv("FUGU_SHARDED_PER_SHARD") != nullptr;
@@ -2886,7 +2904,9 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       ix0->pool.put(p, n);
     }
   } back{gdev, dev0, shards[0], base, got, evs};
-  static const bool trace = getenv("FUGU_SHARD_TRACE") != nullptr;
+  static const bool trace_env = getenv("FUGU_SHARD_TRACE") != nullptr;
+  fgh::SearchTrace& st = fgh::search_trace();
+  const bool trace = trace_env || st.enabled();
   auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_0 = trace ? now() : 0.0;
   double t_plan = 0.0;
@@ -2953,11 +2973,21 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   for (hipEvent_t e : evs)
     if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
   if (!merged) HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
-  if (trace) {
+  if (trace_env) {
     HIPCHK(hipStreamSynchronize(hipStreamPerThread));
     fprintf(stderr, "[fg_search_sharded] nq %u shards %u devices %zu merged %d: plan %.3f launch %.3f kernels+merge %.3f ms\n",
             nq, n_shards, ng, (int)merged, t_plan, t_run - t_0 - t_plan, now() - t_run);
   }
+  // the search trace's phases: planning, launches, then the wait for the hits
+  struct PhaseOut {
+    fgh::SearchTrace& st; bool on; double t0, tp, tr; double (*clk)();
+    ~PhaseOut() {
+      if (!on) return;
+      st.add(fgh::kPhPlan, (uint64_t)(tp * 1e6));
+      st.add(fgh::kPhLaunch, (uint64_t)((tr - t0 - tp) * 1e6));
+      st.add(fgh::kPhWait, (uint64_t)((clk() - tr) * 1e6));
+    }
+  } phase_out{st, st.enabled(), t_0, t_plan, t_run, +now};
   // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
   const size_t span = 3 * o_k + 4ull * nq;
   if (span <= (4ull << 20)) {

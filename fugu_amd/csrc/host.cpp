@@ -15,6 +15,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <stdexcept>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -28,6 +29,7 @@
 
 #include "../../include/fugu.h"
 #include "../../include/fugu_host.h"
+#include "fg_trace.h"
 
 void fg_set_last_error(const std::string& msg);  // fugu.cpp
 int fg_host_threads();                           // fugu.cpp: FUGU_THREADS / the process's CPU share
@@ -198,56 +200,137 @@ struct LocalDict {
   }
 };
 
-// A namespace's term dictionary (term -> id, ids in insertion order): open
-// addressing over an arena, each slot holding the hash's high half beside the
-// id, so a lookup touches one slot line and, on a hash match, the term's bytes
-// (a node-based map chased two or three pointers per lookup; a 1000-doc upsert
-// looks up ~20K distinct words in a dictionary of 10^6 terms).
+// Storage that never moves once published: a directory of atomic pointers to
+// fixed-size chunks.  One writer appends; readers index any slot published
+// before they looked (acquire on the chunk pointer) without a lock.
+template <class T, uint32_t kShift, uint32_t kMaxChunks>
+class ChunkDir {
+  std::unique_ptr<std::atomic<T*>[]> dir_{new std::atomic<T*>[kMaxChunks]()};
+  std::vector<std::unique_ptr<T[]>> own_;  // writer side
+
+ public:
+  static constexpr size_t kChunk = size_t(1) << kShift;
+  T& at(size_t i) const { return dir_[i >> kShift].load(std::memory_order_acquire)[i & (kChunk - 1)]; }
+  // the writer: slot i, its chunk allocated (and published) first if new
+  T& slot(size_t i) {
+    const size_t c = i >> kShift;
+    if (c >= kMaxChunks) throw std::length_error("ChunkDir full");
+    T* p = dir_[c].load(std::memory_order_relaxed);
+    if (!p) {
+      own_.emplace_back(new T[kChunk]());
+      p = own_.back().get();
+      dir_[c].store(p, std::memory_order_release);
+    }
+    return p[i & (kChunk - 1)];
+  }
+};
+
+// A namespace's term dictionary (term -> id, ids in insertion order) whose
+// lookups take no lock: the query path never waits on the IndexWriter, as in
+// the reference (the searcher of each query reads committed segments,
+// src/db/search.rs:86-87, while writers serialise on their own mutex,
+// src/db/core.rs:211).  One writer (under Namespace::writer) inserts.  Term
+// bytes and entries live in chunks that never move; the open-addressing table
+// (hash's high half beside id + 1, one slot line per probe) is published by one
+// release store per slot after the entry and bytes it points at, and replaced
+// whole when it grows (old tables are kept: a reader may still probe one, and
+// they add up to less than the current table).  A reader that finds no slot for
+// a term interned after it looked reports it missing, which it also is in every
+// snapshot the reader can hold.  (A node-based map chased two or three pointers
+// per lookup; a 1000-doc upsert looks up ~20K distinct words in a dictionary of
+// 10^6 terms.)
 struct TermDict {
   static constexpr uint32_t kMissing = 0xFFFFFFFFu;
-  std::string arena;
-  std::vector<uint64_t> ent;                                  // by id: arena offset << 8 | length
-  std::vector<uint64_t> slot = std::vector<uint64_t>(1u << 16, 0);  // (hash >> 32) << 32 | (id + 1); 0 = empty
-  uint32_t size() const { return (uint32_t)ent.size(); }
+  static constexpr size_t kMaxKey = (1u << 20) - 1;  // bytes per term (tokens are < 40, facet paths short)
+  struct Table {
+    std::unique_ptr<std::atomic<uint64_t>[]> s;
+    size_t mask;
+    explicit Table(size_t n) : s(new std::atomic<uint64_t>[n]()), mask(n - 1) {}
+  };
+  // entry of id: arena chunk << 40 | offset in it << 20 | length
+  ChunkDir<uint64_t, 16, 1u << 16> ent;
+  ChunkDir<char, 20, 1u << 16> arena;
+  size_t a_chunk = 0, a_pos = 0;  // writer: where the next term's bytes go
+  std::atomic<uint32_t> n{0};
+  std::atomic<Table*> cur;
+  std::vector<std::unique_ptr<Table>> tables;  // writer: current and retired
+  TermDict() {
+    tables.emplace_back(new Table(1u << 16));
+    cur.store(tables.back().get(), std::memory_order_release);
+  }
+  uint32_t size() const { return n.load(std::memory_order_acquire); }
   static uint64_t hash(std::string_view w) { return LocalDict::hash(w); }
   std::string_view key(uint32_t id) const {
-    return std::string_view(arena.data() + (ent[id] >> 8), ent[id] & 0xFF);
+    const uint64_t e = ent.at(id);
+    const char* c = &arena.at((e >> 40) << 20);
+    return std::string_view(c + ((e >> 20) & kMaxKey), e & kMaxKey);
   }
-  void prefetch(uint64_t h) const { __builtin_prefetch(&slot[h & (slot.size() - 1)]); }
+  void prefetch(uint64_t h) const {
+    const Table* t = cur.load(std::memory_order_relaxed);
+    __builtin_prefetch(&t->s[h & t->mask]);
+  }
   uint32_t find(std::string_view w, uint64_t h) const {
-    for (size_t m = slot.size() - 1, i = h & m;; i = (i + 1) & m) {
-      const uint64_t x = slot[i];
+    const Table* t = cur.load(std::memory_order_acquire);
+    for (size_t i = h & t->mask;; i = (i + 1) & t->mask) {
+      const uint64_t x = t->s[i].load(std::memory_order_acquire);
       if (!x) return kMissing;
       if ((x >> 32) == (h >> 32) && key((uint32_t)x - 1) == w) return (uint32_t)x - 1;
     }
   }
   uint32_t find(std::string_view w) const { return find(w, hash(w)); }
-  uint32_t get(std::string_view w, uint64_t h) {  // find, else insert with the next id
+  static void put(Table& t, uint64_t h, uint32_t id) {
+    for (size_t i = h & t.mask;; i = (i + 1) & t.mask)
+      if (!t.s[i].load(std::memory_order_relaxed)) {
+        t.s[i].store(((h >> 32) << 32) | (id + 1ull), std::memory_order_release);
+        return;
+      }
+  }
+  uint32_t get(std::string_view w, uint64_t h) {  // the writer: find, else insert with the next id
     const uint32_t f = find(w, h);
     if (f != kMissing) return f;
-    if (2 * (ent.size() + 1) > slot.size()) grow();
-    const uint32_t id = (uint32_t)ent.size();
-    ent.push_back(((uint64_t)arena.size() << 8) | w.size());
-    arena.append(w.data(), w.size());
-    for (size_t m = slot.size() - 1, i = h & m;; i = (i + 1) & m)
-      if (!slot[i]) {
-        slot[i] = ((h >> 32) << 32) | (id + 1ull);
-        break;
-      }
+    if (w.size() > kMaxKey) throw std::length_error("term longer than 1 MiB");
+    const uint32_t id = n.load(std::memory_order_relaxed);
+    if (2 * (size_t(id) + 1) > cur.load(std::memory_order_relaxed)->mask + 1) grow();
+    if (a_pos + w.size() > decltype(arena)::kChunk) {
+      ++a_chunk;
+      a_pos = 0;
+    }
+    char* dst = &arena.slot((a_chunk << 20) + a_pos);  // publishes the chunk when new
+    std::memcpy(dst, w.data(), w.size());
+    ent.slot(id) = ((uint64_t)a_chunk << 40) | ((uint64_t)a_pos << 20) | w.size();
+    a_pos += w.size();
+    n.store(id + 1, std::memory_order_release);
+    put(*cur.load(std::memory_order_relaxed), h, id);
     return id;
   }
   uint32_t get(std::string_view w) { return get(w, hash(w)); }
   void grow() {
-    std::vector<uint64_t> ns(slot.size() * 2, 0);
-    for (uint32_t id = 0; id < ent.size(); ++id) {
-      const uint64_t h = hash(key(id));
-      for (size_t m = ns.size() - 1, i = h & m;; i = (i + 1) & m)
-        if (!ns[i]) {
-          ns[i] = ((h >> 32) << 32) | (id + 1ull);
-          break;
-        }
-    }
-    slot.swap(ns);
+    const Table* old = cur.load(std::memory_order_relaxed);
+    auto t = std::make_unique<Table>((old->mask + 1) * 2);
+    const uint32_t nn = n.load(std::memory_order_relaxed);
+    for (uint32_t id = 0; id < nn; ++id) put(*t, hash(key(id)), id);
+    cur.store(t.get(), std::memory_order_release);
+    tables.push_back(std::move(t));
+  }
+};
+
+// A namespace's docs by global id (insertion order): appended by the writer,
+// read by searches' doc fetch without a lock (chunks never move; a search only
+// reads docs of a committed snapshot, all appended before it was published).
+// Only `deleted`, which the read path never touches, changes after an append.
+template <class Doc>
+class DocStore {
+  ChunkDir<Doc, 14, 1u << 18> c_;
+  std::atomic<size_t> n_{0};
+
+ public:
+  size_t size() const { return n_.load(std::memory_order_acquire); }
+  const Doc& operator[](size_t i) const { return c_.at(i); }
+  Doc& operator[](size_t i) { return c_.at(i); }  // the writer
+  void push_back(Doc&& d) {
+    const size_t i = n_.load(std::memory_order_relaxed);
+    c_.slot(i) = std::move(d);
+    n_.store(i + 1, std::memory_order_release);
   }
 };
 
@@ -743,9 +826,10 @@ struct Namespace {
   std::mutex writer;                                   // IndexWriter lock (src/db/core.rs:211)
   std::mutex committer;                                // serialises commits and merge swaps (snapshot order)
   std::mutex merging;                                  // one merge of this namespace at a time
-  // global doc id = insertion order; a deque: appending never moves the ~250 B
-  // Doc records (a vector's reallocation moved all 10M of them inside a commit)
-  std::deque<Doc> docs;
+  // global doc id = insertion order; chunked: appending never moves the ~250 B
+  // Doc records (a vector's reallocation moved all 10M of them inside a commit),
+  // and searches read them without the writer lock
+  DocStore<Doc> docs;
   std::vector<uint8_t> del;                            // del[d] == docs[d].deleted (commits copy this, not the docs)
   // docs deleted by upserts since the last commit, in order: a delete takes
   // effect at the commit (IndexWriter::delete_term), so a merge in between
@@ -753,7 +837,7 @@ struct Namespace {
   std::vector<uint32_t> pend_del;
   bool any_name = false;                               // some doc has a name field
   TermDict dict;                                       // term dictionary (text and name tokens)
-  std::unordered_map<std::string, uint32_t> fdict;     // facet dictionary (encoded facet terms)
+  TermDict fdict;                                      // facet dictionary (encoded facet terms), same rules
   std::unordered_map<std::string, std::vector<uint32_t>> by_id_token;
   std::shared_ptr<Snapshot> snap;                      // committed device snapshot
   std::shared_mutex snap_mu;
@@ -905,6 +989,16 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
                 uint32_t per_page, std::vector<fg_hit>& hits) {
   (void)db;
   hits.clear();
+  fgh::SearchTrace& trace = fgh::search_trace();
+  const uint64_t t_in = trace.enabled() ? fgh::now_ns() : 0;
+  struct TotalOut {
+    fgh::SearchTrace& t; uint64_t t0;
+    ~TotalOut() {
+      if (!t0) return;
+      t.add(fgh::kPhTotal, fgh::now_ns() - t0);
+      t.calls.fetch_add(1, std::memory_order_relaxed);
+    }
+  } total_out{trace, t_in};
   if (per_page == 0) return hfail(FG_EINVAL, "TopDocs::with_limit requires limit >= 1");
   const std::string_view qv = query ? query : "";
   std::vector<std::string> terms;
@@ -928,17 +1022,16 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
     std::shared_lock<std::shared_mutex> l(ns.snap_mu);
     snap = ns.snap;
   }
-  {
-    // term ids are stable once interned; ids interned after the snapshot are >= its n_terms
-    std::lock_guard<std::mutex> w(ns.writer);
-    for (auto& t : terms) {
-      const uint32_t id = ns.dict.find(t);
-      ids.push_back(id == TermDict::kMissing ? FG_TERM_MISSING : id);
-    }
-    for (auto& c : clauses) {
-      auto it = ns.fdict.find(c);
-      fids.push_back(it == ns.fdict.end() ? FG_TERM_MISSING : it->second);
-    }
+  // no lock: term ids are stable once interned, and ids interned after the
+  // snapshot are >= its n_terms (they match nothing there) -- a commit's gather,
+  // an upsert's dictionary merge or a merge never holds up a search
+  for (auto& t : terms) {
+    const uint32_t id = ns.dict.find(t);
+    ids.push_back(id == TermDict::kMissing ? FG_TERM_MISSING : id);
+  }
+  for (auto& c : clauses) {
+    const uint32_t id = ns.fdict.find(c);
+    fids.push_back(id == TermDict::kMissing ? FG_TERM_MISSING : id);
   }
   if (!snap) return FG_OK;  // nothing committed yet: no hits
   // every segment answers the query (TopDocs::with_limit(offset + per_page) per
@@ -954,6 +1047,7 @@ int search_hits(fg_db* db, Namespace& ns, const char* query, const std::vector<s
   std::vector<float> sc(limit);
   std::vector<uint32_t> dc(limit), sh(limit);
   uint32_t n = 0;
+  if (t_in) trace.add(fgh::kPhParse, fgh::now_ns() - t_in);
   int rc = fg_search_sharded(nullptr, segs.data(), (uint32_t)segs.size(), &qb, (uint32_t)limit, sc.data(), dc.data(),
                              sh.data(), &n);
   if (rc) return hfail(rc, fg_last_error());
@@ -1044,6 +1138,11 @@ int search_json(fg_db* db, const char* nsname, const std::string& q, const std::
   if (!post_search && (per_page == 0 || per_page > 100)) per_page = 20;
   std::vector<fg_hit> hits;
   int rc = search_hits(db, *ns, q.c_str(), fl, page, per_page, hits);
+  fgh::SearchTrace& trace = fgh::search_trace();
+  struct FetchOut {
+    fgh::SearchTrace& t; uint64_t t0;
+    ~FetchOut() { if (t0) t.add(fgh::kPhFetch, fgh::now_ns() - t0); }
+  } fetch_out{trace, trace.enabled() ? fgh::now_ns() : 0};
   if (rc) {
     // perform_search wraps Dataset::search's error once, its handler again
     std::string o = "{\"error\":";
@@ -1055,9 +1154,11 @@ int search_json(fg_db* db, const char* nsname, const std::string& q, const std::
   const bool with_text = post_search || include_text;
   std::string res = "[";
   {
-    std::lock_guard<std::mutex> w(ns->writer);
+    // the stored fields of committed docs never change: no lock (searcher.doc
+    // reads the committed segments' doc stores, src/db/search.rs:172-211)
+    const DocStore<Doc>& docs = ns->docs;
     for (size_t i = 0; i < hits.size(); ++i) {
-      const Doc& d = ns->docs[hits[i].doc];
+      const Doc& d = docs[hits[i].doc];
       if (i) res.push_back(',');
       // FuguSearchResult {id, score, text, metadata, facets} (src/db/search.rs:20-27, 534-590) as a Value
       res += "{\"facets\":";
@@ -1181,11 +1282,7 @@ std::vector<uint32_t> intern_facet(Namespace& ns, const std::vector<std::string>
   std::vector<std::string> toks;
   for (auto& e : enc) {
     facet_tokens(e, toks);
-    for (auto& t : toks) {
-      auto it = ns.fdict.find(t);
-      if (it == ns.fdict.end()) it = ns.fdict.emplace(t, (uint32_t)ns.fdict.size()).first;
-      ids.push_back(it->second);
-    }
+    for (auto& t : toks) ids.push_back(ns.fdict.get(t));
   }
   return ids;
 }
@@ -1260,6 +1357,8 @@ int upsert_record(fg_db* db, const char* nsname, const fg_object_record* r, cons
     std::string enc;
     if (facet_from_text(pth, enc)) doc.facets.push_back(std::move(enc));  // add_facets_to_document skips failures
   }
+  for (auto& e : doc.facets)  // (a facet token is a prefix of its path)
+    if (e.size() > TermDict::kMaxKey) return hfail(FG_EINVAL, "facet path longer than 1 MiB");
   std::lock_guard<std::mutex> w(ns->writer);
   // w.delete_term(Term::from_field_text(id_field, &object.id)) (src/db/document.rs:38-42): the
   // RAW id is matched against the tokens of the tokenized `id` field, so ids with

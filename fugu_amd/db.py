@@ -28,7 +28,9 @@ HOST_EXPORTS = (
     "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query", "fg_parse_query_occur",
     "fg_db_upsert_record", "fg_db_upsert_batch", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
     "fg_facet_clauses", "fg_db_search_json_post", "fg_db_merge_wait", "fg_db_merge_info_get", "fg_db_segment_docs",
+    "fg_search_trace",
 )
+SEARCH_PHASES = ("parse_dict", "plan", "launch", "wait_kernels_d2h", "json_fetch", "total")  # FG_SEARCH_PHASES
 
 _lib = native.lib()
 _p = C.c_void_p
@@ -85,6 +87,7 @@ _sig("fg_db_doc_facets", _p, _s, C.c_uint32, _s, _sz, C.POINTER(_sz))
 _sig("fg_facet_tokens", _s, _s, _sz, C.POINTER(_sz))
 _sig("fg_facet_clauses", C.POINTER(_s), C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
 _sig("fg_analyze", _s, _s, _sz, C.POINTER(_sz))
+_sig("fg_search_trace", C.c_int, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint64))
 _sig("fg_parse_query", _s, C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
 _sig("fg_parse_query_occur", _s, _s, _sz, C.POINTER(_sz))
 
@@ -145,6 +148,15 @@ def facet_clauses(filters):
     a, al = C.c_int(0), C.c_int(0)
     out = _string_call(_lib.fg_facet_clauses, arr, n, C.byref(a), C.byref(al))
     return bool(a.value), bool(al.value), (out.split("\n") if (a.value and not al.value) else [])
+
+
+def search_trace(enable: int = -1) -> dict:
+    """fg_search_trace: the summed phase ms of every search since the last read
+    (reset), the number of fg_db_search* calls; enable 1 / 0 switches tracing."""
+    ms = (C.c_double * len(SEARCH_PHASES))()
+    n = C.c_uint64(0)
+    _check(_lib.fg_search_trace(enable, ms, len(SEARCH_PHASES), C.byref(n)))
+    return {"calls": n.value, **{k: ms[i] for i, k in enumerate(SEARCH_PHASES)}}
 
 
 def analyze(text: str) -> list:

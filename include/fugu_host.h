@@ -130,6 +130,14 @@ int fg_db_search_ex(fg_db* db, const char* ns, const char* query, const char* co
                     uint32_t page, uint32_t per_page, fg_hit* out, uint32_t cap, uint32_t* n_out);
 int fg_db_search(fg_db* db, const char* ns, const char* query, uint32_t page, uint32_t per_page, fg_hit* out,
                  uint32_t cap, uint32_t* n_out);
+/* Phase times of every search of the process while enabled (all threads):
+ * out_ms[0..5] = parse + dictionary, host planning (+ upload queued), launches,
+ * kernels + merge + D2H until the hits are on the host, JSON doc fetch +
+ * serialization, the whole fg_db_search* call; *calls = fg_db_search* calls.
+ * Reading resets the sums; enable: 1 on, 0 off, -1 unchanged.  Off by default
+ * (one relaxed load per phase boundary). */
+#define FG_SEARCH_PHASES 6
+int fg_search_trace(int enable, double* out_ms, uint32_t n, uint64_t* calls);
 /* perform_search + handler response JSON (per_page clamp 1..100 else 20). */
 int fg_db_search_json_ex(fg_db* db, const char* ns, const char* query, const char* const* filters,
                          uint32_t n_filters, uint32_t page, uint32_t per_page, int include_text, int shape, char* out,

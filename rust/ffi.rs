@@ -261,6 +261,7 @@ extern "C" {
                            -> c_int;
     pub fn fg_db_search(db: *mut fg_db, ns: *const c_char, query: *const c_char, page: u32, per_page: u32,
                         out: *mut fg_hit, cap: u32, n_out: *mut u32) -> c_int;
+    pub fn fg_search_trace(enable: c_int, out_ms: *mut f64, n: u32, calls: *mut u64) -> c_int;
     pub fn fg_db_search_json_ex(db: *mut fg_db, ns: *const c_char, query: *const c_char,
                                 filters: *const *const c_char, n_filters: u32, page: u32, per_page: u32,
                                 include_text: c_int, shape: c_int, out: *mut c_char, cap: usize, len: *mut usize)
