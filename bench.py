@@ -246,6 +246,10 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     docs fetched).  Parity sample: the oracle's top-20 (an OR does not depend
     on the segmentation)."""
     from fugu_amd import db as fdb
+    # LogMergePolicy::set_max_docs_before_merge(2^20): the 8 bulk segments of
+    # 1.25M docs stay 8 (tantivy's default 10M would merge them into one in the
+    # background), so this line keeps measuring the segmented search path
+    os.environ.setdefault("FUGU_MERGE_MAX_DOCS", str(1 << 20))
     t0 = time.time()
     d = fdb.Database(ctx)
     d.create_namespace("api")

@@ -57,6 +57,26 @@ void parallel_dynamic(uint32_t n, int threads, uint32_t grain, F&& f) {
 }
 
 
+// Device memory some structure keeps cached for reuse (released scoring
+// blocks, plan workspaces).  Every cache registers itself; an allocation that
+// fails drops ALL of them and retries once (dev_malloc), so a build or a plan
+// never fails with FG_EOOM while idle cached blocks sit on the device.
+struct DevCache {
+  DevCache();
+  virtual ~DevCache() { unregister_cache(); }
+  // first thing in a derived destructor: no drop_all_cached reaches a cache
+  // whose own destructor has started
+  void unregister_cache();
+  DevCache(const DevCache&) = delete;
+  DevCache& operator=(const DevCache&) = delete;
+  virtual void drop_cached() = 0;  // free what is cached (not what is handed out)
+};
+void drop_all_cached();
+// hipMalloc, after dropping every registered cache if the first try fails
+hipError_t dev_malloc(void** p, size_t bytes);
+// hipMallocAsync on `s`, likewise
+hipError_t dev_malloc_async(void** p, size_t bytes, hipStream_t s);
+
 struct DevAllocs {
   std::vector<void*> ptrs;
   int dev = 0;
@@ -74,7 +94,7 @@ struct DevAllocs {
 // serialised in the runtime, 10s of ms per commit).  The release waits for the
 // device to drain, as hipFree would, so no kernel still reads a block handed out
 // again.
-struct ScorePool {
+struct ScorePool : DevCache {
   static constexpr size_t kKeep = 2;  // blocks cached per structure
   std::mutex mu;
   std::vector<std::pair<size_t, void*>> free_blocks;
@@ -122,16 +142,11 @@ struct ScorePool {
         }
     }
     void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
-      (void)hipGetLastError();
-      release_all();
-      if (hipMalloc(&p, bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-      }
-    }
+    if (dev_malloc(&p, bytes) != hipSuccess) return nullptr;
     return p;
   }
+  // (the caller runs where waiting for the device is harmless: a snapshot's
+  // last release happens on the db's reaper thread, or a build / test thread)
   void put(void* p, size_t bytes) {
     (void)hipSetDevice(dev);
     (void)hipDeviceSynchronize();
@@ -149,7 +164,9 @@ struct ScorePool {
     for (auto& b : free_blocks) (void)hipFree(b.second);
     free_blocks.clear();
   }
-  ~ScorePool() {
+  void drop_cached() override { release_all(); }
+  ~ScorePool() override {
+    unregister_cache();
     for (auto& b : free_host) (void)hipHostFree(b.second);
     if (free_blocks.empty()) return;
     (void)hipSetDevice(dev);
@@ -230,7 +247,7 @@ struct fg_ctx {
 // device).  Buffers are reused when they fit a request within 2x; at most
 // kPoolKeep bytes stay cached.
 namespace fgh {
-struct WsPool {
+struct WsPool : DevCache {
   static constexpr size_t kPoolKeep = 1ull << 30;
   std::mutex mu;
   std::multimap<size_t, void*> free_bufs;
@@ -249,19 +266,18 @@ struct WsPool {
       }
     }
     void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
-      // the cached workspaces may be what the device lacks: free them, retry once
-      (void)hipGetLastError();
-      {
-        std::lock_guard<std::mutex> l(mu);
-        for (auto& kv : free_bufs) (void)hipFree(kv.second);
-        free_bufs.clear();
-        cached = 0;
-      }
-      if (hipMalloc(&p, bytes) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-    }
+    // the cached workspaces and scoring blocks (of every index) may be what the
+    // device lacks: dev_malloc frees them and retries once
+    if (dev_malloc(&p, bytes) != hipSuccess) return nullptr;
     *got = bytes;
     return p;
+  }
+  void drop_cached() override {
+    std::lock_guard<std::mutex> l(mu);
+    (void)hipSetDevice(dev);
+    for (auto& kv : free_bufs) (void)hipFree(kv.second);
+    free_bufs.clear();
+    cached = 0;
   }
   void put(void* p, size_t bytes) {
     {
@@ -275,7 +291,8 @@ struct WsPool {
     (void)hipSetDevice(dev);
     (void)hipFree(p);
   }
-  ~WsPool() {
+  ~WsPool() override {
+    unregister_cache();
     if (free_bufs.empty()) return;
     (void)hipSetDevice(dev);
     for (auto& kv : free_bufs) (void)hipFree(kv.second);

@@ -163,6 +163,51 @@ int fgh::hw_threads(int req) {
   return n;
 }
 int fg_host_threads() { return hw_threads(0); }
+
+namespace fgh {
+namespace {
+std::mutex& cache_mu() {
+  static std::mutex m;
+  return m;
+}
+std::vector<DevCache*>& caches() {
+  static std::vector<DevCache*> v;
+  return v;
+}
+}  // namespace
+DevCache::DevCache() {
+  std::lock_guard<std::mutex> l(cache_mu());
+  caches().push_back(this);
+}
+void DevCache::unregister_cache() {
+  std::lock_guard<std::mutex> l(cache_mu());
+  auto& v = caches();
+  v.erase(std::remove(v.begin(), v.end(), this), v.end());
+}
+void drop_all_cached() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> l(cache_mu());
+  for (DevCache* c : caches()) c->drop_cached();
+  (void)hipSetDevice(dev);
+}
+hipError_t dev_malloc(void** p, size_t bytes) {
+  if (hipMalloc(p, bytes) == hipSuccess) return hipSuccess;
+  (void)hipGetLastError();
+  drop_all_cached();
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) (void)hipGetLastError();
+  return e;
+}
+hipError_t dev_malloc_async(void** p, size_t bytes, hipStream_t s) {
+  if (hipMallocAsync(p, bytes, s) == hipSuccess) return hipSuccess;
+  (void)hipGetLastError();
+  drop_all_cached();
+  const hipError_t e = hipMallocAsync(p, bytes, s);
+  if (e != hipSuccess) (void)hipGetLastError();
+  return e;
+}
+}  // namespace fgh
 namespace {
 
 // Host-side postings before upload (merged text U name per term).
@@ -224,7 +269,7 @@ template <class T>
 int dev_upload(DevAllocs& m, const T* src, size_t n, T** out, uint64_t* bytes) {
   size_t b = std::max<size_t>(n * sizeof(T), 16);
   void* p = nullptr;
-  if (hipMalloc(&p, b) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", b);
+  if (fgh::dev_malloc(&p, b) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", b);
   m.ptrs.push_back(p);
   if (n) {
     HIPCHK(hipMemcpyAsync(p, src, n * sizeof(T), hipMemcpyHostToDevice, kBuildStream));
@@ -248,7 +293,7 @@ struct UploadBatch {
   }
   int commit(DevAllocs& m, uint64_t* bytes) {
     void* p = nullptr;
-    if (hipMalloc(&p, std::max<size_t>(total, 256)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", total);
+    if (fgh::dev_malloc(&p, std::max<size_t>(total, 256)) != hipSuccess) return fail(FG_EOOM, "hipMalloc(%zu) failed", total);
     m.ptrs.push_back(p);
     // the arrays laid out in a pooled pinned staging buffer by all host threads,
     // then ONE copy: a small segment's arrays are sized by the vocabulary (~40 MB
@@ -335,7 +380,7 @@ static int ktop_pass(const fg_index* ix, fg::ScoreJob& j) {
   const size_t kck_b = (8ull * n_chunks * fg::kTopKs[fg::kNumTopK - 1] + 255) & ~size_t(255);
   const size_t kcc_b = (4ull * n_chunks + 255) & ~size_t(255), kbs_b = 4ull * 3 * n_big;
   void* ktmp = nullptr;
-  if (hipMallocAsync(&ktmp, kck_b + kcc_b + kbs_b + 16, kBuildStream) != hipSuccess)
+  if (fgh::dev_malloc_async(&ktmp, kck_b + kcc_b + kbs_b + 16, kBuildStream) != hipSuccess)
     return fail(FG_EOOM, "hipMallocAsync(%zu) failed", kck_b + kcc_b + kbs_b);
   struct KtmpBack {
     void* p;
@@ -863,7 +908,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     }
     while (!rank_terms.empty()) {
       void* q = nullptr;
-      if (hipMalloc(&q, rank_words * 8ull * rank_terms.size()) == hipSuccess) {
+      if (fgh::dev_malloc(&q, rank_words * 8ull * rank_terms.size()) == hipSuccess) {
         sm.ptrs.push_back(q);
         bytes += rank_words * 8ull * rank_terms.size();
         d_rank = static_cast<uint64_t*>(q);
@@ -887,7 +932,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     // synchronise the device (hipFree would wait for every stream's work)
     void* d_tab = nullptr;
     const size_t nb = sb.size() * 8, nn = sn.size() * 4;
-    if (hipMallocAsync(&d_tab, nb + nn + 16, kBuildStream) != hipSuccess) return fail(FG_EOOM, "hipMallocAsync failed");
+    if (fgh::dev_malloc_async(&d_tab, nb + nn + 16, kBuildStream) != hipSuccess) return fail(FG_EOOM, "hipMallocAsync failed");
     uint64_t* d_sb = static_cast<uint64_t*>(d_tab);
     uint32_t* d_sn = reinterpret_cast<uint32_t*>(static_cast<char*>(d_tab) + nb);
     HIPCHK(hipMemcpyAsync(d_sb, sb.data(), nb, hipMemcpyHostToDevice, kBuildStream));
@@ -1631,7 +1676,7 @@ int fg_index_term_ladder(const fg_index* ix, float* out) {
   // one temporary: the main K-th scores [V * kNumTopK], then the extra levels
   const size_t nm = (size_t)V * fg::kNumTopK, nx = (size_t)V * fg::kNumLadderExtra;
   void* tmp = nullptr;
-  if (hipMallocAsync(&tmp, 4 * (nm + nx) + 16, kBuildStream) != hipSuccess)
+  if (fgh::dev_malloc_async(&tmp, 4 * (nm + nx) + 16, kBuildStream) != hipSuccess)
     return fail(FG_EOOM, "hipMallocAsync(%zu) failed", 4 * (nm + nx));
   struct Back {
     void* p;

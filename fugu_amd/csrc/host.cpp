@@ -16,6 +16,7 @@
 #include <cstring>
 #include <deque>
 #include <stdexcept>
+#include <limits>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -871,34 +872,45 @@ struct fg_db {
   std::condition_variable mq_cv;
   std::deque<std::weak_ptr<Namespace>> queue;
   bool stop = false;
-  // replaced snapshots are released on the reaper thread: releasing a
-  // snapshot's scoring blocks waits for the device to drain (fgh::ScorePool),
-  // which must not hold up the commit or merge that replaced it
+  // Every snapshot is destroyed on the reaper thread, whoever drops its last
+  // reference (new_snapshot's deleter): destroying one releases its segments'
+  // scoring blocks, which waits for the device to drain (fgh::ScorePool), and
+  // that must hold up neither the commit or merge that replaced it nor a search
+  // that still held it when the swap came.
   std::thread reaper;
   std::mutex rq;
   std::condition_variable rq_cv;
-  std::deque<std::shared_ptr<Snapshot>> dead;
+  std::deque<Snapshot*> dead;
   bool rstop = false;
-  void retire(std::shared_ptr<Snapshot> s) {
-    if (!s) return;
-    std::lock_guard<std::mutex> l(rq);
-    dead.push_back(std::move(s));
-    if (!reaper.joinable())
-      reaper = std::thread([this] {
-        for (;;) {
-          std::shared_ptr<Snapshot> x;
-          {
-            std::unique_lock<std::mutex> l2(rq);
-            rq_cv.wait(l2, [&] { return rstop || !dead.empty(); });
-            if (dead.empty()) return;  // stopping, drained
-            x = std::move(dead.front());
-            dead.pop_front();
-          }
-          x.reset();  // the last reference, unless a search still holds it
-        }
-      });
-    rq_cv.notify_one();
+  void reap(Snapshot* p) {
+    {
+      std::lock_guard<std::mutex> l(rq);
+      if (!rstop) {
+        dead.push_back(p);
+        if (!reaper.joinable())
+          reaper = std::thread([this] {
+            for (;;) {
+              Snapshot* x = nullptr;
+              {
+                std::unique_lock<std::mutex> l2(rq);
+                rq_cv.wait(l2, [&] { return rstop || !dead.empty(); });
+                if (dead.empty()) return;  // stopping, drained
+                x = dead.front();
+                dead.pop_front();
+              }
+              delete x;
+            }
+          });
+        rq_cv.notify_one();
+        return;
+      }
+    }
+    delete p;  // the db is being destroyed: its reaper has stopped
   }
+  std::shared_ptr<Snapshot> new_snapshot() {
+    return std::shared_ptr<Snapshot>(new Snapshot, [this](Snapshot* p) { reap(p); });
+  }
+  void retire(std::shared_ptr<Snapshot> s) { s.reset(); }  // the reaper destroys it once unreferenced
   ~fg_db() {
     {
       std::lock_guard<std::mutex> l(mq);
@@ -906,6 +918,14 @@ struct fg_db {
     }
     mq_cv.notify_all();
     if (merger.joinable()) merger.join();
+    {
+      // the namespaces (and their snapshots) go while the reaper still runs
+      std::map<std::string, std::shared_ptr<Namespace>> gone;
+      {
+        std::unique_lock<std::shared_mutex> l(mu);
+        gone.swap(ns);
+      }
+    }
     {
       std::lock_guard<std::mutex> l(rq);
       rstop = true;
@@ -1607,7 +1627,7 @@ int commit_segment(fg_db* db, Namespace& ns) {
   tr.mark("gather (writer lock)");
   const fg_global_stats g = S.global();
   const fg_docs_input in = buf.input(n_terms, n_fterms, any_name);
-  auto snap = std::make_shared<Snapshot>();
+  auto snap = db->new_snapshot();
   // the new segment builds while the older ones rescore (their own threads and streams)
   fg_index* ix = nullptr;
   int brc = FG_OK;
@@ -1646,31 +1666,74 @@ int commit_segment(fg_db* db, Namespace& ns) {
   return FG_OK;
 }
 
-// The merge policy, tantivy's LogMergePolicy (indexer/log_merge_policy.rs:
-// levels of log4 size, kMergeFactor segments of one level merge together,
-// segments of kMergeMaxDocs docs or more are left alone) with runs kept
-// contiguous, so the merged segment keeps global doc order (merge_fruits' (segment,
-// doc) tie order needs it): the newest run of kMergeFactor segments of one level,
-// all under kMergeMaxDocs; else, from kHardSegments on, the two newest.  A
-// commit per upsert thus merges once every kMergeFactor commits, not after each.
-// Returns [j0, j1) or j0 == j1 (nothing to merge).
-constexpr size_t kMergeFactor = 8;            // LogMergePolicy::min_num_segments
-constexpr uint64_t kMergeMaxDocs = 1u << 20;  // ... max_docs_before_merge (a bulk load's segments stay)
-uint32_t merge_level(uint64_t x) {
-  uint32_t l = 0;
-  while (x >= 4) {
-    x >>= 2;
-    ++l;
+// The merge policy: tantivy 0.24.1's LogMergePolicy with its defaults
+// (indexer/log_merge_policy.rs): segments of more than max_docs_before_merge
+// docs are left alone; the others, largest first, form levels -- a segment
+// starts a new level when log2 of its size (clipped up to min_layer_size docs,
+// so every small segment shares the smallest level) is below the current
+// level's first by more than level_log_size -- and a level of at least
+// min_num_segments segments is merged.  Kept contiguous here: the merged
+// segment must keep global doc order (merge_fruits' (segment, doc) tie order),
+// so a level merges as its contiguous runs of >= kMergeFactor segments (the
+// newest such run first).  Levels that interleave in doc order could then
+// stall, so past kBoundSegments segments the kMergeFactor contiguous mergeable
+// segments with the fewest docs merge; from kHardSegments on (every segment
+// past the cap) the two newest.  Returns [j0, j1) or j0 == j1 (nothing).
+constexpr size_t kMergeFactor = 8;             // min_num_segments
+constexpr uint64_t kMinLayerSize = 10000;      // min_layer_size
+constexpr double kLevelLogSize = 0.75;         // level_log_size
+constexpr uint64_t kMaxDocsBeforeMerge = 10000000;  // max_docs_before_merge
+constexpr size_t kBoundSegments = 3 * kMergeFactor;
+// FUGU_MERGE_MAX_DOCS: LogMergePolicy::set_max_docs_before_merge (bench.py holds
+// its 8-segment namespace at 2^20 so the segmented search path stays measured)
+uint64_t merge_max_docs() {
+  const char* e = getenv("FUGU_MERGE_MAX_DOCS");
+  return e && *e ? std::strtoull(e, nullptr, 10) : kMaxDocsBeforeMerge;
+}
+// level of every segment (-1: too large to merge), levels numbered from the largest
+std::vector<int> merge_levels(const std::vector<uint64_t>& n, uint64_t max_docs) {
+  std::vector<size_t> by;
+  for (size_t i = 0; i < n.size(); ++i)
+    if (n[i] <= max_docs) by.push_back(i);
+  std::stable_sort(by.begin(), by.end(), [&](size_t a, size_t b) { return n[a] > n[b]; });
+  std::vector<int> lev(n.size(), -1);
+  double cur = std::numeric_limits<double>::max();
+  int l = -1;
+  for (size_t i : by) {
+    const double ls = std::log2((double)std::max(n[i], kMinLayerSize));
+    if (ls < cur - kLevelLogSize) {
+      cur = ls;
+      ++l;
+    }
+    lev[i] = l;
   }
-  return l;
+  return lev;
 }
 std::pair<size_t, size_t> pick_merge(const std::vector<uint64_t>& n) {
   const size_t c = n.size();
-  if (c >= 2 && n[c - 1] < kMergeMaxDocs) {
-    size_t j = c - 1;
-    while (j > 0 && n[j - 1] < kMergeMaxDocs && merge_level(n[j - 1]) == merge_level(n[c - 1]) && c - j < kMergeFactor)
-      --j;
-    if (c - j >= kMergeFactor) return {j, c};
+  const std::vector<int> lev = merge_levels(n, merge_max_docs());
+  for (size_t j1 = c; j1 > 0;) {  // contiguous runs of one level, newest first
+    size_t j0 = j1 - 1;
+    while (j0 > 0 && lev[j0 - 1] == lev[j1 - 1]) --j0;
+    if (lev[j1 - 1] >= 0 && j1 - j0 >= kMergeFactor) return {j0, j1};
+    j1 = j0;
+  }
+  if (c > kBoundSegments) {
+    size_t best = c;
+    uint64_t best_docs = ~0ull;
+    for (size_t j = 0; j + kMergeFactor <= c; ++j) {
+      uint64_t t = 0;
+      bool ok = true;
+      for (size_t i = j; i < j + kMergeFactor && ok; ++i) {
+        ok = lev[i] >= 0;
+        t += n[i];
+      }
+      if (ok && t < best_docs) {
+        best_docs = t;
+        best = j;
+      }
+    }
+    if (best < c) return {best, best + kMergeFactor};
   }
   if (c >= kHardSegments) return {c - 2, c};
   return {c, c};
@@ -1858,7 +1921,7 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     if (rc) return hfail(rc, fg_last_error());
     mix = re;
   }
-  auto snap = std::make_shared<Snapshot>();
+  auto snap = db->new_snapshot();
   const std::vector<Segment> before(now->segs.begin(), now->segs.begin() + j0),
       after(now->segs.begin() + j0 + src.size(), now->segs.end());
   auto keep = [&](const std::vector<Segment>& v) -> int {
@@ -2001,6 +2064,14 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   }
   const auto run = pick_merge(sizes);
   if (run.first < run.second) enqueue_merge(db, ns);
+  return FG_OK;
+}
+
+int fg_merge_policy_pick(const uint64_t* seg_docs, uint32_t n_segs, uint32_t* j0, uint32_t* j1) {
+  if ((n_segs && !seg_docs) || !j0 || !j1) return hfail(FG_EINVAL, "bad arguments");
+  const auto run = pick_merge(std::vector<uint64_t>(seg_docs, seg_docs + n_segs));
+  *j0 = (uint32_t)run.first;
+  *j1 = (uint32_t)run.second;
   return FG_OK;
 }
 

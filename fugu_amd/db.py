@@ -28,7 +28,7 @@ HOST_EXPORTS = (
     "fg_db_search", "fg_db_search_json", "fg_analyze", "fg_parse_query", "fg_parse_query_occur",
     "fg_db_upsert_record", "fg_db_upsert_batch", "fg_db_search_ex", "fg_db_search_json_ex", "fg_db_doc_facets", "fg_facet_tokens",
     "fg_facet_clauses", "fg_db_search_json_post", "fg_db_merge_wait", "fg_db_merge_info_get", "fg_db_segment_docs",
-    "fg_search_trace",
+    "fg_search_trace", "fg_merge_policy_pick",
 )
 SEARCH_PHASES = ("parse_dict", "plan", "launch", "wait_kernels_d2h", "json_fetch", "total")  # FG_SEARCH_PHASES
 
@@ -88,6 +88,7 @@ _sig("fg_facet_tokens", _s, _s, _sz, C.POINTER(_sz))
 _sig("fg_facet_clauses", C.POINTER(_s), C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
 _sig("fg_analyze", _s, _s, _sz, C.POINTER(_sz))
 _sig("fg_search_trace", C.c_int, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint64))
+_sig("fg_merge_policy_pick", C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32))
 _sig("fg_parse_query", _s, C.POINTER(C.c_int), _s, _sz, C.POINTER(_sz))
 _sig("fg_parse_query_occur", _s, _s, _sz, C.POINTER(_sz))
 
@@ -148,6 +149,15 @@ def facet_clauses(filters):
     a, al = C.c_int(0), C.c_int(0)
     out = _string_call(_lib.fg_facet_clauses, arr, n, C.byref(a), C.byref(al))
     return bool(a.value), bool(al.value), (out.split("\n") if (a.value and not al.value) else [])
+
+
+def merge_policy_pick(seg_docs):
+    """fg_merge_policy_pick: the run [j0, j1) of segments (doc counts, doc order) the
+    merger merges next, or None."""
+    n = (C.c_uint64 * max(len(seg_docs), 1))(*[int(x) for x in seg_docs])
+    j0, j1 = C.c_uint32(0), C.c_uint32(0)
+    _check(_lib.fg_merge_policy_pick(n, len(seg_docs), C.byref(j0), C.byref(j1)))
+    return (j0.value, j1.value) if j0.value < j1.value else None
 
 
 def search_trace(enable: int = -1) -> dict:

@@ -113,6 +113,11 @@ typedef struct fg_merge_info {
   uint64_t tot_facet_tokens; /* total_num_tokens(facet) */
 } fg_merge_info;
 int fg_db_merge_info_get(fg_db* db, const char* ns, fg_merge_info* out);
+/* The merge policy alone (host only): given the namespace's segments in doc
+ * order (their doc counts), the contiguous run [*j0, *j1) the merger merges
+ * next, *j0 == *j1 when none (tantivy LogMergePolicy levels, contiguous runs;
+ * FUGU_MERGE_MAX_DOCS = set_max_docs_before_merge, default 10M). */
+int fg_merge_policy_pick(const uint64_t* seg_docs, uint32_t n_segs, uint32_t* j0, uint32_t* j1);
 /* Global doc ids of segment `seg` of the current snapshot, in its doc order:
  * *n = its size, out[0..min(n, cap)) (out may be NULL). */
 int fg_db_segment_docs(fg_db* db, const char* ns, uint32_t seg, uint32_t* out, uint32_t cap, uint32_t* n);

@@ -252,6 +252,7 @@ extern "C" {
     pub fn fg_db_commit(db: *mut fg_db, ns: *const c_char) -> c_int;
     pub fn fg_db_merge_wait(db: *mut fg_db, ns: *const c_char) -> c_int;
     pub fn fg_db_merge_info_get(db: *mut fg_db, ns: *const c_char, out: *mut fg_merge_info) -> c_int;
+    pub fn fg_merge_policy_pick(seg_docs: *const u64, n_segs: u32, j0: *mut u32, j1: *mut u32) -> c_int;
     pub fn fg_db_segment_docs(db: *mut fg_db, ns: *const c_char, seg: u32, out: *mut u32, cap: u32, n: *mut u32)
                               -> c_int;
     pub fn fg_db_add_file(db: *mut fg_db, ns: *const c_char, name: *const c_char, body: *const c_char) -> c_int;

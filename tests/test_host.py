@@ -621,25 +621,74 @@ def test_json_shapes_with_hits_and_canonical_metadata(db):
     assert g["query"] == "alpha gamma" and (g["page"], g["per_page"]) == (0, 20) and g["results"][0]["id"] == "d2"
 
 
-def pick_merge(n):
-    """host.cpp pick_merge, restated (tantivy's LogMergePolicy with contiguous
-    runs): the newest run of 8 segments of one log4 size level, each under 2^20
-    docs; else, from 48 segments on, the two newest."""
+def pick_merge(n, max_docs=10_000_000):
+    """host.cpp pick_merge, restated: tantivy 0.24.1's LogMergePolicy defaults
+    (min_num_segments 8, min_layer_size 10000, level_log_size 0.75,
+    max_docs_before_merge 10M) with levels merged as contiguous runs of >= 8
+    (newest first); past 24 segments the 8 contiguous mergeable ones with the
+    fewest docs; from 48 on the two newest.  Returns (j0, j1) or None."""
+    import math
     c = len(n)
-
-    def level(x):
-        lv = 0
-        while x >= 4:
-            x >>= 2
-            lv += 1
-        return lv
-    if c >= 2 and n[c - 1] < (1 << 20):
-        j = c - 1
-        while j > 0 and n[j - 1] < (1 << 20) and level(n[j - 1]) == level(n[c - 1]) and c - j < 8:
-            j -= 1
-        if c - j >= 8:
-            return j, c
+    by = sorted([i for i in range(c) if n[i] <= max_docs], key=lambda i: -n[i])  # stable
+    lev = [-1] * c
+    cur, lv = float("inf"), -1
+    for i in by:
+        ls = math.log2(max(n[i], 10000))
+        if ls < cur - 0.75:
+            cur, lv = ls, lv + 1
+        lev[i] = lv
+    j1 = c
+    while j1 > 0:
+        j0 = j1 - 1
+        while j0 > 0 and lev[j0 - 1] == lev[j1 - 1]:
+            j0 -= 1
+        if lev[j1 - 1] >= 0 and j1 - j0 >= 8:
+            return j0, j1
+        j1 = j0
+    if c > 24:
+        wins = [(sum(n[j:j + 8]), j) for j in range(c - 7) if all(lev[i] >= 0 for i in range(j, j + 8))]
+        if wins:
+            j = min(wins)[1]
+            return j, j + 8
     return (c - 2, c) if c >= 48 else None
+
+
+def test_merge_policy_matches_restatement(db):
+    rng = random.Random(3)
+    for _ in range(400):
+        c = rng.randint(0, 60)
+        n = [rng.choice([1, 2, 5, 100, 9999, 10000, 20000, 30000, 1 << 20, 1_250_000, 9_999_999, 10_000_001])
+             if rng.random() < 0.5 else rng.randint(1, 3_000_000) for _ in range(c)]
+        assert db.merge_policy_pick(n) == pick_merge(n), n
+
+
+def test_merge_policy_levels(db):
+    assert db.merge_policy_pick([1_250_000] * 8) == (0, 8)  # one level: tantivy merges the 8
+    assert db.merge_policy_pick([1_250_000] * 7 + [100]) is None  # 100 is the min-layer level, alone
+    assert db.merge_policy_pick([10_000_001] * 8) is None  # past max_docs_before_merge
+    assert db.merge_policy_pick([500_000] + [7] * 8) == (1, 9)  # the newest run of the small level
+    # 2 and 5 docs share the clipped level (the round-4 policy kept them apart: log4 levels)
+    assert db.merge_policy_pick([2, 5] * 4) == (0, 8)
+
+
+def test_merge_policy_bounds_alternating_commits(db):
+    """Commits of mixed small sizes keep the segment count bounded (each commit
+    adds a segment, the merger then applies the policy until it picks nothing)."""
+    for sizes in ([2, 5], [5000, 50000], [3, 40000, 700], [9000, 20000, 45000, 200000]):
+        segs, most = [], 0
+        for i in range(300):
+            segs.append(sizes[i % len(sizes)])
+            while (run := db.merge_policy_pick(segs)) is not None:
+                j0, j1 = run
+                segs[j0:j1] = [sum(segs[j0:j1])]
+            most = max(most, len(segs))
+        assert most <= 25, (sizes, most)
+
+
+def test_merge_policy_max_docs_knob(db, monkeypatch):
+    monkeypatch.setenv("FUGU_MERGE_MAX_DOCS", str(1 << 20))
+    assert db.merge_policy_pick([1_250_000] * 8) is None  # bench.py keeps its 8 segments this way
+    assert db.merge_policy_pick([1_000_000] * 8) == (0, 8)
 
 
 def quantized(n):
@@ -720,6 +769,42 @@ def test_db_incremental_commits_segments_vs_oracle(db):
         assert d.doc_count("inc")[0] == n
     assert checked > 300 and merges >= 3 and dropped > 0
     assert orc.fieldnorm_to_id(41) == 40
+
+
+@pytest.mark.gpu
+def test_db_alternating_small_commits_stay_bounded(db):
+    """Commits of 2 and 5 docs in turn (under log4 levels they never
+    formed a run, so the namespace grew to 48 segments and merged on the commit
+    path): every small segment shares tantivy's min-layer level, so each run of
+    8 merges in the background and the namespace stays at <= 8 segments, the
+    segments' docs always those of the restated policy."""
+    from fugu_amd import native
+    if native.device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+    ctx = native.Context((0,))
+    d = db.Database(ctx)
+    d.create_namespace("alt")
+    recs = build_corpus(31, 350)
+    segs, i, c, most, merges = [], 0, 0, 0, 0
+    while i < len(recs):
+        b = i
+        i = min(len(recs), b + (2, 5)[c % 2])
+        for rid, t, meta in recs[b:i]:
+            d.upsert(db.ObjectRecord(rid, t, metadata=meta), "alt")
+        d.commit("alt")
+        d.merge_wait("alt")
+        c += 1
+        dele = deleted_of(recs[:i])
+        segs.append(list(range(b, i)))
+        while (run := pick_merge([len(sg) for sg in segs])) is not None:
+            j0, j1 = run
+            segs[j0:j1] = [[g for sg in segs[j0:j1] for g in sg if not dele[g]]]
+            merges += 1
+        got = d.segments("alt")
+        assert got == segs, c
+        most = max(most, len(got))
+    assert most <= 8 and merges >= 10 and d.merge_info("alt")["merges"] == merges
+    assert d.search("alt", "alpha beta", 0, 10)
 
 
 @pytest.mark.gpu
