@@ -902,7 +902,12 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t brk = std::min<uint64_t>(want, free_b / 4);
+    // A/B (FUGU_RANK_SKIP_TOP=T): the T densest terms without rank words (with
+    // FUGU_DENSE_GIB they take f32 score tables: one gather per probe)
+    const char* sk = getenv("FUGU_RANK_SKIP_TOP");
+    size_t skip = sk && *sk ? (size_t)atol(sk) : 0;
     for (uint32_t t : by_df) {
+      if (skip) { --skip; continue; }
       if ((rank_terms.size() + 1) * rank_words * 8ull > brk || rank_terms.size() >= fg::kMaxDense) break;
       rank_terms.push_back(t);
     }

@@ -159,3 +159,16 @@ def test_parser_catches_drift():
     args = cf["fg_search_batch"][1]
     with pytest.raises(AssertionError):
         assert list(reversed(args)) == rust_functions()["fg_search_batch"][1]
+
+
+def test_integration_doc_declares_nothing_itself():
+    """rust/ffi.rs is the one FFI source: INTEGRATION.md names its items and
+    declares none (a second hand-written copy would drift unchecked)."""
+    import os
+    from conftest import ROOT
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert not re.search(r"pub fn fg_\w+\s*\(", doc)
+    assert not re.search(r"#\[repr\(C\)\]\s*pub struct fg_", doc)
+    for name in re.findall(r"`(fg_\w+)`", doc):
+        if name.startswith("fg_") and not name.endswith("_"):
+            assert name in rust_source() or name in c_source("fugu.h") or name in c_source("fugu_host.h"), name
