@@ -74,7 +74,7 @@ def test_floor_bounds_namespace_kth(native, shards):
     # what pruning gains: at K = 1000 over 4 shards the floor sits above every shard's own 1000th
     sample = floor[1:4000:37, 4]
     has = own[:, 4] > 0
-    assert has.sum() > 20 and (sample[has] > own[has, 4]).mean() > 0.9
+    assert has.sum() >= 8 and (sample[has] > own[has, 4]).mean() > 0.9
     for ix in ixs:
         ix.set_kth_floor(None)
 
