@@ -323,15 +323,18 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     # reader searches while the writer gathers, builds and swaps
     import threading
     stop = threading.Event()
-    lat_r, err_r = [], []
+    lat_r, err_r, ph_r = [], [], []
+    fdb.search_trace(1)
 
     def reader():
         i = 0
         try:
+            fdb.search_trace()
             while not stop.is_set():
                 t1 = time.perf_counter()
                 d.search("api", qs[i % nq], 0, 20)
                 lat_r.append(time.perf_counter() - t1)
+                ph_r.append(fdb.search_trace())  # this search's phases (only this thread searches)
                 i += 1
         except Exception as e:  # noqa: BLE001
             err_r.append(repr(e))
@@ -348,13 +351,19 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     t_commits = time.perf_counter() - t_all
     stop.set()
     th.join()
+    fdb.search_trace(0)
     if err_r:
         raise RuntimeError(err_r[0])
+    # where the slowest 1% of the searches during commits spent their time
+    cut = float(np.percentile(lat_r, 99))
+    slow = [p for l, p in zip(lat_r, ph_r) if l >= cut]
+    slow_ph = {k: round(float(np.mean([p[k] for p in slow])), 4) for k in fdb.SEARCH_PHASES if k != "json_fetch"}
     d.merge_wait("api")
     t_done = time.perf_counter() - t_all
     out["during_commits"] = {"p50_ms": pct(lat_r, 50), "p90_ms": pct(lat_r, 90), "p99_ms": pct(lat_r, 99),
                              "max_ms": round(max(lat_r) * 1e3, 3), "searches": len(lat_r),
                              "p99_over_idle_p99": round(pct(lat_r, 99) / max(out["p99_ms"], 1e-9), 3),
+                             "slowest_1pct_phases_ms_mean": slow_ph,
                              "note": "GET /search (fg_db_search, OR limit 20) back to back from a second thread while "
                                      "the 16 commits of commit_10M run; the read path takes no writer lock"}
     mi = d.merge_info("api")

@@ -111,6 +111,21 @@ constexpr uint32_t kLadderExtra[kNumLadderExtra] = {2, 3, 5, 13, 25, 50, 125, 25
 constexpr uint32_t kNumLadder = kNumTopK + kNumLadderExtra;  // FG_LADDER_LEVELS
 constexpr uint32_t kLadderKs[kNumLadder] = {1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000};
 
+// Seeded disjunction thresholds (k_seed).  Every term with more than
+// kSeedMinDf postings keeps its kSeedKS best alive keys, sorted (written by the
+// k_ktop kernels, scoring); shorter terms are read whole.  Before k_disj, one
+// workgroup per seeded query scores exactly the union of its clauses' candidate
+// docs (each clause's best min(k, kSeedKS), or all its postings) and publishes
+// the k-th best of those distinct docs as the query's starting threshold
+// (score-only): a set of real docs, so a lower bound of the final k-th score.
+constexpr uint32_t kSeedKS = 256;
+constexpr uint32_t kSeedMinDf = 1024;
+constexpr uint32_t kSeedCap = 2048;  // k_seed's key buffer (truncated to k when full)
+struct SeedIndex {
+  const uint64_t* keys;   // [n_seed_terms * kSeedKS] best alive keys per term, descending (0: none)
+  const uint32_t* slot;   // [V] the term's row in keys, or 0xFFFFFFFF (kSeedMinDf postings or fewer)
+};
+
 constexpr uint32_t kMaxFacetClauses = 8;  // facet clauses per query (FG_MAX_FACET_CLAUSES)
 constexpr uint32_t kFmaskChunk = 8192;    // facet postings per k_fmask workgroup
 constexpr uint32_t kScanMaxGroup = 32;    // k_scan: at most this many 4096-doc tiles per work item
@@ -354,6 +369,8 @@ struct ScoreJob {
   uint32_t n_tiles;           // tiles per term (4096-doc k_disj tiles)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
   float* ladder;              // [V * kNumLadderExtra] out (zeroed first) or nullptr: fg_index_term_ladder only
+  uint64_t* seed_keys;        // [seed rows * kSeedKS] out (zeroed first): SeedIndex::keys, or nullptr
+  const uint32_t* seed_slot;  // [V] SeedIndex::slot
   float* cmax;               // [cmax entries] out: the largest score of each kChunk postings of a term
   const uint32_t* coff;       // [V] first cmax entry of each term
   // packed chunk tables (a chunk: terms [tf, tl], postings / directory entries
@@ -403,6 +420,9 @@ hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);  // packed chunks
 hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s);                        // after k_bucket
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
+// k_seed: n_seed query slots (seed_q) before k_disj on the same stream; six[s] = snapshot s's top lists
+hipError_t launch_seed(const DevIndex& ix, const DevPlan& pl, const SeedIndex* six, const uint32_t* seed_q,
+                       uint32_t n_seed, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

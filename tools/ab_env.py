@@ -45,15 +45,20 @@ def main():
         st = ix.stats()
         print(f"[ab] {name} {env}: f32 tables {st.n_dense_f32}, rank terms {st.n_rank_terms}, "
               f"{st.device_bytes / 2**30:.2f} GiB, built in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
-        ixs[name] = (ix, st.device_bytes)
+        ixs[name] = (ix, st.device_bytes, env)
     os.environ.clear()
     os.environ.update(base_env)
     out = {"docs": args.docs, "s": args.s, "variants": args.variants,
-           "device_gib": {n: round(b / 2**30, 3) for n, (_, b) in ixs.items()}, "workloads": {}}
+           "device_gib": {n: round(b / 2**30, 3) for n, (_, b, _) in ixs.items()}, "workloads": {}}
     for wl in args.workloads.split(","):
         m0, m1, k, mode = SPECS[wl]
         q_off, terms = synth.queries(1024, m0, m1)
-        plans = {n: ix.plan(q_off, terms, k, mode) for n, (ix, _) in ixs.items()}
+        plans = {}
+        for n, (ix, _, env) in ixs.items():  # plan-time knobs (FUGU_SEED) under the variant's environment too
+            os.environ.update(env)
+            plans[n] = ix.plan(q_off, terms, k, mode)
+            os.environ.clear()
+            os.environ.update(base_env)
         times = {n: [] for n in plans}
         hashes = {}
         for n, p in plans.items():
