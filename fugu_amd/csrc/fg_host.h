@@ -466,9 +466,10 @@ struct fg_plan {
   void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
   size_t pin_n = 0;
   hipStream_t up_stream = hipStreamPerThread;  // the stream the plan was uploaded on
-  // k_seed: the query slots it starts and each snapshot's SeedIndex (in the workspace)
+  // k_seed (fg_plan_seed_ladders): the query slots it scores and each snapshot's SeedIndex (in the workspace)
   const uint32_t* seed_q = nullptr;
   const fg::SeedIndex* seed_ix = nullptr;
   uint32_t n_seed = 0;
+  std::vector<uint64_t> h_thr0;  // the planned starting thresholds (fg_plan_set_query_floor)
 };
 

@@ -111,13 +111,14 @@ constexpr uint32_t kLadderExtra[kNumLadderExtra] = {2, 3, 5, 13, 25, 50, 125, 25
 constexpr uint32_t kNumLadder = kNumTopK + kNumLadderExtra;  // FG_LADDER_LEVELS
 constexpr uint32_t kLadderKs[kNumLadder] = {1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000};
 
-// Seeded disjunction thresholds (k_seed).  Every term with more than
-// kSeedMinDf postings keeps its kSeedKS best alive keys, sorted (written by the
-// k_ktop kernels, scoring); shorter terms are read whole.  Before k_disj, one
-// workgroup per seeded query scores exactly the union of its clauses' candidate
-// docs (each clause's best min(k, kSeedKS), or all its postings) and publishes
-// the k-th best of those distinct docs as the query's starting threshold
-// (score-only): a set of real docs, so a lower bound of the final k-th score.
+// Query ladders for thresholds shared across devices (k_seed,
+// fg_plan_seed_ladders).  Every term with more than kSeedMinDf postings keeps
+// its kSeedKS best alive keys, sorted (written by the k_ktop kernels, scoring);
+// shorter terms are read whole.  One workgroup per Should-only query slot
+// scores exactly the union of its clauses' candidate docs (each clause's best
+// min(k, kSeedKS), or all its postings) and writes the scores at the ranks
+// kLadderKs of those distinct docs: real docs, so every shard's ladder bounds
+// the query's k-th score from below, and the shards' ladders combine.
 constexpr uint32_t kSeedKS = 256;
 constexpr uint32_t kSeedMinDf = 1024;
 constexpr uint32_t kSeedCap = 2048;  // k_seed's key buffer (truncated to k when full)
@@ -420,9 +421,9 @@ hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);  // packed chunks
 hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s);                        // after k_bucket
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
-// k_seed: n_seed query slots (seed_q) before k_disj on the same stream; six[s] = snapshot s's top lists
+// k_seed: the ladders of n_seed query slots (seed_q) into out[slot * kNumLadder]; six[s] = snapshot s's top lists
 hipError_t launch_seed(const DevIndex& ix, const DevPlan& pl, const SeedIndex* six, const uint32_t* seed_q,
-                       uint32_t n_seed, hipStream_t s);
+                       uint32_t n_seed, float* out, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

@@ -1950,8 +1950,6 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   q_hhi.assign(nq, 0x3F800000u);
   q_hsh.assign(nq, 31);
   auto present = [&](uint32_t t) { return t < ix->n_terms && ix->off[t + 1] > ix->off[t]; };
-  const char* seed_env = getenv("FUGU_SEED");
-  const bool seed_on = !(seed_env && *seed_env == '0');
   h.seedq.clear();
   // the term's K-th best alive score at level j: the snapshot's own, or the
   // namespace-wide floor of a doc-sharded namespace's shard when higher
@@ -2049,9 +2047,8 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       float ub = fmx;
       for (uint32_t c = 0; c < ns; ++c) ub += ix->tmaxs[qt[c]];
       set_bins(i, ub);
-      // k_seed: the exact k-th best over the clauses' best docs as the starting
-      // threshold (unfiltered, unexcluded unions; FUGU_SEED=0: off, A/B)
-      if (seed_on && q_filter[i] == 0xFFFFFFFFu && nx == 0 && ix->d_seed_keys) h.seedq.push_back(i);
+      // k_seed's slots (fg_plan_seed_ladders): unfiltered, unexcluded unions
+      if (q_filter[i] == 0xFFFFFFFFu && nx == 0 && ix->d_seed_keys) h.seedq.push_back(i);
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
       // tiles per item: ~gpq items per query (capping an item's postings, or the
@@ -2369,6 +2366,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->d.work_n = (const uint32_t*)put(work_n.data(), 4ull * chunks, s_wn);
   p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
   p->d.q_thr0 = (const uint64_t*)put(thr0.data(), 8ull * nq, s_t0);
+  p->h_thr0 = thr0;  // fg_plan_set_query_floor raises it
   p->d.q_ub = (const float*)put(q_ub.data(), 4ull * nq * fg::kMaxTerms, s_ub);
   p->d.f.q_filter = (const uint32_t*)put(q_filter.data(), 4ull * nq, s_qf);
   p->d.f.f_shift = (const uint32_t*)put(f_shift.data(), 4ull * nf, s_fs);
@@ -2462,7 +2460,6 @@ static int execute_impl(fg_plan* p, hipStream_t s, float* os, uint32_t* od, uint
     HIPCHK(hipEventRecord(ev[0], s));
   }
   if (p->d.f.n_chunks) HIPCHK(fg::launch_fmask(p->ix->d, p->d, s));
-  if (p->n_seed) HIPCHK(fg::launch_seed(p->ix->d, p->d, p->seed_ix, p->seed_q, p->n_seed, s));
   if (p->d.n_conj) HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
   if (p->d.total_chunks > p->d.n_conj) HIPCHK(fg::launch_disj(p->ix->d, p->d, s));
   if (p->d.n_scan) HIPCHK(fg::launch_scan(p->ix->d, p->d, s));
@@ -2492,6 +2489,30 @@ int fg_plan_execute_merged(fg_plan* p, void* stream, float* d_out_score, uint32_
   if (p->n_segs < 2 || !p->d.seg_base)
     return fail(FG_EUNSUPPORTED, "not a multi-snapshot plan over < 2^32 docs (use fg_plan_execute + fg_merge_shards)");
   return execute_impl(p, static_cast<hipStream_t>(stream), d_out_score, d_out_doc, d_out_n, d_out_shard);
+}
+
+int fg_plan_seed_ladders(fg_plan* p, void* stream, float* d_out) {
+  if (!p || !d_out) return fail(FG_EINVAL, "bad arguments");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIPCHK(hipSetDevice(p->ix->dev));
+  HIPCHK(hipMemsetAsync(d_out, 0, 4ull * p->nq * fg::kNumLadder, s));
+  HIPCHK(fg::launch_seed(p->ix->d, p->d, p->seed_ix, p->seed_q, p->n_seed, d_out, s));
+  return FG_OK;
+}
+
+int fg_plan_set_query_floor(fg_plan* p, const float* floor) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  std::vector<uint64_t> t0(p->h_thr0);
+  if (floor)
+    for (uint32_t v = 0; v < p->nq; ++v) {
+      const float f = floor[fg::slot_query(p->d, v)];
+      if (f > 0.0f) t0[v] = std::max(t0[v], fg::make_key(f, 0xFFFFFFFFu));  // score-only: the lowest key of f
+    }
+  HIPCHK(hipSetDevice(p->ix->dev));
+  HIPCHK(hipMemcpyAsync(const_cast<uint64_t*>(p->d.q_thr0), t0.data(), 8ull * p->nq, hipMemcpyHostToDevice,
+                        hipStreamPerThread));
+  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+  return FG_OK;
 }
 
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n) {

@@ -1607,16 +1607,21 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
 }
 
 // ---------------------------------------------------------------- k_seed
-// One workgroup per seeded query slot (a Should-only query without MustNot or
-// facet clauses), before k_disj: the union of the clauses' candidate docs --
-// each clause's best min(k, kSeedKS) alive keys (SeedIndex rows) or, for a
-// clause of at most kSeedMinDf postings, all of them -- is scored exactly (every
-// clause probed, SumCombiner in clause order), and the k-th best of those
-// DISTINCT docs becomes the query's threshold, published score-only.  A doc is
-// counted only from the first clause whose candidate list holds it (a clause's
-// list holds d iff d is present and, for a row, its key is >= the row's kk-th
-// key), so no doc counts twice; a doc no clause counts only lowers the result.
-// k_disj items then start from it instead of the per-term K-th score.
+// The score ladder of a query slot's best candidate docs, for thresholds
+// shared ACROSS devices (fg_plan_seed_ladders): one workgroup per Should-only
+// slot without MustNot or facet clauses scores exactly the union of its
+// clauses' candidate docs -- each clause's best min(k, kSeedKS) alive keys
+// (SeedIndex rows) or, for a clause of at most kSeedMinDf postings, all of them
+// -- and writes the scores at the ranks kLadderKs of those DISTINCT docs.  A doc
+// is counted only from the first clause whose candidate list holds it (a
+// clause's list holds d iff d is present and, for a row, its key is >= the
+// row's kk-th key), so no doc counts twice; a doc no clause counts only lowers
+// the ladder.  Every rank of the ladder is a real doc's exact score, so the
+// shards' ladders combine (fg_kth_floor_combine) into a lower bound of the
+// query's k-th score over all shards: the start of every shard's k_disj.
+// (Started from its own slot alone, on one device, it did not pay: the shared
+// score histograms already raise a query's threshold within its first items,
+// profiles/r05/ab/ab_seed_layout.json.)
 struct SeedShared {
   alignas(16) uint64_t buf[kSeedCap];
   uint32_t hist[1u << kHistBits];
@@ -1629,14 +1634,13 @@ struct SeedShared {
 
 template <bool kMulti>
 __global__ __launch_bounds__(kThreads) void k_seed(DevIndex ix0, DevPlan pl, const SeedIndex* __restrict__ six,
-                                                   const uint32_t* __restrict__ seed_q) {
+                                                   const uint32_t* __restrict__ seed_q, float* __restrict__ out) {
   __shared__ SeedShared sh;
   const uint32_t tid = threadIdx.x;
   const uint32_t v = seed_q[blockIdx.x];
   const uint32_t s = kMulti ? v / pl.seg_nq : 0u;
   const DevIndex ix = kMulti ? seg_index(pl, s) : ix0;
   const SeedIndex sx = six[s];
-  const uint32_t ql = kMulti ? v % pl.seg_nq : v;
   const uint32_t qmv = pl.q_m[v];
   const uint32_t m = qm_terms(qmv) - qm_not(qmv);  // Should clauses (a seeded query has no MustNot)
   const uint32_t* terms = pl.q_terms + (size_t)v * kMaxTerms;
@@ -1695,25 +1699,18 @@ __global__ __launch_bounds__(kThreads) void k_seed(DevIndex ix0, DevPlan pl, con
     if (n > kSeedCap - kThreads && n > K) truncate_keys<kSeedCap>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
   }
   __syncthreads();
-  const uint32_t n = sh.n_buf;
-  if (n < K) return;  // fewer than k distinct candidates: no seed
-  uint64_t T;
-  if (n == K) {  // the smallest key
-    uint64_t mn = ~0ull;
-    for (uint32_t i = tid; i < n; i += kThreads) mn = min(mn, sh.buf[i]);
-    for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint64_t)__shfl_xor((long long)mn, o, 64));
-    uint64_t* red = reinterpret_cast<uint64_t*>(sh.hist);
-    if (lane_id() == 0) red[wave_id()] = mn;
-    __syncthreads();
-    T = red[0];
-    for (uint32_t w = 1; w < kThreads / 64; ++w) T = min(T, red[w]);
-  } else {
-    T = select_kth(K, sh.hist, sh.scratch, [&](auto&& f) {
-      for (uint32_t i = tid; i < n; i += kThreads) f(sh.buf[i]);
-    });
+  // the counted keys sorted: the slot's ladder, the j-th best score at the ranks
+  // kLadderKs (exact up to K: a truncation kept the K best of everything counted)
+  const uint32_t n = min(sh.n_buf, kSeedCap);
+  uint32_t P = 16;
+  while (P < n) P <<= 1;
+  for (uint32_t i = n + tid; i < P; i += kThreads) sh.buf[i] = 0;
+  __syncthreads();
+  bitonic_sort_desc(sh.buf, P);
+  if (tid < kNumLadder) {
+    const uint32_t r = kLadderKs[tid];
+    out[(size_t)v * kNumLadder + tid] = r <= n && r <= K ? key_score(sh.buf[r - 1]) : 0.0f;
   }
-  // score-only: every doc scoring the k-th candidate's score or more is kept
-  if (tid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&pl.thresh[ql]), (unsigned long long)(T & 0xFFFFFFFF00000000ull));
 }
 
 // ---------------------------------------------------------------- k_fmask
@@ -2106,10 +2103,10 @@ hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
 }
 
 hipError_t launch_seed(const DevIndex& ix, const DevPlan& pl, const SeedIndex* six, const uint32_t* seed_q,
-                       uint32_t n_seed, hipStream_t s) {
+                       uint32_t n_seed, float* out, hipStream_t s) {
   if (n_seed == 0) return hipSuccess;
-  if (pl.segs) k_seed<true><<<n_seed, kThreads, 0, s>>>(ix, pl, six, seed_q);
-  else k_seed<false><<<n_seed, kThreads, 0, s>>>(ix, pl, six, seed_q);
+  if (pl.segs) k_seed<true><<<n_seed, kThreads, 0, s>>>(ix, pl, six, seed_q, out);
+  else k_seed<false><<<n_seed, kThreads, 0, s>>>(ix, pl, six, seed_q, out);
   return hipGetLastError();
 }
 
