@@ -421,6 +421,8 @@ hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);  // packed chunks
 hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s);                        // after k_bucket
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
+// src -> dst on a compute queue (16-B aligned ends; pinned host memory on one side)
+hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
 // k_seed: the ladders of n_seed query slots (seed_q) into out[slot * kNumLadder]; six[s] = snapshot s's top lists
 hipError_t launch_seed(const DevIndex& ix, const DevPlan& pl, const SeedIndex* six, const uint32_t* seed_q,
                        uint32_t n_seed, float* out, hipStream_t s);

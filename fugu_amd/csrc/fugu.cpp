@@ -243,6 +243,30 @@ namespace {
 thread_local hipStream_t tl_build_stream = hipStreamPerThread;
 #define kBuildStream tl_build_stream
 
+// The latency path's small transfers through pinned host memory (a batch's
+// plan upload, its hits' download): a copy kernel on the search's own stream
+// when at most kKernelCopyMax bytes, so they do not wait behind a commit's bulk
+// transfers on the copy engines; hipMemcpyAsync above that, or with
+// FUGU_KCOPY=0 (A/B).  `host` is a pinned block of a PinnedPool (device-mapped).
+constexpr size_t kKernelCopyMax = 1u << 20;
+static hipError_t pinned_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = getenv("FUGU_KCOPY");
+    return !(e && *e == '0');
+  }();
+  if (!on || bytes > kKernelCopyMax || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15))
+    return hipMemcpyAsync(dst, src, bytes, kind, s);
+  // the host side's device address (the runtime's mapping of the pinned block);
+  // not mapped -> the copy engines after all
+  void* host = kind == hipMemcpyHostToDevice ? const_cast<void*>(src) : dst;
+  void* dmap = nullptr;
+  if (hipHostGetDevicePointer(&dmap, host, 0) != hipSuccess || !dmap) {
+    (void)hipGetLastError();
+    return hipMemcpyAsync(dst, src, bytes, kind, s);
+  }
+  return kind == hipMemcpyHostToDevice ? fg::launch_copy(dst, dmap, bytes, s) : fg::launch_copy(dmap, src, bytes, s);
+}
+
 // low-priority streams of a device for background rescoring, created once
 hipStream_t low_priority_stream(int dev, uint32_t i) {
   static std::mutex mu;
@@ -2397,7 +2421,8 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // on the planning thread's own stream (or the caller's `up`): a plan built
   // while another thread's batch runs does not serialise against it through the
   // legacy null stream
-  HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, up));
+  if (pin.p) HIPCHK(pinned_copy(base, staging, s_up, hipMemcpyHostToDevice, up));
+  else HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, up));
   p->up_stream = up;
   p->zeroed = s_up > s_in;
   if (sync || !pin.p) {
@@ -2528,7 +2553,7 @@ int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* o
   if (span <= (4ull << 20)) {
     PinnedLease pin(p->ix->pinned, span);
     if (pin.p) {
-      HIPCHK(hipMemcpyAsync(pin.p, first, span, hipMemcpyDeviceToHost, s));
+      HIPCHK(pinned_copy(pin.p, first, span, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       const char* h = static_cast<const char*>(pin.p);
       if (out_score) std::memcpy(out_score, h, 4 * nk);
@@ -2901,7 +2926,7 @@ static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32
   if (span <= (4ull << 20)) {
     PinnedLease pin(shards[0]->pinned, span);
     if (pin.p) {
-      HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
+      HIPCHK(pinned_copy(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
       HIPCHK(hipStreamSynchronize(hipStreamPerThread));
       const char* h = static_cast<const char*>(pin.p);
       std::memcpy(out_score, h, 4 * nk);
@@ -3098,7 +3123,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   if (span <= (4ull << 20)) {
     PinnedLease pin(shards[0]->pinned, span);
     if (pin.p) {
-      HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
+      HIPCHK(pinned_copy(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
       HIPCHK(hipStreamSynchronize(hipStreamPerThread));
       const char* h = static_cast<const char*>(pin.p);
       std::memcpy(out_score, h, 4 * nk);
