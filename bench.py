@@ -515,14 +515,11 @@ def bench_c4(ctx, corp, native, synth, torch, dev, nq, K, steps, warmup, threads
             "projected_8gpu": "each GPU runs one namespace: step ~ max(k_conj_ms_per_namespace) + k_final + gather"}
 
 
-def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps, qfloor=False):
+def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps):
     """Every shard's plan run ALONE (no shared threshold word): each shard's
     kernel ms as one GPU of an 8-GPU doc-sharded run sees it (k_disj / k_conj,
-    k_final), and the hash of the hits merged from the shards' lists.  qfloor:
-    every plan first starts from the per-query floor of ALL shards' query
-    ladders (shard.exchange_query_floor: what one all-gather per batch gives
-    the GPUs of the split); returns its wall ms beside."""
-    from fugu_amd.shard import exchange_query_floor, merge_on_device
+    k_final), and the hash of the hits merged from the shards' lists."""
+    from fugu_amd.shard import merge_on_device
     import torch
     nq = len(q_off) - 1
     dev = torch.device(f"cuda:{torch.cuda.current_device()}")
@@ -530,15 +527,8 @@ def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps, qfloor=False):
     gd = torch.empty((len(ixs), nq * K), dtype=torch.int32, device=dev)
     gn = torch.empty((len(ixs), nq), dtype=torch.int32, device=dev)
     ms = []
-    plans = [ix.plan(q_off, terms, K, mode) for ix in ixs]
-    xch_ms = None
-    if qfloor:
-        exchange_query_floor(plans, K, st)  # warm
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        exchange_query_floor(plans, K, st)
-        xch_ms = round((time.perf_counter() - t0) * 1e3, 3)
-    for r, p in enumerate(plans):
+    for r, ix in enumerate(ixs):
+        p = ix.plan(q_off, terms, K, mode)
         p.execute(st, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
         torch.cuda.synchronize()
         p.profile(True)
@@ -548,11 +538,8 @@ def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps, qfloor=False):
         m, n = p.kernel_ms()
         ms.append((round(m[0] / max(n, 1), 4), round(m[1] / max(n, 1), 4)))
         p.close()
-    del plans
     out = merge_on_device(gs, gd, gn, nq, K, st)
     torch.cuda.synchronize()
-    if qfloor:
-        return ms, hits_sha1(out[0], out[1], out[2], out[3], K), xch_ms
     return ms, hits_sha1(out[0], out[1], out[2], out[3], K)
 
 
@@ -620,8 +607,6 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     seed_kth_floor(ixs)
     seed_s = time.time() - t0
     alone_se, sha_se = alone_kernel_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2))
-    alone_qf, sha_qf, xch_ms = alone_kernel_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2),
-                                               qfloor=True)
     log(f"[bench] C5 shards alone: unseeded max {max(x[0] for x in alone_un)} ms, seeded max "
         f"{max(x[0] for x in alone_se)} ms (linked mean {np.mean(per_shard):.3f}); floor in {seed_s:.1f}s")
     # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel),
@@ -669,18 +654,11 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
                "unseeded_max": max(x[0] for x in alone_un), "seeded_max": max(x[0] for x in alone_se),
                "k_final_ms_seeded": [x[1] for x in alone_se],
                "seeded_max_over_linked_mean": round(max(x[0] for x in alone_se) / float(np.mean(per_shard)), 3),
-               "query_floor": [x[0] for x in alone_qf], "query_floor_max": max(x[0] for x in alone_qf),
-               "query_floor_max_over_linked_mean": round(max(x[0] for x in alone_qf) / float(np.mean(per_shard)), 3),
-               "query_floor_exchange_ms": xch_ms,
-               "result_sha1_unseeded": sha_un, "result_sha1_seeded": sha_se, "result_sha1_query_floor": sha_qf,
-               "same_hits": sha_un == sha_se == sha_qf,
+               "result_sha1_unseeded": sha_un, "result_sha1_seeded": sha_se, "same_hits": sha_un == sha_se,
                "floor_s": round(seed_s, 2),
                "note": "each shard's plan alone (no shared threshold word: one GPU of the 8-GPU split); seeded = "
                        "its starting thresholds floored by the namespace-wide per-term K-th score bounds "
-                       "(fg_index_term_ladder of every shard, one all-gather at build, fg_kth_floor_combine); "
-                       "query_floor = seeded + every query started from the combined query ladders of all 8 shards "
-                       "(fg_plan_seed_ladders, one all-gather per batch, fg_plan_set_query_floor; "
-                       "query_floor_exchange_ms = the 8 ladder launches + D2H + combine + upload, one GPU)"},
+                       "(fg_index_term_ladder of every shard, one all-gather at build, fg_kth_floor_combine)"},
            "multi_plan_unseeded": {"ms_per_step": round(el0 * 1e3 / max(2, steps // 2), 4),
                                    "kernels_ms": [round(mk0[0] / max(mkn0, 1), 4), round(mk0[1] / max(mkn0, 1), 4)],
                                    "result_sha1": sha_multi_un},
@@ -802,15 +780,7 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     mouts = [torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)] + [
         torch.empty(nq, dtype=torch.int32, device=dev)]
 
-    # c5: every batch first shares per-query thresholds across the ranks (the query
-    # ladders of every shard, ONE all-gather: shard.exchange_query_floor), so no
-    # rank starts from its own docs' k-th score alone
-    qfloor = (not c4) and os.environ.get("FUGU_C5_QFLOOR", "1") != "0"
-
     def step():
-        if qfloor:
-            from fugu_amd.shard import exchange_query_floor
-            exchange_query_floor(plans, K, st.cuda_stream, device=dev if backend == "nccl" else None)
         if merged_sel:  # the rank's units merged by the plan's own final select
             plans[0].execute_merged(st.cuda_stream, *[x.data_ptr() for x in mouts])
             ms, md, msh, mn = mouts
@@ -905,7 +875,6 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
             **({"per_rank": per_rank} if per_rank else {}),
             "rank_plan": ("one multi-snapshot plan over the rank's units, merged by its final select"
                           if merged_sel else f"{len(plans)} linked plan(s) + k_merge_rank"),
-            "query_floor_exchange": bool(qfloor),
             "result_sha1": h.hexdigest()[:16],
             "hits": int(mn.sum()),
             **({"kth_floor": floor_info} if floor_info else {}),

@@ -408,10 +408,6 @@ struct fg_index {
   // k_ktop's tables (structure): long terms, their first chunk, each chunk's term and first posting
   const uint32_t *d_kb_terms = nullptr, *d_kb_chunk0 = nullptr, *d_kc_big = nullptr, *d_kc_start = nullptr;
   uint32_t n_sc = 0, n_bk = 0, n_kt = 0, n_kbig = 0, n_kchunks = 0;
-  // k_seed (fg_internal.h SeedIndex): each term's row (structure) and the rows' kept keys (scoring)
-  const uint32_t* d_seed_slot = nullptr;
-  uint32_t n_seed_rows = 0;
-  const uint64_t* d_seed_keys = nullptr;
   fg::DevIndex d{};
   DevAllocs mem;
   fgh::ScoreBlock sblock;
@@ -466,10 +462,5 @@ struct fg_plan {
   void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
   size_t pin_n = 0;
   hipStream_t up_stream = hipStreamPerThread;  // the stream the plan was uploaded on
-  // k_seed (fg_plan_seed_ladders): the query slots it scores and each snapshot's SeedIndex (in the workspace)
-  const uint32_t* seed_q = nullptr;
-  const fg::SeedIndex* seed_ix = nullptr;
-  uint32_t n_seed = 0;
-  std::vector<uint64_t> h_thr0;  // the planned starting thresholds (fg_plan_set_query_floor)
 };
 

@@ -111,22 +111,6 @@ constexpr uint32_t kLadderExtra[kNumLadderExtra] = {2, 3, 5, 13, 25, 50, 125, 25
 constexpr uint32_t kNumLadder = kNumTopK + kNumLadderExtra;  // FG_LADDER_LEVELS
 constexpr uint32_t kLadderKs[kNumLadder] = {1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000};
 
-// Query ladders for thresholds shared across devices (k_seed,
-// fg_plan_seed_ladders).  Every term with more than kSeedMinDf postings keeps
-// its kSeedKS best alive keys, sorted (written by the k_ktop kernels, scoring);
-// shorter terms are read whole.  One workgroup per Should-only query slot
-// scores exactly the union of its clauses' candidate docs (each clause's best
-// min(k, kSeedKS), or all its postings) and writes the scores at the ranks
-// kLadderKs of those distinct docs: real docs, so every shard's ladder bounds
-// the query's k-th score from below, and the shards' ladders combine.
-constexpr uint32_t kSeedKS = 256;
-constexpr uint32_t kSeedMinDf = 1024;
-constexpr uint32_t kSeedCap = 2048;  // k_seed's key buffer (truncated to k when full)
-struct SeedIndex {
-  const uint64_t* keys;   // [n_seed_terms * kSeedKS] best alive keys per term, descending (0: none)
-  const uint32_t* slot;   // [V] the term's row in keys, or 0xFFFFFFFF (kSeedMinDf postings or fewer)
-};
-
 constexpr uint32_t kMaxFacetClauses = 8;  // facet clauses per query (FG_MAX_FACET_CLAUSES)
 constexpr uint32_t kFmaskChunk = 8192;    // facet postings per k_fmask workgroup
 constexpr uint32_t kScanMaxGroup = 32;    // k_scan: at most this many 4096-doc tiles per work item
@@ -370,8 +354,6 @@ struct ScoreJob {
   uint32_t n_tiles;           // tiles per term (4096-doc k_disj tiles)
   float* ktop;                // [V * kNumTopK] out (zeroed first)
   float* ladder;              // [V * kNumLadderExtra] out (zeroed first) or nullptr: fg_index_term_ladder only
-  uint64_t* seed_keys;        // [seed rows * kSeedKS] out (zeroed first): SeedIndex::keys, or nullptr
-  const uint32_t* seed_slot;  // [V] SeedIndex::slot
   float* cmax;               // [cmax entries] out: the largest score of each kChunk postings of a term
   const uint32_t* coff;       // [V] first cmax entry of each term
   // packed chunk tables (a chunk: terms [tf, tl], postings / directory entries
@@ -423,9 +405,6 @@ hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s);      
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
 // src -> dst on a compute queue (16-B aligned ends; pinned host memory on one side)
 hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
-// k_seed: the ladders of n_seed query slots (seed_q) into out[slot * kNumLadder]; six[s] = snapshot s's top lists
-hipError_t launch_seed(const DevIndex& ix, const DevPlan& pl, const SeedIndex* six, const uint32_t* seed_q,
-                       uint32_t n_seed, float* out, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

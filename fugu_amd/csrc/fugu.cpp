@@ -478,7 +478,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   struct Part { size_t bytes; void** out; };
   float *d_wt, *d_wn, *d_cache, *d_psc, *d_bmax, *d_ktop, *d_cmax;
   uint64_t* d_tsub = nullptr;
-  uint64_t* d_seed = nullptr;
   uint32_t *d_alive = nullptr, *d_tmaxs, *d_tmax;
   const Part parts[] = {
       {4ull * V, reinterpret_cast<void**>(&d_wt)},
@@ -492,7 +491,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       {4ull * V * fg::kNumTopK, reinterpret_cast<void**>(&d_ktop)},
       {4ull * ix->n_sc, reinterpret_cast<void**>(&d_cmax)},
       {8ull * ix->tile_entries, reinterpret_cast<void**>(&d_tsub)},
-      {8ull * fg::kSeedKS * ix->n_seed_rows, reinterpret_cast<void**>(&d_seed)},
   };
   size_t total = 0;
   for (const Part& pt : parts) total += (std::max<size_t>(pt.bytes, 16) + 255) & ~size_t(255);
@@ -526,7 +524,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, kBuildStream));
   HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), kBuildStream));
   HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, kBuildStream));
-  if (d_seed) HIPCHK(hipMemsetAsync(d_seed, 0, 8ull * fg::kSeedKS * ix->n_seed_rows, kBuildStream));
   fg::ScoreJob j{};
   j.doc = ix->d.doc;
   j.tfp = ix->d_tfp;
@@ -560,8 +557,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.kt_tiny = ix->d_kt_tiny;
   j.n_tiny = ix->n_ktiny;
   j.coff = ix->d.coff;
-  j.seed_keys = d_seed;
-  j.seed_slot = ix->d_seed_slot;
   HIPCHK(fg::launch_score(j, ix->n_scb, kBuildStream));
   HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
   j.tsub = d_tsub;
@@ -649,7 +644,6 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   ix->d.cmax = d_cmax;
   ix->d.alive = d_alive;
   ix->d.dense = d_dense;
-  ix->d_seed_keys = d_seed;
   ix->device_bytes = ix->struct_bytes + bytes;
   return FG_OK;
 }
@@ -769,8 +763,6 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   // long tail of a vocabulary in a workgroup per term was most of a small
   // segment's scoring time
   std::vector<uint32_t> kt, kt_tiny, coff(V), kb_terms, kb_chunk0, kc_big, kc_start;
-  std::vector<uint32_t> seed_slot(V, 0xFFFFFFFFu);  // k_seed: a row of kept keys per term past kSeedMinDf postings
-  uint32_t n_seed_rows = 0;
   std::vector<uint32_t> sc_tf, sc_tl, bk_tf, bk_tl, bk_e0, bk_e1;
   std::vector<uint64_t> sc_e0, sc_e1;
   uint32_t n_cmax = 0;
@@ -846,7 +838,6 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   for (uint32_t t = 0; t < V; ++t) {
     const uint64_t n = hp.off[t + 1] - hp.off[t];
     if (!n) continue;
-    if (n > fg::kSeedMinDf) seed_slot[t] = n_seed_rows++;
     if (n <= fg::kKtopTiny) {
       kt_tiny.push_back(t);
       continue;
@@ -871,8 +862,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc, *d_tterm;
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
-  uint32_t *d_sctf, *d_sctl, *d_bktf, *d_bktl, *d_bke0, *d_bke1, *d_kt, *d_ktt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs,
-      *d_seedslot;
+  uint32_t *d_sctf, *d_sctl, *d_bktf, *d_bktl, *d_bke0, *d_bke1, *d_kt, *d_ktt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs;
   uint64_t *d_sce0, *d_sce1;
   {
     UploadBatch ub;
@@ -903,7 +893,6 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ub.add(kc_big.data(), kc_big.size(), &d_kcb);
     ub.add(kc_start.data(), kc_start.size(), &d_kcs);
     ub.add(coff.data(), coff.size(), &d_coff);
-    ub.add(seed_slot.data(), seed_slot.size(), &d_seedslot);
     if ((rc = ub.commit(sm, &bytes))) return rc;
   }
   std::vector<uint32_t>().swap(hp.tf);
@@ -1008,8 +997,6 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d_kc_start = d_kcs;
   ix->n_kbig = (uint32_t)kb_terms.size();
   ix->n_kchunks = (uint32_t)kc_big.size();
-  ix->d_seed_slot = d_seedslot;
-  ix->n_seed_rows = n_seed_rows;
   ix->n_sc = n_cmax;
   ix->n_scb = (uint32_t)sc_tf.size();
   ix->n_bk = (uint32_t)bk_tf.size();
@@ -1551,8 +1538,6 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->d_kc_start = base->d_kc_start;
   ix->n_kbig = base->n_kbig;
   ix->n_kchunks = base->n_kchunks;
-  ix->d_seed_slot = base->d_seed_slot;
-  ix->n_seed_rows = base->n_seed_rows;
   ix->n_sc = base->n_sc;
   ix->n_scb = base->n_scb;
   ix->n_bk = base->n_bk;
@@ -1860,7 +1845,6 @@ struct HostPlan {
   std::vector<uint32_t> ch_f, ch_c, ch_t, ch_s;
   std::vector<WItem> citems, ditems, scan;
   std::vector<uint32_t> ngroup, q_hlo, q_hhi, q_hsh;
-  std::vector<uint32_t> seedq;  // queries k_seed starts (fg_internal.h kSeedKS)
 };
 
 // n_segs: the snapshots the plan spans; a query's work items are spread over
@@ -1974,7 +1958,6 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   q_hhi.assign(nq, 0x3F800000u);
   q_hsh.assign(nq, 31);
   auto present = [&](uint32_t t) { return t < ix->n_terms && ix->off[t + 1] > ix->off[t]; };
-  h.seedq.clear();
   // the term's K-th best alive score at level j: the snapshot's own, or the
   // namespace-wide floor of a doc-sharded namespace's shard when higher
   // (fg_index_set_kth_floor)
@@ -2071,8 +2054,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       float ub = fmx;
       for (uint32_t c = 0; c < ns; ++c) ub += ix->tmaxs[qt[c]];
       set_bins(i, ub);
-      // k_seed's slots (fg_plan_seed_ladders): unfiltered, unexcluded unions
-      if (q_filter[i] == 0xFFFFFFFFu && nx == 0 && ix->d_seed_keys) h.seedq.push_back(i);
+
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
       const uint32_t nt = thi - tlo + 1;
       // tiles per item: ~gpq items per query (capping an item's postings, or the
@@ -2193,7 +2175,6 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   std::vector<uint64_t> thr0, f_woff;
   std::vector<float> q_ub, f_tab, f_max;
   std::vector<WItem> citems, ditems, scan;
-  std::vector<uint32_t> seedq;
   uint32_t nf = 0;
   if (S == 1) {
     HostPlan& h = hs[0];
@@ -2202,7 +2183,6 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     f_shift.swap(h.f_shift); f_woff.swap(h.f_woff); f_tab.swap(h.f_tab); f_max.swap(h.f_max);
     ch_f.swap(h.ch_f); ch_c.swap(h.ch_c); ch_t.swap(h.ch_t); ch_s.swap(h.ch_s);
     citems.swap(h.citems); ditems.swap(h.ditems); scan.swap(h.scan);
-    seedq.swap(h.seedq);
     nf = h.nf;
   } else {
     auto cat = [](auto& dst, const auto& src) { dst.insert(dst.end(), src.begin(), src.end()); };
@@ -2224,7 +2204,6 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
       for (WItem x : h.citems) { x.q += vb; citems.push_back(x); }
       for (WItem x : h.ditems) { x.q += vb; ditems.push_back(x); }
       for (WItem x : h.scan) { x.q += vb; scan.push_back(x); }
-      for (uint32_t x : h.seedq) seedq.push_back(vb + x);
       nf += h.nf;
     }
     // one bin geometry per batch query over the snapshots where it has work
@@ -2325,8 +2304,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
                s_qf = al(4ull * nq), s_fs = al(4ull * nf),
                s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch),
                s_hb = al(4ull * nq), s_fg = S > 1 ? al(4ull * nf) : 0,
-               s_sg = S > 1 ? al(sizeof(fg::DevIndex) * S) : 0, s_sb = S > 1 ? al(4ull * S) : 0,
-               s_sq = al(4ull * seedq.size()), s_si = seedq.empty() ? 0 : al(sizeof(fg::SeedIndex) * S);
+               s_sg = S > 1 ? al(sizeof(fg::DevIndex) * S) : 0, s_sb = S > 1 ? al(4ull * S) : 0;
   // the snapshots' first docs in their concatenation (k_final's merged select)
   std::vector<uint32_t> seg_base;
   if (S > 1) {
@@ -2338,7 +2316,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     if (b > 0xFFFFFFFFull) seg_base.clear();  // no merged select past 2^32 docs
   }
   const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft +
-                      s_fm + 4 * s_ch + 2 * s_hb + s_fg + s_sg + s_sb + s_sq + s_si;
+                      s_fm + 4 * s_ch + 2 * s_hb + s_fg + s_sg + s_sb;
   // one score histogram per query (DevPlan::hist: k_conj's and k_disj's running thresholds)
   // (thresholds and histograms: one per batch query, shared by its slots)
   const size_t s_thr = al(8ull * nq1), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]),
@@ -2390,7 +2368,6 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->d.work_n = (const uint32_t*)put(work_n.data(), 4ull * chunks, s_wn);
   p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
   p->d.q_thr0 = (const uint64_t*)put(thr0.data(), 8ull * nq, s_t0);
-  p->h_thr0 = thr0;  // fg_plan_set_query_floor raises it
   p->d.q_ub = (const float*)put(q_ub.data(), 4ull * nq * fg::kMaxTerms, s_ub);
   p->d.f.q_filter = (const uint32_t*)put(q_filter.data(), 4ull * nq, s_qf);
   p->d.f.f_shift = (const uint32_t*)put(f_shift.data(), 4ull * nf, s_fs);
@@ -2410,13 +2387,6 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     p->d.segs = (const fg::DevIndex*)put(segs.data(), sizeof(fg::DevIndex) * S, s_sg);
     const uint32_t* sb = (const uint32_t*)put(seg_base.data(), 4ull * seg_base.size(), s_sb);
     p->d.seg_base = seg_base.empty() ? nullptr : sb;
-  }
-  if (!seedq.empty()) {
-    std::vector<fg::SeedIndex> six(S);
-    for (uint32_t s = 0; s < S; ++s) six[s] = fg::SeedIndex{ixs[s]->d_seed_keys, ixs[s]->d_seed_slot};
-    p->seed_q = (const uint32_t*)put(seedq.data(), 4ull * seedq.size(), s_sq);
-    p->seed_ix = (const fg::SeedIndex*)put(six.data(), sizeof(fg::SeedIndex) * S, s_si);
-    p->n_seed = (uint32_t)seedq.size();
   }
   // on the planning thread's own stream (or the caller's `up`): a plan built
   // while another thread's batch runs does not serialise against it through the
@@ -2514,30 +2484,6 @@ int fg_plan_execute_merged(fg_plan* p, void* stream, float* d_out_score, uint32_
   if (p->n_segs < 2 || !p->d.seg_base)
     return fail(FG_EUNSUPPORTED, "not a multi-snapshot plan over < 2^32 docs (use fg_plan_execute + fg_merge_shards)");
   return execute_impl(p, static_cast<hipStream_t>(stream), d_out_score, d_out_doc, d_out_n, d_out_shard);
-}
-
-int fg_plan_seed_ladders(fg_plan* p, void* stream, float* d_out) {
-  if (!p || !d_out) return fail(FG_EINVAL, "bad arguments");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  HIPCHK(hipSetDevice(p->ix->dev));
-  HIPCHK(hipMemsetAsync(d_out, 0, 4ull * p->nq * fg::kNumLadder, s));
-  HIPCHK(fg::launch_seed(p->ix->d, p->d, p->seed_ix, p->seed_q, p->n_seed, d_out, s));
-  return FG_OK;
-}
-
-int fg_plan_set_query_floor(fg_plan* p, const float* floor) {
-  if (!p) return fail(FG_EINVAL, "NULL plan");
-  std::vector<uint64_t> t0(p->h_thr0);
-  if (floor)
-    for (uint32_t v = 0; v < p->nq; ++v) {
-      const float f = floor[fg::slot_query(p->d, v)];
-      if (f > 0.0f) t0[v] = std::max(t0[v], fg::make_key(f, 0xFFFFFFFFu));  // score-only: the lowest key of f
-    }
-  HIPCHK(hipSetDevice(p->ix->dev));
-  HIPCHK(hipMemcpyAsync(const_cast<uint64_t*>(p->d.q_thr0), t0.data(), 8ull * p->nq, hipMemcpyHostToDevice,
-                        hipStreamPerThread));
-  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
-  return FG_OK;
 }
 
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n) {

@@ -1606,113 +1606,6 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
 #undef FG_PHASE
 }
 
-// ---------------------------------------------------------------- k_seed
-// The score ladder of a query slot's best candidate docs, for thresholds
-// shared ACROSS devices (fg_plan_seed_ladders): one workgroup per Should-only
-// slot without MustNot or facet clauses scores exactly the union of its
-// clauses' candidate docs -- each clause's best min(k, kSeedKS) alive keys
-// (SeedIndex rows) or, for a clause of at most kSeedMinDf postings, all of them
-// -- and writes the scores at the ranks kLadderKs of those DISTINCT docs.  A doc
-// is counted only from the first clause whose candidate list holds it (a
-// clause's list holds d iff d is present and, for a row, its key is >= the
-// row's kk-th key), so no doc counts twice; a doc no clause counts only lowers
-// the ladder.  Every rank of the ladder is a real doc's exact score, so the
-// shards' ladders combine (fg_kth_floor_combine) into a lower bound of the
-// query's k-th score over all shards: the start of every shard's k_disj.
-// (Started from its own slot alone, on one device, it did not pay: the shared
-// score histograms already raise a query's threshold within its first items,
-// profiles/r05/ab/ab_seed_layout.json.)
-struct SeedShared {
-  alignas(16) uint64_t buf[kSeedCap];
-  uint32_t hist[1u << kHistBits];
-  uint32_t scratch[8];
-  uint64_t bound[kMaxTerms];   // membership: key >= bound (0: every present posting)
-  uint32_t row[kMaxTerms];     // the clause's SeedIndex row, or kInvalid (read whole)
-  uint32_t cstart[kMaxTerms + 1];  // candidates of clauses [0, c) in the flat list
-  uint32_t n_buf;
-};
-
-template <bool kMulti>
-__global__ __launch_bounds__(kThreads) void k_seed(DevIndex ix0, DevPlan pl, const SeedIndex* __restrict__ six,
-                                                   const uint32_t* __restrict__ seed_q, float* __restrict__ out) {
-  __shared__ SeedShared sh;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t v = seed_q[blockIdx.x];
-  const uint32_t s = kMulti ? v / pl.seg_nq : 0u;
-  const DevIndex ix = kMulti ? seg_index(pl, s) : ix0;
-  const SeedIndex sx = six[s];
-  const uint32_t qmv = pl.q_m[v];
-  const uint32_t m = qm_terms(qmv) - qm_not(qmv);  // Should clauses (a seeded query has no MustNot)
-  const uint32_t* terms = pl.q_terms + (size_t)v * kMaxTerms;
-  const uint32_t K = pl.k, kk = min(K, kSeedKS);
-  if (tid == 0) {
-    uint32_t at = 0;
-    for (uint32_t c = 0; c < m; ++c) {
-      const uint32_t t = terms[c], row = sx.slot[t];
-      sh.row[c] = row;
-      sh.cstart[c] = at;
-      if (row == kInvalid) {
-        sh.bound[c] = 0;
-        at += (uint32_t)(ix.off[t + 1] - ix.off[t]);
-      } else {
-        sh.bound[c] = sx.keys[(size_t)row * kSeedKS + kk - 1];  // 0: the row holds every alive posting
-        at += kk;
-      }
-    }
-    sh.cstart[m] = at;
-    sh.n_buf = 0;
-  }
-  __syncthreads();
-  const uint32_t total = sh.cstart[m];
-  for (uint32_t e0 = 0; e0 < total; e0 += kThreads) {
-    const uint32_t e = e0 + tid;
-    bool keep = false;
-    uint64_t key = 0;
-    if (e < total) {
-      uint32_t c = 0;
-      while (sh.cstart[c + 1] <= e) ++c;
-      const uint32_t i = e - sh.cstart[c], t = terms[c];
-      uint32_t d = 0;
-      if (sh.row[c] != kInvalid) {
-        const uint64_t x = sx.keys[(size_t)sh.row[c] * kSeedKS + i];
-        keep = x != 0;
-        d = key_doc(x);
-      } else {
-        d = ix.doc[ix.off[t] + i];
-        keep = doc_alive(ix, d);
-      }
-      float sum = 0.0f;
-      for (uint32_t j = 0; j < m && keep; ++j) {
-        const uint32_t dd[1] = {d};
-        float sc[1];
-        probe_list<1>(ix, terms[j], dd, 1u, sc);
-        if (sc[0] < 0.0f) continue;  // clause j is not on d
-        sum += sc[0];
-        // an earlier clause whose list holds d counts it instead
-        if (j < c && make_key(sc[0], d) >= sh.bound[j]) keep = false;
-      }
-      key = make_key(sum, d);
-    }
-    wave_append(keep, key, sh.buf, &sh.n_buf, kSeedCap);
-    __syncthreads();
-    const uint32_t n = sh.n_buf;  // uniform
-    if (n > kSeedCap - kThreads && n > K) truncate_keys<kSeedCap>(sh.buf, &sh.n_buf, sh.hist, sh.scratch, n, K);
-  }
-  __syncthreads();
-  // the counted keys sorted: the slot's ladder, the j-th best score at the ranks
-  // kLadderKs (exact up to K: a truncation kept the K best of everything counted)
-  const uint32_t n = min(sh.n_buf, kSeedCap);
-  uint32_t P = 16;
-  while (P < n) P <<= 1;
-  for (uint32_t i = n + tid; i < P; i += kThreads) sh.buf[i] = 0;
-  __syncthreads();
-  bitonic_sort_desc(sh.buf, P);
-  if (tid < kNumLadder) {
-    const uint32_t r = kLadderKs[tid];
-    out[(size_t)v * kNumLadder + tid] = r <= n && r <= K ? key_score(sh.buf[r - 1]) : 0.0f;
-  }
-}
-
 // ---------------------------------------------------------------- k_fmask
 // Facet masks of a batch's filters (DevFilters): one workgroup per 8192
 // postings of one (filter, clause) facet list sets clause bit i of every doc
@@ -2123,14 +2016,6 @@ hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s) 
   return hipGetLastError();
 }
 
-hipError_t launch_seed(const DevIndex& ix, const DevPlan& pl, const SeedIndex* six, const uint32_t* seed_q,
-                       uint32_t n_seed, float* out, hipStream_t s) {
-  if (n_seed == 0) return hipSuccess;
-  if (pl.segs) k_seed<true><<<n_seed, kThreads, 0, s>>>(ix, pl, six, seed_q, out);
-  else k_seed<false><<<n_seed, kThreads, 0, s>>>(ix, pl, six, seed_q, out);
-  return hipGetLastError();
-}
-
 hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   if (pl.f.n_chunks == 0) return hipSuccess;
   if (pl.segs) k_fmask<true><<<pl.f.n_chunks, kThreads, 0, s>>>(ix, pl);
@@ -2460,12 +2345,6 @@ __device__ void ktop_finish(const ScoreJob& j, uint32_t t, uint32_t na, KtopShar
       if (nt >= kTopKs[kk]) j.ktop[(size_t)t * kNumTopK + kk] = key_score(sh.top[kTopKs[kk] - 1]);
   if (j.ladder && threadIdx.x < kNumLadderExtra && nt >= kLadderExtra[threadIdx.x])
     j.ladder[(size_t)t * kNumLadderExtra + threadIdx.x] = key_score(sh.top[kLadderExtra[threadIdx.x] - 1]);
-  // the term's best alive keys for k_seed (terms past kSeedMinDf postings)
-  if (j.seed_keys) {
-    const uint32_t row = j.seed_slot[t];
-    if (row != kInvalid)
-      for (uint32_t i = threadIdx.x; i < min(nt, kSeedKS); i += kThreads) j.seed_keys[(size_t)row * kSeedKS + i] = sh.top[i];
-  }
 }
 
 // postings [b + p0, b + p1) as f(valid && alive, score, doc), U loads per thread

@@ -55,7 +55,6 @@ EXPORTS = (
     "fg_index_rescore_many", "fg_index_build_global",
     "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged", "fg_index_term_kth",
     "fg_model_batch", "fg_abi_version", "fg_index_term_ladder", "fg_kth_floor_combine", "fg_index_set_kth_floor",
-    "fg_plan_seed_ladders", "fg_plan_set_query_floor",
 )
 LADDER_KS = (1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000)  # FG_LADDER_LEVELS ranks
 KTH_KS = (1, 10, 20, 100, 1000)  # fg_index_term_kth / fg_index_set_kth_floor ranks
@@ -155,8 +154,6 @@ _sig("fg_index_term_kth", C.c_int, _p, C.c_uint32, _f32p)
 _sig("fg_index_term_ladder", C.c_int, _p, _f32p)
 _sig("fg_kth_floor_combine", C.c_int, C.c_uint32, C.c_uint32, C.POINTER(_f32p), _f32p)
 _sig("fg_index_set_kth_floor", C.c_int, _p, _f32p, C.c_uint32)
-_sig("fg_plan_seed_ladders", C.c_int, _p, _p, _p)
-_sig("fg_plan_set_query_floor", C.c_int, _p, _f32p)
 _sig("fg_plan_execute", C.c_int, _p, _p, _p, _p, _p)
 _sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
@@ -583,22 +580,6 @@ class Plan:
         """A multi-snapshot plan straight to the merged top-k per batch query
         (device outputs [n_batch*k] x 3, [n_batch]; raw device addresses)."""
         _check(_lib.fg_plan_execute_merged(self._h, stream, out_score, out_doc, out_shard, out_n))
-
-    def seed_ladders(self, stream: int | None, d_out: int):
-        """fg_plan_seed_ladders: every query slot's score ladder ([n_slots, len(LADDER_KS)] f32 at
-        the raw device address d_out), queued on `stream`."""
-        _check(_lib.fg_plan_seed_ladders(self._h, stream, d_out))
-
-    def set_query_floor(self, floor):
-        """fg_plan_set_query_floor: [n_batch] lower bounds of each query's k-th score over all
-        shards (None: the planned thresholds again)."""
-        if floor is None:
-            _check(_lib.fg_plan_set_query_floor(self._h, None))
-            return
-        f = np.ascontiguousarray(floor, np.float32)
-        if f.shape != (self.n_batch,):
-            raise ValueError(f"floor must be [{self.n_batch}]")
-        _check(_lib.fg_plan_set_query_floor(self._h, _ptr(f, _f32p)))
 
     def results(self):
         nq, k = self.n_queries, self.k

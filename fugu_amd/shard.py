@@ -123,50 +123,6 @@ def seed_kth_floor(indexes, group=None, device=None):
     return floor
 
 
-def query_floor(ladders, k: int):
-    """Per-query lower bounds of the k-th score over every shard, from the shards'
-    query ladders ([n_shards][nq, len(LADDER_KS)]: fg_plan_seed_ladders) combined
-    row by row (fg_kth_floor_combine); None when k is past the largest K."""
-    import numpy as np
-
-    from . import native
-    cols = [j for j, K in enumerate(native.KTH_KS) if K >= k]
-    if not cols:
-        return None
-    f = native.kth_floor_combine([np.ascontiguousarray(x, np.float32) for x in ladders])
-    return np.ascontiguousarray(f[:, cols[0]])
-
-
-def exchange_query_floor(plans, k: int, stream=None, group=None, device=None):
-    """Thresholds shared across the devices of a doc-sharded namespace, per batch:
-    every local plan's query ladders (k_seed; a multi-snapshot plan's slots are
-    its shards), ONE all-gather of them over the ranks (RCCL when `device` is the
-    rank's cuda device), the per-query floor, set on every local plan
-    (fg_plan_set_query_floor).  Returns the floor [nq] (equal on every rank)."""
-    from . import native
-    L = len(native.LADDER_KS)
-    rows = []
-    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
-    for p in plans:
-        buf = torch.empty((p.n_queries, L), dtype=torch.float32, device=dev)
-        p.seed_ladders(stream, buf.data_ptr())
-        rows.append(buf.view(-1, p.n_batch, L))
-    torch.cuda.synchronize(dev)  # the ladders were queued on `stream`
-    loc = torch.cat(rows)  # [local shards, nq, L]
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        world = dist.get_world_size(group)
-        src = loc.reshape(-1) if device is not None else loc.reshape(-1).cpu()
-        out = torch.empty(world * src.numel(), dtype=torch.float32, device=src.device)
-        dist.all_gather_into_tensor(out, src, group=group)
-        allv = out.cpu().numpy().reshape((world * loc.shape[0],) + tuple(loc.shape[1:]))
-    else:
-        allv = loc.cpu().numpy()
-    floor = query_floor(list(allv), k)
-    for p in plans:
-        p.set_query_floor(floor)
-    return floor
-
-
 def shard_ranges(n_docs: int, world: int):
     """Contiguous doc-id ranges [b, e) of the shards (tantivy segments)."""
     step = (n_docs + world - 1) // world

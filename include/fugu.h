@@ -235,22 +235,6 @@ int fg_kth_floor_combine(uint32_t n_shards, uint32_t n_terms, const float* const
  * hits.  Safe against concurrent plan creation (plans see the old or new floor). */
 int fg_index_set_kth_floor(fg_index* ix, const float* floor, uint32_t n_terms);
 
-/* Per-QUERY thresholds shared across devices (a doc-sharded namespace's shards
- * on several GPUs run their plans alone, with no threshold word in common):
- * fg_plan_seed_ladders queues, on `stream`, one workgroup per Should-only query
- * slot (no MustNot, no facet clause) that scores exactly the union of its
- * clauses' best docs (each clause's best min(k, 256) alive docs, or every
- * posting of a clause of <= 1024) and writes the scores at the ranks
- * FG_LADDER_LEVELS of those distinct docs into d_out[slot * FG_LADDER_LEVELS]
- * (device memory, n_slots x FG_LADDER_LEVELS floats; zeroed first; 0 beyond the
- * candidates found or past rank k).  The ladders of every shard (all-gathered)
- * combine with fg_kth_floor_combine (one row per query) into lower bounds of the
- * query's k-th score over all shards; fg_plan_set_query_floor(floor[n_batch])
- * then starts every later execute of the plan from them (score-only; NULL:
- * back to the planned thresholds).  Hits are unchanged. */
-int fg_plan_seed_ladders(fg_plan* p, void* stream, float* d_out);
-int fg_plan_set_query_floor(fg_plan* p, const float* floor);
-
 /* ---- query batches -------------------------------------------------------- */
 typedef struct fg_query_batch {
   uint32_t n_queries;

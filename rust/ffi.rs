@@ -205,8 +205,6 @@ extern "C" {
     pub fn fg_index_term_ladder(ix: *const fg_index, out: *mut f32) -> c_int;  // [n_terms * FG_LADDER_LEVELS]
     pub fn fg_kth_floor_combine(n_shards: u32, n_terms: u32, ladders: *const *const f32, out: *mut f32) -> c_int;
     pub fn fg_index_set_kth_floor(ix: *mut fg_index, floor: *const f32, n_terms: u32) -> c_int;
-    pub fn fg_plan_seed_ladders(p: *mut fg_plan, stream: *mut c_void, d_out: *mut f32) -> c_int;
-    pub fn fg_plan_set_query_floor(p: *mut fg_plan, floor: *const f32) -> c_int;
 
     // ---- query batches: the searcher.search(.., TopDocs::with_limit(k)) replacement
     pub fn fg_plan_create(ix: *mut fg_index, q: *const fg_query_batch, k: u32, out: *mut *mut fg_plan) -> c_int;

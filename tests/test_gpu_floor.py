@@ -124,57 +124,3 @@ def test_seeded_shards_same_hits(native, shards, m0, m1, k, mode):
         assert np.array_equal(gdoc, rd.astype(np.uint64))
         rel = np.abs(ms1[i, :m].astype(np.float64) - rs) / np.maximum(np.abs(rs), 1e-30)
         assert (rel <= RTOL).all()
-
-
-@pytest.mark.parametrize("m0,m1,k", [(2, 5, 1000), (2, 4, 100), (2, 3, 20), (2, 5, 10)])
-def test_query_floor_shards_alone_same_hits(native, shards, m0, m1, k):
-    """Shards run alone (no shared threshold word, as on separate GPUs), every
-    query started from the per-query floor of ALL shards' query ladders
-    (fg_plan_seed_ladders -> fg_kth_floor_combine row by row ->
-    fg_plan_set_query_floor): the merged hits equal the unfloored run and the
-    oracle's segmented search; every floor is <= the query's final k-th score;
-    the ladders' ranks are scores of real docs, descending."""
-    import torch
-    from fugu_amd import synth
-    from fugu_amd.shard import exchange_query_floor, merge_on_device
-    from shard_ref import merge_topk_numpy
-    ctx, c, ranges, ixs, ref = shards
-    q_off, terms = synth.queries(96, m0, m1, seed_q=13)
-    nq = len(q_off) - 1
-    plans = [ix.plan(q_off, terms, k, native.MODE_OR) for ix in ixs]
-    dev = torch.device("cuda:0")
-    L = len(native.LADDER_KS)
-    lad = torch.zeros((nq, L), dtype=torch.float32, device=dev)
-    plans[0].seed_ladders(None, lad.data_ptr())
-    torch.cuda.synchronize()
-    lad = lad.cpu().numpy()
-    assert (np.diff(lad, axis=1)[lad[:, 1:] > 0] <= 0).all()  # descending where present
-    res = {}
-    for floored in (False, True):
-        floor = exchange_query_floor(plans, k) if floored else None
-        if not floored:
-            for p in plans:
-                p.set_query_floor(None)
-        per = []
-        for p in plans:
-            p.execute()
-            per.append(p.results())
-        res[floored] = (merge_topk_numpy(np.stack([x[0] for x in per]), np.stack([x[1] for x in per]),
-                                         np.stack([x[2] for x in per]).astype(np.int64), k), floor)
-    (m0_, f0), (m1_, floor) = res[False], res[True]
-    assert floor is not None and (floor > 0).mean() > 0.5
-    for a, b in zip(m0_, m1_):
-        assert np.array_equal(a, b)
-    ms, md, msh, mn = m1_
-    base = np.array([b for b, _ in ranges], np.uint64)
-    bounds = np.array([b for b, _ in ranges] + [c.n_docs], np.uint32)
-    for i in range(nq):
-        m = int(mn[i])
-        rs, rd = ref.search_segments(terms[q_off[i]:q_off[i + 1]], k, bounds, mode=1)
-        assert m == len(rd)
-        gdoc = md[i, :m].astype(np.uint64) + base[msh[i, :m]]
-        assert np.array_equal(gdoc, rd.astype(np.uint64))
-        if m == k:
-            assert floor[i] <= rs[k - 1] * (1 + 1e-7), (i, floor[i], rs[k - 1])
-    for p in plans:
-        p.close()

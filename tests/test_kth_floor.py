@@ -149,23 +149,3 @@ def test_two_rank_ladder_exchange():
     for r in range(world):
         assert np.array_equal(res[r][0], exp)  # every rank holds every shard's ladder, in rank order
         assert np.array_equal(res[r][1], res[0][1])  # and computes the same floor
-
-
-def test_query_floor_rows_and_column_choice():
-    """shard.query_floor: per-query rows of the shards' query ladders, combined
-    like term ladders, read at the smallest K >= k (k past 1000: no floor)."""
-    from fugu_amd.shard import query_floor
-    rng = np.random.default_rng(9)
-    S, nq = 3, 50
-    lists = [[rng.gamma(2.0, 1.0, size=int(rng.integers(0, 700))).astype(np.float32) for _ in range(nq)]
-             for _ in range(S)]
-    lads = [np.stack([ladder_of(lists[s][q]) for q in range(nq)]) for s in range(S)]
-    for k, col in ((1, 0), (7, 1), (10, 1), (20, 2), (50, 3), (100, 3), (1000, 4)):
-        f = query_floor(lads, k)
-        assert f.shape == (nq,)
-        for q in range(nq):
-            allv = np.sort(np.concatenate([lists[s][q] for s in range(S)]))[::-1]
-            assert f[q] == brute_floor([lads[s][q] for s in range(S)])[col]
-            if k <= len(allv):
-                assert f[q] <= allv[k - 1]  # a lower bound of the k-th over all shards
-    assert query_floor(lads, 1024) is None

@@ -1,7 +1,6 @@
 """bench.py's C5 line alone (bench_c5): 100M docs as 8 global-statistics doc
 shards on one GPU; the multi-snapshot step, and every shard ALONE as one GPU of
-the 8-GPU split sees it (unseeded, with the namespace-wide per-term floors, and
-with the per-query floors of all shards' query ladders).
+the 8-GPU split sees it (unseeded, and with the namespace-wide per-term floors).
 
   python tools/c5_bench.py [--steps K]
 """
