@@ -2240,15 +2240,51 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // order gives the same hits), and it takes a fraction of a comparison sort's
   // host time on a 20K-item batch.
   auto single = [&](const W& x) { return q_m[x.q] == fg::qm_pack(1, 1, 0); };
+  // A/B (FUGU_XCD_PART=1): the sweep split into 8 query groups, one per XCD (the
+  // kernels hand XCD x the x-th eighth of the items), queries that probe the
+  // same list -- k_conj's second list, k_disj's densest clause -- in one group
+  // (groups balanced by items), so one XCD's L2 serves that list to all of them
+  const char* xp = getenv("FUGU_XCD_PART");
+  const bool xcd_part = xp && *xp == '1';
+  std::vector<uint8_t> q_grp;
+  auto groups = [&](const std::vector<W>& items, bool conj) {
+    q_grp.assign(nq, 0);
+    std::map<uint32_t, uint64_t> load;  // probed term -> items
+    auto probe_term = [&](uint32_t qv) {
+      const uint32_t* qt = q_terms.data() + (size_t)qv * fg::kMaxTerms;
+      const uint32_t mt = fg::qm_terms(q_m[qv]);
+      if (conj) return mt > 1 ? qt[1] : qt[0];
+      uint32_t best = qt[0];
+      const fg_index* sx = ixs[S > 1 ? qv / nq1 : 0];
+      for (uint32_t j = 1; j < mt - fg::qm_not(q_m[qv]); ++j)
+        if (sx->off[qt[j] + 1] - sx->off[qt[j]] > sx->off[best + 1] - sx->off[best]) best = qt[j];
+      return best;
+    };
+    for (const W& x : items) load[probe_term(x.q)]++;
+    std::vector<std::pair<uint64_t, uint32_t>> by;
+    for (auto& kv : load) by.emplace_back(kv.second, kv.first);
+    std::sort(by.begin(), by.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
+    uint64_t gl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    std::map<uint32_t, uint8_t> tg;
+    for (auto& [cnt, t] : by) {
+      const uint32_t g = (uint32_t)(std::min_element(gl, gl + 8) - gl);
+      gl[g] += cnt;
+      tg[t] = (uint8_t)g;
+    }
+    for (const W& x : items) q_grp[x.q] = tg[probe_term(x.q)];
+  };
   auto radix = [&](std::vector<W>& items, bool conj) {
     const size_t n = items.size();
     std::vector<uint64_t> a(n), bb(n);  // (sort key << 32) | item index
     // (items of queries probing the same list next to each other within each
     // 1/2048 of the sweep, so one XCD's L2 serves that list to all of them:
     // measured slower, profiles/r04/ab/ab_sweep_*.log)
+    if (xcd_part) groups(items, conj);
     for (size_t x = 0; x < n; ++x) {
       const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
-      const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | (uint32_t)(kk * 2147483647.0);
+      const uint32_t sw = xcd_part ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
+                                   : (uint32_t)(kk * 2147483647.0);
+      const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | sw;
       a[x] = ((uint64_t)rk << 32) | (uint64_t)x;
     }
     for (int sh = 32; sh < 64; sh += 11) {
