@@ -1,2 +1,2 @@
 set -o pipefail
-bash tools/gpu_r05e.sh && bash tools/gpu_r05b.sh
+bash tools/gpu_r05g.sh && bash tools/gpu_r05e.sh
