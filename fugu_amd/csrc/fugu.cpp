@@ -243,28 +243,28 @@ namespace {
 thread_local hipStream_t tl_build_stream = hipStreamPerThread;
 #define kBuildStream tl_build_stream
 
-// The latency path's small transfers through pinned host memory (a batch's
-// plan upload, its hits' download): a copy kernel on the search's own stream
-// when at most kKernelCopyMax bytes, so they do not wait behind a commit's bulk
-// transfers on the copy engines; hipMemcpyAsync above that, or with
-// FUGU_KCOPY=0 (A/B).  `host` is a pinned block of a PinnedPool (device-mapped).
-constexpr size_t kKernelCopyMax = 1u << 20;
-static hipError_t pinned_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+// The calling thread's high-priority stream on device `dev` (the search path's
+// own: its kernels are dispatched ahead of a commit's rescores and builds on the
+// same GPU), created on first use and kept for the thread's life;
+// FUGU_SEARCH_PRIO=0: the per-thread default stream (A/B)
+static hipStream_t search_stream(int dev) {
   static const bool on = [] {
-    const char* e = getenv("FUGU_KCOPY");
+    const char* e = getenv("FUGU_SEARCH_PRIO");
     return !(e && *e == '0');
   }();
-  if (!on || bytes > kKernelCopyMax || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15))
-    return hipMemcpyAsync(dst, src, bytes, kind, s);
-  // the host side's device address (the runtime's mapping of the pinned block);
-  // not mapped -> the copy engines after all
-  void* host = kind == hipMemcpyHostToDevice ? const_cast<void*>(src) : dst;
-  void* dmap = nullptr;
-  if (hipHostGetDevicePointer(&dmap, host, 0) != hipSuccess || !dmap) {
+  if (!on) return hipStreamPerThread;
+  thread_local std::map<int, hipStream_t> mine;
+  auto it = mine.find(dev);
+  if (it != mine.end()) return it->second;
+  int least = 0, greatest = 0;
+  hipStream_t s = nullptr;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+      hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) != hipSuccess) {
     (void)hipGetLastError();
-    return hipMemcpyAsync(dst, src, bytes, kind, s);
+    s = hipStreamPerThread;
   }
-  return kind == hipMemcpyHostToDevice ? fg::launch_copy(dst, dmap, bytes, s) : fg::launch_copy(dmap, src, bytes, s);
+  mine[dev] = s;
+  return s;
 }
 
 // low-priority streams of a device for background rescoring, created once
@@ -2240,25 +2240,23 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // order gives the same hits), and it takes a fraction of a comparison sort's
   // host time on a 20K-item batch.
   auto single = [&](const W& x) { return q_m[x.q] == fg::qm_pack(1, 1, 0); };
-  // A/B (FUGU_XCD_PART=1): the sweep split into 8 query groups, one per XCD (the
-  // kernels hand XCD x the x-th eighth of the items), queries that probe the
-  // same list -- k_conj's second list, k_disj's densest clause -- in one group
-  // (groups balanced by items), so one XCD's L2 serves that list to all of them
+  // k_conj: the sweep split into 8 query groups, one per XCD (the kernel hands
+  // XCD x the x-th eighth of its items), the queries whose second list (the
+  // first one probed) is the same term in one group, groups balanced by items:
+  // headline k_conj 1.037 -> 1.001 ms, identical hits (profiles/r05/ab/
+  // ab_xcd_part.json; L2 hit rate 0.32 -> 0.23, DRAM 4.09 -> 4.57 GB: each XCD
+  // walks the whole doc range for fewer queries).  The same split of k_disj by
+  // densest clause: OR top-20 2.78 -> 3.30 ms, top-1000 5.26 -> 6.86 ms -- its
+  // sweep stays doc-ordered.  FUGU_XCD_PART=0: the doc sweep for k_conj (A/B).
   const char* xp = getenv("FUGU_XCD_PART");
-  const bool xcd_part = xp && *xp == '1';
+  const bool xcd_part = !(xp && *xp == '0');
   std::vector<uint8_t> q_grp;
-  auto groups = [&](const std::vector<W>& items, bool conj) {
+  auto groups = [&](const std::vector<W>& items) {
     q_grp.assign(nq, 0);
     std::map<uint32_t, uint64_t> load;  // probed term -> items
     auto probe_term = [&](uint32_t qv) {
       const uint32_t* qt = q_terms.data() + (size_t)qv * fg::kMaxTerms;
-      const uint32_t mt = fg::qm_terms(q_m[qv]);
-      if (conj) return mt > 1 ? qt[1] : qt[0];
-      uint32_t best = qt[0];
-      const fg_index* sx = ixs[S > 1 ? qv / nq1 : 0];
-      for (uint32_t j = 1; j < mt - fg::qm_not(q_m[qv]); ++j)
-        if (sx->off[qt[j] + 1] - sx->off[qt[j]] > sx->off[best + 1] - sx->off[best]) best = qt[j];
-      return best;
+      return fg::qm_terms(q_m[qv]) > 1 ? qt[1] : qt[0];
     };
     for (const W& x : items) load[probe_term(x.q)]++;
     std::vector<std::pair<uint64_t, uint32_t>> by;
@@ -2279,11 +2277,12 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     // (items of queries probing the same list next to each other within each
     // 1/2048 of the sweep, so one XCD's L2 serves that list to all of them:
     // measured slower, profiles/r04/ab/ab_sweep_*.log)
-    if (xcd_part) groups(items, conj);
+    const bool part = conj && xcd_part;
+    if (part) groups(items);
     for (size_t x = 0; x < n; ++x) {
       const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
-      const uint32_t sw = xcd_part ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
-                                   : (uint32_t)(kk * 2147483647.0);
+      const uint32_t sw = part ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
+                               : (uint32_t)(kk * 2147483647.0);
       const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | sw;
       a[x] = ((uint64_t)rk << 32) | (uint64_t)x;
     }
@@ -2427,8 +2426,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // on the planning thread's own stream (or the caller's `up`): a plan built
   // while another thread's batch runs does not serialise against it through the
   // legacy null stream
-  if (pin.p) HIPCHK(pinned_copy(base, staging, s_up, hipMemcpyHostToDevice, up));
-  else HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, up));
+  HIPCHK(hipMemcpyAsync(base, staging, s_up, hipMemcpyHostToDevice, up));
   p->up_stream = up;
   p->zeroed = s_up > s_in;
   if (sync || !pin.p) {
@@ -2535,7 +2533,7 @@ int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* o
   if (span <= (4ull << 20)) {
     PinnedLease pin(p->ix->pinned, span);
     if (pin.p) {
-      HIPCHK(pinned_copy(pin.p, first, span, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(pin.p, first, span, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       const char* h = static_cast<const char*>(pin.p);
       if (out_score) std::memcpy(out_score, h, 4 * nk);
@@ -2908,7 +2906,7 @@ static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32
   if (span <= (4ull << 20)) {
     PinnedLease pin(shards[0]->pinned, span);
     if (pin.p) {
-      HIPCHK(pinned_copy(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
+      HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
       HIPCHK(hipStreamSynchronize(hipStreamPerThread));
       const char* h = static_cast<const char*>(pin.p);
       std::memcpy(out_score, h, 4 * nk);
@@ -2998,13 +2996,17 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     }
   }
   const size_t ng = groups.size();
+  // every shard on the first device: the calling thread's high-priority stream
+  // there (FUGU_SEARCH_PRIO=0: its per-thread stream), so a search's kernels are
+  // dispatched ahead of a commit's rescores and builds; else per-thread streams
+  const hipStream_t hs = ng == 1 && gdev[0] == dev0 ? search_stream(dev0) : hipStreamPerThread;
   bool merged = false;  // the plan's merged select already wrote ms / md / msh / mn
   std::vector<std::unique_ptr<fg_plan>> plans(ng);
   std::vector<hipEvent_t> evs(ng, nullptr);
   // teardown (also on error returns): every device's stream drained, then the
   // events, the plans and the buffers
   struct Back {
-    const std::vector<int>& dv; int d0; fg_index* ix0; void* p; size_t n; std::vector<hipEvent_t>& ev;
+    const std::vector<int>& dv; int d0; fg_index* ix0; void* p; size_t n; std::vector<hipEvent_t>& ev; hipStream_t s0;
     ~Back() {
       for (size_t g = 0; g < dv.size(); ++g) {
         (void)hipSetDevice(dv[g]);
@@ -3012,10 +3014,10 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
         if (ev[g]) (void)hipEventDestroy(ev[g]);
       }
       (void)hipSetDevice(d0);
-      (void)hipStreamSynchronize(hipStreamPerThread);
+      (void)hipStreamSynchronize(s0);
       ix0->pool.put(p, n);
     }
-  } back{gdev, dev0, shards[0], base, got, evs};
+  } back{gdev, dev0, shards[0], base, got, evs, hs};
   static const bool trace_env = getenv("FUGU_SHARD_TRACE") != nullptr;
   fgh::SearchTrace& st = fgh::search_trace();
   const bool trace = trace_env || st.enabled();
@@ -3031,7 +3033,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     // the upload is queued on this thread's stream of the device, ahead of the
     // execute on the same stream: no host round trip
     const double t_p = trace ? now() : 0.0;
-    if (int rc = plan_create_multi(ixs.data(), S, q, k, &p, false, hipStreamPerThread)) {
+    if (int rc = plan_create_multi(ixs.data(), S, q, k, &p, false, hs)) {
       if (n_shards == 1) return rc;
       const std::string e = fg_last_error();
       return fail(rc, "device %d: %s", gdev[g], e.c_str());
@@ -3048,7 +3050,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 256u;
     }();
     if (ng == 1 && gdev[0] == dev0 && S > 1 && p->d.seg_base && nq >= merged_min) {
-      if (int rc = execute_impl(p, hipStreamPerThread, ms, md, mn, msh)) return rc;
+      if (int rc = execute_impl(p, hs, ms, md, mn, msh)) return rc;
       merged = true;
       break;
     }
@@ -3056,37 +3058,37 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     // consecutive and on dev0 ([S][nq][k] is the gathered layout)
     const bool direct = gdev[g] == dev0 && gi.back() - gi.front() + 1 == S;
     const size_t s0 = gi.front();
-    if (int rc = direct ? fg_plan_execute(p, hipStreamPerThread, gs + s0 * nk, gd + s0 * nk, gn + s0 * nq)
-                        : fg_plan_execute(p, hipStreamPerThread, nullptr, nullptr, nullptr))
+    if (int rc = direct ? fg_plan_execute(p, hs, gs + s0 * nk, gd + s0 * nk, gn + s0 * nq)
+                        : fg_plan_execute(p, hs, nullptr, nullptr, nullptr))
       return rc;
     if (!direct) {
       for (uint32_t j = 0; j < S; ++j) {
         const size_t s = gi[j];
         if (gdev[g] == dev0) {
-          HIPCHK(hipMemcpyAsync(gs + s * nk, p->own_score + j * nk, 4 * nk, hipMemcpyDeviceToDevice, hipStreamPerThread));
-          HIPCHK(hipMemcpyAsync(gd + s * nk, p->own_doc + j * nk, 4 * nk, hipMemcpyDeviceToDevice, hipStreamPerThread));
+          HIPCHK(hipMemcpyAsync(gs + s * nk, p->own_score + j * nk, 4 * nk, hipMemcpyDeviceToDevice, hs));
+          HIPCHK(hipMemcpyAsync(gd + s * nk, p->own_doc + j * nk, 4 * nk, hipMemcpyDeviceToDevice, hs));
           HIPCHK(hipMemcpyAsync(gn + s * nq, p->own_n + (size_t)j * nq, 4ull * nq, hipMemcpyDeviceToDevice,
-                                hipStreamPerThread));
+                                hs));
         } else {
-          HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score + j * nk, gdev[g], 4 * nk, hipStreamPerThread));
-          HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc + j * nk, gdev[g], 4 * nk, hipStreamPerThread));
+          HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score + j * nk, gdev[g], 4 * nk, hs));
+          HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc + j * nk, gdev[g], 4 * nk, hs));
           HIPCHK(hipMemcpyPeerAsync(gn + s * nq, dev0, p->own_n + (size_t)j * nq, gdev[g], 4ull * nq,
-                                    hipStreamPerThread));
+                                    hs));
         }
       }
     }
     if (gdev[g] != dev0) {
       HIPCHK(hipEventCreateWithFlags(&evs[g], hipEventDisableTiming));
-      HIPCHK(hipEventRecord(evs[g], hipStreamPerThread));
+      HIPCHK(hipEventRecord(evs[g], hs));
     }
   }
   const double t_run = trace ? now() : 0.0;
   HIPCHK(hipSetDevice(dev0));
   for (hipEvent_t e : evs)
-    if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
-  if (!merged) HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
+    if (e) HIPCHK(hipStreamWaitEvent(hs, e, 0));
+  if (!merged) HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hs));
   if (trace_env) {
-    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+    HIPCHK(hipStreamSynchronize(hs));
     fprintf(stderr, "[fg_search_sharded] nq %u shards %u devices %zu merged %d: plan %.3f launch %.3f kernels+merge %.3f ms\n",
             nq, n_shards, ng, (int)merged, t_plan, t_run - t_0 - t_plan, now() - t_run);
   }
@@ -3105,8 +3107,8 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   if (span <= (4ull << 20)) {
     PinnedLease pin(shards[0]->pinned, span);
     if (pin.p) {
-      HIPCHK(pinned_copy(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
-      HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+      HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hs));
+      HIPCHK(hipStreamSynchronize(hs));
       const char* h = static_cast<const char*>(pin.p);
       std::memcpy(out_score, h, 4 * nk);
       std::memcpy(out_doc, h + o_k, 4 * nk);
@@ -3115,11 +3117,11 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       return FG_OK;
     }
   }
-  HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
-  HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
-  if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
-  HIPCHK(hipMemcpyAsync(out_n, mn, 4ull * nq, hipMemcpyDeviceToHost, hipStreamPerThread));
-  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
+  HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hs));
+  HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hs));
+  if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hs));
+  HIPCHK(hipMemcpyAsync(out_n, mn, 4ull * nq, hipMemcpyDeviceToHost, hs));
+  HIPCHK(hipStreamSynchronize(hs));
   return FG_OK;
 }
 

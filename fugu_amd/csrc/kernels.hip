@@ -1995,27 +1995,6 @@ hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   return hipGetLastError();
 }
 
-// A small copy between pinned host memory and the device on a COMPUTE queue:
-// the latency path's plan upload and hit download (tens of KB) then never
-// queue behind bulk transfers on the shared copy engines (a commit's uploads
-// and read-backs, hundreds of MB).  16-B vectors, the tail byte by byte.
-__global__ __launch_bounds__(kThreads) void k_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                   size_t n) {
-  const size_t n16 = n / 16, stride = (size_t)gridDim.x * kThreads;
-  const uint4* __restrict__ s4 = reinterpret_cast<const uint4*>(src);
-  uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dst);
-  for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n16; i += stride) d4[i] = s4[i];
-  if (blockIdx.x == 0)
-    for (size_t i = n16 * 16 + threadIdx.x; i < n; i += kThreads) dst[i] = src[i];
-}
-
-hipError_t launch_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  if (!bytes) return hipSuccess;
-  const uint32_t blocks = (uint32_t)std::min<size_t>(64, (bytes / 16 + kThreads - 1) / kThreads + 1);
-  k_copy<<<blocks, kThreads, 0, s>>>(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), bytes);
-  return hipGetLastError();
-}
-
 hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   if (pl.f.n_chunks == 0) return hipSuccess;
   if (pl.segs) k_fmask<true><<<pl.f.n_chunks, kThreads, 0, s>>>(ix, pl);
