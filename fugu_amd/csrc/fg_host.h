@@ -395,7 +395,8 @@ struct fg_index {
   std::shared_ptr<DevAllocs> smem;
   std::shared_ptr<fgh::ScorePool> spool;
   uint64_t struct_bytes = 0;
-  const uint32_t* d_tfp = nullptr;
+  const uint32_t* d_tfp = nullptr;   // tf_text | tf_name << 16 per posting, or nullptr ...
+  const uint16_t* d_tf16 = nullptr;  // ... tf_text alone when the snapshot has no `name` postings
   const uint8_t* d_fn_text = nullptr;
   const uint8_t* d_fn_name = nullptr;
   // packed chunk tables of k_score / k_bucket (fg_internal.h ScoreJob::sc_* / bk_*)

@@ -332,7 +332,8 @@ constexpr uint32_t kBucketChunk = 2048;  // buckets per k_bucket workgroup
 static_assert(kScoreChunk == kChunk, "DevIndex::cmax: a k_score chunk is a k_conj lead chunk");
 struct ScoreJob {
   const uint32_t* doc;
-  const uint32_t* tfp;        // [P] tf_text | tf_name << 16
+  const uint32_t* tfp;        // [P] tf_text | tf_name << 16, or nullptr ...
+  const uint16_t* tf16;       // [P] ... tf_text (no `name` postings)
   const uint8_t* fn_text;     // [N] fieldnorm ids
   const uint8_t* fn_name;     // [N] or nullptr
   const uint64_t* off;        // [V+1]

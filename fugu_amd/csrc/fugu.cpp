@@ -527,6 +527,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   fg::ScoreJob j{};
   j.doc = ix->d.doc;
   j.tfp = ix->d_tfp;
+  j.tf16 = ix->d_tf16;
   j.fn_text = ix->d_fn_text;
   j.fn_name = ix->has_name ? ix->d_fn_name : nullptr;
   j.off = ix->d.off;
@@ -859,15 +860,28 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   DevAllocs& sm = *ix->smem;
   uint64_t& bytes = ix->struct_bytes;
   int rc;
-  uint32_t *d_doc, *d_tfp, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc, *d_tterm;
+  uint32_t *d_doc, *d_tfp = nullptr, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc, *d_tterm;
+  uint16_t* d_tf16 = nullptr;
   uint8_t *d_fnt, *d_fnn = nullptr;
   uint64_t *d_off, *d_foff;
   uint32_t *d_sctf, *d_sctl, *d_bktf, *d_bktl, *d_bke0, *d_bke1, *d_kt, *d_ktt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs;
   uint64_t *d_sce0, *d_sce1;
+  // without `name` postings every tf_name is 0: the term frequencies (k_score's
+  // input, read at every rescore) as u16, 2 B per posting instead of 4 (1 GiB
+  // of a 10M-doc namespace)
+  std::vector<uint16_t> tf16;
+  if (!hp.has_name) {
+    tf16.resize(hp.tf.size());
+    const size_t np = hp.tf.size(), piece = (np + 1023) / 1024;  // > 2^32 postings: 64-bit pieces
+    parallel_dynamic(1024, hw_threads(0), 8, [&](int, uint32_t b, uint32_t e) {
+      for (size_t i = (size_t)b * piece; i < std::min(np, (size_t)e * piece); ++i) tf16[i] = (uint16_t)hp.tf[i];
+    });
+  }
   {
     UploadBatch ub;
     ub.add(hp.doc.data(), hp.doc.size(), &d_doc);
-    ub.add(hp.tf.data(), hp.tf.size(), &d_tfp);
+    if (hp.has_name) ub.add(hp.tf.data(), hp.tf.size(), &d_tfp);
+    else ub.add(tf16.data(), tf16.size(), &d_tf16);
     ub.add(hp.fn_text.data(), hp.fn_text.size(), &d_fnt);
     if (hp.has_name) ub.add(hp.fn_name.data(), hp.fn_name.size(), &d_fnn);
     ub.add(hp.off.data(), hp.off.size(), &d_off);
@@ -975,6 +989,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->tmeta = tmeta;
   g_bt.mark("rank words");
   ix->d_tfp = d_tfp;
+  ix->d_tf16 = d_tf16;
   ix->d_fn_text = d_fnt;
   ix->d_fn_name = d_fnn;
   ix->d_sc_tf = d_sctf;
@@ -1516,6 +1531,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->ffirst = base->ffirst;
   ix->flast = base->flast;
   ix->d_tfp = base->d_tfp;
+  ix->d_tf16 = base->d_tf16;
   ix->d_fn_text = base->d_fn_text;
   ix->d_fn_name = base->d_fn_name;
   ix->d_sc_tf = base->d_sc_tf;
@@ -2254,9 +2270,17 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   auto groups = [&](const std::vector<W>& items) {
     q_grp.assign(nq, 0);
     std::map<uint32_t, uint64_t> load;  // probed term -> items
+    // FUGU_XCD_KEY (A/B): 1 the second list (default), 0 the lead, 2 the last
+    // list, q the query itself (groups by items alone)
+    const char* xk = getenv("FUGU_XCD_KEY");
+    const char key = xk && *xk ? *xk : '1';
     auto probe_term = [&](uint32_t qv) {
       const uint32_t* qt = q_terms.data() + (size_t)qv * fg::kMaxTerms;
-      return fg::qm_terms(q_m[qv]) > 1 ? qt[1] : qt[0];
+      const uint32_t mt = fg::qm_terms(q_m[qv]);
+      if (key == 'q') return 0x80000000u | qv;
+      if (key == '0' || mt == 1) return qt[0];
+      if (key == '2') return qt[mt - 1];
+      return qt[1];
     };
     for (const W& x : items) load[probe_term(x.q)]++;
     std::vector<std::pair<uint64_t, uint32_t>> by;

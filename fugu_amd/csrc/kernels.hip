@@ -2150,7 +2150,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
   for (uint32_t r = 0; r < R; ++r) {
     const uint64_t p = e0 + r * kThreads + threadIdx.x;
     d[r] = p < e1 ? j.doc[p] : 0xFFFFFFFFu;
-    tfp[r] = p < e1 ? j.tfp[p] : 0u;
+    tfp[r] = p < e1 ? (j.tf16 ? (uint32_t)j.tf16[p] : j.tfp[p]) : 0u;
   }
   uint32_t fnt[R], fnn[R];
 #pragma unroll
