@@ -323,7 +323,7 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     # reader searches while the writer gathers, builds and swaps
     import threading
     stop = threading.Event()
-    lat_r, err_r, ph_r = [], [], []
+    lat_r, err_r, ph_r, t_r = [], [], [], []
     fdb.search_trace(1)
 
     def reader():
@@ -331,9 +331,11 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
         try:
             fdb.search_trace()
             while not stop.is_set():
+                t0 = time.monotonic()  # the steady clock of the native traces' @ stamps
                 t1 = time.perf_counter()
                 d.search("api", qs[i % nq], 0, 20)
                 lat_r.append(time.perf_counter() - t1)
+                t_r.append(t0)
                 ph_r.append(fdb.search_trace())  # this search's phases (only this thread searches)
                 i += 1
         except Exception as e:  # noqa: BLE001
@@ -360,6 +362,9 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     slow_ph = {k: round(float(np.mean([p[k] for p in slow])), 4) for k in fdb.SEARCH_PHASES if k != "json_fetch"}
     d.merge_wait("api")
     t_done = time.perf_counter() - t_all
+    if os.environ.get("FUGU_STALL_TRACE"):  # tools/stall_trace.py: every reader search (start ms, latency ms)
+        with open(os.environ["FUGU_STALL_TRACE"], "w") as f:
+            json.dump([[round(t * 1e3, 3), round(l * 1e3, 4)] for t, l in zip(t_r, lat_r)], f)
     out["during_commits"] = {"p50_ms": pct(lat_r, 50), "p90_ms": pct(lat_r, 90), "p99_ms": pct(lat_r, 99),
                              "max_ms": round(max(lat_r) * 1e3, 3), "searches": len(lat_r),
                              "p99_over_idle_p99": round(pct(lat_r, 99) / max(out["p99_ms"], 1e-9), 3),

@@ -82,8 +82,10 @@ struct DevAllocs {
   int dev = 0;
   ~DevAllocs() {
     if (ptrs.empty()) return;
+    const uint64_t t0 = commit_trace_on() ? now_ns() : 0;
     (void)hipSetDevice(dev);
     for (void* p : ptrs) (void)hipFree(p);
+    if (t0) trace_span("free", "snapshot arrays (hipFree)", t0);
   }
 };
 
@@ -148,8 +150,10 @@ struct ScorePool : DevCache {
   // (the caller runs where waiting for the device is harmless: a snapshot's
   // last release happens on the db's reaper thread, or a build / test thread)
   void put(void* p, size_t bytes) {
+    const uint64_t t0 = commit_trace_on() ? now_ns() : 0;
     (void)hipSetDevice(dev);
     (void)hipDeviceSynchronize();
+    if (t0) trace_span("free", "scoring block: device drain", t0);
     {
       std::lock_guard<std::mutex> l(mu);
       if (free_blocks.size() < kKeep) {
@@ -157,7 +161,9 @@ struct ScorePool : DevCache {
         return;
       }
     }
+    const uint64_t t1 = commit_trace_on() ? now_ns() : 0;
     (void)hipFree(p);
+    if (t1) trace_span("free", "scoring block (hipFree)", t1);
   }
   void release_all() {
     std::lock_guard<std::mutex> l(mu);
@@ -362,7 +368,8 @@ struct fg_index {
   uint32_t n_docs = 0, n_terms = 0;
   bool has_name = false;
   uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0, tile_entries = 0;
-  uint32_t n_dense = 0, n_rank = 0;
+  uint32_t n_dense = 0, n_rank = 0;  // n_rank: rank-kind slots, plain (d.n_prank) and sparse
+  uint64_t n_srank_words = 0;        // sparse rank words (d.srank_w)
   // ---- statistics and scoring (this snapshot's own)
   uint64_t tot[2] = {0, 0};
   uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)

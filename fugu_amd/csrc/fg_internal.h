@@ -46,6 +46,12 @@ constexpr uint64_t kRankBudget = (uint64_t)FG_RANK_GIB << 30;    // ... densest 
 #define FG_RANK_FACTOR 4.0  // tools/ab_rank_budget.py sweep (profiles/r03/ab_rank_sweep.log); env FUGU_RANK_FACTOR
 #endif
 constexpr double kRankFactor = FG_RANK_FACTOR;  // ... and within this many times the snapshot's posting bytes
+#ifndef FG_RANK_PLAIN_DIV
+#define FG_RANK_PLAIN_DIV 32  // env FUGU_RANK_PLAIN_DIV; profiles/r05/ab/ab_rank_layout.log
+#endif
+// ... a term in >= 1/kRankPlainDiv of the docs gets plain rank words, a sparser
+// one sparse rank words (DevIndex::srank), unless plain ones cost it less
+constexpr uint32_t kRankPlainDiv = FG_RANK_PLAIN_DIV;
 constexpr uint32_t kMaxDense = 32767;     // slots per kind (tmeta bits 16-30)
 constexpr uint32_t kRankChunkWords = 2048;  // k_rank: words (65536 docs) per workgroup
 #ifndef FG_DISJ_GPQ
@@ -156,6 +162,30 @@ __host__ __device__ inline uint32_t rank_pos(uint64_t x, uint32_t d) {
 #endif
 }
 
+// Sparse rank words (DevIndex::srank, rank-kind slots above n_prank): per
+// 1024-doc block one u64, the low half a bit per 32-doc word of the block that
+// holds any of the term's docs, the high half the index in srank_w of the
+// block's first such word; srank_w holds only those words, in the rank-word
+// format above, after a zero word at index 0 (the word of every doc no sparse
+// term holds: a probe loads it unconditionally, with no predicate kept live
+// across the load).  A probe is the block's 8-B load, then the word's.  A term
+// in 1/2000 of the docs takes ~1/25 of its plain rank words' bytes.
+__host__ __device__ inline uint32_t srank_block(uint32_t d) { return d >> 10; }
+// the srank_w index of doc d's word from its block entry (0: the zero word)
+__host__ __device__ inline uint32_t srank_index(uint64_t e, uint32_t d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(d));  // as rank_pos: nothing derived from d stays live across the word's load
+#endif
+  const uint32_t w = (d >> 5) & 31u;
+  const uint32_t below = (uint32_t)e & ((1u << w) - 1u);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t i = (uint32_t)(e >> 32) + (uint32_t)__popc(below);
+#else
+  const uint32_t i = (uint32_t)(e >> 32) + (uint32_t)__builtin_popcount(below);
+#endif
+  return ((e >> w) & 1ull) ? i : 0u;
+}
+
 // u8 bounds of a score range [0, M] (k_disj's sub-tile maxima): a score s as
 // the least q with q8_bound(q, M) >= s; q8_bound(255, M) = M covers every
 // rounding.  The kernels compute q8_bound with the same f32 operations
@@ -172,7 +202,8 @@ __host__ __device__ inline uint32_t quant8(float s, float M) {
 constexpr uint32_t kSubShift = 9;  // 512-doc blocks: 8 per k_disj tile
 
 // tmeta of a term: bits 0-7 = B_t (bucket shift), 8-15 = S_t (search steps),
-// 16-30 = dense slot + 1 (0: none), bit 31 = the slot's kind (1: rank words, 0: f32 table)
+// 16-30 = dense slot + 1 (0: none), bit 31 = the slot's kind (1: rank words, 0: f32 table);
+// rank-kind slots 1..n_prank are plain rank words, the ones above sparse (srank)
 __host__ __device__ inline uint32_t meta_slot(uint32_t meta) { return (meta >> 16) & 0x7FFFu; }
 __host__ __device__ inline bool meta_rank(uint32_t meta) { return (meta >> 31) != 0; }
 
@@ -204,7 +235,9 @@ struct DevIndex {
   const uint32_t* dir_off;   // [V] first directory entry of each term
   const uint32_t* tmeta;     // [V] meta_slot / meta_rank above
   const float* dense;        // [n_dense * N] doc-indexed term score (-1 = absent), f32-kind slots
-  const uint64_t* rank;      // [n_rank * rank_words] rank words, rank-kind slots
+  const uint64_t* rank;      // [n_prank * rank_words] rank words, rank-kind slots 1..n_prank
+  const uint64_t* srank;     // [n_srank * srank_blocks] sparse rank block entries, rank-kind slots above
+  const uint64_t* srank_w;   // sparse rank words (srank_index)
   const float* tmaxs;        // [V] largest posting score of each term (MaxScore bound)
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
@@ -224,7 +257,9 @@ struct DevIndex {
   uint32_t n_terms;
   uint32_t has_name;
   uint32_t n_fterms;
-  uint32_t rank_words;       // words per rank-kind term: ceil(N / 32)
+  uint32_t rank_words;       // words per plain rank-kind term: ceil(N / 32)
+  uint32_t n_prank;          // plain rank-kind slots
+  uint32_t srank_blocks;     // block entries per sparse rank-kind term: ceil(N / 1024)
 };
 
 // Facet filters of a planned batch (DevPlan).  Every distinct clause list

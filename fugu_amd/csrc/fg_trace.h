@@ -4,6 +4,8 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 
 namespace fgh {
 
@@ -30,6 +32,17 @@ SearchTrace& search_trace();
 inline uint64_t now_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// FUGU_COMMIT_TRACE: device memory releases (the reaper's frees) on stderr as
+// "[fg free] <what> <ms> ms @<end on the steady clock, ms>", like the commit phases
+inline bool commit_trace_on() {
+  static const bool on = getenv("FUGU_COMMIT_TRACE") != nullptr;
+  return on;
+}
+inline void trace_span(const char* tag, const char* what, uint64_t t0_ns) {
+  const uint64_t t1 = now_ns();
+  fprintf(stderr, "[fg %s] %-28s %9.2f ms @%.3f\n", tag, what, (double)(t1 - t0_ns) * 1e-6, (double)t1 * 1e-6);
 }
 
 }  // namespace fgh

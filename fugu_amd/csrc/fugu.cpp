@@ -124,7 +124,10 @@ struct BuildTrace {
   void mark(const char* what) {
     if (!on) return;
     const auto n = std::chrono::steady_clock::now();
-    fprintf(stderr, "[fg build] %-24s %9.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    // @: the phase's end on the steady clock (ms; Python's time.monotonic), to line
+    // phases up with other threads' events (tools/stall_trace.py)
+    fprintf(stderr, "[fg build] %-24s %9.1f ms @%.3f\n", what, std::chrono::duration<double, std::milli>(n - t).count(),
+            std::chrono::duration<double, std::milli>(n.time_since_epoch()).count());
     t = n;
   }
 };
@@ -192,7 +195,11 @@ void drop_all_cached() {
   (void)hipSetDevice(dev);
 }
 hipError_t dev_malloc(void** p, size_t bytes) {
-  if (hipMalloc(p, bytes) == hipSuccess) return hipSuccess;
+  const uint64_t t0 = commit_trace_on() ? now_ns() : 0;
+  if (hipMalloc(p, bytes) == hipSuccess) {
+    if (t0 && now_ns() - t0 > 200000) trace_span("alloc", "hipMalloc (> 0.2 ms)", t0);
+    return hipSuccess;
+  }
   (void)hipGetLastError();
   drop_all_cached();
   const hipError_t e = hipMalloc(p, bytes);
@@ -913,24 +920,49 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   std::vector<uint32_t>().swap(dir);
   std::vector<uint32_t>().swap(tdir);
   g_bt.mark("upload");
-  // rank words for the densest terms (fg_internal.h DevIndex): df >= N /
-  // kRankDiv, densest first (ties by term id), within a budget of the
-  // snapshot's own: FUGU_RANK_FACTOR (default kRankFactor) times its postings'
-  // bytes (doc id + tf + score, 12 B each), at most FUGU_RANK_GIB -- so a
-  // namespace's share depends on its size, not on how many namespaces were
-  // built on the device before it.  A quarter of the free memory caps it only
-  // when HBM is short, and a failed allocation is retried with half the terms
-  // (down to none), so a build never fails for want of them.  They hang on doc
-  // ids only, so rescored snapshots share them.
+  // rank words (fg_internal.h DevIndex) for the terms with df >= N / kRankDiv,
+  // densest first (ties by term id), within a budget of the snapshot's own:
+  // FUGU_RANK_FACTOR (default kRankFactor) times its postings' bytes (doc id +
+  // tf + score, 12 B each), at most FUGU_RANK_GIB -- so a namespace's share
+  // depends on its size, not on how many namespaces were built on the device
+  // before it.  A term with df >= N / kRankPlainDiv (FUGU_RANK_PLAIN_DIV) gets
+  // plain rank words (8 B per 32 docs), a sparser one sparse rank words (8 B per
+  // 1024-doc block + 8 B per word holding any of its docs) unless plain ones
+  // cost it less (small snapshots).  A quarter of the free memory caps them
+  // only when HBM is short, and a failed allocation is retried with half the
+  // terms (down to none), so a build never fails for want of them.  They hang
+  // on doc ids only, so rescored snapshots share them.
   std::vector<uint32_t> by_df;
   for (uint32_t t = 0; t < V; ++t)
     if (hp.off[t + 1] > hp.off[t] && (hp.off[t + 1] - hp.off[t]) * fg::kRankDiv >= N) by_df.push_back(t);
   std::stable_sort(by_df.begin(), by_df.end(), [&](uint32_t a, uint32_t b) {
     return hp.off[a + 1] - hp.off[a] > hp.off[b + 1] - hp.off[b];
   });
-  const uint32_t rank_words = (uint32_t)((N + 31) / 32);
-  std::vector<uint32_t> rank_terms;
+  const uint32_t rank_words = (uint32_t)((N + 31) / 32), sblocks = (N + 1023) / 1024;
+  const uint32_t pdiv = [] {
+    const char* e = getenv("FUGU_RANK_PLAIN_DIV");
+    return e && *e ? (uint32_t)std::max(1l, atol(e)) : fg::kRankPlainDiv;
+  }();
+  auto plain_df = [&](uint32_t t) { return (hp.off[t + 1] - hp.off[t]) * pdiv >= N; };
+  // the words of each sparse candidate that hold any of its docs
+  std::vector<uint32_t> nwords(by_df.size(), 0);
+  parallel_dynamic((uint32_t)by_df.size(), hw_threads(0), 16, [&](int, uint32_t b, uint32_t e) {
+    for (uint32_t i = b; i < e; ++i) {
+      const uint32_t t = by_df[i];
+      if (plain_df(t)) continue;
+      uint32_t n = 0, last = 0xFFFFFFFFu;
+      for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) {
+        const uint32_t w = hp.doc[p] >> 5;
+        n += w != last;
+        last = w;
+      }
+      nwords[i] = n;
+    }
+  });
+  std::vector<uint32_t> rank_terms, sparse_terms, sparse_nw;
   uint64_t* d_rank = nullptr;
+  uint64_t* d_srank = nullptr;
+  uint64_t n_swords = 0;
   {
     const char* v = getenv("FUGU_RANK_GIB");
     const uint64_t cap = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kRankBudget;
@@ -944,10 +976,22 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     // FUGU_DENSE_GIB they take f32 score tables: one gather per probe)
     const char* sk = getenv("FUGU_RANK_SKIP_TOP");
     size_t skip = sk && *sk ? (size_t)atol(sk) : 0;
-    for (uint32_t t : by_df) {
+    uint64_t used = 0;
+    for (size_t i = 0; i < by_df.size(); ++i) {
       if (skip) { --skip; continue; }
-      if ((rank_terms.size() + 1) * rank_words * 8ull > brk || rank_terms.size() >= fg::kMaxDense) break;
-      rank_terms.push_back(t);
+      const uint64_t cp = rank_words * 8ull, cs = (sblocks + (uint64_t)nwords[i]) * 8ull;
+      const bool plain = plain_df(by_df[i]) || cp <= cs;
+      const uint64_t c = plain ? cp : cs;
+      if (used + c > brk || rank_terms.size() + sparse_terms.size() >= fg::kMaxDense) break;
+      if (!plain && n_swords + nwords[i] >= 0xFFFFFFFFull) break;  // srank_w indices are u32
+      used += c;
+      if (plain) {
+        rank_terms.push_back(by_df[i]);
+      } else {
+        sparse_terms.push_back(by_df[i]);
+        sparse_nw.push_back(nwords[i]);
+        n_swords += nwords[i];
+      }
     }
     while (!rank_terms.empty()) {
       void* q = nullptr;
@@ -960,6 +1004,56 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       (void)hipGetLastError();
       rank_terms.resize(rank_terms.size() / 2);
     }
+    while (!sparse_terms.empty()) {
+      const uint64_t sb = (sblocks * (uint64_t)sparse_terms.size() + 1 + n_swords) * 8ull;
+      void* q = nullptr;
+      if (fgh::dev_malloc(&q, sb) == hipSuccess) {
+        sm.ptrs.push_back(q);
+        bytes += sb;
+        d_srank = static_cast<uint64_t*>(q);
+        break;
+      }
+      (void)hipGetLastError();
+      sparse_terms.resize(sparse_terms.size() / 2);
+      sparse_nw.resize(sparse_terms.size());
+      n_swords = 0;
+      for (uint32_t n : sparse_nw) n_swords += n;
+    }
+  }
+  if (!sparse_terms.empty()) {
+    // built on the host from the postings: per term its block entries, then
+    // the zero word and all terms' words (term by term), one upload
+    const uint32_t ns = (uint32_t)sparse_terms.size();
+    const uint32_t first_slot = (uint32_t)rank_terms.size() + 1;
+    std::vector<uint64_t> wbase(ns + 1, 1);
+    for (uint32_t s2 = 0; s2 < ns; ++s2) wbase[s2 + 1] = wbase[s2] + sparse_nw[s2];
+    std::vector<uint64_t> hs(sblocks * (uint64_t)ns + 1 + n_swords);
+    hs[sblocks * (uint64_t)ns] = 0;
+    parallel_dynamic(ns, hw_threads(0), 16, [&](int, uint32_t b, uint32_t e) {
+      for (uint32_t s2 = b; s2 < e; ++s2) {
+        const uint32_t t = sparse_terms[s2];
+        uint64_t* blk = hs.data() + (uint64_t)s2 * sblocks;
+        uint64_t* wd = hs.data() + (uint64_t)ns * sblocks;
+        std::fill(blk, blk + sblocks, 0ull);
+        uint64_t cur = wbase[s2];
+        uint32_t last = 0xFFFFFFFFu;
+        for (uint64_t p = hp.off[t]; p < hp.off[t + 1]; ++p) {
+          const uint32_t d = hp.doc[p], w = d >> 5;
+          if (w != last) {
+            if (last != 0xFFFFFFFFu) ++cur;
+            last = w;
+            wd[cur] = (uint64_t)(p - hp.off[t]) << 32;  // postings before the word's first doc
+            uint64_t& be = blk[fg::srank_block(d)];
+            if (!(uint32_t)be) be = cur << 32;  // the block's first word
+            be |= 1ull << (w & 31u);
+          }
+          wd[cur] |= 1ull << (d & 31u);
+        }
+      }
+    });
+    HIPCHK(hipMemcpyAsync(d_srank, hs.data(), hs.size() * 8, hipMemcpyHostToDevice, kBuildStream));
+    HIPCHK(hipStreamSynchronize(kBuildStream));
+    for (uint32_t s2 = 0; s2 < ns; ++s2) tmeta[sparse_terms[s2]] |= ((first_slot + s2) << 16) | 0x80000000u;
   }
   if (!rank_terms.empty()) {
     // one k_rank launch for every rank term: per slot the term's posting range
@@ -984,7 +1078,8 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     HIPCHK(hipFreeAsync(d_tab, kBuildStream));
     HIPCHK(hipStreamSynchronize(kBuildStream));
   }
-  ix->n_rank = (uint32_t)rank_terms.size();
+  ix->n_rank = (uint32_t)(rank_terms.size() + sparse_terms.size());
+  ix->n_srank_words = sparse_terms.empty() ? 0 : 1 + n_swords;
   if ((rc = dev_upload(sm, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
   ix->tmeta = tmeta;
   g_bt.mark("rank words");
@@ -1022,6 +1117,10 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->d.dir_off = d_dir_off;
   ix->d.tmeta = d_tmeta;
   ix->d.rank = d_rank;
+  ix->d.srank = d_srank;
+  ix->d.srank_w = d_srank ? d_srank + (uint64_t)sblocks * sparse_terms.size() : nullptr;
+  ix->d.n_prank = (uint32_t)rank_terms.size();
+  ix->d.srank_blocks = sblocks;
   ix->d.toff = d_toff;
   ix->d.tdir = d_tdir;
   ix->d.coff = d_coff;
@@ -1508,6 +1607,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->dir_entries = base->dir_entries;
   ix->tile_entries = base->tile_entries;
   ix->n_rank = base->n_rank;
+  ix->n_srank_words = base->n_srank_words;
   ix->off = base->off;
   ix->df_text = base->df_text;
   ix->df_name = base->df_name;
@@ -1693,6 +1793,10 @@ int fg_index_stats_get(const fg_index* ix, fg_index_stats* o) {
   o->tot_facet_tokens = ix->tot_f;
   o->n_dense_f32 = ix->n_dense;
   o->n_rank_terms = ix->n_rank;
+  o->n_sparse_rank_terms = ix->n_rank - ix->d.n_prank;
+  o->reserved0 = 0;
+  o->rank_bytes = 8ull * ix->d.n_prank * ix->d.rank_words +
+                  8ull * (ix->n_rank - ix->d.n_prank) * ix->d.srank_blocks + 8ull * ix->n_srank_words;
   return FG_OK;
 }
 

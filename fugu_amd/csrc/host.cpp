@@ -1413,7 +1413,9 @@ struct PhaseTrace {
   void mark(const char* phase) {
     if (!on) return;
     const auto n = std::chrono::steady_clock::now();
-    fprintf(stderr, "[fg %s] %-28s %9.2f ms\n", what, phase, std::chrono::duration<double, std::milli>(n - t).count());
+    // @: the phase's end on the steady clock (ms; Python's time.monotonic)
+    fprintf(stderr, "[fg %s] %-28s %9.2f ms @%.3f\n", what, phase, std::chrono::duration<double, std::milli>(n - t).count(),
+            std::chrono::duration<double, std::milli>(n.time_since_epoch()).count());
     t = n;
   }
 };

@@ -72,10 +72,27 @@ __device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f
 // Term score at doc d through the term's dense structure (meta_slot != 0),
 // -1 = the term is absent from d.  Rank words: one 8-B load, and on a hit the
 // posting score at position rank + popcount(presence bits below d).
+// The rank word of doc d for rank-kind slot `slot`: plain, or sparse (block
+// entry, then the word: the zero word when the term has none of the word's docs).
+__device__ inline uint64_t rank_word_of(const DevIndex& ix, uint32_t slot, uint32_t d) {
+  if (slot <= ix.n_prank) return ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(d)];
+  return ix.srank_w[srank_index(ix.srank[(size_t)(slot - 1 - ix.n_prank) * ix.srank_blocks + srank_block(d)], d)];
+}
+// A term's rank-kind structure as one array indexed by d >> shift: the plain
+// rank words (shift 5) or the sparse block entries (shift 10, then srank_index)
+__device__ inline const uint64_t* rank_base(const DevIndex& ix, uint32_t slot, uint32_t& shift) {
+  if (slot <= ix.n_prank) {
+    shift = 5u;
+    return ix.rank + (size_t)(slot - 1) * ix.rank_words;
+  }
+  shift = 10u;
+  return ix.srank + (size_t)(slot - 1 - ix.n_prank) * ix.srank_blocks;
+}
+
 __device__ inline float dense_score(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t d) {
   const uint32_t slot = meta_slot(meta);
   if (meta_rank(meta)) {
-    const uint32_t p = rank_pos(ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(d)], d);
+    const uint32_t p = rank_pos(rank_word_of(ix, slot, d), d);
     return p == kInvalid ? -1.0f : ix.psc[base + p];
   }
   return ix.dense[(size_t)(slot - 1) * ix.n_docs + d];
@@ -90,7 +107,7 @@ __device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t t
 // Does term (meta, postings at base, directory at dir_off) hold doc d?  (MustNot probes)
 __device__ inline bool term_has_doc(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t dir_off, uint32_t d) {
   const uint32_t slot = meta_slot(meta);
-  if (slot && meta_rank(meta)) return (ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(d)] >> (d & 31u)) & 1ull;
+  if (slot && meta_rank(meta)) return (rank_word_of(ix, slot, d) >> (d & 31u)) & 1ull;
   if (slot) return ix.dense[(size_t)(slot - 1) * ix.n_docs + d] >= 0.0f;
   const uint32_t* __restrict__ dir = ix.dir + dir_off;
   const uint32_t b = d >> (meta & 0xFFu);
@@ -384,12 +401,20 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
   const uint32_t dslot = meta_slot(meta);
   if (dslot && meta_rank(meta)) {
     // rank words: presence + rank in one 8-B load per item (all items'
-    // loads in flight together), then the posting score of the hits
-    const uint64_t* __restrict__ rw = ix.rank + (size_t)(dslot - 1) * ix.rank_words;
+    // loads in flight together; sparse ones: the block entries, then the
+    // words), then the posting score of the hits
+    uint32_t sh;
+    const uint64_t* __restrict__ rw = rank_base(ix, dslot, sh);
     const float* __restrict__ ps = ix.psc + ix.off[ti];
     uint64_t x[N];
 #pragma unroll
-    for (uint32_t j = 0; j < N; ++j) x[j] = (live & (1u << j)) ? rw[rank_word(doc[j])] : 0ull;
+    for (uint32_t j = 0; j < N; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> sh] : 0ull;
+    if (sh != 5u) {
+#pragma unroll
+      for (uint32_t j = 0; j < N; ++j) {
+        x[j] = ix.srank_w[srank_index(x[j], doc[j])];
+      }
+    }
 #pragma unroll
     for (uint32_t j = 0; j < N; ++j) {
       const uint32_t p = rank_pos(x[j], doc[j]);
@@ -658,12 +683,20 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
       float sc[kItems];
       if (dslot && meta_rank(meta)) {
         // rank words: presence + rank in one 8-B load per item (all items'
-        // loads in flight together), then the posting score of the hits
-        const uint64_t* __restrict__ rw = ix.rank + (size_t)(dslot - 1) * ix.rank_words;
+        // loads in flight together; sparse ones: the block entries, then the
+        // words), then the posting score of the hits
+        uint32_t sh;
+        const uint64_t* __restrict__ rw = rank_base(ix, dslot, sh);
         const float* __restrict__ ps = ix.psc + ix.off[ti];
         uint64_t x[kItems];
 #pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[rank_word(doc[j])] : 0ull;
+        for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> sh] : 0ull;
+        if (sh != 5u) {
+#pragma unroll
+          for (uint32_t j = 0; j < kItems; ++j) {
+            x[j] = ix.srank_w[srank_index(x[j], doc[j])];
+          }
+        }
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j) {
           const uint32_t p = rank_pos(x[j], doc[j]);
@@ -1398,16 +1431,27 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
             const uint32_t meta = i < m ? sh.c_meta[i] : 0u;
             const uint32_t slot = meta_slot(meta);
             const bool rank = slot && meta_rank(meta);
+            uint32_t rsh = 5u;
+            const uint64_t* __restrict__ rw = rank ? rank_base(ix, slot, rsh) : nullptr;
 #pragma unroll
             for (uint32_t j = 0; j < J; ++j) {
               x[g][j] = kAbsent;
               if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
                 need |= 1u << (g * J + j);
-                if (rank) x[g][j] = ix.rank[(size_t)(slot - 1) * ix.rank_words + rank_word(pd[j])];
+                if (rank) x[g][j] = rw[pd[j] >> rsh];
                 else if (slot) x[g][j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
                 else x[g][j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
               }
             }
+          }
+          // sparse rank clauses: from the block entries to the words
+#pragma unroll
+          for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t meta = i0 + g < m ? sh.c_meta[i0 + g] : 0u;
+            if (!(meta_rank(meta) && meta_slot(meta) > ix.n_prank)) continue;
+#pragma unroll
+            for (uint32_t j = 0; j < J; ++j)
+              if ((need >> (g * J + j)) & 1u) x[g][j] = ix.srank_w[srank_index(x[g][j], pd[j])];
           }
 #pragma unroll
           for (uint32_t g = 0; g < G; ++g) {

@@ -27,7 +27,7 @@ using fgh::parallel_dynamic;
 
 namespace {
 
-enum Arr : uint32_t { A_DOC, A_PSC, A_RANK, A_DENSE, A_DIR, A_BMAX, A_TMAX, A_TDIR, A_CMAX, A_TSUB, A_N };
+enum Arr : uint32_t { A_DOC, A_PSC, A_RANK, A_SRANK, A_SRANKW, A_DENSE, A_DIR, A_BMAX, A_TMAX, A_TDIR, A_CMAX, A_TSUB, A_N };
 constexpr uint64_t kLine = 128;
 constexpr float kInflate = 1.00000762939453125f;  // kernels.hip inflate_bound: 1 + 2^-17
 
@@ -37,7 +37,7 @@ struct Snap {
   const fg_index* ix = nullptr;
   const uint32_t* doc = nullptr;
   std::vector<float> psc, tmax, bmax, cmax;
-  std::vector<uint64_t> tsub;
+  std::vector<uint64_t> tsub, srank;  // srank: the sparse rank block entries
   std::vector<uint32_t> dir_off, toff, coff;
   uint64_t bytes[A_N] = {0};
   int load(const fg_index* x) {
@@ -64,14 +64,31 @@ struct Snap {
     HIPCHK(rd(tsub.data(), x->d.tsub, 8 * tsub.size()));
     HIPCHK(rd(bmax.data(), x->d.bmax, 4 * bmax.size()));
     HIPCHK(rd(cmax.data(), x->d.cmax, 4 * cmax.size()));
+    srank.resize((uint64_t)(x->n_rank - x->d.n_prank) * x->d.srank_blocks);
+    HIPCHK(rd(srank.data(), x->d.srank, 8 * srank.size()));
     bytes[A_DOC] = bytes[A_PSC] = 4 * P;
-    bytes[A_RANK] = 8ull * x->n_rank * x->d.rank_words;
+    bytes[A_RANK] = 8ull * x->d.n_prank * x->d.rank_words;
+    bytes[A_SRANK] = 8ull * srank.size();
+    bytes[A_SRANKW] = 8ull * x->n_srank_words;
     bytes[A_DENSE] = 4ull * x->n_dense * x->n_docs;
     bytes[A_DIR] = bytes[A_BMAX] = 4 * x->dir_entries;
     bytes[A_TMAX] = bytes[A_TDIR] = 4 * x->tile_entries;
     bytes[A_CMAX] = 4ull * x->n_sc;
     bytes[A_TSUB] = 8ull * tsub.size();
     return FG_OK;
+  }
+  // the loads of a rank-kind probe of doc d (plain: the word; sparse: the
+  // block entry, then the word when the term holds any of its docs)
+  template <class Acc>
+  void rank_loads(Acc& A, uint32_t s, uint32_t slot, uint32_t d, double& cat) const {
+    if (slot <= ix->d.n_prank) {
+      A.gather(s, A_RANK, ((uint64_t)(slot - 1) * ix->d.rank_words + fg::rank_word(d)) * 8, 8, cat);
+      return;
+    }
+    const uint64_t at = (uint64_t)(slot - 1 - ix->d.n_prank) * ix->d.srank_blocks + fg::srank_block(d);
+    A.gather(s, A_SRANK, at * 8, 8, cat);
+    const uint32_t w = fg::srank_index(srank[at], d);
+    if (w != 0xFFFFFFFFu) A.gather(s, A_SRANKW, (uint64_t)w * 8, 8, cat);
   }
   uint64_t len(uint32_t t) const { return ix->off[t + 1] - ix->off[t]; }
   const uint32_t* list(uint32_t t) const { return doc + ix->off[t]; }
@@ -164,7 +181,7 @@ float probe_term(const Snap& S, Acc& A, uint32_t s, uint32_t t, uint32_t d, doub
   const uint32_t* l = S.list(t);
   const uint64_t n = S.len(t), base = S.ix->off[t];
   if (slot && fg::meta_rank(meta)) {
-    A.gather(s, A_RANK, ((uint64_t)(slot - 1) * S.ix->d.rank_words + fg::rank_word(d)) * 8, 8, cat);
+    S.rank_loads(A, s, slot, d, cat);
     const uint64_t p = std::lower_bound(l, l + n, d) - l;
     if (p < n && l[p] == d) {
       A.gather(s, A_PSC, (base + p) * 4, 4, cat);
@@ -433,7 +450,7 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
           while (cur[i] < hi[i] && li[cur[i]] < d) ++cur[i];
           const bool here = cur[i] < hi[i] && li[cur[i]] == d;
           if (slot && fg::meta_rank(meta[i])) {
-            A.gather(i, A_RANK, ((uint64_t)(slot - 1) * ix->d.rank_words + fg::rank_word(d)) * 8, 8, A.probe);
+            S.rank_loads(A, i, slot, d, A.probe);
             if (here) {
               A.gather(i, A_PSC, (bi + cur[i]) * 4, 4, A.probe);
               v[i] = S.psc[bi + cur[i]];
@@ -556,7 +573,7 @@ int fg_model_batch(const fg_index* ix, const fg_query_batch* q, uint32_t k, cons
   out->alg_bytes = out->stream_bytes + out->probe_bytes + out->output_bytes;
   out->line_bytes = (double)kLine * (double)U.count();
   if (getenv("FUGU_MODEL_TRACE")) {  // the line floor and the per-query line sum, by array
-    static const char* names[A_N] = {"doc", "psc", "rank", "dense", "dir", "bmax", "tmax", "tdir", "cmax", "tsub"};
+    static const char* names[A_N] = {"doc", "psc", "rank", "srank", "srankw", "dense", "dir", "bmax", "tmax", "tdir", "cmax", "tsub"};
     for (uint32_t a = 0; a < A_N; ++a)
       fprintf(stderr, "[fg model] %-6s floor %8.3f GB  per-query sum %8.3f GB\n", names[a],
               (double)kLine * (double)U.count(a) * 1e-9, (double)kLine * (double)U.qlines[a].load() * 1e-9);

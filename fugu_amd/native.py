@@ -104,7 +104,8 @@ class IndexStats(C.Structure):
     _fields_ = [("n_docs", C.c_uint32), ("n_terms", C.c_uint32), ("n_postings", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("tot_tokens", C.c_uint64 * 2), ("avgdl", C.c_float * 2),
                 ("has_name", C.c_int), ("device", C.c_int), ("n_facet_terms", C.c_uint32),
-                ("tot_facet_tokens", C.c_uint64), ("n_dense_f32", C.c_uint32), ("n_rank_terms", C.c_uint32)]
+                ("tot_facet_tokens", C.c_uint64), ("n_dense_f32", C.c_uint32), ("n_rank_terms", C.c_uint32),
+                ("n_sparse_rank_terms", C.c_uint32), ("reserved0", C.c_uint32), ("rank_bytes", C.c_uint64)]
 
 
 class ModelOut(C.Structure):
@@ -253,6 +254,8 @@ class Stats:
     tot_facet_tokens: int = 0
     n_dense_f32: int = 0
     n_rank_terms: int = 0
+    n_sparse_rank_terms: int = 0
+    rank_bytes: int = 0
 
 
 def _u64(a):
@@ -441,7 +444,8 @@ class Index:
         s = IndexStats()
         _check(_lib.fg_index_stats_get(self._h, C.byref(s)))
         return Stats(s.n_docs, s.n_terms, s.n_postings, s.device_bytes, tuple(s.tot_tokens), tuple(s.avgdl),
-                     bool(s.has_name), s.device, s.n_facet_terms, s.tot_facet_tokens, s.n_dense_f32, s.n_rank_terms)
+                     bool(s.has_name), s.device, s.n_facet_terms, s.tot_facet_tokens, s.n_dense_f32, s.n_rank_terms,
+                     s.n_sparse_rank_terms, s.rank_bytes)
 
     def df(self, term: int, field: int = -1) -> int:
         return int(_lib.fg_index_df(self._h, field, term))

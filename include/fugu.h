@@ -193,6 +193,9 @@ typedef struct fg_index_stats {
   uint64_t tot_facet_tokens;
   uint32_t n_dense_f32;      /* terms with an f32 score table */
   uint32_t n_rank_terms;     /* terms with rank words */
+  uint32_t n_sparse_rank_terms;  /* ... of which sparse rank words (block entries + the words holding docs) */
+  uint32_t reserved0;
+  uint64_t rank_bytes;       /* device bytes of the rank words, plain and sparse */
 } fg_index_stats;
 int fg_index_stats_get(const fg_index* ix, fg_index_stats* out);
 /* doc_freq of `term` in `field` (tantivy Searcher::doc_freq; FG_FIELD_FACET:

@@ -102,6 +102,9 @@ pub struct fg_index_stats {
     pub tot_facet_tokens: u64,
     pub n_dense_f32: u32,
     pub n_rank_terms: u32,
+    pub n_sparse_rank_terms: u32,
+    pub reserved0: u32,
+    pub rank_bytes: u64,
 }
 
 #[repr(C)]

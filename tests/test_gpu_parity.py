@@ -464,17 +464,22 @@ def test_single_list_block_max_vs_oracle(native, ctx, gpu_1m, oracle_1m, k):
         assert_same(s[i], d[i], n[i], rs[i, :rn[i]], rd[i, :rn[i]], ("deletes", k, int(terms[i])))
 
 
-@pytest.mark.parametrize("env", [{"FUGU_RANK_GIB": "0"}, {"FUGU_RANK_GIB": "0.02"},
+@pytest.mark.parametrize("env", [{"FUGU_RANK_GIB": "0"}, {"FUGU_RANK_GIB": "0.02", "FUGU_RANK_PLAIN_DIV": "16384"},
                                  {"FUGU_RANK_GIB": "0", "FUGU_DENSE_GIB": "0.5"},
-                                 {"FUGU_RANK_GIB": "0.02", "FUGU_DENSE_GIB": "0.05"}],
-                         ids=["directory_only", "few_rank_terms", "f32_tables", "mixed_kinds"])
+                                 {"FUGU_RANK_GIB": "0.02", "FUGU_DENSE_GIB": "0.05", "FUGU_RANK_PLAIN_DIV": "16384"},
+                                 {"FUGU_RANK_PLAIN_DIV": "16384"}, {"FUGU_RANK_PLAIN_DIV": "1"},
+                                 {"FUGU_RANK_GIB": "0.05", "FUGU_DENSE_GIB": "0.05", "FUGU_RANK_PLAIN_DIV": "16"}],
+                         ids=["directory_only", "few_rank_terms", "f32_tables", "mixed_kinds", "plain_rank_only",
+                              "sparse_rank_only", "all_kinds"])
 def test_probe_structure_budgets_vs_oracle(native, ctx, corpus_1m, oracle_1m, env):
     """Every probe kind gives the oracle's results: the bucket directory alone
     (no rank words), a budget that fits only the densest terms' rank words, the
-    f32 score tables, and both dense kinds at once (fg_internal.h DevIndex)."""
+    f32 score tables, both dense kinds at once, plain rank words only (the
+    round-4 layout), sparse rank words wherever they are smaller, and every kind
+    at once (fg_internal.h DevIndex)."""
     import os
     from fugu_amd import synth
-    old = {k: os.environ.get(k) for k in ("FUGU_RANK_GIB", "FUGU_DENSE_GIB")}
+    old = {k: os.environ.get(k) for k in ("FUGU_RANK_GIB", "FUGU_DENSE_GIB", "FUGU_RANK_PLAIN_DIV")}
     os.environ.update(env)
     try:
         ix = native.Index.from_docs(ctx, corpus_1m.off, corpus_1m.tok, 1 << 20, threads=16)
@@ -487,8 +492,20 @@ def test_probe_structure_budgets_vs_oracle(native, ctx, corpus_1m, oracle_1m, en
     st = ix.stats()
     if env.get("FUGU_RANK_GIB") == "0":
         assert st.n_rank_terms == 0
+    elif "FUGU_RANK_GIB" in env:
+        assert 0 < st.n_rank_terms < 4000
     else:
-        assert 0 < st.n_rank_terms < 2000
+        assert st.n_rank_terms > 4000
+    if env.get("FUGU_RANK_PLAIN_DIV") == "16384":
+        assert st.n_sparse_rank_terms == 0
+        assert st.rank_bytes == st.n_rank_terms * 8 * ((1_000_000 + 31) // 32)
+    elif env.get("FUGU_RANK_GIB") != "0":
+        assert 0 < st.n_sparse_rank_terms <= st.n_rank_terms
+        if env.get("FUGU_RANK_PLAIN_DIV") == "1":
+            # only terms in most 32-doc words keep plain ones (smaller for them)
+            assert st.n_sparse_rank_terms >= st.n_rank_terms - 200
+        else:
+            assert st.n_sparse_rank_terms < st.n_rank_terms  # the densest terms keep plain rank words
     assert (st.n_dense_f32 > 0) == ("FUGU_DENSE_GIB" in env)
     for (m0, m1, k, mode) in [(3, 3, 100, native.MODE_AND), (1, 5, 1000, native.MODE_AND),
                               (2, 4, 1000, native.MODE_OR)]:

@@ -43,13 +43,17 @@ def main():
         t0 = time.time()
         ix = native.Index.from_docs(ctx, corp.off, corp.tok, synth.VOCAB, threads=16, keep_host=False)
         st = ix.stats()
-        print(f"[ab] {name} {env}: f32 tables {st.n_dense_f32}, rank terms {st.n_rank_terms}, "
+        print(f"[ab] {name} {env}: f32 tables {st.n_dense_f32}, rank terms {st.n_rank_terms} "
+              f"({st.n_sparse_rank_terms} sparse, {st.rank_bytes / 2**30:.2f} GiB), "
               f"{st.device_bytes / 2**30:.2f} GiB, built in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
         ixs[name] = (ix, st.device_bytes, env)
     os.environ.clear()
     os.environ.update(base_env)
     out = {"docs": args.docs, "s": args.s, "variants": args.variants,
-           "device_gib": {n: round(b / 2**30, 3) for n, (_, b, _) in ixs.items()}, "workloads": {}}
+           "device_gib": {n: round(b / 2**30, 3) for n, (_, b, _) in ixs.items()},
+           "rank": {n: {"terms": ix.stats().n_rank_terms, "sparse": ix.stats().n_sparse_rank_terms,
+                        "gib": round(ix.stats().rank_bytes / 2**30, 3)} for n, (ix, _, _) in ixs.items()},
+           "workloads": {}}
     for wl in args.workloads.split(","):
         m0, m1, k, mode = SPECS[wl]
         q_off, terms = synth.queries(1024, m0, m1)
