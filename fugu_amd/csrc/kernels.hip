@@ -533,8 +533,10 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
   uint64_t t_start = FG_NOW(), t_probe = 0, t_keys = 0, t_sel = 0, n_app = 0;
   (void)t_start; (void)t_probe; (void)t_keys; (void)t_sel; (void)n_app;
   const uint32_t q = pl.work_q[w];
-  const DevIndex ix = kMulti ? seg_index(pl, q / pl.seg_nq) : ix0;
-  const uint32_t ql = kMulti ? q % pl.seg_nq : q;  // the batch query (threshold, histogram)
+  const DevIndex ix = kMulti ? seg_index(pl, __builtin_amdgcn_readfirstlane(q / pl.seg_nq)) : ix0;
+  // the batch query (threshold, histogram); uniform, and kept in SGPRs (the
+  // division runs on the VALU: without readfirstlane its pointers took VGPRs)
+  const uint32_t ql = kMulti ? __builtin_amdgcn_readfirstlane(q % pl.seg_nq) : q;
   const uint32_t c0 = pl.work_c[w], nc = pl.work_n[w];
   // terms: [Must (cost order)][MustNot][Should]; a query with Should clauses is
   // Must-driven (RequiredOptionalScorer): the Shoulds only add score
@@ -1033,8 +1035,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   const uint32_t w = pl.n_conj + (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 
   const uint32_t q = pl.work_q[w];
-  const DevIndex ix = kMulti ? seg_index(pl, q / pl.seg_nq) : ix0;
-  const uint32_t ql = kMulti ? q % pl.seg_nq : q;  // the batch query (threshold, histogram)
+  const DevIndex ix = kMulti ? seg_index(pl, __builtin_amdgcn_readfirstlane(q / pl.seg_nq)) : ix0;
+  // the batch query (threshold, histogram); uniform, and kept in SGPRs (the
+  // division runs on the VALU: without readfirstlane its pointers took VGPRs)
+  const uint32_t ql = kMulti ? __builtin_amdgcn_readfirstlane(q % pl.seg_nq) : q;
   const uint32_t tile0 = pl.work_c[w], ntile = pl.work_n[w];
   // terms: [Should clauses (clause order)][MustNot]; m = the Should clauses
   const uint32_t qmv = pl.q_m[q];
@@ -1711,8 +1715,8 @@ __global__ __launch_bounds__(kThreads) void k_scan(DevIndex ix0, DevPlan pl) {
   const uint32_t tid = threadIdx.x;
   const uint32_t w = pl.total_chunks + blockIdx.x;  // scan items follow the k_conj / k_disj items
   const uint32_t q = pl.work_q[w];
-  const DevIndex ix = kMulti ? seg_index(pl, q / pl.seg_nq) : ix0;
-  const uint32_t ql = kMulti ? q % pl.seg_nq : q;
+  const DevIndex ix = kMulti ? seg_index(pl, __builtin_amdgcn_readfirstlane(q / pl.seg_nq)) : ix0;
+  const uint32_t ql = kMulti ? __builtin_amdgcn_readfirstlane(q % pl.seg_nq) : q;
   const uint32_t tile0 = pl.work_c[w], ntile = pl.work_n[w];
   const uint32_t K = pl.k;
   uint64_t* gthr = &pl.thresh[ql];

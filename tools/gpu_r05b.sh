@@ -1,7 +1,7 @@
 set -o pipefail
 # k_disj item size (tiles per item, items per query): the concurrent doc window
 # each XCD's L2 has to hold.  Time at k = 20 / 1000, then DRAM bytes per launch
-O=gpurun_out/r05b; mkdir -p $O
+O=gpurun_out/r05k/items; mkdir -p $O
 V=fugu_amd/variants
 B=$V/libfugu_i8w4t1024b4d256m0g8f4096q896x448h10n16o64_32z12y11u5r512h9g1s16k32768.so
 G16=$V/libfugu_i8w4t1024b4d256m0g8f4096q896x448h10n16o128_16z12y11u5r512h9g1s16k32768.so
