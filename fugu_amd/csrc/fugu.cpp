@@ -245,10 +245,25 @@ namespace {
 // background merger's build run side by side.  Uploads are synchronous with
 // the host (the sources may be freed right after).
 // (a thread may point it at another stream: fg_index_rescore_many's workers
-// use low-priority ones, so a commit's new segment and the searches running
-// beside its rescores are dispatched first)
-thread_local hipStream_t tl_build_stream = hipStreamPerThread;
-#define kBuildStream tl_build_stream
+// use the device's background streams; a thread under fg_thread_background
+// uses one of them for everything it builds)
+thread_local hipStream_t tl_build_stream = nullptr;
+thread_local int tl_background = 0;
+hipStream_t background_stream(int dev, uint32_t i);
+hipStream_t build_stream() {
+  if (tl_build_stream) return tl_build_stream;
+  if (tl_background) {
+    thread_local const uint32_t mine = [] {
+      static std::atomic<uint32_t> next{0};
+      return next.fetch_add(1);
+    }();
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess)
+      if (hipStream_t st = background_stream(dev, mine)) return st;
+  }
+  return hipStreamPerThread;
+}
+#define kBuildStream build_stream()
 
 // The calling thread's high-priority stream on device `dev` (the search path's
 // own: its kernels are dispatched ahead of a commit's rescores and builds on the
@@ -274,24 +289,44 @@ static hipStream_t search_stream(int dev) {
   return s;
 }
 
-// low-priority streams of a device for background rescoring, created once
-hipStream_t low_priority_stream(int dev, uint32_t i) {
+// The background streams of a device (a db's rescores, segment builds and
+// merges), created once: restricted by a CU mask to FUGU_BG_CU_FRAC of the
+// device's CUs (default kBgCuFrac; the CUs left out spread evenly over the
+// XCDs), so the searches running beside a commit always find CUs free -- the
+// slow searches during commits sat behind the commits' scoring kernels
+// (tools/stall_trace.py) -- or, at FUGU_BG_CU_FRAC=1, low-priority streams
+constexpr double kBgCuFrac = 0.75;
+hipStream_t background_stream(int dev, uint32_t i) {
   static std::mutex mu;
   static std::map<int, std::vector<hipStream_t>> streams;
   constexpr uint32_t kN = 8;
   std::lock_guard<std::mutex> l(mu);
   auto& v = streams[dev];
   if (v.empty()) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    const char* e = getenv("FUGU_BG_CU_FRAC");
+    const double frac = e && *e ? atof(e) : kBgCuFrac;
+    hipDeviceProp_t prop;
+    const int n_cu = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 0;
+    std::vector<uint32_t> mask((std::max(n_cu, 1) + 31) / 32, 0u);
+    const uint32_t off = n_cu > 0 && frac < 1.0 ? (uint32_t)((1.0 - std::max(frac, 0.125)) * n_cu + 0.5) : 0u;
+    for (uint32_t c = 0; c < (uint32_t)n_cu; ++c)  // CU c left out when a multiple of n/off falls in [c, c+1)
+      if (!off || (uint64_t)(c + 1) * off / n_cu == (uint64_t)c * off / n_cu) mask[c / 32] |= 1u << (c % 32);
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
     for (uint32_t j = 0; j < kN; ++j) {
       hipStream_t st = nullptr;
-      if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least) != hipSuccess) {
+      const hipError_t rc = off ? hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data())
+                                : hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least);
+      if (rc != hipSuccess) {
         (void)hipGetLastError();
         st = nullptr;
       }
       v.push_back(st);
     }
+    (void)hipSetDevice(cur);
   }
   return v[i % kN];
 }
@@ -1735,7 +1770,7 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
     for (uint32_t i; (i = next.fetch_add(1)) < n;) {
       const int dev = bases[i]->dev;
       if (hipSetDevice(dev) == hipSuccess)
-        if (hipStream_t st = low_priority_stream(dev, slot.fetch_add(1))) tl_build_stream = st;
+        if (hipStream_t st = background_stream(dev, slot.fetch_add(1))) tl_build_stream = st;
       if ((rc[i] = rescore_one(bases[i], g, deleted ? deleted[i] : nullptr, &outs[i], &wts))) err[i] = fg_last_error();
       tl_build_stream = saved;
     }
@@ -1763,6 +1798,12 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
       return fail(rc[i], "snapshot %u: %s", i, err[i].c_str());
     }
   return FG_OK;
+}
+
+int fg_thread_background(int on) {
+  const int prev = tl_background;
+  tl_background = on ? 1 : 0;
+  return prev;
 }
 
 int fg_index_retain(fg_index* ix) {
@@ -2386,18 +2427,25 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
       if (key == '2') return qt[mt - 1];
       return qt[1];
     };
-    for (const W& x : items) load[probe_term(x.q)]++;
-    std::vector<std::pair<uint64_t, uint32_t>> by;
-    for (auto& kv : load) by.emplace_back(kv.second, kv.first);
-    std::sort(by.begin(), by.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
-    uint64_t gl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    std::map<uint32_t, uint8_t> tg;
-    for (auto& [cnt, t] : by) {
-      const uint32_t g = (uint32_t)(std::min_element(gl, gl + 8) - gl);
-      gl[g] += cnt;
-      tg[t] = (uint8_t)g;
+    // single-list items and the others run as two launches (k_conj<true> over
+    // the first n_single items): each set is balanced over the 8 groups on its own
+    for (int set = 0; set < 2; ++set) {
+      load.clear();
+      for (const W& x : items)
+        if (single(x) == (set == 0)) load[probe_term(x.q)]++;
+      std::vector<std::pair<uint64_t, uint32_t>> by;
+      for (auto& kv : load) by.emplace_back(kv.second, kv.first);
+      std::sort(by.begin(), by.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
+      uint64_t gl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      std::map<uint32_t, uint8_t> tg;
+      for (auto& [cnt, t] : by) {
+        const uint32_t g = (uint32_t)(std::min_element(gl, gl + 8) - gl);
+        gl[g] += cnt;
+        tg[t] = (uint8_t)g;
+      }
+      for (const W& x : items)
+        if (single(x) == (set == 0)) q_grp[x.q] = tg[probe_term(x.q)];
     }
-    for (const W& x : items) q_grp[x.q] = tg[probe_term(x.q)];
   };
   auto radix = [&](std::vector<W>& items, bool conj) {
     const size_t n = items.size();

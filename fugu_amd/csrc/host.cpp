@@ -1635,6 +1635,7 @@ int commit_segment(fg_db* db, Namespace& ns) {
   int brc = FG_OK;
   std::string berr;
   std::thread builder([&] {
+    fg_thread_background(1);
     if (const char* f = getenv("FUGU_FAULT_INJECT"))  // tests only: a commit whose device build fails
       if (std::strcmp(f, "commit_build") == 0) {
         brc = FG_EHIP;
@@ -1972,6 +1973,7 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
 }
 
 void merger_main(fg_db* db) {
+  fg_thread_background(1);  // merges build on the device's CU-masked background streams
   for (;;) {
     std::shared_ptr<Namespace> ns;
     {
@@ -2048,6 +2050,12 @@ int fg_db_commit(fg_db* db, const char* nsname) {
   auto ns = find_ns(db, nsname);
   if (!ns) return hfail(FG_ENOTFOUND, std::string("Namespace '") + (nsname ? nsname : "") + "' not found");
   if (!db->ctx) return hfail(FG_ENODEV, "fg_db created without a device context");
+  // the commit's device work (new segment, rescores, an inline merge) on the
+  // background streams, leaving CUs to the searches running beside it
+  struct Background {
+    int prev = fg_thread_background(1);
+    ~Background() { fg_thread_background(prev); }
+  } bg;
   size_t nseg = 0;
   {
     std::shared_lock<std::shared_mutex> l(ns->snap_mu);

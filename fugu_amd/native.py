@@ -47,6 +47,7 @@ DIAG_PER_WG = 16  # fg_internal.h kDiagPerWg
 EXPORTS = (
     "fg_device_count", "fg_ctx_create", "fg_ctx_destroy", "fg_last_error", "fg_version",
     "fg_index_build_from_docs", "fg_index_build", "fg_index_retain", "fg_index_release",
+    "fg_thread_background",
     "fg_index_stats_get", "fg_index_df", "fg_index_bm25",
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
@@ -144,6 +145,7 @@ _sig("fg_index_rescore", C.c_int, _p, C.POINTER(GlobalStats), _u8p, C.POINTER(_p
 _sig("fg_index_rescore_many", C.c_int, C.POINTER(_p), C.c_uint32, C.POINTER(GlobalStats), C.POINTER(_u8p),
      C.POINTER(_p))
 _sig("fg_index_retain", C.c_int, _p)
+_sig("fg_thread_background", C.c_int, C.c_int)
 _sig("fg_index_release", C.c_int, _p)
 _sig("fg_index_stats_get", C.c_int, _p, C.POINTER(IndexStats))
 _sig("fg_index_df", C.c_uint64, _p, C.c_int, C.c_uint32)

@@ -176,6 +176,13 @@ int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8
  * (outs[] all NULL). */
 int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_global_stats* g,
                           const uint8_t* const* deleted, fg_index** outs);
+/* on != 0: the calling thread's snapshot builds and rescores run on the
+ * device's background streams -- restricted by a CU mask to FUGU_BG_CU_FRAC of
+ * the CUs (default 0.75, the rest spread over every XCD), so searches beside
+ * them always find free CUs (fugu's writer / merge threads beside its
+ * searchers, src/db/core.rs:247-249).  fg_db's commits and merger use it.
+ * Returns the previous setting. */
+int fg_thread_background(int on);
 
 int fg_index_retain(fg_index* ix);
 int fg_index_release(fg_index* ix);

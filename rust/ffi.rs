@@ -198,6 +198,7 @@ extern "C" {
                             out: *mut *mut fg_index) -> c_int;
     pub fn fg_index_rescore_many(bases: *const *const fg_index, n: u32, g: *const fg_global_stats,
                                  deleted: *const *const u8, outs: *mut *mut fg_index) -> c_int;
+    pub fn fg_thread_background(on: c_int) -> c_int;
     pub fn fg_index_retain(ix: *mut fg_index) -> c_int;
     pub fn fg_index_release(ix: *mut fg_index) -> c_int;
     pub fn fg_index_stats_get(ix: *const fg_index, out: *mut fg_index_stats) -> c_int;
