@@ -305,9 +305,9 @@ struct WsPool : DevCache {
   }
 };
 
-// Pinned host buffers of one index: plan uploads and result copies go through
-// them (a pageable copy is staged by the runtime and synchronises on the way),
-// which takes ~tens of us off a batch-of-one search.
+// Pinned host buffers of a device's snapshots: plan uploads and result copies
+// go through them (a pageable copy is staged by the runtime and synchronises on
+// the way), which takes ~tens of us off a batch-of-one search.
 struct PinnedPool {
   const size_t kKeep;  // bytes kept cached
   std::mutex mu;
@@ -361,6 +361,14 @@ struct PinnedLease {
 using fgh::PinnedLease;
 using fgh::PinnedPool;
 using fgh::WsPool;
+namespace fgh {
+// The plan-workspace and pinned pools of device `dev`, shared by every live
+// snapshot on it: a commit's rescored snapshots (new fg_index objects) reuse
+// the buffers of the ones they replace, so the first search after a commit does
+// not hipMalloc / hipHostMalloc (those sat in the slowest 1% of the searches
+// beside commits: tools/stall_trace.py).  Freed with the device's last snapshot.
+void device_pools(int dev, std::shared_ptr<WsPool>* ws, std::shared_ptr<PinnedPool>* pin);
+}  // namespace fgh
 
 struct fg_index {
   std::atomic<int> refs{1};
@@ -419,8 +427,10 @@ struct fg_index {
   fg::DevIndex d{};
   DevAllocs mem;
   fgh::ScoreBlock sblock;
-  WsPool pool;  // plan workspaces (destroyed before mem: declared after it)
-  PinnedPool pinned;  // host staging of plan uploads and result copies
+  // plan workspaces and the pinned host staging of plan uploads and result
+  // copies: the device's pools, shared by every snapshot on it (fgh::device_pools)
+  std::shared_ptr<WsPool> pool;
+  std::shared_ptr<PinnedPool> pinned;
 };
 
 struct fg_plan {
@@ -458,8 +468,8 @@ struct fg_plan {
         (void)hipSetDevice(ix->dev);
         (void)hipStreamSynchronize(last_stream);
       }
-      if (pin) ix->pinned.put(pin, pin_n);
-      ix->pool.put(ws, ws_got);
+      if (pin) ix->pinned->put(pin, pin_n);
+      ix->pool->put(ws, ws_got);
     }
     if (ix) fg_index_release(ix);
     for (fg_index* x : segs) fg_index_release(x);

@@ -194,6 +194,23 @@ void drop_all_cached() {
   for (DevCache* c : caches()) c->drop_cached();
   (void)hipSetDevice(dev);
 }
+void device_pools(int dev, std::shared_ptr<WsPool>* ws, std::shared_ptr<PinnedPool>* pin) {
+  static std::mutex mu;
+  static std::map<int, std::pair<std::weak_ptr<WsPool>, std::weak_ptr<PinnedPool>>> reg;
+  std::lock_guard<std::mutex> l(mu);
+  auto& e = reg[dev];
+  *ws = e.first.lock();
+  if (!*ws) {
+    *ws = std::make_shared<WsPool>();
+    (*ws)->dev = dev;
+    e.first = *ws;
+  }
+  *pin = e.second.lock();
+  if (!*pin) {
+    *pin = std::make_shared<PinnedPool>(64ull << 20);
+    e.second = *pin;
+  }
+}
 hipError_t dev_malloc(void** p, size_t bytes) {
   const uint64_t t0 = commit_trace_on() ? now_ns() : 0;
   if (hipMalloc(p, bytes) == hipSuccess) {
@@ -699,7 +716,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   auto ix = std::make_unique<fg_index>();
   ix->dev = dev;
   ix->mem.dev = dev;
-  ix->pool.dev = dev;
+  fgh::device_pools(dev, &ix->pool, &ix->pinned);
   ix->smem = std::make_shared<DevAllocs>();
   ix->smem->dev = dev;
   ix->n_docs = hp.n_docs;
@@ -1630,7 +1647,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   auto ix = std::make_unique<fg_index>();
   ix->dev = base->dev;
   ix->mem.dev = base->dev;
-  ix->pool.dev = base->dev;
+  fgh::device_pools(base->dev, &ix->pool, &ix->pinned);
   // the structure: shared device arrays and host bookkeeping (SharedVec)
   ix->smem = base->smem;
   ix->spool = base->spool;  // the structure's scoring blocks (a released rescore's block comes back)
@@ -2402,11 +2419,11 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // host time on a 20K-item batch.
   auto single = [&](const W& x) { return q_m[x.q] == fg::qm_pack(1, 1, 0); };
   // k_conj: the sweep split into 8 query groups, one per XCD (the kernel hands
-  // XCD x the x-th eighth of its items), the queries whose second list (the
-  // first one probed) is the same term in one group, groups balanced by items:
-  // headline k_conj 1.037 -> 1.001 ms, identical hits (profiles/r05/ab/
-  // ab_xcd_part.json; L2 hit rate 0.32 -> 0.23, DRAM 4.09 -> 4.57 GB: each XCD
-  // walks the whole doc range for fewer queries).  The same split of k_disj by
+  // XCD x the x-th eighth of its items), the queries whose lead list is the
+  // same term in one group, groups balanced by items: headline k_conj 1.049 ->
+  // 1.001 ms, identical hits (profiles/r05/ab/ab_xcd_key_balanced.log; by the
+  // second list, ab_xcd_part.json: L2 hit rate 0.32 -> 0.23, DRAM 4.09 -> 4.57
+  // GB, each XCD walks the whole doc range for fewer queries).  The same split of k_disj by
   // densest clause: OR top-20 2.78 -> 3.30 ms, top-1000 5.26 -> 6.86 ms -- its
   // sweep stays doc-ordered.  FUGU_XCD_PART=0: the doc sweep for k_conj (A/B).
   const char* xp = getenv("FUGU_XCD_PART");
@@ -2415,10 +2432,11 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   auto groups = [&](const std::vector<W>& items) {
     q_grp.assign(nq, 0);
     std::map<uint32_t, uint64_t> load;  // probed term -> items
-    // FUGU_XCD_KEY (A/B): 1 the second list (default), 0 the lead, 2 the last
+    // FUGU_XCD_KEY (A/B): 0 the lead list (default: ab_xcd_key_balanced.log,
+    // and3 1.001 vs 1.009 ms by the second list), 1 the second list, 2 the last
     // list, q the query itself (groups by items alone)
     const char* xk = getenv("FUGU_XCD_KEY");
-    const char key = xk && *xk ? *xk : '1';
+    const char key = xk && *xk ? *xk : '0';
     auto probe_term = [&](uint32_t qv) {
       const uint32_t* qt = q_terms.data() + (size_t)qv * fg::kMaxTerms;
       const uint32_t mt = fg::qm_terms(q_m[qv]);
@@ -2427,25 +2445,22 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
       if (key == '2') return qt[mt - 1];
       return qt[1];
     };
-    // single-list items and the others run as two launches (k_conj<true> over
-    // the first n_single items): each set is balanced over the 8 groups on its own
-    for (int set = 0; set < 2; ++set) {
-      load.clear();
-      for (const W& x : items)
-        if (single(x) == (set == 0)) load[probe_term(x.q)]++;
-      std::vector<std::pair<uint64_t, uint32_t>> by;
-      for (auto& kv : load) by.emplace_back(kv.second, kv.first);
-      std::sort(by.begin(), by.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
-      uint64_t gl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      std::map<uint32_t, uint8_t> tg;
-      for (auto& [cnt, t] : by) {
-        const uint32_t g = (uint32_t)(std::min_element(gl, gl + 8) - gl);
-        gl[g] += cnt;
-        tg[t] = (uint8_t)g;
-      }
-      for (const W& x : items)
-        if (single(x) == (set == 0)) q_grp[x.q] = tg[probe_term(x.q)];
+    // the multi-list items only (single-list ones keep the sweep and run as a
+    // launch of their own, k_conj<true> over the first n_single items)
+    for (const W& x : items)
+      if (!single(x)) load[probe_term(x.q)]++;
+    std::vector<std::pair<uint64_t, uint32_t>> by;
+    for (auto& kv : load) by.emplace_back(kv.second, kv.first);
+    std::sort(by.begin(), by.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
+    uint64_t gl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    std::map<uint32_t, uint8_t> tg;
+    for (auto& [cnt, t] : by) {
+      const uint32_t g = (uint32_t)(std::min_element(gl, gl + 8) - gl);
+      gl[g] += cnt;
+      tg[t] = (uint8_t)g;
     }
+    for (const W& x : items)
+      if (!single(x)) q_grp[x.q] = tg[probe_term(x.q)];
   };
   auto radix = [&](std::vector<W>& items, bool conj) {
     const size_t n = items.size();
@@ -2457,8 +2472,9 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     if (part) groups(items);
     for (size_t x = 0; x < n; ++x) {
       const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
-      const uint32_t sw = part ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
-                               : (uint32_t)(kk * 2147483647.0);
+      // single-list items keep the plain sweep (grouped: C3's mix 1.07 -> 1.11 ms)
+      const uint32_t sw = part && !single(items[x]) ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
+                                                    : (uint32_t)(kk * 2147483647.0);
       const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | sw;
       a[x] = ((uint64_t)rk << 32) | (uint64_t)x;
     }
@@ -2541,7 +2557,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
 #endif
   const size_t total = s_in + s_thr + s_cc + s_mask + s_hist + s_ck + s_os + s_od + s_on + s_dg;
   HIPCHK(hipSetDevice(ix->dev));
-  char* base = static_cast<char*>(ix->pool.get(std::max<size_t>(total, 256), &p->ws_got));
+  char* base = static_cast<char*>(ix->pool->get(std::max<size_t>(total, 256), &p->ws_got));
   if (!base) return fail(FG_EOOM, "plan workspace hipMalloc(%zu) failed", total);
   p->ws = base;
   p->ix = ix;  // owns the workspace from here on (returned to ix->pool); retained below
@@ -2555,7 +2571,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // zeroed with the upload, so the first execute needs no memset
   const size_t s_zero = s_thr + s_cc + s_mask + s_hist;
   const size_t s_up = s_in + (s_zero <= (64u << 10) ? s_zero : 0);
-  PinnedLease pin(ix->pinned, s_up);
+  PinnedLease pin(*ix->pinned, s_up);
   std::vector<char> staging_pageable;  // only if the pinned allocation failed
   char* staging = static_cast<char*>(pin.p);
   if (!staging) {
@@ -2707,7 +2723,7 @@ int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* o
   const char* first = reinterpret_cast<const char*>(p->own_score);
   const size_t span = reinterpret_cast<const char*>(p->own_n) + 4ull * p->nq - first;
   if (span <= (4ull << 20)) {
-    PinnedLease pin(p->ix->pinned, span);
+    PinnedLease pin(*p->ix->pinned, span);
     if (pin.p) {
       HIPCHK(hipMemcpyAsync(pin.p, first, span, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
@@ -2940,7 +2956,7 @@ static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32
   const size_t total = 2 * g_s + g_n + 3 * o_k + o_n;
   size_t got = 0;
   HIPCHK(hipSetDevice(dev0));
-  char* base = static_cast<char*>(shards[0]->pool.get(total, &got));
+  char* base = static_cast<char*>(shards[0]->pool->get(total, &got));
   if (!base) return fail(FG_EOOM, "hipMalloc of the shard merge buffers failed");
   float* gs = reinterpret_cast<float*>(base);
   uint32_t* gd = reinterpret_cast<uint32_t*>(base + g_s);
@@ -2972,7 +2988,7 @@ static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32
       // leave them in flight)
       (void)hipSetDevice(sh[0]->dev);
       (void)hipStreamSynchronize(hipStreamPerThread);
-      sh[0]->pool.put(p, n);
+      sh[0]->pool->put(p, n);
     }
   } back{shards, n_shards, base, got, sst, evs};
   // every shard of a multi-shard call runs on a side stream of its device, so a
@@ -3080,7 +3096,7 @@ static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32
   // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
   const size_t span = 3 * o_k + 4ull * nq;
   if (span <= (4ull << 20)) {
-    PinnedLease pin(shards[0]->pinned, span);
+    PinnedLease pin(*shards[0]->pinned, span);
     if (pin.p) {
       HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
       HIPCHK(hipStreamSynchronize(hipStreamPerThread));
@@ -3150,7 +3166,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   const size_t total = 2 * g_s + g_n + 3 * o_k + o_n;
   size_t got = 0;
   HIPCHK(hipSetDevice(dev0));
-  char* base = static_cast<char*>(shards[0]->pool.get(total, &got));
+  char* base = static_cast<char*>(shards[0]->pool->get(total, &got));
   if (!base) return fail(FG_EOOM, "hipMalloc of the shard merge buffers failed");
   float* gs = reinterpret_cast<float*>(base);
   uint32_t* gd = reinterpret_cast<uint32_t*>(base + g_s);
@@ -3191,7 +3207,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       }
       (void)hipSetDevice(d0);
       (void)hipStreamSynchronize(s0);
-      ix0->pool.put(p, n);
+      ix0->pool->put(p, n);
     }
   } back{gdev, dev0, shards[0], base, got, evs, hs};
   static const bool trace_env = getenv("FUGU_SHARD_TRACE") != nullptr;
@@ -3281,7 +3297,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
   const size_t span = 3 * o_k + 4ull * nq;
   if (span <= (4ull << 20)) {
-    PinnedLease pin(shards[0]->pinned, span);
+    PinnedLease pin(*shards[0]->pinned, span);
     if (pin.p) {
       HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hs));
       HIPCHK(hipStreamSynchronize(hs));

@@ -17,3 +17,12 @@ for k in ('k_conj','k_disj'):
 "
   grep -h "k_conj\|k_disj" $D/kernel_stats.csv | cut -d, -f1-8
 done
+# GET /search during commits under runtime settings: more hardware queues per
+# process (streams otherwise share HIP's default 4), copies without the SDMA engines
+for V in "GPU_MAX_HW_QUEUES=16" "HSA_ENABLE_SDMA=0" "GPU_MAX_HW_QUEUES=16 HSA_ENABLE_SDMA=0"; do
+  N=$(echo $V | tr ' =' '__')
+  env $V timeout -k 10 400 python -u tools/stall_trace.py run --out $O/stall_$N > $O/stall_$N.json 2> $O/stall_$N.err || { tail -30 $O/stall_$N.err; exit 1; }
+  python3 -c "
+import json; d=json.load(open('$O/stall_$N/bench.json')); a=d['db_api_default_search']; c=d['commit']
+print('$V idle', a['p50_ms'], a['p99_ms'], 'during', {k: a['during_commits'][k] for k in ('p50_ms','p99_ms','max_ms','searches')}, 'commit', c['p50_ms'], c['p99_ms'])"
+done
