@@ -87,6 +87,11 @@ def roofline(kname, kernel_ms, model, key, alg_model, pruned=None):
 
 
 NO_MODEL = False  # --no-model: profiling passes skip the host replays
+# C5 over N GPUs: the fraction of each rank's k_disj sweep run before the ranks'
+# score histograms are summed (shard.exchange_hist; FUGU_C5_XFRAC=0: none), and
+# the split points the one-GPU rehearsal reports
+C5_XFRAC = float(os.environ.get("FUGU_C5_XFRAC", "0.125"))
+C5_EXCHANGE_FRACS = (0.0625, 0.125, 0.25)
 
 
 def model_sum(ixs, q_off, terms, k, thr, mode):
@@ -548,6 +553,58 @@ def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps):
     return ms, hits_sha1(out[0], out[1], out[2], out[3], K)
 
 
+def alone_exchanged_ms(ixs, q_off, terms, K, mode, st, reps, frac):
+    """Every shard's plan ALONE as in alone_kernel_ms, its k_disj sweep in two
+    parts with the shards' score histograms summed between them (what
+    shard.exchange_hist's all-reduce does across N GPUs): each shard's kernel ms
+    over both parts, the exchange's device time here, and the merged hash."""
+    from fugu_amd import native
+    from fugu_amd.shard import agree_hist_span, merge_on_device
+    import torch
+    nq = len(q_off) - 1
+    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
+    plans = [ix.plan(q_off, terms, K, mode) for ix in ixs]
+    agree_hist_span(plans)
+    S = len(plans)
+    gs = torch.empty((S, nq * K), dtype=torch.float32, device=dev)
+    gd = torch.empty((S, nq * K), dtype=torch.int32, device=dev)
+    gn = torch.empty((S, nq), dtype=torch.int32, device=dev)
+    hb = torch.zeros((S, nq * native.HIST_BINS), dtype=torch.int32, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    xch = []
+
+    def run():
+        for p in plans:
+            p.execute_part(st, 0.0, frac)
+        ev[0].record()
+        for r, p in enumerate(plans):
+            p.hist_copy(st, hb[r].data_ptr(), False)
+        tot = hb.sum(0, dtype=torch.int32)
+        for p in plans:
+            p.hist_copy(st, tot.data_ptr(), True)
+        ev[1].record()
+        for r, p in enumerate(plans):
+            p.execute_part(st, frac, 1.0, gs[r].data_ptr(), gd[r].data_ptr(), None, gn[r].data_ptr())
+        return tot
+
+    run()
+    torch.cuda.synchronize()
+    for p in plans:
+        p.profile(True)
+    for _ in range(reps):
+        run()
+        torch.cuda.synchronize()
+        xch.append(ev[0].elapsed_time(ev[1]))
+    ms = []
+    for p in plans:
+        m, n = p.kernel_ms()
+        ms.append((round(m[0] / max(n // 2, 1), 4), round(m[1] / max(n // 2, 1), 4)))
+        p.close()
+    out = merge_on_device(gs, gd, gn, nq, K, st)
+    torch.cuda.synchronize()
+    return ms, round(float(np.median(xch)), 4), hits_sha1(out[0], out[1], out[2], out[3], K)
+
+
 def hits_sha1(s, d, sh, n, K):
     """sha1 (16 hex) of merged (score, doc, shard) lists, each query's first n entries."""
     import hashlib
@@ -614,6 +671,17 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     alone_se, sha_se = alone_kernel_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2))
     log(f"[bench] C5 shards alone: unseeded max {max(x[0] for x in alone_un)} ms, seeded max "
         f"{max(x[0] for x in alone_se)} ms (linked mean {np.mean(per_shard):.3f}); floor in {seed_s:.1f}s")
+    # ... and with the histograms exchanged once mid-sweep (the N-GPU step's
+    # all-reduce, shard.exchange_hist), at a few split points
+    exch = {}
+    for f in C5_EXCHANGE_FRACS:
+        ex_ms, ex_dev, ex_sha = alone_exchanged_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2), f)
+        mx = max(x[0] for x in ex_ms)
+        exch[str(f)] = {"k_disj_ms": [x[0] for x in ex_ms], "max": mx, "k_final_ms": [x[1] for x in ex_ms],
+                        "max_over_linked_mean": round(mx / float(np.mean(per_shard)), 3),
+                        "exchange_device_ms_8_shards_one_gpu": ex_dev, "result_sha1": ex_sha}
+        log(f"[bench] C5 shards alone, histograms exchanged at {f}: max {mx} ms ({exch[str(f)]['max_over_linked_mean']}"
+            f" x linked mean), sha {ex_sha}")
     # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel),
     # planned with the floor; beside it the same plan without the floor
     outs = tuple(torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)) + (
@@ -661,6 +729,7 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
                "seeded_max_over_linked_mean": round(max(x[0] for x in alone_se) / float(np.mean(per_shard)), 3),
                "result_sha1_unseeded": sha_un, "result_sha1_seeded": sha_se, "same_hits": sha_un == sha_se,
                "floor_s": round(seed_s, 2),
+               "seeded_hist_exchanged": exch,
                "note": "each shard's plan alone (no shared threshold word: one GPU of the 8-GPU split); seeded = "
                        "its starting thresholds floored by the namespace-wide per-term K-th score bounds "
                        "(fg_index_term_ladder of every shard, one all-gather at build, fg_kth_floor_combine)"},
@@ -784,9 +853,27 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     merged_sel = len(plans) == 1 and len(ixs) > 1
     mouts = [torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)] + [
         torch.empty(nq, dtype=torch.int32, device=dev)]
+    # C5 over N ranks: the rank's k_disj sweep in two parts, the ranks' score
+    # histograms summed between them (one all-reduce per batch); bins agreed once
+    xfrac = C5_XFRAC if (not c4 and world > 1 and len(plans) == 1 and 0.0 < C5_XFRAC < 1.0) else 0.0
+    if xfrac:
+        from fugu_amd.shard import agree_hist_span, exchange_hist
+        agree_hist_span(plans, device=dev if backend == "nccl" else None)
+        hbuf = torch.zeros(nq * native.HIST_BINS, dtype=torch.int32, device=dev)
 
     def step():
-        if merged_sel:  # the rank's units merged by the plan's own final select
+        if xfrac:
+            p0 = plans[0]
+            p0.execute_part(st.cuda_stream, 0.0, xfrac)
+            exchange_hist(p0, st.cuda_stream, hbuf)
+            if merged_sel:
+                p0.execute_part(st.cuda_stream, xfrac, 1.0, *[x.data_ptr() for x in mouts])
+                ms, md, msh, mn = mouts
+            else:
+                p0.execute_part(st.cuda_stream, xfrac, 1.0, gs[0].data_ptr(), gd[0].data_ptr(), None,
+                                gn[0].data_ptr())
+                ms, md, msh, mn = merge_on_device(gs, gd, gn, nq, K, st.cuda_stream)
+        elif merged_sel:  # the rank's units merged by the plan's own final select
             plans[0].execute_merged(st.cuda_stream, *[x.data_ptr() for x in mouts])
             ms, md, msh, mn = mouts
         else:
@@ -821,8 +908,9 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     el = time.perf_counter() - t1
     el_rank = el
     kms = [p.kernel_ms() for p in plans]
-    kern = sum(m[0][0] for m in kms) / max(kms[0][1], 1)
-    fin = sum(m[0][1] for m in kms) / max(kms[0][1], 1)
+    n_ex = max(kms[0][1] // (2 if xfrac else 1), 1)  # executes per plan (two parts each when exchanging)
+    kern = sum(m[0][0] for m in kms) / n_ex
+    fin = sum(m[0][1] for m in kms) / n_ex
     if world > 1:
         t = torch.tensor([el, kern], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -838,7 +926,7 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     # this rank's roofline: its units replayed (fg_model_batch) at the merged
     # k-th score of the whole job (c4: also k_conj's exhaustive cascade)
     kname = "k_conj" if c4 else "k_disj"
-    my_ms = sum(m[0][0] for m in kms) / max(kms[0][1], 1)
+    my_ms = sum(m[0][0] for m in kms) / n_ex
     thr = final_thresholds(ms, mn, K)
     key = workload_key(kname, N, nq, K, 3 if c4 else "2-5 OR", f"c4 {per}ns" if c4 else f"c5 s=1.1 {per} shards")
     if c4:
@@ -883,6 +971,11 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
             "result_sha1": h.hexdigest()[:16],
             "hits": int(mn.sum()),
             **({"kth_floor": floor_info} if floor_info else {}),
+            **({"hist_exchange": {"frac": xfrac, "all_reduce_bytes_per_rank": 4 * nq * native.HIST_BINS,
+                                  "note": "each rank's k_disj sweep in two parts ([0, frac), [frac, 1)); between "
+                                          "them ONE all-reduce sums the ranks' per-query score histograms "
+                                          "(shard.exchange_hist), so the second part prunes with every shard's "
+                                          "first-part counts"}} if xfrac else {}),
             "snapshot_build_s_rank0": round(build_s, 1),
             "cpu_baseline": None,
             "note": "strong scaling of one fixed corpus; roofline = rank 0's units (per_rank: every rank's); the "

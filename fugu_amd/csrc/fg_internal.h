@@ -426,7 +426,10 @@ constexpr uint32_t kPackTerms = 256;            // k_score / k_bucket: term ids 
 
 // kernels.hip entry points (host-callable launchers)
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
-hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
+// k_disj over the items [first, first + count) of the plan's k_disj range (in
+// sweep order: the first part of every query's doc range first)
+hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s, uint32_t first = 0,
+                       uint32_t count = 0xFFFFFFFFu);
 hipError_t launch_fmask(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 // out_shard != nullptr: the merged select of a multi-snapshot plan (one list per batch query)

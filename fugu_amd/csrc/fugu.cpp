@@ -2661,6 +2661,9 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // doc of another snapshot tied with the k-th score is never pruned (the merge
   // breaks such ties by snapshot)
   p->d.pub_mask = S > 1 ? 0xFFFFFFFF00000000ull : ~0ull;
+  p->h_any.assign(nq1, 0);
+  for (uint32_t v = 0; v < nq; ++v)
+    if (ngroup[v]) p->h_any[v % nq1] = 1;
   p->h_lo.swap(q_hlo);
   p->h_hi.swap(q_hhi);
   p->d.f.n_filters = nf;
@@ -2669,23 +2672,33 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   return FG_OK;
 }
 
-// the kernels of a planned batch on stream s; out_shard != nullptr: a
-// multi-snapshot plan's merged select (one list per batch query)
-static int execute_impl(fg_plan* p, hipStream_t s, float* os, uint32_t* od, uint32_t* on, uint32_t* oshard) {
+// the kernels of a planned batch on stream s, or of one part of it: the k_disj
+// items [from, to) of its sweep (fractions of the k_disj range, in sweep order:
+// every query's first docs first).  The first part (from = 0) zeroes the plan's
+// state and runs k_fmask + k_conj, the last (to = 1) k_scan + k_final;
+// out_shard != nullptr: a multi-snapshot plan's merged select
+static int execute_impl(fg_plan* p, hipStream_t s, float* os, uint32_t* od, uint32_t* on, uint32_t* oshard,
+                        double from = 0.0, double to = 1.0) {
   HIPCHK(hipSetDevice(p->ix->dev));
-  if (p->zeroed) p->zeroed = false;  // the first execute after the upload
-  else HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
+  const bool first = from <= 0.0, last = to >= 1.0;
+  if (first) {
+    if (p->zeroed) p->zeroed = false;  // the first execute after the upload
+    else HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
+  }
   hipEvent_t ev[3] = {};
   if (p->profile) {
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventRecord(ev[0], s));
   }
-  if (p->d.f.n_chunks) HIPCHK(fg::launch_fmask(p->ix->d, p->d, s));
-  if (p->d.n_conj) HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
-  if (p->d.total_chunks > p->d.n_conj) HIPCHK(fg::launch_disj(p->ix->d, p->d, s));
-  if (p->d.n_scan) HIPCHK(fg::launch_scan(p->ix->d, p->d, s));
+  if (first && p->d.f.n_chunks) HIPCHK(fg::launch_fmask(p->ix->d, p->d, s));
+  if (first && p->d.n_conj) HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
+  const uint32_t nd = p->d.total_chunks - p->d.n_conj;
+  const uint32_t a = first ? 0u : (uint32_t)std::min<double>(nd, std::llround(from * nd));
+  const uint32_t b = last ? nd : (uint32_t)std::min<double>(nd, std::llround(to * nd));
+  if (b > a) HIPCHK(fg::launch_disj(p->ix->d, p->d, s, a, b - a));
+  if (last && p->d.n_scan) HIPCHK(fg::launch_scan(p->ix->d, p->d, s));
   if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
-  HIPCHK(fg::launch_final(p->d, os, od, on, s, oshard));
+  if (last) HIPCHK(fg::launch_final(p->d, os, od, on, s, oshard));
   if (p->profile) {
     HIPCHK(hipEventRecord(ev[2], s));
     p->pending.insert(p->pending.end(), ev, ev + 3);
@@ -2710,6 +2723,72 @@ int fg_plan_execute_merged(fg_plan* p, void* stream, float* d_out_score, uint32_
   if (p->n_segs < 2 || !p->d.seg_base)
     return fail(FG_EUNSUPPORTED, "not a multi-snapshot plan over < 2^32 docs (use fg_plan_execute + fg_merge_shards)");
   return execute_impl(p, static_cast<hipStream_t>(stream), d_out_score, d_out_doc, d_out_n, d_out_shard);
+}
+
+// One part of a plan's k_disj sweep (fugu.h): doc-sharded namespaces over
+// several devices or processes exchange their per-query score histograms
+// between the parts, so every shard's later items prune with the counts of all
+// shards' earlier ones (what linked plans share through memory on one device)
+int fg_plan_execute_part(fg_plan* p, void* stream, double from, double to, float* d_out_score, uint32_t* d_out_doc,
+                         uint32_t* d_out_shard, uint32_t* d_out_n) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  if (!(from >= 0.0 && from < to && to <= 1.0)) return fail(FG_EINVAL, "part [%g, %g) not inside [0, 1)", from, to);
+  if (d_out_shard && (p->n_segs < 2 || !p->d.seg_base))
+    return fail(FG_EUNSUPPORTED, "merged select: not a multi-snapshot plan over < 2^32 docs");
+  if (d_out_shard && (!d_out_score || !d_out_doc || !d_out_n)) return fail(FG_EINVAL, "merged select needs every output");
+  return execute_impl(p, static_cast<hipStream_t>(stream), d_out_score ? d_out_score : p->own_score,
+                      d_out_doc ? d_out_doc : p->own_doc, d_out_n ? d_out_n : p->own_n, d_out_shard, from, to);
+}
+
+static_assert(fg::kQBins == FG_HIST_BINS, "fugu.h's histogram size");
+
+int fg_plan_hist_span(const fg_plan* p, uint32_t* lo, uint32_t* hi) {
+  if (!p || !lo || !hi) return fail(FG_EINVAL, "bad arguments");
+  const uint32_t nb = p->nq_batch;
+  for (uint32_t i = 0; i < nb; ++i) {
+    const bool any = i < p->h_any.size() && p->h_any[i];
+    lo[i] = any ? p->h_lo[i] : 0u;
+    hi[i] = any ? p->h_hi[i] : 0u;
+  }
+  return FG_OK;
+}
+
+int fg_plan_set_hist_span(fg_plan* p, const uint32_t* lo, const uint32_t* hi) {
+  if (!p || !lo || !hi) return fail(FG_EINVAL, "bad arguments");
+  const uint32_t nb = p->nq_batch, S = p->n_segs;
+  if (p->h_lo.size() < (size_t)nb * S || p->h_hi.size() < (size_t)nb * S)
+    return fail(FG_EUNSUPPORTED, "a linked plan's bins are redrawn by fg_plan_link");
+  std::vector<uint32_t> L(p->nq), SH(p->nq);
+  for (uint32_t s = 0; s < S; ++s)
+    for (uint32_t i = 0; i < nb; ++i) {
+      const size_t v = (size_t)s * nb + i;
+      uint32_t l = lo[i], h = std::max(hi[i], lo[i]);
+      if (l == 0 && h == 0) {  // no shard has work for the query: keep the plan's own bins
+        l = p->h_lo[v];
+        h = p->h_hi[v];
+      }
+      p->h_lo[v] = l;
+      p->h_hi[v] = h;
+      L[v] = l;
+      SH[v] = bin_shift(l, h);
+    }
+  HIPCHK(hipSetDevice(p->ix->dev));
+  if (p->pin) HIPCHK(hipStreamSynchronize(p->up_stream));  // an upload still in flight would overwrite them
+  if (p->nq) {
+    HIPCHK(hipMemcpy(const_cast<uint32_t*>(p->d.q_hlo), L.data(), 4ull * p->nq, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(const_cast<uint32_t*>(p->d.q_hsh), SH.data(), 4ull * p->nq, hipMemcpyHostToDevice));
+  }
+  return FG_OK;
+}
+
+int fg_plan_hist_copy(fg_plan* p, void* stream, uint32_t* d_buf, int into_plan) {
+  if (!p || !d_buf) return fail(FG_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(p->ix->dev));
+  const size_t bytes = 4ull * p->nq_batch * fg::kQBins;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (into_plan) HIPCHK(hipMemcpyAsync(p->d.hist, d_buf, bytes, hipMemcpyDeviceToDevice, s));
+  else HIPCHK(hipMemcpyAsync(d_buf, p->d.hist, bytes, hipMemcpyDeviceToDevice, s));
+  return FG_OK;
 }
 
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n) {
@@ -2826,6 +2905,7 @@ int fg_plan_link(fg_plan* const* plans, uint32_t n) {
       HIPCHK(hipMemcpy(const_cast<uint32_t*>(p->d.q_hsh), sh.data(), 4ull * nq, hipMemcpyHostToDevice));
     }
     p->h_lo = lo;
+    for (uint32_t q = 0; q < nq; ++q) p->h_hi[q] = std::max(p->h_hi[q], lo[q]);
     p->d.thresh = o->d.thresh;
     p->d.hist = o->d.hist;
     p->d.pub_mask = 0xFFFFFFFF00000000ull;  // score-only

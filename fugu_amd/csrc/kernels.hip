@@ -2036,10 +2036,16 @@ hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
-  if (pl.total_chunks <= pl.n_conj) return hipSuccess;
-  if (pl.segs) k_disj<true><<<pl.total_chunks - pl.n_conj, kThreads, 0, s>>>(ix, pl);
-  else k_disj<false><<<pl.total_chunks - pl.n_conj, kThreads, 0, s>>>(ix, pl);
+hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s, uint32_t first, uint32_t count) {
+  const uint32_t n = pl.total_chunks > pl.n_conj ? pl.total_chunks - pl.n_conj : 0u;
+  if (first >= n) return hipSuccess;
+  count = min(count, n - first);
+  if (!count) return hipSuccess;
+  // a part of the sweep: the kernel's items start at pl.n_conj
+  DevPlan part = pl;
+  part.n_conj = pl.n_conj + first;
+  if (pl.segs) k_disj<true><<<count, kThreads, 0, s>>>(ix, part);
+  else k_disj<false><<<count, kThreads, 0, s>>>(ix, part);
   return hipGetLastError();
 }
 

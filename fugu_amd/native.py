@@ -50,6 +50,7 @@ EXPORTS = (
     "fg_thread_background",
     "fg_index_stats_get", "fg_index_df", "fg_index_bm25",
     "fg_plan_create", "fg_plan_execute", "fg_plan_results", "fg_plan_info_get",
+    "fg_plan_execute_part", "fg_plan_hist_span", "fg_plan_set_hist_span", "fg_plan_hist_copy",
     "fg_plan_profile", "fg_plan_kernel_ms", "fg_plan_diag", "fg_plan_destroy",
     "fg_search_batch", "fg_search_sharded", "fg_merge_shards", "fg_bytes_model", "fg_bytes_model_gpu",
     "fg_docs_stats", "fg_index_build_from_docs_global", "fg_docs_facet_stats", "fg_index_rescore",
@@ -59,6 +60,7 @@ EXPORTS = (
 )
 LADDER_KS = (1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000)  # FG_LADDER_LEVELS ranks
 KTH_KS = (1, 10, 20, 100, 1000)  # fg_index_term_kth / fg_index_set_kth_floor ranks
+HIST_BINS = 512  # fugu.h FG_HIST_BINS: score-histogram bins per query
 ABI_VERSION = 4  # include/fugu.h FG_ABI_VERSION this binding's structs follow
 
 if not os.path.exists(LIB_PATH):
@@ -159,6 +161,10 @@ _sig("fg_kth_floor_combine", C.c_int, C.c_uint32, C.c_uint32, C.POINTER(_f32p), 
 _sig("fg_index_set_kth_floor", C.c_int, _p, _f32p, C.c_uint32)
 _sig("fg_plan_execute", C.c_int, _p, _p, _p, _p, _p)
 _sig("fg_plan_results", C.c_int, _p, _f32p, _u32p, _u32p)
+_sig("fg_plan_hist_span", C.c_int, _p, _u32p, _u32p)
+_sig("fg_plan_set_hist_span", C.c_int, _p, _u32p, _u32p)
+_sig("fg_plan_execute_part", C.c_int, _p, _p, C.c_double, C.c_double, _p, _p, _p, _p)
+_sig("fg_plan_hist_copy", C.c_int, _p, _p, _p, C.c_int)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
 _sig("fg_plan_profile", C.c_int, _p, C.c_int)
 _sig("fg_plan_kernel_ms", C.c_int, _p, _f64p, _u32p)
@@ -586,6 +592,30 @@ class Plan:
         """A multi-snapshot plan straight to the merged top-k per batch query
         (device outputs [n_batch*k] x 3, [n_batch]; raw device addresses)."""
         _check(_lib.fg_plan_execute_merged(self._h, stream, out_score, out_doc, out_shard, out_n))
+
+    def execute_part(self, stream: int | None, frm: float, to: float, out_score: int | None = None,
+                     out_doc: int | None = None, out_shard: int | None = None, out_n: int | None = None):
+        """fg_plan_execute_part: the k_disj items [frm, to) of the sweep (to = 1:
+        the final select too, merged when out_shard is given)."""
+        _check(_lib.fg_plan_execute_part(self._h, stream, frm, to, out_score, out_doc, out_shard, out_n))
+
+    def hist_span(self):
+        """(lo, hi) u32 [n_batch]: the f32 bits each query's histogram spans (0, 0: no work)."""
+        lo = np.zeros(self.n_batch, np.uint32)
+        hi = np.zeros(self.n_batch, np.uint32)
+        _check(_lib.fg_plan_hist_span(self._h, _ptr(lo, _u32p), _ptr(hi, _u32p)))
+        return lo, hi
+
+    def set_hist_span(self, lo, hi):
+        lo = np.ascontiguousarray(lo, np.uint32)
+        hi = np.ascontiguousarray(hi, np.uint32)
+        if lo.shape != (self.n_batch,) or hi.shape != (self.n_batch,):
+            raise ValueError(f"spans of {lo.shape} / {hi.shape}, expected ({self.n_batch},)")
+        _check(_lib.fg_plan_set_hist_span(self._h, _ptr(lo, _u32p), _ptr(hi, _u32p)))
+
+    def hist_copy(self, stream: int | None, d_buf: int, into_plan: bool):
+        """Copy the histograms [n_batch, HIST_BINS] u32 to / from device memory d_buf."""
+        _check(_lib.fg_plan_hist_copy(self._h, stream, d_buf, 1 if into_plan else 0))
 
     def results(self):
         nq, k = self.n_queries, self.k

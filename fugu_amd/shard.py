@@ -123,6 +123,50 @@ def seed_kth_floor(indexes, group=None, device=None):
     return floor
 
 
+def agree_hist_span(plans, group=None, device=None):
+    """Doc shards on several ranks: give the plans of one batch the same
+    histogram bins on every rank -- the elementwise max of their spans
+    (fg_plan_hist_span) over this rank's plans, then over the ranks (one
+    all-reduce MAX of 2 x n_batch u32 when a group is up) -- so the histograms
+    can be summed bin by bin (exchange_hist).  Returns (lo, hi)."""
+    import numpy as np
+    lo = hi = None
+    for p in plans:
+        a, b = p.hist_span()
+        lo = a if lo is None else np.maximum(lo, a)
+        hi = b if hi is None else np.maximum(hi, b)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        t = torch.from_numpy(np.concatenate([lo, hi]).astype(np.int64))
+        if device is not None:
+            t = t.to(device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        t = t.cpu().numpy().astype(np.uint32)
+        lo, hi = t[:len(lo)], t[len(lo):]
+    for p in plans:
+        p.set_hist_span(lo, hi)
+    return lo, hi
+
+
+def exchange_hist(plan, stream: int, buf: torch.Tensor, group=None):
+    """Between two parts of a plan's k_disj sweep (fg_plan_execute_part): sum the
+    per-query score histograms of every rank's shards into this plan's, ONE
+    all-reduce of [n_batch * HIST_BINS] int32 (RCCL over xGMI with "nccl"; gloo
+    through host memory).  `buf` is an int32 device tensor of that size, and
+    `stream` torch's current stream of the plan's device (the copies and the
+    collective are ordered on it).  The shards' counted docs are distinct, so
+    the summed histogram's threshold is still a lower bound of the merged k-th
+    score: merged results are unchanged."""
+    plan.hist_copy(stream, buf.data_ptr(), False)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.get_backend(group) == "gloo" and buf.is_cuda:
+            h = buf.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            buf.copy_(h)
+        else:
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    plan.hist_copy(stream, buf.data_ptr(), True)
+
+
 def shard_ranges(n_docs: int, world: int):
     """Contiguous doc-id ranges [b, e) of the shards (tantivy segments)."""
     step = (n_docs + world - 1) // world

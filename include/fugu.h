@@ -302,6 +302,33 @@ int fg_plan_execute(fg_plan* p, void* stream, float* d_out_score, uint32_t* d_ou
  * execute plans[0] first in every round and the others after it on the same
  * stream (or ordered after it); destroy plans[0] last. */
 int fg_plan_link(fg_plan* const* plans, uint32_t n);
+/* ---- doc shards on several devices / processes (C5 over N GPUs) ----------
+ * Linked plans share their per-query score histograms through memory on one
+ * device.  Shards on different GPUs exchange them instead, between PARTS of the
+ * k_disj sweep: every rank runs part [0, f) of its plan, the histograms are
+ * summed over the ranks (one all-reduce of n_queries * FG_HIST_BINS u32), and
+ * part [f, 1) then prunes with the counts of every shard's first part.  The
+ * counted docs of different shards are distinct, so the summed histogram's
+ * threshold is a lower bound of the namespace's k-th score and the merged
+ * top-k is unchanged (a shard's own list may then hold fewer than k hits).
+ * Reference: tantivy's Searcher-global statistics, src/db/search.rs:162. */
+#define FG_HIST_BINS 512
+/* lo[n_queries], hi[n_queries]: the f32 bit patterns the query's histogram bins
+ * span (0, 0: no shard of this plan has work for the query).  Before the
+ * exchange every rank sets the elementwise MAX over the ranks' spans
+ * (fg_plan_set_hist_span), so a bin counts the same scores on every rank. */
+int fg_plan_hist_span(const fg_plan* p, uint32_t* lo, uint32_t* hi);
+int fg_plan_set_hist_span(fg_plan* p, const uint32_t* lo, const uint32_t* hi);
+/* Run the k_disj items [from, to) of the plan's sweep (fractions, 0 <= from <
+ * to <= 1; every query's first docs come first).  from = 0 also zeroes the
+ * plan's state and runs the facet masks and k_conj; to = 1 also runs the scans
+ * and the final select into the outputs (as fg_plan_execute; d_out_shard !=
+ * NULL: fg_plan_execute_merged's merged select).  Asynchronous. */
+int fg_plan_execute_part(fg_plan* p, void* stream, double from, double to, float* d_out_score, uint32_t* d_out_doc,
+                         uint32_t* d_out_shard, uint32_t* d_out_n);
+/* Copy the plan's histograms [n_queries][FG_HIST_BINS] u32 to (into_plan = 0)
+ * or from (1) device memory d_buf of the plan's device, on `stream`. */
+int fg_plan_hist_copy(fg_plan* p, void* stream, uint32_t* d_buf, int into_plan);
 /* Copy the plan's own result buffers to host (synchronises the plan's stream). */
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n);
 typedef struct fg_plan_info {

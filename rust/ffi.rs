@@ -32,6 +32,7 @@ pub const FG_EUNSUPPORTED: c_int = -5;  // outside the device subset: run tantiv
 pub const FG_MAX_TERMS: u32 = 16;
 pub const FG_MAX_FACET_CLAUSES: u32 = 8;
 pub const FG_MAX_K: u32 = 1024;
+pub const FG_HIST_BINS: u32 = 512;
 pub const FG_MAX_SEGMENTS: u32 = 64;
 pub const FG_TERM_MISSING: u32 = 0xFFFF_FFFF;
 pub const FG_MODE_AND: c_int = 0;
@@ -219,6 +220,11 @@ extern "C" {
     pub fn fg_plan_execute(p: *mut fg_plan, stream: *mut c_void, d_out_score: *mut f32, d_out_doc: *mut u32,
                            d_out_n: *mut u32) -> c_int;
     pub fn fg_plan_link(plans: *const *mut fg_plan, n: u32) -> c_int;
+    pub fn fg_plan_hist_span(p: *const fg_plan, lo: *mut u32, hi: *mut u32) -> c_int;
+    pub fn fg_plan_set_hist_span(p: *mut fg_plan, lo: *const u32, hi: *const u32) -> c_int;
+    pub fn fg_plan_execute_part(p: *mut fg_plan, stream: *mut c_void, from: f64, to: f64, d_out_score: *mut f32,
+                                d_out_doc: *mut u32, d_out_shard: *mut u32, d_out_n: *mut u32) -> c_int;
+    pub fn fg_plan_hist_copy(p: *mut fg_plan, stream: *mut c_void, d_buf: *mut u32, into_plan: c_int) -> c_int;
     pub fn fg_plan_results(p: *mut fg_plan, out_score: *mut f32, out_doc: *mut u32, out_n: *mut u32) -> c_int;
     pub fn fg_plan_info_get(p: *const fg_plan, out: *mut fg_plan_info) -> c_int;
     pub fn fg_plan_profile(p: *mut fg_plan, enable: c_int) -> c_int;

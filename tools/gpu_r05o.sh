@@ -1,0 +1,7 @@
+set -o pipefail
+# re-entry check of HEAD: the whole GPU suite, then the driver's default bench
+O=gpurun_out/r05o; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+head -c 3000 $O/bench.json
