@@ -556,8 +556,13 @@ def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps):
 def alone_exchanged_ms(ixs, q_off, terms, K, mode, st, reps, frac):
     """Every shard's plan ALONE as in alone_kernel_ms, its k_disj sweep in two
     parts with the shards' score histograms summed between them (what
-    shard.exchange_hist's all-reduce does across N GPUs): each shard's kernel ms
-    over both parts, the exchange's device time here, and the merged hash."""
+    shard.exchange_hist's all-reduce does across N GPUs).  One round of every
+    shard's first part gives the summed histogram; then each shard runs its
+    rounds back to back (as its own GPU would: part 1, the summed histogram in,
+    part 2), so its timing sees the caches its GPU would.  Returns each shard's
+    kernel ms over both parts, the exchange's device time on one GPU, the merged
+    hash.  (Any earlier round's counts are valid: counted docs are distinct docs
+    of their shards, so the summed threshold stays a lower bound of the k-th.)"""
     from fugu_amd import native
     from fugu_amd.shard import agree_hist_span, merge_on_device
     import torch
@@ -571,38 +576,36 @@ def alone_exchanged_ms(ixs, q_off, terms, K, mode, st, reps, frac):
     gn = torch.empty((S, nq), dtype=torch.int32, device=dev)
     hb = torch.zeros((S, nq * native.HIST_BINS), dtype=torch.int32, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    xch = []
-
-    def run():
-        for p in plans:
-            p.execute_part(st, 0.0, frac)
-        ev[0].record()
-        for r, p in enumerate(plans):
-            p.hist_copy(st, hb[r].data_ptr(), False)
-        tot = hb.sum(0, dtype=torch.int32)
-        for p in plans:
-            p.hist_copy(st, tot.data_ptr(), True)
-        ev[1].record()
-        for r, p in enumerate(plans):
-            p.execute_part(st, frac, 1.0, gs[r].data_ptr(), gd[r].data_ptr(), None, gn[r].data_ptr())
-        return tot
-
-    run()
-    torch.cuda.synchronize()
     for p in plans:
-        p.profile(True)
-    for _ in range(reps):
+        p.execute_part(st, 0.0, frac)
+    ev[0].record()
+    for r, p in enumerate(plans):
+        p.hist_copy(st, hb[r].data_ptr(), False)
+    tot = hb.sum(0, dtype=torch.int32)
+    for p in plans:
+        p.hist_copy(st, tot.data_ptr(), True)
+    ev[1].record()
+    torch.cuda.synchronize()
+    xch = ev[0].elapsed_time(ev[1])
+    ms = []
+    for r, p in enumerate(plans):
+        def run():
+            p.execute_part(st, 0.0, frac)
+            p.hist_copy(st, tot.data_ptr(), True)
+            p.execute_part(st, frac, 1.0, gs[r].data_ptr(), gd[r].data_ptr(), None, gn[r].data_ptr())
         run()
         torch.cuda.synchronize()
-        xch.append(ev[0].elapsed_time(ev[1]))
-    ms = []
-    for p in plans:
+        p.profile(True)
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize()
         m, n = p.kernel_ms()
         ms.append((round(m[0] / max(n // 2, 1), 4), round(m[1] / max(n // 2, 1), 4)))
+    for p in plans:
         p.close()
     out = merge_on_device(gs, gd, gn, nq, K, st)
     torch.cuda.synchronize()
-    return ms, round(float(np.median(xch)), 4), hits_sha1(out[0], out[1], out[2], out[3], K)
+    return ms, round(float(xch), 4), hits_sha1(out[0], out[1], out[2], out[3], K)
 
 
 def hits_sha1(s, d, sh, n, K):

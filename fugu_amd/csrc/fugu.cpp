@@ -187,11 +187,49 @@ void DevCache::unregister_cache() {
   auto& v = caches();
   v.erase(std::remove(v.begin(), v.end(), this), v.end());
 }
+// Stream-ordered allocations (hipMallocAsync: scoring scratch, rescore
+// weights) keep their memory in the device's default pool instead of returning
+// it at every synchronisation (release threshold: no limit).  A hipMallocAsync
+// that maps fresh memory held up a search kernel on another stream for ~1 ms
+// (4 MiB) to ~8.6 ms (256 MiB); with the pool kept, 0.04 ms
+// (tools/stall_probe.hip, profiles/r05/stall/probe_r05q.json).  The pools are
+// trimmed with the other caches when an allocation fails.
+std::mutex& pool_mu() {
+  static std::mutex m;
+  return m;
+}
+std::vector<int>& kept_pools() {
+  static std::vector<int> v;
+  return v;
+}
+void keep_async_pool(int dev) {
+  std::lock_guard<std::mutex> l(pool_mu());
+  auto& v = kept_pools();
+  if (std::find(v.begin(), v.end(), dev) != v.end()) return;
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
+    uint64_t thr = ~0ull;
+    if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) != hipSuccess) (void)hipGetLastError();
+  } else {
+    (void)hipGetLastError();
+  }
+  v.push_back(dev);
+}
 void drop_all_cached() {
   int dev = 0;
   (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> l(cache_mu());
-  for (DevCache* c : caches()) c->drop_cached();
+  {
+    std::lock_guard<std::mutex> l(cache_mu());
+    for (DevCache* c : caches()) c->drop_cached();
+  }
+  {
+    std::lock_guard<std::mutex> l(pool_mu());
+    for (int d : kept_pools()) {
+      hipMemPool_t pool = nullptr;
+      if (hipDeviceGetDefaultMemPool(&pool, d) == hipSuccess && pool) (void)hipMemPoolTrimTo(pool, 0);
+      (void)hipGetLastError();
+    }
+  }
   (void)hipSetDevice(dev);
 }
 void device_pools(int dev, std::shared_ptr<WsPool>* ws, std::shared_ptr<PinnedPool>* pin) {
@@ -224,6 +262,8 @@ hipError_t dev_malloc(void** p, size_t bytes) {
   return e;
 }
 hipError_t dev_malloc_async(void** p, size_t bytes, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) keep_async_pool(dev);
   if (hipMallocAsync(p, bytes, s) == hipSuccess) return hipSuccess;
   (void)hipGetLastError();
   drop_all_cached();
@@ -307,12 +347,14 @@ static hipStream_t search_stream(int dev) {
 }
 
 // The background streams of a device (a db's rescores, segment builds and
-// merges), created once: restricted by a CU mask to FUGU_BG_CU_FRAC of the
-// device's CUs (default kBgCuFrac; the CUs left out spread evenly over the
-// XCDs), so the searches running beside a commit always find CUs free -- the
-// slow searches during commits sat behind the commits' scoring kernels
-// (tools/stall_trace.py) -- or, at FUGU_BG_CU_FRAC=1, low-priority streams
-constexpr double kBgCuFrac = 0.75;
+// merges), created once: low-priority streams (the searches' own are high
+// priority), or at FUGU_BG_CU_FRAC < 1 streams restricted by a CU mask to that
+// fraction of the CUs (the CUs left out spread evenly over the XCDs).  The mask
+// is not honoured on this platform: a background kernel of 8 workgroups per CU
+// took as long on a 3/4 mask as on all CUs and held a search up just as long
+// (tools/stall_probe.hip, profiles/r05/stall/probe_r05p.json), so the default
+// is the priority alone
+constexpr double kBgCuFrac = 1.0;
 hipStream_t background_stream(int dev, uint32_t i) {
   static std::mutex mu;
   static std::map<int, std::vector<hipStream_t>> streams;
@@ -1762,7 +1804,7 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
   void* d_w = nullptr;
   if (one_dev && n > 1) {
     HIPCHK(hipSetDevice(bases[0]->dev));
-    if (hipMallocAsync(&d_w, 8ull * V, kBuildStream) == hipSuccess) {
+    if (fgh::dev_malloc_async(&d_w, 8ull * V, kBuildStream) == hipSuccess) {
       const hipError_t e1 = hipMemcpyAsync(d_w, wts.wt.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream);
       const hipError_t e2 = hipMemcpyAsync(static_cast<float*>(d_w) + V, wts.wn.data(), 4ull * V, hipMemcpyHostToDevice,
                                            kBuildStream);
@@ -2129,6 +2171,14 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   const uint32_t gpq_batch =
       fg::kGroupsPerQuery * std::min<uint32_t>(fg::kDisjSmallSpread, std::max<uint32_t>(1, 256 / std::max(nq, 1u)));
   const uint32_t gpq = std::max<uint32_t>(1, gpq_batch / n_segs);
+  // k_conj items per query per snapshot of a multi-snapshot plan: the single-
+  // snapshot count / n_segs, so a query keeps ~the single-snapshot item count
+  // over all its slots (C4, 8 x 1.25M namespaces: k_conj 1.300 -> 1.085 ms, /16
+  // 1.065 ms, identical hits: profiles/r05/ab/c4_ab_r05q.json; round 4 measured
+  // the opposite before the sparse rank words and the XCD split);
+  // FUGU_CONJ_SEG_DIV overrides the divisor (1: per-snapshot counts)
+  const char* cde = getenv("FUGU_CONJ_SEG_DIV");
+  const uint32_t cdiv = n_segs <= 1 ? 1u : cde && *cde ? (uint32_t)std::max(1, atoi(cde)) : n_segs;
   auto &citems = h.citems, &ditems = h.ditems, &scan = h.scan;
   auto &ngroup = h.ngroup, &q_hlo = h.q_hlo, &q_hhi = h.q_hhi, &q_hsh = h.q_hsh;
   ngroup.assign(nq, 0);
@@ -2298,9 +2348,9 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     // batch of one: the p50 latency) spreads a query over up to 64 items so its
     // chunks run side by side instead of up to kMaxGroup in a row, while its
     // k_final still reads at most 64 x k candidates
-    // (not divided over a multi-snapshot plan's snapshots: fewer, longer k_conj
-    // items per snapshot measured slower, multi_ab AND 1.45 -> 1.52 ms)
-    const uint32_t per_q = std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u)));
+    // (a multi-snapshot plan: divided by cdiv, above)
+    const uint32_t per_q =
+        std::max<uint32_t>(1, std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u))) / cdiv);
     const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + per_q - 1) / per_q));
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;
@@ -2441,6 +2491,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
       const uint32_t* qt = q_terms.data() + (size_t)qv * fg::kMaxTerms;
       const uint32_t mt = fg::qm_terms(q_m[qv]);
       if (key == 'q') return 0x80000000u | qv;
+      if (key == 's') return 0x40000000u | (qv / nq1);  // the slot's snapshot (a multi-snapshot plan)
       if (key == '0' || mt == 1) return qt[0];
       if (key == '2') return qt[mt - 1];
       return qt[1];

@@ -58,6 +58,18 @@ __global__ __launch_bounds__(256) void k_stream(const uint32_t* __restrict__ a, 
   if (s == 0x12345678u) out[blockIdx.x] = s;
 }
 
+// background: short workgroups, each one u32 per thread of one 1024-u32 slice per rep
+__global__ __launch_bounds__(256) void k_short(const uint32_t* __restrict__ a, size_t n, int reps, uint32_t* out) {
+  uint32_t s = 0;
+  const size_t base = (size_t)blockIdx.x * 1024;
+  for (int r = 0; r < reps; ++r)
+    for (int j = 0; j < 4; ++j) {
+      const size_t i = base + j * 256 + threadIdx.x;
+      if (i < n) s += a[i] ^ r;
+    }
+  if (s == 0x12345678u) out[blockIdx.x & 1023] = s;
+}
+
 // background: few long-lived workgroups (one per "term", like k_ktop on a
 // long list), each spinning `us` microseconds on the 100 MHz clock with
 // `lds` bytes of LDS held
@@ -143,6 +155,35 @@ int main(int argc, char** argv) {
           // ~5 ms of HBM streaming per launch, 4 launches queued
           for (int i = 0; i < 4; ++i) k_stream<<<4096, 256, 0, s>>>(d_bg, n_bg, 5, d_bg_out);
           CK(hipStreamSynchronize(s));
+        } else if (ph == "short" || ph == "short_lowprio") {
+          hipStream_t s = ph == "short" ? bs : bs_lo;
+          // the same ~5 ms of streaming per launch as "stream", in 1M short workgroups
+          for (int i = 0; i < 4; ++i) k_short<<<(unsigned)(n_bg / 1024), 256, 0, s>>>(d_bg, n_bg, 5, d_bg_out);
+          CK(hipStreamSynchronize(s));
+        } else if (ph == "long_half" || ph == "long_half_lowprio") {
+          hipStream_t s = ph == "long_half" ? bs : bs_lo;
+          // 4 workgroups per CU (half the wave slots), each 5 ms
+          k_long<0><<<4 * n_cu, 256, 0, s>>>(ticks_5ms, d_bg_out);
+          CK(hipStreamSynchronize(s));
+        } else if (ph == "spin_short_lowprio") {
+          // 100 us workgroups, 16 per CU queued per launch round, low priority
+          k_long<0><<<64 * n_cu, 256, 0, bs_lo>>>(10000, d_bg_out);
+          CK(hipStreamSynchronize(bs_lo));
+        } else if (ph == "malloc_async_keep" || ph == "malloc_async_small") {
+          static bool once = false;
+          if (!once && ph == "malloc_async_keep") {
+            hipMemPool_t pool;
+            CK(hipDeviceGetDefaultMemPool(&pool, 0));
+            uint64_t thr = ~0ull;
+            CK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr));
+            once = true;
+          }
+          const size_t b = ph == "malloc_async_small" ? (4u << 20) : (256u << 20);
+          void* p;
+          CK(hipMallocAsync(&p, b, bs));
+          k_stream<<<64, 256, 0, bs>>>((const uint32_t*)p, b / 4 < (1u << 20) ? b / 4 : (1u << 20), 1, d_bg_out);
+          CK(hipFreeAsync(p, bs));
+          CK(hipStreamSynchronize(bs));
         } else if (ph == "long" || ph == "long_masked") {
           hipStream_t s = ph == "long" ? bs : bs_mask;
           // 8 workgroups per CU, each 5 ms
