@@ -87,11 +87,13 @@ def roofline(kname, kernel_ms, model, key, alg_model, pruned=None):
 
 
 NO_MODEL = False  # --no-model: profiling passes skip the host replays
-# C5 over N GPUs: the fraction of each rank's k_disj sweep run before the ranks'
-# score histograms are summed (shard.exchange_hist; FUGU_C5_XFRAC=0: none), and
-# the split points the one-GPU rehearsal reports
-C5_XFRAC = float(os.environ.get("FUGU_C5_XFRAC", "0.125"))
-C5_EXCHANGE_FRACS = (0.0625, 0.125, 0.25)
+# C5 over N GPUs, opt-in: the fraction of each rank's k_disj sweep run before the
+# ranks' score histograms are summed (shard.exchange_hist).  Default 0 (none):
+# the sweep's first items are its longest (no threshold yet), so a launch split
+# after 1/16 / 1/4 / 1/2 of them idles the GPU through their tail -- one shard
+# 5.96 ms whole, 8.08 / 7.52 / 7.04 ms in two parts with the summed histogram
+# (tools/c5_parts.py, profiles/r05/ab/c5_parts_r05r.json)
+C5_XFRAC = float(os.environ.get("FUGU_C5_XFRAC", "0"))
 
 
 def model_sum(ixs, q_off, terms, k, thr, mode):
@@ -553,61 +555,6 @@ def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps):
     return ms, hits_sha1(out[0], out[1], out[2], out[3], K)
 
 
-def alone_exchanged_ms(ixs, q_off, terms, K, mode, st, reps, frac):
-    """Every shard's plan ALONE as in alone_kernel_ms, its k_disj sweep in two
-    parts with the shards' score histograms summed between them (what
-    shard.exchange_hist's all-reduce does across N GPUs).  One round of every
-    shard's first part gives the summed histogram; then each shard runs its
-    rounds back to back (as its own GPU would: part 1, the summed histogram in,
-    part 2), so its timing sees the caches its GPU would.  Returns each shard's
-    kernel ms over both parts, the exchange's device time on one GPU, the merged
-    hash.  (Any earlier round's counts are valid: counted docs are distinct docs
-    of their shards, so the summed threshold stays a lower bound of the k-th.)"""
-    from fugu_amd import native
-    from fugu_amd.shard import agree_hist_span, merge_on_device
-    import torch
-    nq = len(q_off) - 1
-    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
-    plans = [ix.plan(q_off, terms, K, mode) for ix in ixs]
-    agree_hist_span(plans)
-    S = len(plans)
-    gs = torch.empty((S, nq * K), dtype=torch.float32, device=dev)
-    gd = torch.empty((S, nq * K), dtype=torch.int32, device=dev)
-    gn = torch.empty((S, nq), dtype=torch.int32, device=dev)
-    hb = torch.zeros((S, nq * native.HIST_BINS), dtype=torch.int32, device=dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    for p in plans:
-        p.execute_part(st, 0.0, frac)
-    ev[0].record()
-    for r, p in enumerate(plans):
-        p.hist_copy(st, hb[r].data_ptr(), False)
-    tot = hb.sum(0, dtype=torch.int32)
-    for p in plans:
-        p.hist_copy(st, tot.data_ptr(), True)
-    ev[1].record()
-    torch.cuda.synchronize()
-    xch = ev[0].elapsed_time(ev[1])
-    ms = []
-    for r, p in enumerate(plans):
-        def run():
-            p.execute_part(st, 0.0, frac)
-            p.hist_copy(st, tot.data_ptr(), True)
-            p.execute_part(st, frac, 1.0, gs[r].data_ptr(), gd[r].data_ptr(), None, gn[r].data_ptr())
-        run()
-        torch.cuda.synchronize()
-        p.profile(True)
-        for _ in range(reps):
-            run()
-        torch.cuda.synchronize()
-        m, n = p.kernel_ms()
-        ms.append((round(m[0] / max(n // 2, 1), 4), round(m[1] / max(n // 2, 1), 4)))
-    for p in plans:
-        p.close()
-    out = merge_on_device(gs, gd, gn, nq, K, st)
-    torch.cuda.synchronize()
-    return ms, round(float(xch), 4), hits_sha1(out[0], out[1], out[2], out[3], K)
-
-
 def hits_sha1(s, d, sh, n, K):
     """sha1 (16 hex) of merged (score, doc, shard) lists, each query's first n entries."""
     import hashlib
@@ -674,17 +621,6 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     alone_se, sha_se = alone_kernel_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2))
     log(f"[bench] C5 shards alone: unseeded max {max(x[0] for x in alone_un)} ms, seeded max "
         f"{max(x[0] for x in alone_se)} ms (linked mean {np.mean(per_shard):.3f}); floor in {seed_s:.1f}s")
-    # ... and with the histograms exchanged once mid-sweep (the N-GPU step's
-    # all-reduce, shard.exchange_hist), at a few split points
-    exch = {}
-    for f in C5_EXCHANGE_FRACS:
-        ex_ms, ex_dev, ex_sha = alone_exchanged_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2), f)
-        mx = max(x[0] for x in ex_ms)
-        exch[str(f)] = {"k_disj_ms": [x[0] for x in ex_ms], "max": mx, "k_final_ms": [x[1] for x in ex_ms],
-                        "max_over_linked_mean": round(mx / float(np.mean(per_shard)), 3),
-                        "exchange_device_ms_8_shards_one_gpu": ex_dev, "result_sha1": ex_sha}
-        log(f"[bench] C5 shards alone, histograms exchanged at {f}: max {mx} ms ({exch[str(f)]['max_over_linked_mean']}"
-            f" x linked mean), sha {ex_sha}")
     # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel),
     # planned with the floor; beside it the same plan without the floor
     outs = tuple(torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)) + (
@@ -732,7 +668,6 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
                "seeded_max_over_linked_mean": round(max(x[0] for x in alone_se) / float(np.mean(per_shard)), 3),
                "result_sha1_unseeded": sha_un, "result_sha1_seeded": sha_se, "same_hits": sha_un == sha_se,
                "floor_s": round(seed_s, 2),
-               "seeded_hist_exchanged": exch,
                "note": "each shard's plan alone (no shared threshold word: one GPU of the 8-GPU split); seeded = "
                        "its starting thresholds floored by the namespace-wide per-term K-th score bounds "
                        "(fg_index_term_ladder of every shard, one all-gather at build, fg_kth_floor_combine)"},

@@ -2177,6 +2177,11 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   // 1.065 ms, identical hits: profiles/r05/ab/c4_ab_r05q.json; round 4 measured
   // the opposite before the sparse rank words and the XCD split);
   // FUGU_CONJ_SEG_DIV overrides the divisor (1: per-snapshot counts)
+  // FUGU_CONJ_GPQ / FUGU_CONJ_MAXGROUP (A/B): kConjGroupsPerQuery / kMaxGroup
+  const char* gqe = getenv("FUGU_CONJ_GPQ");
+  const uint32_t conj_gpq = gqe && *gqe ? (uint32_t)std::max(1, atoi(gqe)) : fg::kConjGroupsPerQuery;
+  const char* mge = getenv("FUGU_CONJ_MAXGROUP");
+  const uint32_t conj_maxg = mge && *mge ? (uint32_t)std::max(1, atoi(mge)) : fg::kMaxGroup;
   const char* cde = getenv("FUGU_CONJ_SEG_DIV");
   const uint32_t cdiv = n_segs <= 1 ? 1u : cde && *cde ? (uint32_t)std::max(1, atoi(cde)) : n_segs;
   auto &citems = h.citems, &ditems = h.ditems, &scan = h.scan;
@@ -2350,8 +2355,8 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     // k_final still reads at most 64 x k candidates
     // (a multi-snapshot plan: divided by cdiv, above)
     const uint32_t per_q =
-        std::max<uint32_t>(1, std::min<uint32_t>(64, std::max<uint32_t>(fg::kConjGroupsPerQuery, 1024 / std::max(nq, 1u))) / cdiv);
-    const uint32_t G = std::min<uint32_t>(fg::kMaxGroup, std::max<uint32_t>(1, (nch + per_q - 1) / per_q));
+        std::max<uint32_t>(1, std::min<uint32_t>(64, std::max<uint32_t>(conj_gpq, 1024 / std::max(nq, 1u))) / cdiv);
+    const uint32_t G = std::min<uint32_t>(conj_maxg, std::max<uint32_t>(1, (nch + per_q - 1) / per_q));
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;
     for (uint32_t g = 0; g < ng; ++g)

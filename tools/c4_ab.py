@@ -1,5 +1,5 @@
-"""A/B of PLAN-time knobs (environment read at fg_plan_create_multi) on bench.py's
-C4 shape: the 10M corpus as 8 namespaces x 1.25M (own statistics each), one
+"""A/B of PLAN-time knobs (environment read at fg_plan_create[_multi]) on bench.py's
+C4 shape (--units 1: the headline's one 10M snapshot instead): the 10M corpus as 8 namespaces x 1.25M (own statistics each), one
 multi-snapshot plan per variant over the same 1024 3-term AND top-100 batch,
 run interleaved round by round with the merged select; per variant the median
 k_conj and k_final ms and the merged-hit hash (every variant must match).
@@ -54,21 +54,28 @@ def main():
         os.environ.clear()
         os.environ.update(base_env)
         os.environ.update(env)
-        plans[name] = native.Plan(ixs, q_off, terms, K, args.mode)
+        plans[name] = native.Plan(ixs if len(ixs) > 1 else ixs[0], q_off, terms, K, args.mode)
     os.environ.clear()
     os.environ.update(base_env)
     outs = [torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)]
     outs.append(torch.empty(nq, dtype=torch.int32, device=dev))
+    multi = len(ixs) > 1
+
+    def run(p):  # a multi-snapshot plan: its merged select; one snapshot: its own lists (shard column unused)
+        if multi:
+            p.execute_merged(st, *[x.data_ptr() for x in outs])
+        else:
+            p.execute(st, outs[0].data_ptr(), outs[1].data_ptr(), outs[3].data_ptr())
     times = {n: [] for n in plans}
     sha = {}
     for r in range(args.rounds):
         for n, p in plans.items():
-            p.execute_merged(st, *[x.data_ptr() for x in outs])
+            run(p)
             torch.cuda.synchronize()
             p.kernel_ms()
             p.profile(True)
             for _ in range(args.steps):
-                p.execute_merged(st, *[x.data_ptr() for x in outs])
+                run(p)
             torch.cuda.synchronize()
             m, c = p.kernel_ms()
             p.profile(False)
@@ -76,7 +83,7 @@ def main():
             if r == 0:
                 h = hashlib.sha1()
                 mn = outs[3].cpu().numpy()
-                a = [x.cpu().numpy().reshape(nq, K) for x in outs[:3]]
+                a = [x.cpu().numpy().reshape(nq, K) for x in (outs[:3] if multi else outs[:2])]
                 for i in range(nq):
                     for x in a:
                         h.update(x[i, :mn[i]].tobytes())
