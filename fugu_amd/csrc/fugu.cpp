@@ -2295,6 +2295,9 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       // ab_disj_heavy_k*.log)
       const uint32_t G = std::min<uint32_t>(std::min(fg::kDisjMaxGroup, fg::kDisjMaxPairs / ns),
                                             std::max<uint32_t>(1, (nt + gpq - 1) / gpq));
+      // (shorter first items -- G >> r, G >> (r-1), ... tiles -- so the items that
+      // start with no threshold publish one early: r = 2 / 3 / 5 / 8 slower at
+      // k = 1000 and 20, +0.4% to +7%: profiles/r05/ab/disj_ramp_r05t.log)
       const uint32_t ng = (nt + G - 1) / G;
       ngroup[i] = ng;
       for (uint32_t g = 0; g < ng; ++g) {

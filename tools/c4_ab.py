@@ -29,13 +29,14 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--terms", default="3,3")
     ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--s", type=float, default=1.0, help="corpus Zipf exponent (C5: 1.1)")
     args = ap.parse_args()
     import torch
 
     from fugu_amd import native, synth
     from fugu_amd.shard import shard_ranges
     ctx = native.Context((0,))
-    corp = synth.corpus(args.docs, synth.VOCAB, 1.0, threads=16)
+    corp = synth.corpus(args.docs, synth.VOCAB, args.s, threads=16)
     ixs = []
     for b, e in shard_ranges(corp.n_docs, args.units):
         off = corp.off[b:e + 1] - corp.off[b]

@@ -1,0 +1,2 @@
+set -o pipefail
+bash tools/gpu_r05t.sh && bash tools/gpu_r05s.sh

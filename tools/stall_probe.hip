@@ -120,6 +120,12 @@ int main(int argc, char** argv) {
   for (int c = 0; c < n_cu; ++c)
     if ((uint64_t)(c + 1) * off / n_cu == (uint64_t)c * off / n_cu) mask[c / 32] |= 1u << (c % 32);
   CK(hipExtStreamCreateWithCUMask(&bs_mask, (uint32_t)mask.size(), mask.data()));
+  // several background streams at once (a commit rescores 8 segments side by side)
+  hipStream_t bs8[8], bs8_lo[8];
+  for (int i = 0; i < 8; ++i) {
+    CK(hipStreamCreateWithFlags(&bs8[i], hipStreamNonBlocking));
+    CK(hipStreamCreateWithPriority(&bs8_lo[i], hipStreamNonBlocking, least));
+  }
 
   const size_t n_search = 8u << 20;  // 32 MiB
   const size_t n_bg = 1u << 30;      // 4 GiB
@@ -160,6 +166,14 @@ int main(int argc, char** argv) {
           // the same ~5 ms of streaming per launch as "stream", in 1M short workgroups
           for (int i = 0; i < 4; ++i) k_short<<<(unsigned)(n_bg / 1024), 256, 0, s>>>(d_bg, n_bg, 5, d_bg_out);
           CK(hipStreamSynchronize(s));
+        } else if (ph == "short8" || ph == "short8_lowprio" || ph == "short2_lowprio" || ph == "short4_lowprio") {
+          // short-workgroup kernels on several streams at once, 1/N of the work each
+          const int N = ph == "short2_lowprio" ? 2 : ph == "short4_lowprio" ? 4 : 8;
+          hipStream_t* v = ph == "short8" ? bs8 : bs8_lo;
+          for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < N; ++j)
+              k_short<<<(unsigned)(n_bg / 1024 / N), 256, 0, v[j]>>>(d_bg + j * (n_bg / N), n_bg / N, 5, d_bg_out);
+          for (int j = 0; j < N; ++j) CK(hipStreamSynchronize(v[j]));
         } else if (ph == "long_half" || ph == "long_half_lowprio") {
           hipStream_t s = ph == "long_half" ? bs : bs_lo;
           // 4 workgroups per CU (half the wave slots), each 5 ms
