@@ -358,7 +358,11 @@ constexpr double kBgCuFrac = 1.0;
 hipStream_t background_stream(int dev, uint32_t i) {
   static std::mutex mu;
   static std::map<int, std::vector<hipStream_t>> streams;
-  constexpr uint32_t kN = 8;
+  // FUGU_BG_STREAMS (A/B, default 8): how many background streams a device has
+  static const uint32_t kN = [] {
+    const char* e = getenv("FUGU_BG_STREAMS");
+    return e && *e ? (uint32_t)std::min(64, std::max(1, atoi(e))) : 8u;
+  }();
   std::lock_guard<std::mutex> l(mu);
   auto& v = streams[dev];
   if (v.empty()) {
