@@ -403,6 +403,7 @@ struct ScoreJob {
   const uint32_t* bk_e0;
   const uint32_t* bk_e1;
   uint32_t n_terms;
+  uint32_t grid_cap;          // at most this many workgroups per scoring launch (0: one per item)
   uint64_t n_dir;             // directory entries (dir_off of term n_terms)
   const uint32_t* kt_tiny;    // k_ktop_tiny: terms with 1..kKtopTiny postings (one wave each)
   uint32_t n_tiny;
@@ -442,6 +443,7 @@ hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s);  // packed chunks
 hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s);                        // after k_bucket
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s);
+hipError_t launch_copy32(uint32_t* dst, const uint32_t* src, uint64_t n, uint32_t grid_cap, hipStream_t s);
 hipError_t launch_merge(uint32_t n_shards, uint32_t n_queries, uint32_t k, const float* score, const uint32_t* doc,
                         const uint32_t* n, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n,
                         hipStream_t s);

@@ -322,6 +322,27 @@ hipStream_t build_stream() {
 }
 #define kBuildStream build_stream()
 
+// The workgroup cap of a background scoring's launches (fg::ScoreJob::grid_cap):
+// FUGU_BG_GRID workgroups per CU (default kBgGridPerCu; 0: no cap) when the
+// calling thread works in the background (fg_thread_background, or a rescore
+// worker on a background stream), so a commit's scoring kernels leave most wave
+// slots to the searches running beside it; 0 for a foreground build
+constexpr uint32_t kBgGridPerCu = 2;
+uint32_t bg_grid_cap(int dev) {
+  if (!tl_background && !tl_build_stream) return 0;
+  static const uint32_t per_cu = [] {
+    const char* e = getenv("FUGU_BG_GRID");
+    return e && *e ? (uint32_t)std::max(0, atoi(e)) : kBgGridPerCu;
+  }();
+  if (!per_cu) return 0;
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return per_cu * (uint32_t)n_cu;
+}
+
 // The calling thread's high-priority stream on device `dev` (the search path's
 // own: its kernels are dispatched ahead of a commit's rescores and builds on the
 // same GPU), created on first use and kept for the thread's life;
@@ -663,6 +684,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.kt_tiny = ix->d_kt_tiny;
   j.n_tiny = ix->n_ktiny;
   j.coff = ix->d.coff;
+  j.grid_cap = bg_grid_cap(ix->dev);
   // FUGU_DIAG_SCORE_SKIP (stall diagnosis only; the snapshot is then WRONG): bit 0
   // skips the k_ktop pass, bit 1 the tables' read-back, bit 2 k_score / k_bucket / k_tsub
   static const int diag_skip = [] {
@@ -694,8 +716,16 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       h = ix->hown.data();
     }
     if (!(diag_skip & 2)) {
-      HIPCHK(hipMemcpyAsync(h, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
-      HIPCHK(hipMemcpyAsync(h + V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
+      if (j.grid_cap && ix->sblock.hp) {
+        // a background scoring: the read-back as a capped copy kernel (pinned host
+        // memory is device-visible), not a copy-engine transfer
+        HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h), d_tmaxs, V, j.grid_cap, kBuildStream));
+        HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h + V), reinterpret_cast<const uint32_t*>(d_ktop),
+                                 (uint64_t)V * fg::kNumTopK, j.grid_cap, kBuildStream));
+      } else {
+        HIPCHK(hipMemcpyAsync(h, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
+        HIPCHK(hipMemcpyAsync(h + V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
+      }
     }
     HIPCHK(hipStreamSynchronize(kBuildStream));
     ix->tmaxs = h;

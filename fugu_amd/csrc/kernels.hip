@@ -2186,13 +2186,20 @@ __device__ inline uint32_t slot_of(const Off* s_off, uint32_t nterm, uint64_t p)
   return lo;
 }
 
-__global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
+// The scoring kernels take their logical workgroup count n and loop over it in
+// steps of gridDim.x: a background scoring (a commit's rescores) launches at most
+// ScoreJob::grid_cap workgroups, so a search beside it finds wave slots free
+// (launch_* below; tools/stall_probe.hip: a background kernel filling every slot
+// held a search up for its whole span, one filling half of them did not).
+__global__ __launch_bounds__(kThreads) void k_score(ScoreJob j, uint32_t n) {
   __shared__ float cache[512];
   __shared__ uint64_t s_off[kPackTerms + 1];
   __shared__ uint32_t s_max[kPackTerms];
-  const uint32_t c = blockIdx.x, tf = j.sc_tf[c], nterm = j.sc_tl[c] - tf + 1;
-  const uint64_t e0 = j.sc_e0[c], e1 = j.sc_e1[c];
   for (uint32_t i = threadIdx.x; i < 512; i += kThreads) cache[i] = j.cache[i];
+  for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+  __syncthreads();  // the previous chunk's LDS reads are done
+  const uint32_t tf = j.sc_tf[c], nterm = j.sc_tl[c] - tf + 1;
+  const uint64_t e0 = j.sc_e0[c], e1 = j.sc_e1[c];
   for (uint32_t i = threadIdx.x; i <= nterm; i += kThreads) s_off[i] = j.off[tf + i];
   for (uint32_t i = threadIdx.x; i < nterm; i += kThreads) s_max[i] = 0u;
   __syncthreads();
@@ -2238,15 +2245,18 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j) {
     const uint64_t first = e0 > b ? e0 : b;
     j.cmax[j.coff[t] + (uint32_t)((first - b) / kChunk)] = __uint_as_float(s_max[i]);
   }
+  }
 }
 
 // Bucket maxima (-0.0: empty bucket, a score may be +0.0), the term maxima and
 // the 4096-doc tile maxima (terms whose buckets are no wider than a tile).
 // Scores are >= 0, so their f32 bits order like the values (atomicMax on u32).
-__global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs) {
+__global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs, uint32_t n) {
   __shared__ uint32_t s_doff[kPackTerms + 1];
   __shared__ uint32_t s_max[kPackTerms];
-  const uint32_t c = blockIdx.x, tf = j.bk_tf[c], nterm = j.bk_tl[c] - tf + 1;
+  for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+  __syncthreads();  // the previous chunk's LDS reads are done
+  const uint32_t tf = j.bk_tf[c], nterm = j.bk_tl[c] - tf + 1;
   const uint32_t e0 = j.bk_e0[c], e1 = j.bk_e1[c];
   for (uint32_t i = threadIdx.x; i <= nterm; i += kThreads)
     s_doff[i] = tf + i < j.n_terms ? j.dir_off[tf + i] : (uint32_t)j.n_dir;
@@ -2290,6 +2300,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
   // the term maxima (a long term spans chunks: atomics)
   for (uint32_t i = threadIdx.x; i < nterm; i += kThreads)
     if (s_max[i]) atomicMax(&j.tmaxs[tf + i], s_max[i]);
+  }
 }
 
 // Sub-tile maxima (DevIndex::tsub): one thread per tile entry walks
@@ -2299,12 +2310,12 @@ __global__ __launch_bounds__(kThreads) void k_bucket(ScoreJob j, uint32_t n_docs
 static_assert(kDisjTileShift - kSubShift == 3, "8 sub-tile blocks per tile: one byte each of a u64");
 __global__ __launch_bounds__(kThreads) void k_tsub(ScoreJob j, uint32_t n_docs) {
   const uint32_t nt1 = j.n_tiles + 1;
-  const uint64_t e = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (e >= (uint64_t)j.n_tterm * nt1) return;
+  const uint64_t n_e = (uint64_t)j.n_tterm * nt1;
+  for (uint64_t e = (uint64_t)blockIdx.x * kThreads + threadIdx.x; e < n_e; e += (uint64_t)gridDim.x * kThreads) {
   const uint32_t k = (uint32_t)(e / nt1), tile = (uint32_t)(e - (uint64_t)k * nt1);
   if (tile >= j.n_tiles) {  // the entry past a term's last tile (tdir's end): never read as a tile
     j.tsub[e] = ~0ull;
-    return;
+    continue;
   }
   const uint32_t t = j.tterm[k];
   const uint32_t B = j.tmeta[t] & 0xFFu;  // <= kDisjTileShift for a tile-table term
@@ -2328,6 +2339,7 @@ __global__ __launch_bounds__(kThreads) void k_tsub(ScoreJob j, uint32_t n_docs) 
 #pragma unroll
   for (uint32_t z = 0; z < 8; ++z) w |= (uint64_t)quant8(mx[z], M) << (8 * z);
   j.tsub[e] = w;
+  }
 }
 
 // Per term the K-th best score over its ALIVE postings for K in kTopKs (0 when
@@ -2435,9 +2447,9 @@ __device__ inline void ktop_reduce(const ScoreJob& j, uint64_t b, uint32_t p0, u
 // terms of <= kKtopTiny postings: one wave per term (four per workgroup), the
 // alive keys sorted descending by a wave bitonic network (lane i: the i-th best)
 __global__ __launch_bounds__(kThreads) void k_ktop_tiny(ScoreJob j) {
-  const uint32_t lane = threadIdx.x & 63, x = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (x >= j.n_tiny) return;  // wave-uniform
-  const uint32_t t = j.kt_tiny[x];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t x = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); x < j.n_tiny; x += gridDim.x * (kThreads / 64)) {
+  const uint32_t t = j.kt_tiny[x];  // (a wave per term: the loop is wave-uniform)
   const uint64_t b = j.off[t];
   const uint32_t n = (uint32_t)(j.off[t + 1] - b);
   uint64_t key = 0;
@@ -2446,7 +2458,7 @@ __global__ __launch_bounds__(kThreads) void k_ktop_tiny(ScoreJob j) {
     if (!j.alive || ((j.alive[d >> 5] >> (d & 31u)) & 1u)) key = make_key(j.psc[b + lane], d);
   }
   const uint32_t na = (uint32_t)__popcll(__ballot(key != 0));
-  if (na == 0) return;
+  if (na == 0) continue;
   for (uint32_t k = 2; k <= 64; k <<= 1)
     for (uint32_t h = k >> 1; h > 0; h >>= 1) {
       const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)key, (int)h, 64);
@@ -2463,28 +2475,34 @@ __global__ __launch_bounds__(kThreads) void k_ktop_tiny(ScoreJob j) {
     for (uint32_t kk = 0; kk < kNumLadderExtra; ++kk)
       if (kLadderExtra[kk] <= na && lane == kLadderExtra[kk] - 1)
         j.ladder[(size_t)t * kNumLadderExtra + kk] = key_score(key);
+  }
 }
 
 // one workgroup per term of <= kKtopChunk postings
-__global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j) {
+__global__ __launch_bounds__(kThreads) void k_ktop(ScoreJob j, uint32_t n) {
   __shared__ KtopShared sh;
-  const uint32_t t = j.kt_terms[blockIdx.x];
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+  __syncthreads();  // the previous term's LDS reads are done
+  const uint32_t t = j.kt_terms[w];
   const uint64_t b = j.off[t];
-  const uint32_t n = (uint32_t)(j.off[t + 1] - b);
-  ktop_reduce(j, b, 0, n, sh);
+  const uint32_t np = (uint32_t)(j.off[t + 1] - b);
+  ktop_reduce(j, b, 0, np, sh);
   const uint32_t na = sh.red[0];
   if (threadIdx.x == 0 && na) j.ktop[(size_t)t * kNumTopK] = __uint_as_float(sh.red[2]);  // K = 1: the maximum
   ktop_finish(j, t, na, sh, [&](auto&& f) {
-    ktop_each_posting(j, b, 0, n, [&](bool ok, float sv, uint32_t d) { f(ok, make_key(sv, d)); });
+    ktop_each_posting(j, b, 0, np, [&](bool ok, float sv, uint32_t d) { f(ok, make_key(sv, d)); });
   });
+  }
 }
 
 // one workgroup per kKtopChunk-posting chunk of a long term: the chunk's alive
 // count and extremes (atomics into the term's slots) and its KM best keys
-__global__ __launch_bounds__(kThreads) void k_ktop_part(ScoreJob j) {
+__global__ __launch_bounds__(kThreads) void k_ktop_part(ScoreJob j, uint32_t n_chunks) {
   __shared__ KtopShared sh;
   constexpr uint32_t KM = kKtopKM;
-  const uint32_t c = blockIdx.x, bt = j.kc_big[c];
+  for (uint32_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+  __syncthreads();  // the previous chunk's LDS reads are done
+  const uint32_t bt = j.kc_big[c];
   const uint32_t t = j.kb_terms[bt];
   const uint64_t b = j.off[t];
   const uint32_t n = (uint32_t)(j.off[t + 1] - b);
@@ -2511,13 +2529,16 @@ __global__ __launch_bounds__(kThreads) void k_ktop_part(ScoreJob j) {
   uint64_t* out = j.kc_keys + (size_t)c * KM;
   for (uint32_t i = threadIdx.x; i < nt; i += kThreads) out[i] = sh.top[i];
   if (threadIdx.x == 0) j.kc_cnt[c] = nt;
+  }
 }
 
 // one workgroup per long term: its K-th best scores over its chunks' best keys
 __global__ __launch_bounds__(kThreads) void k_ktop_big(ScoreJob j) {
   __shared__ KtopShared sh;
   constexpr uint32_t KM = kKtopKM;
-  const uint32_t bt = blockIdx.x, t = j.kb_terms[bt];
+  for (uint32_t bt = blockIdx.x; bt < j.n_big; bt += gridDim.x) {
+  __syncthreads();  // the previous term's LDS reads are done
+  const uint32_t t = j.kb_terms[bt];
   const uint32_t na = j.kb_stat[bt], mx = j.kb_stat[2 * j.n_big + bt];
   if (threadIdx.x == 0) {
     sh.n_top = 0;
@@ -2535,17 +2556,24 @@ __global__ __launch_bounds__(kThreads) void k_ktop_big(ScoreJob j) {
       }
     }
   });
+  }
+}
+
+// a background scoring's grid: at most j.grid_cap workgroups (0: one per item)
+static inline uint32_t capped(const ScoreJob& j, uint64_t n) {
+  const uint64_t g = j.grid_cap && n > j.grid_cap ? j.grid_cap : n;
+  return (uint32_t)(g < 0x7FFFFFFFull ? g : 0x7FFFFFFFull);
 }
 
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s) {
   if (!n_chunks) return hipSuccess;
-  k_score<<<n_chunks, kThreads, 0, s>>>(j);
+  k_score<<<capped(j, n_chunks), kThreads, 0, s>>>(j, n_chunks);
   return hipGetLastError();
 }
 
 hipError_t launch_bucket(const ScoreJob& j, uint32_t n_chunks, uint32_t n_docs, hipStream_t s) {
   if (!n_chunks) return hipSuccess;
-  k_bucket<<<n_chunks, kThreads, 0, s>>>(j, n_docs);
+  k_bucket<<<capped(j, n_chunks), kThreads, 0, s>>>(j, n_docs, n_chunks);
   return hipGetLastError();
 }
 
@@ -2553,27 +2581,45 @@ hipError_t launch_tsub(const ScoreJob& j, uint32_t n_docs, hipStream_t s) {
   const uint64_t n = (uint64_t)j.n_tterm * (j.n_tiles + 1);
   if (!n || !j.tsub) return hipSuccess;
   if ((n + kThreads - 1) / kThreads > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  k_tsub<<<(uint32_t)((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(j, n_docs);
+  k_tsub<<<capped(j, (n + kThreads - 1) / kThreads), kThreads, 0, s>>>(j, n_docs);
   return hipGetLastError();
 }
 
 hipError_t launch_ktop(const ScoreJob& j, uint32_t n_terms, uint32_t n_chunks, uint32_t n_big, hipStream_t s) {
   if (j.n_tiny) {
-    k_ktop_tiny<<<(j.n_tiny + kThreads / 64 - 1) / (kThreads / 64), kThreads, 0, s>>>(j);
+    k_ktop_tiny<<<capped(j, (j.n_tiny + kThreads / 64 - 1) / (kThreads / 64)), kThreads, 0, s>>>(j);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   if (n_terms) {
-    k_ktop<<<n_terms, kThreads, 0, s>>>(j);
+    k_ktop<<<capped(j, n_terms), kThreads, 0, s>>>(j, n_terms);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   if (n_chunks) {
-    k_ktop_part<<<n_chunks, kThreads, 0, s>>>(j);
+    k_ktop_part<<<capped(j, n_chunks), kThreads, 0, s>>>(j, n_chunks);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (n_big) k_ktop_big<<<n_big, kThreads, 0, s>>>(j);
+  if (n_big) k_ktop_big<<<capped(j, n_big), kThreads, 0, s>>>(j);
+  return hipGetLastError();
+}
+
+// n u32 from src to dst in steps of the grid: a background scoring's read-back
+// into pinned host memory as a capped kernel on its low-priority stream instead
+// of a copy-engine transfer (the read-backs of a rescore held searches up:
+// tools/rescore_stall.py)
+__global__ __launch_bounds__(kThreads) void k_copy32(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                    uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kThreads)
+    dst[i] = src[i];
+}
+
+hipError_t launch_copy32(uint32_t* dst, const uint32_t* src, uint64_t n, uint32_t grid_cap, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t want = (n + kThreads - 1) / kThreads;
+  const uint64_t g = grid_cap && want > grid_cap ? grid_cap : want;
+  k_copy32<<<(uint32_t)(g < 0x7FFFFFFFull ? g : 0x7FFFFFFFull), kThreads, 0, s>>>(dst, src, n);
   return hipGetLastError();
 }
 

@@ -49,3 +49,39 @@ def test_term_kth_equals_single_term_topk(native, with_deletes):
         got = ix.term_kth(t)
         want = np.array([s[i, k - 1] if n[i] >= k else 0.0 for k in KS], np.float32)
         assert np.array_equal(got, want), (t, ix.df(t), int(n[i]), got.tolist(), want.tolist())
+
+
+def test_background_capped_scoring_identical(native):
+    """A commit's scorings run in the background with at most FUGU_BG_GRID
+    workgroups per CU per launch (fg::ScoreJob::grid_cap: every scoring kernel
+    loops over its items in steps of the grid) and read the per-term tables back
+    through a copy kernel.  The rescored snapshot must equal the foreground
+    (uncapped) one: per-term K-th scores and maxima bit for bit, and every
+    search's hits."""
+    from fugu_amd import synth
+    ctx = native.Context((0,))
+    c = synth.corpus(600_000)
+    g = native.docs_stats(c.off, c.tok, synth.VOCAB, threads=16)
+    ix = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, global_stats=g)
+    rng = np.random.default_rng(3)
+    deleted = (rng.random(c.n_docs) < 0.05).astype(np.uint8)
+    fg = ix.rescore(g, deleted)
+    prev = native._lib.fg_thread_background(1)
+    try:
+        bg = ix.rescore(g, deleted)
+    finally:
+        native._lib.fg_thread_background(prev)
+    terms = [t for t in range(0, 300_000, 97) if ix.df(t) > 0]
+    assert len(terms) > 1000
+    for t in terms:
+        assert np.array_equal(fg.term_kth(t), bg.term_kth(t)), t
+    q_off, qt = synth.queries(256, 1, 4, seed_q=21)
+    for mode, k in ((native.MODE_OR, 20), (native.MODE_OR, 1000), (native.MODE_AND, 100)):
+        a = fg.search_batch(q_off, qt, k, mode=mode)
+        b = bg.search_batch(q_off, qt, k, mode=mode)
+        assert np.array_equal(a[2], b[2])
+        for i in range(len(a[2])):
+            m = int(a[2][i])
+            assert np.array_equal(a[0][i, :m], b[0][i, :m]) and np.array_equal(a[1][i, :m], b[1][i, :m])
+    for x in (fg, bg, ix):
+        x.close()
