@@ -322,14 +322,18 @@ hipStream_t build_stream() {
 }
 #define kBuildStream build_stream()
 
+// Does the calling thread work in the background (fg_thread_background, or a
+// rescore worker on a background stream)?
+bool on_background() { return tl_background || tl_build_stream; }
 // The workgroup cap of a background scoring's launches (fg::ScoreJob::grid_cap):
-// FUGU_BG_GRID workgroups per CU (default kBgGridPerCu; 0: no cap) when the
-// calling thread works in the background (fg_thread_background, or a rescore
-// worker on a background stream), so a commit's scoring kernels leave most wave
-// slots to the searches running beside it; 0 for a foreground build
-constexpr uint32_t kBgGridPerCu = 2;
+// FUGU_BG_GRID workgroups per CU (default kBgGridPerCu; 0: no cap).  Measured
+// (profiles/r05/stall/): at 2 per CU the searches beside rescores alone drop from
+// max 24 to 3.4 ms, but beside whole commits p99 rises (0.89 -> 1.49 ms: the
+// capped kernels run longer and hold their slots for their whole span), so the
+// default is no cap
+constexpr uint32_t kBgGridPerCu = 0;
 uint32_t bg_grid_cap(int dev) {
-  if (!tl_background && !tl_build_stream) return 0;
+  if (!on_background()) return 0;
   static const uint32_t per_cu = [] {
     const char* e = getenv("FUGU_BG_GRID");
     return e && *e ? (uint32_t)std::max(0, atoi(e)) : kBgGridPerCu;
@@ -716,9 +720,12 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       h = ix->hown.data();
     }
     if (!(diag_skip & 2)) {
-      if (j.grid_cap && ix->sblock.hp) {
-        // a background scoring: the read-back as a capped copy kernel (pinned host
-        // memory is device-visible), not a copy-engine transfer
+      if (on_background() && ix->sblock.hp) {
+        // a background scoring: the read-back as a copy kernel of short workgroups
+        // on its low-priority stream (pinned host memory is device-visible), not a
+        // copy-engine transfer: the copy-engine read-backs of a rescore's eight
+        // segments held searches up (tools/rescore_stall.py, bit 1 of
+        // FUGU_DIAG_SCORE_SKIP: max 18 -> 6 ms)
         HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h), d_tmaxs, V, j.grid_cap, kBuildStream));
         HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h + V), reinterpret_cast<const uint32_t*>(d_ktop),
                                  (uint64_t)V * fg::kNumTopK, j.grid_cap, kBuildStream));
