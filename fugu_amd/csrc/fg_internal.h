@@ -63,11 +63,14 @@ constexpr uint32_t kGroupsPerQuery = FG_DISJ_GPQ;  // k_disj / k_scan: a query's
 #endif
 constexpr uint32_t kDisjSmallSpread = FG_DISJ_SPREAD;  // ... times up to this for a small batch (batch of one: x16)
 #ifndef FG_GPQ
-#define FG_GPQ 16  // tools/ab_variants.py (ab_group*.log): 64 -> 16 with FG_MAXGROUP 16 -> 8: k_conj 1.08 -> 1.00 ms
+// tools/ab_variants.py (ab_group*.log, round 2): 64 -> 16 with FG_MAXGROUP 16 -> 8: k_conj 1.08 -> 1.00 ms;
+// round 5 (after the XCD split and the sparse rank words), 16 -> 8 with FG_MAXGROUP 8 -> 16: headline
+// k_conj + k_final 1.043 -> 1.032 ms, C3 1.112 -> 1.075 ms, identical hits (profiles/r05/ab/conj_group_r05ab.log)
+#define FG_GPQ 8
 #endif
 constexpr uint32_t kConjGroupsPerQuery = FG_GPQ;  // k_conj: a query's lead chunks in ~this many work items
 #ifndef FG_MAXGROUP
-#define FG_MAXGROUP 8
+#define FG_MAXGROUP 16
 #endif
 constexpr uint32_t kMaxGroup = FG_MAXGROUP;  // ... of at most this many chunks each
 #ifndef FG_HIST_BITS
