@@ -11,3 +11,5 @@ timeout -k 10 500 python -u tools/c5_bench.py --steps 5 > $O/c5.json 2> $O/c5.er
 grep "\[bench\] C5" $O/c5.err
 FUGU_DIST_BACKEND=gloo timeout -k 10 500 python -u bench.py --gpus 2 --config c5 --steps 5 --warmup 2 > $O/c5_n2_gloo.json 2> $O/c5_n2_gloo.err || { tail -30 $O/c5_n2_gloo.err; exit 1; }
 head -c 1500 $O/c5_n2_gloo.json
+timeout -k 10 400 python -u tools/c4_ab.py --rounds 7 base: snap:FUGU_XCD_KEY=s div2:FUGU_CONJ_SEG_DIV=2 div8:FUGU_CONJ_SEG_DIV=8 snapdiv2:FUGU_XCD_KEY=s,FUGU_CONJ_SEG_DIV=2 nopart:FUGU_XCD_PART=0 > $O/c4_ab.json 2> $O/c4_ab.err || { tail -30 $O/c4_ab.err; exit 1; }
+grep "\[ab\]" $O/c4_ab.err

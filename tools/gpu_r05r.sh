@@ -11,3 +11,5 @@ import json; d=json.load(open('$O/db_api.json')); a=d['db_api_default_search']; 
 print('idle', a['p50_ms'], a['p99_ms'], 'during', {k: a['during_commits'][k] for k in ('p50_ms','p99_ms','max_ms','searches','p99_over_idle_p99','slowest_1pct_phases_ms_mean')}, 'commit', c['p50_ms'], c['p99_ms'])"
 timeout -k 10 400 python -u tools/c5_parts.py > $O/c5_parts.json 2> $O/c5_parts.err || { tail -30 $O/c5_parts.err; exit 1; }
 grep "\[parts\]" $O/c5_parts.err
+timeout -k 10 400 python -u tools/c4_ab.py --units 1 --rounds 7 base: gpq8:FUGU_CONJ_GPQ=8 gpq32:FUGU_CONJ_GPQ=32 maxg16:FUGU_CONJ_MAXGROUP=16 gpq8maxg16:FUGU_CONJ_GPQ=8,FUGU_CONJ_MAXGROUP=16 gpq4maxg32:FUGU_CONJ_GPQ=4,FUGU_CONJ_MAXGROUP=32 > $O/and3_ab.json 2> $O/and3_ab.err || { tail -30 $O/and3_ab.err; exit 1; }
+grep "\[ab\]" $O/and3_ab.err
