@@ -960,8 +960,8 @@ def main():
     ap.add_argument("--extra-steps", type=int, default=5)
     ap.add_argument("--no-c5", action="store_true", help="skip the 100M-doc C5 secondary line")
     ap.add_argument("--e2e-workers", type=int, default=4,
-                    help="batches in flight in the end-to-end line (tools/e2e_workers.py with the radix planner: "
-                         "1 -> 697K, 2 -> 816K, 4 -> 934K, 8 -> 868K q/s)")
+                    help="batches in flight in the end-to-end line (tools/e2e_workers.py, 96 batches: 2 -> 800-943K, "
+                         "4 -> 991K-1.035M, 6 -> 1.035-1.055M, 8 -> 1.03M q/s)")
     ap.add_argument("--disj", action="store_true",
                     help="headline batch = 2-5-term OR (k_disj; profiling runs, pass --k 1000 --no-cpu)")
     ap.add_argument("--overlap", action="store_true",
@@ -1294,7 +1294,9 @@ def main():
 
     # ---- end-to-end batches, then the fan-out configs C4 and C5 on this one GPU
     if rank == 0 and world == 1 and not args.no_extra:
-        extra["e2e_pipelined"] = e2e_pipeline(ix, native, synth, torch, dev, nq, K, 24, args.e2e_workers)
+        # 96 batches: the steady state (24 measured mostly the 4 workers' ramp-up and drain: 770K vs ~1.0M
+        # q/s on the same box, profiles/r05/ab/e2e_workers_r05ad.json)
+        extra["e2e_pipelined"] = e2e_pipeline(ix, native, synth, torch, dev, nq, K, 96, args.e2e_workers)
         log(f"[bench] e2e pipelined: {extra['e2e_pipelined']['value']} q/s")
     if rank == 0 and world == 1 and not args.no_extra:
         extra["db_api_default_search_10M_8seg"], extra["commit_10M"] = bench_db_api(ctx, corp, native, synth, ref,

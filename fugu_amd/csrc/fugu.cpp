@@ -689,23 +689,17 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.n_tiny = ix->n_ktiny;
   j.coff = ix->d.coff;
   j.grid_cap = bg_grid_cap(ix->dev);
-  // FUGU_DIAG_SCORE_SKIP (stall diagnosis only; the snapshot is then WRONG): bit 0
-  // skips the k_ktop pass, bit 1 the tables' read-back, bit 2 k_score / k_bucket / k_tsub
-  static const int diag_skip = [] {
-    const char* e = getenv("FUGU_DIAG_SCORE_SKIP");
-    return e && *e ? atoi(e) : 0;
-  }();
-  if (!(diag_skip & 4)) {
-    HIPCHK(fg::launch_score(j, ix->n_scb, kBuildStream));
-    HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
-  }
+  // (a bisect of what held searches up beside a rescore -- skipping the k_ktop
+  // pass, the tables' read-back, k_score / k_bucket / k_tsub in turn -- is in
+  // profiles/r05/stall/bisect/)
+  HIPCHK(fg::launch_score(j, ix->n_scb, kBuildStream));
+  HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
   j.tsub = d_tsub;
   j.tterm = ix->d_tterm;
   j.n_tterm = ix->n_tterm;
   j.n_tiles = ix->n_tiles;
-  if (!(diag_skip & 4)) HIPCHK(fg::launch_tsub(j, ix->n_docs, kBuildStream));
-  if (!(diag_skip & 1))
-    if (int rc = ktop_pass(ix, j)) return rc;
+  HIPCHK(fg::launch_tsub(j, ix->n_docs, kBuildStream));
+  if (int rc = ktop_pass(ix, j)) return rc;
   g_bt.mark("scoring launches");
   // tmaxs [V] then ktop [V * kNumTopK], read straight into the structure's
   // pooled pinned block (a released snapshot's, after the first rescores)
@@ -719,7 +713,7 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       ix->hown.resize((size_t)V * (1 + fg::kNumTopK));
       h = ix->hown.data();
     }
-    if (!(diag_skip & 2)) {
+    {
       if (on_background() && ix->sblock.hp) {
         // a background scoring: the read-back as a copy kernel of short workgroups
         // on its low-priority stream (pinned host memory is device-visible), not a

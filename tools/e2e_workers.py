@@ -14,6 +14,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", default="1,2,4,8")
     ap.add_argument("--docs", type=int, default=10_000_000)
+    ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--repeat", type=int, default=1)
     args = ap.parse_args()
     import torch
 
@@ -24,10 +26,12 @@ def main():
     c = synth.corpus(args.docs, threads=16)
     ix = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, keep_host=False)
     out = {}
-    for w in [int(x) for x in args.workers.split(",")]:
-        r = bench.e2e_pipeline(ix, native, synth, torch, dev, 1024, 100, 24, w)
-        out[w] = {k: r[k] for k in ("value", "ms_per_batch", "plan_ms_per_batch_p50")}
-        print(json.dumps({"workers": w, **out[w]}), flush=True)
+    for rep in range(args.repeat):
+        for w in [int(x) for x in args.workers.split(",")]:
+            r = bench.e2e_pipeline(ix, native, synth, torch, dev, 1024, 100, args.steps, w)
+            out[w] = {k: r[k] for k in ("value", "ms_per_batch", "plan_ms_per_batch_p50", "breakdown_ms_p50",
+                                        "breakdown_ms_p90")}
+            print(json.dumps({"workers": w, "steps": args.steps, "rep": rep, **out[w]}), flush=True)
 
 
 if __name__ == "__main__":
