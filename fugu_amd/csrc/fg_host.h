@@ -477,6 +477,7 @@ struct fg_plan {
   bool last_stream_used = false;
   std::vector<uint32_t> h_lo, h_hi;  // per query slot: f32 bits spanned by its score histogram (fg_plan_link)
   std::vector<uint8_t> h_any;        // per batch query: some slot has work items (fg_plan_hist_span)
+  double part_next = 0.0;            // where the next fg_plan_execute_part must start (0: a new round)
   bool zeroed = false;        // the zero region arrived zeroed with the upload: the first execute skips its memset
   void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
   size_t pin_n = 0;

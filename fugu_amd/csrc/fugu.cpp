@@ -2838,11 +2838,18 @@ int fg_plan_execute_part(fg_plan* p, void* stream, double from, double to, float
                          uint32_t* d_out_shard, uint32_t* d_out_n) {
   if (!p) return fail(FG_EINVAL, "NULL plan");
   if (!(from >= 0.0 && from < to && to <= 1.0)) return fail(FG_EINVAL, "part [%g, %g) not inside [0, 1)", from, to);
+  // parts in sweep order, each starting where the last one ended (the first
+  // zeroes the plan's state, the last runs the final select)
+  if (from > 0.0 && from != p->part_next)
+    return fail(FG_EINVAL, "part [%g, %g) does not continue the plan's sweep (next part starts at %g)", from, to,
+                p->part_next);
   if (d_out_shard && (p->n_segs < 2 || !p->d.seg_base))
     return fail(FG_EUNSUPPORTED, "merged select: not a multi-snapshot plan over < 2^32 docs");
   if (d_out_shard && (!d_out_score || !d_out_doc || !d_out_n)) return fail(FG_EINVAL, "merged select needs every output");
-  return execute_impl(p, static_cast<hipStream_t>(stream), d_out_score ? d_out_score : p->own_score,
-                      d_out_doc ? d_out_doc : p->own_doc, d_out_n ? d_out_n : p->own_n, d_out_shard, from, to);
+  const int rc = execute_impl(p, static_cast<hipStream_t>(stream), d_out_score ? d_out_score : p->own_score,
+                              d_out_doc ? d_out_doc : p->own_doc, d_out_n ? d_out_n : p->own_n, d_out_shard, from, to);
+  if (rc == FG_OK) p->part_next = to >= 1.0 ? 0.0 : to;
+  return rc;
 }
 
 static_assert(fg::kQBins == FG_HIST_BINS, "fugu.h's histogram size");

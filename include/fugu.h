@@ -323,7 +323,8 @@ int fg_plan_set_hist_span(fg_plan* p, const uint32_t* lo, const uint32_t* hi);
  * to <= 1; every query's first docs come first).  from = 0 also zeroes the
  * plan's state and runs the facet masks and k_conj; to = 1 also runs the scans
  * and the final select into the outputs (as fg_plan_execute; d_out_shard !=
- * NULL: fg_plan_execute_merged's merged select).  Asynchronous. */
+ * NULL: fg_plan_execute_merged's merged select).  Asynchronous.  Parts run in
+ * order, each from where the last ended (FG_EINVAL otherwise). */
 int fg_plan_execute_part(fg_plan* p, void* stream, double from, double to, float* d_out_score, uint32_t* d_out_doc,
                          uint32_t* d_out_shard, uint32_t* d_out_n);
 /* Copy the plan's histograms [n_queries][FG_HIST_BINS] u32 to (into_plan = 0)

@@ -209,4 +209,12 @@ def test_multi_plan_parts_equal_merged(native, shards):
     assert int(hb.sum().item()) > 0
     with pytest.raises(native.FuguError):
         mp.execute_part(st, 0.5, 0.5)
+    with pytest.raises(native.FuguError):  # parts must continue the sweep
+        mp.execute_part(st, 0.3, 1.0, *[x.data_ptr() for x in b])
+    mp.execute_part(st, 0.0, 0.5)
+    with pytest.raises(native.FuguError):
+        mp.execute_part(st, 0.6, 1.0, *[x.data_ptr() for x in b])
+    mp.execute_part(st, 0.5, 1.0, *[x.data_ptr() for x in b])
+    torch.cuda.synchronize()
+    assert np.array_equal(n, b[3].cpu().numpy())
     mp.close()
