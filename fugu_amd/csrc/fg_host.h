@@ -383,7 +383,9 @@ struct fg_index {
   uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
   float avgdl[2] = {0, 0};
   float cache[512];
-  const float* ktop = nullptr;   // [V * kNumTopK] K-th best alive score per term (kTopKs)
+  const float* ktop = nullptr;   // [V * kNumTopK] K-th best alive score per term (kTopKs), or a lower bound of it
+                                 // (a rescore without new deletions: kth_reuse_bound)
+  fgh::SharedVec<uint32_t> h_alive;  // the alive bitset this snapshot was scored with (empty: every doc)
   const float* tmaxs = nullptr;  // [V] largest posting score per term
   std::vector<float> hown;       // ktop / tmaxs when no pinned block was had (sblock.hp)
   // [V * kNumTopK] namespace-wide floor of ktop (fg_index_set_kth_floor) or null;

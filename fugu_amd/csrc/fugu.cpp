@@ -563,9 +563,45 @@ static int ktop_pass(const fg_index* ix, fg::ScoreJob& j) {
 }
 
 // wts: the weights of (Ns, df_t, df_n) for at least ix's terms, or nullptr (computed here)
+// A rescore whose alive docs are the base snapshot's (no new deletions: a commit
+// that only adds docs) need not select every term's K-th best scores again: each
+// posting's new score is at least r(t) times its old one, r(t) the smallest
+// ratio of new to old BM25 weight times tf factor over the term's fields and
+// fieldnorms, so r(t) times the old K-th best is a lower bound of the new one --
+// a valid starting threshold (kth_reuse_bound).  k_ktop was the larger part of a
+// rescore's device time and what held searches beside commits up longest
+// (profiles/r05/stall/bisect/); a segment with new deletions, a merge and a
+// build select exactly.
+static void kth_reuse_bound(const fg_index* base, const fg_index* ix, float* out) {
+  const uint32_t V = ix->n_terms;
+  double cmin[2];
+  for (int f = 0; f < 2; ++f) {  // tf / (tf + c) over tf >= 1: the new / old ratio is smallest at tf = 1 or 1
+    cmin[f] = 1.0;
+    for (int fn = 0; fn < 256; ++fn) {
+      const double q = (1.0 + base->cache[256 * f + fn]) / (1.0 + ix->cache[256 * f + fn]);
+      if (std::isfinite(q)) cmin[f] = std::min(cmin[f], q);  // (a field without tokens: no postings score in it)
+    }
+  }
+  const double margin = 1.0 - std::ldexp(1.0, -18);  // f32 rounding of the old and the new scores
+  for (uint32_t t = 0; t < V; ++t) {
+    double r = 1.0;
+    const double wo[2] = {base->w_text[t], base->w_name.size() > t ? (double)base->w_name[t] : 0.0};
+    const double wn[2] = {ix->w_text[t], ix->w_name.size() > t ? (double)ix->w_name[t] : 0.0};
+    for (int f = 0; f < (ix->has_name ? 2 : 1); ++f)  // (no `name` postings: the field adds 0 to every score)
+      if (wo[f] > 0.0) r = std::min(r, wn[f] / wo[f] * cmin[f]);
+    r = std::max(0.0, r) * margin;
+    for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
+      const size_t x = (size_t)t * fg::kNumTopK + j;
+      float v = (float)((double)base->ktop[x] * r);
+      if ((double)v > (double)base->ktop[x] * r) v = std::nextafter(v, 0.0f);
+      out[x] = v > 0.0f ? v : 0.0f;
+    }
+  }
+}
+
 int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_t* df_t, const uint32_t* df_n,
                 const std::vector<uint32_t>& alive, uint64_t tot_f, const uint32_t* df_f,
-                const fgh::Weights* wts = nullptr) {
+                const fgh::Weights* wts = nullptr, const fg_index* reuse = nullptr) {
   const uint32_t V = ix->n_terms;
   const uint64_t N = ix->n_docs;
   ix->n_stats = Ns;
@@ -586,6 +622,14 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   }
   // the weights already on this device (one upload for every snapshot of a rescore_many)
   const bool dev_w = wts && wts->d_w && wts->dev == ix->dev;
+  ix->h_alive = alive;
+  // FUGU_KTOP_REUSE=0: select exactly on every rescore (A/B)
+  static const bool reuse_on = [] {
+    const char* e = getenv("FUGU_KTOP_REUSE");
+    return !(e && *e == '0');
+  }();
+  const bool reuse_kth = reuse_on && reuse && reuse->ktop && reuse->n_terms == V && reuse->h_alive.vec() == alive &&
+                         reuse->w_text.size() >= V;
   // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
   // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
   const uint32_t VF = ix->n_fterms;
@@ -699,7 +743,8 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
   j.n_tterm = ix->n_tterm;
   j.n_tiles = ix->n_tiles;
   HIPCHK(fg::launch_tsub(j, ix->n_docs, kBuildStream));
-  if (int rc = ktop_pass(ix, j)) return rc;
+  if (!reuse_kth)
+    if (int rc = ktop_pass(ix, j)) return rc;
   g_bt.mark("scoring launches");
   // tmaxs [V] then ktop [V * kNumTopK], read straight into the structure's
   // pooled pinned block (a released snapshot's, after the first rescores)
@@ -721,12 +766,15 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
         // segments held searches up (tools/rescore_stall.py, bit 1 of
         // FUGU_DIAG_SCORE_SKIP: max 18 -> 6 ms)
         HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h), d_tmaxs, V, j.grid_cap, kBuildStream));
-        HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h + V), reinterpret_cast<const uint32_t*>(d_ktop),
-                                 (uint64_t)V * fg::kNumTopK, j.grid_cap, kBuildStream));
+        if (!reuse_kth)
+          HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h + V), reinterpret_cast<const uint32_t*>(d_ktop),
+                                   (uint64_t)V * fg::kNumTopK, j.grid_cap, kBuildStream));
       } else {
         HIPCHK(hipMemcpyAsync(h, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
-        HIPCHK(hipMemcpyAsync(h + V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
+        if (!reuse_kth)
+          HIPCHK(hipMemcpyAsync(h + V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
       }
+      if (reuse_kth) kth_reuse_bound(reuse, ix, h + V);  // (host work beside the device's)
     }
     HIPCHK(hipStreamSynchronize(kBuildStream));
     ix->tmaxs = h;
@@ -1814,7 +1862,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
       if (!deleted[d]) alive[d >> 5] |= 1u << (d & 31);
   }
   if ((rc = score_index(ix.get(), g->n_docs, g->tot_tokens, g->df_text, g->df_name, alive, g->tot_facet_tokens,
-                        VF ? g->df_facet : nullptr, wts)))
+                        VF ? g->df_facet : nullptr, wts, base)))
     return rc;
   *out = ix.release();
   return FG_OK;

@@ -85,3 +85,50 @@ def test_background_capped_scoring_identical(native):
             assert np.array_equal(a[0][i, :m], b[0][i, :m]) and np.array_equal(a[1][i, :m], b[1][i, :m])
     for x in (fg, bg, ix):
         x.close()
+
+
+def test_rescore_without_deletions_reuses_kth_bound(native):
+    """A rescore whose alive docs are the base snapshot's skips k_ktop: its per-term
+    K-th scores are the base's times the smallest new / old score ratio of the
+    term's postings (kth_reuse_bound).  They must never exceed the exact K-th
+    scores under the new statistics (a fresh build with them), stay within 0.1%
+    of them, and the searches must return the fresh build's hits; with new
+    deletions the rescore selects exactly."""
+    from fugu_amd import synth
+    ctx = native.Context((0,))
+    c = synth.corpus(400_000)
+    big = synth.corpus(440_000)  # statistics of the namespace after a commit of 40K more docs
+    g1 = native.docs_stats(c.off, c.tok, synth.VOCAB, threads=16)
+    g2 = native.docs_stats(big.off, big.tok, synth.VOCAB, threads=16)
+    ix = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, global_stats=g1)
+    re = ix.rescore(g2)
+    fresh = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, global_stats=g2)
+    terms = [t for t in range(0, 200_000, 53) if ix.df(t) > 0]
+    assert len(terms) > 1000
+    below, n = 0, 0
+    for t in terms:
+        a, b = re.term_kth(t), fresh.term_kth(t)
+        assert (a <= b).all(), (t, a, b)
+        assert np.array_equal(a > 0, b > 0), (t, a, b)
+        nz = b > 0
+        assert (a[nz] >= b[nz] * 0.999).all(), (t, a, b)
+        below += int((a[nz] < b[nz]).sum())
+        n += int(nz.sum())
+    assert n > 1000
+    q_off, qt = synth.queries(256, 1, 4, seed_q=23)
+    for mode, k in ((native.MODE_OR, 20), (native.MODE_OR, 1000), (native.MODE_AND, 100)):
+        x = re.search_batch(q_off, qt, k, mode=mode)
+        y = fresh.search_batch(q_off, qt, k, mode=mode)
+        assert np.array_equal(x[2], y[2])
+        for i in range(len(x[2])):
+            m = int(x[2][i])
+            assert np.array_equal(x[1][i, :m], y[1][i, :m]) and np.array_equal(x[0][i, :m], y[0][i, :m])
+    # new deletions: an exact select again
+    rng = np.random.default_rng(5)
+    deleted = (rng.random(c.n_docs) < 0.02).astype(np.uint8)
+    re2 = ix.rescore(g2, deleted)
+    fresh2 = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, global_stats=g2, deleted=deleted)
+    for t in terms[::7]:
+        assert np.array_equal(re2.term_kth(t), fresh2.term_kth(t)), t
+    for x in (re, re2, fresh, fresh2, ix):
+        x.close()
