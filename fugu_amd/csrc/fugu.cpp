@@ -584,12 +584,12 @@ static void kth_reuse_bound(const fg_index* base, const fg_index* ix, float* out
   }
   const double margin = 1.0 - std::ldexp(1.0, -18);  // f32 rounding of the old and the new scores
   for (uint32_t t = 0; t < V; ++t) {
-    double r = 1.0;
+    double r = HUGE_VAL;  // (> 1 when the new statistics raise every score of the term)
     const double wo[2] = {base->w_text[t], base->w_name.size() > t ? (double)base->w_name[t] : 0.0};
     const double wn[2] = {ix->w_text[t], ix->w_name.size() > t ? (double)ix->w_name[t] : 0.0};
     for (int f = 0; f < (ix->has_name ? 2 : 1); ++f)  // (no `name` postings: the field adds 0 to every score)
       if (wo[f] > 0.0) r = std::min(r, wn[f] / wo[f] * cmin[f]);
-    r = std::max(0.0, r) * margin;
+    r = (std::isfinite(r) ? std::max(0.0, r) : 1.0) * margin;
     for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
       const size_t x = (size_t)t * fg::kNumTopK + j;
       float v = (float)((double)base->ktop[x] * r);
