@@ -326,12 +326,11 @@ hipStream_t build_stream() {
 // rescore worker on a background stream)?
 bool on_background() { return tl_background || tl_build_stream; }
 // The workgroup cap of a background scoring's launches (fg::ScoreJob::grid_cap):
-// FUGU_BG_GRID workgroups per CU (default kBgGridPerCu; 0: no cap).  Measured
-// (profiles/r05/stall/): at 2 per CU the searches beside rescores alone drop from
-// max 24 to 3.4 ms, but beside whole commits p99 rises (0.89 -> 1.49 ms: the
-// capped kernels run longer and hold their slots for their whole span), so the
-// default is no cap
-constexpr uint32_t kBgGridPerCu = 0;
+// FUGU_BG_GRID workgroups per CU (default kBgGridPerCu; 0: no cap).  With the
+// K-th reuse (kth_reuse_bound) and one background stream, GET /search during
+// commits p99 0.37 -> 0.25 ms, 1.5x its idle p99 (profiles/r05/stall/bg_j2/);
+// before the reuse the cap had raised p99 (the capped k_ktop held its slots)
+constexpr uint32_t kBgGridPerCu = 2;
 uint32_t bg_grid_cap(int dev) {
   if (!on_background()) return 0;
   static const uint32_t per_cu = [] {
@@ -383,10 +382,13 @@ constexpr double kBgCuFrac = 1.0;
 hipStream_t background_stream(int dev, uint32_t i) {
   static std::mutex mu;
   static std::map<int, std::vector<hipStream_t>> streams;
-  // FUGU_BG_STREAMS (A/B, default 8): how many background streams a device has
+  // FUGU_BG_STREAMS (default 1): how many background streams a device has.  One:
+  // a commit's segment rescores queue their kernels one after another instead of
+  // all hitting the GPU together -- GET /search during commits p99 0.62 -> 0.37 ms
+  // at the same commit latency (profiles/r05/stall/bg_j2/)
   static const uint32_t kN = [] {
     const char* e = getenv("FUGU_BG_STREAMS");
-    return e && *e ? (uint32_t)std::min(64, std::max(1, atoi(e))) : 8u;
+    return e && *e ? (uint32_t)std::min(64, std::max(1, atoi(e))) : 1u;
   }();
   std::lock_guard<std::mutex> l(mu);
   auto& v = streams[dev];
