@@ -212,7 +212,11 @@ uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term);
 int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512);
 /* The snapshot's per-term K-th best alive posting scores for K = 1, 10, 20, 100,
  * 1000 (0 when the term has fewer alive postings): the starting thresholds of
- * its disjunctions.  out[5]. */
+ * its disjunctions.  out[5].  A snapshot from fg_index_rescore[_many] whose
+ * alive docs are its base's (no new deletions) holds a lower bound instead: the
+ * base's values times the term's smallest new / old posting-score ratio (within
+ * ~0.2% for a commit that grows the namespace by 10%); builds, merges and
+ * rescores with new deletions select exactly. */
 int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out);
 
 /* ---- doc-sharded namespaces: namespace-wide starting thresholds ----------------
