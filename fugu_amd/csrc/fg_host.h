@@ -184,6 +184,7 @@ struct ScoreBlock {
   size_t bytes = 0;
   void* hp = nullptr;  // pinned host block (tmaxs, ktop) or nullptr
   size_t hbytes = 0;
+  std::vector<float> hown;  // tmaxs / ktop when no pinned block was had
   std::shared_ptr<ScorePool> pool;
   ~ScoreBlock() {
     if (hp && pool) pool->put_host(hp, hbytes);
@@ -224,12 +225,9 @@ class SharedVec {
 };
 
 // BM25 weights of one set of statistics, shared by the snapshots scored with
-// them (fg_index_rescore_many); d_w: the same on the device (text [V], name [V])
-// or nullptr
+// them (fg_index_rescore_many)
 struct Weights {
   SharedVec<float> wt, wn;
-  const float* d_w = nullptr;
-  int dev = -1;
 };
 
 
@@ -378,20 +376,32 @@ struct fg_index {
   uint64_t n_postings = 0, device_bytes = 0, dir_entries = 0, tile_entries = 0;
   uint32_t n_dense = 0, n_rank = 0;  // n_rank: rank-kind slots, plain (d.n_prank) and sparse
   uint64_t n_srank_words = 0;        // sparse rank words (d.srank_w)
-  // ---- statistics and scoring (this snapshot's own)
+  // ---- statistics (this snapshot's own: the Searcher-wide ones of its commit).
+  // Scores are formed at query time from them (DevIndex::tfn, DevPlan::q_wt /
+  // q_wn, the plan's copy of `cache`), as tantivy's TermScorer does.
   uint64_t tot[2] = {0, 0};
   uint64_t n_stats = 0;  // N the BM25 statistics use (global N of a doc-sharded namespace)
   float avgdl[2] = {0, 0};
   float cache[512];
-  const float* ktop = nullptr;   // [V * kNumTopK] K-th best alive score per term (kTopKs), or a lower bound of it
-                                 // (a rescore without new deletions: kth_reuse_bound)
-  fgh::SharedVec<uint32_t> h_alive;  // the alive bitset this snapshot was scored with (empty: every doc)
-  const float* tmaxs = nullptr;  // [V] largest posting score per term
-  std::vector<float> hown;       // ktop / tmaxs when no pinned block was had (sblock.hp)
-  // [V * kNumTopK] namespace-wide floor of ktop (fg_index_set_kth_floor) or null;
-  // read and replaced with std::atomic_load / atomic_store
-  std::shared_ptr<const std::vector<float>> kth_floor;
   fgh::SharedVec<float> w_text, w_name;
+  fgh::SharedVec<uint32_t> h_alive;  // the alive bitset of this snapshot (empty: every doc)
+  // ---- bounds: computed ONCE when the structure is built (k_score / k_bucket /
+  // k_tsub / k_ktop under the build's statistics) and shared by every rescore of
+  // it; a plan scales them by the ratio of the current to the build statistics
+  // (term_ratio).  sblock holds the device tables and the host tmaxs / ktop.
+  std::shared_ptr<fgh::ScoreBlock> sblock;
+  const float* ktop = nullptr;   // [V * kNumTopK] K-th best score per term at the build (alive docs then)
+  const float* tmaxs = nullptr;  // [V] largest posting score per term at the build
+  fgh::SharedVec<float> wb_text, wb_name;  // the build's BM25 weights
+  float cache_b[512];                      // the build's tf caches
+  fgh::SharedVec<uint32_t> h_alive_b;      // the alive bitset ktop was selected over (empty: every doc)
+  uint32_t n_dead = 0;     // docs dead now that were alive in h_alive_b (ktop's K-th then needs K + n_dead)
+  bool same_stats = true;  // the current statistics are the build's (every ratio exactly 1)
+  double cup[2] = {1, 1}, cdn[2] = {1, 1};  // per field: max / min over fieldnorms of the tf-factor ratio
+  std::shared_ptr<void> alive_hold;         // the device alive bitset when it is this snapshot's own
+  // [V * kNumTopK] namespace-wide floor of the current K-th scores (fg_index_set_kth_floor) or
+  // null; read and replaced with std::atomic_load / atomic_store
+  std::shared_ptr<const std::vector<float>> kth_floor;
   // ---- structure (independent of the statistics; shared with rescored snapshots)
   fgh::SharedVec<uint64_t> off;
   fgh::SharedVec<uint32_t> df_text, df_name;  // this snapshot's own postings (tantivy's per-segment cost order)
@@ -412,10 +422,6 @@ struct fg_index {
   std::shared_ptr<DevAllocs> smem;
   std::shared_ptr<fgh::ScorePool> spool;
   uint64_t struct_bytes = 0;
-  const uint32_t* d_tfp = nullptr;   // tf_text | tf_name << 16 per posting, or nullptr ...
-  const uint16_t* d_tf16 = nullptr;  // ... tf_text alone when the snapshot has no `name` postings
-  const uint8_t* d_fn_text = nullptr;
-  const uint8_t* d_fn_name = nullptr;
   // packed chunk tables of k_score / k_bucket (fg_internal.h ScoreJob::sc_* / bk_*)
   const uint32_t *d_sc_tf = nullptr, *d_sc_tl = nullptr, *d_bk_tf = nullptr, *d_bk_tl = nullptr, *d_bk_e0 = nullptr,
                  *d_bk_e1 = nullptr, *d_kt_terms = nullptr, *d_kt_tiny = nullptr;
@@ -428,7 +434,6 @@ struct fg_index {
   uint32_t n_sc = 0, n_bk = 0, n_kt = 0, n_kbig = 0, n_kchunks = 0;
   fg::DevIndex d{};
   DevAllocs mem;
-  fgh::ScoreBlock sblock;
   // plan workspaces and the pinned host staging of plan uploads and result
   // copies: the device's pools, shared by every snapshot on it (fgh::device_pools)
   std::shared_ptr<WsPool> pool;
@@ -442,6 +447,7 @@ struct fg_plan {
   std::vector<fg_index*> segs;  // a multi-snapshot plan's snapshots after ix (retained)
   int mode = FG_MODE_AND;
   fg::DevPlan d{};
+  fg::DevIndex d0{};  // the first snapshot's view with the plan's copy of its tf caches (DevIndex::cache)
   void* ws = nullptr;  // workspace from ix->pool
   size_t ws_got = 0;
   float* own_score = nullptr;
@@ -486,3 +492,13 @@ struct fg_plan {
   hipStream_t up_stream = hipStreamPerThread;  // the stream the plan was uploaded on
 };
 
+
+namespace fgh {
+// Per-term bounds under a snapshot's current statistics from its build-time
+// tables (fugu.cpp): the score ratio factors, the largest score, and a lower
+// bound of the K-th best alive score (K the smallest stored level >= k; with_floor:
+// or the namespace-wide floor of a doc-sharded namespace's shard when higher)
+void term_ratio(const fg_index* ix, uint32_t t, float* rdn, float* rup);
+float term_max_now(const fg_index* ix, uint32_t t);
+float term_kth_now(const fg_index* ix, uint32_t t, uint32_t k, bool with_floor);
+}  // namespace fgh

@@ -26,20 +26,12 @@ constexpr uint32_t kMaxK = 1024;          // largest top-k the device select sup
 #endif
 constexpr uint32_t kFinalCap = FG_FINALCAP;  // candidates kept in LDS by the final select (>= kMaxK)
 static_assert(FG_FINALCAP >= 1024, "the final sort runs in place for up to kMaxK keys");
-#ifndef FG_DENSE_DIV
-#define FG_DENSE_DIV 256  // tools/ab_variants.py sweep 8..512: DESIGN.md §3
-#endif
-#ifndef FG_DENSE_GIB
-#define FG_DENSE_GIB 0    // f32 score tables: superseded by rank words; env FUGU_DENSE_GIB
-#endif
 #ifndef FG_RANK_DIV
 #define FG_RANK_DIV 16384
 #endif
 #ifndef FG_RANK_GIB
 #define FG_RANK_GIB 64    // env FUGU_RANK_GIB
 #endif
-constexpr uint32_t kDenseDiv = FG_DENSE_DIV;  // terms in >= 1/kDenseDiv of the docs may get a dense f32 score table
-constexpr uint64_t kDenseBudget = (uint64_t)FG_DENSE_GIB << 30;  // ... densest first, within this many bytes
 constexpr uint32_t kRankDiv = FG_RANK_DIV;    // terms in >= 1/kRankDiv of the docs may get rank words
 constexpr uint64_t kRankBudget = (uint64_t)FG_RANK_GIB << 30;    // ... densest first, within this many bytes
 #ifndef FG_RANK_FACTOR
@@ -205,43 +197,57 @@ __host__ __device__ inline uint32_t quant8(float s, float M) {
 constexpr uint32_t kSubShift = 9;  // 512-doc blocks: 8 per k_disj tile
 
 // tmeta of a term: bits 0-7 = B_t (bucket shift), 8-15 = S_t (search steps),
-// 16-30 = dense slot + 1 (0: none), bit 31 = the slot's kind (1: rank words, 0: f32 table);
+// 16-30 = rank slot + 1 (0: none), bit 31 = set with a slot (the round-1 f32 score tables, bit 31
+// clear, went with the precomputed scores);
 // rank-kind slots 1..n_prank are plain rank words, the ones above sparse (srank)
 __host__ __device__ inline uint32_t meta_slot(uint32_t meta) { return (meta >> 16) & 0x7FFFu; }
 __host__ __device__ inline bool meta_rank(uint32_t meta) { return (meta >> 31) != 0; }
 
 // Device view of one namespace snapshot (all pointers device-resident).
 //
-// Per term t the postings are doc[off[t] .. off[t+1]) (ascending) with psc[]
-// (the posting's BM25 term score) alongside, and a doc -> position directory: bucket b covers docs
-// [b << B_t, (b+1) << B_t) and dir[dir_off[t] + b] = first position in the
-// list with doc >= b << B_t (the last entry is df_t).  B_t is chosen so a
-// bucket holds ~kBucketTarget (4) postings; a probe is one
-// directory load and a <= S_t step search inside one or two lines.  The
-// densest terms (within a byte budget) additionally get RANK WORDS: one u64 per
-// 32 docs, the low half the docs' presence bits, the high half the number of
-// the term's postings before the word's first doc.  A probe is one 8-B load; on
-// a hit the posting's position is rank + popcount(bits below the doc), and its
-// score one psc[] load.  Scattered single-dword probes each move a 128-B line
-// (profiles/r02_start: tools/calib_fetch gather_lines), and a line of rank words
-// covers 512 docs where a line of a doc-indexed f32 score table covers 32, so
-// the candidates of a long lead list share lines.  (f32 tables, a probe = one
-// 4-B load giving the score, remain available: FUGU_DENSE_GIB.)
+// Per term t the postings are doc[off[t] .. off[t+1]) (ascending) with tfn[]
+// (the posting's term frequency and its doc's fieldnorm id) alongside, and a
+// doc -> position directory: bucket b covers docs [b << B_t, (b+1) << B_t) and
+// dir[dir_off[t] + b] = first position in the list with doc >= b << B_t (the
+// last entry is df_t).  B_t is chosen so a bucket holds ~kBucketTarget (4)
+// postings; a probe is one directory load and a <= S_t step search inside one
+// or two lines.  The densest terms (within a byte budget) additionally get
+// RANK WORDS: one u64 per 32 docs, the low half the docs' presence bits, the
+// high half the number of the term's postings before the word's first doc.  A
+// probe is one 8-B load; on a hit the posting's position is rank + popcount(bits
+// below the doc), and its tfn one 2-B load.  Scattered single-dword probes each
+// move a 128-B line (profiles/r02_start: tools/calib_fetch gather_lines), and a
+// line of rank words covers 512 docs, so the candidates of a long lead list
+// share lines.
+//
+// Scores are formed AT QUERY TIME, as tantivy's TermScorer does
+// (src/db/search.rs:162 -> query/bm25.rs Bm25Weight::score): a posting's score
+// is w_text * (tf / (tf + cache[fn])) (+ the name field's part), with the
+// query's per-clause weights (DevPlan::q_wt / q_wn, from the Searcher-wide
+// statistics of the moment) and the snapshot's tf cache (DevIndex::cache, set by
+// the plan).  A commit therefore only builds its new segment; the older ones
+// keep every device array.  The MaxScore bounds (bmax, tmax, tsub, tmaxs,
+// cmax) are the scores' maxima under the statistics the snapshot was BUILT
+// with; a plan scales them by a per-clause factor q_rup >= the largest ratio of
+// a posting's current score to its build-time one (1 exactly when the
+// statistics are the build's).
+constexpr uint32_t kTfEsc = 255;  // tfn's tf byte: >= this -> the exact tf is in esc_pos / esc_tf
+__host__ __device__ inline uint32_t tfn_pack(uint32_t tf, uint32_t fn) { return (fn << 8) | (tf < kTfEsc ? tf : kTfEsc); }
 struct DevIndex {
   const uint32_t* doc;       // [P] doc ids, CSR by term, ascending within a term
-  const float* psc;          // [P] the posting's term score: Should(text:t, name:t) in the doc, i.e.
-                             //     0.0 + w_text*(tf/(tf+cache[fn])) + w_name*(...), computed at snapshot
-                             //     build in tantivy's f32 operation order (a snapshot's BM25 statistics
-                             //     are fixed, so this is the value tantivy computes at query time)
+  const uint16_t* tfn;       // [P] (fn_text[doc] << 8) | min(tf_text, 255): tf_text 0 = no text occurrence
+  const uint16_t* tfn_name;  // [P] the same for the `name` field, or nullptr (no name postings)
+  const uint64_t* esc_pos;   // [n_esc] postings whose tf byte is kTfEsc in either field, ascending
+  const uint32_t* esc_tf;    // [n_esc] their exact tf_text | tf_name << 16
+  const float* cache;        // [256 or 512] K1 * ((1 - B) + B * TABLE[id] / avgdl): text, then name (plan-set)
   const uint64_t* off;       // [V+1] posting offsets
   const uint32_t* dir;       // [D] bucket directory (positions within the list)
   const uint32_t* dir_off;   // [V] first directory entry of each term
   const uint32_t* tmeta;     // [V] meta_slot / meta_rank above
-  const float* dense;        // [n_dense * N] doc-indexed term score (-1 = absent), f32-kind slots
   const uint64_t* rank;      // [n_prank * rank_words] rank words, rank-kind slots 1..n_prank
   const uint64_t* srank;     // [n_srank * srank_blocks] sparse rank block entries, rank-kind slots above
   const uint64_t* srank_w;   // sparse rank words (srank_index)
-  const float* tmaxs;        // [V] largest posting score of each term (MaxScore bound)
+  const float* tmaxs;        // [V] largest posting score of each term (build statistics)
   const uint32_t* alive;     // [ceil(N/32)] alive bitset, or nullptr (no deletes)
   const float* bmax;         // [D] parallel to dir: max term score of the postings in each bucket
   const float* tmax;         // tile maxima (k_disj tiles) of the terms with B_t <= kDisjTileShift
@@ -256,6 +262,7 @@ struct DevIndex {
   const uint32_t* coff;      // [V] index of each term's first chunk in cmax
   const uint32_t* fdoc;      // [PF] facet postings (doc ids, ascending), CSR by facet term
   const uint64_t* foff;      // [VF+1]
+  uint64_t n_esc;
   uint32_t n_docs;
   uint32_t n_terms;
   uint32_t has_name;
@@ -264,6 +271,25 @@ struct DevIndex {
   uint32_t n_prank;          // plain rank-kind slots
   uint32_t srank_blocks;     // block entries per sparse rank-kind term: ceil(N / 1024)
 };
+
+// The exact tf_text | tf_name << 16 of posting p whose tf byte escaped (binary
+// search of the snapshot's escape list; rare: tf >= 255)
+__host__ __device__ inline uint32_t tf_escaped(const uint64_t* esc_pos, const uint32_t* esc_tf, uint64_t n, uint64_t p) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (esc_pos[mid] < p) lo = mid + 1; else hi = mid;
+  }
+  return lo < n ? esc_tf[lo] : 0u;
+}
+
+// Bm25Weight::score in tantivy's f32 operation order (query/bm25.rs: weight *
+// (tf / (tf + cache[fieldnorm_id]))) for one field.  -ffp-contract=off and IEEE
+// f32 division: bit-identical to the host arithmetic (fugu.cpp, the oracle).
+__host__ __device__ inline float field_score(uint32_t tf, uint32_t fn, float w, const float* cache) {
+  const float f = (float)tf;
+  return w * (f / (f + cache[fn]));
+}
 
 // Facet filters of a planned batch (DevPlan).  Every distinct clause list
 // (filter) gets a doc-indexed mask in HBM built by k_fmask from the facet
@@ -310,7 +336,11 @@ struct DevPlan {
   const uint64_t* cand_off;     // [nq+1] candidate-list capacity offsets (work items of q * k)
   const uint64_t* q_thr0;       // [nq] starting threshold key (k_disj: per-term top-K bound), 0 = none
   const float* q_ub;            // [nq * kMaxTerms] k_conj MaxScore bounds: q_ub[i] = sum over the query's
-                                //     terms j >= i (intersection order) of tmaxs, i >= 1
+                                //     terms j >= i (intersection order) of their scaled tmaxs, i >= 1
+  const float* q_wt;            // [nq * kMaxTerms] each clause's BM25 weight, text field (query time)
+  const float* q_wn;            // [nq * kMaxTerms] ... and name field
+  const float* q_rup;           // [nq * kMaxTerms] factor on the clause's build-time bounds (tmax, bmax,
+                                //     cmax, tsub's tile maxima): >= current score / build score of any posting
   const uint32_t* q_hlo;        // [nq] f32 bits of the histogram's bin 0 lower edge
   const uint32_t* q_hsh;        // [nq] bin width: 2^q_hsh f32 ulps
   // workspace, zeroed per run (thresh and hist may be a linked group's shared ones)
@@ -320,6 +350,8 @@ struct DevPlan {
   uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list
   uint64_t* cand_keys;          // [cand_off[nq]] per-query candidate lists
   uint64_t* diag;               // diagnostic builds only (-DFG_DIAG): per-workgroup stamps
+  uint32_t feat;                // kernel features the plan's snapshots need: bit 0 `name` postings (tfn_name),
+                                // bit 1 escaped tf bytes (DevIndex::esc_pos); the kernels are instantiated per value
   uint32_t n_single;            // k_conj: the first n_single work items belong to single-list queries
   uint32_t n_scan;              // k_scan work items (queries with no text terms), after the total_chunks
                                 // k_conj / k_disj items in work_q / work_c / work_n
@@ -359,10 +391,11 @@ __host__ __device__ inline float key_score(uint64_t k) {
 }
 __host__ __device__ inline uint32_t key_doc(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
 
-// Snapshot scoring on the device (k_score / k_bucket / k_ktop): every posting's
-// BM25 term score from its term frequencies and the doc's fieldnorm ids with
-// the snapshot's statistics, then the bounds the kernels prune with.  Run at
-// build and again by fg_index_rescore when a commit changes the statistics.
+// Bound tables of a snapshot build (k_score / k_bucket / k_tsub / k_ktop), run
+// ONCE per segment build or merge: every posting's BM25 term score under the
+// build's statistics (into a temporary), then the bounds the kernels prune with
+// and the per-term K-th best scores.  A commit never runs them on an older
+// segment (fg_index_rescore only scales them at query time: DevPlan::q_rup).
 // Work is split into chunks of one term: k_score over postings, k_bucket over
 // directory buckets; ch_* arrays are the chunk tables.
 constexpr uint32_t kScoreChunk = kChunk;  // postings per k_score workgroup (= a k_conj lead chunk: cmax)
@@ -370,10 +403,11 @@ constexpr uint32_t kBucketChunk = 2048;  // buckets per k_bucket workgroup
 static_assert(kScoreChunk == kChunk, "DevIndex::cmax: a k_score chunk is a k_conj lead chunk");
 struct ScoreJob {
   const uint32_t* doc;
-  const uint32_t* tfp;        // [P] tf_text | tf_name << 16, or nullptr ...
-  const uint16_t* tf16;       // [P] ... tf_text (no `name` postings)
-  const uint8_t* fn_text;     // [N] fieldnorm ids
-  const uint8_t* fn_name;     // [N] or nullptr
+  const uint16_t* tfn;        // [P] DevIndex::tfn
+  const uint16_t* tfn_name;   // [P] or nullptr
+  const uint64_t* esc_pos;    // DevIndex::esc_pos / esc_tf
+  const uint32_t* esc_tf;
+  uint64_t n_esc;
   const uint64_t* off;        // [V+1]
   const uint32_t* dir;
   const uint32_t* dir_off;
@@ -383,7 +417,7 @@ struct ScoreJob {
   const float* w_text;        // [V] idf * (1 + K1)
   const float* w_name;        // [V]
   const float* cache;         // [512] K1 * ((1 - B) + B * TABLE[id] / avgdl), text then name
-  float* psc;                 // [P] out
+  float* psc;                 // [P] out: the build's posting scores (a temporary, freed after the build)
   float* bmax;                // [D] out
   uint32_t* tmaxs;            // [V] out (f32 bits, zeroed first)
   uint32_t* tmax;             // [tiles] out (f32 bits, zeroed first)
@@ -439,7 +473,6 @@ hipError_t launch_scan(const DevIndex& ix, const DevPlan& pl, hipStream_t s);
 // out_shard != nullptr: the merged select of a multi-snapshot plan (one list per batch query)
 hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, uint32_t* out_n, hipStream_t s,
                         uint32_t* out_shard = nullptr);
-hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s);
 hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uint32_t* slot_n, uint32_t n_slots,
                        uint32_t n_words, uint64_t* out, hipStream_t s);
 hipError_t launch_score(const ScoreJob& j, uint32_t n_chunks, hipStream_t s);

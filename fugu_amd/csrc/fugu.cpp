@@ -346,79 +346,72 @@ uint32_t bg_grid_cap(int dev) {
   return per_cu * (uint32_t)n_cu;
 }
 
-// The calling thread's high-priority stream on device `dev` (the search path's
-// own: its kernels are dispatched ahead of a commit's rescores and builds on the
-// same GPU), created on first use and kept for the thread's life;
-// FUGU_SEARCH_PRIO=0: the per-thread default stream (A/B)
+// A high-priority stream on device `dev` for the calling thread's searches (the
+// search path's own: its kernels are dispatched ahead of a commit's builds on
+// the same GPU).  Streams come from a fixed per-device pool (kSearchStreams),
+// handed out round-robin at a thread's first search and kept in a thread_local
+// -- a server whose worker threads come and go (tokio's spawn_blocking pool
+// retires idle threads) reuses the pool's streams instead of creating one per
+// thread without bound.  Work on one stream is ordered, so threads sharing a
+// stream serialise only their own launches; 16 streams >> the hardware queues.
+static constexpr uint32_t kSearchStreams = 16;
 static hipStream_t search_stream(int dev) {
-  static const bool on = [] {
-    const char* e = getenv("FUGU_SEARCH_PRIO");
-    return !(e && *e == '0');
-  }();
-  if (!on) return hipStreamPerThread;
   thread_local std::map<int, hipStream_t> mine;
   auto it = mine.find(dev);
   if (it != mine.end()) return it->second;
-  int least = 0, greatest = 0;
-  hipStream_t s = nullptr;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
-      hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) != hipSuccess) {
-    (void)hipGetLastError();
-    s = hipStreamPerThread;
+  static std::mutex mu;
+  static std::map<int, std::pair<std::vector<hipStream_t>, uint32_t>> pools;
+  hipStream_t s = hipStreamPerThread;
+  {
+    std::lock_guard<std::mutex> l(mu);
+    auto& pool = pools[dev];
+    if (pool.first.empty()) {
+      int cur = 0, least = 0, greatest = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(dev);
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+      for (uint32_t i = 0; i < kSearchStreams; ++i) {
+        hipStream_t x = nullptr;
+        if (hipStreamCreateWithPriority(&x, hipStreamNonBlocking, greatest) != hipSuccess) {
+          (void)hipGetLastError();
+          x = hipStreamPerThread;
+        }
+        pool.first.push_back(x);
+      }
+      (void)hipSetDevice(cur);
+    }
+    s = pool.first[pool.second++ % kSearchStreams];
   }
   mine[dev] = s;
   return s;
 }
 
-// The background streams of a device (a db's rescores, segment builds and
-// merges), created once: low-priority streams (the searches' own are high
-// priority), or at FUGU_BG_CU_FRAC < 1 streams restricted by a CU mask to that
-// fraction of the CUs (the CUs left out spread evenly over the XCDs).  The mask
-// is not honoured on this platform: a background kernel of 8 workgroups per CU
-// took as long on a 3/4 mask as on all CUs and held a search up just as long
-// (tools/stall_probe.hip, profiles/r05/stall/probe_r05p.json), so the default
-// is the priority alone
-constexpr double kBgCuFrac = 1.0;
-hipStream_t background_stream(int dev, uint32_t i) {
+// The background stream of a device (a db's segment builds and merges),
+// created once at low priority (the searches' own are high priority).  ONE
+// stream: a commit's device work queues behind itself instead of all hitting the
+// GPU together (GET /search during commits p99 0.62 -> 0.37 ms at the same
+// commit latency, profiles/r05/stall/bg_j2/).  (A CU-masked stream measured no
+// better: the mask is not honoured on this platform, tools/stall_probe.hip,
+// profiles/r05/stall/probe_r05p.json.)
+hipStream_t background_stream(int dev, uint32_t) {
   static std::mutex mu;
-  static std::map<int, std::vector<hipStream_t>> streams;
-  // FUGU_BG_STREAMS (default 1): how many background streams a device has.  One:
-  // a commit's segment rescores queue their kernels one after another instead of
-  // all hitting the GPU together -- GET /search during commits p99 0.62 -> 0.37 ms
-  // at the same commit latency (profiles/r05/stall/bg_j2/)
-  static const uint32_t kN = [] {
-    const char* e = getenv("FUGU_BG_STREAMS");
-    return e && *e ? (uint32_t)std::min(64, std::max(1, atoi(e))) : 1u;
-  }();
+  static std::map<int, hipStream_t> streams;
   std::lock_guard<std::mutex> l(mu);
-  auto& v = streams[dev];
-  if (v.empty()) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    (void)hipSetDevice(dev);
-    const char* e = getenv("FUGU_BG_CU_FRAC");
-    const double frac = e && *e ? atof(e) : kBgCuFrac;
-    hipDeviceProp_t prop;
-    const int n_cu = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 0;
-    std::vector<uint32_t> mask((std::max(n_cu, 1) + 31) / 32, 0u);
-    const uint32_t off = n_cu > 0 && frac < 1.0 ? (uint32_t)((1.0 - std::max(frac, 0.125)) * n_cu + 0.5) : 0u;
-    for (uint32_t c = 0; c < (uint32_t)n_cu; ++c)  // CU c left out when a multiple of n/off falls in [c, c+1)
-      if (!off || (uint64_t)(c + 1) * off / n_cu == (uint64_t)c * off / n_cu) mask[c / 32] |= 1u << (c % 32);
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
-    for (uint32_t j = 0; j < kN; ++j) {
-      hipStream_t st = nullptr;
-      const hipError_t rc = off ? hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data())
-                                : hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least);
-      if (rc != hipSuccess) {
-        (void)hipGetLastError();
-        st = nullptr;
-      }
-      v.push_back(st);
-    }
-    (void)hipSetDevice(cur);
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(dev);
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least) != hipSuccess) {
+    (void)hipGetLastError();
+    st = nullptr;
   }
-  return v[i % kN];
+  (void)hipSetDevice(cur);
+  streams[dev] = st;
+  return st;
 }
 
 template <class T>
@@ -504,13 +497,13 @@ int check_device(int dev) {
   return FG_OK;
 }
 
-// ---------------------------------------------------------------- snapshot scoring
-// The statistics-dependent half of a snapshot: BM25 weights and tf cache (host,
-// tantivy's f32 order with the host libm), then on the device every posting's
-// score (k_score), the bucket / term / tile maxima (k_bucket) and the per-term
-// K-th best alive scores (k_ktop), optional f32 score tables, the alive
-// bitset.  `df_t`/`df_n`/`df_f`: the statistics' doc frequencies (global for a
-// doc-sharded namespace).  Structure arrays must be in ix->d already.
+// ---------------------------------------------------------------- statistics and bounds
+// The statistics-dependent state of a snapshot is host-only: BM25 weights and
+// tf caches (tantivy's f32 order with the host libm), read by the plans; the
+// device forms the scores at query time.  The bound tables (maxima and K-th
+// best scores the kernels prune with) are computed on the device once per
+// structure under its build statistics.  `df_t`/`df_n`/`df_f`: the statistics'
+// doc frequencies (global for a doc-sharded namespace).
 
 // BM25 weights of terms [0, V) for statistics (Ns, df_t, df_n) (tantivy's f32 order)
 void bm25_weights(uint64_t Ns, const uint32_t* df_t, const uint32_t* df_n, uint32_t V, std::vector<float>& wt,
@@ -525,7 +518,137 @@ void bm25_weights(uint64_t Ns, const uint32_t* df_t, const uint32_t* df_n, uint3
   });
 }
 
-// k_ktop over the snapshot's scores (j.psc, j.alive -> j.ktop, and j.ladder when
+// The statistics of a snapshot (host only, tantivy's f32 order with the host
+// libm): N, token totals, avgdl and the tf caches, the BM25 weights (`wts`:
+// shared precomputed ones of the same statistics, or nullptr: computed here),
+// the facet clause scores.  The device sees them only through plans (query-time
+// scoring: DevPlan::q_wt / q_wn and the plan's copy of the caches).
+void set_stats(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_t* df_t, const uint32_t* df_n,
+               uint64_t tot_f, const uint32_t* df_f, const fgh::Weights* wts) {
+  const uint32_t V = ix->n_terms;
+  ix->n_stats = Ns;
+  ix->tot[0] = tot2[0];
+  ix->tot[1] = tot2[1];
+  for (int f = 0; f < 2; ++f) {
+    ix->avgdl[f] = (float)ix->tot[f] / (float)Ns;  // total_num_tokens as f32 / N as f32
+    bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
+  }
+  if (wts) {  // shared: at least V terms
+    ix->w_text = wts->wt;
+    ix->w_name = wts->wn;
+  } else {
+    std::vector<float> wt, wn;
+    bm25_weights(Ns, df_t, df_n, V, wt, wn);
+    ix->w_text = std::move(wt);
+    ix->w_name = std::move(wn);
+  }
+  // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
+  // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
+  const uint32_t VF = ix->n_fterms;
+  ix->tot_f = tot_f;
+  ix->df_facet.assign(df_f, df_f + VF);
+  ix->fscore.assign(VF, 0.0f);
+  if (ix->tot_f > 0) {
+    float cf[256];
+    ix->avgdl_f = (float)ix->tot_f / (float)Ns;
+    bm25_cache(ix->avgdl_f, cf);
+    ix->cache_f1 = cf[1];
+    for (uint32_t t = 0; t < VF; ++t) ix->fscore[t] = bm25_weight(ix->df_facet[t], Ns) * (1.0f / (1.0f + ix->cache_f1));
+  }
+}
+
+// How the current statistics relate to the build's (fg_index::same_stats,
+// cup / cdn): a posting's score w * tf / (tf + c[fn]) changes by (w' / w) *
+// (tf + c[fn]) / (tf + c'[fn]); over tf >= 1 the second factor lies between 1
+// and its value at tf = 1, so per field it is bounded by the extremes over the
+// fieldnorm ids of (1 + c) / (1 + c').
+void relate_stats(fg_index* ix) {
+  ix->same_stats = std::memcmp(ix->cache, ix->cache_b, sizeof ix->cache) == 0 &&
+                   (ix->w_text.data() == ix->wb_text.data() || ix->w_text.vec() == ix->wb_text.vec()) &&
+                   (ix->w_name.data() == ix->wb_name.data() || ix->w_name.vec() == ix->wb_name.vec());
+  for (int f = 0; f < 2; ++f) {
+    double up = 1.0, dn = 1.0;
+    for (int fn = 0; fn < 256; ++fn) {
+      const double q = (1.0 + (double)ix->cache_b[256 * f + fn]) / (1.0 + (double)ix->cache[256 * f + fn]);
+      if (!std::isfinite(q)) continue;  // (a field without tokens: no posting scores in it)
+      up = std::max(up, q);
+      dn = std::min(dn, q);
+    }
+    ix->cup[f] = up;
+    ix->cdn[f] = dn;
+  }
+}
+
+}  // namespace
+
+// Per-term bounds under the CURRENT statistics from the build-time tables
+// (shared by the planner, fg_index_term_kth and the byte models).
+namespace fgh {
+// f32 factors with rdn * s_build <= s_now <= rup * s_build for every posting of
+// term t (relate_stats' extremes times the weight ratio, over the fields the term
+// has postings in, with a 2^-19 margin for the f32 roundings of both scores);
+// exactly 1 when the statistics are the build's
+void term_ratio(const fg_index* ix, uint32_t t, float* rdn, float* rup) {
+  *rdn = *rup = 1.0f;
+  if (ix->same_stats || t >= ix->n_terms) return;
+  double lo = HUGE_VAL, hi = 0.0;
+  for (int f = 0; f < (ix->has_name ? 2 : 1); ++f) {
+    if ((f == 0 ? ix->df_text[t] : ix->df_name[t]) == 0) continue;  // no posting scores in the field
+    const double wb = f == 0 ? ix->wb_text[t] : ix->wb_name[t], wn = f == 0 ? ix->w_text[t] : ix->w_name[t];
+    if (!(wb > 0.0)) continue;
+    const double r = wn / wb;
+    hi = std::max(hi, r * ix->cup[f]);
+    lo = std::min(lo, r * ix->cdn[f]);
+  }
+  if (!(hi > 0.0) || !std::isfinite(lo)) return;
+  const double m = std::ldexp(1.0, -19);
+  const double u = hi * (1.0 + m), d = lo * (1.0 - m);
+  float fu = (float)u, fd = (float)d;
+  if ((double)fu < u) fu = std::nextafter(fu, HUGE_VALF);
+  if ((double)fd > d) fd = std::nextafter(fd, 0.0f);
+  *rup = fu;
+  *rdn = std::max(fd, 0.0f);
+}
+// the largest current score of term t (an upper bound; exact without a statistics change)
+float term_max_now(const fg_index* ix, uint32_t t) {
+  if (t >= ix->n_terms) return 0.0f;
+  float rdn, rup;
+  term_ratio(ix, t, &rdn, &rup);
+  const double v = (double)ix->tmaxs[t] * rup;
+  float f = (float)v;
+  if ((double)f < v) f = std::nextafter(f, HUGE_VALF);
+  return f;
+}
+// a lower bound of term t's K-th best current score over the alive docs, K the
+// smallest stored level >= k (0: none): the build's K'-th best for the smallest
+// stored K' >= K + n_dead (at most n_dead of those docs died since), times rdn;
+// or the namespace-wide floor of a doc-sharded namespace's shard when higher
+float term_kth_now(const fg_index* ix, uint32_t t, uint32_t k, bool with_floor) {
+  if (t >= ix->n_terms) return 0.0f;
+  float v = 0.0f;
+  const uint64_t need = (uint64_t)k + ix->n_dead;
+  for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
+    if (fg::kTopKs[j] < need) continue;
+    float rdn, rup;
+    term_ratio(ix, t, &rdn, &rup);
+    const double x = (double)ix->ktop[(size_t)t * fg::kNumTopK + j] * rdn;
+    v = (float)x;
+    if ((double)v > x) v = std::nextafter(v, 0.0f);
+    break;
+  }
+  if (!with_floor) return v;
+  if (const std::shared_ptr<const std::vector<float>> floor = std::atomic_load(&ix->kth_floor))
+    for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
+      if (fg::kTopKs[j] < k) continue;
+      v = std::max(v, (*floor)[(size_t)t * fg::kNumTopK + j]);
+      break;
+    }
+  return v;
+}
+}  // namespace fgh
+namespace {
+
+// k_ktop over the build's scores (j.psc, j.alive -> j.ktop, and j.ladder when
 // set): terms of <= kKtopChunk postings one workgroup each; longer terms in
 // kKtopChunk-posting chunks (k_ktop_part), then one select per term over its
 // chunks' best keys (k_ktop_big).  The chunk tables are the structure's; the key
@@ -564,103 +687,68 @@ static int ktop_pass(const fg_index* ix, fg::ScoreJob& j) {
   return FG_OK;
 }
 
-// wts: the weights of (Ns, df_t, df_n) for at least ix's terms, or nullptr (computed here)
-// A rescore whose alive docs are the base snapshot's (no new deletions: a commit
-// that only adds docs) need not select every term's K-th best scores again: each
-// posting's new score is at least r(t) times its old one, r(t) the smallest
-// ratio of new to old BM25 weight times tf factor over the term's fields and
-// fieldnorms, so r(t) times the old K-th best is a lower bound of the new one --
-// a valid starting threshold (kth_reuse_bound).  k_ktop was the larger part of a
-// rescore's device time and what held searches beside commits up longest
-// (profiles/r05/stall/bisect/); a segment with new deletions, a merge and a
-// build select exactly.
-static void kth_reuse_bound(const fg_index* base, const fg_index* ix, float* out) {
+// Every posting's score under the snapshot's CURRENT statistics into a
+// stream-ordered temporary (k_score), for the bound kernels of a build and for
+// fg_index_term_ladder.  `tmp` returns the temporary (freed stream-ordered by
+// the caller); j gets the postings inputs, the weights and caches (inside tmp)
+// and j.psc / j.cmax (cmax: the caller's, or a scratch part of tmp).
+static int score_postings(const fg_index* ix, fg::ScoreJob& j, float* cmax, void** tmp) {
   const uint32_t V = ix->n_terms;
-  double cmin[2];
-  for (int f = 0; f < 2; ++f) {  // tf / (tf + c) over tf >= 1: the new / old ratio is smallest at tf = 1 or 1
-    cmin[f] = 1.0;
-    for (int fn = 0; fn < 256; ++fn) {
-      const double q = (1.0 + base->cache[256 * f + fn]) / (1.0 + ix->cache[256 * f + fn]);
-      if (std::isfinite(q)) cmin[f] = std::min(cmin[f], q);  // (a field without tokens: no postings score in it)
-    }
-  }
-  const double margin = 1.0 - std::ldexp(1.0, -18);  // f32 rounding of the old and the new scores
-  for (uint32_t t = 0; t < V; ++t) {
-    double r = HUGE_VAL;  // (> 1 when the new statistics raise every score of the term)
-    const double wo[2] = {base->w_text[t], base->w_name.size() > t ? (double)base->w_name[t] : 0.0};
-    const double wn[2] = {ix->w_text[t], ix->w_name.size() > t ? (double)ix->w_name[t] : 0.0};
-    for (int f = 0; f < (ix->has_name ? 2 : 1); ++f)  // (no `name` postings: the field adds 0 to every score)
-      if (wo[f] > 0.0) r = std::min(r, wn[f] / wo[f] * cmin[f]);
-    r = (std::isfinite(r) ? std::max(0.0, r) : 1.0) * margin;
-    for (uint32_t j = 0; j < fg::kNumTopK; ++j) {
-      const size_t x = (size_t)t * fg::kNumTopK + j;
-      float v = (float)((double)base->ktop[x] * r);
-      if ((double)v > (double)base->ktop[x] * r) v = std::nextafter(v, 0.0f);
-      out[x] = v > 0.0f ? v : 0.0f;
-    }
-  }
+  auto al = [](size_t x) { return (std::max<size_t>(x, 16) + 255) & ~size_t(255); };
+  const size_t b_psc = al(4ull * ix->n_postings + 16), b_w = al(4ull * V), b_c = al(4ull * 512),
+               b_cm = cmax ? 0 : al(4ull * ix->n_sc);
+  if (fgh::dev_malloc_async(tmp, b_psc + 2 * b_w + b_c + b_cm, kBuildStream) != hipSuccess)
+    return fail(FG_EOOM, "hipMallocAsync(%zu) failed", b_psc + 2 * b_w + b_c + b_cm);
+  char* t = static_cast<char*>(*tmp);
+  float* d_psc = reinterpret_cast<float*>(t);
+  float* d_wt = reinterpret_cast<float*>(t + b_psc);
+  float* d_wn = reinterpret_cast<float*>(t + b_psc + b_w);
+  float* d_cache = reinterpret_cast<float*>(t + b_psc + 2 * b_w);
+  HIPCHK(hipMemcpyAsync(d_wt, ix->w_text.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
+  HIPCHK(hipMemcpyAsync(d_wn, ix->w_name.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
+  HIPCHK(hipMemcpyAsync(d_cache, ix->cache, 4ull * 512, hipMemcpyHostToDevice, kBuildStream));
+  j.doc = ix->d.doc;
+  j.tfn = ix->d.tfn;
+  j.tfn_name = ix->d.tfn_name;
+  j.esc_pos = ix->d.esc_pos;
+  j.esc_tf = ix->d.esc_tf;
+  j.n_esc = ix->d.n_esc;
+  j.off = ix->d.off;
+  j.dir = ix->d.dir;
+  j.dir_off = ix->d.dir_off;
+  j.tmeta = ix->d.tmeta;
+  j.toff = ix->d.toff;
+  j.w_text = d_wt;
+  j.w_name = d_wn;
+  j.cache = d_cache;
+  j.psc = d_psc;
+  j.cmax = cmax ? cmax : reinterpret_cast<float*>(t + b_psc + 2 * b_w + b_c);
+  j.coff = ix->d.coff;
+  j.sc_tf = ix->d_sc_tf;
+  j.sc_tl = ix->d_sc_tl;
+  j.sc_e0 = ix->d_sc_e0;
+  j.sc_e1 = ix->d_sc_e1;
+  j.n_terms = V;
+  j.grid_cap = bg_grid_cap(ix->dev);
+  HIPCHK(fg::launch_score(j, ix->n_scb, kBuildStream));
+  return FG_OK;
 }
 
-int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_t* df_t, const uint32_t* df_n,
-                const std::vector<uint32_t>& alive, uint64_t tot_f, const uint32_t* df_f,
-                const fgh::Weights* wts = nullptr, const fg_index* reuse = nullptr) {
+// The bounds of a freshly built structure under its build statistics (which
+// are its current ones): the posting scores into a temporary (k_score, with the
+// block-max per 2048 postings), bucket / term / tile maxima (k_bucket), sub-tile
+// maxima (k_tsub), per-term K-th best alive scores (k_ktop), and the read-back
+// of tmaxs / ktop for the planner.  Once per build or merge: a commit's
+// rescores of older segments share them (rescore_one).
+int build_bounds(fg_index* ix, const std::vector<uint32_t>& alive) {
   const uint32_t V = ix->n_terms;
-  const uint64_t N = ix->n_docs;
-  ix->n_stats = Ns;
-  ix->tot[0] = tot2[0];
-  ix->tot[1] = tot2[1];
-  for (int f = 0; f < 2; ++f) {
-    ix->avgdl[f] = (float)ix->tot[f] / (float)Ns;  // total_num_tokens as f32 / N as f32
-    bm25_cache(ix->avgdl[f], ix->cache + 256 * f);
-  }
-  if (wts) {  // shared: at least V terms
-    ix->w_text = wts->wt;
-    ix->w_name = wts->wn;
-  } else {
-    std::vector<float> wt, wn;
-    bm25_weights(Ns, df_t, df_n, V, wt, wn);
-    ix->w_text = std::move(wt);
-    ix->w_name = std::move(wn);
-  }
-  // the weights already on this device (one upload for every snapshot of a rescore_many)
-  const bool dev_w = wts && wts->d_w && wts->dev == ix->dev;
-  ix->h_alive = alive;
-  // FUGU_KTOP_REUSE=0: select exactly on every rescore (A/B)
-  static const bool reuse_on = [] {
-    const char* e = getenv("FUGU_KTOP_REUSE");
-    return !(e && *e == '0');
-  }();
-  const bool reuse_kth = reuse_on && reuse && reuse->ktop && reuse->n_terms == V && reuse->h_alive.vec() == alive &&
-                         reuse->w_text.size() >= V;
-  // facet field: Bm25Weight of a facet TermQuery (tf 1, no fieldnorms ->
-  // FieldNormReader::constant(max_doc, 1) -> id 1, avg = total_num_tokens / N)
-  const uint32_t VF = ix->n_fterms;
-  ix->tot_f = tot_f;
-  ix->df_facet.assign(df_f, df_f + VF);
-  ix->fscore.assign(VF, 0.0f);
-  if (ix->tot_f > 0) {
-    float cf[256];
-    ix->avgdl_f = (float)ix->tot_f / (float)Ns;
-    bm25_cache(ix->avgdl_f, cf);
-    ix->cache_f1 = cf[1];
-    for (uint32_t t = 0; t < VF; ++t) ix->fscore[t] = bm25_weight(ix->df_facet[t], Ns) * (1.0f / (1.0f + ix->cache_f1));
-  }
-  g_bt.mark("weights");
   HIPCHK(hipSetDevice(ix->dev));
-  uint64_t bytes = 0;
-  int rc;
-  // every scoring table in ONE block of the structure's pool (a rescore of the
-  // same structure gets a released snapshot's block back: ScorePool)
   struct Part { size_t bytes; void** out; };
-  float *d_wt, *d_wn, *d_cache, *d_psc, *d_bmax, *d_ktop, *d_cmax;
+  float *d_bmax, *d_ktop, *d_cmax;
   uint64_t* d_tsub = nullptr;
   uint32_t *d_alive = nullptr, *d_tmaxs, *d_tmax;
   const Part parts[] = {
-      {4ull * V, reinterpret_cast<void**>(&d_wt)},
-      {4ull * V, reinterpret_cast<void**>(&d_wn)},
-      {4ull * 512, reinterpret_cast<void**>(&d_cache)},
       {alive.empty() ? 0 : 4ull * alive.size(), reinterpret_cast<void**>(&d_alive)},
-      {4ull * ix->n_postings + 16, reinterpret_cast<void**>(&d_psc)},  // 16 B of slack after the scores
       {4ull * ix->dir_entries, reinterpret_cast<void**>(&d_bmax)},
       {4ull * V, reinterpret_cast<void**>(&d_tmaxs)},
       {4ull * ix->tile_entries, reinterpret_cast<void**>(&d_tmax)},
@@ -674,12 +762,13 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
     ix->spool = std::make_shared<fgh::ScorePool>();
     ix->spool->dev = ix->dev;
   }
+  auto sb = std::make_shared<fgh::ScoreBlock>();
   char* blk = static_cast<char*>(ix->spool->get(total));
-  if (!blk) return fail(FG_EOOM, "scoring tables: hipMalloc(%zu) failed", total);
-  ix->sblock.p = blk;
-  ix->sblock.bytes = total;
-  ix->sblock.pool = ix->spool;
-  bytes += total;
+  if (!blk) return fail(FG_EOOM, "bound tables: hipMalloc(%zu) failed", total);
+  sb->p = blk;
+  sb->bytes = total;
+  sb->pool = ix->spool;
+  ix->sblock = sb;
   {
     size_t o = 0;
     for (const Part& pt : parts) {
@@ -687,162 +776,78 @@ int score_index(fg_index* ix, uint64_t Ns, const uint64_t tot2[2], const uint32_
       o += (std::max<size_t>(pt.bytes, 16) + 255) & ~size_t(255);
     }
   }
-  if (dev_w) {  // (the block keeps its two weight parts: one block size for every scoring of the structure)
-    d_wt = const_cast<float*>(wts->d_w);
-    d_wn = const_cast<float*>(wts->d_w) + wts->wt.size();
-  } else {
-    HIPCHK(hipMemcpyAsync(d_wt, ix->w_text.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
-    HIPCHK(hipMemcpyAsync(d_wn, ix->w_name.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream));
-  }
-  HIPCHK(hipMemcpyAsync(d_cache, ix->cache, 4ull * 512, hipMemcpyHostToDevice, kBuildStream));
   if (d_alive) HIPCHK(hipMemcpyAsync(d_alive, alive.data(), 4ull * alive.size(), hipMemcpyHostToDevice, kBuildStream));
-  g_bt.mark("scoring uploads + allocs");
   HIPCHK(hipMemsetAsync(d_tmaxs, 0, 4ull * V, kBuildStream));
   HIPCHK(hipMemsetAsync(d_tmax, 0, std::max<size_t>(4ull * ix->tile_entries, 16), kBuildStream));
   HIPCHK(hipMemsetAsync(d_ktop, 0, 4ull * V * fg::kNumTopK, kBuildStream));
+  g_bt.mark("bound tables + uploads");
   fg::ScoreJob j{};
-  j.doc = ix->d.doc;
-  j.tfp = ix->d_tfp;
-  j.tf16 = ix->d_tf16;
-  j.fn_text = ix->d_fn_text;
-  j.fn_name = ix->has_name ? ix->d_fn_name : nullptr;
-  j.off = ix->d.off;
-  j.dir = ix->d.dir;
-  j.dir_off = ix->d.dir_off;
-  j.tmeta = ix->d.tmeta;
-  j.toff = ix->d.toff;
+  void* tmp = nullptr;
+  if (int rc = score_postings(ix, j, d_cmax, &tmp)) return rc;
+  struct TmpBack {
+    void* p;
+    ~TmpBack() { (void)hipFreeAsync(p, kBuildStream); }
+  } tmp_back{tmp};
   j.alive = d_alive;
-  j.w_text = d_wt;
-  j.w_name = d_wn;
-  j.cache = d_cache;
-  j.psc = d_psc;
   j.bmax = d_bmax;
   j.tmaxs = d_tmaxs;
   j.tmax = d_tmax;
   j.ktop = d_ktop;
-  j.cmax = d_cmax;
-  j.sc_tf = ix->d_sc_tf;
-  j.sc_tl = ix->d_sc_tl;
-  j.sc_e0 = ix->d_sc_e0;
-  j.sc_e1 = ix->d_sc_e1;
   j.bk_tf = ix->d_bk_tf;
   j.bk_tl = ix->d_bk_tl;
   j.bk_e0 = ix->d_bk_e0;
   j.bk_e1 = ix->d_bk_e1;
-  j.n_terms = V;
   j.n_dir = ix->dir_entries;
-  j.kt_tiny = ix->d_kt_tiny;
-  j.n_tiny = ix->n_ktiny;
-  j.coff = ix->d.coff;
-  j.grid_cap = bg_grid_cap(ix->dev);
-  // (a bisect of what held searches up beside a rescore -- skipping the k_ktop
-  // pass, the tables' read-back, k_score / k_bucket / k_tsub in turn -- is in
-  // profiles/r05/stall/bisect/)
-  HIPCHK(fg::launch_score(j, ix->n_scb, kBuildStream));
   HIPCHK(fg::launch_bucket(j, ix->n_bk, ix->n_docs, kBuildStream));
   j.tsub = d_tsub;
   j.tterm = ix->d_tterm;
   j.n_tterm = ix->n_tterm;
   j.n_tiles = ix->n_tiles;
   HIPCHK(fg::launch_tsub(j, ix->n_docs, kBuildStream));
-  if (!reuse_kth)
-    if (int rc = ktop_pass(ix, j)) return rc;
-  g_bt.mark("scoring launches");
-  // tmaxs [V] then ktop [V * kNumTopK], read straight into the structure's
-  // pooled pinned block (a released snapshot's, after the first rescores)
+  if (int rc = ktop_pass(ix, j)) return rc;
+  g_bt.mark("bound launches");
+  // tmaxs [V] then ktop [V * kNumTopK], read straight into a pooled pinned block
   {
     const size_t hb = 4ull * V * (1 + fg::kNumTopK);
     float* h = static_cast<float*>(ix->spool->get_host(hb));
     if (h) {
-      ix->sblock.hp = h;
-      ix->sblock.hbytes = hb;
+      sb->hp = h;
+      sb->hbytes = hb;
     } else {
-      ix->hown.resize((size_t)V * (1 + fg::kNumTopK));
-      h = ix->hown.data();
+      sb->hown.resize((size_t)V * (1 + fg::kNumTopK));
+      h = sb->hown.data();
     }
-    {
-      if (on_background() && ix->sblock.hp) {
-        // a background scoring: the read-back as a copy kernel of short workgroups
-        // on its low-priority stream (pinned host memory is device-visible), not a
-        // copy-engine transfer: the copy-engine read-backs of a rescore's eight
-        // segments held searches up (tools/rescore_stall.py, bit 1 of
-        // FUGU_DIAG_SCORE_SKIP: max 18 -> 6 ms)
-        HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h), d_tmaxs, V, j.grid_cap, kBuildStream));
-        if (!reuse_kth)
-          HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h + V), reinterpret_cast<const uint32_t*>(d_ktop),
-                                   (uint64_t)V * fg::kNumTopK, j.grid_cap, kBuildStream));
-      } else {
-        HIPCHK(hipMemcpyAsync(h, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
-        if (!reuse_kth)
-          HIPCHK(hipMemcpyAsync(h + V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
-      }
-      if (reuse_kth) kth_reuse_bound(reuse, ix, h + V);  // (host work beside the device's)
+    if (on_background() && sb->hp) {
+      // a background build: the read-back as a copy kernel of short workgroups
+      // on its low-priority stream (pinned host memory is device-visible), not a
+      // copy-engine transfer (those held searches up: tools/rescore_stall.py)
+      HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h), d_tmaxs, V, j.grid_cap, kBuildStream));
+      HIPCHK(fg::launch_copy32(reinterpret_cast<uint32_t*>(h + V), reinterpret_cast<const uint32_t*>(d_ktop),
+                               (uint64_t)V * fg::kNumTopK, j.grid_cap, kBuildStream));
+    } else {
+      HIPCHK(hipMemcpyAsync(h, d_tmaxs, 4ull * V, hipMemcpyDeviceToHost, kBuildStream));
+      HIPCHK(hipMemcpyAsync(h + V, d_ktop, 4ull * V * fg::kNumTopK, hipMemcpyDeviceToHost, kBuildStream));
     }
     HIPCHK(hipStreamSynchronize(kBuildStream));
     ix->tmaxs = h;
     ix->ktop = h + V;
   }
-  g_bt.mark("device scoring");
-  // f32 score tables (FUGU_DENSE_GIB, default none: rank words serve the dense
-  // terms) for the densest terms without rank words, filled from the new scores
-  std::vector<uint32_t> f32_terms;
-  float* d_dense = nullptr;
-  {
-    const char* v = getenv("FUGU_DENSE_GIB");
-    const uint64_t want = v && *v ? (uint64_t)(atof(v) * (double)(1ull << 30)) : fg::kDenseBudget;
-    if (want > 0) {
-      size_t free_b = 0, total_b = 0;
-      HIPCHK(hipMemGetInfo(&free_b, &total_b));
-      const uint64_t b32 = std::min<uint64_t>(want, free_b / 4);
-      std::vector<uint32_t> by_df;
-      for (uint32_t t = 0; t < V; ++t)
-        if (!fg::meta_slot(ix->tmeta[t]) && (ix->off[t + 1] - ix->off[t]) * fg::kDenseDiv >= N) by_df.push_back(t);
-      std::stable_sort(by_df.begin(), by_df.end(), [&](uint32_t a, uint32_t b) {
-        return ix->off[a + 1] - ix->off[a] > ix->off[b + 1] - ix->off[b];
-      });
-      for (uint32_t t : by_df) {
-        if ((f32_terms.size() + 1) * N * 4ull > b32 || f32_terms.size() >= fg::kMaxDense) break;
-        f32_terms.push_back(t);
-      }
-      while (!f32_terms.empty()) {
-        void* q = nullptr;
-        if (hipMalloc(&q, N * 4ull * f32_terms.size()) == hipSuccess) {
-          ix->mem.ptrs.push_back(q);
-          bytes += N * 4ull * f32_terms.size();
-          d_dense = static_cast<float*>(q);
-          break;
-        }
-        (void)hipGetLastError();
-        f32_terms.resize(f32_terms.size() / 2);
-      }
-    }
-  }
-  std::vector<uint32_t> tmeta;
-  if (!f32_terms.empty()) {
-    tmeta = ix->tmeta.vec();
-    HIPCHK(hipMemsetD32Async(d_dense, (int)0xBF800000u, N * f32_terms.size(), kBuildStream));  // -1.0f: absent
-    for (uint32_t s2 = 0; s2 < f32_terms.size(); ++s2) {
-      const uint32_t t = f32_terms[s2];
-      HIPCHK(fg::launch_dense(ix->d.doc, d_psc, ix->off[t], (uint32_t)(ix->off[t + 1] - ix->off[t]),
-                              d_dense + (size_t)s2 * N, kBuildStream));
-      tmeta[t] |= (s2 + 1) << 16;  // f32 kind (bit 31 clear)
-    }
-    HIPCHK(hipStreamSynchronize(kBuildStream));
-    uint32_t* d_tm;
-    if ((rc = dev_upload(ix->mem, tmeta.data(), tmeta.size(), &d_tm, &bytes))) return rc;
-    ix->d.tmeta = d_tm;
-    ix->tmeta = tmeta;
-  }
-  ix->n_dense = (uint32_t)f32_terms.size();
-  ix->d.psc = d_psc;
+  g_bt.mark("device bounds");
+  // the build's statistics are the bounds' reference
+  ix->wb_text = ix->w_text;
+  ix->wb_name = ix->w_name;
+  std::memcpy(ix->cache_b, ix->cache, sizeof ix->cache);
+  ix->h_alive = alive;
+  ix->h_alive_b = ix->h_alive;
+  ix->n_dead = 0;
+  relate_stats(ix);
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
   ix->d.tsub = d_tsub;
   ix->d.cmax = d_cmax;
   ix->d.alive = d_alive;
-  ix->d.dense = d_dense;
-  ix->device_bytes = ix->struct_bytes + bytes;
+  ix->device_bytes = ix->struct_bytes + total;
   return FG_OK;
 }
 
@@ -1057,30 +1062,46 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   DevAllocs& sm = *ix->smem;
   uint64_t& bytes = ix->struct_bytes;
   int rc;
-  uint32_t *d_doc, *d_tfp = nullptr, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc, *d_tterm;
-  uint16_t* d_tf16 = nullptr;
-  uint8_t *d_fnt, *d_fnn = nullptr;
+  uint32_t *d_doc, *d_dir, *d_dir_off, *d_tmeta, *d_toff, *d_tdir, *d_fdoc, *d_tterm, *d_esc_tf = nullptr;
+  uint16_t *d_tfn = nullptr, *d_tfn_name = nullptr;
+  uint64_t* d_esc_pos = nullptr;
   uint64_t *d_off, *d_foff;
   uint32_t *d_sctf, *d_sctl, *d_bktf, *d_bktl, *d_bke0, *d_bke1, *d_kt, *d_ktt, *d_coff, *d_kbt, *d_kb0, *d_kcb, *d_kcs;
   uint64_t *d_sce0, *d_sce1;
-  // without `name` postings every tf_name is 0: the term frequencies (k_score's
-  // input, read at every rescore) as u16, 2 B per posting instead of 4 (1 GiB
-  // of a 10M-doc namespace)
-  std::vector<uint16_t> tf16;
-  if (!hp.has_name) {
-    tf16.resize(hp.tf.size());
+  // the postings' payloads (DevIndex::tfn): per field (fieldnorm id of the doc
+  // << 8) | tf, 2 B per posting -- what a query-time score needs besides the
+  // clause's weight, beside the doc id -- and the postings whose tf does not fit
+  // the byte (>= 255) in a sorted escape list
+  std::vector<uint16_t> tfn(hp.tf.size()), tfn_name(hp.has_name ? hp.tf.size() : 0);
+  std::vector<uint64_t> esc_pos;
+  std::vector<uint32_t> esc_tf;
+  {
     const size_t np = hp.tf.size(), piece = (np + 1023) / 1024;  // > 2^32 postings: 64-bit pieces
+    std::vector<std::vector<uint64_t>> ep(1024);
     parallel_dynamic(1024, hw_threads(0), 8, [&](int, uint32_t b, uint32_t e) {
-      for (size_t i = (size_t)b * piece; i < std::min(np, (size_t)e * piece); ++i) tf16[i] = (uint16_t)hp.tf[i];
+      for (uint32_t pc = b; pc < e; ++pc)
+        for (size_t i = (size_t)pc * piece; i < std::min(np, (size_t)(pc + 1) * piece); ++i) {
+          const uint32_t d = hp.doc[i], tt = hp.tf[i] & 0xFFFFu, tn = hp.tf[i] >> 16;
+          tfn[i] = (uint16_t)fg::tfn_pack(tt, hp.fn_text[d]);
+          if (hp.has_name) tfn_name[i] = (uint16_t)(tn ? fg::tfn_pack(tn, hp.fn_name[d]) : 0u);
+          if (tt >= fg::kTfEsc || (hp.has_name && tn >= fg::kTfEsc)) ep[pc].push_back(i);
+        }
     });
+    for (auto& v : ep)
+      for (uint64_t i : v) {
+        esc_pos.push_back(i);
+        esc_tf.push_back(hp.tf[i]);
+      }
   }
   {
     UploadBatch ub;
     ub.add(hp.doc.data(), hp.doc.size(), &d_doc);
-    if (hp.has_name) ub.add(hp.tf.data(), hp.tf.size(), &d_tfp);
-    else ub.add(tf16.data(), tf16.size(), &d_tf16);
-    ub.add(hp.fn_text.data(), hp.fn_text.size(), &d_fnt);
-    if (hp.has_name) ub.add(hp.fn_name.data(), hp.fn_name.size(), &d_fnn);
+    ub.add(tfn.data(), tfn.size(), &d_tfn);
+    if (hp.has_name) ub.add(tfn_name.data(), tfn_name.size(), &d_tfn_name);
+    if (!esc_pos.empty()) {
+      ub.add(esc_pos.data(), esc_pos.size(), &d_esc_pos);
+      ub.add(esc_tf.data(), esc_tf.size(), &d_esc_tf);
+    }
     ub.add(hp.off.data(), hp.off.size(), &d_off);
     ub.add(dir.data(), dir.size(), &d_dir);
     ub.add(dir_off.data(), dir_off.size(), &d_dir_off);
@@ -1106,6 +1127,8 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     ub.add(coff.data(), coff.size(), &d_coff);
     if ((rc = ub.commit(sm, &bytes))) return rc;
   }
+  std::vector<uint16_t>().swap(tfn);
+  std::vector<uint16_t>().swap(tfn_name);
   std::vector<uint32_t>().swap(hp.tf);
   std::vector<uint32_t>().swap(dir);
   std::vector<uint32_t>().swap(tdir);
@@ -1162,13 +1185,8 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t brk = std::min<uint64_t>(want, free_b / 4);
-    // A/B (FUGU_RANK_SKIP_TOP=T): the T densest terms without rank words (with
-    // FUGU_DENSE_GIB they take f32 score tables: one gather per probe)
-    const char* sk = getenv("FUGU_RANK_SKIP_TOP");
-    size_t skip = sk && *sk ? (size_t)atol(sk) : 0;
     uint64_t used = 0;
     for (size_t i = 0; i < by_df.size(); ++i) {
-      if (skip) { --skip; continue; }
       const uint64_t cp = rank_words * 8ull, cs = (sblocks + (uint64_t)nwords[i]) * 8ull;
       const bool plain = plain_df(by_df[i]) || cp <= cs;
       const uint64_t c = plain ? cp : cs;
@@ -1273,10 +1291,11 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   if ((rc = dev_upload(sm, tmeta.data(), tmeta.size(), &d_tmeta, &bytes))) return rc;
   ix->tmeta = tmeta;
   g_bt.mark("rank words");
-  ix->d_tfp = d_tfp;
-  ix->d_tf16 = d_tf16;
-  ix->d_fn_text = d_fnt;
-  ix->d_fn_name = d_fnn;
+  ix->d.tfn = d_tfn;
+  ix->d.tfn_name = d_tfn_name;
+  ix->d.esc_pos = d_esc_pos;
+  ix->d.esc_tf = d_esc_tf;
+  ix->d.n_esc = esc_pos.size();
   ix->d_sc_tf = d_sctf;
   ix->d_sc_tl = d_sctl;
   ix->d_sc_e0 = d_sce0;
@@ -1357,10 +1376,11 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     for (uint32_t t = 0; t < VF; ++t)
       if (g->df_facet[t] < ix->df_facet_local[t]) return fail(FG_EINVAL, "global facet df of term %u is below this shard's", t);
   const uint64_t tot_local[2] = {ix->tot_local[0], ix->tot_local[1]};
-  if ((rc = score_index(ix.get(), g ? g->n_docs : N, g ? g->tot_tokens : tot_local,
-                        g ? g->df_text : ix->df_text.data(), g ? g->df_name : ix->df_name.data(), hp.alive,
-                        g ? g->tot_facet_tokens : ix->tot_f_local, g && VF ? g->df_facet : ix->df_facet_local.data())))
-    return rc;
+  set_stats(ix.get(), g ? g->n_docs : N, g ? g->tot_tokens : tot_local, g ? g->df_text : ix->df_text.data(),
+            g ? g->df_name : ix->df_name.data(), g ? g->tot_facet_tokens : ix->tot_f_local,
+            g && VF ? g->df_facet : ix->df_facet_local.data(), nullptr);
+  g_bt.mark("weights");
+  if ((rc = build_bounds(ix.get(), hp.alive))) return rc;
   g_bt.mark("tail");
   *out = ix.release();
   return FG_OK;
@@ -1768,7 +1788,12 @@ int fg_index_build_global(fg_ctx* ctx, int dev, const fg_index_input* in, const 
 
 }  // extern "C"
 
-// one snapshot rescored (fg_index_rescore); wts: shared precomputed weights or nullptr
+// one snapshot rescored (fg_index_rescore); wts: shared precomputed weights or
+// nullptr.  Host only: tantivy scores at query time (src/db/search.rs:162), so
+// a new Searcher's statistics need no device work -- the snapshot shares every
+// device array of its base (structure and bound tables) and gets the new
+// statistics (plans read them), a new alive bitset when docs were deleted, and
+// the ratios that scale the build-time bounds (relate_stats).
 static int rescore_one(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out,
                        const fgh::Weights* wts) {
   if (!base || !g || !out || !g->df_text) return fail(FG_EINVAL, "bad arguments");
@@ -1788,7 +1813,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   fgh::device_pools(base->dev, &ix->pool, &ix->pinned);
   // the structure: shared device arrays and host bookkeeping (SharedVec)
   ix->smem = base->smem;
-  ix->spool = base->spool;  // the structure's scoring blocks (a released rescore's block comes back)
+  ix->spool = base->spool;
   ix->struct_bytes = base->struct_bytes;
   ix->n_docs = N;
   ix->n_terms = V;
@@ -1806,24 +1831,13 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->h_doc = base->h_doc;
   ix->tot_local[0] = base->tot_local[0];
   ix->tot_local[1] = base->tot_local[1];
-  // f32 score tables belong to the scoring: drop base's slots of that kind
   ix->tmeta = base->tmeta;
-  bool f32_slots = false;
-  for (uint32_t m : base->tmeta)
-    if (fg::meta_slot(m) && !fg::meta_rank(m)) { f32_slots = true; break; }
-  if (f32_slots)
-    for (auto& m : ix->tmeta.mut())
-      if (fg::meta_slot(m) && !fg::meta_rank(m)) m &= 0xFFFFu;
   ix->n_fterms = VF;
   ix->tot_f_local = base->tot_f_local;
   ix->foff = base->foff;
   ix->df_facet_local = base->df_facet_local;
   ix->ffirst = base->ffirst;
   ix->flast = base->flast;
-  ix->d_tfp = base->d_tfp;
-  ix->d_tf16 = base->d_tf16;
-  ix->d_fn_text = base->d_fn_text;
-  ix->d_fn_name = base->d_fn_name;
   ix->d_sc_tf = base->d_sc_tf;
   ix->d_sc_tl = base->d_sc_tl;
   ix->d_sc_e0 = base->d_sc_e0;
@@ -1849,23 +1863,53 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->n_bk = base->n_bk;
   ix->n_kt = base->n_kt;
   ix->d = base->d;
-  int rc;
-  if (f32_slots) {
-    HIPCHK(hipSetDevice(ix->dev));
-    uint32_t* d_tm;
-    uint64_t b = 0;
-    if ((rc = dev_upload(ix->mem, ix->tmeta.data(), ix->tmeta.size(), &d_tm, &b))) return rc;
-    ix->d.tmeta = d_tm;
-  }
+  // the bounds and the build statistics they are under
+  ix->sblock = base->sblock;
+  ix->ktop = base->ktop;
+  ix->tmaxs = base->tmaxs;
+  ix->wb_text = base->wb_text;
+  ix->wb_name = base->wb_name;
+  std::memcpy(ix->cache_b, base->cache_b, sizeof ix->cache_b);
+  ix->h_alive_b = base->h_alive_b;
+  ix->device_bytes = base->device_bytes;
+  set_stats(ix.get(), g->n_docs, g->tot_tokens, g->df_text, g->df_name, g->tot_facet_tokens, VF ? g->df_facet : nullptr,
+            wts);
+  relate_stats(ix.get());
+  // deletions: the alive bitset (the base's device copy when unchanged), and
+  // the docs dead now that ktop's selection counted alive (term_kth)
   std::vector<uint32_t> alive;
   if (deleted) {
     alive.assign((N + 31) / 32, 0);
     for (uint32_t d = 0; d < N; ++d)
       if (!deleted[d]) alive[d >> 5] |= 1u << (d & 31);
   }
-  if ((rc = score_index(ix.get(), g->n_docs, g->tot_tokens, g->df_text, g->df_name, alive, g->tot_facet_tokens,
-                        VF ? g->df_facet : nullptr, wts, base)))
-    return rc;
+  if (alive == base->h_alive.vec()) {
+    ix->h_alive = base->h_alive;
+    ix->alive_hold = base->alive_hold;
+  } else if (alive.empty()) {
+    ix->d.alive = nullptr;
+  } else {
+    HIPCHK(hipSetDevice(ix->dev));
+    auto m = std::make_shared<DevAllocs>();
+    m->dev = ix->dev;
+    uint32_t* d_alive = nullptr;
+    uint64_t b = 0;
+    if (int rc = dev_upload(*m, alive.data(), alive.size(), &d_alive, &b)) return rc;
+    ix->d.alive = d_alive;
+    ix->alive_hold = m;
+    ix->h_alive = std::move(alive);
+  }
+  {
+    uint64_t dead = 0;
+    const auto& now = ix->h_alive.vec();
+    const auto& then = ix->h_alive_b.vec();
+    for (uint32_t w = 0; w < (N + 31) / 32; ++w) {
+      const uint32_t valid = (w + 1) * 32 <= N ? 0xFFFFFFFFu : (1u << (N & 31)) - 1u;
+      const uint32_t a0 = then.empty() ? valid : then[w], a1 = now.empty() ? valid : now[w];
+      dead += (uint32_t)__builtin_popcount(a0 & ~a1 & valid);
+    }
+    ix->n_dead = (uint32_t)std::min<uint64_t>(dead, 0xFFFFFFFFu);
+  }
   *out = ix.release();
   return FG_OK;
 }
@@ -1886,8 +1930,7 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
     outs[i] = nullptr;
   }
   if (n == 0) return FG_OK;
-  // the weights once for every snapshot (they depend on the statistics only),
-  // and once on the device when the snapshots share one
+  // the weights once for every snapshot (they depend on the statistics only)
   fgh::Weights wts;
   {
     std::vector<float> wt, wn;
@@ -1895,63 +1938,17 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
     wts.wt = std::move(wt);
     wts.wn = std::move(wn);
   }
-  bool one_dev = true;
-  for (uint32_t i = 1; i < n; ++i) one_dev &= bases[i]->dev == bases[0]->dev;
-  void* d_w = nullptr;
-  if (one_dev && n > 1) {
-    HIPCHK(hipSetDevice(bases[0]->dev));
-    if (fgh::dev_malloc_async(&d_w, 8ull * V, kBuildStream) == hipSuccess) {
-      const hipError_t e1 = hipMemcpyAsync(d_w, wts.wt.data(), 4ull * V, hipMemcpyHostToDevice, kBuildStream);
-      const hipError_t e2 = hipMemcpyAsync(static_cast<float*>(d_w) + V, wts.wn.data(), 4ull * V, hipMemcpyHostToDevice,
-                                           kBuildStream);
-      const hipError_t e3 = hipStreamSynchronize(kBuildStream);
-      if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
-        (void)hipFreeAsync(d_w, kBuildStream);
-        return fail(FG_EHIP, "rescore weights upload: %s", hipGetErrorString(e1 ? e1 : e2 ? e2 : e3));
-      }
-      wts.d_w = static_cast<const float*>(d_w);
-      wts.dev = bases[0]->dev;
-    } else {
-      (void)hipGetLastError();
-      d_w = nullptr;  // each snapshot uploads its own
-    }
-  }
-  std::vector<int> rc(n, FG_OK);
-  std::vector<std::string> err(n);
-  std::atomic<uint32_t> next{0};
-  std::atomic<uint32_t> slot{0};
-  auto worker = [&] {
-    const hipStream_t saved = tl_build_stream;
-    for (uint32_t i; (i = next.fetch_add(1)) < n;) {
-      const int dev = bases[i]->dev;
-      if (hipSetDevice(dev) == hipSuccess)
-        if (hipStream_t st = background_stream(dev, slot.fetch_add(1))) tl_build_stream = st;
-      if ((rc[i] = rescore_one(bases[i], g, deleted ? deleted[i] : nullptr, &outs[i], &wts))) err[i] = fg_last_error();
-      tl_build_stream = saved;
-    }
-  };
-  std::vector<std::thread> th;
-  for (uint32_t t = 1; t < std::min<uint32_t>(n, 8); ++t) th.emplace_back(worker);
-  worker();
-  for (auto& x : th) x.join();
-  bool any_fail = false;
-  for (uint32_t i = 0; i < n; ++i) any_fail |= rc[i] != FG_OK;
-  if (d_w) {
-    // a successful scoring waited for its kernels (its read-back); a failed one
-    // may have left some reading the weights
-    (void)hipSetDevice(wts.dev);
-    if (any_fail) (void)hipDeviceSynchronize();
-    (void)hipFreeAsync(d_w, kBuildStream);
-  }
-  for (uint32_t i = 0; i < n; ++i)
-    if (rc[i]) {
+  for (uint32_t i = 0; i < n; ++i) {
+    if (int rc = rescore_one(bases[i], g, deleted ? deleted[i] : nullptr, &outs[i], &wts)) {
+      const std::string e = fg_last_error();
       for (uint32_t j2 = 0; j2 < n; ++j2)
         if (outs[j2]) {
           fg_index_release(outs[j2]);
           outs[j2] = nullptr;
         }
-      return fail(rc[i], "snapshot %u: %s", i, err[i].c_str());
+      return fail(rc, "snapshot %u: %s", i, e.c_str());
     }
+  }
   return FG_OK;
 }
 
@@ -2007,8 +2004,7 @@ uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term) {
 int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out) {
   if (!ix || !out) return fail(FG_EINVAL, "bad arguments");
   static_assert(fg::kNumTopK == 5, "fugu.h documents five K");
-  for (uint32_t k = 0; k < fg::kNumTopK; ++k)
-    out[k] = term < ix->n_terms ? ix->ktop[(size_t)term * fg::kNumTopK + k] : 0.0f;
+  for (uint32_t k = 0; k < fg::kNumTopK; ++k) out[k] = fgh::term_kth_now(ix, term, fg::kTopKs[k], false);
   return FG_OK;
 }
 
@@ -2029,12 +2025,15 @@ int fg_index_term_ladder(const fg_index* ix, float* out) {
   } back{tmp};
   float* d = static_cast<float*>(tmp);
   HIPCHK(hipMemsetAsync(d, 0, 4 * (nm + nx), kBuildStream));
+  // the posting scores under the snapshot's statistics (a temporary), then k_ktop with the extra levels
   fg::ScoreJob j{};
-  j.doc = ix->d.doc;
-  j.off = ix->d.off;
+  void* ptmp = nullptr;
+  if (int rc = score_postings(ix, j, nullptr, &ptmp)) return rc;
+  struct PBack {
+    void* p;
+    ~PBack() { (void)hipFreeAsync(p, kBuildStream); }
+  } pback{ptmp};
   j.alive = ix->d.alive;
-  j.psc = const_cast<float*>(ix->d.psc);  // read only by k_ktop*
-  j.n_terms = V;
   j.ktop = d;
   j.ladder = d + nm;
   if (int rc = ktop_pass(ix, j)) return rc;
@@ -2153,7 +2152,7 @@ struct WItem { double key; uint32_t q, c, n; };
 struct HostPlan {
   std::vector<uint32_t> q_m, q_terms, lead, nchunk, q_filter;
   std::vector<uint64_t> thr0;
-  std::vector<float> q_ub;
+  std::vector<float> q_ub, q_wt, q_wn, q_rup;
   uint32_t nf = 0;
   std::vector<uint32_t> f_shift;
   std::vector<uint64_t> f_woff;
@@ -2185,6 +2184,9 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   nchunk.assign(nq, 0);
   thr0.assign(nq, 0);
   q_ub.assign((size_t)nq * fg::kMaxTerms, 0.0f);
+  h.q_wt.assign((size_t)nq * fg::kMaxTerms, 0.0f);
+  h.q_wn.assign((size_t)nq * fg::kMaxTerms, 0.0f);
+  h.q_rup.assign((size_t)nq * fg::kMaxTerms, 1.0f);
 
   // ---- facet filters: one mask per distinct clause list (fg_internal.h DevFilters)
   auto& q_filter = h.q_filter;
@@ -2272,14 +2274,8 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   // over all its slots (C4, 8 x 1.25M namespaces: k_conj 1.300 -> 1.085 ms, /16
   // 1.065 ms, identical hits: profiles/r05/ab/c4_ab_r05q.json; round 4 measured
   // the opposite before the sparse rank words and the XCD split);
-  // FUGU_CONJ_SEG_DIV overrides the divisor (1: per-snapshot counts)
-  // FUGU_CONJ_GPQ / FUGU_CONJ_MAXGROUP (A/B): kConjGroupsPerQuery / kMaxGroup
-  const char* gqe = getenv("FUGU_CONJ_GPQ");
-  const uint32_t conj_gpq = gqe && *gqe ? (uint32_t)std::max(1, atoi(gqe)) : fg::kConjGroupsPerQuery;
-  const char* mge = getenv("FUGU_CONJ_MAXGROUP");
-  const uint32_t conj_maxg = mge && *mge ? (uint32_t)std::max(1, atoi(mge)) : fg::kMaxGroup;
-  const char* cde = getenv("FUGU_CONJ_SEG_DIV");
-  const uint32_t cdiv = n_segs <= 1 ? 1u : cde && *cde ? (uint32_t)std::max(1, atoi(cde)) : n_segs;
+  const uint32_t conj_gpq = fg::kConjGroupsPerQuery, conj_maxg = fg::kMaxGroup;
+  const uint32_t cdiv = n_segs <= 1 ? 1u : n_segs;
   auto &citems = h.citems, &ditems = h.ditems, &scan = h.scan;
   auto &ngroup = h.ngroup, &q_hlo = h.q_hlo, &q_hhi = h.q_hhi, &q_hsh = h.q_hsh;
   ngroup.assign(nq, 0);
@@ -2287,13 +2283,14 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   q_hhi.assign(nq, 0x3F800000u);
   q_hsh.assign(nq, 31);
   auto present = [&](uint32_t t) { return t < ix->n_terms && ix->off[t + 1] > ix->off[t]; };
-  // the term's K-th best alive score at level j: the snapshot's own, or the
-  // namespace-wide floor of a doc-sharded namespace's shard when higher
-  // (fg_index_set_kth_floor)
-  const std::shared_ptr<const std::vector<float>> floor = std::atomic_load(&ix->kth_floor);
-  auto kth = [&](uint32_t t, uint32_t j) {
-    const size_t x = (size_t)t * fg::kNumTopK + j;
-    return floor ? std::max(ix->ktop[x], (*floor)[x]) : ix->ktop[x];
+  // a clause's query-time weights and bound factor (DevPlan::q_wt / q_wn / q_rup)
+  auto set_clause = [&](uint32_t i, uint32_t j, uint32_t t) {
+    const size_t x = (size_t)i * fg::kMaxTerms + j;
+    h.q_wt[x] = ix->w_text[t];
+    h.q_wn[x] = ix->w_name[t];
+    float rdn, rup;
+    fgh::term_ratio(ix, t, &rdn, &rup);
+    h.q_rup[x] = rup;
   };
   // histogram bins of query i: bin 0 at the starting threshold (or ub / 256), the
   // top bin at the query's largest possible score ub; ~kQBins bins between
@@ -2364,6 +2361,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
         dhi = std::max(dhi, ix->last_doc[ts_[j]]);
       }
       for (uint32_t j = 0; j < nx; ++j) qt[ns + j] = tx[j];
+      for (uint32_t j = 0; j < ns + nx; ++j) set_clause(i, j, qt[j]);
       q_m[i] = fg::qm_pack(ns + nx, 0, nx);
       if (q_filter[i] != 0xFFFFFFFFu) {
         dlo = std::max(dlo, f_lo[q_filter[i]]);
@@ -2373,15 +2371,13 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       // starting threshold: the best per-clause K'-th score for the smallest stored
       // K' >= k (unfiltered and unexcluded only: a filter or an exclusion may
       // remove a term's best docs)
-      for (uint32_t j = 0; j < fg::kNumTopK && q_filter[i] == 0xFFFFFFFFu && nx == 0; ++j) {
-        if (fg::kTopKs[j] < k) continue;
+      if (q_filter[i] == 0xFFFFFFFFu && nx == 0) {
         float v = 0.0f;
-        for (uint32_t c = 0; c < ns; ++c) v = std::max(v, kth(qt[c], j));
+        for (uint32_t c = 0; c < ns; ++c) v = std::max(v, fgh::term_kth_now(ix, qt[c], k, true));
         if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
-        break;
       }
       float ub = fmx;
-      for (uint32_t c = 0; c < ns; ++c) ub += ix->tmaxs[qt[c]];
+      for (uint32_t c = 0; c < ns; ++c) ub += fgh::term_max_now(ix, qt[c]);
       set_bins(i, ub);
 
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
@@ -2415,6 +2411,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     for (uint32_t j = 0; j < nx; ++j) qt[nm + j] = tx[j];
     for (uint32_t j = 0; j < ns; ++j) qt[nm + nx + j] = ts_[j];
     const uint32_t mt = nm + nx + ns;
+    for (uint32_t j = 0; j < mt; ++j) set_clause(i, j, qt[j]);
     q_m[i] = fg::qm_pack(mt, nm, nx);
     // MaxScore suffix bounds of the probed lists (k_conj prunes a candidate once its
     // partial score plus these cannot reach the query's threshold): the Must and
@@ -2422,7 +2419,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     {
       float acc = 0.0f;
       for (uint32_t j = mt; j-- > 1;) {
-        if (j < nm || j >= nm + nx) acc += ix->tmaxs[qt[j]];
+        if (j < nm || j >= nm + nx) acc += fgh::term_max_now(ix, qt[j]);
         q_ub[(size_t)i * fg::kMaxTerms + j] = acc;
       }
     }
@@ -2430,16 +2427,14 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     // the query's k-th best from below, so k_conj starts from that threshold and
     // skips the lead chunks whose block-max cannot reach it (the block-max
     // pruning tantivy's TopDocs runs on a single TermScorer: block_wand_single_scorer)
-    for (uint32_t j = 0; j < fg::kNumTopK && mt == 1 && q_filter[i] == 0xFFFFFFFFu; ++j) {
-      if (fg::kTopKs[j] < k) continue;
-      const float v = kth(qt[0], j);
+    if (mt == 1 && q_filter[i] == 0xFFFFFFFFu) {
+      const float v = fgh::term_kth_now(ix, qt[0], k, true);
       if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
-      break;
     }
     {
-      float ub = fmx + ix->tmaxs[qt[0]];
+      float ub = fmx + fgh::term_max_now(ix, qt[0]);
       for (uint32_t j = 1; j < mt; ++j)
-        if (j < nm || j >= nm + nx) ub += ix->tmaxs[qt[j]];
+        if (j < nm || j >= nm + nx) ub += fgh::term_max_now(ix, qt[j]);
       set_bins(i, ub);
     }
     const uint64_t df0 = ix->off[qt[0] + 1] - ix->off[qt[0]];
@@ -2505,13 +2500,14 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // ---- join the snapshots' tables (one snapshot: its own, moved)
   std::vector<uint32_t> q_m, q_terms, lead, q_filter, ngroup, q_hlo, q_hhi, q_hsh, f_shift, f_seg, ch_f, ch_c, ch_t, ch_s;
   std::vector<uint64_t> thr0, f_woff;
-  std::vector<float> q_ub, f_tab, f_max;
+  std::vector<float> q_ub, q_wt, q_wn, q_rup, f_tab, f_max;
   std::vector<WItem> citems, ditems, scan;
   uint32_t nf = 0;
   if (S == 1) {
     HostPlan& h = hs[0];
     q_m.swap(h.q_m); q_terms.swap(h.q_terms); lead.swap(h.lead); q_filter.swap(h.q_filter); ngroup.swap(h.ngroup);
     q_hlo.swap(h.q_hlo); q_hhi.swap(h.q_hhi); q_hsh.swap(h.q_hsh); thr0.swap(h.thr0); q_ub.swap(h.q_ub);
+    q_wt.swap(h.q_wt); q_wn.swap(h.q_wn); q_rup.swap(h.q_rup);
     f_shift.swap(h.f_shift); f_woff.swap(h.f_woff); f_tab.swap(h.f_tab); f_max.swap(h.f_max);
     ch_f.swap(h.ch_f); ch_c.swap(h.ch_c); ch_t.swap(h.ch_t); ch_s.swap(h.ch_s);
     citems.swap(h.citems); ditems.swap(h.ditems); scan.swap(h.scan);
@@ -2523,7 +2519,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
       HostPlan& h = hs[s];
       const uint32_t fb = nf, vb = s * nq1;
       cat(q_m, h.q_m); cat(q_terms, h.q_terms); cat(lead, h.lead); cat(ngroup, h.ngroup); cat(thr0, h.thr0);
-      cat(q_ub, h.q_ub);
+      cat(q_ub, h.q_ub); cat(q_wt, h.q_wt); cat(q_wn, h.q_wn); cat(q_rup, h.q_rup);
       for (uint32_t f : h.q_filter) q_filter.push_back(f == 0xFFFFFFFFu ? f : fb + f);
       cat(f_shift, h.f_shift); cat(f_tab, h.f_tab); cat(f_max, h.f_max);
       const uint64_t wb = f_woff.back();
@@ -2579,43 +2575,46 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // second list, ab_xcd_part.json: L2 hit rate 0.32 -> 0.23, DRAM 4.09 -> 4.57
   // GB, each XCD walks the whole doc range for fewer queries).  The same split of k_disj by
   // densest clause: OR top-20 2.78 -> 3.30 ms, top-1000 5.26 -> 6.86 ms -- its
-  // sweep stays doc-ordered.  FUGU_XCD_PART=0: the doc sweep for k_conj (A/B).
-  const char* xp = getenv("FUGU_XCD_PART");
-  const bool xcd_part = !(xp && *xp == '0');
+  // sweep stays doc-ordered.
+  constexpr bool xcd_part = true;
   std::vector<uint8_t> q_grp;
   auto groups = [&](const std::vector<W>& items) {
     q_grp.assign(nq, 0);
-    std::map<uint32_t, uint64_t> load;  // probed term -> items
-    // FUGU_XCD_KEY (A/B): 0 the lead list (default: ab_xcd_key_balanced.log,
-    // and3 1.001 vs 1.009 ms by the second list), 1 the second list, 2 the last
-    // list, q the query itself (groups by items alone)
-    const char* xk = getenv("FUGU_XCD_KEY");
-    const char key = xk && *xk ? *xk : '0';
-    auto probe_term = [&](uint32_t qv) {
-      const uint32_t* qt = q_terms.data() + (size_t)qv * fg::kMaxTerms;
-      const uint32_t mt = fg::qm_terms(q_m[qv]);
-      if (key == 'q') return 0x80000000u | qv;
-      if (key == 's') return 0x40000000u | (qv / nq1);  // the slot's snapshot (a multi-snapshot plan)
-      if (key == '0' || mt == 1) return qt[0];
-      if (key == '2') return qt[mt - 1];
-      return qt[1];
-    };
+    // grouped by the lead list (ab_xcd_key_balanced.log: and3 1.001 ms, against 1.009
+    // by the second list; the last list, the query alone and the slot's snapshot
+    // measured no better)
+    auto probe_term = [&](uint32_t qv) { return q_terms[(size_t)qv * fg::kMaxTerms]; };
     // the multi-list items only (single-list ones keep the sweep and run as a
-    // launch of their own, k_conj<true> over the first n_single items)
+    // launch of their own, k_conj<true> over the first n_single items); the
+    // (term, items) counts by sorting the items' terms (a map per item cost
+    // ~1 ms of an 8-snapshot batch's planning)
+    std::vector<uint32_t> ts;
+    ts.reserve(items.size());
     for (const W& x : items)
-      if (!single(x)) load[probe_term(x.q)]++;
-    std::vector<std::pair<uint64_t, uint32_t>> by;
-    for (auto& kv : load) by.emplace_back(kv.second, kv.first);
+      if (!single(x)) ts.push_back(probe_term(x.q));
+    std::sort(ts.begin(), ts.end());
+    std::vector<std::pair<uint64_t, uint32_t>> by;  // (items, term)
+    for (size_t i = 0; i < ts.size();) {
+      size_t j = i;
+      while (j < ts.size() && ts[j] == ts[i]) ++j;
+      by.emplace_back(j - i, ts[i]);
+      i = j;
+    }
     std::sort(by.begin(), by.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
     uint64_t gl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    std::map<uint32_t, uint8_t> tg;
+    std::vector<std::pair<uint32_t, uint8_t>> tg;  // (term, group), by term
+    tg.reserve(by.size());
     for (auto& [cnt, t] : by) {
       const uint32_t g = (uint32_t)(std::min_element(gl, gl + 8) - gl);
       gl[g] += cnt;
-      tg[t] = (uint8_t)g;
+      tg.emplace_back(t, (uint8_t)g);
     }
+    std::sort(tg.begin(), tg.end());
     for (const W& x : items)
-      if (!single(x)) q_grp[x.q] = tg[probe_term(x.q)];
+      if (!single(x)) {
+        const uint32_t t = probe_term(x.q);
+        q_grp[x.q] = std::lower_bound(tg.begin(), tg.end(), std::make_pair(t, (uint8_t)0))->second;
+      }
   };
   auto radix = [&](std::vector<W>& items, bool conj) {
     const size_t n = items.size();
@@ -2683,6 +2682,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   const size_t s_qm = al(4ull * nq), s_qt = al(4ull * nq * fg::kMaxTerms), s_lead = al(4ull * nq),
                s_wq = al(4ull * chunks), s_wc = al(4ull * chunks), s_wn = al(4ull * chunks),
                s_co = al(8ull * (nq + 1)), s_t0 = al(8ull * nq), s_ub = al(4ull * nq * fg::kMaxTerms),
+               s_cache = al(4ull * 512 * S),
                s_qf = al(4ull * nq), s_fs = al(4ull * nf),
                s_fw = al(8ull * nf), s_ft = al(4ull * nf * 256), s_fm = al(4ull * nf), s_ch = al(4ull * nch),
                s_hb = al(4ull * nq), s_fg = S > 1 ? al(4ull * nf) : 0,
@@ -2697,8 +2697,16 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     }
     if (b > 0xFFFFFFFFull) seg_base.clear();  // no merged select past 2^32 docs
   }
-  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + s_ub + s_qf + s_fs + s_fw + s_ft +
-                      s_fm + 4 * s_ch + 2 * s_hb + s_fg + s_sg + s_sb;
+  // the snapshots' tf caches (query-time scoring, DevIndex::cache): one copy per
+  // distinct set of statistics (a namespace's segments share one)
+  std::vector<uint32_t> cache_of(S, 0);
+  for (uint32_t x = 0; x < S; ++x) {
+    uint32_t c = 0;
+    while (c < x && std::memcmp(ixs[cache_of[c]]->cache, ixs[x]->cache, sizeof ixs[x]->cache) != 0) ++c;
+    cache_of[x] = c < x ? cache_of[c] : x;  // x: the first snapshot with these statistics
+  }
+  const size_t s_in = s_qm + s_qt + s_lead + s_wq + s_wc + s_wn + s_co + s_t0 + 4 * s_ub + s_cache + s_qf + s_fs + s_fw +
+                      s_ft + s_fm + 4 * s_ch + 2 * s_hb + s_fg + s_sg + s_sb;
   // one score histogram per query (DevPlan::hist: k_conj's and k_disj's running thresholds)
   // (thresholds and histograms: one per batch query, shared by its slots)
   const size_t s_thr = al(8ull * nq1), s_cc = al(4ull * nq), s_mask = al(4ull * f_woff[nf]),
@@ -2751,6 +2759,23 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->d.cand_off = (const uint64_t*)put(cand_off.data(), 8ull * (nq + 1), s_co);
   p->d.q_thr0 = (const uint64_t*)put(thr0.data(), 8ull * nq, s_t0);
   p->d.q_ub = (const float*)put(q_ub.data(), 4ull * nq * fg::kMaxTerms, s_ub);
+  p->d.q_wt = (const float*)put(q_wt.data(), 4ull * nq * fg::kMaxTerms, s_ub);
+  p->d.q_wn = (const float*)put(q_wn.data(), 4ull * nq * fg::kMaxTerms, s_ub);
+  p->d.q_rup = (const float*)put(q_rup.data(), 4ull * nq * fg::kMaxTerms, s_ub);
+  std::vector<const float*> d_cache(S, nullptr);
+  {
+    const size_t o0 = o;
+    for (uint32_t x = 0; x < S; ++x) {
+      if (cache_of[x] != x) continue;
+      std::memcpy(staging + o, ixs[x]->cache, 4ull * 512);
+      d_cache[x] = (const float*)(base + o);
+      o += 4ull * 512;
+    }
+    for (uint32_t x = 0; x < S; ++x) d_cache[x] = d_cache[cache_of[x]];
+    o = o0 + s_cache;
+  }
+  p->d0 = ix->d;
+  p->d0.cache = d_cache[0];
   p->d.f.q_filter = (const uint32_t*)put(q_filter.data(), 4ull * nq, s_qf);
   p->d.f.f_shift = (const uint32_t*)put(f_shift.data(), 4ull * nf, s_fs);
   p->d.f.f_woff = (const uint64_t*)put(f_woff.data(), 8ull * nf, s_fw);
@@ -2764,7 +2789,10 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->d.q_hsh = (const uint32_t*)put(q_hsh.data(), 4ull * nq, s_hb);
   if (S > 1) {
     std::vector<fg::DevIndex> segs(S);
-    for (uint32_t s = 0; s < S; ++s) segs[s] = ixs[s]->d;
+    for (uint32_t s = 0; s < S; ++s) {
+      segs[s] = ixs[s]->d;
+      segs[s].cache = d_cache[s];
+    }
     p->d.f.f_seg = (const uint32_t*)put(f_seg.data(), 4ull * nf, s_fg);
     p->d.segs = (const fg::DevIndex*)put(segs.data(), sizeof(fg::DevIndex) * S, s_sg);
     const uint32_t* sb = (const uint32_t*)put(seg_base.data(), 4ull * seg_base.size(), s_sb);
@@ -2812,6 +2840,9 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->d.k = k;
   p->d.seg_nq = S > 1 ? nq1 : 0;
   p->d.n_segs = S;
+  p->d.feat = 0;
+  for (uint32_t x = 0; x < S; ++x)
+    p->d.feat |= (ixs[x]->d.tfn_name ? 1u : 0u) | (ixs[x]->d.n_esc ? 2u : 0u);
   // several snapshots: a batch query's slots share its threshold score-only, so a
   // doc of another snapshot tied with the k-th score is never pruned (the merge
   // breaks such ties by snapshot)
@@ -2845,13 +2876,13 @@ static int execute_impl(fg_plan* p, hipStream_t s, float* os, uint32_t* od, uint
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventRecord(ev[0], s));
   }
-  if (first && p->d.f.n_chunks) HIPCHK(fg::launch_fmask(p->ix->d, p->d, s));
-  if (first && p->d.n_conj) HIPCHK(fg::launch_conj(p->ix->d, p->d, s));
+  if (first && p->d.f.n_chunks) HIPCHK(fg::launch_fmask(p->d0, p->d, s));
+  if (first && p->d.n_conj) HIPCHK(fg::launch_conj(p->d0, p->d, s));
   const uint32_t nd = p->d.total_chunks - p->d.n_conj;
   const uint32_t a = first ? 0u : (uint32_t)std::min<double>(nd, std::llround(from * nd));
   const uint32_t b = last ? nd : (uint32_t)std::min<double>(nd, std::llround(to * nd));
-  if (b > a) HIPCHK(fg::launch_disj(p->ix->d, p->d, s, a, b - a));
-  if (last && p->d.n_scan) HIPCHK(fg::launch_scan(p->ix->d, p->d, s));
+  if (b > a) HIPCHK(fg::launch_disj(p->d0, p->d, s, a, b - a));
+  if (last && p->d.n_scan) HIPCHK(fg::launch_scan(p->d0, p->d, s));
   if (p->profile) HIPCHK(hipEventRecord(ev[1], s));
   if (last) HIPCHK(fg::launch_final(p->d, os, od, on, s, oshard));
   if (p->profile) {
@@ -3149,215 +3180,6 @@ class ShardWorkers {
 
 static void run_parallel(uint32_t n, const std::function<void(uint32_t)>& f) { ShardWorkers::get().run(n, f); }
 
-// Side streams of fg_search_sharded, per device, created once and shared by
-// every caller (a stream takes work from any thread; each call orders its own
-// work with events)
-static constexpr uint32_t kSideStreams = 8;
-static hipStream_t side_stream(int dev, uint32_t i) {
-  static std::mutex mu;
-  static std::map<int, std::vector<hipStream_t>> pool;
-  std::lock_guard<std::mutex> l(mu);
-  auto& v = pool[dev];
-  while (v.size() <= i) {
-    hipStream_t st = nullptr;
-    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
-      return nullptr;
-    v.push_back(st);
-  }
-  return v[i];
-}
-
-// One batch over several shards / segments / namespaces of one logical index
-// (SURVEY.md §8b fg_search_sharded, §8e).  Every shard's top-k lists land in
-// gathered buffers on the first shard's device -- directly, or over xGMI
-// (hipMemcpyPeerAsync) from the shard's own device -- and k_merge_rank merges
-// them there into (score desc, shard asc, doc asc): tantivy's merge_fruits over
-// DocAddress (segment_ord, doc).
-//   batch (>= 64 queries, > 1 shard): one host thread per shard plans it and
-//     launches it at once on a side stream of its device, so later shards are
-//     planned while earlier ones run and a device's shards overlap each other;
-//   otherwise (a single query: the host mirror's segment fan-out) everything
-//     runs inline on the calling thread's per-thread streams.
-static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q,
-                                    uint32_t k, float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
-  if (!shards || n_shards == 0 || n_shards > 64 || !q || k == 0 || !out_score || !out_doc || !out_n)
-    return fail(FG_EINVAL, "bad arguments");
-  for (uint32_t s = 0; s < n_shards; ++s) {
-    if (!shards[s]) return fail(FG_EINVAL, "NULL shard");
-    if (ctx && std::find(ctx->devs.begin(), ctx->devs.end(), shards[s]->dev) == ctx->devs.end())
-      return fail(FG_EINVAL, "a shard lives on a device outside the context");
-  }
-  const uint32_t nq = q->n_queries;
-  if (nq == 0) return FG_OK;
-  if (k > FG_MAX_K) return fail(FG_EUNSUPPORTED, "k > FG_MAX_K");
-  // ---- gathered lists + merged output on the first shard's device (its pool)
-  const int dev0 = shards[0]->dev;
-  const size_t nk = (size_t)nq * k;
-  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t g_s = al(4 * nk * n_shards), g_n = al(4ull * nq * n_shards), o_k = al(4 * nk), o_n = al(4ull * nq);
-  const size_t total = 2 * g_s + g_n + 3 * o_k + o_n;
-  size_t got = 0;
-  HIPCHK(hipSetDevice(dev0));
-  char* base = static_cast<char*>(shards[0]->pool->get(total, &got));
-  if (!base) return fail(FG_EOOM, "hipMalloc of the shard merge buffers failed");
-  float* gs = reinterpret_cast<float*>(base);
-  uint32_t* gd = reinterpret_cast<uint32_t*>(base + g_s);
-  uint32_t* gn = reinterpret_cast<uint32_t*>(base + 2 * g_s);
-  float* ms = reinterpret_cast<float*>(base + 2 * g_s + g_n);
-  uint32_t* md = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + o_k);
-  uint32_t* msh = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 2 * o_k);
-  uint32_t* mn = reinterpret_cast<uint32_t*>(base + 2 * g_s + g_n + 3 * o_k);
-  // per shard: its plan, the stream it ran on, the event the merge waits for
-  const bool threaded = nq >= 64 && n_shards > 1;
-  std::vector<std::unique_ptr<fg_plan>> plans(n_shards);
-  std::vector<hipStream_t> sst(n_shards, nullptr);
-  std::vector<hipEvent_t> evs(n_shards, nullptr);
-  std::vector<int> rcs(n_shards, FG_OK);
-  std::vector<std::string> errs(n_shards);
-  // teardown (also on error returns): every stream drained, then the events,
-  // the plans (their destructors sync their own streams) and the buffers
-  struct Back {
-    fg_index* const* sh; uint32_t ns; void* p; size_t n;
-    std::vector<hipStream_t>& st; std::vector<hipEvent_t>& ev;
-    ~Back() {
-      for (uint32_t s = 0; s < ns; ++s) {
-        (void)hipSetDevice(sh[s]->dev);
-        (void)hipStreamSynchronize(st[s] ? st[s] : hipStreamPerThread);
-        if (ev[s]) (void)hipEventDestroy(ev[s]);
-      }
-      // the merge and its copies run on the first device's per-thread stream:
-      // drained before the buffers go back to the pool (an error return may
-      // leave them in flight)
-      (void)hipSetDevice(sh[0]->dev);
-      (void)hipStreamSynchronize(hipStreamPerThread);
-      sh[0]->pool->put(p, n);
-    }
-  } back{shards, n_shards, base, got, sst, evs};
-  // every shard of a multi-shard call runs on a side stream of its device, so a
-  // single query's shards overlap on the GPU too
-  if (n_shards > 1)
-    for (uint32_t s = 0, nth = 0; s < n_shards; ++s, nth = 0) {
-      for (uint32_t t = 0; t < s; ++t) nth += shards[t]->dev == shards[s]->dev ? 1u : 0u;
-      if (!(sst[s] = side_stream(shards[s]->dev, nth % kSideStreams))) return fail(FG_EHIP, "side stream creation failed");
-    }
-  // 1. plan every shard (one host thread per shard for a batch)
-  auto plan = [&](uint32_t s) -> int {
-    fg_plan* p = nullptr;
-    // inline (one query): the upload is queued on this thread's stream, ahead of
-    // the execute on the same stream -- no host round trip per shard
-    // a batch: planned on its shard's thread, uploaded on the shard's side
-    // stream (a fresh thread's per-thread stream would be created per call)
-    int rc = threaded ? plan_create(shards[s], q, k, &p, true, sst[s])
-                      : plan_create(shards[s], q, k, &p, false, sst[s] ? sst[s] : hipStreamPerThread);
-    if (rc) return rc;
-    plans[s].reset(p);
-    return FG_OK;
-  };
-  auto each = [&](auto&& f) {
-    if (threaded) {
-      ShardWorkers::get().run(n_shards, [&](uint32_t s) {
-        rcs[s] = f(s);
-        if (rcs[s]) errs[s] = fg_last_error();
-      });
-    } else {
-      for (uint32_t s = 0; s < n_shards; ++s)
-        if ((rcs[s] = f(s))) errs[s] = fg_last_error();
-    }
-    for (uint32_t s = 0; s < n_shards; ++s)
-      if (rcs[s]) return fail(rcs[s], "shard %u: %s", s, errs[s].c_str());
-    return FG_OK;
-  };
-  static const bool trace = getenv("FUGU_SHARD_TRACE") != nullptr;
-  auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  const double t_0 = trace ? now() : 0.0;
-  if (int rc = each(plan)) return rc;
-  const double t_plan = trace ? now() : 0.0;
-  // 2. the shards of one device share per-query thresholds (fg_plan_link): the
-  // merge keeps the k best across shards, so a shard need not keep a doc below
-  // the k-th best score any shard has found.  The shared state is zeroed once,
-  // before any of the device's shards runs.
-  std::vector<hipEvent_t> zev;
-  struct ZevBack {
-    std::vector<hipEvent_t>& v;
-    ~ZevBack() { for (hipEvent_t e : v) (void)hipEventDestroy(e); }
-  } zback{zev};
-  std::vector<int> owner(n_shards, -1);
-  for (uint32_t s = 0; s < n_shards; ++s) {
-    if (owner[s] >= 0) continue;
-    std::vector<fg_plan*> grp{plans[s].get()};
-    owner[s] = (int)s;
-    for (uint32_t t = s + 1; t < n_shards; ++t)
-      if (shards[t]->dev == shards[s]->dev) { grp.push_back(plans[t].get()); owner[t] = (int)s; }
-    // a single query gains little from shared thresholds over a few segments and
-    // would pay the link's synchronous uploads on its latency path
-    if (grp.size() < 2 || !threaded) continue;
-    if (int rc = fg_plan_link(grp.data(), (uint32_t)grp.size())) return rc;
-    fg_plan* o = plans[s].get();
-    HIPCHK(hipSetDevice(shards[s]->dev));
-    HIPCHK(hipMemsetAsync(o->zero_region, 0, o->zero_bytes, hipStreamPerThread));
-    o->zeroed = true;  // its execute skips the memset (it would wipe what the others share)
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    zev.push_back(e);
-    HIPCHK(hipEventRecord(e, hipStreamPerThread));
-    for (uint32_t t = s; t < n_shards; ++t)
-      if (owner[t] == (int)s && sst[t]) HIPCHK(hipStreamWaitEvent(sst[t], e, 0));
-  }
-  // 3. launch each shard, move its lists to dev0, record the event the merge waits for
-  auto run = [&](uint32_t s) -> int {
-    fg_plan* p = plans[s].get();
-    const int d = shards[s]->dev;
-    hipStream_t st = sst[s] ? sst[s] : hipStreamPerThread;
-    const bool local = d == dev0;
-    int rc = local ? fg_plan_execute(p, st, gs + s * nk, gd + s * nk, gn + (size_t)s * nq)
-                   : fg_plan_execute(p, st, nullptr, nullptr, nullptr);  // selects device d
-    if (rc) return rc;
-    if (!local) {
-      HIPCHK(hipMemcpyPeerAsync(gs + s * nk, dev0, p->own_score, d, 4 * nk, st));
-      HIPCHK(hipMemcpyPeerAsync(gd + s * nk, dev0, p->own_doc, d, 4 * nk, st));
-      HIPCHK(hipMemcpyPeerAsync(gn + (size_t)s * nq, dev0, p->own_n, d, 4ull * nq, st));
-    }
-    if (sst[s] || !local) {
-      HIPCHK(hipEventCreateWithFlags(&evs[s], hipEventDisableTiming));
-      HIPCHK(hipEventRecord(evs[s], st));
-    }
-    return FG_OK;
-  };
-  const double t_link = trace ? now() : 0.0;
-  if (int rc = each(run)) return rc;
-  const double t_run = trace ? now() : 0.0;
-  HIPCHK(hipSetDevice(dev0));
-  for (hipEvent_t e : evs)
-    if (e) HIPCHK(hipStreamWaitEvent(hipStreamPerThread, e, 0));
-  HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hipStreamPerThread));
-  if (trace) {
-    HIPCHK(hipStreamSynchronize(hipStreamPerThread));
-    fprintf(stderr, "[fg_search_sharded] nq %u shards %u threaded %d: plan %.3f link %.3f launch %.3f kernels+merge %.3f ms\n",
-            nq, n_shards, (int)threaded, t_plan - t_0, t_link - t_plan, t_run - t_link, now() - t_run);
-  }
-  // the merged lists are consecutive: one D2H into a pinned buffer (small batches)
-  const size_t span = 3 * o_k + 4ull * nq;
-  if (span <= (4ull << 20)) {
-    PinnedLease pin(*shards[0]->pinned, span);
-    if (pin.p) {
-      HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hipStreamPerThread));
-      HIPCHK(hipStreamSynchronize(hipStreamPerThread));
-      const char* h = static_cast<const char*>(pin.p);
-      std::memcpy(out_score, h, 4 * nk);
-      std::memcpy(out_doc, h + o_k, 4 * nk);
-      if (out_shard) std::memcpy(out_shard, h + 2 * o_k, 4 * nk);
-      std::memcpy(out_n, h + 3 * o_k, 4ull * nq);
-      return FG_OK;
-    }
-  }
-  HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
-  HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
-  if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hipStreamPerThread));
-  HIPCHK(hipMemcpyAsync(out_n, mn, 4ull * nq, hipMemcpyDeviceToHost, hipStreamPerThread));
-  HIPCHK(hipStreamSynchronize(hipStreamPerThread));
-  return FG_OK;
-}
-
 // One batch over several shards / segments / namespaces of one logical index
 // (SURVEY.md §8b fg_search_sharded, §8e).  The shards of each device run as ONE
 // multi-snapshot plan (fg_plan_create_multi: one upload, one launch per kernel,
@@ -3366,8 +3188,7 @@ static int search_sharded_per_shard(fg_ctx* ctx, fg_index* const* shards, uint32
 // (hipMemcpyPeerAsync) from another device -- and k_merge_rank merges them
 // there into (score desc, shard asc, doc asc): tantivy's merge_fruits over
 // DocAddress (segment_ord, doc).  Everything runs on the calling thread's
-// per-thread streams.  FUGU_SHARDED_PER_SHARD=1 selects the round-2 path (one
-// plan per shard, linked; A/B builds).
+// per-thread streams.
 }  // extern "C"
 namespace fgh {
 SearchTrace& search_trace() {
@@ -3388,8 +3209,6 @@ int fg_search_trace(int enable, double* out_ms, uint32_t n, uint64_t* calls) {
 
 int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, const fg_query_batch* q, uint32_t k,
                       float* out_score, uint32_t* out_doc, uint32_t* out_shard, uint32_t* out_n) {
-  static const bool per_shard = getenv("FUGU_SHARDED_PER_SHARD") != nullptr;
-  if (per_shard) return search_sharded_per_shard(ctx, shards, n_shards, q, k, out_score, out_doc, out_shard, out_n);
   if (!shards || n_shards == 0 || n_shards > FG_MAX_SEGMENTS || !q || k == 0 || !out_score || !out_doc || !out_n)
     return fail(FG_EINVAL, "bad arguments");
   for (uint32_t s = 0; s < n_shards; ++s) {
@@ -3477,12 +3296,9 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     // every shard on dev0 in one plan, a batch: its merged select writes the
     // merged lists directly (no per-shard lists, no k_merge_rank); a small batch
     // keeps one final select per shard (more workgroups in parallel: a single
-    // query over 8 segments 0.070 vs 0.077 ms p50).  FUGU_SHARDED_MERGED_MIN:
-    // the smallest batch that takes the merged select (A/B)
-    static const uint32_t merged_min = [] {
-      const char* e = getenv("FUGU_SHARDED_MERGED_MIN");
-      return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 256u;
-    }();
+    // query over 8 segments 0.070 vs 0.077 ms p50): the merged select from
+    // batches of merged_min queries (tools/multi_ab.py, round 3)
+    constexpr uint32_t merged_min = 256u;
     if (ng == 1 && gdev[0] == dev0 && S > 1 && p->d.seg_base && nq >= merged_min) {
       if (int rc = execute_impl(p, hs, ms, md, mn, msh)) return rc;
       merged = true;

@@ -202,27 +202,45 @@ struct LocalDict {
 };
 
 // Storage that never moves once published: a directory of atomic pointers to
-// fixed-size chunks.  One writer appends; readers index any slot published
-// before they looked (acquire on the chunk pointer) without a lock.
-template <class T, uint32_t kShift, uint32_t kMaxChunks>
+// chunks of GEOMETRIC sizes (chunk c holds 2^c << kFirstShift slots), so a small
+// namespace costs a few KB and a large one still a few dozen chunks (ADVICE r05:
+// fixed 2^18-entry directories and 4 MiB first chunks cost ~12 MiB per namespace).
+// One writer appends; readers index any slot published before they looked
+// (acquire on the chunk pointer) without a lock.
+template <class T, uint32_t kFirstShift>
 class ChunkDir {
-  std::unique_ptr<std::atomic<T*>[]> dir_{new std::atomic<T*>[kMaxChunks]()};
+  static constexpr uint32_t kMaxChunks = 48;
+  std::atomic<T*> dir_[kMaxChunks] = {};
   std::vector<std::unique_ptr<T[]>> own_;  // writer side
 
  public:
-  static constexpr size_t kChunk = size_t(1) << kShift;
-  T& at(size_t i) const { return dir_[i >> kShift].load(std::memory_order_acquire)[i & (kChunk - 1)]; }
+  // chunk of slot i and i's offset in it: chunk c covers [(2^c - 1) << s, (2^(c+1) - 1) << s)
+  static void locate(size_t i, uint32_t& c, size_t& o) {
+    const size_t x = (i >> kFirstShift) + 1;
+    c = 63u - (uint32_t)__builtin_clzll(x);
+    o = i - (((size_t(1) << c) - 1) << kFirstShift);
+  }
+  static size_t chunk_begin(uint32_t c) { return ((size_t(1) << c) - 1) << kFirstShift; }
+  static size_t chunk_size(uint32_t c) { return size_t(1) << (c + kFirstShift); }
+  T& at(size_t i) const {
+    uint32_t c;
+    size_t o;
+    locate(i, c, o);
+    return dir_[c].load(std::memory_order_acquire)[o];
+  }
   // the writer: slot i, its chunk allocated (and published) first if new
   T& slot(size_t i) {
-    const size_t c = i >> kShift;
+    uint32_t c;
+    size_t o;
+    locate(i, c, o);
     if (c >= kMaxChunks) throw std::length_error("ChunkDir full");
     T* p = dir_[c].load(std::memory_order_relaxed);
     if (!p) {
-      own_.emplace_back(new T[kChunk]());
+      own_.emplace_back(new T[chunk_size(c)]());
       p = own_.back().get();
       dir_[c].store(p, std::memory_order_release);
     }
-    return p[i & (kChunk - 1)];
+    return p[o];
   }
 };
 
@@ -248,23 +266,23 @@ struct TermDict {
     size_t mask;
     explicit Table(size_t n) : s(new std::atomic<uint64_t>[n]()), mask(n - 1) {}
   };
-  // entry of id: arena chunk << 40 | offset in it << 20 | length
-  ChunkDir<uint64_t, 16, 1u << 16> ent;
-  ChunkDir<char, 20, 1u << 16> arena;
-  size_t a_chunk = 0, a_pos = 0;  // writer: where the next term's bytes go
+  // entry of id: byte offset of the term in the arena << 20 | length (a term
+  // never straddles two arena chunks)
+  ChunkDir<uint64_t, 10> ent;
+  ChunkDir<char, 14> arena;
+  size_t a_pos = 0;  // writer: where the next term's bytes go
   std::atomic<uint32_t> n{0};
   std::atomic<Table*> cur;
   std::vector<std::unique_ptr<Table>> tables;  // writer: current and retired
   TermDict() {
-    tables.emplace_back(new Table(1u << 16));
+    tables.emplace_back(new Table(1u << 10));
     cur.store(tables.back().get(), std::memory_order_release);
   }
   uint32_t size() const { return n.load(std::memory_order_acquire); }
   static uint64_t hash(std::string_view w) { return LocalDict::hash(w); }
   std::string_view key(uint32_t id) const {
     const uint64_t e = ent.at(id);
-    const char* c = &arena.at((e >> 40) << 20);
-    return std::string_view(c + ((e >> 20) & kMaxKey), e & kMaxKey);
+    return std::string_view(&arena.at(e >> 20), e & kMaxKey);
   }
   void prefetch(uint64_t h) const {
     const Table* t = cur.load(std::memory_order_relaxed);
@@ -292,13 +310,16 @@ struct TermDict {
     if (w.size() > kMaxKey) throw std::length_error("term longer than 1 MiB");
     const uint32_t id = n.load(std::memory_order_relaxed);
     if (2 * (size_t(id) + 1) > cur.load(std::memory_order_relaxed)->mask + 1) grow();
-    if (a_pos + w.size() > decltype(arena)::kChunk) {
-      ++a_chunk;
-      a_pos = 0;
+    for (;;) {  // the term's bytes inside one chunk: skip to the next chunk start until they fit
+      uint32_t c;
+      size_t o;
+      decltype(arena)::locate(a_pos, c, o);
+      if (w.empty() || o + w.size() <= decltype(arena)::chunk_size(c)) break;
+      a_pos = decltype(arena)::chunk_begin(c + 1);
     }
-    char* dst = &arena.slot((a_chunk << 20) + a_pos);  // publishes the chunk when new
-    std::memcpy(dst, w.data(), w.size());
-    ent.slot(id) = ((uint64_t)a_chunk << 40) | ((uint64_t)a_pos << 20) | w.size();
+    char* dst = &arena.slot(a_pos);  // publishes the chunk when new
+    if (!w.empty()) std::memcpy(dst, w.data(), w.size());
+    ent.slot(id) = ((uint64_t)a_pos << 20) | w.size();
     a_pos += w.size();
     n.store(id + 1, std::memory_order_release);
     put(*cur.load(std::memory_order_relaxed), h, id);
@@ -321,7 +342,7 @@ struct TermDict {
 // Only `deleted`, which the read path never touches, changes after an append.
 template <class Doc>
 class DocStore {
-  ChunkDir<Doc, 14, 1u << 18> c_;
+  ChunkDir<Doc, 8> c_;
   std::atomic<size_t> n_{0};
 
  public:

@@ -6,12 +6,14 @@
 //            chunks of the query's lead list, the lowest-cost term).  Each
 //            lane holds 8 lead candidates.  The other lists are probed in
 //            tantivy's intersection order (query/intersection.rs: children
-//            sorted by cost): a dense list through its doc-indexed score
-//            table, any other through the per-term doc -> position bucket
+//            sorted by cost): a dense list through its rank words (presence
+//            bits + rank), any other through the per-term doc -> position bucket
 //            directory (one directory load, then a branchless search inside
 //            the ~4-posting bucket), all 8 items in lockstep so their loads
-//            overlap.  Posting scores are precomputed at snapshot build with
-//            tantivy's Bm25Weight f32 arithmetic; before each probe a MaxScore
+//            overlap.  Posting scores are formed at query time from the
+//            posting's tf and fieldnorm id (DevIndex::tfn) with the query's
+//            BM25 weights, in tantivy's Bm25Weight f32 arithmetic (the statistics
+//            of the moment: a commit re-scores nothing); before each probe a MaxScore
 //            bound (partial score + the remaining lists' maxima) drops
 //            candidates that cannot reach the query's threshold.  Survivors
 //            are summed in tantivy's order (Intersection::score), compacted
@@ -69,9 +71,6 @@ __device__ inline uint32_t wave_id() { return threadIdx.x >> 6; }
 // threshold.
 __device__ inline float inflate_bound(float x) { return x * 1.00000762939453125f; }  // 1 + 2^-17
 
-// Term score at doc d through the term's dense structure (meta_slot != 0),
-// -1 = the term is absent from d.  Rank words: one 8-B load, and on a hit the
-// posting score at position rank + popcount(presence bits below d).
 // The rank word of doc d for rank-kind slot `slot`: plain, or sparse (block
 // entry, then the word: the zero word when the term has none of the word's docs).
 __device__ inline uint64_t rank_word_of(const DevIndex& ix, uint32_t slot, uint32_t d) {
@@ -89,13 +88,51 @@ __device__ inline const uint64_t* rank_base(const DevIndex& ix, uint32_t slot, u
   return ix.srank + (size_t)(slot - 1 - ix.n_prank) * ix.srank_blocks;
 }
 
-__device__ inline float dense_score(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t d) {
-  const uint32_t slot = meta_slot(meta);
-  if (meta_rank(meta)) {
-    const uint32_t p = rank_pos(rank_word_of(ix, slot, d), d);
-    return p == kInvalid ? -1.0f : ix.psc[base + p];
+// ---------------------------------------------------------------- query-time BM25
+
+// A posting's tf / fieldnorm payload: tfn (text) in the low half, tfn_name
+// (name, when the snapshot has name postings) in the high half.
+// kF (the plan's DevPlan::feat, a template argument of the search kernels): bit 0
+// some snapshot has `name` postings, bit 1 some posting's tf byte escaped.  The
+// common plan (neither) carries no name or escape code: query-time scoring then
+// fits the kernels' register budgets (k_conj 128 VGPRs at 4 waves, k_disj 96 at 5).
+constexpr uint32_t kFName = 1, kFEsc = 2;
+template <uint32_t kF>
+__device__ inline uint32_t tfn_load(const DevIndex& ix, uint64_t p) {
+  uint32_t v = ix.tfn[p];
+  if ((kF & kFName) && ix.tfn_name) v |= (uint32_t)ix.tfn_name[p] << 16;
+  return v;
+}
+// The posting's score for a clause of weights (wt, wn): Should(text:t, name:t)
+// summed from 0.0 (SumCombiner), each field's part tantivy's Bm25Weight::score
+// (field_score).  ct / cn: the text / name tf caches (LDS or the plan's copy).
+// tfn_score_fast takes the tf bytes as they are; a payload with an escaped tf
+// byte (tfn_escaped: tf >= 255, rare) is then scored again by tfn_score with
+// the posting's position, in a fix-up pass outside the hot loops' registers.
+template <uint32_t kF>
+__device__ inline float tfn_score_fast(uint32_t v, float wt, float wn, const float* ct, const float* cn) {
+  const uint32_t tt = v & 0xFFu, tn = (kF & kFName) ? (v >> 16) & 0xFFu : 0u;
+  float s = 0.0f;
+  if (tt) s += field_score(tt, (v >> 8) & 0xFFu, wt, ct);
+  if (tn) s += field_score(tn, v >> 24, wn, cn);
+  return s;
+}
+template <uint32_t kF>
+__device__ inline bool tfn_escaped(uint32_t v) {
+  return (kF & kFEsc) && ((v & 0xFFu) == kTfEsc || ((v >> 16) & 0xFFu) == kTfEsc);
+}
+__device__ inline float tfn_score(const DevIndex& ix, uint64_t p, uint32_t v, float wt, float wn, const float* ct,
+                                  const float* cn) {
+  uint32_t tt = v & 0xFFu, tn = (v >> 16) & 0xFFu;
+  if (tt == kTfEsc || tn == kTfEsc) {
+    const uint32_t e = tf_escaped(ix.esc_pos, ix.esc_tf, ix.n_esc, p);
+    if (tt == kTfEsc) tt = e & 0xFFFFu;
+    if (tn == kTfEsc) tn = e >> 16;
   }
-  return ix.dense[(size_t)(slot - 1) * ix.n_docs + d];
+  float s = 0.0f;
+  if (tt) s += field_score(tt, (v >> 8) & 0xFFu, wt, ct);
+  if (tn) s += field_score(tn, v >> 24, wn, cn);
+  return s;
 }
 
 // Upper bound of term t's score in doc d: the tile maximum (4096-doc tiles)
@@ -107,8 +144,7 @@ __device__ inline float term_bound(const DevIndex& ix, uint32_t meta, uint32_t t
 // Does term (meta, postings at base, directory at dir_off) hold doc d?  (MustNot probes)
 __device__ inline bool term_has_doc(const DevIndex& ix, uint32_t meta, uint64_t base, uint32_t dir_off, uint32_t d) {
   const uint32_t slot = meta_slot(meta);
-  if (slot && meta_rank(meta)) return (rank_word_of(ix, slot, d) >> (d & 31u)) & 1ull;
-  if (slot) return ix.dense[(size_t)(slot - 1) * ix.n_docs + d] >= 0.0f;
+  if (slot) return (rank_word_of(ix, slot, d) >> (d & 31u)) & 1ull;
   const uint32_t* __restrict__ dir = ix.dir + dir_off;
   const uint32_t b = d >> (meta & 0xFFu);
   uint32_t lo = dir[b], hi = dir[b + 1];
@@ -118,6 +154,23 @@ __device__ inline bool term_has_doc(const DevIndex& ix, uint32_t meta, uint64_t 
     if (di[mid] < d) lo = mid + 1; else hi = mid;
   }
   return lo < dir[b + 1] && di[lo] == d;
+}
+
+// Position of doc d in term t's list (kInvalid: absent), through its rank words
+// or its directory: the escaped-tf path recomputes it instead of keeping every
+// probe's position live through the payload loads (registers)
+__device__ inline uint32_t posting_pos(const DevIndex& ix, uint32_t t, uint32_t d) {
+  const uint32_t meta = ix.tmeta[t], slot = meta_slot(meta);
+  if (slot) return rank_pos(rank_word_of(ix, slot, d), d);
+  const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[t];
+  const uint32_t b = d >> (meta & 0xFFu);
+  uint32_t lo = dir[b], hi = dir[b + 1];
+  const uint32_t* __restrict__ di = ix.doc + ix.off[t];
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (di[mid] < d) lo = mid + 1; else hi = mid;
+  }
+  return lo < dir[b + 1] && di[lo] == d ? lo : kInvalid;
 }
 
 // DevPlan::pub_mask: a linked group's shared thresholds are published
@@ -318,6 +371,7 @@ static_assert(kTrunc + kDeferCap <= kBuf, "a flush after truncation must fit the
 
 struct ConjShared {
   alignas(16) uint64_t buf[kBuf];
+  float cache[512];  // the snapshot's tf caches (text, then name): DevIndex::cache
   uint32_t hist[1u << kConjHistBits];
   uint32_t scratch[8];
   uint32_t n_buf;
@@ -392,20 +446,22 @@ __device__ uint32_t flush_candidates(const DevPlan& pl, uint32_t q, const uint64
 }
 
 // Term ti's score at the doc of each live item (-1: the term is absent from
-// it), through the term's rank words, its f32 score table or its bucket
-// directory; the N items' loads are in flight together.
-template <uint32_t N>
+// it), through the term's rank words or its bucket directory, then the hits'
+// tf / fieldnorm payloads and their query-time scores (weights wt / wn, caches
+// ct / cn); the N items' loads are in flight together.
+template <uint32_t N, uint32_t kF>
 __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_t (&doc)[N], uint32_t live,
-                                  float (&sc)[N]) {
+                                  float wt, float wn, const float* ct, const float* cn, float (&sc)[N]) {
   const uint32_t meta = ix.tmeta[ti];
   const uint32_t dslot = meta_slot(meta);
-  if (dslot && meta_rank(meta)) {
+  const uint64_t bi = ix.off[ti];
+  uint32_t pos[N];
+  if (dslot) {
     // rank words: presence + rank in one 8-B load per item (all items'
     // loads in flight together; sparse ones: the block entries, then the
-    // words), then the posting score of the hits
+    // words), then the payload of the hits
     uint32_t sh;
     const uint64_t* __restrict__ rw = rank_base(ix, dslot, sh);
-    const float* __restrict__ ps = ix.psc + ix.off[ti];
     uint64_t x[N];
 #pragma unroll
     for (uint32_t j = 0; j < N; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> sh] : 0ull;
@@ -416,22 +472,13 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
       }
     }
 #pragma unroll
-    for (uint32_t j = 0; j < N; ++j) {
-      const uint32_t p = rank_pos(x[j], doc[j]);
-      sc[j] = p != kInvalid ? ps[p] : -1.0f;
-    }
-  } else if (dslot) {
-    // f32 score table: doc-indexed, one 4-B load per item (-1 = absent)
-    const float* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
-#pragma unroll
-    for (uint32_t j = 0; j < N; ++j) sc[j] = (live & (1u << j)) ? dt[doc[j]] : -1.0f;
+    for (uint32_t j = 0; j < N; ++j) pos[j] = rank_pos(x[j], doc[j]);
   } else {
-    const uint64_t bi = ix.off[ti];
     const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu;
     const uint32_t* __restrict__ di = ix.doc + bi;
     const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[ti];
     // bucket of each live item, then a branchless power-of-two search in it
-    uint32_t pos[N], hi[N];
+    uint32_t hi[N];
 #pragma unroll
     for (uint32_t j = 0; j < N; ++j) {
       pos[j] = 0;
@@ -451,10 +498,30 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
       }
     }
 #pragma unroll
-    for (uint32_t j = 0; j < N; ++j) {
-      sc[j] = -1.0f;
-      if ((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j]) sc[j] = ix.psc[bi + pos[j]];
-    }
+    for (uint32_t j = 0; j < N; ++j)
+      if (!((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j])) pos[j] = kInvalid;
+  }
+  // the hits' payloads (a posting's is never 0: tf >= 1 in some field), then their
+  // scores; an escaped tf finds its position again (posting_pos)
+  uint32_t v[N];
+#pragma unroll
+  for (uint32_t j = 0; j < N; ++j) v[j] = pos[j] != kInvalid ? tfn_load<kF>(ix, bi + pos[j]) : 0u;
+  uint32_t esc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < N; ++j) {
+    sc[j] = v[j] ? tfn_score_fast<kF>(v[j], wt, wn, ct, cn) : -1.0f;
+    esc |= (tfn_escaped<kF>(v[j]) ? 1u : 0u) << j;
+    // one item's IEEE division at a time: interleaved, the N divisions' temporaries
+    // pushed k_conj past its 128 VGPRs
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {
+#pragma unroll
+    for (uint32_t j = 0; j < N; ++j)
+      if ((esc >> j) & 1u) {
+        const uint64_t p = bi + posting_pos(ix, ti, doc[j]);
+        sc[j] = tfn_score(ix, p, ix.tfn[p] | (ix.tfn_name ? (uint32_t)ix.tfn_name[p] << 16 : 0u), wt, wn, ct, cn);
+      }
   }
 }
 
@@ -462,8 +529,9 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
 // score), in intersection order with the MaxScore bound after each, and append
 // the survivors' keys.  The sums are the ones the inline path forms:
 // (left + right) + (0.0 + s_2 + ...).  Unfiltered queries only (no facet term).
-__device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_t* terms, uint32_t m,
-                               const float* qub, uint64_t thr, uint32_t nd) {
+template <uint32_t kF>
+__device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_t* terms, const float* qwt,
+                               const float* qwn, uint32_t m, const float* qub, uint64_t thr, uint32_t nd) {
   const uint32_t tid = threadIdx.x;
   uint32_t doc[kDeferR], live = 0;
   float s01[kDeferR], acc[kDeferR];
@@ -479,7 +547,7 @@ __device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_
   for (uint32_t i = 2; i < m; ++i) {
     if (!__any(live != 0)) break;
     float sc[kDeferR];
-    probe_list<kDeferR>(ix, terms[i], doc, live, sc);
+    probe_list<kDeferR, kF>(ix, terms[i], doc, live, qwt[i], qwn[i], sh.cache, sh.cache + 256, sc);
 #pragma unroll
     for (uint32_t r = 0; r < kDeferR; ++r) {
       if (sc[r] < 0.0f) live &= ~(1u << r);
@@ -518,7 +586,7 @@ __device__ void flush_deferred(const DevIndex& ix, ConjShared& sh, const uint32_
 // single item's k-th key (items reading the bins themselves cost more than
 // they pruned: profiles/r03/ab/ab_conj_hist.log).
 // kMulti: a multi-snapshot plan (DevPlan::segs): the item's snapshot from its query slot
-template <bool kSingle, bool kMulti>
+template <bool kSingle, bool kMulti, uint32_t kF>
 __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPlan pl) {
   __shared__ ConjShared sh;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -545,6 +613,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
   const bool has_opt = m > nmx;
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const float* qub = pl.q_ub + (size_t)q * kMaxTerms;
+  // the clauses' query-time BM25 weights (uniform: scalar loads)
+  const float* qwt = pl.q_wt + (size_t)q * kMaxTerms;
+  const float* qwn = pl.q_wn + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
   const uint32_t t0 = terms[0];
   const uint64_t lead_base = ix.off[t0];
@@ -579,14 +650,18 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     sh.thr = thr0;
     pend = atomicMax(gthr, (unsigned long long)(thr0 & pl.pub_mask));
   }
+  // the tf caches into LDS (read after the first chunk's barrier)
+  for (uint32_t i = tid; i < (ix.tfn_name ? 512u : 256u); i += kThreads) sh.cache[i] = ix.cache[i];
 #ifdef FG_DIAG
   if (tid < 8) sh.dgc[tid] = 0;
 #endif
   uint64_t local_T = 0;
   // block-max skip (single lists): a chunk whose largest score (+ the facet
   // maximum) cannot reach the threshold is not loaded.  thr_k is the threshold
-  // as every thread last saw it (uniform), so the skip is uniform too.
+  // as every thread last saw it (uniform), so the skip is uniform too.  The
+  // build-time chunk maxima scale by the lead's bound factor (DevPlan::q_rup).
   const float* __restrict__ cmax = ix.cmax + ix.coff[t0];
+  const float rup0 = pl.q_rup[(size_t)q * kMaxTerms];
   uint64_t thr_k = thr0;
   // pure conjunctions (the multi-snapshot instantiation too: without deferred
   // probes it fits 128 VGPRs with no scratch, but C4 ran 1.44 -> 1.57 ms,
@@ -597,25 +672,45 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     const uint32_t c = c0 + cc;
     uint64_t tp0 = FG_NOW(), tp1 = tp0;
     (void)tp0; (void)tp1;
-    if (!kSingle || make_key(inflate_bound(cmax[c] + fmax), 0u) >= thr_k) {
+    if (!kSingle || make_key(inflate_bound(cmax[c] * rup0 + fmax), 0u) >= thr_k) {
     const uint64_t base0 = lead_base + (uint64_t)c * kChunk;
     const uint32_t cnt = min(kChunk, lead_df - c * kChunk);
     // lead candidates: item j of lane l = wv*512 + j*64 + l (coalesced per j)
     uint32_t doc[kItems];
     float s0[kItems];
     uint32_t live = 0;
+    {
+      uint32_t tv[kItems];
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; ++j) {
-      const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
-      const bool in = idx < cnt;
-      // predicated loads: tools/ab_variants.py measured clamped unconditional
-      // loads (every lane issuing) slower here, 1.57 -> 2.05 ms
-      doc[j] = in ? ix.doc[base0 + idx] : kInvalid;
-      s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
-      live |= (in ? 1u : 0u) << j;
+      for (uint32_t j = 0; j < kItems; ++j) {
+        const uint32_t idx = wv * kWaveSpan + j * 64 + lane;
+        const bool in = idx < cnt;
+        // predicated loads: tools/ab_variants.py measured clamped unconditional
+        // loads (every lane issuing) slower here, 1.57 -> 2.05 ms
+        doc[j] = in ? ix.doc[base0 + idx] : kInvalid;
+        tv[j] = in ? tfn_load<kF>(ix, base0 + idx) : 0u;
+        live |= (in ? 1u : 0u) << j;
+      }
+      if (tid == 0 && pend > sh.thr) sh.thr = pend;
+      __syncthreads();
+      // the lead postings' scores (query-time BM25, the caches now in LDS)
+      const float w0t = qwt[0], w0n = qwn[0];
+      uint32_t esc = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kItems; ++j) {
+        s0[j] = tv[j] ? tfn_score_fast<kF>(tv[j], w0t, w0n, sh.cache, sh.cache + 256) : 0.0f;
+        esc |= (tfn_escaped<kF>(tv[j]) ? 1u : 0u) << j;
+        __builtin_amdgcn_sched_barrier(0);  // (as probe_list: one division at a time)
+      }
+      if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {
+#pragma unroll
+        for (uint32_t j = 0; j < kItems; ++j)
+          if ((esc >> j) & 1u) {
+            const uint64_t p = base0 + wv * kWaveSpan + j * 64 + lane;
+            s0[j] = tfn_score(ix, p, tfn_load<kF>(ix, p), w0t, w0n, sh.cache, sh.cache + 256);
+          }
+      }
     }
-    if (tid == 0 && pend > sh.thr) sh.thr = pend;
-    __syncthreads();
     const uint64_t thr = sh.thr;
     thr_k = thr;
     // MaxScore (uniform): once the query has a threshold, a candidate whose
@@ -680,66 +775,8 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
         }
       }
       const uint32_t ti = terms[i];
-      const uint32_t meta = ix.tmeta[ti];
-      const uint32_t dslot = meta_slot(meta);
       float sc[kItems];
-      if (dslot && meta_rank(meta)) {
-        // rank words: presence + rank in one 8-B load per item (all items'
-        // loads in flight together; sparse ones: the block entries, then the
-        // words), then the posting score of the hits
-        uint32_t sh;
-        const uint64_t* __restrict__ rw = rank_base(ix, dslot, sh);
-        const float* __restrict__ ps = ix.psc + ix.off[ti];
-        uint64_t x[kItems];
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) x[j] = (live & (1u << j)) ? rw[doc[j] >> sh] : 0ull;
-        if (sh != 5u) {
-#pragma unroll
-          for (uint32_t j = 0; j < kItems; ++j) {
-            x[j] = ix.srank_w[srank_index(x[j], doc[j])];
-          }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) {
-          const uint32_t p = rank_pos(x[j], doc[j]);
-          sc[j] = p != kInvalid ? ps[p] : -1.0f;
-        }
-      } else if (dslot) {
-        // f32 score table: doc-indexed, one 4-B load per item (-1 = absent)
-        const float* __restrict__ dt = ix.dense + (size_t)(dslot - 1) * ix.n_docs;
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) sc[j] = (live & (1u << j)) ? dt[doc[j]] : -1.0f;
-      } else {
-        const uint64_t bi = ix.off[ti];
-        const uint32_t B = meta & 0xFFu, S = (meta >> 8) & 0xFFu;
-        const uint32_t* __restrict__ di = ix.doc + bi;
-        const uint32_t* __restrict__ dir = ix.dir + ix.dir_off[ti];
-        // bucket of each live item, then a branchless power-of-two search in it
-        uint32_t pos[kItems], hi[kItems];
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) {
-          pos[j] = 0;
-          hi[j] = 0;
-          if (live & (1u << j)) {
-            const uint32_t b = doc[j] >> B;
-            pos[j] = dir[b];
-            hi[j] = dir[b + 1];
-          }
-        }
-        for (uint32_t st = S; st > 0; --st) {
-          const uint32_t half = 1u << (st - 1);
-#pragma unroll
-          for (uint32_t j = 0; j < kItems; ++j) {
-            const uint32_t idx = pos[j] + half - 1;
-            if ((live & (1u << j)) && idx < hi[j] && di[idx] < doc[j]) pos[j] += half;
-          }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kItems; ++j) {
-          sc[j] = -1.0f;
-          if ((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j]) sc[j] = ix.psc[bi + pos[j]];
-        }
-      }
+      probe_list<kItems, kF>(ix, ti, doc, live, qwt[i], qwn[i], sh.cache, sh.cache + 256, sc);
       // Intersection::score = left + right + (0.0 + others...)
       if (i < nm) {
 #pragma unroll
@@ -824,7 +861,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
           local_T = truncate_topk(sh, n, K);
           if (local_T > thr_k) thr_k = local_T;
         }
-        flush_deferred(ix, sh, terms, m, qub, thr_k, nd);
+        flush_deferred<kF>(ix, sh, terms, qwt, qwn, m, qub, thr_k, nd);
         __syncthreads();
         n = sh.n_buf;
         if (tid == 0) sh.n_dq = 0;
@@ -949,13 +986,31 @@ struct DisjShared {
   // per-clause constants of the work item's query
   uint32_t c_meta[kMaxTerms], c_dir[kMaxTerms], c_toff[kMaxTerms];
   uint64_t c_base[kMaxTerms];
+  float c_wt[kMaxTerms], c_wn[kMaxTerms];  // query-time BM25 weights (text, name)
+  float c_rup[kMaxTerms];                  // bound factors (DevPlan::q_rup)
   uint32_t max_s, n_seg, n_post;
   uint32_t n_buf, n_cand;
   uint32_t n_q;                      // P: queued postings
   uint32_t n_cnt;                    // buf[0, n_cnt) are counted in the query's histogram
+  uint32_t n_lh;                     // keys counted into lh since its last flush (< 2^16: u16 halves)
   uint64_t thr;
-  uint32_t lh[kQBins];               // hits per score bin not yet added to the global histogram
+  // hits per score bin not yet added to the global histogram: two u16 bins per
+  // word (bin b in the half b & 1), flushed before any half could pass 65535
+  uint32_t lh[kQBins / 2];
+  float cache[256];                  // the text field's tf cache (DevIndex::cache; name: from the plan)
 };
+
+// Add the packed LDS bins (DisjShared::lh) to the query's global histogram and clear them.
+__device__ inline void hist_add16(uint32_t* lh, uint32_t* gh) {
+  for (uint32_t b = threadIdx.x; b < kQBins / 2; b += kThreads) {
+    const uint32_t c = lh[b];
+    if (c) {
+      if (c & 0xFFFFu) atomicAdd(&gh[2 * b], c & 0xFFFFu);
+      if (c >> 16) atomicAdd(&gh[2 * b + 1], c >> 16);
+      lh[b] = 0;
+    }
+  }
+}
 
 __device__ inline bool doc_alive(const DevIndex& ix, uint32_t d) {
   return !ix.alive || ((ix.alive[d >> 5] >> (d & 31)) & 1u);
@@ -1007,9 +1062,14 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
     __syncthreads();
     n = sh.n_buf;
   }
+  if (sh.n_lh + (n - sh.n_cnt) > 0xFFFFu) {  // uniform (LDS after a barrier): a u16 bin could overflow
+    hist_add16(sh.lh, hq.gh);
+    __syncthreads();
+    if (threadIdx.x == 0) sh.n_lh = 0;
+  }
   for (uint32_t i = sh.n_cnt + threadIdx.x; i < n; i += kThreads) {
     const uint32_t b = qbin(sh.buf[i], hq.lo, hq.sh);
-    if (b < kQBins) atomicAdd(&sh.lh[b], 1u);
+    if (b < kQBins) atomicAdd(&sh.lh[b >> 1], 1u << (16 * (b & 1u)));
   }
   __syncthreads();
   uint64_t T = 0;
@@ -1020,13 +1080,14 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
     // next pass starts (pend), after that pass's posting loads are in flight
     if (publish) pend = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)(mine & hq.pub));
     sh.thr = mine;
+    sh.n_lh += n - sh.n_cnt;
     sh.n_cnt = sh.n_buf;
   }
   __syncthreads();
 }
 
 
-template <bool kMulti>
+template <bool kMulti, uint32_t kF>
 __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, DevPlan pl) {
   __shared__ DisjShared sh;
   const uint32_t tid = threadIdx.x;
@@ -1074,17 +1135,25 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   if (tid == 0) {
     sh.n_buf = 0;
     sh.n_cnt = 0;
+    sh.n_lh = 0;
     const uint64_t t0 = pl.q_thr0[q];
     const uint64_t g = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)t0);
     sh.thr = g > t0 ? g : t0;
   }
-  for (uint32_t b = tid; b < kQBins; b += kThreads) sh.lh[b] = 0;
+  for (uint32_t b = tid; b < kQBins / 2; b += kThreads) sh.lh[b] = 0;
+  for (uint32_t i = tid; i < 256; i += kThreads) sh.cache[i] = ix.cache[i];
+  // the name field's tf cache stays in the plan's copy (global, L1 / L2-resident): LDS
+  // past ~32 KB drops k_disj from 5 to 4 workgroups per CU
+  const float* const cn = ix.cache + 256;
   if (tid < mq) {
     const uint32_t t = terms[tid];
     sh.c_meta[tid] = ix.tmeta[t];
     sh.c_dir[tid] = ix.dir_off[t];
     sh.c_toff[tid] = ix.toff[t];
     sh.c_base[tid] = ix.off[t];
+    sh.c_wt[tid] = pl.q_wt[(size_t)q * kMaxTerms + tid];
+    sh.c_wn[tid] = pl.q_wn[(size_t)q * kMaxTerms + tid];
+    sh.c_rup[tid] = pl.q_rup[(size_t)q * kMaxTerms + tid];
   }
   __syncthreads();
   if (tid == 0) {
@@ -1135,7 +1204,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     }
     sh.r_lo[p] = lo;
     sh.r_n[p] = (uint16_t)(hi > lo ? hi - lo : 0u);
-    sh.r_ub[p] = lo < hi ? ub : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
+    // the build-time bound scaled to the query's statistics (q8_bound of tsub then
+    // scales with it: DevPlan::q_rup carries a margin for the rounding)
+    sh.r_ub[p] = lo < hi ? ub * sh.c_rup[i] : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
     if (!(B <= kTileShift && sh.c_toff[i] != kInvalid)) sh.r_sub[p] = ~0ull;
   }
   {
@@ -1311,20 +1382,20 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   __syncthreads();
   // the next pass's postings are loaded before this pass's bound 1, so they are
   // in flight through its queue append and any flush (bound 2) that follows
-  uint32_t npd[J], npcl[J];
-  float nps[J];
+  // (the tf / fieldnorm payloads; their scores are formed when the pass starts)
+  uint32_t npd[J], npcl[J], npv[J];
   auto load_pass = [&](uint32_t e1) {
 #pragma unroll
     for (uint32_t j = 0; j < J; ++j) {
       const uint32_t e = e1 + j * kThreads + tid;
       npd[j] = dbase;
       npcl[j] = 0;
-      nps[j] = 0.0f;
+      npv[j] = 0;
       if (e < n_post) {
         uint32_t t;
         const uint64_t at = locate(e, t, npcl[j]);
         npd[j] = ix.doc[at];
-        nps[j] = ix.psc[at];
+        npv[j] = tfn_load<kF>(ix, at);
       }
     }
   };
@@ -1333,12 +1404,25 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     uint32_t pd[J], pcl[J];
     float ps[J];
     bool pk[J];
+    uint32_t esc = 0;
 #pragma unroll
     for (uint32_t j = 0; j < J; ++j) {
-      pk[j] = e0 + j * kThreads + tid < n_post;
+      const uint32_t e = e0 + j * kThreads + tid;
+      pk[j] = e < n_post;
       pd[j] = npd[j];
       pcl[j] = npcl[j];
-      ps[j] = nps[j];
+      // the posting's query-time score
+      ps[j] = pk[j] ? tfn_score_fast<kF>(npv[j], sh.c_wt[pcl[j]], sh.c_wn[pcl[j]], sh.cache, cn) : 0.0f;
+      esc |= (pk[j] && tfn_escaped<kF>(npv[j]) ? 1u : 0u) << j;
+    }
+    if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {  // an escaped tf: its position from the segment list again
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j)
+        if ((esc >> j) & 1u) {
+          uint32_t t_, c_;
+          const uint64_t at = locate(e0 + j * kThreads + tid, t_, c_);
+          ps[j] = tfn_score(ix, at, npv[j], sh.c_wt[pcl[j]], sh.c_wn[pcl[j]], sh.cache, cn);
+        }
     }
     if (e0 + kRound < n_post) load_pass(e0 + kRound);
     // with this pass's posting loads in flight: the last exchange's reply
@@ -1407,9 +1491,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         ess[j] = sh.b_ess[rel >> kSubShift];
       }
       // bound 2: every other clause at d, one clause at a time in clause order:
-      // its rank word (presence bits + rank) and then the posting score, its
-      // f32 table score, or its bucket maximum (-0.0: empty bucket).  When every
-      // other clause is dense (or has no posting in the tile) the clause-order
+      // its rank word (presence bits + rank) and then the posting's query-time
+      // score, or its bucket maximum (scaled; -0.0: empty bucket).  When every
+      // other clause has rank words (or no posting in the tile) the clause-order
       // sum IS the doc's exact SumCombiner score: a hit right here.
       float sum[J];
       uint32_t maybe[J];  // clauses whose structure at d says they may match (the rest cannot)
@@ -1443,8 +1527,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
               if (i < m && pk[j] && i != pcl[j] && !signbit(sh.r_ub[pt[j] * m + i])) {
                 need |= 1u << (g * J + j);
                 if (rank) x[g][j] = rw[pd[j] >> rsh];
-                else if (slot) x[g][j] = __float_as_uint(ix.dense[(size_t)(slot - 1) * ix.n_docs + pd[j]]);
-                else x[g][j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))]);
+                else x[g][j] = __float_as_uint(ix.bmax[sh.c_dir[i] + (pd[j] >> (meta & 0xFFu))] * sh.c_rup[i]);
               }
             }
           }
@@ -1476,10 +1559,26 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         for (uint32_t g = 0; g < G; ++g) {
           const uint32_t meta = i0 + g < m ? sh.c_meta[i0 + g] : 0u;
           if (!(meta_slot(meta) && meta_rank(meta))) continue;
-          const float* __restrict__ sp = ix.psc + sh.c_base[i0 + g];
+          // the rank hits' payloads (all in flight), then their query-time scores
+          const uint64_t cb = sh.c_base[i0 + g];
+          const float wt = sh.c_wt[i0 + g], wn = sh.c_wn[i0 + g];
+          uint32_t v[J];
 #pragma unroll
           for (uint32_t j = 0; j < J; ++j)
-            if (((need >> (g * J + j)) & 1u) && y[g][j] < 0x80000000u) y[g][j] = __float_as_uint(sp[y[g][j]]);
+            v[j] = (((need >> (g * J + j)) & 1u) && y[g][j] < 0x80000000u) ? tfn_load<kF>(ix, cb + y[g][j]) : 0u;
+          uint32_t esc = 0;
+#pragma unroll
+          for (uint32_t j = 0; j < J; ++j) {
+            if (v[j]) y[g][j] = __float_as_uint(tfn_score_fast<kF>(v[j], wt, wn, sh.cache, cn));  // a hit (payloads != 0)
+            esc |= (tfn_escaped<kF>(v[j]) ? 1u : 0u) << j;
+          }
+          if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {  // an escaped tf finds its position again
+            const uint32_t ti = terms[i0 + g];
+#pragma unroll
+            for (uint32_t j = 0; j < J; ++j)
+              if ((esc >> j) & 1u) y[g][j] = __float_as_uint(tfn_score(ix, cb + posting_pos(ix, ti, pd[j]), v[j], wt, wn,
+                                                                       sh.cache, cn));
+          }
         }
         // the clause-order sum (the own clause: the streamed posting's score)
 #pragma unroll
@@ -1553,8 +1652,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
           if (!(pc[j] & 0x80000000u)) {
             const uint32_t meta = sh.c_meta[pc[j]];
             if (meta_slot(meta)) {
-              pv[j] = dense_score(ix, meta, sh.c_base[pc[j]], rd[j]);
-              pc[j] |= 0x80000000u;  // resolved
+              pos[j] = rank_pos(rank_word_of(ix, meta_slot(meta), rd[j]), rd[j]);  // kInvalid: absent
+              pc[j] |= 0x40000000u;  // resolved by its rank word
             } else {
               const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[pc[j]];
               const uint32_t b = rd[j] >> (meta & 0xFFu);
@@ -1566,18 +1665,39 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         for (uint32_t st = sh.max_s; st > 0; --st) {
 #pragma unroll
           for (uint32_t j = 0; j < R; ++j) {
-            if (pc[j] & 0x80000000u) continue;  // invalid or resolved
+            if (pc[j] & 0xC0000000u) continue;  // invalid or resolved
             if (st > ((sh.c_meta[pc[j]] >> 8) & 0xFFu)) continue;
             const uint32_t half = 1u << (st - 1);
             const uint32_t idx = pos[j] + half - 1;
             if (idx < hi[j] && ix.doc[sh.c_base[pc[j]] + idx] < rd[j]) pos[j] += half;
           }
         }
+        // the found postings' payloads (all in flight), then their query-time scores
+        uint32_t pvv[R];
 #pragma unroll
         for (uint32_t j = 0; j < R; ++j) {
-          if (pc[j] & 0x80000000u) continue;
-          const uint64_t base = sh.c_base[pc[j]];
-          if (pos[j] < hi[j] && ix.doc[base + pos[j]] == rd[j]) pv[j] = ix.psc[base + pos[j]];
+          const uint32_t ci = pc[j] & 15u;
+          const uint64_t base = sh.c_base[ci];
+          bool hit = false;
+          if (!(pc[j] & 0x80000000u))
+            hit = (pc[j] & 0x40000000u) ? pos[j] != kInvalid : pos[j] < hi[j] && ix.doc[base + pos[j]] == rd[j];
+          pvv[j] = hit ? tfn_load<kF>(ix, base + pos[j]) : 0u;
+        }
+        uint32_t esc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < R; ++j) {
+          const uint32_t ci = pc[j] & 15u;
+          if (pvv[j]) pv[j] = tfn_score_fast<kF>(pvv[j], sh.c_wt[ci], sh.c_wn[ci], sh.cache, cn);  // a hit
+          esc |= (tfn_escaped<kF>(pvv[j]) ? 1u : 0u) << j;
+        }
+        if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {  // an escaped tf finds its position again
+#pragma unroll
+          for (uint32_t j = 0; j < R; ++j)
+            if ((esc >> j) & 1u) {
+              const uint32_t ci = pc[j] & 15u;
+              pv[j] = tfn_score(ix, sh.c_base[ci] + posting_pos(ix, terms[ci], rd[j]), pvv[j], sh.c_wt[ci], sh.c_wn[ci],
+                                sh.cache, cn);
+            }
         }
 #pragma unroll
         for (uint32_t j = 0; j < R; ++j) {
@@ -1627,7 +1747,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   }
   // the item's counted hits join the query's histogram (every key was counted
   // by the last disj_truncate)
-  hist_add(sh.lh, hq.gh);
+  hist_add16(sh.lh, hq.gh);
   if (tid == 0 && pend > sh.thr) sh.thr = pend;
   __syncthreads();
   flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
@@ -2021,19 +2141,35 @@ __global__ __launch_bounds__(kThreads) void k_merge(uint32_t n_shards, uint32_t 
 
 }  // namespace
 
+template <bool kSingle, uint32_t kF>
+static void conj_launch(const DevIndex& ix, const DevPlan& pl, uint32_t grid, hipStream_t s) {
+  if (pl.segs) k_conj<kSingle, true, kF><<<grid, kThreads, 0, s>>>(ix, pl);
+  else k_conj<kSingle, false, kF><<<grid, kThreads, 0, s>>>(ix, pl);
+}
+template <bool kSingle>
+static void conj_launch_f(const DevIndex& ix, const DevPlan& pl, uint32_t grid, hipStream_t s) {
+  switch (pl.feat & 3u) {
+    case 0: conj_launch<kSingle, 0>(ix, pl, grid, s); break;
+    case 1: conj_launch<kSingle, 1>(ix, pl, grid, s); break;
+    case 2: conj_launch<kSingle, 2>(ix, pl, grid, s); break;
+    default: conj_launch<kSingle, 3>(ix, pl, grid, s); break;
+  }
+}
+
 hipError_t launch_conj(const DevIndex& ix, const DevPlan& pl, hipStream_t s) {
-  const bool multi = pl.segs != nullptr;
   if (pl.n_single) {
-    if (multi) k_conj<true, true><<<pl.n_single, kThreads, 0, s>>>(ix, pl);
-    else k_conj<true, false><<<pl.n_single, kThreads, 0, s>>>(ix, pl);
+    conj_launch_f<true>(ix, pl, pl.n_single, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (pl.n_conj > pl.n_single) {
-    if (multi) k_conj<false, true><<<pl.n_conj - pl.n_single, kThreads, 0, s>>>(ix, pl);
-    else k_conj<false, false><<<pl.n_conj - pl.n_single, kThreads, 0, s>>>(ix, pl);
-  }
+  if (pl.n_conj > pl.n_single) conj_launch_f<false>(ix, pl, pl.n_conj - pl.n_single, s);
   return hipGetLastError();
+}
+
+template <uint32_t kF>
+static void disj_launch(const DevIndex& ix, const DevPlan& pl, uint32_t grid, hipStream_t s) {
+  if (pl.segs) k_disj<true, kF><<<grid, kThreads, 0, s>>>(ix, pl);
+  else k_disj<false, kF><<<grid, kThreads, 0, s>>>(ix, pl);
 }
 
 hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s, uint32_t first, uint32_t count) {
@@ -2044,8 +2180,12 @@ hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s, uin
   // a part of the sweep: the kernel's items start at pl.n_conj
   DevPlan part = pl;
   part.n_conj = pl.n_conj + first;
-  if (pl.segs) k_disj<true><<<count, kThreads, 0, s>>>(ix, part);
-  else k_disj<false><<<count, kThreads, 0, s>>>(ix, part);
+  switch (pl.feat & 3u) {
+    case 0: disj_launch<0>(ix, part, count, s); break;
+    case 1: disj_launch<1>(ix, part, count, s); break;
+    case 2: disj_launch<2>(ix, part, count, s); break;
+    default: disj_launch<3>(ix, part, count, s); break;
+  }
   return hipGetLastError();
 }
 
@@ -2083,14 +2223,6 @@ hipError_t launch_final(const DevPlan& pl, float* out_score, uint32_t* out_doc, 
   if (merged) k_final<true><<<grid, kThreads, kFinalLds, s>>>(pl, out_score, out_doc, out_n, out_shard);
   else k_final<false><<<grid, kThreads, kFinalLds, s>>>(pl, out_score, out_doc, out_n, nullptr);
   return hipGetLastError();
-}
-
-// Snapshot build: scatter one term's posting scores into its dense
-// doc-indexed table (pre-filled with -1.0 = absent).
-__global__ __launch_bounds__(kThreads) void k_dense(const uint32_t* __restrict__ doc, const float* __restrict__ psc,
-                                                    uint64_t base, uint32_t n, float* __restrict__ row) {
-  for (uint32_t p = blockIdx.x * kThreads + threadIdx.x; p < n; p += gridDim.x * kThreads)
-    row[doc[base + p]] = psc[base + p];
 }
 
 // Snapshot build: the rank words of every rank-kind term (fg_internal.h
@@ -2152,23 +2284,20 @@ hipError_t launch_rank(const uint32_t* doc, const uint64_t* slot_base, const uin
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- snapshot scoring
-// Bm25Weight::score in tantivy's f32 operation order (query/bm25.rs:
-// weight * (tf / (tf + cache[fieldnorm_id]))) for each field of the union
-// Should(text:t, name:t), summed from 0.0 (SumCombiner).  -ffp-contract=off and
-// IEEE f32 division: bit-identical to the oracle's host arithmetic.
-__device__ inline float posting_score(uint32_t tfp, uint32_t fn_t, uint32_t fn_n, float wt, float wn,
-                                      const float* cache) {
+// ---------------------------------------------------------------- build-time bounds
+// The build's posting scores (ScoreJob::psc, a temporary) from the same
+// payloads and arithmetic the search kernels use at query time (tfn_score):
+// bounds computed from them hold bit for bit under the build's statistics.
+__device__ inline float build_score(const ScoreJob& j, uint64_t p, uint32_t v, float wt, float wn, const float* cache) {
+  uint32_t tt = v & 0xFFu, tn = (v >> 16) & 0xFFu;
+  if (tt == kTfEsc || tn == kTfEsc) {
+    const uint32_t e = tf_escaped(j.esc_pos, j.esc_tf, j.n_esc, p);
+    if (tt == kTfEsc) tt = e & 0xFFFFu;
+    if (tn == kTfEsc) tn = e >> 16;
+  }
   float s = 0.0f;
-  const uint32_t tt = tfp & 0xFFFFu, tn = tfp >> 16;
-  if (tt) {
-    const float tf = (float)tt;
-    s += wt * (tf / (tf + cache[fn_t]));
-  }
-  if (tn) {
-    const float tf = (float)tn;
-    s += wn * (tf / (tf + cache[256 + fn_n]));
-  }
+  if (tt) s += field_score(tt, (v >> 8) & 0xFFu, wt, cache);
+  if (tn) s += field_score(tn, v >> 24, wn, cache + 256);
   return s;
 }
 
@@ -2203,22 +2332,13 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j, uint32_t n) {
   for (uint32_t i = threadIdx.x; i <= nterm; i += kThreads) s_off[i] = j.off[tf + i];
   for (uint32_t i = threadIdx.x; i < nterm; i += kThreads) s_max[i] = 0u;
   __syncthreads();
-  // the chunk's postings in one step per thread: every doc / tf load, then every
-  // fieldnorm gather, in flight together (kScoreChunk / kThreads per thread)
+  // the chunk's payloads in one step per thread, in flight together (kScoreChunk / kThreads per thread)
   constexpr uint32_t R = kScoreChunk / kThreads;
-  uint32_t d[R], tfp[R];
+  uint32_t tv[R];
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint64_t p = e0 + r * kThreads + threadIdx.x;
-    d[r] = p < e1 ? j.doc[p] : 0xFFFFFFFFu;
-    tfp[r] = p < e1 ? (j.tf16 ? (uint32_t)j.tf16[p] : j.tfp[p]) : 0u;
-  }
-  uint32_t fnt[R], fnn[R];
-#pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const bool in = d[r] != 0xFFFFFFFFu;
-    fnt[r] = in ? j.fn_text[d[r]] : 0u;
-    fnn[r] = in && j.fn_name ? j.fn_name[d[r]] : 0u;
+    tv[r] = p < e1 ? (uint32_t)j.tfn[p] | (j.tfn_name ? (uint32_t)j.tfn_name[p] << 16 : 0u) : 0u;
   }
   float mx = 0.0f;  // one term (uniform): reduced per wave, one LDS atomic
 #pragma unroll
@@ -2227,7 +2347,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreJob j, uint32_t n) {
     if (p >= e1) continue;
     const uint32_t sl = nterm == 1 ? 0u : slot_of(s_off, nterm, p);
     const uint32_t t = tf + sl;
-    const float v = posting_score(tfp[r], fnt[r], fnn[r], j.w_text[t], j.w_name[t], cache);
+    const float v = build_score(j, p, tv[r], j.w_text[t], j.w_name[t], cache);
     j.psc[p] = v;
     if (nterm == 1) mx = fmaxf(mx, v);
     else atomicMax(&s_max[sl], __float_as_uint(v));
@@ -2620,13 +2740,6 @@ hipError_t launch_copy32(uint32_t* dst, const uint32_t* src, uint64_t n, uint32_
   const uint64_t want = (n + kThreads - 1) / kThreads;
   const uint64_t g = grid_cap && want > grid_cap ? grid_cap : want;
   k_copy32<<<(uint32_t)(g < 0x7FFFFFFFull ? g : 0x7FFFFFFFull), kThreads, 0, s>>>(dst, src, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_dense(const uint32_t* doc, const float* psc, uint64_t base, uint32_t n, float* row, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  const uint32_t want = (n + kThreads - 1) / kThreads;
-  k_dense<<<want < 2048u ? want : 2048u, kThreads, 0, s>>>(doc, psc, base, n, row);
   return hipGetLastError();
 }
 

@@ -27,15 +27,19 @@ using fgh::parallel_dynamic;
 
 namespace {
 
-enum Arr : uint32_t { A_DOC, A_PSC, A_RANK, A_SRANK, A_SRANKW, A_DENSE, A_DIR, A_BMAX, A_TMAX, A_TDIR, A_CMAX, A_TSUB, A_N };
+enum Arr : uint32_t { A_DOC, A_TFN, A_RANK, A_SRANK, A_SRANKW, A_DIR, A_BMAX, A_TMAX, A_TDIR, A_CMAX, A_TSUB, A_N };
 constexpr uint64_t kLine = 128;
 constexpr float kInflate = 1.00000762939453125f;  // kernels.hip inflate_bound: 1 + 2^-17
 
 // host view of one snapshot: the postings (host copy) and the device tables the
-// kernels read, copied back
+// kernels read, copied back; psc: every posting's score under the snapshot's
+// current statistics, formed on the host from the payloads as the kernels form
+// it at query time; the bound tables scaled to the current statistics as the
+// plans scale them (term_ratio)
 struct Snap {
   const fg_index* ix = nullptr;
   const uint32_t* doc = nullptr;
+  uint32_t pw = 2;  // payload bytes per posting the kernels load (tfn, + tfn_name)
   std::vector<float> psc, tmax, bmax, cmax;
   std::vector<uint64_t> tsub, srank;  // srank: the sparse rank block entries
   std::vector<uint32_t> dir_off, toff, coff;
@@ -56,7 +60,32 @@ struct Snap {
     auto rd = [](void* dst, const void* src, size_t n) -> hipError_t {
       return n && src ? hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) : hipSuccess;
     };
-    HIPCHK(rd(psc.data(), x->d.psc, 4 * P));
+    {
+      std::vector<uint16_t> tv(P), tn(x->d.tfn_name ? P : 0);
+      std::vector<uint64_t> ep(x->d.n_esc);
+      std::vector<uint32_t> et(x->d.n_esc);
+      HIPCHK(rd(tv.data(), x->d.tfn, 2 * P));
+      HIPCHK(rd(tn.data(), x->d.tfn_name, 2 * tn.size()));
+      HIPCHK(rd(ep.data(), x->d.esc_pos, 8 * ep.size()));
+      HIPCHK(rd(et.data(), x->d.esc_tf, 4 * et.size()));
+      pw = x->d.tfn_name ? 4 : 2;
+      parallel_dynamic(x->n_terms, hw_threads(0), 256, [&](int, uint32_t b, uint32_t e) {
+        for (uint32_t t = b; t < e; ++t)
+          for (uint64_t p = x->off[t]; p < x->off[t + 1]; ++p) {
+            const uint32_t v = tv[p] | (tn.empty() ? 0u : (uint32_t)tn[p] << 16);
+            uint32_t tt = v & 0xFFu, tm = (v >> 16) & 0xFFu;
+            if (tt == fg::kTfEsc || tm == fg::kTfEsc) {
+              const uint32_t ex = fg::tf_escaped(ep.data(), et.data(), ep.size(), p);
+              if (tt == fg::kTfEsc) tt = ex & 0xFFFFu;
+              if (tm == fg::kTfEsc) tm = ex >> 16;
+            }
+            float sc = 0.0f;
+            if (tt) sc += fg::field_score(tt, (v >> 8) & 0xFFu, x->w_text[t], x->cache);
+            if (tm) sc += fg::field_score(tm, v >> 24, x->w_name[t], x->cache + 256);
+            psc[p] = sc;
+          }
+      });
+    }
     HIPCHK(rd(dir_off.data(), x->d.dir_off, 4 * V));
     HIPCHK(rd(toff.data(), x->d.toff, 4 * V));
     HIPCHK(rd(coff.data(), x->d.coff, 4 * V));
@@ -66,11 +95,25 @@ struct Snap {
     HIPCHK(rd(cmax.data(), x->d.cmax, 4 * cmax.size()));
     srank.resize((uint64_t)(x->n_rank - x->d.n_prank) * x->d.srank_blocks);
     HIPCHK(rd(srank.data(), x->d.srank, 8 * srank.size()));
-    bytes[A_DOC] = bytes[A_PSC] = 4 * P;
+    if (!x->same_stats)  // the bounds as a plan scales them (DevPlan::q_rup)
+      parallel_dynamic(x->n_terms, hw_threads(0), 256, [&](int, uint32_t b, uint32_t e) {
+        for (uint32_t t = b; t < e; ++t) {
+          float rdn, rup;
+          fgh::term_ratio(x, t, &rdn, &rup);
+          if (rup == 1.0f) continue;
+          const uint32_t d0 = dir_off[t], d1 = t + 1 < x->n_terms ? dir_off[t + 1] : (uint32_t)x->dir_entries;
+          for (uint32_t i = d0; i < d1; ++i) bmax[i] *= rup;
+          if (toff[t] != 0xFFFFFFFFu)
+            for (uint64_t i = toff[t]; i <= toff[t] + (uint64_t)x->n_tiles; ++i) tmax[i] *= rup;
+          const uint64_t nc = (len(t) + fg::kChunk - 1) / fg::kChunk;
+          for (uint64_t i = 0; i < nc; ++i) cmax[coff[t] + i] *= rup;
+        }
+      });
+    bytes[A_DOC] = 4 * P;
+    bytes[A_TFN] = (uint64_t)pw * P;
     bytes[A_RANK] = 8ull * x->d.n_prank * x->d.rank_words;
     bytes[A_SRANK] = 8ull * srank.size();
     bytes[A_SRANKW] = 8ull * x->n_srank_words;
-    bytes[A_DENSE] = 4ull * x->n_dense * x->n_docs;
     bytes[A_DIR] = bytes[A_BMAX] = 4 * x->dir_entries;
     bytes[A_TMAX] = bytes[A_TDIR] = 4 * x->tile_entries;
     bytes[A_CMAX] = 4ull * x->n_sc;
@@ -173,7 +216,7 @@ struct Union {
 
 inline uint64_t key_of(float s, uint32_t d) { return fg::make_key(s, d); }
 
-// Probe of term t at doc d as k_conj's probe_list / k_disj's dense_score and
+// Probe of term t at doc d as k_conj's probe_list / k_disj's rank probe and
 // directory search issue it (stream s); returns the posting score or -1.
 float probe_term(const Snap& S, Acc& A, uint32_t s, uint32_t t, uint32_t d, double& cat) {
   const uint32_t meta = S.ix->tmeta[t];
@@ -184,15 +227,10 @@ float probe_term(const Snap& S, Acc& A, uint32_t s, uint32_t t, uint32_t d, doub
     S.rank_loads(A, s, slot, d, cat);
     const uint64_t p = std::lower_bound(l, l + n, d) - l;
     if (p < n && l[p] == d) {
-      A.gather(s, A_PSC, (base + p) * 4, 4, cat);
+      A.gather(s, A_TFN, (base + p) * S.pw, S.pw, cat);
       return S.psc[base + p];
     }
     return -1.0f;
-  }
-  if (slot) {
-    A.gather(s, A_DENSE, ((uint64_t)(slot - 1) * S.ix->n_docs + d) * 4, 4, cat);
-    const uint64_t p = std::lower_bound(l, l + n, d) - l;
-    return p < n && l[p] == d ? S.psc[base + p] : -1.0f;
   }
   const uint32_t B = meta & 0xFFu, St = (meta >> 8) & 0xFFu;
   const uint64_t b = d >> B;
@@ -211,7 +249,7 @@ float probe_term(const Snap& S, Acc& A, uint32_t s, uint32_t t, uint32_t d, doub
   if (pos < hi) {
     A.gather(s, A_DOC, (base + pos) * 4, 4, cat);
     if (l[pos] == d) {
-      A.gather(s, A_PSC, (base + pos) * 4, 4, cat);
+      A.gather(s, A_TFN, (base + pos) * S.pw, S.pw, cat);
       return S.psc[base + pos];
     }
   }
@@ -239,7 +277,7 @@ uint64_t model_conj(const Snap& S, const uint32_t* terms, uint32_t m, bool has_t
       if (thk && key_of(S.cmax[S.coff[t0] + c] * kInflate, 0u) < thk) continue;
       const uint64_t p0 = c * fg::kChunk, n = std::min<uint64_t>(fg::kChunk, df - p0);
       A.range(0, A_DOC, base + p0, n, 4, A.stream);
-      A.range(0, A_PSC, base + p0, n, 4, A.stream);
+      A.range(0, A_TFN, base + p0, n, S.pw, A.stream);
       for (uint64_t p = p0; p < p0 + n; ++p) kept += key_of(S.psc[base + p], ld[p]) >= thk ? 1 : 0;
     }
     return kept;
@@ -249,12 +287,12 @@ uint64_t model_conj(const Snap& S, const uint32_t* terms, uint32_t m, bool has_t
   {
     float acc = 0.0f;
     for (uint32_t j = m; j-- > 1;) {
-      acc += ix->tmaxs[terms[j]];
+      acc += fgh::term_max_now(ix, terms[j]);
       qub[j] = acc;
     }
   }
   A.range(0, A_DOC, base, df, 4, A.stream);
-  A.range(0, A_PSC, base, df, 4, A.stream);
+  A.range(0, A_TFN, base, df, S.pw, A.stream);
   for (uint64_t p = 0; p < df; ++p) {
     const uint32_t d = ld[p];
     float s0 = S.psc[base + p], acc = 0.0f;
@@ -318,7 +356,7 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
         A.gather(c, A_DIR, (dob + ((d1 - 1) >> B[c]) + 1) * 4, 4, A.stream);
         lo[c] = S.pos_ge(t[c], d0);
         hi[c] = S.pos_ge(t[c], d1);
-        u = S.ix->tmaxs[t[c]];
+        u = fgh::term_max_now(S.ix, t[c]);
       } else {
         const uint64_t b = d0 >> B[c];
         A.gather(c, A_DIR, (dob + b) * 4, 4, A.stream);
@@ -421,7 +459,7 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
       const uint64_t base = ix->off[t[c]];
       const uint32_t* l = S.list(t[c]);
       A.range(c, A_DOC, base + plo, phi - plo, 4, A.stream);
-      A.range(c, A_PSC, base + plo, phi - plo, 4, A.stream);
+      A.range(c, A_TFN, base + plo, phi - plo, S.pw, A.stream);
       uint32_t cur[fg::kMaxTerms];
       for (uint32_t i = 0; i < m; ++i) cur[i] = lo[i];
       for (uint32_t p = plo; p < phi; ++p) {
@@ -452,14 +490,7 @@ uint64_t model_disj(const Snap& S, const uint32_t* t, uint32_t m, float thr, Acc
           if (slot && fg::meta_rank(meta[i])) {
             S.rank_loads(A, i, slot, d, A.probe);
             if (here) {
-              A.gather(i, A_PSC, (bi + cur[i]) * 4, 4, A.probe);
-              v[i] = S.psc[bi + cur[i]];
-              maybe |= 1u << i;
-              sum += v[i];
-            }
-          } else if (slot) {
-            A.gather(i, A_DENSE, ((uint64_t)(slot - 1) * N + d) * 4, 4, A.probe);
-            if (here) {
+              A.gather(i, A_TFN, (bi + cur[i]) * S.pw, S.pw, A.probe);
               v[i] = S.psc[bi + cur[i]];
               maybe |= 1u << i;
               sum += v[i];
@@ -573,7 +604,7 @@ int fg_model_batch(const fg_index* ix, const fg_query_batch* q, uint32_t k, cons
   out->alg_bytes = out->stream_bytes + out->probe_bytes + out->output_bytes;
   out->line_bytes = (double)kLine * (double)U.count();
   if (getenv("FUGU_MODEL_TRACE")) {  // the line floor and the per-query line sum, by array
-    static const char* names[A_N] = {"doc", "psc", "rank", "srank", "srankw", "dense", "dir", "bmax", "tmax", "tdir", "cmax", "tsub"};
+    static const char* names[A_N] = {"doc", "tfn", "rank", "srank", "srankw", "dir", "bmax", "tmax", "tdir", "cmax", "tsub"};
     for (uint32_t a = 0; a < A_N; ++a)
       fprintf(stderr, "[fg model] %-6s floor %8.3f GB  per-query sum %8.3f GB\n", names[a],
               (double)kLine * (double)U.count(a) * 1e-9, (double)kLine * (double)U.qlines[a].load() * 1e-9);

@@ -61,7 +61,7 @@ EXPORTS = (
 LADDER_KS = (1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000)  # FG_LADDER_LEVELS ranks
 KTH_KS = (1, 10, 20, 100, 1000)  # fg_index_term_kth / fg_index_set_kth_floor ranks
 HIST_BINS = 512  # fugu.h FG_HIST_BINS: score-histogram bins per query
-ABI_VERSION = 4  # include/fugu.h FG_ABI_VERSION this binding's structs follow
+ABI_VERSION = 5  # include/fugu.h FG_ABI_VERSION this binding's structs follow
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -147,7 +147,7 @@ def agree_hist_span(plans, group=None, device=None):
     return lo, hi
 
 
-def exchange_hist(plan, stream: int, buf: torch.Tensor, group=None):
+def exchange_hist(plan, stream: int, buf: torch.Tensor, group=None, prev: "torch.Tensor | None" = None):
     """Between two parts of a plan's k_disj sweep (fg_plan_execute_part): sum the
     per-query score histograms of every rank's shards into this plan's, ONE
     all-reduce of [n_batch * HIST_BINS] int32 (RCCL over xGMI with "nccl"; gloo
@@ -155,16 +155,29 @@ def exchange_hist(plan, stream: int, buf: torch.Tensor, group=None):
     `stream` torch's current stream of the plan's device (the copies and the
     collective are ordered on it).  The shards' counted docs are distinct, so
     the summed histogram's threshold is still a lower bound of the merged k-th
-    score: merged results are unchanged."""
+    score: merged results are unchanged.
+
+    A second exchange in the same round (a sweep in three or more parts) passes
+    `prev`, the tensor the previous exchange returned: the plan's histogram then
+    already holds every rank's earlier counts, so only this rank's counts since
+    (its histogram minus `prev`) are summed and added back -- summing the whole
+    histogram again would count the earlier counts once per rank, and the
+    threshold of an over-counted histogram can pass the merged k-th score
+    (ADVICE r05).  Returns the merged histogram (a new tensor) for the next call."""
     plan.hist_copy(stream, buf.data_ptr(), False)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if prev is not None:
+            buf.sub_(prev)  # this rank's counts since the last exchange
         if dist.get_backend(group) == "gloo" and buf.is_cuda:
             h = buf.cpu()
             dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
             buf.copy_(h)
         else:
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        if prev is not None:
+            buf.add_(prev)
     plan.hist_copy(stream, buf.data_ptr(), True)
+    return buf.clone()
 
 
 def shard_ranges(n_docs: int, world: int):

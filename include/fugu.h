@@ -28,10 +28,13 @@
 extern "C" {
 #endif
 
-/* ABI revision: bumped whenever a struct of this header changes layout
- * (4: fg_query_batch.occur; fg_model_out).  A binding checks fg_abi_version()
- * against the value it was written for before passing any struct. */
-#define FG_ABI_VERSION 4
+/* ABI revision: bumped whenever a struct of this header changes layout or a
+ * call's contract changes (4: fg_query_batch.occur; fg_model_out.  5:
+ * fg_index_stats.n_sparse_rank_terms / reserved0 / rank_bytes (16 B more);
+ * query-time scoring: fg_index_rescore[_many] do no device work, fg_index_term_kth
+ * of a rescore is a lower bound).  A binding checks fg_abi_version() against the
+ * value it was written for before passing any struct. */
+#define FG_ABI_VERSION 5
 
 #define FG_OK 0
 #define FG_EINVAL (-1)        /* bad argument (e.g. k == 0: tantivy asserts limit >= 1) */
@@ -159,27 +162,30 @@ int fg_docs_facet_stats(const fg_docs_input* in, uint32_t* df_facet, uint64_t* t
 int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g,
                                     fg_index** out);
 
-/* A new snapshot of `base` scored with other statistics: after a commit added
- * docs elsewhere in the namespace (a new segment) or deleted some.  tantivy's
+/* A new snapshot of `base` with other statistics: after a commit added docs
+ * elsewhere in the namespace (a new segment) or deleted some.  tantivy's
  * Bm25Weight reads the Searcher's statistics at query time, so every segment
  * scores with the namespace's current N, df and token totals
  * (core/searcher.rs Bm25StatisticsProvider; one segment per commit,
- * src/db/document.rs:65).  The postings, directory and rank words stay shared
- * with `base` (no host inversion, no upload); the posting scores, bounds and
- * the alive bitset are recomputed on the device.  `deleted` [n_docs of base]
- * or NULL (none).  g must cover base's own doc frequencies. */
+ * src/db/document.rs:65) -- and so does this library: the kernels form each
+ * posting's score at query time from its tf and fieldnorm id, so a rescore is
+ * host work only (the new weights and tf caches, read by the plans; an upload
+ * of the alive bitset when deletions changed).  Every device array stays
+ * shared with `base`; the bounds the kernels prune with (computed once when the
+ * segment was built) are scaled per query by the ratio of the statistics.
+ * `deleted` [n_docs of base] or NULL (none).  g must cover base's own doc
+ * frequencies. */
 int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out);
 /* n snapshots rescored with ONE set of statistics (a commit's older segments):
- * the BM25 weights computed once, every snapshot's device work on its own
- * host thread and stream, side by side.  deleted[i] as fg_index_rescore's
+ * the BM25 weights computed once and shared.  deleted[i] as fg_index_rescore's
  * (deleted itself may be NULL: none anywhere).  On error no snapshot is made
  * (outs[] all NULL). */
 int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_global_stats* g,
                           const uint8_t* const* deleted, fg_index** outs);
-/* on != 0: the calling thread's snapshot builds and rescores run on the
- * device's background streams -- restricted by a CU mask to FUGU_BG_CU_FRAC of
- * the CUs (default 0.75, the rest spread over every XCD), so searches beside
- * them always find free CUs (fugu's writer / merge threads beside its
+/* on != 0: the calling thread's snapshot builds run on the device's
+ * low-priority background stream with their kernels capped at FUGU_BG_GRID
+ * workgroups per CU (default 2), so searches beside them -- on high-priority
+ * streams -- find wave slots free (fugu's writer / merge threads beside its
  * searchers, src/db/core.rs:247-249).  fg_db's commits and merger use it.
  * Returns the previous setting. */
 int fg_thread_background(int on);
@@ -212,11 +218,11 @@ uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term);
 int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512);
 /* The snapshot's per-term K-th best alive posting scores for K = 1, 10, 20, 100,
  * 1000 (0 when the term has fewer alive postings): the starting thresholds of
- * its disjunctions.  out[5].  A snapshot from fg_index_rescore[_many] whose
- * alive docs are its base's (no new deletions) holds a lower bound instead: the
- * base's values times the term's smallest new / old posting-score ratio (within
- * ~0.2% for a commit that grows the namespace by 10%); builds, merges and
- * rescores with new deletions select exactly. */
+ * its disjunctions.  out[5].  Exact for a snapshot built (or merged) under its
+ * statistics; a snapshot from fg_index_rescore[_many] holds a lower bound
+ * instead: the build's K'-th best for the smallest stored K' >= K + the docs
+ * deleted since, times the term's smallest current / build posting-score ratio
+ * (within ~0.2% for a commit that grows the namespace by 10%). */
 int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out);
 
 /* ---- doc-sharded namespaces: namespace-wide starting thresholds ----------------

@@ -22,7 +22,7 @@ use std::os::raw::{c_char, c_int, c_void};
 #[repr(C)] pub struct fg_db { _p: [u8; 0] }
 
 // ---- constants (fugu.h)
-pub const FG_ABI_VERSION: c_int = 4;  // checked against fg_abi_version() before any struct is passed
+pub const FG_ABI_VERSION: c_int = 5;  // checked against fg_abi_version() before any struct is passed
 pub const FG_OK: c_int = 0;
 pub const FG_EINVAL: c_int = -1;
 pub const FG_ENODEV: c_int = -2;

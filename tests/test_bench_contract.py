@@ -38,3 +38,31 @@ def test_headline_value_comes_from_throughput_fields():
     assert "tput = throughput_fields(nq, world, args.steps, elapsed)" in body
     assert "qps = tput['value']" in body
     assert "nq * world * args.steps" not in body
+
+
+def test_roofline_carries_three_fractions():
+    """Every kernel line's roofline quotes the model's fraction, the fraction at
+    each query's final threshold (frac_pruned) and the measured DRAM fraction; a
+    model more than 1.5x the measured DRAM bytes is not the line's `frac`
+    (C3's exhaustive cascade read 0.89 where the kernel moved
+    0.38 of HBM)."""
+    b = _bench()
+    model = {"alg_bytes": 7.5e9, "stream_bytes": 5e9, "probe_bytes": 2.5e9, "output_bytes": 0,
+             "line_bytes": 1.7e9, "query_line_bytes": 9e9}
+    pruned = {"alg_bytes": 2.0e9, "line_bytes": 1.5e9, "query_line_bytes": 2.6e9}
+    orig = b.measured_traffic
+    try:
+        b.measured_traffic = lambda key: (3.2e9, "profiles/test.json")
+        r = b.roofline("k_conj", 1.0, model, "k", "exhaustive cascade", pruned)
+        assert r["frac_model"] == round(7.5e9 / 1e-3 / 1e9 / b.HBM_PEAK_GBS, 4)
+        assert r["frac_pruned"] == round(2.0e9 / 1e-3 / 1e9 / b.HBM_PEAK_GBS, 4)
+        assert r["frac"] == r["hbm_frac_measured"] == round(3.2e9 / 1e-3 / 1e9 / b.HBM_PEAK_GBS, 4)
+        assert "measured" in r["frac_rule"]
+        b.measured_traffic = lambda key: (6.0e9, "profiles/test.json")
+        r = b.roofline("k_conj", 1.0, model, "k", "exhaustive cascade", pruned)
+        assert r["frac"] == r["frac_model"] and r["frac_pruned"] < r["frac"]
+        b.measured_traffic = lambda key: (None, "no profile")
+        r = b.roofline("k_disj", 1.0, model, "k", "k_disj at each query's final k-th score")
+        assert r["frac"] == r["frac_model"] == r["frac_pruned"] and r["traffic"] is None
+    finally:
+        b.measured_traffic = orig

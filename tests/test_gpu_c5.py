@@ -81,24 +81,44 @@ def test_c5_shards_use_global_statistics(native, c5):
 
 
 @pytest.fixture(scope="module")
-def c5_ref(c5):
-    """The 64-query OR top-1000 sample and ONE 100M-doc oracle index's answers."""
+def c5_oracle(c5):
+    """ONE 100M-doc oracle index (the unsharded namespace)."""
     from fugu_amd import synth
     from oracle import oracle as orc
-    c = c5[0]
-    q_off, terms = synth.queries(64, 2, 5)
-    ref = orc.OracleIndex(synth.VOCAB, c.off, c.tok, threads=16)
-    rs, rd, rn, _, _ = ref.search_batch(q_off, terms, K, mode=orc.OR, threads=16)
+    ref = orc.OracleIndex(synth.VOCAB, c5[0].off, c5[0].tok, threads=16)
+    yield ref
     ref.close()
-    return q_off, terms, rs, rd, rn
 
 
-def test_c5_or_top1000_100m_vs_oracle(native, c5, c5_ref):
+def _c5_ref(ref, half):
+    """Half `half` (512 queries) of the bench's 1024-query OR top-1000 batch and
+    the 100M oracle's answers (two passes keep each test's oracle time short)."""
+    from fugu_amd import synth
+    from oracle import oracle as orc
+    q_off, terms = synth.queries(1024, 2, 5)
+    lo, hi = 512 * half, 512 * (half + 1)
+    qo = (q_off[lo:hi + 1] - q_off[lo]).astype(q_off.dtype)
+    qt = terms[q_off[lo]:q_off[hi]]
+    rs, rd, rn, _, _ = ref.search_batch(qo, qt, K, mode=orc.OR, threads=16)
+    return qo, qt, rs, rd, rn
+
+
+@pytest.fixture(scope="module")
+def c5_ref(c5_oracle):
+    return _c5_ref(c5_oracle, 0)
+
+
+@pytest.fixture(scope="module")
+def c5_ref2(c5_oracle):
+    return _c5_ref(c5_oracle, 1)
+
+
+def _c5_sharded_vs_oracle(native, c5, ref):
     import torch
 
     from fugu_amd.shard import merge_on_device
     c, ranges, shards, g, _ = c5
-    q_off, terms, rs, rd, rn = c5_ref
+    q_off, terms, rs, rd, rn = ref
     nq = len(q_off) - 1
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev).cuda_stream
@@ -123,6 +143,17 @@ def test_c5_or_top1000_100m_vs_oracle(native, c5, c5_ref):
         assert np.array_equal(gdoc[q, :m], rd[q, :m].astype(np.uint64)), q
         assert np.array_equal(ms[q, :m], rs[q, :m]), q
     assert (rn == K).mean() > 0.9
+
+
+def test_c5_or_top1000_100m_vs_oracle(native, c5, c5_ref):
+    """The bench's C5 batch, queries 0-511: the 8 global-statistics shards
+    merged on the device vs ONE 100M-doc oracle index."""
+    _c5_sharded_vs_oracle(native, c5, c5_ref)
+
+
+def test_c5_or_top1000_100m_vs_oracle_second_half(native, c5, c5_ref2):
+    """... and queries 512-1023: all 1024 of the bench's batch are checked."""
+    _c5_sharded_vs_oracle(native, c5, c5_ref2)
 
 
 def test_c5_as_one_index_past_2_32_postings(native, c5, c5_ref):

@@ -87,13 +87,14 @@ def test_background_capped_scoring_identical(native):
         x.close()
 
 
-def test_rescore_without_deletions_reuses_kth_bound(native):
-    """A rescore whose alive docs are the base snapshot's skips k_ktop: its per-term
-    K-th scores are the base's times the smallest new / old score ratio of the
-    term's postings (kth_reuse_bound).  They must never exceed the exact K-th
-    scores under the new statistics (a fresh build with them), stay within 1%
-    of them (a 10% larger namespace: ~0.2% below in practice), and the searches must return the fresh build's hits; with new
-    deletions the rescore selects exactly."""
+def test_rescore_kth_is_a_lower_bound(native):
+    """A rescore runs no device work: its per-term K-th scores are the build's
+    times the smallest current / build score ratio of the term's postings
+    (fugu.cpp term_ratio), with new deletions taken from the level K + the docs
+    deleted since (term_kth_now).  They must never exceed the exact K-th scores
+    under the new statistics (a fresh build with them), stay within 1% of them
+    without deletions (a 10% larger namespace), and the searches must return the
+    fresh build's hits."""
     from fugu_amd import synth
     ctx = native.Context((0,))
     c = synth.corpus(400_000)
@@ -123,12 +124,19 @@ def test_rescore_without_deletions_reuses_kth_bound(native):
         for i in range(len(x[2])):
             m = int(x[2][i])
             assert np.array_equal(x[1][i, :m], y[1][i, :m]) and np.array_equal(x[0][i, :m], y[0][i, :m])
-    # new deletions: an exact select again
+    # new deletions: lower bounds still, and the fresh build's hits
     rng = np.random.default_rng(5)
     deleted = (rng.random(c.n_docs) < 0.02).astype(np.uint8)
     re2 = ix.rescore(g2, deleted)
     fresh2 = native.Index.from_docs(ctx, c.off, c.tok, synth.VOCAB, threads=16, global_stats=g2, deleted=deleted)
     for t in terms[::7]:
-        assert np.array_equal(re2.term_kth(t), fresh2.term_kth(t)), t
+        assert (re2.term_kth(t) <= fresh2.term_kth(t)).all(), t
+    for mode, k in ((native.MODE_OR, 20), (native.MODE_AND, 100)):
+        x = re2.search_batch(q_off, qt, k, mode=mode)
+        y = fresh2.search_batch(q_off, qt, k, mode=mode)
+        assert np.array_equal(x[2], y[2])
+        for i in range(len(x[2])):
+            m = int(x[2][i])
+            assert np.array_equal(x[1][i, :m], y[1][i, :m]) and np.array_equal(x[0][i, :m], y[0][i, :m])
     for x in (re, re2, fresh, fresh2, ix):
         x.close()

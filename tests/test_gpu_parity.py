@@ -465,21 +465,18 @@ def test_single_list_block_max_vs_oracle(native, ctx, gpu_1m, oracle_1m, k):
 
 
 @pytest.mark.parametrize("env", [{"FUGU_RANK_GIB": "0"}, {"FUGU_RANK_GIB": "0.02", "FUGU_RANK_PLAIN_DIV": "16384"},
-                                 {"FUGU_RANK_GIB": "0", "FUGU_DENSE_GIB": "0.5"},
-                                 {"FUGU_RANK_GIB": "0.02", "FUGU_DENSE_GIB": "0.05", "FUGU_RANK_PLAIN_DIV": "16384"},
                                  {"FUGU_RANK_PLAIN_DIV": "16384"}, {"FUGU_RANK_PLAIN_DIV": "1"},
-                                 {"FUGU_RANK_GIB": "0.05", "FUGU_DENSE_GIB": "0.05", "FUGU_RANK_PLAIN_DIV": "16"}],
-                         ids=["directory_only", "few_rank_terms", "f32_tables", "mixed_kinds", "plain_rank_only",
-                              "sparse_rank_only", "all_kinds"])
+                                 {"FUGU_RANK_GIB": "0.05", "FUGU_RANK_PLAIN_DIV": "16"}],
+                         ids=["directory_only", "few_rank_terms", "plain_rank_only", "sparse_rank_only", "all_kinds"])
 def test_probe_structure_budgets_vs_oracle(native, ctx, corpus_1m, oracle_1m, env):
     """Every probe kind gives the oracle's results: the bucket directory alone
-    (no rank words), a budget that fits only the densest terms' rank words, the
-    f32 score tables, both dense kinds at once, plain rank words only (the
-    round-4 layout), sparse rank words wherever they are smaller, and every kind
-    at once (fg_internal.h DevIndex)."""
+    (no rank words), a budget that fits only the densest terms' rank words, plain
+    rank words only (the round-4 layout), sparse rank words wherever they are
+    smaller, and every kind at once (fg_internal.h DevIndex; the round-1 f32 score
+    tables went with the precomputed scores in round 6)."""
     import os
     from fugu_amd import synth
-    old = {k: os.environ.get(k) for k in ("FUGU_RANK_GIB", "FUGU_DENSE_GIB", "FUGU_RANK_PLAIN_DIV")}
+    old = {k: os.environ.get(k) for k in ("FUGU_RANK_GIB", "FUGU_RANK_PLAIN_DIV")}
     os.environ.update(env)
     try:
         ix = native.Index.from_docs(ctx, corpus_1m.off, corpus_1m.tok, 1 << 20, threads=16)
@@ -506,7 +503,7 @@ def test_probe_structure_budgets_vs_oracle(native, ctx, corpus_1m, oracle_1m, en
             assert st.n_sparse_rank_terms >= st.n_rank_terms - 200
         else:
             assert st.n_sparse_rank_terms < st.n_rank_terms  # the densest terms keep plain rank words
-    assert (st.n_dense_f32 > 0) == ("FUGU_DENSE_GIB" in env)
+    assert st.n_dense_f32 == 0
     for (m0, m1, k, mode) in [(3, 3, 100, native.MODE_AND), (1, 5, 1000, native.MODE_AND),
                               (2, 4, 1000, native.MODE_OR)]:
         q_off, terms = synth.queries(256, m0, m1, seed_q=55)

@@ -220,10 +220,19 @@ def _hist_worker(rank, world, port, outq):
                 hist[q, min((int(v) - int(alo[q])) >> sh, 511)] += 1
     p.hist = hist.reshape(-1).copy()
     buf = torch.zeros(nq * 512, dtype=torch.int32)
-    exchange_hist(p, 0, buf)
+    merged = exchange_hist(p, 0, buf)
     thr = [_hist_threshold(p.hist.reshape(nq, 512)[q], K, int(alo[q]), _bin_shift(int(alo[q]), int(max(ahi[q], alo[q]))))
            for q in range(nq)]
-    outq.put((rank, alo, ahi, hist, p.hist.reshape(nq, 512), thr))
+    after1 = p.hist.reshape(nq, 512).copy()
+    # a third part of the sweep: this rank counts more docs into the merged
+    # histogram, and the second exchange sums only what is new (prev)
+    more = np.zeros((nq, 512), np.int32)
+    rng = np.random.default_rng(200 + rank)
+    for q in range(nq):
+        more[q, rng.integers(0, 512, int(rng.integers(0, 30)))] += 1
+    p.hist = (after1 + more).reshape(-1).copy()
+    exchange_hist(p, 0, buf, prev=merged)
+    outq.put((rank, alo, ahi, hist, after1, thr, more, p.hist.reshape(nq, 512).copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -261,9 +270,11 @@ def test_two_rank_hist_exchange():
     nq, K = 48, 50
     sc = [_scores(r, nq) for r in range(world)]
     for r in range(world):
-        alo, ahi, own, summed, thr = got[r]
+        alo, ahi, own, summed, thr, _, summed2 = got[r]
         assert np.array_equal(alo, got[0][0]) and np.array_equal(ahi, got[0][1])
         assert np.array_equal(summed, got[0][2] + got[1][2])
+        # the second exchange: every rank's counts exactly once
+        assert np.array_equal(summed2, got[0][2] + got[1][2] + got[0][5] + got[1][5])
         for q in range(nq):
             los = [max(1, int(np.float32(s[q].max() / 256 if len(s[q]) else 0).view(np.uint32))) for s in sc]
             his = [int(np.float32(s[q].max() if len(s[q]) else 0).view(np.uint32)) for s in sc]
