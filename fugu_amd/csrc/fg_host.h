@@ -403,6 +403,15 @@ struct fg_index {
   // null; read and replaced with std::atomic_load / atomic_store
   std::shared_ptr<const std::vector<float>> kth_floor;
   // ---- structure (independent of the statistics; shared with rescored snapshots)
+  // The snapshot's own term dictionary (tantivy keeps one per segment): a build
+  // over far fewer distinct terms than the vocabulary it was given (a commit's
+  // new docs) numbers its terms locally, tmap[l] = the vocabulary id of local
+  // term l (ascending); empty: local ids ARE vocabulary ids.  Every per-term
+  // array here and on the device is indexed by local id; the C ABI takes
+  // vocabulary ids (fgh::local_term).  n_terms counts local terms, n_vocab the
+  // vocabulary (fg_index_stats::n_terms).
+  fgh::SharedVec<uint32_t> tmap;
+  uint32_t n_vocab = 0;
   fgh::SharedVec<uint64_t> off;
   fgh::SharedVec<uint32_t> df_text, df_name;  // this snapshot's own postings (tantivy's per-segment cost order)
   fgh::SharedVec<uint32_t> first_doc, last_doc;
@@ -494,11 +503,19 @@ struct fg_plan {
 
 
 namespace fgh {
+// the local id of vocabulary term t in snapshot ix (fg_index::tmap), or
+// 0xFFFFFFFF (>= n_terms: absent) when the snapshot holds no posting of it
+inline uint32_t local_term(const fg_index* ix, uint32_t t) {
+  if (ix->tmap.empty()) return t;
+  const auto it = std::lower_bound(ix->tmap.begin(), ix->tmap.end(), t);
+  return it != ix->tmap.end() && *it == t ? (uint32_t)(it - ix->tmap.begin()) : 0xFFFFFFFFu;
+}
 // Per-term bounds under a snapshot's current statistics from its build-time
 // tables (fugu.cpp): the score ratio factors, the largest score, and a lower
 // bound of the K-th best alive score (K the smallest stored level >= k; with_floor:
 // or the namespace-wide floor of a doc-sharded namespace's shard when higher)
 void term_ratio(const fg_index* ix, uint32_t t, float* rdn, float* rup);
 float term_max_now(const fg_index* ix, uint32_t t);
+float term_max_scaled(const fg_index* ix, uint32_t t, float rup);  // tmaxs[t] x rup, rounded up
 float term_kth_now(const fg_index* ix, uint32_t t, uint32_t k, bool with_floor);
 }  // namespace fgh

@@ -220,21 +220,26 @@ __host__ __device__ inline bool meta_rank(uint32_t meta) { return (meta >> 31) !
 // line of rank words covers 512 docs, so the candidates of a long lead list
 // share lines.
 //
-// Scores are formed AT QUERY TIME, as tantivy's TermScorer does
-// (src/db/search.rs:162 -> query/bm25.rs Bm25Weight::score): a posting's score
-// is w_text * (tf / (tf + cache[fn])) (+ the name field's part), with the
-// query's per-clause weights (DevPlan::q_wt / q_wn, from the Searcher-wide
-// statistics of the moment) and the snapshot's tf cache (DevIndex::cache, set by
-// the plan).  A commit therefore only builds its new segment; the older ones
-// keep every device array.  The MaxScore bounds (bmax, tmax, tsub, tmaxs,
-// cmax) are the scores' maxima under the statistics the snapshot was BUILT
-// with; a plan scales them by a per-clause factor q_rup >= the largest ratio of
-// a posting's current score to its build-time one (1 exactly when the
-// statistics are the build's).
+// Scores follow the statistics of the moment, as tantivy's TermScorer's do
+// (src/db/search.rs:162 -> query/bm25.rs Bm25Weight::score).  While a
+// snapshot's statistics are the ones it was built with, its postings' scores
+// are the build's (psc: one 4-B load, k_score computed them once).  After a
+// commit elsewhere in the namespace changed the statistics (fg_index_rescore),
+// the kernels form them AT QUERY TIME instead: w_text * (tf / (tf + cache[fn]))
+// (+ the name field's part) from the posting's payload (tfn), the query's
+// per-clause weights (DevPlan::q_wt / q_wn) and the snapshot's tf cache
+// (DevIndex::cache, set by the plan) -- so a commit only builds its new segment
+// and the older ones keep every device array.  The MaxScore bounds (bmax, tmax,
+// tsub, tmaxs, cmax) are the maxima under the build's statistics; a plan scales
+// them by a per-clause factor q_rup >= the largest ratio of a posting's current
+// score to its build-time one (1 exactly when the statistics are the build's).
 constexpr uint32_t kTfEsc = 255;  // tfn's tf byte: >= this -> the exact tf is in esc_pos / esc_tf
 __host__ __device__ inline uint32_t tfn_pack(uint32_t tf, uint32_t fn) { return (fn << 8) | (tf < kTfEsc ? tf : kTfEsc); }
 struct DevIndex {
   const uint32_t* doc;       // [P] doc ids, CSR by term, ascending within a term
+  const float* psc;          // [P] the posting's score under the statistics the snapshot was BUILT with
+                             //     (k_score, tantivy's f32 order): what a plan over snapshots whose
+                             //     statistics are still the build's reads (DevPlan::feat without kFQt)
   const uint16_t* tfn;       // [P] (fn_text[doc] << 8) | min(tf_text, 255): tf_text 0 = no text occurrence
   const uint16_t* tfn_name;  // [P] the same for the `name` field, or nullptr (no name postings)
   const uint64_t* esc_pos;   // [n_esc] postings whose tf byte is kTfEsc in either field, ascending
@@ -350,8 +355,10 @@ struct DevPlan {
   uint32_t* cand_cnt;           // [nq] keys appended to each query's candidate list
   uint64_t* cand_keys;          // [cand_off[nq]] per-query candidate lists
   uint64_t* diag;               // diagnostic builds only (-DFG_DIAG): per-workgroup stamps
-  uint32_t feat;                // kernel features the plan's snapshots need: bit 0 `name` postings (tfn_name),
-                                // bit 1 escaped tf bytes (DevIndex::esc_pos); the kernels are instantiated per value
+  uint32_t feat;                // kernel features the plan's snapshots need: bit 2 query-time scores (a snapshot
+                                // whose statistics changed since its build), with bit 0 `name` postings
+                                // (tfn_name) and bit 1 escaped tf bytes (esc_pos); the kernels are instantiated
+                                // per value (0, 4 = query-time, 7 = query-time with names / escapes)
   uint32_t n_single;            // k_conj: the first n_single work items belong to single-list queries
   uint32_t n_scan;              // k_scan work items (queries with no text terms), after the total_chunks
                                 // k_conj / k_disj items in work_q / work_c / work_n

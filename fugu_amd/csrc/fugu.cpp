@@ -610,14 +610,19 @@ void term_ratio(const fg_index* ix, uint32_t t, float* rdn, float* rup) {
   *rdn = std::max(fd, 0.0f);
 }
 // the largest current score of term t (an upper bound; exact without a statistics change)
-float term_max_now(const fg_index* ix, uint32_t t) {
+float term_max_scaled(const fg_index* ix, uint32_t t, float rup) {
   if (t >= ix->n_terms) return 0.0f;
-  float rdn, rup;
-  term_ratio(ix, t, &rdn, &rup);
+  if (rup == 1.0f) return ix->tmaxs[t];
   const double v = (double)ix->tmaxs[t] * rup;
   float f = (float)v;
   if ((double)f < v) f = std::nextafter(f, HUGE_VALF);
   return f;
+}
+float term_max_now(const fg_index* ix, uint32_t t) {
+  if (t >= ix->n_terms) return 0.0f;
+  float rdn, rup;
+  term_ratio(ix, t, &rdn, &rup);
+  return term_max_scaled(ix, t, rup);
 }
 // a lower bound of term t's K-th best current score over the alive docs, K the
 // smallest stored level >= k (0: none): the build's K'-th best for the smallest
@@ -687,20 +692,21 @@ static int ktop_pass(const fg_index* ix, fg::ScoreJob& j) {
   return FG_OK;
 }
 
-// Every posting's score under the snapshot's CURRENT statistics into a
-// stream-ordered temporary (k_score), for the bound kernels of a build and for
-// fg_index_term_ladder.  `tmp` returns the temporary (freed stream-ordered by
-// the caller); j gets the postings inputs, the weights and caches (inside tmp)
-// and j.psc / j.cmax (cmax: the caller's, or a scratch part of tmp).
-static int score_postings(const fg_index* ix, fg::ScoreJob& j, float* cmax, void** tmp) {
+// Every posting's score under the snapshot's CURRENT statistics (k_score) into
+// `psc` (a build's bound block) or a stream-ordered temporary, for the bound
+// kernels of a build and for fg_index_term_ladder.  `tmp` returns the temporary
+// (freed stream-ordered by the caller); j gets the postings inputs, the weights
+// and caches (inside tmp) and j.psc / j.cmax (cmax: the caller's, or a scratch
+// part of tmp).
+static int score_postings(const fg_index* ix, fg::ScoreJob& j, float* cmax, float* psc, void** tmp) {
   const uint32_t V = ix->n_terms;
   auto al = [](size_t x) { return (std::max<size_t>(x, 16) + 255) & ~size_t(255); };
-  const size_t b_psc = al(4ull * ix->n_postings + 16), b_w = al(4ull * V), b_c = al(4ull * 512),
+  const size_t b_psc = psc ? 0 : al(4ull * ix->n_postings + 16), b_w = al(4ull * V), b_c = al(4ull * 512),
                b_cm = cmax ? 0 : al(4ull * ix->n_sc);
   if (fgh::dev_malloc_async(tmp, b_psc + 2 * b_w + b_c + b_cm, kBuildStream) != hipSuccess)
     return fail(FG_EOOM, "hipMallocAsync(%zu) failed", b_psc + 2 * b_w + b_c + b_cm);
   char* t = static_cast<char*>(*tmp);
-  float* d_psc = reinterpret_cast<float*>(t);
+  float* d_psc = psc ? psc : reinterpret_cast<float*>(t);
   float* d_wt = reinterpret_cast<float*>(t + b_psc);
   float* d_wn = reinterpret_cast<float*>(t + b_psc + b_w);
   float* d_cache = reinterpret_cast<float*>(t + b_psc + 2 * b_w);
@@ -744,10 +750,11 @@ int build_bounds(fg_index* ix, const std::vector<uint32_t>& alive) {
   const uint32_t V = ix->n_terms;
   HIPCHK(hipSetDevice(ix->dev));
   struct Part { size_t bytes; void** out; };
-  float *d_bmax, *d_ktop, *d_cmax;
+  float *d_psc, *d_bmax, *d_ktop, *d_cmax;
   uint64_t* d_tsub = nullptr;
   uint32_t *d_alive = nullptr, *d_tmaxs, *d_tmax;
   const Part parts[] = {
+      {4ull * ix->n_postings + 16, reinterpret_cast<void**>(&d_psc)},  // 16 B of slack after the scores
       {alive.empty() ? 0 : 4ull * alive.size(), reinterpret_cast<void**>(&d_alive)},
       {4ull * ix->dir_entries, reinterpret_cast<void**>(&d_bmax)},
       {4ull * V, reinterpret_cast<void**>(&d_tmaxs)},
@@ -783,7 +790,7 @@ int build_bounds(fg_index* ix, const std::vector<uint32_t>& alive) {
   g_bt.mark("bound tables + uploads");
   fg::ScoreJob j{};
   void* tmp = nullptr;
-  if (int rc = score_postings(ix, j, d_cmax, &tmp)) return rc;
+  if (int rc = score_postings(ix, j, d_cmax, d_psc, &tmp)) return rc;
   struct TmpBack {
     void* p;
     ~TmpBack() { (void)hipFreeAsync(p, kBuildStream); }
@@ -841,6 +848,7 @@ int build_bounds(fg_index* ix, const std::vector<uint32_t>& alive) {
   ix->h_alive_b = ix->h_alive;
   ix->n_dead = 0;
   relate_stats(ix);
+  ix->d.psc = d_psc;
   ix->d.bmax = d_bmax;
   ix->d.tmaxs = reinterpret_cast<const float*>(d_tmaxs);
   ix->d.tmax = reinterpret_cast<const float*>(d_tmax);
@@ -864,6 +872,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
   ix->smem->dev = dev;
   ix->n_docs = hp.n_docs;
   ix->n_terms = hp.n_terms;
+  ix->n_vocab = hp.n_terms;
   ix->has_name = hp.has_name;
   ix->n_postings = hp.off[hp.n_terms];
   ix->tot_local[0] = hp.tot[0];
@@ -1593,6 +1602,86 @@ int fg_docs_facet_stats(const fg_docs_input* in, uint32_t* df_facet, uint64_t* t
   return FG_OK;
 }
 
+}  // extern "C"
+
+// A build's own term dictionary (fg_index::tmap).  Its docs' distinct terms are
+// marked in a vocabulary bitset; when they are fewer than 1/kLocalDiv of the
+// vocabulary (a commit's 1000 new docs hold ~2% of a 10M-doc namespace's), the
+// build runs on local ids: the tokens renumbered in vocabulary order (a rank in
+// the bitset) and the statistics gathered to them, so its work and its device
+// arrays scale with its own terms, not the vocabulary's.  The marking stops as
+// soon as the count passes the limit (a large build decides within its first
+// docs).  L.tmap stays empty: vocabulary ids.
+namespace {
+constexpr uint32_t kLocalDiv = 4;
+struct LocalDict {
+  std::vector<uint32_t> tmap, ttok, ntok, df_t, df_n;
+  fg_docs_input in{};
+  fg_global_stats g{};
+};
+int local_dict(const fg_docs_input* in, const fg_global_stats* g, LocalDict& L) {
+  const uint32_t N = in->n_docs, V = in->n_terms;
+  const bool has_name = in->name_off && in->name_tok;
+  const uint64_t limit = V / kLocalDiv;
+  std::vector<uint64_t> bits(((uint64_t)V + 63) / 64, 0);
+  uint64_t n = 0;
+  auto mark = [&](const uint32_t* tok, uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      const uint32_t t = tok[i];
+      if (t >= V) return false;
+      uint64_t& w = bits[t >> 6];
+      const uint64_t m = 1ull << (t & 63);
+      n += (w & m) == 0;
+      w |= m;
+    }
+    return true;
+  };
+  for (uint32_t d = 0; d < N && n <= limit; ++d) {
+    if (!mark(in->text_tok, in->text_off[d], in->text_off[d + 1])) return fail(FG_EINVAL, "token id >= n_terms");
+    if (has_name && !mark(in->name_tok, in->name_off[d], in->name_off[d + 1]))
+      return fail(FG_EINVAL, "token id >= n_terms");
+  }
+  if (n > limit || n == 0) return FG_OK;
+  const uint32_t v = (uint32_t)n;
+  std::vector<uint32_t> rank(bits.size());
+  L.tmap.reserve(v);
+  for (size_t w = 0; w < bits.size(); ++w) {
+    rank[w] = (uint32_t)L.tmap.size();
+    for (uint64_t x = bits[w]; x; x &= x - 1) L.tmap.push_back((uint32_t)(w * 64 + __builtin_ctzll(x)));
+  }
+  auto local = [&](uint32_t t) {
+    return rank[t >> 6] + (uint32_t)__builtin_popcountll(bits[t >> 6] & ((1ull << (t & 63)) - 1));
+  };
+  const uint64_t nt = in->text_off[N], nn = has_name ? in->name_off[N] : 0;
+  L.ttok.resize(nt);
+  for (uint64_t i = in->text_off[0]; i < nt; ++i) L.ttok[i] = local(in->text_tok[i]);
+  if (has_name) {
+    L.ntok.resize(nn);
+    for (uint64_t i = in->name_off[0]; i < nn; ++i) L.ntok[i] = local(in->name_tok[i]);
+  }
+  L.in = *in;
+  L.in.n_terms = v;
+  L.in.text_tok = L.ttok.data();
+  if (has_name) L.in.name_tok = L.ntok.data();
+  if (g) {
+    L.df_t.resize(v);
+    L.df_n.resize(v);
+    for (uint32_t l = 0; l < v; ++l) {
+      L.df_t[l] = g->df_text[L.tmap[l]];
+      L.df_n[l] = g->df_name ? g->df_name[L.tmap[l]] : 0u;
+    }
+    L.g = *g;
+    L.g.df_text = L.df_t.data();
+    L.g.df_name = g->df_name ? L.df_n.data() : nullptr;
+  }
+  return FG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+static int build_from_docs(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g, fg_index** out);
+
 int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g,
                                     fg_index** out) {
   if (!ctx || !in || !out || !in->text_off || (!in->text_tok && in->text_off[in->n_docs] > 0))
@@ -1601,9 +1690,29 @@ int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* i
     return fail(FG_EINVAL, "bad global statistics");
   if (in->n_docs == 0) return fail(FG_EINVAL, "empty index (n_docs == 0)");
   if (in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs must be < 2^31 (tantivy DocId)");
+  g_bt.start();
+  LocalDict L;
+  if (int rc = local_dict(in, g, L)) return rc;
+  if (L.tmap.empty()) return build_from_docs(ctx, dev, in, g, out);
+  g_bt.mark("local dictionary");
+  const uint32_t V = in->n_terms;
+  fg_index* ix = nullptr;
+  if (int rc = build_from_docs(ctx, dev, &L.in, g ? &L.g : nullptr, &ix)) return rc;
+  ix->tmap = std::move(L.tmap);
+  ix->n_vocab = V;
+  *out = ix;
+  return FG_OK;
+}
+
+static int build_from_docs(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g, fg_index** out) {
+  if (!ctx || !in || !out || !in->text_off || (!in->text_tok && in->text_off[in->n_docs] > 0))
+    return fail(FG_EINVAL, "bad arguments");
+  if (g && (!g->df_text || g->n_docs < in->n_docs || g->n_docs >= 0x7FFFFFFFull))
+    return fail(FG_EINVAL, "bad global statistics");
+  if (in->n_docs == 0) return fail(FG_EINVAL, "empty index (n_docs == 0)");
+  if (in->n_docs >= 0x7FFFFFFFu) return fail(FG_EINVAL, "n_docs must be < 2^31 (tantivy DocId)");
   if (std::find(ctx->devs.begin(), ctx->devs.end(), dev) == ctx->devs.end())
     return fail(FG_EINVAL, "device %d not in context", dev);
-  g_bt.start();
   const uint32_t N = in->n_docs, V = in->n_terms;
   const bool has_name_in = in->name_off && in->name_tok;
   // every thread of pass 1 zeroes and merges three vocabulary-sized count
@@ -1801,11 +1910,36 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   if (g->n_docs < N || g->n_docs >= 0x7FFFFFFFull) return fail(FG_EINVAL, "bad global statistics");
   if (base->has_name && !g->df_name) return fail(FG_EINVAL, "global statistics lack df_name for a snapshot with names");
   if (VF && !g->df_facet) return fail(FG_EINVAL, "global statistics lack df_facet for a faceted snapshot");
-  for (uint32_t t = 0; t < V; ++t)
-    if (g->df_text[t] < base->df_text[t] || (g->df_name ? g->df_name[t] : 0u) < base->df_name[t])
-      return fail(FG_EINVAL, "global df of term %u is below this snapshot's", t);
-  for (uint32_t t = 0; t < VF; ++t)
-    if (g->df_facet[t] < base->df_facet_local[t]) return fail(FG_EINVAL, "global facet df of term %u is below this snapshot's", t);
+  // the statistics' doc frequencies of the snapshot's terms (gathered to local
+  // ids when it has its own dictionary: a commit's rescores then cost its terms)
+  const uint32_t* gt = g->df_text;
+  const uint32_t* gn = g->df_name;
+  std::vector<uint32_t> lt, ln;
+  if (!base->tmap.empty()) {
+    const uint32_t* tm = base->tmap.data();
+    lt.resize(V);
+    for (uint32_t t = 0; t < V; ++t) lt[t] = g->df_text[tm[t]];
+    gt = lt.data();
+    if (g->df_name) {
+      ln.resize(V);
+      for (uint32_t t = 0; t < V; ++t) ln[t] = g->df_name[tm[t]];
+      gn = ln.data();
+    }
+    wts = nullptr;  // (shared weights are vocabulary-indexed)
+  }
+  {  // (branch-free scans: every older segment of every commit runs them over its terms)
+    const uint32_t* bt = base->df_text.data();
+    bool bad = false;
+    for (uint32_t t = 0; t < V; ++t) bad |= gt[t] < bt[t];
+    if (gn) {
+      const uint32_t* bn = base->df_name.data();
+      for (uint32_t t = 0; t < V; ++t) bad |= gn[t] < bn[t];
+    } else if (base->has_name) {
+      bad = true;
+    }
+    for (uint32_t t = 0; t < VF; ++t) bad |= g->df_facet[t] < base->df_facet_local[t];
+    if (bad) return fail(FG_EINVAL, "global doc frequencies below this snapshot's own");
+  }
   g_bt.start();
   auto ix = std::make_unique<fg_index>();
   ix->dev = base->dev;
@@ -1817,6 +1951,8 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   ix->struct_bytes = base->struct_bytes;
   ix->n_docs = N;
   ix->n_terms = V;
+  ix->n_vocab = base->n_vocab;
+  ix->tmap = base->tmap;
   ix->has_name = base->has_name;
   ix->n_postings = base->n_postings;
   ix->dir_entries = base->dir_entries;
@@ -1872,8 +2008,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
   std::memcpy(ix->cache_b, base->cache_b, sizeof ix->cache_b);
   ix->h_alive_b = base->h_alive_b;
   ix->device_bytes = base->device_bytes;
-  set_stats(ix.get(), g->n_docs, g->tot_tokens, g->df_text, g->df_name, g->tot_facet_tokens, VF ? g->df_facet : nullptr,
-            wts);
+  set_stats(ix.get(), g->n_docs, g->tot_tokens, gt, gn, g->tot_facet_tokens, VF ? g->df_facet : nullptr, wts);
   relate_stats(ix.get());
   // deletions: the alive bitset (the base's device copy when unchanged), and
   // the docs dead now that ktop's selection counted alive (term_kth)
@@ -1926,13 +2061,14 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
   uint32_t V = 0;
   for (uint32_t i = 0; i < n; ++i) {
     if (!bases[i]) return fail(FG_EINVAL, "NULL snapshot %u", i);
-    V = std::max(V, bases[i]->n_terms);
+    if (bases[i]->tmap.empty()) V = std::max(V, bases[i]->n_terms);
     outs[i] = nullptr;
   }
   if (n == 0) return FG_OK;
-  // the weights once for every snapshot (they depend on the statistics only)
+  // the weights once for every snapshot on vocabulary ids (they depend on the
+  // statistics only; a snapshot with its own dictionary gathers its own)
   fgh::Weights wts;
-  {
+  if (V) {
     std::vector<float> wt, wn;
     bm25_weights(g->n_docs, g->df_text, g->df_name, V, wt, wn);
     wts.wt = std::move(wt);
@@ -1973,7 +2109,7 @@ int fg_index_release(fg_index* ix) {
 int fg_index_stats_get(const fg_index* ix, fg_index_stats* o) {
   if (!ix || !o) return fail(FG_EINVAL, "bad arguments");
   o->n_docs = ix->n_docs;
-  o->n_terms = ix->n_terms;
+  o->n_terms = ix->n_vocab;
   o->n_postings = ix->n_postings;
   o->device_bytes = ix->device_bytes;
   o->tot_tokens[0] = ix->tot[0];
@@ -1995,7 +2131,9 @@ int fg_index_stats_get(const fg_index* ix, fg_index_stats* o) {
 
 uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term) {
   if (ix && field == FG_FIELD_FACET) return term < ix->n_fterms ? ix->df_facet[term] : 0;
-  if (!ix || term >= ix->n_terms) return 0;
+  if (!ix) return 0;
+  term = fgh::local_term(ix, term);
+  if (term >= ix->n_terms) return 0;
   if (field == FG_FIELD_TEXT) return ix->df_text[term];
   if (field == FG_FIELD_NAME) return ix->df_name[term];
   return ix->off[term + 1] - ix->off[term];
@@ -2004,6 +2142,7 @@ uint64_t fg_index_df(const fg_index* ix, int field, uint32_t term) {
 int fg_index_term_kth(const fg_index* ix, uint32_t term, float* out) {
   if (!ix || !out) return fail(FG_EINVAL, "bad arguments");
   static_assert(fg::kNumTopK == 5, "fugu.h documents five K");
+  term = fgh::local_term(ix, term);
   for (uint32_t k = 0; k < fg::kNumTopK; ++k) out[k] = fgh::term_kth_now(ix, term, fg::kTopKs[k], false);
   return FG_OK;
 }
@@ -2028,7 +2167,7 @@ int fg_index_term_ladder(const fg_index* ix, float* out) {
   // the posting scores under the snapshot's statistics (a temporary), then k_ktop with the extra levels
   fg::ScoreJob j{};
   void* ptmp = nullptr;
-  if (int rc = score_postings(ix, j, nullptr, &ptmp)) return rc;
+  if (int rc = score_postings(ix, j, nullptr, nullptr, &ptmp)) return rc;
   struct PBack {
     void* p;
     ~PBack() { (void)hipFreeAsync(p, kBuildStream); }
@@ -2050,10 +2189,13 @@ int fg_index_term_ladder(const fg_index* ix, float* out) {
       if (fg::kLadderExtra[i] == fg::kLadderKs[l]) src[l] = 0x10000u | i;
     if (src[l] == 0xFFFFFFFFu) return fail(FG_EINVAL, "ladder level %u unmapped", l);
   }
+  // (vocabulary ids: a snapshot with its own dictionary scatters its terms, zeros elsewhere)
+  const uint32_t* tm = ix->tmap.empty() ? nullptr : ix->tmap.data();
+  if (tm) std::fill(out, out + (size_t)ix->n_vocab * fg::kNumLadder, 0.0f);
   for (uint32_t t = 0; t < V; ++t)
     for (uint32_t l = 0; l < fg::kNumLadder; ++l) {
       const uint32_t s = src[l];
-      out[(size_t)t * fg::kNumLadder + l] = (s & 0x10000u) ? h[nm + (size_t)t * fg::kNumLadderExtra + (s & 0xFFFFu)]
+      out[(size_t)(tm ? tm[t] : t) * fg::kNumLadder + l] = (s & 0x10000u) ? h[nm + (size_t)t * fg::kNumLadderExtra + (s & 0xFFFFu)]
                                                             : h[(size_t)t * fg::kNumTopK + s];
     }
   return FG_OK;
@@ -2100,8 +2242,16 @@ int fg_index_set_kth_floor(fg_index* ix, const float* floor, uint32_t n_terms) {
   if (!ix) return fail(FG_EINVAL, "NULL index");
   std::shared_ptr<const std::vector<float>> f;
   if (floor) {
-    if (n_terms != ix->n_terms) return fail(FG_EINVAL, "floor of %u terms for a snapshot of %u", n_terms, ix->n_terms);
-    f = std::make_shared<const std::vector<float>>(floor, floor + (size_t)n_terms * fg::kNumTopK);
+    if (n_terms != ix->n_vocab) return fail(FG_EINVAL, "floor of %u terms for a snapshot of %u", n_terms, ix->n_vocab);
+    if (ix->tmap.empty()) {
+      f = std::make_shared<const std::vector<float>>(floor, floor + (size_t)n_terms * fg::kNumTopK);
+    } else {  // gathered to local ids
+      std::vector<float> v((size_t)ix->n_terms * fg::kNumTopK);
+      for (uint32_t t = 0; t < ix->n_terms; ++t)
+        std::copy(floor + (size_t)ix->tmap[t] * fg::kNumTopK, floor + (size_t)(ix->tmap[t] + 1) * fg::kNumTopK,
+                  v.begin() + (size_t)t * fg::kNumTopK);
+      f = std::make_shared<const std::vector<float>>(std::move(v));
+    }
   }
   std::atomic_store(&ix->kth_floor, f);
   return FG_OK;
@@ -2109,6 +2259,7 @@ int fg_index_set_kth_floor(fg_index* ix, const float* floor, uint32_t n_terms) {
 
 int fg_index_bm25(const fg_index* ix, uint32_t term, float* w_text, float* w_name, float* cache512) {
   if (!ix) return fail(FG_EINVAL, "NULL index");
+  term = fgh::local_term(ix, term);
   if (term < ix->n_terms) {
     if (w_text) *w_text = ix->w_text[term];
     if (w_name) *w_name = ix->w_name[term];
@@ -2283,7 +2434,9 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   q_hhi.assign(nq, 0x3F800000u);
   q_hsh.assign(nq, 31);
   auto present = [&](uint32_t t) { return t < ix->n_terms && ix->off[t + 1] > ix->off[t]; };
-  // a clause's query-time weights and bound factor (DevPlan::q_wt / q_wn / q_rup)
+  // a clause's query-time weights and bound factor (DevPlan::q_wt / q_wn / q_rup),
+  // and its largest current score into cm[j] (the ratio computed once per clause)
+  float cm[fg::kMaxTerms];
   auto set_clause = [&](uint32_t i, uint32_t j, uint32_t t) {
     const size_t x = (size_t)i * fg::kMaxTerms + j;
     h.q_wt[x] = ix->w_text[t];
@@ -2291,6 +2444,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     float rdn, rup;
     fgh::term_ratio(ix, t, &rdn, &rup);
     h.q_rup[x] = rup;
+    cm[j] = fgh::term_max_scaled(ix, t, rup);
   };
   // histogram bins of query i: bin 0 at the starting threshold (or ub / 256), the
   // top bin at the query's largest possible score ub; ~kQBins bins between
@@ -2334,7 +2488,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     uint32_t nm = 0, ns = 0, nx = 0;
     bool must_missing = false;
     for (uint32_t j = 0; j < m; ++j) {
-      const uint32_t t = q->terms[b + j];
+      const uint32_t t = fgh::local_term(ix, q->terms[b + j]);  // (the snapshot's own ids from here on)
       const uint8_t oc = q->occur ? q->occur[b + j] : (disj ? FG_OCCUR_SHOULD : FG_OCCUR_MUST);
       if (oc > FG_OCCUR_MUST_NOT) return fail(FG_EINVAL, "query %u: bad occur %u", i, (unsigned)oc);
       if (oc == FG_OCCUR_MUST) {
@@ -2377,7 +2531,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
         if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
       }
       float ub = fmx;
-      for (uint32_t c = 0; c < ns; ++c) ub += fgh::term_max_now(ix, qt[c]);
+      for (uint32_t c = 0; c < ns; ++c) ub += cm[c];
       set_bins(i, ub);
 
       const uint32_t tlo = dlo >> fg::kDisjTileShift, thi = dhi >> fg::kDisjTileShift;
@@ -2419,7 +2573,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     {
       float acc = 0.0f;
       for (uint32_t j = mt; j-- > 1;) {
-        if (j < nm || j >= nm + nx) acc += fgh::term_max_now(ix, qt[j]);
+        if (j < nm || j >= nm + nx) acc += cm[j];
         q_ub[(size_t)i * fg::kMaxTerms + j] = acc;
       }
     }
@@ -2432,9 +2586,9 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       if (v > 0.0f) thr0[i] = fg::make_key(v, 0xFFFFFFFFu);  // lowest key with score v
     }
     {
-      float ub = fmx + fgh::term_max_now(ix, qt[0]);
+      float ub = fmx + cm[0];
       for (uint32_t j = 1; j < mt; ++j)
-        if (j < nm || j >= nm + nx) ub += fgh::term_max_now(ix, qt[j]);
+        if (j < nm || j >= nm + nx) ub += cm[j];
       set_bins(i, ub);
     }
     const uint64_t df0 = ix->off[qt[0] + 1] - ix->off[qt[0]];
@@ -2840,8 +2994,12 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->d.k = k;
   p->d.seg_nq = S > 1 ? nq1 : 0;
   p->d.n_segs = S;
+  // query-time scores when some snapshot's statistics changed since its build
+  // (a commit elsewhere in the namespace); else the build-time scores
   p->d.feat = 0;
   for (uint32_t x = 0; x < S; ++x)
+    if (!ixs[x]->same_stats) p->d.feat = 4u;
+  for (uint32_t x = 0; x < S && p->d.feat; ++x)
     p->d.feat |= (ixs[x]->d.tfn_name ? 1u : 0u) | (ixs[x]->d.n_esc ? 2u : 0u);
   // several snapshots: a batch query's slots share its threshold score-only, so a
   // doc of another snapshot tied with the k-th score is never pruned (the merge

@@ -1795,16 +1795,26 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
   uint64_t ver0 = 0;
   uint32_t n_terms = 0, n_fterms = 0;
   bool any_name = false;
+  // under the writer lock only what upserts change (the deletion flags, the
+  // statistics); the docs' tokens are read after it (appended docs never change
+  // but for `deleted`), so upserts and commits go on while a large merge gathers
+  std::vector<uint8_t> del0;
   {
     std::lock_guard<std::mutex> w(ns.writer);
     n_terms = std::max<uint32_t>(1, (uint32_t)ns.dict.size());
     n_fterms = (uint32_t)ns.fdict.size();
+    del0 = ns.del;
+    for (uint32_t g : ns.pend_del) del0[g] = 0;  // committed deletions only
+    any_name = ns.any_name;
+    S.load(ns, n_terms, n_fterms);
+    ver0 = ns.st_ver;
+  }
+  tr.mark("gather (writer lock)");
+  {
     std::vector<uint32_t> dt(n_terms, 0), dn(n_terms, 0), dfc(n_fterms, 0), scratch;
-    const std::unordered_set<uint32_t> pend(ns.pend_del.begin(), ns.pend_del.end());
-    auto gone = [&](uint32_t g) { return ns.del[g] && !pend.count(g); };  // a committed deletion
     for (const Segment& sg : src) {
       bool has_del = false;
-      for (uint32_t d = 0; d < sg.n && !has_del; ++d) has_del = gone(sg.global(d));
+      for (uint32_t d = 0; d < sg.n && !has_del; ++d) has_del = del0[sg.global(d)] != 0;
       if (!has_del) {
         mst->tot[0] += sg.st->tot[0];
         mst->tot[1] += sg.st->tot[1];
@@ -1812,8 +1822,8 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
       }
       for (uint32_t d = 0; d < sg.n; ++d) {
         const uint32_t gd = sg.global(d);
+        if (del0[gd]) continue;
         const Doc& doc = ns.docs[gd];
-        if (gone(gd)) continue;
         ids.push_back(gd);
         buf.add(doc, false);
         mst->n++;
@@ -1830,13 +1840,10 @@ int merge_once(fg_db* db, Namespace& ns, bool* did) {
     mst->df_t = sparse_of(dt);
     mst->df_n = sparse_of(dn);
     mst->df_f = sparse_of(dfc);
-    any_name = ns.any_name;
-    S.load(ns, n_terms, n_fterms);
     for (const Segment& sg : src) S.add(*sg.st, true);
     S.add(*mst, false);
-    ver0 = ns.st_ver;
   }
-  tr.mark("gather (writer lock)");
+  tr.mark("gather docs");
   fg_index* mix = nullptr;
   if (!ids.empty()) {
     const fg_global_stats g = S.global();

@@ -92,11 +92,14 @@ __device__ inline const uint64_t* rank_base(const DevIndex& ix, uint32_t slot, u
 
 // A posting's tf / fieldnorm payload: tfn (text) in the low half, tfn_name
 // (name, when the snapshot has name postings) in the high half.
-// kF (the plan's DevPlan::feat, a template argument of the search kernels): bit 0
-// some snapshot has `name` postings, bit 1 some posting's tf byte escaped.  The
-// common plan (neither) carries no name or escape code: query-time scoring then
-// fits the kernels' register budgets (k_conj 128 VGPRs at 4 waves, k_disj 96 at 5).
-constexpr uint32_t kFName = 1, kFEsc = 2;
+// kF (the plan's DevPlan::feat, a template argument of the search kernels): 0
+// every snapshot's statistics are its build's: the build-time posting scores
+// (psc, one load); kFQt: scores formed at query time from the payloads, with
+// kFName (some snapshot has `name` postings) and kFEsc (some posting's tf byte
+// escaped) in the full variant.  Three instantiations (0, kFQt, kFQt | kFName |
+// kFEsc): the common ones carry no name or escape code and fit the kernels'
+// register budgets (k_conj 128 VGPRs at 4 waves, k_disj 96 at 5).
+constexpr uint32_t kFName = 1, kFEsc = 2, kFQt = 4;
 template <uint32_t kF>
 __device__ inline uint32_t tfn_load(const DevIndex& ix, uint64_t p) {
   uint32_t v = ix.tfn[p];
@@ -459,7 +462,7 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
   if (dslot) {
     // rank words: presence + rank in one 8-B load per item (all items'
     // loads in flight together; sparse ones: the block entries, then the
-    // words), then the payload of the hits
+    // words), then the score (or payload) of the hits
     uint32_t sh;
     const uint64_t* __restrict__ rw = rank_base(ix, dslot, sh);
     uint64_t x[N];
@@ -470,6 +473,15 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
       for (uint32_t j = 0; j < N; ++j) {
         x[j] = ix.srank_w[srank_index(x[j], doc[j])];
       }
+    }
+    if constexpr (!(kF & kFQt)) {  // the build-time scores: one load per hit
+      const float* __restrict__ ps = ix.psc + bi;
+#pragma unroll
+      for (uint32_t j = 0; j < N; ++j) {
+        const uint32_t p = rank_pos(x[j], doc[j]);
+        sc[j] = p != kInvalid ? ps[p] : -1.0f;
+      }
+      return;
     }
 #pragma unroll
     for (uint32_t j = 0; j < N; ++j) pos[j] = rank_pos(x[j], doc[j]);
@@ -497,6 +509,14 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
         if ((live & (1u << j)) && idx < hi[j] && di[idx] < doc[j]) pos[j] += half;
       }
     }
+    if constexpr (!(kF & kFQt)) {
+#pragma unroll
+      for (uint32_t j = 0; j < N; ++j) {
+        sc[j] = -1.0f;
+        if ((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j]) sc[j] = ix.psc[bi + pos[j]];
+      }
+      return;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < N; ++j)
       if (!((live & (1u << j)) && pos[j] < hi[j] && di[pos[j]] == doc[j])) pos[j] = kInvalid;
@@ -511,11 +531,8 @@ __device__ inline void probe_list(const DevIndex& ix, uint32_t ti, const uint32_
   for (uint32_t j = 0; j < N; ++j) {
     sc[j] = v[j] ? tfn_score_fast<kF>(v[j], wt, wn, ct, cn) : -1.0f;
     esc |= (tfn_escaped<kF>(v[j]) ? 1u : 0u) << j;
-    // one item's IEEE division at a time: interleaved, the N divisions' temporaries
-    // pushed k_conj past its 128 VGPRs
-    __builtin_amdgcn_sched_barrier(0);
   }
-  if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {
+  if constexpr ((kF & kFEsc) != 0) if (__builtin_expect(esc != 0, 0)) {
 #pragma unroll
     for (uint32_t j = 0; j < N; ++j)
       if ((esc >> j) & 1u) {
@@ -650,8 +667,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     sh.thr = thr0;
     pend = atomicMax(gthr, (unsigned long long)(thr0 & pl.pub_mask));
   }
-  // the tf caches into LDS (read after the first chunk's barrier)
-  for (uint32_t i = tid; i < (ix.tfn_name ? 512u : 256u); i += kThreads) sh.cache[i] = ix.cache[i];
+  // query-time scores: the tf caches into LDS (read after the first chunk's barrier)
+  if constexpr (kF & kFQt)
+    for (uint32_t i = tid; i < ((kF & kFName) && ix.tfn_name ? 512u : 256u); i += kThreads) sh.cache[i] = ix.cache[i];
 #ifdef FG_DIAG
   if (tid < 8) sh.dgc[tid] = 0;
 #endif
@@ -688,21 +706,21 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
         // predicated loads: tools/ab_variants.py measured clamped unconditional
         // loads (every lane issuing) slower here, 1.57 -> 2.05 ms
         doc[j] = in ? ix.doc[base0 + idx] : kInvalid;
-        tv[j] = in ? tfn_load<kF>(ix, base0 + idx) : 0u;
+        if constexpr (kF & kFQt) tv[j] = in ? tfn_load<kF>(ix, base0 + idx) : 0u;
+        else s0[j] = in ? ix.psc[base0 + idx] : 0.0f;
         live |= (in ? 1u : 0u) << j;
       }
       if (tid == 0 && pend > sh.thr) sh.thr = pend;
       __syncthreads();
-      // the lead postings' scores (query-time BM25, the caches now in LDS)
+      // the lead postings' query-time scores (the caches now in LDS)
       const float w0t = qwt[0], w0n = qwn[0];
       uint32_t esc = 0;
 #pragma unroll
-      for (uint32_t j = 0; j < kItems; ++j) {
+      for (uint32_t j = 0; j < kItems && (kF & kFQt); ++j) {
         s0[j] = tv[j] ? tfn_score_fast<kF>(tv[j], w0t, w0n, sh.cache, sh.cache + 256) : 0.0f;
         esc |= (tfn_escaped<kF>(tv[j]) ? 1u : 0u) << j;
-        __builtin_amdgcn_sched_barrier(0);  // (as probe_list: one division at a time)
       }
-      if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {
+      if constexpr ((kF & kFEsc) != 0) if (__builtin_expect(esc != 0, 0)) {
 #pragma unroll
         for (uint32_t j = 0; j < kItems; ++j)
           if ((esc >> j) & 1u) {
@@ -959,7 +977,19 @@ constexpr uint32_t kMaxSeg = kDisjMaxPairs;    // (tile, clause) pairs per work 
 static_assert(kMaxSeg <= 2 * kThreads, "k_disj segment list: two (tile, clause) pairs per thread");
 static_assert(kMaxTiles <= 255 && kMaxTerms <= 16, "seg_info packs (tile << 4) | clause; cand (tile << 8) | clause");
 
-struct DisjShared {
+// Query-time scoring's LDS (kFQt plans only: a build-time-score plan's k_disj
+// keeps the LDS of round 5 -- past ~31.9 KB a CU holds 4 k_disj workgroups
+// instead of 5, ab_rsub_lds_cliff.log)
+template <bool kQt>
+struct DisjQt {
+  float c_wt[kMaxTerms], c_wn[kMaxTerms];  // query-time BM25 weights (text, name)
+  float cache[256];                        // the text field's tf cache (DevIndex::cache; name: from the plan)
+};
+template <>
+struct DisjQt<false> {};
+
+template <bool kQt>
+struct DisjShared : DisjQt<kQt> {
   alignas(16) uint64_t buf[kBufD];
   struct {
     // P: postings past bound 1 waiting for bound 2, (score bits << 32) | (clause
@@ -980,14 +1010,13 @@ struct DisjShared {
   float r_ub[kMaxSeg];
   uint16_t b_ess[kMaxTiles * 8];     // S: essential-clause mask per 512-doc block
   uint64_t r_sub[kMaxSeg];           // R: the pair's sub-tile maxima (DevIndex::tsub; ~0: the tile bound)
-  uint32_t t_ess[kMaxTiles];         // essential-clause mask per tile (the union of its blocks')
-  uint32_t t_post[kMaxTiles];        // 1: the tile's essential postings are streamed, 0: skipped
+  uint16_t t_ess[kMaxTiles];         // essential-clause mask per tile (the union of its blocks')
+  uint32_t t_post;                   // bit t: tile t's essential postings are streamed (else skipped)
   uint16_t seg_info[kMaxSeg];        // P: (tile << 4) | clause of each segment
   // per-clause constants of the work item's query
-  uint32_t c_meta[kMaxTerms], c_dir[kMaxTerms], c_toff[kMaxTerms];
+  uint32_t c_meta[kMaxTerms], c_dir[kMaxTerms];
   uint64_t c_base[kMaxTerms];
-  float c_wt[kMaxTerms], c_wn[kMaxTerms];  // query-time BM25 weights (text, name)
-  float c_rup[kMaxTerms];                  // bound factors (DevPlan::q_rup)
+  float c_rup[kMaxTerms];            // bound factors (DevPlan::q_rup)
   uint32_t max_s, n_seg, n_post;
   uint32_t n_buf, n_cand;
   uint32_t n_q;                      // P: queued postings
@@ -997,8 +1026,8 @@ struct DisjShared {
   // hits per score bin not yet added to the global histogram: two u16 bins per
   // word (bin b in the half b & 1), flushed before any half could pass 65535
   uint32_t lh[kQBins / 2];
-  float cache[256];                  // the text field's tf cache (DevIndex::cache; name: from the plan)
 };
+static_assert(kMaxTiles <= 32, "DisjShared::t_post: one bit per tile");
 
 // Add the packed LDS bins (DisjShared::lh) to the query's global histogram and clear them.
 __device__ inline void hist_add16(uint32_t* lh, uint32_t* gh) {
@@ -1037,7 +1066,8 @@ struct QHist {
 // shared) threshold word.  A query's work items run about one after another
 // (the doc sweep keeps ~one per query in flight), so the LDS bins join the
 // query's histogram once, when the item ends.
-__device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr,
+template <class Sh>
+__device__ inline void disj_truncate(const DevIndex& ix, Sh& sh, uint32_t K, uint32_t limit, uint64_t* gthr,
                                      bool publish, const QHist& hq, uint64_t& pend) {
   uint32_t n = sh.n_buf;
   __syncthreads();  // every thread has read n before anyone appends again
@@ -1089,7 +1119,7 @@ __device__ inline void disj_truncate(const DevIndex& ix, DisjShared& sh, uint32_
 
 template <bool kMulti, uint32_t kF>
 __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, DevPlan pl) {
-  __shared__ DisjShared sh;
+  __shared__ DisjShared<(kF & kFQt) != 0> sh;
   const uint32_t tid = threadIdx.x;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
   const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -1136,12 +1166,14 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     sh.n_buf = 0;
     sh.n_cnt = 0;
     sh.n_lh = 0;
+    sh.t_post = 0;
     const uint64_t t0 = pl.q_thr0[q];
     const uint64_t g = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)t0);
     sh.thr = g > t0 ? g : t0;
   }
   for (uint32_t b = tid; b < kQBins / 2; b += kThreads) sh.lh[b] = 0;
-  for (uint32_t i = tid; i < 256; i += kThreads) sh.cache[i] = ix.cache[i];
+  if constexpr (kF & kFQt)
+    for (uint32_t i = tid; i < 256; i += kThreads) sh.cache[i] = ix.cache[i];
   // the name field's tf cache stays in the plan's copy (global, L1 / L2-resident): LDS
   // past ~32 KB drops k_disj from 5 to 4 workgroups per CU
   const float* const cn = ix.cache + 256;
@@ -1149,11 +1181,12 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     const uint32_t t = terms[tid];
     sh.c_meta[tid] = ix.tmeta[t];
     sh.c_dir[tid] = ix.dir_off[t];
-    sh.c_toff[tid] = ix.toff[t];
     sh.c_base[tid] = ix.off[t];
-    sh.c_wt[tid] = pl.q_wt[(size_t)q * kMaxTerms + tid];
-    sh.c_wn[tid] = pl.q_wn[(size_t)q * kMaxTerms + tid];
     sh.c_rup[tid] = pl.q_rup[(size_t)q * kMaxTerms + tid];
+    if constexpr (kF & kFQt) {
+      sh.c_wt[tid] = pl.q_wt[(size_t)q * kMaxTerms + tid];
+      sh.c_wn[tid] = pl.q_wn[(size_t)q * kMaxTerms + tid];
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -1172,9 +1205,10 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     const uint32_t* __restrict__ dir = ix.dir + sh.c_dir[i];
     uint32_t lo, hi;
     float ub;
-    if (B <= kTileShift && sh.c_toff[i] != kInvalid) {
+    const uint32_t toff = ix.toff[terms[i]];  // (L1-resident: the query's few terms)
+    if (B <= kTileShift && toff != kInvalid) {
       // the tile directory: adjacent entries (32 tiles of a clause per line)
-      const uint32_t to = sh.c_toff[i] + tile;
+      const uint32_t to = toff + tile;
       lo = ix.tdir[to];
       hi = ix.tdir[to + 1];
       ub = ix.tmax[to];
@@ -1207,7 +1241,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     // the build-time bound scaled to the query's statistics (q8_bound of tsub then
     // scales with it: DevPlan::q_rup carries a margin for the rounding)
     sh.r_ub[p] = lo < hi ? ub * sh.c_rup[i] : -0.0f;  // -0.0: no posting in the tile (a posting score may be +0.0)
-    if (!(B <= kTileShift && sh.c_toff[i] != kInvalid)) sh.r_sub[p] = ~0ull;
+    if (!(B <= kTileShift && toff != kInvalid)) sh.r_sub[p] = ~0ull;
   }
   {
     // the query's running threshold (every work item's counted hits so far)
@@ -1244,8 +1278,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       ess |= 1u << ord[j];
       any |= n ? 1u : 0u;
     }
-    sh.t_ess[t] = ess;
-    sh.t_post[t] = (P < m && any) ? 1u : 0u;
+    sh.t_ess[t] = (uint16_t)ess;
+    if (P < m && any) atomicOr(&sh.t_post, 1u << t);
   }
   __syncthreads();
   static_assert(kMaxTiles * 8 <= kThreads, "one thread per (tile, block)");
@@ -1285,9 +1319,9 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
 #ifdef FG_DIAG
   if (tid == 0)
     for (uint32_t t = 0; t < ntile; ++t) {
-      dg_mode[sh.t_post[t] ? 2 : 0]++;
+      dg_mode[((sh.t_post >> t) & 1u) ? 2 : 0]++;
       for (uint32_t i = 0; i < m; ++i)
-        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) dg_post += sh.r_n[t * m + i];
+        if (((sh.t_post >> t) & 1u) && ((sh.t_ess[t] >> i) & 1u)) dg_post += sh.r_n[t * m + i];
     }
 #endif
 
@@ -1303,7 +1337,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       len[r] = 0;
       if (p < npair) {
         const uint32_t t = p / m, i = p - t * m;
-        if (sh.t_post[t] && ((sh.t_ess[t] >> i) & 1u)) {
+        if (((sh.t_post >> t) & 1u) && ((sh.t_ess[t] >> i) & 1u)) {
           // the segment trimmed to the blocks where the clause is essential
           // (first to last; the bucket directory's entries at those block
           // boundaries, or the enclosing buckets' when a bucket spans blocks)
@@ -1395,7 +1429,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         uint32_t t;
         const uint64_t at = locate(e, t, npcl[j]);
         npd[j] = ix.doc[at];
-        npv[j] = tfn_load<kF>(ix, at);
+        if constexpr (kF & kFQt) npv[j] = tfn_load<kF>(ix, at);
+        else npv[j] = __float_as_uint(ix.psc[at]);
       }
     }
   };
@@ -1411,11 +1446,12 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
       pk[j] = e < n_post;
       pd[j] = npd[j];
       pcl[j] = npcl[j];
-      // the posting's query-time score
-      ps[j] = pk[j] ? tfn_score_fast<kF>(npv[j], sh.c_wt[pcl[j]], sh.c_wn[pcl[j]], sh.cache, cn) : 0.0f;
+      // the posting's score: the build's, or formed at query time
+      if constexpr (kF & kFQt) ps[j] = pk[j] ? tfn_score_fast<kF>(npv[j], sh.c_wt[pcl[j]], sh.c_wn[pcl[j]], sh.cache, cn) : 0.0f;
+      else ps[j] = pk[j] ? __uint_as_float(npv[j]) : 0.0f;
       esc |= (pk[j] && tfn_escaped<kF>(npv[j]) ? 1u : 0u) << j;
     }
-    if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {  // an escaped tf: its position from the segment list again
+    if constexpr ((kF & kFEsc) != 0) if (__builtin_expect(esc != 0, 0)) {  // an escaped tf: its position from the segment list again
 #pragma unroll
       for (uint32_t j = 0; j < J; ++j)
         if ((esc >> j) & 1u) {
@@ -1559,8 +1595,13 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
         for (uint32_t g = 0; g < G; ++g) {
           const uint32_t meta = i0 + g < m ? sh.c_meta[i0 + g] : 0u;
           if (!(meta_slot(meta) && meta_rank(meta))) continue;
-          // the rank hits' payloads (all in flight), then their query-time scores
           const uint64_t cb = sh.c_base[i0 + g];
+          if constexpr (!(kF & kFQt)) {  // the build-time scores
+#pragma unroll
+            for (uint32_t j = 0; j < J; ++j)
+              if (((need >> (g * J + j)) & 1u) && y[g][j] < 0x80000000u) y[g][j] = __float_as_uint(ix.psc[cb + y[g][j]]);
+          } else {
+          // the rank hits' payloads (all in flight), then their query-time scores
           const float wt = sh.c_wt[i0 + g], wn = sh.c_wn[i0 + g];
           uint32_t v[J];
 #pragma unroll
@@ -1572,13 +1613,14 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
             if (v[j]) y[g][j] = __float_as_uint(tfn_score_fast<kF>(v[j], wt, wn, sh.cache, cn));  // a hit (payloads != 0)
             esc |= (tfn_escaped<kF>(v[j]) ? 1u : 0u) << j;
           }
-          if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {  // an escaped tf finds its position again
+          if constexpr ((kF & kFEsc) != 0) if (__builtin_expect(esc != 0, 0)) {  // an escaped tf finds its position again
             const uint32_t ti = terms[i0 + g];
 #pragma unroll
             for (uint32_t j = 0; j < J; ++j)
               if ((esc >> j) & 1u) y[g][j] = __float_as_uint(tfn_score(ix, cb + posting_pos(ix, ti, pd[j]), v[j], wt, wn,
                                                                        sh.cache, cn));
           }
+          }  // query-time scores
         }
         // the clause-order sum (the own clause: the streamed posting's score)
 #pragma unroll
@@ -1672,7 +1714,8 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
             if (idx < hi[j] && ix.doc[sh.c_base[pc[j]] + idx] < rd[j]) pos[j] += half;
           }
         }
-        // the found postings' payloads (all in flight), then their query-time scores
+        // the found postings' scores: the build's, or their payloads (all in flight)
+        // and then their query-time scores
         uint32_t pvv[R];
 #pragma unroll
         for (uint32_t j = 0; j < R; ++j) {
@@ -1681,16 +1724,19 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
           bool hit = false;
           if (!(pc[j] & 0x80000000u))
             hit = (pc[j] & 0x40000000u) ? pos[j] != kInvalid : pos[j] < hi[j] && ix.doc[base + pos[j]] == rd[j];
-          pvv[j] = hit ? tfn_load<kF>(ix, base + pos[j]) : 0u;
+          if constexpr (kF & kFQt) pvv[j] = hit ? tfn_load<kF>(ix, base + pos[j]) : 0u;
+          else if (hit) pv[j] = ix.psc[base + pos[j]];
         }
         uint32_t esc = 0;
+        if constexpr ((kF & kFQt) != 0) {
 #pragma unroll
-        for (uint32_t j = 0; j < R; ++j) {
-          const uint32_t ci = pc[j] & 15u;
-          if (pvv[j]) pv[j] = tfn_score_fast<kF>(pvv[j], sh.c_wt[ci], sh.c_wn[ci], sh.cache, cn);  // a hit
-          esc |= (tfn_escaped<kF>(pvv[j]) ? 1u : 0u) << j;
+          for (uint32_t j = 0; j < R; ++j) {
+            const uint32_t ci = pc[j] & 15u;
+            if (pvv[j]) pv[j] = tfn_score_fast<kF>(pvv[j], sh.c_wt[ci], sh.c_wn[ci], sh.cache, cn);  // a hit
+            esc |= (tfn_escaped<kF>(pvv[j]) ? 1u : 0u) << j;
+          }
         }
-        if ((kF & kFEsc) && __builtin_expect(esc != 0, 0)) {  // an escaped tf finds its position again
+        if constexpr ((kF & kFEsc) != 0) if (__builtin_expect(esc != 0, 0)) {  // an escaped tf finds its position again
 #pragma unroll
           for (uint32_t j = 0; j < R; ++j)
             if ((esc >> j) & 1u) {
@@ -2146,13 +2192,16 @@ static void conj_launch(const DevIndex& ix, const DevPlan& pl, uint32_t grid, hi
   if (pl.segs) k_conj<kSingle, true, kF><<<grid, kThreads, 0, s>>>(ix, pl);
   else k_conj<kSingle, false, kF><<<grid, kThreads, 0, s>>>(ix, pl);
 }
+// the instantiation of a plan's features: 0 (build-time scores), kFQt, or kFQt with names / escapes
+static inline uint32_t feat_of(const DevPlan& pl) {
+  return !(pl.feat & kFQt) ? 0u : (pl.feat & (kFName | kFEsc)) ? (kFQt | kFName | kFEsc) : kFQt;
+}
 template <bool kSingle>
 static void conj_launch_f(const DevIndex& ix, const DevPlan& pl, uint32_t grid, hipStream_t s) {
-  switch (pl.feat & 3u) {
+  switch (feat_of(pl)) {
     case 0: conj_launch<kSingle, 0>(ix, pl, grid, s); break;
-    case 1: conj_launch<kSingle, 1>(ix, pl, grid, s); break;
-    case 2: conj_launch<kSingle, 2>(ix, pl, grid, s); break;
-    default: conj_launch<kSingle, 3>(ix, pl, grid, s); break;
+    case kFQt: conj_launch<kSingle, kFQt>(ix, pl, grid, s); break;
+    default: conj_launch<kSingle, kFQt | kFName | kFEsc>(ix, pl, grid, s); break;
   }
 }
 
@@ -2180,11 +2229,10 @@ hipError_t launch_disj(const DevIndex& ix, const DevPlan& pl, hipStream_t s, uin
   // a part of the sweep: the kernel's items start at pl.n_conj
   DevPlan part = pl;
   part.n_conj = pl.n_conj + first;
-  switch (pl.feat & 3u) {
+  switch (feat_of(pl)) {
     case 0: disj_launch<0>(ix, part, count, s); break;
-    case 1: disj_launch<1>(ix, part, count, s); break;
-    case 2: disj_launch<2>(ix, part, count, s); break;
-    default: disj_launch<3>(ix, part, count, s); break;
+    case kFQt: disj_launch<kFQt>(ix, part, count, s); break;
+    default: disj_launch<kFQt | kFName | kFEsc>(ix, part, count, s); break;
   }
   return hipGetLastError();
 }

@@ -68,7 +68,9 @@ struct Snap {
       HIPCHK(rd(tn.data(), x->d.tfn_name, 2 * tn.size()));
       HIPCHK(rd(ep.data(), x->d.esc_pos, 8 * ep.size()));
       HIPCHK(rd(et.data(), x->d.esc_tf, 4 * et.size()));
-      pw = x->d.tfn_name ? 4 : 2;
+      // the kernels read the build-time scores (4 B) while the statistics are the
+      // build's, else the payloads (2 B; 4 B with names)
+      pw = x->same_stats || x->d.tfn_name ? 4 : 2;
       parallel_dynamic(x->n_terms, hw_threads(0), 256, [&](int, uint32_t b, uint32_t e) {
         for (uint32_t t = b; t < e; ++t)
           for (uint64_t p = x->off[t]; p < x->off[t + 1]; ++p) {
@@ -555,7 +557,7 @@ int fg_model_batch(const fg_index* ix, const fg_query_batch* q, uint32_t k, cons
       uint32_t tm[fg::kMaxTerms], ts[fg::kMaxTerms], nm = 0, ns = 0;
       bool must_missing = false, other = false;
       for (uint32_t j = b; j < e; ++j) {
-        const uint32_t t = q->terms[j];
+        const uint32_t t = fgh::local_term(ix, q->terms[j]);
         const uint8_t oc = q->occur ? q->occur[j] : (q->mode == FG_MODE_OR ? FG_OCCUR_SHOULD : FG_OCCUR_MUST);
         const bool present = t < ix->n_terms && ix->off[t + 1] > ix->off[t];
         if (oc == FG_OCCUR_MUST) { tm[nm++] = t; must_missing |= !present; }
@@ -626,7 +628,7 @@ int fg_bytes_model(const fg_index* ix, const fg_query_batch* q, uint32_t k, doub
     std::vector<L> ls;
     bool missing = false;
     for (uint32_t j = 0; j < m; ++j) {
-      uint32_t t = q->terms[b + j];
+      uint32_t t = fgh::local_term(ix, q->terms[b + j]);
       if (t >= ix->n_terms || ix->off[t + 1] == ix->off[t]) { missing = true; break; }
       ls.push_back(L{ix->off[t + 1] - ix->off[t], ix->off[t], j});
     }
