@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -16,6 +18,7 @@
 
 #include "../../include/fugu.h"
 #include "fg_internal.h"
+#include "fg_pool.h"
 #include "fg_trace.h"
 
 namespace fgh {
@@ -25,37 +28,7 @@ int fail(int code, const char* fmt, ...);
 // host threads for builds, planning and models (FUGU_THREADS, the CPU share)
 int hw_threads(int req);
 
-template <class F>
-void parallel_ranges(uint32_t n, int threads, F&& f) {
-  if (threads <= 1 || n < 1024) { f(0, 0u, n); return; }
-  std::vector<std::thread> ts;
-  uint32_t step = (n + threads - 1) / threads;
-  for (int t = 0; t < threads; ++t) {
-    uint32_t b = std::min<uint64_t>((uint64_t)t * step, n), e = std::min<uint64_t>((uint64_t)(t + 1) * step, n);
-    ts.emplace_back([&f, t, b, e] { f(t, b, e); });
-  }
-  for (auto& t : ts) t.join();
-}
-
-// Dynamic schedule over [0, n) in chunks of `grain` (per-term loops: Zipf term
-// ids put most postings in the first terms, so a static split leaves one
-// thread with nearly all the work).  f(thread, begin, end).
-template <class F>
-void parallel_dynamic(uint32_t n, int threads, uint32_t grain, F&& f) {
-  if (threads <= 1 || n <= grain) { f(0, 0u, n); return; }
-  std::atomic<uint64_t> next{0};
-  std::vector<std::thread> ts;
-  for (int t = 0; t < threads; ++t)
-    ts.emplace_back([&, t] {
-      for (;;) {
-        const uint64_t b = next.fetch_add(grain);
-        if (b >= n) break;
-        f(t, (uint32_t)b, (uint32_t)std::min<uint64_t>(n, b + grain));
-      }
-    });
-  for (auto& t : ts) t.join();
-}
-
+// parallel_ranges / parallel_dynamic / run_helped: fg_pool.h
 
 // Device memory some structure keeps cached for reuse (released scoring
 // blocks, plan workspaces).  Every cache registers itself; an allocation that
@@ -251,6 +224,16 @@ struct fg_ctx {
 // device).  Buffers are reused when they fit a request within 2x; at most
 // kPoolKeep bytes stay cached.
 namespace fgh {
+// the size a pooled buffer of `bytes` is allocated at: the next power of two
+// (>= 4 KiB; past 256 MiB the next 1/16 of one), so a cached buffer serves the
+// requests a little smaller than it
+inline size_t size_class(size_t bytes) {
+  size_t n = 4096;
+  while (n < bytes) n <<= 1;
+  if (n <= (256ull << 20)) return n;
+  const size_t step = n / 16;
+  return (bytes + step - 1) / step * step;
+}
 struct WsPool : DevCache {
   static constexpr size_t kPoolKeep = 1ull << 30;
   std::mutex mu;
@@ -270,10 +253,13 @@ struct WsPool : DevCache {
       }
     }
     void* p = nullptr;
-    // the cached workspaces and scoring blocks (of every index) may be what the
-    // device lacks: dev_malloc frees them and retries once
-    if (dev_malloc(&p, bytes) != hipSuccess) return nullptr;
-    *got = bytes;
+    // sized up to a power of two: a plan a little larger than the last (one
+    // more segment after a commit) reuses its buffer instead of a hipMalloc in
+    // the search's path.  The cached workspaces and scoring blocks (of every
+    // index) may be what the device lacks: dev_malloc frees them and retries once
+    const size_t n = size_class(bytes);
+    if (dev_malloc(&p, n) != hipSuccess) return nullptr;
+    *got = n;
     return p;
   }
   void drop_cached() override {
@@ -325,7 +311,7 @@ struct PinnedPool {
       }
     }
     void* p = nullptr;
-    const size_t n = std::max<size_t>(bytes, 4096);
+    const size_t n = size_class(bytes);  // (as WsPool::get)
     if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
     *got = n;
     return p;

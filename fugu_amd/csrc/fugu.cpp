@@ -167,6 +167,38 @@ int fgh::hw_threads(int req) {
 }
 int fg_host_threads() { return hw_threads(0); }
 
+// fgh::pool_post's threads: as many as the host threads builds use, started on
+// first use, never destroyed (idle ones end with the process)
+void fgh::pool_post(std::function<void()> job) {
+  struct Pool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+  };
+  static Pool* pool = [] {
+    auto* p = new Pool;
+    for (int i = 0, n = std::max(1, hw_threads(0) - 1); i < n; ++i)
+      std::thread([p] {
+        for (;;) {
+          std::function<void()> j;
+          {
+            std::unique_lock<std::mutex> l(p->mu);
+            p->cv.wait(l, [&] { return !p->q.empty(); });
+            j = std::move(p->q.front());
+            p->q.pop_front();
+          }
+          j();
+        }
+      }).detach();
+    return p;
+  }();
+  {
+    std::lock_guard<std::mutex> l(pool->mu);
+    pool->q.push_back(std::move(job));
+  }
+  pool->cv.notify_one();
+}
+
 namespace fgh {
 namespace {
 std::mutex& cache_mu() {
@@ -1191,8 +1223,8 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     const char* f = getenv("FUGU_RANK_FACTOR");
     const double factor = f && *f ? atof(f) : fg::kRankFactor;
     const uint64_t want = std::min<uint64_t>(cap, (uint64_t)(factor * 12.0 * (double)hp.off[V]));
-    size_t free_b = 0, total_b = 0;
-    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    size_t free_b = ~size_t(0), total_b = 0;
+    if (want > (256ull << 20)) HIPCHK(hipMemGetInfo(&free_b, &total_b));  // (~1 ms: not for a small segment's)
     const uint64_t brk = std::min<uint64_t>(want, free_b / 4);
     uint64_t used = 0;
     for (size_t i = 0; i < by_df.size(); ++i) {
@@ -1237,6 +1269,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
       for (uint32_t n : sparse_nw) n_swords += n;
     }
   }
+  g_bt.mark("rank words: budget");
   if (!sparse_terms.empty()) {
     // built on the host from the postings: per term its block entries, then
     // the zero word and all terms' words (term by term), one upload
@@ -1272,6 +1305,7 @@ int finish_index(int dev, HostPostings& hp, bool keep_host, fg_index** out, cons
     HIPCHK(hipStreamSynchronize(kBuildStream));
     for (uint32_t s2 = 0; s2 < ns; ++s2) tmeta[sparse_terms[s2]] |= ((first_slot + s2) << 16) | 0x80000000u;
   }
+  g_bt.mark("rank words: sparse");
   if (!rank_terms.empty()) {
     // one k_rank launch for every rank term: per slot the term's posting range
     std::vector<uint64_t> sb(rank_terms.size());
@@ -1940,7 +1974,6 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
     for (uint32_t t = 0; t < VF; ++t) bad |= g->df_facet[t] < base->df_facet_local[t];
     if (bad) return fail(FG_EINVAL, "global doc frequencies below this snapshot's own");
   }
-  g_bt.start();
   auto ix = std::make_unique<fg_index>();
   ix->dev = base->dev;
   ix->mem.dev = base->dev;
@@ -2052,6 +2085,7 @@ static int rescore_one(const fg_index* base, const fg_global_stats* g, const uin
 extern "C" {
 
 int fg_index_rescore(const fg_index* base, const fg_global_stats* g, const uint8_t* deleted, fg_index** out) {
+  g_bt.start();
   return rescore_one(base, g, deleted, out, nullptr);
 }
 
@@ -2068,14 +2102,18 @@ int fg_index_rescore_many(const fg_index* const* bases, uint32_t n, const fg_glo
   // the weights once for every snapshot on vocabulary ids (they depend on the
   // statistics only; a snapshot with its own dictionary gathers its own)
   fgh::Weights wts;
+  g_bt.start();
   if (V) {
     std::vector<float> wt, wn;
     bm25_weights(g->n_docs, g->df_text, g->df_name, V, wt, wn);
     wts.wt = std::move(wt);
     wts.wn = std::move(wn);
   }
+  g_bt.mark("rescore: shared weights");
   for (uint32_t i = 0; i < n; ++i) {
-    if (int rc = rescore_one(bases[i], g, deleted ? deleted[i] : nullptr, &outs[i], &wts)) {
+    const int rc = rescore_one(bases[i], g, deleted ? deleted[i] : nullptr, &outs[i], &wts);
+    g_bt.mark(bases[i]->tmap.empty() ? "rescore: a snapshot" : "rescore: a snapshot (own dictionary)");
+    if (rc) {
       const std::string e = fg_last_error();
       for (uint32_t j2 = 0; j2 < n; ++j2)
         if (outs[j2]) {
@@ -2311,6 +2349,12 @@ struct HostPlan {
   std::vector<uint32_t> ch_f, ch_c, ch_t, ch_s;
   std::vector<WItem> citems, ditems, scan;
   std::vector<uint32_t> ngroup, q_hlo, q_hhi, q_hsh;
+  // (a thread's plans reuse one set: assign / push_back into kept capacity, no
+  // page faults on fresh arrays -- ~0.2 ms of an 8-snapshot batch's planning)
+  void clear_lists() {
+    ch_f.clear(); ch_c.clear(); ch_t.clear(); ch_s.clear();
+    citems.clear(); ditems.clear(); scan.clear();
+  }
 };
 
 // n_segs: the snapshots the plan spans; a query's work items are spread over
@@ -2326,6 +2370,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   const uint32_t nq = q->n_queries;
   const uint64_t N = ix->n_docs;
   const bool disj = q->mode == FG_MODE_OR;
+  h.clear_lists();
   auto &q_m = h.q_m, &q_terms = h.q_terms, &lead = h.lead, &nchunk = h.nchunk;
   auto& thr0 = h.thr0;
   auto& q_ub = h.q_ub;
@@ -2631,7 +2676,15 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     if (ixs[s]->dev != ixs[0]->dev) return fail(FG_EINVAL, "the snapshots of one plan live on different devices");
   }
   fg_index* ix = ixs[0];
-  std::vector<HostPlan> hs(S);
+  // FUGU_SHARD_TRACE: the planning phases of a multi-snapshot batch on stderr
+  static const bool ptrace = getenv("FUGU_SHARD_TRACE") != nullptr;
+  auto pnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double pt[5] = {ptrace ? pnow() : 0.0, 0, 0, 0, 0};
+  // (reused: HostPlan::clear_lists; a plain reference, so the planning workers'
+  // lambdas see THIS thread's copy, not their own thread_local one)
+  static thread_local std::vector<HostPlan> hs_tl;
+  std::vector<HostPlan>& hs = hs_tl;
+  if (hs.size() < S) hs.resize(S);
   if (S > 1 && q->n_queries >= 64) {
     std::vector<int> rcs(S, FG_OK);
     std::vector<std::string> errs(S);
@@ -2648,14 +2701,32 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
         return fail(rc, "snapshot %u: %s", s, e.c_str());
       }
   }
+  if (ptrace) pt[1] = pnow();
   const uint32_t nq1 = q->n_queries;  // batch queries
   if ((uint64_t)S * nq1 > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%u x %u query slots)", S, nq1);
   const uint32_t nq = S * nq1;  // query slots
   // ---- join the snapshots' tables (one snapshot: its own, moved)
-  std::vector<uint32_t> q_m, q_terms, lead, q_filter, ngroup, q_hlo, q_hhi, q_hsh, f_shift, f_seg, ch_f, ch_c, ch_t, ch_s;
-  std::vector<uint64_t> thr0, f_woff;
-  std::vector<float> q_ub, q_wt, q_wn, q_rup, f_tab, f_max;
-  std::vector<WItem> citems, ditems, scan;
+  // (this thread's join buffers, reused like hs)
+  struct Join {
+    std::vector<uint32_t> q_m, q_terms, lead, q_filter, ngroup, q_hlo, q_hhi, q_hsh, f_shift, f_seg, ch_f, ch_c, ch_t, ch_s;
+    std::vector<uint64_t> thr0, f_woff;
+    std::vector<float> q_ub, q_wt, q_wn, q_rup, f_tab, f_max;
+    std::vector<WItem> citems, ditems, scan, items;
+  };
+  static thread_local Join J_tl;
+  Join& J = J_tl;
+  for (auto* v : {&J.q_m, &J.q_terms, &J.lead, &J.q_filter, &J.ngroup, &J.q_hlo, &J.q_hhi, &J.q_hsh, &J.f_shift, &J.f_seg,
+                  &J.ch_f, &J.ch_c, &J.ch_t, &J.ch_s})
+    v->clear();
+  for (auto* v : {&J.thr0, &J.f_woff}) v->clear();
+  for (auto* v : {&J.q_ub, &J.q_wt, &J.q_wn, &J.q_rup, &J.f_tab, &J.f_max}) v->clear();
+  for (auto* v : {&J.citems, &J.ditems, &J.scan, &J.items}) v->clear();
+  auto &q_m = J.q_m, &q_terms = J.q_terms, &lead = J.lead, &q_filter = J.q_filter, &ngroup = J.ngroup, &q_hlo = J.q_hlo,
+       &q_hhi = J.q_hhi, &q_hsh = J.q_hsh, &f_shift = J.f_shift, &f_seg = J.f_seg, &ch_f = J.ch_f, &ch_c = J.ch_c,
+       &ch_t = J.ch_t, &ch_s = J.ch_s;
+  auto &thr0 = J.thr0, &f_woff = J.f_woff;
+  auto &q_ub = J.q_ub, &q_wt = J.q_wt, &q_wn = J.q_wn, &q_rup = J.q_rup, &f_tab = J.f_tab, &f_max = J.f_max;
+  auto &citems = J.citems, &ditems = J.ditems, &scan = J.scan;
   uint32_t nf = 0;
   if (S == 1) {
     HostPlan& h = hs[0];
@@ -2711,6 +2782,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
       }
     }
   }
+  if (ptrace) pt[2] = pnow();
   if (f_woff[nf] * 4 > (8ull << 30)) return fail(FG_EUNSUPPORTED, "facet masks of this batch exceed 8 GiB");
   if (ch_f.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "facet postings of this batch too large");
   if (citems.size() + ditems.size() + scan.size() > 0x7FFFFFFFull)
@@ -2739,40 +2811,47 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     // measured no better)
     auto probe_term = [&](uint32_t qv) { return q_terms[(size_t)qv * fg::kMaxTerms]; };
     // the multi-list items only (single-list ones keep the sweep and run as a
-    // launch of their own, k_conj<true> over the first n_single items); the
-    // (term, items) counts by sorting the items' terms (a map per item cost
-    // ~1 ms of an 8-snapshot batch's planning)
-    std::vector<uint32_t> ts;
-    ts.reserve(items.size());
-    for (const W& x : items)
-      if (!single(x)) ts.push_back(probe_term(x.q));
-    std::sort(ts.begin(), ts.end());
-    std::vector<std::pair<uint64_t, uint32_t>> by;  // (items, term)
-    for (size_t i = 0; i < ts.size();) {
+    // launch of their own, k_conj<true> over the first n_single items), counted
+    // per query slot (all of a slot's items share its lead term): the slots
+    // radix-sorted by term, the (term, items) counts, the terms by items
+    // (a comparison sort over every item's term cost ~0.4 ms of an 8-snapshot batch)
+    static thread_local std::vector<uint64_t> ka, kb;
+    ka.clear();
+    for (uint32_t v = 0; v < nq; ++v)
+      if (ngroup[v] && fg::qm_must(q_m[v]) && q_m[v] != fg::qm_pack(1, 1, 0))  // (k_conj slots only)
+        ka.push_back(((uint64_t)probe_term(v) << 32) | v);
+    kb.resize(ka.size());
+    for (int sh = 32; sh < 64; sh += 11) {
+      uint32_t cnt[2049] = {0};
+      for (uint64_t x : ka) cnt[((x >> sh) & 2047u) + 1]++;
+      for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
+      for (uint64_t x : ka) kb[cnt[(x >> sh) & 2047u]++] = x;
+      ka.swap(kb);
+    }
+    std::vector<std::pair<uint64_t, uint32_t>> by;  // (items, first index in ka)
+    for (size_t i = 0; i < ka.size();) {
       size_t j = i;
-      while (j < ts.size() && ts[j] == ts[i]) ++j;
-      by.emplace_back(j - i, ts[i]);
+      uint64_t c = 0;
+      for (; j < ka.size() && (ka[j] >> 32) == (ka[i] >> 32); ++j) c += ngroup[(uint32_t)ka[j]];
+      by.emplace_back(c, (uint32_t)i);
       i = j;
     }
-    std::sort(by.begin(), by.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
+    std::sort(by.begin(), by.end(), [&](auto& a, auto& b) {
+      return a.first > b.first || (a.first == b.first && (ka[a.second] >> 32) < (ka[b.second] >> 32));
+    });
     uint64_t gl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    std::vector<std::pair<uint32_t, uint8_t>> tg;  // (term, group), by term
-    tg.reserve(by.size());
-    for (auto& [cnt, t] : by) {
+    for (auto& [c, i0] : by) {
       const uint32_t g = (uint32_t)(std::min_element(gl, gl + 8) - gl);
-      gl[g] += cnt;
-      tg.emplace_back(t, (uint8_t)g);
+      gl[g] += c;
+      for (size_t j = i0; j < ka.size() && (ka[j] >> 32) == (ka[i0] >> 32); ++j) q_grp[(uint32_t)ka[j]] = (uint8_t)g;
     }
-    std::sort(tg.begin(), tg.end());
-    for (const W& x : items)
-      if (!single(x)) {
-        const uint32_t t = probe_term(x.q);
-        q_grp[x.q] = std::lower_bound(tg.begin(), tg.end(), std::make_pair(t, (uint8_t)0))->second;
-      }
+    (void)items;
   };
   auto radix = [&](std::vector<W>& items, bool conj) {
     const size_t n = items.size();
-    std::vector<uint64_t> a(n), bb(n);  // (sort key << 32) | item index
+    static thread_local std::vector<uint64_t> a, bb;  // (sort key << 32) | item index
+    a.resize(n);
+    bb.resize(n);
     // (items of queries probing the same list next to each other within each
     // 1/2048 of the sweep, so one XCD's L2 serves that list to all of them:
     // measured slower, profiles/r04/ab/ab_sweep_*.log)
@@ -2793,13 +2872,14 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
       for (size_t x = 0; x < n; ++x) bb[cnt[(a[x] >> sh) & 2047u]++] = a[x];
       a.swap(bb);
     }
-    std::vector<W> sorted(n);
+    static thread_local std::vector<W> sorted;
+    sorted.resize(n);
     for (size_t x = 0; x < n; ++x) sorted[x] = items[(uint32_t)a[x]];
     items.swap(sorted);
   };
   radix(citems, true);
   radix(ditems, false);
-  std::vector<W> items;
+  auto& items = J.items;
   items.reserve(citems.size() + ditems.size() + scan.size());
   items.insert(items.end(), citems.begin(), citems.end());
   const uint64_t n_conj = citems.size();
@@ -2811,8 +2891,12 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   const uint64_t chunks = n_main + n_scan;  // from here on: work items (k_conj / k_disj, then k_scan)
   if (chunks > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%llu work items)", (unsigned long long)chunks);
   items.insert(items.end(), scan.begin(), scan.end());
-  std::vector<uint32_t> work_q(chunks), work_c(chunks), work_n(chunks);
-  std::vector<uint64_t> cand_off(nq + 1, 0);
+  static thread_local std::vector<uint32_t> work_q, work_c, work_n;
+  static thread_local std::vector<uint64_t> cand_off;
+  work_q.resize(chunks);
+  work_c.resize(chunks);
+  work_n.resize(chunks);
+  cand_off.assign(nq + 1, 0);
   for (uint64_t w = 0; w < chunks; ++w) {
     work_q[w] = items[w].q;
     work_c[w] = items[w].c;
@@ -2821,6 +2905,7 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // each work item appends at most k keys to its query's candidate list
   for (uint32_t i = 0; i < nq; ++i) cand_off[i + 1] = cand_off[i] + (uint64_t)ngroup[i] * k;
 
+  if (ptrace) pt[3] = pnow();
   auto p = std::make_unique<fg_plan>();
   p->nq = nq;
   p->nq_batch = nq1;
@@ -3012,6 +3097,11 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   p->h_hi.swap(q_hhi);
   p->d.f.n_filters = nf;
   p->d.f.n_chunks = (uint32_t)nch;
+  if (ptrace && S > 1) {
+    pt[4] = pnow();
+    fprintf(stderr, "[fg plan] %u snapshots x %u queries: plan_host %.3f join %.3f items %.3f stage+upload %.3f ms\n", S,
+            nq1, pt[1] - pt[0], pt[2] - pt[1], pt[3] - pt[2], pt[4] - pt[3]);
+  }
   *out = p.release();
   return FG_OK;
 }

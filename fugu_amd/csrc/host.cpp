@@ -30,6 +30,7 @@
 
 #include "../../include/fugu.h"
 #include "../../include/fugu_host.h"
+#include "fg_pool.h"
 #include "fg_trace.h"
 
 void fg_set_last_error(const std::string& msg);  // fugu.cpp
@@ -867,7 +868,8 @@ struct Namespace {
   uint64_t next_seg = 1;
   // BM25 statistics of the committed segments (the sum of their SegStats),
   // deleted docs included: N, token totals, doc frequencies.  Written under the
-  // writer lock together with the snapshot; st_ver counts the changes.
+  // writer AND committer locks together with the snapshot (so a committer reads
+  // them without the writer lock); st_ver counts the changes.
   uint64_t st_n = 0, st_tot[2] = {0, 0}, st_tot_f = 0, st_ver = 0;
   std::vector<uint32_t> st_df_text, st_df_name, st_df_facet;
   // merger bookkeeping
@@ -1457,6 +1459,30 @@ uint64_t quantized_len(uint64_t n) {
   return *(std::upper_bound(t.begin(), t.end(), n) - 1);
 }
 
+// (term, docs holding it) of a few docs' field, sparse: each doc's distinct
+// terms gathered, then sorted and counted (a commit's 1000 docs: no
+// vocabulary-sized arrays)
+struct SparseDf {
+  std::vector<uint32_t> all, scratch;
+  void add(const std::vector<uint32_t>& toks) {
+    scratch = toks;
+    std::sort(scratch.begin(), scratch.end());
+    scratch.erase(std::unique(scratch.begin(), scratch.end()), scratch.end());
+    all.insert(all.end(), scratch.begin(), scratch.end());
+  }
+  std::vector<std::pair<uint32_t, uint32_t>> take() {
+    std::sort(all.begin(), all.end());
+    std::vector<std::pair<uint32_t, uint32_t>> v;
+    for (size_t i = 0; i < all.size();) {
+      size_t j = i;
+      while (j < all.size() && all[j] == all[i]) ++j;
+      v.emplace_back(all[i], (uint32_t)(j - i));
+      i = j;
+    }
+    return v;
+  }
+};
+
 // the distinct terms of a doc counted once into df
 void count_distinct(const std::vector<uint32_t>& toks, std::vector<uint32_t>& scratch, std::vector<uint32_t>& df) {
   scratch = toks;
@@ -1479,6 +1505,14 @@ void df_add(std::vector<uint32_t>& df, const std::vector<std::pair<uint32_t, uin
   }
 }
 
+// Runs f(0..n-1) on up to `width` threads (this one and the helper pool's).
+template <class F>
+void run_threads(size_t n, size_t width, F&& f) {
+  fgh::parallel_dynamic((uint32_t)n, (int)width, 1, [&](int, uint32_t b, uint32_t e) {
+    for (uint32_t i = b; i < e; ++i) f(i);
+  });
+}
+
 // Dense namespace statistics in local copies (fg_global_stats points into them).
 struct Stats {
   uint64_t n = 0, tot[2] = {0, 0}, tot_f = 0;
@@ -1488,12 +1522,18 @@ struct Stats {
     tot[0] = ns.st_tot[0];
     tot[1] = ns.st_tot[1];
     tot_f = ns.st_tot_f;
-    df_t = ns.st_df_text;
-    df_n = ns.st_df_name;
-    df_f = ns.st_df_facet;
-    df_t.resize(n_terms, 0);
-    df_n.resize(n_terms, 0);
-    df_f.resize(n_fterms, 0);
+    // the vocabulary-sized arrays copied in 1 MiB pieces on the pool (~12 MB per commit)
+    auto copy = [](std::vector<uint32_t>& dst, const std::vector<uint32_t>& src, uint32_t size) {
+      dst.assign(size, 0);
+      const size_t m = std::min<size_t>(size, src.size()), piece = 1u << 18;
+      run_threads((m + piece - 1) / piece, 8, [&](size_t i) {
+        const size_t b = i * piece, e = std::min(m, b + piece);
+        std::memcpy(dst.data() + b, src.data() + b, 4 * (e - b));
+      });
+    };
+    copy(df_t, ns.st_df_text, std::max<uint32_t>(n_terms, (uint32_t)ns.st_df_text.size()));
+    copy(df_n, ns.st_df_name, std::max<uint32_t>(n_terms, (uint32_t)ns.st_df_name.size()));
+    copy(df_f, ns.st_df_facet, std::max<uint32_t>(n_fterms, (uint32_t)ns.st_df_facet.size()));
   }
   void add(const SegStats& s, bool sub) {
     n = sub ? n - s.n : n + s.n;
@@ -1515,14 +1555,14 @@ struct Stats {
     g.tot_facet_tokens = tot_f;
     return g;
   }
-  void store(Namespace& ns) {  // under the writer lock
+  void store(Namespace& ns) {  // under the writer and committer locks; the arrays move (S is spent)
     ns.st_n = n;
     ns.st_tot[0] = tot[0];
     ns.st_tot[1] = tot[1];
     ns.st_tot_f = tot_f;
-    ns.st_df_text = df_t;
-    ns.st_df_name = df_n;
-    ns.st_df_facet = df_f;
+    ns.st_df_text = std::move(df_t);
+    ns.st_df_name = std::move(df_n);
+    ns.st_df_facet = std::move(df_f);
     ns.st_ver++;
   }
 };
@@ -1562,19 +1602,6 @@ struct DocsBuf {
   }
 };
 
-// Runs f(0..n-1) on up to `width` threads (this one included).
-template <class F>
-void run_threads(size_t n, size_t width, F&& f) {
-  std::atomic<size_t> next{0};
-  auto worker = [&] {
-    for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
-  };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < std::min(n, width); ++t) th.emplace_back(worker);
-  worker();
-  for (auto& x : th) x.join();
-}
-
 // every segment of `segs` rescored with g and the current deleted flags
 // (`del`, global); appended to out in order.  One fg_index_rescore_many: the
 // weights once, the segments side by side on their own threads and streams.
@@ -1588,6 +1615,8 @@ int rescore_into(const std::vector<Segment>& segs, const fg_global_stats& g, con
   run_threads(n, 8, [&](size_t i) {
     const Segment& s0 = segs[i];
     bases[i] = s0.ix;
+    // (a contiguous segment without deleted docs: one memchr)
+    if (!s0.gid && !std::memchr(del.data() + s0.base, 1, s0.n)) return;
     sdel[i].assign(s0.n, 0);
     bool sany = false;
     for (uint32_t d = 0; d < s0.n; ++d) sany |= (sdel[i][d] = del[s0.global(d)]) != 0;
@@ -1625,7 +1654,7 @@ int commit_segment(fg_db* db, Namespace& ns) {
   const uint32_t n_fterms = (uint32_t)ns.fdict.size();
   DocsBuf buf;
   auto st = std::make_shared<SegStats>();
-  std::vector<uint32_t> dt(n_terms, 0), dn(n_terms, 0), dfc(n_fterms, 0), scratch;
+  SparseDf dt, dn, dfc;
   for (uint32_t d = old; d < N; ++d) {
     const Doc& doc = ns.docs[d];
     buf.add(doc, doc.deleted);
@@ -1633,21 +1662,23 @@ int commit_segment(fg_db* db, Namespace& ns) {
     st->tot[0] += doc.text_tok.size();
     st->tot[1] += doc.name_tok.size();
     st->tot_f += doc.facet_tok.size();
-    count_distinct(doc.text_tok, scratch, dt);
-    count_distinct(doc.name_tok, scratch, dn);
-    count_distinct(doc.facet_tok, scratch, dfc);
+    dt.add(doc.text_tok);
+    dn.add(doc.name_tok);
+    dfc.add(doc.facet_tok);
   }
-  st->df_t = sparse_of(dt);
-  st->df_n = sparse_of(dn);
-  st->df_f = sparse_of(dfc);
   const bool any_name = ns.any_name;
   const std::vector<uint8_t> del(ns.del.begin(), ns.del.begin() + N);
   const size_t n_pend = ns.pend_del.size();  // committed by this commit
+  w.unlock();
+  tr.mark("gather (writer lock)");
+  st->df_t = dt.take();
+  st->df_n = dn.take();
+  st->df_f = dfc.take();
+  // the statistics change only under the committer lock (held): read without the writer's
   Stats S;
   S.load(ns, n_terms, n_fterms);
   S.add(*st, false);
-  w.unlock();
-  tr.mark("gather (writer lock)");
+  tr.mark("statistics");
   const fg_global_stats g = S.global();
   const fg_docs_input in = buf.input(n_terms, n_fterms, any_name);
   auto snap = db->new_snapshot();
@@ -1667,8 +1698,9 @@ int commit_segment(fg_db* db, Namespace& ns) {
   });
   const int rrc = cur ? rescore_into(cur->segs, g, del, snap->segs) : FG_OK;  // snap releases the rescored ones
   const std::string rerr = rrc ? fg_last_error() : std::string();
+  tr.mark("rescore older (beside the build)");
   builder.join();
-  tr.mark("rescore older + build new");
+  tr.mark("build new (rest)");
   if (rrc || brc) {
     if (ix) fg_index_release(ix);
     return rrc ? hfail(rrc, rerr) : hfail(brc, berr);
@@ -2195,54 +2227,50 @@ int fg_db_upsert_batch(fg_db* db, const char* nsname, uint32_t n, const char* id
     if (e) return hfail(FG_EINVAL, "Validation failed for object at index " + std::to_string(i) + ": " + e);
   }
   PhaseTrace tr("upsert");
-  const int T = std::max(1, std::min<int>(fg_host_threads(), (int)(n / 4096) + 1));
+  // ~256 docs per thread: a commit's 1000 docs analyze on 4 (the pool's)
+  const int T = std::max(1, std::min<int>(fg_host_threads(), (int)(n / 256) + 1));
   std::vector<LocalDict> ldict(T);
   std::vector<Doc> docs(n);
-  {
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; ++t)
-      th.emplace_back([&, t] {
-        const uint32_t b = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T);
-        std::vector<std::string> toks;
-        std::string scratch;
-        for (uint32_t i = b; i < e; ++i) {
-          Doc& d = docs[i];
-          d.id = std::string(sv(ids, id_off, i));
-          d.text = std::string(sv(texts, text_off, i));
-          // thread-local term ids until the merge
-          analyze_each(d.text, scratch, toks, [&](std::string_view w) { d.text_tok.push_back(ldict[t].get(w)); });
-          analyze(d.id, d.id_tokens);
-        }
-      });
-    for (auto& x : th) x.join();
-  }
+  // per thread: its docs analyzed into its own dictionary, then its terms looked
+  // up in the namespace's without a lock (ids never change once interned; a
+  // term missing here is interned under the writer lock below)
+  std::vector<std::vector<uint32_t>> remap(T);
+  std::vector<std::vector<uint64_t>> hsh(T);
+  run_threads((size_t)T, (size_t)T, [&](size_t t) {
+    const uint32_t b = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T);
+    std::vector<std::string> toks;
+    std::string scratch;
+    for (uint32_t i = b; i < e; ++i) {
+      Doc& d = docs[i];
+      d.id = std::string(sv(ids, id_off, i));
+      d.text = std::string(sv(texts, text_off, i));
+      // thread-local term ids until the merge
+      analyze_each(d.text, scratch, toks, [&](std::string_view w) { d.text_tok.push_back(ldict[t].get(w)); });
+      analyze(d.id, d.id_tokens);
+    }
+    const uint32_t ne = (uint32_t)ldict[t].ent.size();
+    hsh[t].resize(ne);
+    remap[t].resize(ne);
+    for (uint32_t j = 0; j < ne; ++j) hsh[t][j] = TermDict::hash(ldict[t].key(j));
+    constexpr uint32_t kAhead = 16;  // the slot lines of later lookups in flight
+    for (uint32_t j = 0; j < std::min(ne, kAhead); ++j) ns->dict.prefetch(hsh[t][j]);
+    for (uint32_t j = 0; j < ne; ++j) {
+      if (j + kAhead < ne) ns->dict.prefetch(hsh[t][j + kAhead]);
+      remap[t][j] = ns->dict.find(ldict[t].key(j), hsh[t][j]);
+    }
+  });
   tr.mark("analyze");
-  {  // the writer lock: the dictionary merge and the ordered upserts
+  {  // the writer lock: the new terms interned, the ordered upserts
     std::lock_guard<std::mutex> w(ns->writer);
-    std::vector<std::vector<uint32_t>> remap(T);
-    for (int t = 0; t < T; ++t) {
-      const uint32_t ne = (uint32_t)ldict[t].ent.size();
-      std::vector<uint64_t> hs(ne);
-      for (uint32_t j = 0; j < ne; ++j) hs[j] = TermDict::hash(ldict[t].key(j));
-      remap[t].resize(ne);
-      constexpr uint32_t kAhead = 16;  // the slot lines of later lookups in flight
-      for (uint32_t j = 0; j < std::min(ne, kAhead); ++j) ns->dict.prefetch(hs[j]);
-      for (uint32_t j = 0; j < ne; ++j) {
-        if (j + kAhead < ne) ns->dict.prefetch(hs[j + kAhead]);
-        remap[t][j] = ns->dict.get(ldict[t].key(j), hs[j]);
-      }
-    }
+    for (int t = 0; t < T; ++t)
+      for (uint32_t j = 0; j < (uint32_t)remap[t].size(); ++j)
+        if (remap[t][j] == TermDict::kMissing) remap[t][j] = ns->dict.get(ldict[t].key(j), hsh[t][j]);
     tr.mark("dictionary merge");
-    {
-      std::vector<std::thread> th;
-      for (int t = 0; t < T; ++t)
-        th.emplace_back([&, t] {
-          const uint32_t b = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T);
-          for (uint32_t i = b; i < e; ++i)
-            for (auto& x : docs[i].text_tok) x = remap[t][x];
-        });
-      for (auto& x : th) x.join();
-    }
+    run_threads((size_t)T, (size_t)T, [&](size_t t) {
+      const uint32_t b = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T);
+      for (uint32_t i = b; i < e; ++i)
+        for (auto& x : docs[i].text_tok) x = remap[t][x];
+    });
     tr.mark("remap");
     // a bulk load sizes the id map once; a small batch lets it grow geometrically
     // (reserving size + n on every call rehashed all 10M entries per commit)
