@@ -2685,28 +2685,12 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   static thread_local std::vector<HostPlan> hs_tl;
   std::vector<HostPlan>& hs = hs_tl;
   if (hs.size() < S) hs.resize(S);
-  if (S > 1 && q->n_queries >= 64) {
-    std::vector<int> rcs(S, FG_OK);
-    std::vector<std::string> errs(S);
-    run_parallel(S, [&](uint32_t s) {
-      if ((rcs[s] = plan_host(ixs[s], q, k, S, hs[s]))) errs[s] = fg_last_error();
-    });
-    for (uint32_t s = 0; s < S; ++s)
-      if (rcs[s]) return fail(rcs[s], "snapshot %u: %s", s, errs[s].c_str());
-  } else {
-    for (uint32_t s = 0; s < S; ++s)
-      if (int rc = plan_host(ixs[s], q, k, S, hs[s])) {
-        if (S == 1) return rc;
-        const std::string e = fg_last_error();
-        return fail(rc, "snapshot %u: %s", s, e.c_str());
-      }
-  }
-  if (ptrace) pt[1] = pnow();
   const uint32_t nq1 = q->n_queries;  // batch queries
   if ((uint64_t)S * nq1 > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%u x %u query slots)", S, nq1);
   const uint32_t nq = S * nq1;  // query slots
-  // ---- join the snapshots' tables (one snapshot: its own, moved)
-  // (this thread's join buffers, reused like hs)
+  // ---- the joined tables (this thread's buffers, reused like hs): several
+  // snapshots' per-query tables are copied into their slots by the planning
+  // workers themselves, the lists joined after
   struct Join {
     std::vector<uint32_t> q_m, q_terms, lead, q_filter, ngroup, q_hlo, q_hhi, q_hsh, f_shift, f_seg, ch_f, ch_c, ch_t, ch_s;
     std::vector<uint64_t> thr0, f_woff;
@@ -2727,6 +2711,51 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   auto &thr0 = J.thr0, &f_woff = J.f_woff;
   auto &q_ub = J.q_ub, &q_wt = J.q_wt, &q_wn = J.q_wn, &q_rup = J.q_rup, &f_tab = J.f_tab, &f_max = J.f_max;
   auto &citems = J.citems, &ditems = J.ditems, &scan = J.scan;
+  const size_t nqt = (size_t)nq1 * fg::kMaxTerms;
+  if (S > 1) {
+    q_m.resize(nq);
+    lead.resize(nq);
+    ngroup.resize(nq);
+    thr0.resize(nq);
+    q_terms.resize(nqt * S);
+    q_ub.resize(nqt * S);
+    q_wt.resize(nqt * S);
+    q_wn.resize(nqt * S);
+    q_rup.resize(nqt * S);
+  }
+  auto put_slot = [&](uint32_t s) {  // snapshot s's per-query tables into its slots
+    const HostPlan& h = hs[s];
+    auto cp = [](auto& dst, const auto& src, size_t at) { std::copy(src.begin(), src.end(), dst.begin() + at); };
+    cp(q_m, h.q_m, (size_t)s * nq1);
+    cp(lead, h.lead, (size_t)s * nq1);
+    cp(ngroup, h.ngroup, (size_t)s * nq1);
+    cp(thr0, h.thr0, (size_t)s * nq1);
+    cp(q_terms, h.q_terms, s * nqt);
+    cp(q_ub, h.q_ub, s * nqt);
+    cp(q_wt, h.q_wt, s * nqt);
+    cp(q_wn, h.q_wn, s * nqt);
+    cp(q_rup, h.q_rup, s * nqt);
+  };
+  if (S > 1 && q->n_queries >= 64) {
+    std::vector<int> rcs(S, FG_OK);
+    std::vector<std::string> errs(S);
+    run_parallel(S, [&](uint32_t s) {
+      if ((rcs[s] = plan_host(ixs[s], q, k, S, hs[s]))) errs[s] = fg_last_error();
+      else put_slot(s);
+    });
+    for (uint32_t s = 0; s < S; ++s)
+      if (rcs[s]) return fail(rcs[s], "snapshot %u: %s", s, errs[s].c_str());
+  } else {
+    for (uint32_t s = 0; s < S; ++s) {
+      if (int rc = plan_host(ixs[s], q, k, S, hs[s])) {
+        if (S == 1) return rc;
+        const std::string e = fg_last_error();
+        return fail(rc, "snapshot %u: %s", s, e.c_str());
+      }
+      if (S > 1) put_slot(s);
+    }
+  }
+  if (ptrace) pt[1] = pnow();
   uint32_t nf = 0;
   if (S == 1) {
     HostPlan& h = hs[0];
@@ -2743,8 +2772,6 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     for (uint32_t s = 0; s < S; ++s) {
       HostPlan& h = hs[s];
       const uint32_t fb = nf, vb = s * nq1;
-      cat(q_m, h.q_m); cat(q_terms, h.q_terms); cat(lead, h.lead); cat(ngroup, h.ngroup); cat(thr0, h.thr0);
-      cat(q_ub, h.q_ub); cat(q_wt, h.q_wt); cat(q_wn, h.q_wn); cat(q_rup, h.q_rup);
       for (uint32_t f : h.q_filter) q_filter.push_back(f == 0xFFFFFFFFu ? f : fb + f);
       cat(f_shift, h.f_shift); cat(f_tab, h.f_tab); cat(f_max, h.f_max);
       const uint64_t wb = f_woff.back();
@@ -3502,7 +3529,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   // dispatched ahead of a commit's rescores and builds; else per-thread streams
   const hipStream_t hs = ng == 1 && gdev[0] == dev0 ? search_stream(dev0) : hipStreamPerThread;
   bool merged = false;  // the plan's merged select already wrote ms / md / msh / mn
-  std::vector<std::unique_ptr<fg_plan>> plans(ng);
+  std::vector<std::unique_ptr<fg_plan>> plans(ng), parts;
   std::vector<hipEvent_t> evs(ng, nullptr);
   // teardown (also on error returns): every device's stream drained, then the
   // events, the plans and the buffers
@@ -3531,6 +3558,35 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     std::vector<fg_index*> ixs(S);
     for (uint32_t j = 0; j < S; ++j) ixs[j] = shards[gi[j]];
     fg_plan* p = nullptr;
+    // every shard on dev0 in one plan, a batch: its merged select writes the
+    // merged lists directly (no per-shard lists, no k_merge_rank); a small batch
+    // keeps one final select per shard (more workgroups in parallel: a single
+    // query over 8 segments 0.070 vs 0.077 ms p50): the merged select from
+    // batches of merged_min queries (tools/multi_ab.py, round 3).  A batch of
+    // 2 x kPipeMin queries or more runs as two halves, the second planned on the
+    // host while the first one's kernels run (C4, 1024 queries: one plan 478K
+    // q/s, two halves 560K, four quarters 487K, 256 + 768 queries 513K)
+    constexpr uint32_t merged_min = 256u, kPipeMin = 256u;
+    uint64_t docs = 0;
+    for (fg_index* x : ixs) docs += x->n_docs;
+    if (ng == 1 && gdev[0] == dev0 && S > 1 && docs <= 0xFFFFFFFFull && nq >= merged_min) {
+      const uint32_t np = nq >= 2 * kPipeMin ? 2u : 1u;
+      for (uint32_t i = 0; i < np; ++i) {
+        const uint32_t b = (uint32_t)((uint64_t)nq * i / np), e = (uint32_t)((uint64_t)nq * (i + 1) / np);
+        fg_query_batch qi = *q;  // queries [b, e): the same term arrays, offsets from q_off[b]
+        qi.n_queries = e - b;
+        qi.q_off = q->q_off + b;
+        if (q->f_off) qi.f_off = q->f_off + b;
+        const double t_p = trace ? now() : 0.0;
+        fg_plan* pi = nullptr;
+        if (int rc = plan_create_multi(ixs.data(), S, &qi, k, &pi, false, hs)) return rc;
+        parts.emplace_back(pi);
+        if (trace) t_plan += now() - t_p;
+        if (int rc = execute_impl(pi, hs, ms + (size_t)b * k, md + (size_t)b * k, mn + b, msh + (size_t)b * k)) return rc;
+      }
+      merged = true;
+      break;
+    }
     // the upload is queued on this thread's stream of the device, ahead of the
     // execute on the same stream: no host round trip
     const double t_p = trace ? now() : 0.0;
@@ -3541,17 +3597,6 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
     }
     plans[g].reset(p);
     if (trace) t_plan += now() - t_p;
-    // every shard on dev0 in one plan, a batch: its merged select writes the
-    // merged lists directly (no per-shard lists, no k_merge_rank); a small batch
-    // keeps one final select per shard (more workgroups in parallel: a single
-    // query over 8 segments 0.070 vs 0.077 ms p50): the merged select from
-    // batches of merged_min queries (tools/multi_ab.py, round 3)
-    constexpr uint32_t merged_min = 256u;
-    if (ng == 1 && gdev[0] == dev0 && S > 1 && p->d.seg_base && nq >= merged_min) {
-      if (int rc = execute_impl(p, hs, ms, md, mn, msh)) return rc;
-      merged = true;
-      break;
-    }
     // lists straight into the gathered buffers when the group's shards are
     // consecutive and on dev0 ([S][nq][k] is the gathered layout)
     const bool direct = gdev[g] == dev0 && gi.back() - gi.front() + 1 == S;

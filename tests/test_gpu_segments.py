@@ -173,3 +173,28 @@ def test_rescore_shares_structure_and_leaves_base_intact(native, ctx, parts):
         assert np.array_equal(np.stack([base.term_kth(t) for t in (0, 7, 300)]), kth)
     base.close()
     fresh.close()
+
+
+def test_sharded_batch_in_halves_equals_quarters(native, ctx, parts):
+    """fg_search_sharded plans a batch of >= 512 queries over several snapshots as
+    two halves, the second planned while the first one's kernels run: the merged
+    hits equal those of the same queries searched 256 at a time (one plan each)."""
+    from fugu_amd import synth
+    c, cut, (ao, at), (bo, bt) = parts
+    V = synth.VOCAB
+    g = native.docs_stats(ao, at, V, threads=16) + native.docs_stats(bo, bt, V, threads=16)
+    segs = [native.Index.from_docs(ctx, ao, at, V, threads=16, global_stats=g),
+            native.Index.from_docs(ctx, bo, bt, V, threads=16, global_stats=g)]
+    for (m0, m1, k, mode) in [(2, 5, 1000, native.MODE_OR), (3, 3, 100, native.MODE_AND), (1, 4, 20, native.MODE_OR)]:
+        q_off, terms = synth.queries(1024, m0, m1, seed_q=51)
+        whole = native.search_sharded(segs, q_off, terms, k, mode=mode, ctx=ctx)
+        for b in range(0, 1024, 256):
+            qo = (q_off[b:b + 257] - q_off[b]).astype(q_off.dtype)
+            part = native.search_sharded(segs, qo, terms[q_off[b]:q_off[b + 256]], k, mode=mode, ctx=ctx)
+            assert np.array_equal(part[3], whole[3][b:b + 256]), (k, mode, b)
+            for i in range(256):
+                m = int(part[3][i])
+                for a in range(3):
+                    assert np.array_equal(part[a][i, :m], whole[a][b + i, :m]), (k, mode, b + i, a)
+    for x in segs:
+        x.close()
