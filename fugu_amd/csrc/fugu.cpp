@@ -2589,13 +2589,16 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
       // (shorter first items -- G >> r, G >> (r-1), ... tiles -- so the items that
       // start with no threshold publish one early: r = 2 / 3 / 5 / 8 slower at
       // k = 1000 and 20, +0.4% to +7%: profiles/r05/ab/disj_ramp_r05t.log)
+      // (shorter items at the end of each query's range -- half-size in its last
+      // 1/8, 1/4, 1/2 -- measured +8.6 / +18 / +34% at top-20, +9 / +18 / +33% at
+      // top-1000; 64-tile items -0.5% / +1.8%: profiles/r06/ab/)
       const uint32_t ng = (nt + G - 1) / G;
-      ngroup[i] = ng;
       for (uint32_t g = 0; g < ng; ++g) {
         const uint32_t t0 = tlo + g * G, n = std::min(G, nt - g * G);
         const double mid = ((double)t0 + 0.5 * n) * (double)(1u << fg::kDisjTileShift) / (double)ix->n_docs;
         ditems.push_back(W{mid, i, t0, n});
       }
+      ngroup[i] = ng;
       if (ditems.size() > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%zu work items)", ditems.size());
       continue;
     }

@@ -68,6 +68,16 @@ def main():
     }
     post = wg[:, 5].astype(np.int64)
     b1 = (wg[:, 6] >> np.uint64(32)).astype(np.int64)
+    # the sweep (rows in plan order) in sixteenths: workgroup time, streamed
+    # postings, postings past bound 1 and candidates rescored in each
+    cuts = np.linspace(0, len(wg), 17).astype(int)
+    cand = (wg[:, 6] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    out["by_sweep_16th"] = {
+        "wg_ms": [round(float(dt[a:b].sum()) * 1e-3, 1) for a, b in zip(cuts[:-1], cuts[1:])],
+        "postings_M": [round(float(post[a:b].sum()) * 1e-6, 2) for a, b in zip(cuts[:-1], cuts[1:])],
+        "past_bound1_M": [round(float(b1[a:b].sum()) * 1e-6, 3) for a, b in zip(cuts[:-1], cuts[1:])],
+        "candidates_M": [round(float(cand[a:b].sum()) * 1e-6, 3) for a, b in zip(cuts[:-1], cuts[1:])],
+    }
     qid = (wg[:, 7] & np.uint64(0xFFFFFFFF)).astype(np.int64)
     top = np.argsort(-dt)[:12]
     out["longest_items"] = [{"q": int(qid[i]), "us": round(float(dt[i]), 1), "start_us": round(float(st[i]), 1),
