@@ -582,6 +582,44 @@ def alone_kernel_ms(ixs, q_off, terms, K, mode, st, reps):
     return ms, hits_sha1(out[0], out[1], out[2], out[3], K)
 
 
+def peers_rehearsal(ixs, q_off, terms, K, native, torch, gs, gd, gn, st, reps):
+    """C5's 8-GPU threshold sharing rehearsed on one GPU: every shard's plan a
+    PEER of the others' (fg_plan_set_peers: its thresholds and hit counts also
+    published into theirs during the launch), the 8 plans on 8 streams at once.
+    Sharing one GPU, each shard progresses at ~1/8 of its speed, so thresholds
+    evolve per posting as on 8 GPUs: wall / 8 is the per-GPU time of the split."""
+    from fugu_amd.shard import agree_hist_span, merge_on_device
+    nq = len(q_off) - 1
+    plans = [ix.plan(q_off, terms, K, native.MODE_OR) for ix in ixs]
+    agree_hist_span(plans)
+    for i, p in enumerate(plans):
+        p.set_peers([x for j, x in enumerate(plans) if j != i])
+    streams = [torch.cuda.Stream() for _ in plans]
+
+    def rnd():
+        for p in plans:
+            p.reset(st)
+        torch.cuda.synchronize()  # every reset before any peer's kernels
+        t = time.perf_counter()
+        for r, (p, s) in enumerate(zip(plans, streams)):
+            p.execute(s.cuda_stream, gs[r].data_ptr(), gd[r].data_ptr(), gn[r].data_ptr())
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) * 1e3
+
+    rnd()
+    walls = [rnd() for _ in range(reps)]
+    out = merge_on_device(gs, gd, gn, nq, K, st)
+    torch.cuda.synchronize()
+    sha = hits_sha1(out[0], out[1], out[2], out[3], K)
+    for p in plans:
+        p.set_peers([])
+        p.close()
+    w = float(np.median(walls))
+    return {"wall_ms": round(w, 4), "per_gpu_ms": round(w / len(plans), 4), "result_sha1": sha,
+            "note": "8 shard plans, peers of each other (fg_plan_set_peers), on 8 streams of this GPU; per_gpu_ms = "
+                    "wall / 8 (tools/c5_peers.py)"}
+
+
 def hits_sha1(s, d, sh, n, K):
     """sha1 (16 hex) of merged (score, doc, shard) lists, each query's first n entries."""
     import hashlib
@@ -648,6 +686,8 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
     alone_se, sha_se = alone_kernel_ms(ixs, q_off, terms, K, native.MODE_OR, st, max(2, steps // 2))
     log(f"[bench] C5 shards alone: unseeded max {max(x[0] for x in alone_un)} ms, seeded max "
         f"{max(x[0] for x in alone_se)} ms (linked mean {np.mean(per_shard):.3f}); floor in {seed_s:.1f}s")
+    peers = peers_rehearsal(ixs, q_off, terms, K, native, torch, gs, gd, gn, st, max(2, steps // 2))
+    log(f"[bench] C5 peers on 8 streams: {peers['wall_ms']} ms wall, {peers['per_gpu_ms']} ms per shard")
     # the step: ONE multi-snapshot plan over the 8 shards (one launch per kernel),
     # planned with the floor; beside it the same plan without the floor
     outs = tuple(torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)) + (
@@ -698,6 +738,8 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
                "note": "each shard's plan alone (no shared threshold word: one GPU of the 8-GPU split); seeded = "
                        "its starting thresholds floored by the namespace-wide per-term K-th score bounds "
                        "(fg_index_term_ladder of every shard, one all-gather at build, fg_kth_floor_combine)"},
+           "peers_8_streams": {**peers, "per_gpu_over_linked_mean": round(peers["per_gpu_ms"] / float(np.mean(per_shard)), 3),
+                               "same_hits": peers["result_sha1"] == sha_se},
            "multi_plan_unseeded": {"ms_per_step": round(el0 * 1e3 / max(2, steps // 2), 4),
                                    "kernels_ms": [round(mk0[0] / max(mkn0, 1), 4), round(mk0[1] / max(mkn0, 1), 4)],
                                    "result_sha1": sha_multi_un},
@@ -706,8 +748,9 @@ def bench_c5(ctx, native, synth, torch, dev, nq, steps, warmup, threads, cpu_sec
            "workload": "C5: 100M docs s=1.1 as 8 doc shards with global BM25 statistics, 2-5-term OR top-1000 on "
                        "all 8 + device merge, all 8 shards on this one GPU (the step: one multi-snapshot plan, "
                        "seeded with the namespace-wide K-th floors)",
-           "projected_8gpu": "each GPU runs one shard alone: step ~ max(k_disj_ms_per_shard_independent.seeded) + "
-                             "k_final + all-gather + merge"}
+           "projected_8gpu": "each GPU runs one shard, its plan a peer of the others' (bench --config c5 over N "
+                             "GPUs: shard.link_peers): step ~ peers_8_streams.per_gpu_ms + reset barrier + all-gather "
+                             "+ merge; without peers max(k_disj_ms_per_shard_independent.seeded)"}
     del mp
     for ix in ixs:
         ix.close()
@@ -818,15 +861,25 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
     merged_sel = len(plans) == 1 and len(ixs) > 1
     mouts = [torch.empty(nq * K, dtype=t, device=dev) for t in (torch.float32, torch.int32, torch.int32)] + [
         torch.empty(nq, dtype=torch.int32, device=dev)]
-    # C5 over N ranks: the rank's k_disj sweep in two parts, the ranks' score
-    # histograms summed between them (one all-reduce per batch); bins agreed once
+    # C5 over N ranks: the ranks' plans are PEERS -- each publishes its thresholds
+    # and hit counts into every other rank's during the launch, over xGMI
+    # (shard.link_peers; one-GPU rehearsal: tools/c5_peers.py); FUGU_C5_XFRAC > 0
+    # instead runs the sweep in two parts with the histograms summed between them
     xfrac = C5_XFRAC if (not c4 and world > 1 and len(plans) == 1 and 0.0 < C5_XFRAC < 1.0) else 0.0
+    peers = 0
+    if not c4 and world > 1 and len(plans) == 1 and backend == "nccl":
+        from fugu_amd.shard import agree_hist_span
+        agree_hist_span(plans, device=dev)
+        if not xfrac:
+            from fugu_amd.shard import link_peers, reset_peers
+            peers = link_peers(plans[0])
     if xfrac:
-        from fugu_amd.shard import agree_hist_span, exchange_hist
-        agree_hist_span(plans, device=dev if backend == "nccl" else None)
+        from fugu_amd.shard import exchange_hist
         hbuf = torch.zeros(nq * native.HIST_BINS, dtype=torch.int32, device=dev)
 
     def step():
+        if peers:
+            reset_peers(plans[0], st.cuda_stream)
         if xfrac:
             p0 = plans[0]
             p0.execute_part(st.cuda_stream, 0.0, xfrac)
@@ -936,6 +989,10 @@ def run_config(args, cfg, rank, world, local, dev, backend, threads, torch, dist
             "result_sha1": h.hexdigest()[:16],
             "hits": int(mn.sum()),
             **({"kth_floor": floor_info} if floor_info else {}),
+            **({"peers": {"per_rank": peers, "note": "each rank's plan publishes its thresholds and hit counts into "
+                                                       "every other rank's during the launch (device atomics over "
+                                                       "xGMI on HIP-IPC-mapped words: shard.link_peers); a step "
+                                                       "starts with reset_peers (reset + barrier)"}} if peers else {}),
             **({"hist_exchange": {"frac": xfrac, "all_reduce_bytes_per_rank": 4 * nq * native.HIST_BINS,
                                   "note": "each rank's k_disj sweep in two parts ([0, frac), [frac, 1)); between "
                                           "them ONE all-reduce sums the ranks' per-query score histograms "

@@ -474,6 +474,10 @@ struct fg_plan {
       if (pin) ix->pinned->put(pin, pin_n);
       ix->pool->put(ws, ws_got);
     }
+    if (!ipc_maps.empty()) {
+      (void)hipSetDevice(ix->dev);
+      for (void* m : ipc_maps) (void)hipIpcCloseMemHandle(m);
+    }
     if (ix) fg_index_release(ix);
     for (fg_index* x : segs) fg_index_release(x);
   }
@@ -484,6 +488,7 @@ struct fg_plan {
   bool zeroed = false;        // the zero region arrived zeroed with the upload: the first execute skips its memset
   void* pin = nullptr;        // pinned upload staging still in flight (create without sync), returned at destroy
   size_t pin_n = 0;
+  std::vector<void*> ipc_maps;  // peers' workspaces mapped through HIP IPC (fg_plan_set_ipc_peers), closed at destroy
   hipStream_t up_stream = hipStreamPerThread;  // the stream the plan was uploaded on
 };
 

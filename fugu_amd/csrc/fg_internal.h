@@ -327,6 +327,8 @@ __host__ __device__ inline uint32_t filter_bits(const uint32_t* mask, uint32_t s
 // of the query's lead list) are ordered as a doc sweep across the batch:
 // items covering similar doc ranges of different queries run together, so the
 // segments of hot posting lists they probe are shared through L2 / MALL.
+constexpr uint32_t kMaxPeers = 15;  // peers of one plan (fugu.h FG_MAX_PEERS, fg_plan_set_peers)
+
 struct DevPlan {
   uint32_t n_queries;
   uint32_t total_chunks;        // k_conj items [0, n_conj) then k_disj items [n_conj, total_chunks)
@@ -374,6 +376,15 @@ struct DevPlan {
   const uint32_t* seg_base;     // [n_segs] first doc of each snapshot in the concatenation (k_final's merged
                                 // select), or nullptr when the snapshots hold >= 2^32 docs together
   DevFilters f;
+  // Peer plans (fg_plan_set_peers: the other doc shards of one namespace, on
+  // other devices or in other processes): every threshold this plan publishes
+  // and every count it adds to its histogram also go, score-only, into the
+  // peers' thresh / hist of the same batch query, so each shard prunes with the
+  // hits of all of them as they are found (the cross-device form of
+  // fg_plan_link's shared words)
+  uint32_t n_peers;
+  uint32_t* peer_hist[kMaxPeers];
+  uint64_t* peer_thr[kMaxPeers];
 };
 
 // The batch query of a query slot (thresh / hist index)

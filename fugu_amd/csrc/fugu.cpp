@@ -3145,7 +3145,7 @@ static int execute_impl(fg_plan* p, hipStream_t s, float* os, uint32_t* od, uint
                         double from = 0.0, double to = 1.0) {
   HIPCHK(hipSetDevice(p->ix->dev));
   const bool first = from <= 0.0, last = to >= 1.0;
-  if (first) {
+  if (first && !p->d.n_peers) {  // (with peers: fg_plan_reset, ordered before every peer's execute)
     if (p->zeroed) p->zeroed = false;  // the first execute after the upload
     else HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, s));
   }
@@ -3211,7 +3211,89 @@ int fg_plan_execute_part(fg_plan* p, void* stream, double from, double to, float
   return rc;
 }
 
+int fg_plan_set_peers(fg_plan* p, fg_plan* const* peers, uint32_t n) {
+  if (!p || (n && !peers)) return fail(FG_EINVAL, "bad arguments");
+  if (n > FG_MAX_PEERS) return fail(FG_EUNSUPPORTED, "%u peers (> FG_MAX_PEERS = %d)", n, FG_MAX_PEERS);
+  for (uint32_t i = 0; i < n; ++i) {
+    const fg_plan* o = peers[i];
+    if (!o || o == p) return fail(FG_EINVAL, "peer %u: NULL or the plan itself", i);
+    if (o->nq_batch != p->nq_batch || o->k != p->k) return fail(FG_EINVAL, "peer %u plans another batch or k", i);
+    if (o->h_lo.size() != p->h_lo.size()) return fail(FG_EINVAL, "peer %u: another number of query slots", i);
+    if (o->ix->dev != p->ix->dev) {
+      int ok = 0;
+      HIPCHK(hipDeviceCanAccessPeer(&ok, p->ix->dev, o->ix->dev));
+      if (!ok) return fail(FG_EUNSUPPORTED, "device %d cannot reach peer %u's device %d", p->ix->dev, i, o->ix->dev);
+    }
+  }
+  p->d.n_peers = n;
+  for (uint32_t i = 0; i < n; ++i) {
+    p->d.peer_hist[i] = peers[i]->d.hist;
+    p->d.peer_thr[i] = peers[i]->d.thresh;
+  }
+  if (n) p->d.pub_mask = 0xFFFFFFFF00000000ull;  // score-only: the peers' docs are other docs
+  return FG_OK;
+}
+
+int fg_plan_ipc_export(const fg_plan* p, fg_plan_ipc* out) {
+  if (!p || !out) return fail(FG_EINVAL, "bad arguments");
+  const char* ws = static_cast<const char*>(p->ws);
+  const char* th = reinterpret_cast<const char*>(p->d.thresh);
+  const char* hi = reinterpret_cast<const char*>(p->d.hist);
+  if (th < ws || th >= ws + p->ws_got || hi < ws || hi >= ws + p->ws_got)
+    return fail(FG_EUNSUPPORTED, "the plan's thresholds are another plan's (linked): export that plan");
+  std::memset(out, 0, sizeof *out);
+  hipIpcMemHandle_t h;
+  HIPCHK(hipSetDevice(p->ix->dev));
+  HIPCHK(hipIpcGetMemHandle(&h, p->ws));
+  static_assert(sizeof h <= sizeof out->handle, "fg_plan_ipc::handle");
+  std::memcpy(out->handle, &h, sizeof h);
+  out->thresh_off = (uint64_t)(th - ws);
+  out->hist_off = (uint64_t)(hi - ws);
+  out->n_queries = p->nq_batch;
+  out->k = p->k;
+  out->device = p->ix->dev;
+  return FG_OK;
+}
+
+int fg_plan_set_ipc_peers(fg_plan* p, const fg_plan_ipc* peers, uint32_t n) {
+  if (!p || (n && !peers)) return fail(FG_EINVAL, "bad arguments");
+  if (n > FG_MAX_PEERS) return fail(FG_EUNSUPPORTED, "%u peers (> FG_MAX_PEERS = %d)", n, FG_MAX_PEERS);
+  for (uint32_t i = 0; i < n; ++i)
+    if (peers[i].n_queries != p->nq_batch || peers[i].k != p->k) return fail(FG_EINVAL, "peer %u plans another batch or k", i);
+  HIPCHK(hipSetDevice(p->ix->dev));
+  std::vector<void*> maps;
+  for (uint32_t i = 0; i < n; ++i) {
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, peers[i].handle, sizeof h);
+    void* base = nullptr;
+    if (hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      (void)hipGetLastError();
+      for (void* m : maps) (void)hipIpcCloseMemHandle(m);
+      return fail(FG_EHIP, "peer %u: hipIpcOpenMemHandle failed", i);
+    }
+    maps.push_back(base);
+  }
+  for (void* m : p->ipc_maps) (void)hipIpcCloseMemHandle(m);
+  p->ipc_maps = maps;
+  p->d.n_peers = n;
+  for (uint32_t i = 0; i < n; ++i) {
+    p->d.peer_thr[i] = reinterpret_cast<uint64_t*>(static_cast<char*>(maps[i]) + peers[i].thresh_off);
+    p->d.peer_hist[i] = reinterpret_cast<uint32_t*>(static_cast<char*>(maps[i]) + peers[i].hist_off);
+  }
+  if (n) p->d.pub_mask = 0xFFFFFFFF00000000ull;
+  return FG_OK;
+}
+
+int fg_plan_reset(fg_plan* p, void* stream) {
+  if (!p) return fail(FG_EINVAL, "NULL plan");
+  HIPCHK(hipSetDevice(p->ix->dev));
+  HIPCHK(hipMemsetAsync(p->zero_region, 0, p->zero_bytes, static_cast<hipStream_t>(stream)));
+  p->zeroed = false;
+  return FG_OK;
+}
+
 static_assert(fg::kQBins == FG_HIST_BINS, "fugu.h's histogram size");
+static_assert(fg::kMaxPeers == FG_MAX_PEERS, "fugu.h's peer count");
 
 int fg_plan_hist_span(const fg_plan* p, uint32_t* lo, uint32_t* hi) {
   if (!p || !lo || !hi) return fail(FG_EINVAL, "bad arguments");

@@ -228,8 +228,22 @@ __device__ uint64_t hist_threshold(const uint32_t* gh, uint32_t K, uint32_t lo, 
   return b < kQBins ? (uint64_t)(lo + (b << sh)) << 32 : 0ull;
 }
 
-// Add the LDS bins to the query's global histogram and clear them.
-__device__ inline void hist_add(uint32_t* lh, uint32_t* gh) {
+constexpr uint64_t kScoreOnly = 0xFFFFFFFF00000000ull;  // a key's score bits (thresholds shared across shards)
+
+// A threshold published for batch query ql goes, score-only, to the peer plans
+// too (DevPlan::peer_thr; their histograms: hist_add / hist_add16)
+__device__ inline void peer_thr_max(const DevPlan& pl, uint32_t ql, uint64_t key) {
+  for (uint32_t i = 0; i < pl.n_peers; ++i)
+    atomicMax(reinterpret_cast<unsigned long long*>(pl.peer_thr[i] + ql), (unsigned long long)(key & kScoreOnly));
+}
+
+// Add the LDS bins to the query's global histogram (and the peers', a pass
+// each over the bins: one loop holding every peer's address took k_conj past
+// its register budget) and clear them.
+__device__ inline void hist_add(uint32_t* lh, uint32_t* gh, const DevPlan& pl, uint32_t ql) {
+  for (uint32_t i = 0; i < pl.n_peers; ++i)
+    for (uint32_t b = threadIdx.x; b < kQBins; b += kThreads)
+      if (const uint32_t c = lh[b]) atomicAdd(pl.peer_hist[i] + (size_t)ql * kQBins + b, c);
   for (uint32_t b = threadIdx.x; b < kQBins; b += kThreads) {
     const uint32_t c = lh[b];
     if (c) {
@@ -666,6 +680,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     sh.n_dq = 0;
     sh.thr = thr0;
     pend = atomicMax(gthr, (unsigned long long)(thr0 & pl.pub_mask));
+    peer_thr_max(pl, ql, thr0);
   }
   // query-time scores: the tf caches into LDS (read after the first chunk's barrier)
   if constexpr (kF & kFQt)
@@ -901,6 +916,9 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
     }
   }
   if (tid == 0 && pend > sh.thr) sh.thr = pend;
+  // the peers get the item's threshold once, when it ends (inside the chunk loop
+  // the publication cost k_conj a spilled register)
+  if (tid == 0) peer_thr_max(pl, ql, sh.thr);
   __syncthreads();
 
   // write the kept keys that still clear the freshest threshold
@@ -918,7 +936,7 @@ __global__ __launch_bounds__(kThreads, FG_WAVES) void k_conj(DevIndex ix0, DevPl
       if (b < kQBins) atomicAdd(&sh.hist[b], 1u);
     }
     __syncthreads();
-    hist_add(sh.hist, gh);
+    hist_add(sh.hist, gh, pl, ql);
   }
   FG_STAMP(w, 0, t_start);
   FG_STAMP(w, 1, t_probe);
@@ -1029,8 +1047,17 @@ struct DisjShared : DisjQt<kQt> {
 };
 static_assert(kMaxTiles <= 32, "DisjShared::t_post: one bit per tile");
 
-// Add the packed LDS bins (DisjShared::lh) to the query's global histogram and clear them.
-__device__ inline void hist_add16(uint32_t* lh, uint32_t* gh) {
+// Add the packed LDS bins (DisjShared::lh) to the query's global histogram
+// (and the peers') and clear them.
+__device__ inline void hist_add16(uint32_t* lh, uint32_t* gh, const DevPlan& pl, uint32_t ql) {
+  for (uint32_t i = 0; i < pl.n_peers; ++i) {  // (a pass per peer, as hist_add)
+    uint32_t* ph = pl.peer_hist[i] + (size_t)ql * kQBins;
+    for (uint32_t b = threadIdx.x; b < kQBins / 2; b += kThreads)
+      if (const uint32_t c = lh[b]) {
+        if (c & 0xFFFFu) atomicAdd(&ph[2 * b], c & 0xFFFFu);
+        if (c >> 16) atomicAdd(&ph[2 * b + 1], c >> 16);
+      }
+  }
   for (uint32_t b = threadIdx.x; b < kQBins / 2; b += kThreads) {
     const uint32_t c = lh[b];
     if (c) {
@@ -1057,6 +1084,8 @@ struct QHist {
   uint32_t lo, sh;
   uint64_t pub;      // DevPlan::pub_mask
   uint32_t m, mq;    // MustNot clauses: c_meta[m, mq)
+  const DevPlan* pl;  // its peers (DevPlan::peer_*)
+  uint32_t ql;        // the batch query
 };
 
 // Keep the threshold fresh: drop the keys appended since the last call whose
@@ -1093,7 +1122,7 @@ __device__ inline void disj_truncate(const DevIndex& ix, Sh& sh, uint32_t K, uin
     n = sh.n_buf;
   }
   if (sh.n_lh + (n - sh.n_cnt) > 0xFFFFu) {  // uniform (LDS after a barrier): a u16 bin could overflow
-    hist_add16(sh.lh, hq.gh);
+    hist_add16(sh.lh, hq.gh, *hq.pl, hq.ql);
     __syncthreads();
     if (threadIdx.x == 0) sh.n_lh = 0;
   }
@@ -1108,7 +1137,10 @@ __device__ inline void disj_truncate(const DevIndex& ix, Sh& sh, uint32_t K, uin
     const uint64_t mine = T > sh.thr ? T : sh.thr;
     // the exchange does not wait: the returned best is folded in when the
     // next pass starts (pend), after that pass's posting loads are in flight
-    if (publish) pend = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)(mine & hq.pub));
+    if (publish) {
+      pend = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)(mine & hq.pub));
+      peer_thr_max(*hq.pl, hq.ql, mine);
+    }
     sh.thr = mine;
     sh.n_lh += n - sh.n_cnt;
     sh.n_cnt = sh.n_buf;
@@ -1137,7 +1169,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   const uint32_t* terms = pl.q_terms + (size_t)q * kMaxTerms;
   const uint32_t K = pl.k;
   uint64_t* gthr = &pl.thresh[ql];
-  const QHist hq{pl.hist + (size_t)ql * kQBins, pl.q_hlo[q], pl.q_hsh[q], pl.pub_mask, m, mq};
+  const QHist hq{pl.hist + (size_t)ql * kQBins, pl.q_hlo[q], pl.q_hsh[q], pl.pub_mask, m, mq, &pl, ql};
   uint64_t pend = 0;  // thread 0: the last threshold exchange's reply, not yet folded in
 
   // facet filter: the union is intersected with the facet union, score = union + facet;
@@ -1169,6 +1201,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
     sh.t_post = 0;
     const uint64_t t0 = pl.q_thr0[q];
     const uint64_t g = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)t0);
+    peer_thr_max(pl, ql, t0);
     sh.thr = g > t0 ? g : t0;
   }
   for (uint32_t b = tid; b < kQBins / 2; b += kThreads) sh.lh[b] = 0;
@@ -1793,7 +1826,7 @@ __global__ __launch_bounds__(kThreads, FG_DISJ_WAVES) void k_disj(DevIndex ix0, 
   }
   // the item's counted hits join the query's histogram (every key was counted
   // by the last disj_truncate)
-  hist_add16(sh.lh, hq.gh);
+  hist_add16(sh.lh, hq.gh, pl, ql);
   if (tid == 0 && pend > sh.thr) sh.thr = pend;
   __syncthreads();
   flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
@@ -1859,7 +1892,7 @@ struct ScanShared {
 };
 
 __device__ inline void scan_truncate(ScanShared& sh, uint32_t K, uint32_t limit, uint64_t* gthr, bool publish,
-                                     uint64_t pub) {
+                                     uint64_t pub, const DevPlan& pl, uint32_t ql) {
   const uint32_t n = sh.n_buf;
   __syncthreads();
   uint64_t T = 0;
@@ -1868,6 +1901,7 @@ __device__ inline void scan_truncate(ScanShared& sh, uint32_t K, uint32_t limit,
     uint64_t mine = T > sh.thr ? T : sh.thr;
     if (publish) {
       const uint64_t old = atomicMax(reinterpret_cast<unsigned long long*>(gthr), (unsigned long long)(mine & pub));
+      peer_thr_max(pl, ql, mine);
       mine = old > mine ? old : mine;
     }
     sh.thr = mine;
@@ -1922,9 +1956,9 @@ __global__ __launch_bounds__(kThreads) void k_scan(DevIndex ix0, DevPlan pl) {
         wave_append(keep && key >= thr, key, sh.buf, &sh.n_buf, kBufD);
       }
       __syncthreads();
-      scan_truncate(sh, K, kTrunc, gthr, false, pl.pub_mask);
+      scan_truncate(sh, K, kTrunc, gthr, false, pl.pub_mask, pl, ql);
     }
-    scan_truncate(sh, K, K, gthr, true, pl.pub_mask);
+    scan_truncate(sh, K, K, gthr, true, pl.pub_mask, pl, ql);
   }
   flush_candidates(pl, q, sh.buf, sh.n_buf, sh.thr, sh.scratch);
 }

@@ -57,10 +57,12 @@ EXPORTS = (
     "fg_index_rescore_many", "fg_index_build_global",
     "fg_ctx_peer_access", "fg_plan_link", "fg_bytes_model_or", "fg_plan_create_multi", "fg_plan_execute_merged", "fg_index_term_kth",
     "fg_model_batch", "fg_abi_version", "fg_index_term_ladder", "fg_kth_floor_combine", "fg_index_set_kth_floor",
+    "fg_plan_set_peers", "fg_plan_ipc_export", "fg_plan_set_ipc_peers", "fg_plan_reset",
 )
 LADDER_KS = (1, 2, 3, 5, 10, 13, 20, 25, 50, 100, 125, 250, 500, 1000)  # FG_LADDER_LEVELS ranks
 KTH_KS = (1, 10, 20, 100, 1000)  # fg_index_term_kth / fg_index_set_kth_floor ranks
 HIST_BINS = 512  # fugu.h FG_HIST_BINS: score-histogram bins per query
+MAX_PEERS = 15  # fugu.h FG_MAX_PEERS
 ABI_VERSION = 5  # include/fugu.h FG_ABI_VERSION this binding's structs follow
 
 if not os.path.exists(LIB_PATH):
@@ -116,6 +118,12 @@ class ModelOut(C.Structure):
                                           "query_line_bytes", "loads", "candidates")]
 
 
+class PlanIpc(C.Structure):
+    """fugu.h fg_plan_ipc: a plan's threshold / histogram words as another process maps them."""
+    _fields_ = [("handle", C.c_uint8 * 64), ("thresh_off", C.c_uint64), ("hist_off", C.c_uint64),
+                ("n_queries", C.c_uint32), ("k", C.c_uint32), ("device", C.c_int), ("reserved", C.c_uint32)]
+
+
 class PlanInfo(C.Structure):
     _fields_ = [("n_queries", C.c_uint32), ("k", C.c_uint32), ("total_chunks", C.c_uint32),
                 ("workspace_bytes", C.c_uint64)]
@@ -165,6 +173,10 @@ _sig("fg_plan_hist_span", C.c_int, _p, _u32p, _u32p)
 _sig("fg_plan_set_hist_span", C.c_int, _p, _u32p, _u32p)
 _sig("fg_plan_execute_part", C.c_int, _p, _p, C.c_double, C.c_double, _p, _p, _p, _p)
 _sig("fg_plan_hist_copy", C.c_int, _p, _p, _p, C.c_int)
+_sig("fg_plan_set_peers", C.c_int, _p, C.POINTER(_p), C.c_uint32)
+_sig("fg_plan_ipc_export", C.c_int, _p, C.POINTER(PlanIpc))
+_sig("fg_plan_set_ipc_peers", C.c_int, _p, C.POINTER(PlanIpc), C.c_uint32)
+_sig("fg_plan_reset", C.c_int, _p, _p)
 _sig("fg_plan_info_get", C.c_int, _p, C.POINTER(PlanInfo))
 _sig("fg_plan_profile", C.c_int, _p, C.c_int)
 _sig("fg_plan_kernel_ms", C.c_int, _p, _f64p, _u32p)
@@ -616,6 +628,32 @@ class Plan:
     def hist_copy(self, stream: int | None, d_buf: int, into_plan: bool):
         """Copy the histograms [n_batch, HIST_BINS] u32 to / from device memory d_buf."""
         _check(_lib.fg_plan_hist_copy(self._h, stream, d_buf, 1 if into_plan else 0))
+
+    def set_peers(self, peers):
+        """fg_plan_set_peers: publish thresholds / hit counts into these plans too
+        (same process; [] clears).  Executes then need reset() first."""
+        hs = (_p * max(len(peers), 1))(*[x._h for x in peers])
+        self._peers = list(peers)  # (kept alive while this plan can publish into them)
+        _check(_lib.fg_plan_set_peers(self._h, hs, len(peers)))
+
+    def ipc_export(self) -> bytes:
+        """fg_plan_ipc_export: the plan's words for another process (set_ipc_peers)."""
+        x = PlanIpc()
+        _check(_lib.fg_plan_ipc_export(self._h, C.byref(x)))
+        return bytes(x)
+
+    def set_ipc_peers(self, blobs):
+        """fg_plan_set_ipc_peers: peers in other processes, from their ipc_export() bytes."""
+        arr = (PlanIpc * max(len(blobs), 1))()
+        for i, b in enumerate(blobs):
+            if len(b) != C.sizeof(PlanIpc):
+                raise ValueError(f"peer {i}: {len(b)} bytes, expected {C.sizeof(PlanIpc)}")
+            C.memmove(C.byref(arr, i * C.sizeof(PlanIpc)), b, len(b))
+        _check(_lib.fg_plan_set_ipc_peers(self._h, arr, len(blobs)))
+
+    def reset(self, stream: int | None = None):
+        """fg_plan_reset: zero thresholds, histograms and candidate counts (peers: before every round)."""
+        _check(_lib.fg_plan_reset(self._h, stream))
 
     def results(self):
         nq, k = self.n_queries, self.k

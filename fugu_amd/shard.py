@@ -180,6 +180,33 @@ def exchange_hist(plan, stream: int, buf: torch.Tensor, group=None, prev: "torch
     return buf.clone()
 
 
+def link_peers(plan, group=None):
+    """Doc shards on several ranks (C5 over N GPUs): make this rank's plan a PEER
+    of every other rank's plan of the same batch -- its thresholds and hit counts
+    published into theirs during the launch, over xGMI (fg_plan_set_ipc_peers)
+    -- through ONE all-gather of the plans' IPC words (fg_plan_ipc_export, 96 B
+    per rank).  Agree on the histogram span first (agree_hist_span).  Every
+    round then runs reset_peers() before the executes.  Returns the peer count."""
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if world <= 1:
+        return 0
+    me = dist.get_rank(group)
+    blobs = [None] * world
+    dist.all_gather_object(blobs, plan.ipc_export(), group=group)
+    peers = [b for r, b in enumerate(blobs) if r != me]
+    plan.set_ipc_peers(peers)
+    return len(peers)
+
+
+def reset_peers(plan, stream=None, group=None):
+    """A round of peer plans: this rank's plan reset, then a barrier, so every
+    rank's words are zero before any rank's kernels publish into them."""
+    plan.reset(stream)
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.barrier(group=group)
+
+
 def shard_ranges(n_docs: int, world: int):
     """Contiguous doc-id ranges [b, e) of the shards (tantivy segments)."""
     step = (n_docs + world - 1) // world

@@ -340,6 +340,32 @@ int fg_plan_execute_part(fg_plan* p, void* stream, double from, double to, float
 /* Copy the plan's histograms [n_queries][FG_HIST_BINS] u32 to (into_plan = 0)
  * or from (1) device memory d_buf of the plan's device, on `stream`. */
 int fg_plan_hist_copy(fg_plan* p, void* stream, uint32_t* d_buf, int into_plan);
+/* ---- peer plans: thresholds shared DURING a launch, across devices or
+ * processes (C5's shards, one per GPU).  Each shard's plan keeps its own
+ * per-query threshold and histogram; with peers set, every threshold it
+ * publishes and every hit count it adds ALSO go, score-only, into the peers'
+ * words of the same batch query (device atomics: in-process peer access, or
+ * the peer's workspace mapped through HIP IPC), so every shard prunes with the
+ * hits of all of them as they are found, not only between parts.  Peers plan
+ * the same batch and k with one histogram span (fg_plan_set_hist_span).  With
+ * peers set an execute no longer zeroes the plan's state: before each round
+ * call fg_plan_reset on every peer and order all resets before any peer's
+ * execute (a barrier across the devices or processes); destroy no plan while
+ * a peer can still publish into it.  n = 0 clears the peers. */
+#define FG_MAX_PEERS 15
+int fg_plan_set_peers(fg_plan* p, fg_plan* const* peers, uint32_t n);
+/* A plan's threshold / histogram words as another process maps them. */
+typedef struct fg_plan_ipc {
+  uint8_t handle[64]; /* hipIpcMemHandle_t of the plan's workspace */
+  uint64_t thresh_off, hist_off;
+  uint32_t n_queries, k;
+  int device;
+  uint32_t reserved;
+} fg_plan_ipc;
+int fg_plan_ipc_export(const fg_plan* p, fg_plan_ipc* out);
+int fg_plan_set_ipc_peers(fg_plan* p, const fg_plan_ipc* peers, uint32_t n);
+/* Zero the plan's thresholds, histograms and candidate counts on `stream`. */
+int fg_plan_reset(fg_plan* p, void* stream);
 /* Copy the plan's own result buffers to host (synchronises the plan's stream). */
 int fg_plan_results(fg_plan* p, float* out_score, uint32_t* out_doc, uint32_t* out_n);
 typedef struct fg_plan_info {

@@ -120,6 +120,17 @@ pub struct fg_query_batch {
 }
 
 #[repr(C)]
+pub struct fg_plan_ipc {
+    pub handle: [u8; 64],           // hipIpcMemHandle_t of the plan's workspace
+    pub thresh_off: u64,
+    pub hist_off: u64,
+    pub n_queries: u32,
+    pub k: u32,
+    pub device: c_int,
+    pub reserved: u32,
+}
+
+#[repr(C)]
 pub struct fg_plan_info {
     pub n_queries: u32,
     pub k: u32,
@@ -225,6 +236,10 @@ extern "C" {
     pub fn fg_plan_execute_part(p: *mut fg_plan, stream: *mut c_void, from: f64, to: f64, d_out_score: *mut f32,
                                 d_out_doc: *mut u32, d_out_shard: *mut u32, d_out_n: *mut u32) -> c_int;
     pub fn fg_plan_hist_copy(p: *mut fg_plan, stream: *mut c_void, d_buf: *mut u32, into_plan: c_int) -> c_int;
+    pub fn fg_plan_set_peers(p: *mut fg_plan, peers: *const *mut fg_plan, n: u32) -> c_int;
+    pub fn fg_plan_ipc_export(p: *const fg_plan, out: *mut fg_plan_ipc) -> c_int;
+    pub fn fg_plan_set_ipc_peers(p: *mut fg_plan, peers: *const fg_plan_ipc, n: u32) -> c_int;
+    pub fn fg_plan_reset(p: *mut fg_plan, stream: *mut c_void) -> c_int;
     pub fn fg_plan_results(p: *mut fg_plan, out_score: *mut f32, out_doc: *mut u32, out_n: *mut u32) -> c_int;
     pub fn fg_plan_info_get(p: *const fg_plan, out: *mut fg_plan_info) -> c_int;
     pub fn fg_plan_profile(p: *mut fg_plan, enable: c_int) -> c_int;

@@ -287,3 +287,71 @@ def test_two_rank_hist_exchange():
             else:
                 assert thr[q] == 0 or int(summed[q].sum()) >= K
     assert sum(1 for q in range(nq) if got[0][4][q] > 0) > nq // 2  # the exchange gives most queries a threshold
+
+
+class _FakePeerPlan:
+    """Stands in for a native.Plan in the peer-linking exchange: ipc_export()
+    returns this rank's 112-byte fg_plan_ipc words, set_ipc_peers() / reset()
+    record what the exchange hands it (the device side runs in the gpu tests)."""
+
+    def __init__(self, rank):
+        self.blob = bytes([rank + 1]) * 112
+        self.peers = None
+        self.resets = 0
+
+    def ipc_export(self):
+        return self.blob
+
+    def set_ipc_peers(self, blobs):
+        self.peers = list(blobs)
+
+    def reset(self, stream=None):
+        self.resets += 1
+
+
+def _peer_worker(rank, world, port, outq):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import fugu_amd.shard as shard
+    p = _FakePeerPlan(rank)
+    n = shard.link_peers(p)
+    torch.cuda.synchronize = lambda *a, **k: None  # (no device here: the barrier is what is checked)
+    shard.reset_peers(p)
+    outq.put((rank, n, p.peers, p.resets))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_link_peers_exchange(world):
+    """shard.link_peers over a gloo group: every rank's plan gets the IPC words of
+    every OTHER rank's plan, in rank order, through one all-gather; reset_peers
+    resets the rank's own plan before its barrier (bench.py's C5 step over N GPUs)."""
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer_worker, args=(r, world, port, outq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    import queue
+    for _ in range(240):
+        try:
+            r, *rest = outq.get(timeout=1)
+            got[r] = rest
+            if len(got) == world:
+                break
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, "a rank failed"
+    for r in range(world):
+        n, peers, resets = got[r]
+        assert n == world - 1 and resets == 1
+        assert peers == [bytes([q + 1]) * 112 for q in range(world) if q != r]
