@@ -2887,11 +2887,20 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     // measured slower, profiles/r04/ab/ab_sweep_*.log)
     const bool part = conj && xcd_part;
     if (part) groups(items);
+    const int ord = [] { const char* e = getenv("FUGU_CONJ_ORDER"); return e ? atoi(e) : 0; }();
     for (size_t x = 0; x < n; ++x) {
       const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
       // single-list items keep the plain sweep (grouped: C3's mix 1.07 -> 1.11 ms)
-      const uint32_t sw = part && !single(items[x]) ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
-                                                    : (uint32_t)(kk * 2147483647.0);
+      uint32_t sw = part && !single(items[x]) ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
+                                              : (uint32_t)(kk * 2147483647.0);
+      if (ord && part && !single(items[x])) {
+        const uint32_t* qt = &q_terms[(size_t)items[x].q * fg::kMaxTerms];
+        const uint32_t t = ord == 2 ? qt[0] : ord == 3 ? qt[2] : qt[1];
+        const uint32_t hsh = (t * 2654435761u) >> 8;
+        const uint32_t qb = ord == 2 ? 6u : 4u;  // sweep bucket bits
+        sw = ((uint32_t)q_grp[items[x].q] << 28) | ((uint32_t)(kk * ((1u << qb) - 1) + 0.5) << (28 - qb)) |
+             (hsh & ((1u << (28 - qb)) - 1));
+      }
       const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | sw;
       a[x] = ((uint64_t)rk << 32) | (uint64_t)x;
     }
@@ -3610,8 +3619,8 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   }
   const size_t ng = groups.size();
   // every shard on the first device: the calling thread's high-priority stream
-  // there (FUGU_SEARCH_PRIO=0: its per-thread stream), so a search's kernels are
-  // dispatched ahead of a commit's rescores and builds; else per-thread streams
+  // there, so a search's kernels are dispatched ahead of a commit's segment
+  // build and the merger's; else per-thread streams
   const hipStream_t hs = ng == 1 && gdev[0] == dev0 ? search_stream(dev0) : hipStreamPerThread;
   bool merged = false;  // the plan's merged select already wrote ms / md / msh / mn
   std::vector<std::unique_ptr<fg_plan>> plans(ng), parts;
