@@ -2887,20 +2887,14 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     // measured slower, profiles/r04/ab/ab_sweep_*.log)
     const bool part = conj && xcd_part;
     if (part) groups(items);
-    const int ord = [] { const char* e = getenv("FUGU_CONJ_ORDER"); return e ? atoi(e) : 0; }();
     for (size_t x = 0; x < n; ++x) {
       const double kk = std::min(std::max(items[x].key, 0.0), 1.0);
       // single-list items keep the plain sweep (grouped: C3's mix 1.07 -> 1.11 ms)
-      uint32_t sw = part && !single(items[x]) ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
-                                              : (uint32_t)(kk * 2147483647.0);
-      if (ord && part && !single(items[x])) {
-        const uint32_t* qt = &q_terms[(size_t)items[x].q * fg::kMaxTerms];
-        const uint32_t t = ord == 2 ? qt[0] : ord == 3 ? qt[2] : qt[1];
-        const uint32_t hsh = (t * 2654435761u) >> 8;
-        const uint32_t qb = ord == 2 ? 6u : 4u;  // sweep bucket bits
-        sw = ((uint32_t)q_grp[items[x].q] << 28) | ((uint32_t)(kk * ((1u << qb) - 1) + 0.5) << (28 - qb)) |
-             (hsh & ((1u << (28 - qb)) - 1));
-      }
+      // (within a group, the sweep alone: also keying the items of one second / third /
+      // lead list together inside each 1/16 or 1/64 of the sweep ran 0.971 -> 1.004 /
+      // 0.999 / 0.982 ms, identical hits: profiles/r06/ab/conj_order.log)
+      const uint32_t sw = part && !single(items[x]) ? ((uint32_t)q_grp[items[x].q] << 28) | (uint32_t)(kk * 268435455.0)
+                                                    : (uint32_t)(kk * 2147483647.0);
       const uint32_t rk = (conj && single(items[x]) ? 0u : 0x80000000u) | sw;
       a[x] = ((uint64_t)rk << 32) | (uint64_t)x;
     }
