@@ -57,8 +57,11 @@ constexpr uint32_t kDisjSmallSpread = FG_DISJ_SPREAD;  // ... times up to this f
 #ifndef FG_GPQ
 // tools/ab_variants.py (ab_group*.log, round 2): 64 -> 16 with FG_MAXGROUP 16 -> 8: k_conj 1.08 -> 1.00 ms;
 // round 5 (after the XCD split and the sparse rank words), 16 -> 8 with FG_MAXGROUP 8 -> 16: headline
-// k_conj + k_final 1.043 -> 1.032 ms, C3 1.112 -> 1.075 ms, identical hits (profiles/r05/ab/conj_group_r05ab.log)
-#define FG_GPQ 8
+// k_conj + k_final 1.043 -> 1.032 ms, C3 1.112 -> 1.075 ms, identical hits (profiles/r05/ab/conj_group_r05ab.log);
+// round 6 (query-time-scoring build), 8 -> 4 items: headline k_conj + k_final 1.012 -> 0.984 ms, C3 1.049 ->
+// 1.046 ms (2: 0.978 / 1.065; 1: 0.981 / 1.058; 3, 5, 6 and caps 12 / 20 / 24 / 32 between or worse),
+// identical hits (profiles/r06/ab/conj_group_*.log)
+#define FG_GPQ 4
 #endif
 constexpr uint32_t kConjGroupsPerQuery = FG_GPQ;  // k_conj: a query's lead chunks in ~this many work items
 #ifndef FG_MAXGROUP
