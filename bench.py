@@ -333,8 +333,9 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
     if ref is not None:
         out["parity"] = {"queries_checked": nq, "mismatches": mism}
     # ---- commits on the 10M namespace: 16 consecutive POST
-    # /batch/upsert calls of 1000 new docs, each one fg_db_commit (a new segment,
-    # every older segment rescored with the new statistics: src/db/document.rs:65);
+    # /batch/upsert calls of 1000 new docs, each one fg_db_commit (a new segment;
+    # the older ones take the new statistics on the host, scored at query time:
+    # src/db/document.rs:65);
     # past 8 segments the background merger folds the small ones together
     # (IndexWriter merge threads, src/db/core.rs:247-249), off the commit path
     n_new, n_commits = 1000, 16
@@ -414,8 +415,9 @@ def bench_db_api(ctx, corp, native, synth, ref, threads, nq=200, n_seg=8):
                "merges": mi["merges"], "merge_ms_max": round(mi["merge_ms_max"], 1),
                "merge_ms_total": round(mi["merge_ms_total"], 1), "segments_after": mi["segments"],
                "note": "each commit = POST /batch/upsert of 1000 docs through fg_db_upsert_batch (analyzer, dictionary, "
-                       "raw-id deletes, a new segment built with the namespace statistics, every older segment "
-                       "rescored on the device); merges run on the background merger and are waited for at the end"}
+                       "raw-id deletes, a new segment built with the namespace statistics over its own term "
+                       "dictionary, the older segments given the new statistics on the host: no device work, scores "
+                       "formed at query time); merges run on the background merger and are waited for at the end"}
     d.close()
     return out, commits
 
