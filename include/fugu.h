@@ -158,7 +158,13 @@ struct fg_global_stats {
 int fg_docs_stats(const fg_docs_input* in, uint32_t* df_text, uint32_t* df_name, uint64_t* tot_tokens2);
 /* ... and of its facet field: df_facet [n_facet_terms], *tot_facet. */
 int fg_docs_facet_stats(const fg_docs_input* in, uint32_t* df_facet, uint64_t* tot_facet);
-/* fg_index_build_from_docs scored with global statistics (g may be NULL = local). */
+/* fg_index_build_from_docs scored with global statistics (g may be NULL = local).
+ * A build whose docs hold fewer than a quarter of the n_terms vocabulary's terms
+ * (a commit's new docs) keeps its own term dictionary -- its work and device
+ * arrays then scale with its own terms, as a tantivy segment's do -- and every
+ * call on the snapshot still takes vocabulary ids (a term it lacks matches
+ * nothing; fg_index_stats::n_terms, term_ladder and set_kth_floor speak the
+ * vocabulary's size). */
 int fg_index_build_from_docs_global(fg_ctx* ctx, int dev, const fg_docs_input* in, const fg_global_stats* g,
                                     fg_index** out);
 
