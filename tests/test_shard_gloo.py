@@ -1,4 +1,4 @@
-"""N > 1 path on CPU: world_size-2 gloo group, one namespace per rank.
+"""N > 1 path on CPU: world_size-2 (and 4) gloo groups, one namespace per rank.
 
 Each rank searches its own namespace (the CPU oracle stands in for the
 device, whose per-shard results are checked against the same oracle by the
@@ -52,8 +52,9 @@ def _worker(rank, world, port, n_docs, k, outq):
     dist.destroy_process_group()
 
 
-def test_two_rank_fanout_matches_direct_merge():
-    world, n_docs, k = 2, 3000, 10
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rank_fanout_matches_direct_merge(world):
+    n_docs, k = 3000, 10
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
@@ -118,9 +119,9 @@ def _stats_worker(rank, world, port, outq):
     dist.destroy_process_group()
 
 
-def test_two_rank_global_stats_allreduce():
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rank_global_stats_allreduce(world):
     """Doc-sharded namespace: the summed shard statistics equal the whole corpus's."""
-    world = 2
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
