@@ -387,13 +387,15 @@ uint32_t bg_grid_cap(int dev) {
 // thread without bound.  Work on one stream is ordered, so threads sharing a
 // stream serialise only their own launches; 16 streams >> the hardware queues.
 static constexpr uint32_t kSearchStreams = 16;
-static hipStream_t search_stream(int dev) {
-  thread_local std::map<int, hipStream_t> mine;
+// alt: the thread's second stream (the pool's stream half way round from its
+// own), for a batch whose second half overlaps the first (fg_search_sharded)
+static hipStream_t search_stream(int dev, bool alt = false) {
+  thread_local std::map<int, std::pair<hipStream_t, hipStream_t>> mine;
   auto it = mine.find(dev);
-  if (it != mine.end()) return it->second;
+  if (it != mine.end()) return alt ? it->second.second : it->second.first;
   static std::mutex mu;
   static std::map<int, std::pair<std::vector<hipStream_t>, uint32_t>> pools;
-  hipStream_t s = hipStreamPerThread;
+  hipStream_t s = hipStreamPerThread, s2 = hipStreamPerThread;
   {
     std::lock_guard<std::mutex> l(mu);
     auto& pool = pools[dev];
@@ -412,10 +414,12 @@ static hipStream_t search_stream(int dev) {
       }
       (void)hipSetDevice(cur);
     }
-    s = pool.first[pool.second++ % kSearchStreams];
+    const uint32_t i = pool.second++ % kSearchStreams;
+    s = pool.first[i];
+    s2 = pool.first[(i + kSearchStreams / 2) % kSearchStreams];
   }
-  mine[dev] = s;
-  return s;
+  mine[dev] = {s, s2};
+  return alt ? s2 : s;
 }
 
 // The background stream of a device (a db's segment builds and merges),
@@ -2358,8 +2362,11 @@ struct HostPlan {
 };
 
 // n_segs: the snapshots the plan spans; a query's work items are spread over
-// all of them, so each snapshot gets its share of the per-query item counts
-int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t n_segs, HostPlan& h) {
+// all of them, so each snapshot gets its share of the per-query item counts.
+// nq_size: the batch size the item counts are sized for (q may be a slice of
+// that batch: plan_create_multi plans a snapshot's queries in pieces)
+int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t n_segs, HostPlan& h,
+              uint32_t nq_size) {
   if (!ix || !q || (q->n_queries && !q->q_off)) return fail(FG_EINVAL, "bad arguments");
   if (q->n_queries && q->q_off[q->n_queries] > q->q_off[0] && !q->terms) return fail(FG_EINVAL, "q_off without terms");
   if (q->f_off && q->n_queries && q->f_off[q->n_queries] > q->f_off[0] && !q->f_terms)
@@ -2463,7 +2470,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
   // batch (the batch-of-one latency: the GPU holds nothing else) splits each
   // query over up to 16x more, shorter items that run side by side
   const uint32_t gpq_batch =
-      fg::kGroupsPerQuery * std::min<uint32_t>(fg::kDisjSmallSpread, std::max<uint32_t>(1, 256 / std::max(nq, 1u)));
+      fg::kGroupsPerQuery * std::min<uint32_t>(fg::kDisjSmallSpread, std::max<uint32_t>(1, 256 / std::max(nq_size, 1u)));
   const uint32_t gpq = std::max<uint32_t>(1, gpq_batch / n_segs);
   // k_conj items per query per snapshot of a multi-snapshot plan: the single-
   // snapshot count / n_segs, so a query keeps ~the single-snapshot item count
@@ -2651,7 +2658,7 @@ int plan_host(const fg_index* ix, const fg_query_batch* q, uint32_t k, uint32_t 
     // k_final still reads at most 64 x k candidates
     // (a multi-snapshot plan: divided by cdiv, above)
     const uint32_t per_q =
-        std::max<uint32_t>(1, std::min<uint32_t>(64, std::max<uint32_t>(conj_gpq, 1024 / std::max(nq, 1u))) / cdiv);
+        std::max<uint32_t>(1, std::min<uint32_t>(64, std::max<uint32_t>(conj_gpq, 1024 / std::max(nq_size, 1u))) / cdiv);
     const uint32_t G = std::min<uint32_t>(conj_maxg, std::max<uint32_t>(1, (nch + per_q - 1) / per_q));
     const uint32_t ng = (nch + G - 1) / G;
     ngroup[i] = ng;
@@ -2687,10 +2694,19 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   // lambdas see THIS thread's copy, not their own thread_local one)
   static thread_local std::vector<HostPlan> hs_tl;
   std::vector<HostPlan>& hs = hs_tl;
-  if (hs.size() < S) hs.resize(S);
   const uint32_t nq1 = q->n_queries;  // batch queries
   if ((uint64_t)S * nq1 > 0x7FFFFFFFull) return fail(FG_EUNSUPPORTED, "batch too large (%u x %u query slots)", S, nq1);
   const uint32_t nq = S * nq1;  // query slots
+  // pieces: each snapshot's queries planned in P slices of >= 128 queries so
+  // the host's threads all plan (8 snapshots on 16 threads: 2 pieces each);
+  // piece p = s * P + r holds snapshot s's queries [pa(r), pa(r + 1)), and the
+  // pieces joined in order give the same tables and item lists as one plan per
+  // snapshot (plan_host sizes items by the whole batch)
+  const bool par = S > 1 && nq1 >= 64;
+  const uint32_t P =
+      par ? std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)fgh::hw_threads(0) / S, nq1 / 128)) : 1u;
+  auto pa = [&](uint32_t r) { return (uint32_t)((uint64_t)nq1 * r / P); };
+  if (hs.size() < (size_t)S * P) hs.resize((size_t)S * P);
   // ---- the joined tables (this thread's buffers, reused like hs): several
   // snapshots' per-query tables are copied into their slots by the planning
   // workers themselves, the lists joined after
@@ -2726,31 +2742,37 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     q_wn.resize(nqt * S);
     q_rup.resize(nqt * S);
   }
-  auto put_slot = [&](uint32_t s) {  // snapshot s's per-query tables into its slots
-    const HostPlan& h = hs[s];
+  auto put_slot = [&](uint32_t pc) {  // piece pc's per-query tables into its slots
+    const HostPlan& h = hs[pc];
+    const size_t v0 = (size_t)(pc / P) * nq1 + pa(pc % P), t0 = v0 * fg::kMaxTerms;
     auto cp = [](auto& dst, const auto& src, size_t at) { std::copy(src.begin(), src.end(), dst.begin() + at); };
-    cp(q_m, h.q_m, (size_t)s * nq1);
-    cp(lead, h.lead, (size_t)s * nq1);
-    cp(ngroup, h.ngroup, (size_t)s * nq1);
-    cp(thr0, h.thr0, (size_t)s * nq1);
-    cp(q_terms, h.q_terms, s * nqt);
-    cp(q_ub, h.q_ub, s * nqt);
-    cp(q_wt, h.q_wt, s * nqt);
-    cp(q_wn, h.q_wn, s * nqt);
-    cp(q_rup, h.q_rup, s * nqt);
+    cp(q_m, h.q_m, v0);
+    cp(lead, h.lead, v0);
+    cp(ngroup, h.ngroup, v0);
+    cp(thr0, h.thr0, v0);
+    cp(q_terms, h.q_terms, t0);
+    cp(q_ub, h.q_ub, t0);
+    cp(q_wt, h.q_wt, t0);
+    cp(q_wn, h.q_wn, t0);
+    cp(q_rup, h.q_rup, t0);
   };
-  if (S > 1 && q->n_queries >= 64) {
-    std::vector<int> rcs(S, FG_OK);
-    std::vector<std::string> errs(S);
-    run_parallel(S, [&](uint32_t s) {
-      if ((rcs[s] = plan_host(ixs[s], q, k, S, hs[s]))) errs[s] = fg_last_error();
-      else put_slot(s);
+  if (par) {
+    std::vector<int> rcs((size_t)S * P, FG_OK);
+    std::vector<std::string> errs((size_t)S * P);
+    run_parallel(S * P, [&](uint32_t pc) {
+      const uint32_t a = pa(pc % P), b = pa(pc % P + 1);
+      fg_query_batch qp = *q;  // the slice: q_off / f_off hold absolute offsets
+      qp.n_queries = b - a;
+      qp.q_off = q->q_off + a;
+      if (q->f_off) qp.f_off = q->f_off + a;
+      if ((rcs[pc] = plan_host(ixs[pc / P], &qp, k, S, hs[pc], nq1))) errs[pc] = fg_last_error();
+      else put_slot(pc);
     });
-    for (uint32_t s = 0; s < S; ++s)
-      if (rcs[s]) return fail(rcs[s], "snapshot %u: %s", s, errs[s].c_str());
+    for (uint32_t pc = 0; pc < S * P; ++pc)
+      if (rcs[pc]) return fail(rcs[pc], "snapshot %u: %s", pc / P, errs[pc].c_str());
   } else {
     for (uint32_t s = 0; s < S; ++s) {
-      if (int rc = plan_host(ixs[s], q, k, S, hs[s])) {
+      if (int rc = plan_host(ixs[s], q, k, S, hs[s], nq1)) {
         if (S == 1) return rc;
         const std::string e = fg_last_error();
         return fail(rc, "snapshot %u: %s", s, e.c_str());
@@ -2772,9 +2794,9 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
   } else {
     auto cat = [](auto& dst, const auto& src) { dst.insert(dst.end(), src.begin(), src.end()); };
     f_woff.push_back(0);
-    for (uint32_t s = 0; s < S; ++s) {
-      HostPlan& h = hs[s];
-      const uint32_t fb = nf, vb = s * nq1;
+    for (uint32_t pc = 0; pc < S * P; ++pc) {
+      HostPlan& h = hs[pc];
+      const uint32_t s = pc / P, fb = nf, vb = s * nq1 + pa(pc % P);
       for (uint32_t f : h.q_filter) q_filter.push_back(f == 0xFFFFFFFFu ? f : fb + f);
       cat(f_shift, h.f_shift); cat(f_tab, h.f_tab); cat(f_max, h.f_max);
       const uint64_t wb = f_woff.back();
@@ -2794,13 +2816,16 @@ static int plan_create_multi(fg_index* const* ixs, uint32_t S, const fg_query_ba
     q_hlo.assign(nq, 0x3F800000u);
     q_hhi.assign(nq, 0x3F800000u);
     q_hsh.assign(nq, 31);
-    for (uint32_t i = 0; i < nq1; ++i) {
+    for (uint32_t i = 0, r = 0; i < nq1; ++i) {
+      while (i >= pa(r + 1)) ++r;  // the piece of query i
+      const uint32_t li = i - pa(r);
       uint32_t l = 0, hh = 0;
       bool any = false;
       for (uint32_t s = 0; s < S; ++s) {
-        if (!hs[s].ngroup[i]) continue;
-        l = std::max(l, hs[s].q_hlo[i]);
-        hh = std::max(hh, hs[s].q_hhi[i]);
+        const HostPlan& h = hs[s * P + r];
+        if (!h.ngroup[li]) continue;
+        l = std::max(l, h.q_hlo[li]);
+        hh = std::max(hh, h.q_hhi[li]);
         any = true;
       }
       if (!any) continue;
@@ -3616,13 +3641,18 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   // there, so a search's kernels are dispatched ahead of a commit's segment
   // build and the merger's; else per-thread streams
   const hipStream_t hs = ng == 1 && gdev[0] == dev0 ? search_stream(dev0) : hipStreamPerThread;
+  // a batch run in two halves: the second half on the thread's second stream
+  // there, so its kernels start while the first half's drain
+  const hipStream_t hs2 = ng == 1 && gdev[0] == dev0 ? search_stream(dev0, true) : hs;
+  uint32_t split = 0;  // the second half's first query (0: one part)
   bool merged = false;  // the plan's merged select already wrote ms / md / msh / mn
   std::vector<std::unique_ptr<fg_plan>> plans(ng), parts;
   std::vector<hipEvent_t> evs(ng, nullptr);
   // teardown (also on error returns): every device's stream drained, then the
   // events, the plans and the buffers
   struct Back {
-    const std::vector<int>& dv; int d0; fg_index* ix0; void* p; size_t n; std::vector<hipEvent_t>& ev; hipStream_t s0;
+    const std::vector<int>& dv; int d0; fg_index* ix0; void* p; size_t n; std::vector<hipEvent_t>& ev; hipStream_t s0,
+        s1;
     ~Back() {
       for (size_t g = 0; g < dv.size(); ++g) {
         (void)hipSetDevice(dv[g]);
@@ -3631,9 +3661,10 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       }
       (void)hipSetDevice(d0);
       (void)hipStreamSynchronize(s0);
+      if (s1 != s0) (void)hipStreamSynchronize(s1);
       ix0->pool->put(p, n);
     }
-  } back{gdev, dev0, shards[0], base, got, evs, hs};
+  } back{gdev, dev0, shards[0], base, got, evs, hs, hs2};
   static const bool trace_env = getenv("FUGU_SHARD_TRACE") != nullptr;
   fgh::SearchTrace& st = fgh::search_trace();
   const bool trace = trace_env || st.enabled();
@@ -3667,10 +3698,12 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
         if (q->f_off) qi.f_off = q->f_off + b;
         const double t_p = trace ? now() : 0.0;
         fg_plan* pi = nullptr;
-        if (int rc = plan_create_multi(ixs.data(), S, &qi, k, &pi, false, hs)) return rc;
+        const hipStream_t si = i == 0 ? hs : hs2;
+        if (i > 0) split = b;
+        if (int rc = plan_create_multi(ixs.data(), S, &qi, k, &pi, false, si)) return rc;
         parts.emplace_back(pi);
         if (trace) t_plan += now() - t_p;
-        if (int rc = execute_impl(pi, hs, ms + (size_t)b * k, md + (size_t)b * k, mn + b, msh + (size_t)b * k)) return rc;
+        if (int rc = execute_impl(pi, si, ms + (size_t)b * k, md + (size_t)b * k, mn + b, msh + (size_t)b * k)) return rc;
       }
       merged = true;
       break;
@@ -3718,8 +3751,10 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   for (hipEvent_t e : evs)
     if (e) HIPCHK(hipStreamWaitEvent(hs, e, 0));
   if (!merged) HIPCHK(fg::launch_merge(n_shards, nq, k, gs, gd, gn, ms, md, msh, mn, hs));
+  const bool two = split && hs2 != hs;
   if (trace_env) {
     HIPCHK(hipStreamSynchronize(hs));
+    if (two) HIPCHK(hipStreamSynchronize(hs2));
     fprintf(stderr, "[fg_search_sharded] nq %u shards %u devices %zu merged %d: plan %.3f launch %.3f kernels+merge %.3f ms\n",
             nq, n_shards, ng, (int)merged, t_plan, t_run - t_0 - t_plan, now() - t_run);
   }
@@ -3737,6 +3772,30 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
   const size_t span = 3 * o_k + 4ull * nq;
   if (span <= (4ull << 20)) {
     PinnedLease pin(*shards[0]->pinned, span);
+    if (pin.p && two) {
+      // each half's hits copied back on its own stream, the first half's copied
+      // out of the pinned buffer while the second half's kernels run
+      char* h = static_cast<char*>(pin.p);
+      const char* d = reinterpret_cast<const char*>(ms);
+      for (int half = 0; half < 2; ++half) {
+        const hipStream_t sh = half ? hs2 : hs;
+        const size_t q0 = half ? split : 0, q1 = half ? nq : split;
+        for (size_t a = 0; a < 3; ++a)
+          HIPCHK(hipMemcpyAsync(h + a * o_k + 4 * q0 * k, d + a * o_k + 4 * q0 * k, 4 * (q1 - q0) * k,
+                                hipMemcpyDeviceToHost, sh));
+        HIPCHK(hipMemcpyAsync(h + 3 * o_k + 4 * q0, d + 3 * o_k + 4 * q0, 4 * (q1 - q0), hipMemcpyDeviceToHost, sh));
+      }
+      for (int half = 0; half < 2; ++half) {
+        HIPCHK(hipStreamSynchronize(half ? hs2 : hs));
+        const size_t q0 = half ? split : 0, q1 = half ? nq : split;
+        std::memcpy(out_score + q0 * k, h + 4 * q0 * k, 4 * (q1 - q0) * k);
+        std::memcpy(out_doc + q0 * k, h + o_k + 4 * q0 * k, 4 * (q1 - q0) * k);
+        if (out_shard) std::memcpy(out_shard + q0 * k, h + 2 * o_k + 4 * q0 * k, 4 * (q1 - q0) * k);
+        std::memcpy(out_n + q0, h + 3 * o_k + 4 * q0, 4 * (q1 - q0));
+      }
+      return FG_OK;
+    }
+    if (two) HIPCHK(hipStreamSynchronize(hs2));  // (no pinned buffer: one copy on hs)
     if (pin.p) {
       HIPCHK(hipMemcpyAsync(pin.p, ms, span, hipMemcpyDeviceToHost, hs));
       HIPCHK(hipStreamSynchronize(hs));
@@ -3748,6 +3807,7 @@ int fg_search_sharded(fg_ctx* ctx, fg_index* const* shards, uint32_t n_shards, c
       return FG_OK;
     }
   }
+  if (two) HIPCHK(hipStreamSynchronize(hs2));
   HIPCHK(hipMemcpyAsync(out_score, ms, 4 * nk, hipMemcpyDeviceToHost, hs));
   HIPCHK(hipMemcpyAsync(out_doc, md, 4 * nk, hipMemcpyDeviceToHost, hs));
   if (out_shard) HIPCHK(hipMemcpyAsync(out_shard, msh, 4 * nk, hipMemcpyDeviceToHost, hs));
